@@ -1,0 +1,185 @@
+/*
+ * kartdiff.h — C ABI of libkartdiff.so, the MI355X (gfx950) bulk feature-diff engine.
+ *
+ * Drop-in boundary.  Each entry point replaces one reference interface:
+ *
+ *   kd_diff2       <- libgit2 tree-to-tree diff as consumed by RichBaseDataset.diff_feature
+ *                     (/root/reference/kart/rich_base_dataset.py:205-300; the FFI call is
+ *                     Tree.diff_to_tree at :212-232).  Returns the insert/update/delete delta set.
+ *   kd_fielddiff   <- Dataset3.get_feature (kart/dataset3.py:185-223) + Schema.feature_from_raw_dict
+ *                     (kart/schema.py:288-293) + the per-field Python `==` compare of
+ *                     TextDiffWriter.write_feature_delta (kart/text_diff_writer.py:135-145).
+ *   kd_merge3      <- repo.merge_trees(ancestor, ours, theirs) (kart/merge.py:99-100; libgit2
+ *                     git_merge_trees) feeding MergeIndex.from_pygit2_index (kart/merge_util.py:92-103).
+ *   kd_envelopes   <- SpatialFilter.matches envelope quick-check (kart/spatial_filter/__init__.py:534-590,
+ *                     709-734) + get_envelope_for_indexing/EnvelopeEncoder.encode for an identity
+ *                     CRS (kart/spatial_filter/index.py:485-579,639-707).
+ *   kd_env_overlap <- sf_filter_blob decode + cyclic_range_overlaps
+ *                     (vendor/spatial-filter/spatial_filter.cpp:170-260).
+ *   kd_pack_*      <- Dataset3.decode_path_to_1pk / PathEncoder (kart/dataset3.py:250-259,
+ *                     kart/dataset3_paths.py:202-215,292-299): host-side key packing.
+ *
+ * Conventions: plain pointers and sizes only; return 0 on success, KD_EINVAL (-1) on bad
+ * arguments, KD_EHIP (-2) on a HIP runtime error, KD_EUNSUPPORTED (-3) when the input needs
+ * the CPU path (caller falls back); kd_last_error() gives a thread-local message.  One kd_ctx per
+ * GPU; calls on one context are serialised by the caller.  Index arrays are uint32 (a side may
+ * hold at most 2^32-2 entries per GPU); KD_NONE marks "absent".
+ */
+#ifndef KARTDIFF_H
+#define KARTDIFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KD_ABI_VERSION 1
+
+#define KD_OK 0
+#define KD_EINVAL (-1)
+#define KD_EHIP (-2)
+#define KD_EUNSUPPORTED (-3)
+
+#define KD_NONE 0xFFFFFFFFu
+
+/* where a buffer lives */
+#define KD_MEM_HOST 0u
+#define KD_MEM_DEVICE 1u
+
+/* key modes (see DESIGN.md "join key") */
+#define KD_KEY_INT 0u  /* IntPathEncoder: key = bucket24 | wrap34 | pk%64, bijective with pk  */
+#define KD_KEY_HASH 1u /* MsgpackHashPathEncoder: key = bucket bits | FNV-1a(filename) bits;
+                          matched keys are verified against the filename bytes            */
+
+typedef struct kd_ctx kd_ctx;
+
+/* One commit's dataset feature tree, flattened: n leaf entries sorted by strictly ascending key. */
+typedef struct kd_side {
+    uint64_t n;
+    const uint64_t* key;      /* [n] join keys, strictly ascending                                 */
+    const uint8_t* oid;       /* [n*20] git blob OIDs (raw bytes)                                  */
+    const uint8_t* name;      /* KD_KEY_HASH only: concatenated filenames (may be NULL for INT)    */
+    const uint64_t* name_off; /* [n+1] offsets into name (KD_KEY_HASH only)                        */
+    uint32_t mem;             /* KD_MEM_HOST or KD_MEM_DEVICE: where the arrays above live         */
+    uint32_t key_mode;        /* KD_KEY_INT or KD_KEY_HASH                                         */
+} kd_side;
+
+/* A blob arena: blob b = data[off[b] .. off[b+1]).  Feature blobs are msgpack
+ * [legend_hex40, [values...]] (kart/dataset3.py:185-215); geometry blobs are GPKG binary. */
+typedef struct kd_blobs {
+    uint64_t n;
+    const uint8_t* data;
+    const uint64_t* off; /* [n+1] */
+    uint32_t mem;
+    uint32_t _pad;
+} kd_blobs;
+
+/* Legend -> union-key maps for kd_fielddiff (host memory).  Union keys are the old schema's
+ * column names in order, then the new schema's names not in the old one
+ * (BaseDiffWriter._all_feature_keys, kart/base_diff_writer.py:181-187).
+ * map[l*n_keys + k] = value index in legend l's non-pk array, or
+ *   -1 key not in that side's schema (_NULL), -2 column absent from the legend (None),
+ *   -3 the primary-key column (value from the path). */
+typedef struct kd_legend_maps {
+    int32_t n_keys;
+    int32_t words;            /* ceil(n_keys / 64): uint64 mask words per update */
+    int32_t n_leg_old;
+    int32_t n_leg_new;
+    const uint8_t* leg_old_hex; /* [n_leg_old*40] legend hexhash strings */
+    const int16_t* map_old;     /* [n_leg_old*n_keys] */
+    const uint8_t* leg_new_hex;
+    const int16_t* map_new;
+    const uint64_t* cmp_mask;   /* [words] keys to compare ("__"-prefixed keys are excluded) */
+} kd_legend_maps;
+
+typedef struct kd_diff_result {
+    uint64_t n_insert, n_update, n_delete, n_delta;
+    uint32_t* delta;  /* [2*n_delta] (base index | KD_NONE, target index | KD_NONE), key order */
+    uint32_t* upd;    /* [2*n_update] (base index, target index) of the updates, key order     */
+} kd_diff_result;
+
+typedef struct kd_merge_result {
+    uint64_t n_clean;     /* merged entries present without conflict                          */
+    uint64_t n_conflict;
+    uint64_t n_mdelta;    /* entries where the merge result differs from ours                 */
+    uint32_t* conflict;   /* [3*n_conflict] (ancestor, ours, theirs) index | KD_NONE          */
+    uint32_t* mdelta;     /* [2*n_mdelta] (ours | KD_NONE, theirs | KD_NONE): take theirs     */
+} kd_merge_result;
+
+/* -------- context -------- */
+int kd_abi_version(void);
+const char* kd_last_error(void);
+int kd_init(int device_ordinal, kd_ctx** out);
+int kd_fini(kd_ctx* ctx);
+/* Launch on an external HIP stream (e.g. torch's current stream); NULL = the context's own. */
+int kd_set_stream(kd_ctx* ctx, void* hip_stream);
+int kd_sync(kd_ctx* ctx);
+/* Pre-size device workspaces so the first timed call does not allocate. */
+int kd_reserve(kd_ctx* ctx, uint64_t max_entries_per_side, uint64_t max_updates);
+void kd_free(void* p); /* frees kd_diff_result / kd_merge_result and their arrays */
+
+/* -------- two-way diff: classify2 (+ optional fused field diff) -------- */
+/* Host-convenience form: sides may be host or device; results are host memory (kd_free). */
+int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags,
+             kd_diff_result** out);
+/* Device form: everything device-resident, asynchronous on the context stream.
+ * d_delta / d_upd capacity must cover the worst case (base.n + target.n pairs).
+ * d_counts[4] <- inserts, updates, deletes, deltas.  d_err <- nonzero if a side is not strictly
+ * ascending (1) or a KD_KEY_HASH key matched two different filenames (2). */
+int kd_diff2_device(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags,
+                    uint32_t* d_delta, uint32_t* d_upd, uint64_t* d_counts, uint32_t* d_err);
+
+/* -------- field diff -------- */
+/* For each update u: old blob = old->data[old->off[pu[2u]] ..], new blob = neu->...[pu[2u+1]]
+ * (pu = the (base, target) update pairs, or NULL: blob u on both sides).  masks[u*words + w]
+ * bit k set iff union key k changed under Python `==`.  status[u]: 0 ok, 1 malformed blob,
+ * 2 unknown legend, 3 too many values, 4 unsupported value (nested container, invalid ext 'G'):
+ * nonzero -> the caller recomputes that update on the CPU path.
+ * pairs_mem / out_mem say where pu and masks/status live; n_upd may be read from a device
+ * counter (d_n_upd != NULL, device form) so no host sync is needed between classify and diff. */
+int kd_fielddiff(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_blobs* new_blobs,
+                 const uint32_t* pu, uint64_t n_upd, const uint64_t* d_n_upd, uint32_t pairs_mem,
+                 const kd_legend_maps* maps, uint64_t* masks, uint8_t* status, uint32_t out_mem);
+
+/* -------- three-way merge classification -------- */
+int kd_merge3(kd_ctx* ctx, const kd_side* ancestor, const kd_side* ours, const kd_side* theirs,
+              uint32_t flags, kd_merge_result** out);
+
+/* -------- spatial -------- */
+/* Per geometry blob (GPKG; length 0 = null geometry):
+ *   match[i]: 0 NON_MATCHING, 1 CANDIDATE (bbox passed; exact GEOS test is the caller's),
+ *             2 MATCHING (null geometry), 3 FALLBACK (needs the CPU path)
+ *   enc[i*bits/2 ..] EnvelopeEncoder bytes of the identity-CRS index envelope; enc_ok[i]=1 when
+ *   the spatial indexer would store a row.
+ * filt_env = (min-x, max-x, min-y, max-y) of the filter (SpatialFilter.filter_env). */
+int kd_envelopes(kd_ctx* ctx, const kd_blobs* geoms, const double filt_env[4], int bits,
+                 uint8_t* match, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem,
+                 uint64_t* n_candidates);
+/* Decode n encoded envelopes (bits/2 bytes each) and test them against q = (w, s, e, n):
+ * out[i] = cyclic(w,e) && range(s,n) overlap (spatial_filter.cpp:187-260). */
+int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const double q[4],
+                   uint8_t* out, uint32_t mem);
+
+/* -------- host-side key packing (CPU, multithreaded) -------- */
+/* KD_KEY_INT: filenames b64(msgpack([pk])) -> keys.  status[i] = 0 ok / 1 not an int pk /
+ * 2 pk outside [-2^63, 2^63).  Returns number of bad entries. */
+int64_t kd_pack_int_keys(const uint8_t* names, const uint64_t* name_off, uint64_t n,
+                         uint64_t* keys, uint8_t* status);
+/* KD_KEY_HASH: "c1/../cL/<filename>" relative paths -> keys (levels, hex=0 base64 / 1 hex). */
+int64_t kd_pack_hash_keys(const uint8_t* paths, const uint64_t* path_off, uint64_t n, int levels,
+                          int hex, uint64_t* keys, uint8_t* status);
+/* Inverse of the KD_KEY_INT key: pk = ((wrap - 2^33) * 2^24 + bucket) * 64 + r. */
+int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks);
+
+/* -------- profiling (hipEvents around every launch on the context stream) -------- */
+int kd_prof_enable(kd_ctx* ctx, int on);
+/* name = kernel name; returns launches and summed milliseconds since the last reset. */
+int kd_prof_get(kd_ctx* ctx, const char* name, uint64_t* launches, double* total_ms);
+int kd_prof_reset(kd_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KARTDIFF_H */

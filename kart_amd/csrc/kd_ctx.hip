@@ -1,0 +1,336 @@
+// kd_ctx.hip — context, errors, workspaces, profiling and host-side key packing of libkartdiff.
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+
+#include "kd_internal.h"
+
+namespace kd {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out) {
+    DevBuf& b = ctx->bufs[slot];
+    if (bytes == 0) bytes = 16;
+    if (b.bytes < bytes) {
+        if (b.p) {
+            hipError_t e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) { set_error("sync before realloc: %s", hipGetErrorString(e)); return KD_EHIP; }
+            KD_HIP(hipFree(b.p));
+            b.p = nullptr;
+            b.bytes = 0;
+        }
+        size_t want = bytes + bytes / 8;  // headroom
+        KD_HIP(hipMalloc(&b.p, want));
+        b.bytes = want;
+    }
+    *out = b.p;
+    return KD_OK;
+}
+
+int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem, const void** dev) {
+    if (p == nullptr || bytes == 0 || mem == KD_MEM_DEVICE) {
+        *dev = p;
+        return KD_OK;
+    }
+    void* d = nullptr;
+    int rc = ensure(ctx, slot, bytes, &d);
+    if (rc) return rc;
+    KD_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
+    *dev = d;
+    return KD_OK;
+}
+
+void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a) {
+    (void)name;
+    if (ctx->ev_pool.empty()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) { *a = nullptr; return; }
+        ctx->ev_pool.push_back(e);
+    }
+    *a = ctx->ev_pool.back();
+    ctx->ev_pool.pop_back();
+    (void)hipEventRecord(*a, ctx->stream);
+}
+
+void prof_end(kd_ctx* ctx, const char* name, hipEvent_t a) {
+    if (!a) return;
+    hipEvent_t b;
+    if (ctx->ev_pool.empty()) {
+        if (hipEventCreate(&b) != hipSuccess) return;
+    } else {
+        b = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+    }
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->pending.push_back({name, a, b});
+}
+
+int prof_flush(kd_ctx* ctx) {
+    for (auto& p : ctx->pending) {
+        KD_HIP(hipEventSynchronize(p.b));
+        float ms = 0;
+        KD_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        ProfStat& s = ctx->stats[p.name];
+        s.launches++;
+        s.ms += ms;
+        ctx->ev_pool.push_back(p.a);
+        ctx->ev_pool.push_back(p.b);
+    }
+    ctx->pending.clear();
+    return KD_OK;
+}
+
+// host-side key packing helpers
+static inline int b64v(u8 c) {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '-') return 62;
+    if (c == '_') return 63;
+    return -1;
+}
+
+// pk (sign, magnitude) -> int key; 0 ok, 2 out of range
+static inline int int_key(bool neg, u64 mag, u64* key) {
+    __int128 pk = neg ? -(__int128)mag : (__int128)mag;
+    // floor division by powers of two == arithmetic shift on two's complement
+    __int128 q = pk >> 6;                       // pk // 64
+    u64 r = (u64)(pk - q * 64);                 // pk % 64 in [0, 64)
+    u64 bucket = (u64)(q & ((1 << 24) - 1));    // (pk // 64) % 2^24
+    __int128 k = (pk >> 30) + ((__int128)1 << 33);
+    if (k < 0 || k >= ((__int128)1 << 34)) return 2;
+    *key = (bucket << 40) | ((u64)k << 6) | r;
+    return 0;
+}
+
+static int decode_int_name(const u8* s, int n, u64* key) {
+    u8 buf[16];
+    int o = 0, acc = 0, bits = 0;
+    for (int i = 0; i < n; i++) {
+        if (s[i] == '=') break;
+        int v = b64v(s[i]);
+        if (v < 0) return 1;
+        acc = (acc << 6) | v;
+        bits += 6;
+        if (bits >= 8) {
+            bits -= 8;
+            if (o >= 16) return 1;
+            buf[o++] = (u8)((acc >> bits) & 0xFF);
+        }
+    }
+    if (o < 2 || buf[0] != 0x91) return 1;
+    u8 t = buf[1];
+    int w = 0;
+    bool sgn = false;
+    u64 u = 0;
+    if (t <= 0x7f) { u = t; }
+    else if (t >= 0xe0) { sgn = true; u = (u64)(i64)(int8_t)t; }
+    else if (t >= 0xcc && t <= 0xcf) { w = 1 << (t - 0xcc); }
+    else if (t >= 0xd0 && t <= 0xd3) { w = 1 << (t - 0xd0); sgn = true; }
+    else return 1;
+    if (o != 2 + w) return 1;
+    if (w) {
+        for (int i = 0; i < w; i++) u = (u << 8) | buf[2 + i];
+        if (sgn) { int sh = 64 - 8 * w; u = (u64)(((i64)(u << sh)) >> sh); }
+    }
+    if (sgn) {
+        i64 v = (i64)u;
+        return int_key(v < 0, v < 0 ? (u64)(-(__int128)v) : (u64)v, key);
+    }
+    return int_key(false, u, key);
+}
+
+template <typename F>
+static void par_for(u64 n, F&& f) {
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt == 0) nt = 1;
+    if (nt > 32) nt = 32;
+    if (n < 65536) nt = 1;
+    std::vector<std::thread> th;
+    u64 chunk = (n + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; t++) {
+        u64 a = t * chunk, b = std::min<u64>(n, a + chunk);
+        if (a >= b) break;
+        th.emplace_back([&f, a, b] { for (u64 i = a; i < b; i++) f(i); });
+    }
+    for (auto& t : th) t.join();
+}
+
+static inline u64 fnv1a64(const u8* p, u64 n) {
+    u64 h = 1469598103934665603ull;
+    for (u64 i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+}  // namespace kd
+
+using namespace kd;
+
+extern "C" {
+
+int kd_abi_version(void) { return KD_ABI_VERSION; }
+
+const char* kd_last_error(void) { return kd::g_err; }
+
+int kd_init(int device_ordinal, kd_ctx** out) {
+    KD_CHECK(out != nullptr, "kd_init: out is NULL");
+    int n = 0;
+    KD_HIP(hipGetDeviceCount(&n));
+    KD_CHECK(device_ordinal >= 0 && device_ordinal < n, "kd_init: device %d of %d", device_ordinal, n);
+    KD_HIP(hipSetDevice(device_ordinal));
+    kd_ctx* c = new kd_ctx();
+    c->device = device_ordinal;
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        set_error("hipStreamCreate: %s", hipGetErrorString(e));
+        return KD_EHIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return KD_OK;
+}
+
+int kd_fini(kd_ctx* ctx) {
+    if (!ctx) return KD_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    prof_flush(ctx);
+    for (auto& kv : ctx->bufs)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return KD_OK;
+}
+
+int kd_set_stream(kd_ctx* ctx, void* hip_stream) {
+    KD_CHECK(ctx, "kd_set_stream: ctx is NULL");
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return KD_OK;
+}
+
+int kd_sync(kd_ctx* ctx) {
+    KD_CHECK(ctx, "kd_sync: ctx is NULL");
+    KD_HIP(hipSetDevice(ctx->device));
+    KD_HIP(hipStreamSynchronize(ctx->stream));
+    return prof_flush(ctx);
+}
+
+void kd_free(void* p) {
+    if (!p) return;
+    // both result structs begin with counters and hold malloc'd arrays; they are allocated as a
+    // single block (struct + arrays), see kd_classify.hip
+    std::free(p);
+}
+
+int kd_prof_enable(kd_ctx* ctx, int on) {
+    KD_CHECK(ctx, "kd_prof_enable: ctx is NULL");
+    ctx->prof = on != 0;
+    return KD_OK;
+}
+
+int kd_prof_get(kd_ctx* ctx, const char* name, uint64_t* launches, double* total_ms) {
+    KD_CHECK(ctx && name, "kd_prof_get: bad args");
+    int rc = prof_flush(ctx);
+    if (rc) return rc;
+    auto it = ctx->stats.find(name);
+    if (launches) *launches = it == ctx->stats.end() ? 0 : it->second.launches;
+    if (total_ms) *total_ms = it == ctx->stats.end() ? 0 : it->second.ms;
+    return KD_OK;
+}
+
+int kd_prof_reset(kd_ctx* ctx) {
+    KD_CHECK(ctx, "kd_prof_reset: ctx is NULL");
+    int rc = prof_flush(ctx);
+    ctx->stats.clear();
+    return rc;
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side key packing (Dataset3.decode_path_to_1pk / PathEncoder, see kartdiff.h)
+// ------------------------------------------------------------------------------------------
+
+int64_t kd_pack_int_keys(const uint8_t* names, const uint64_t* name_off, uint64_t n, uint64_t* keys,
+                         uint8_t* status) {
+    if (!names || !name_off || !keys || !status) { set_error("kd_pack_int_keys: NULL"); return KD_EINVAL; }
+    std::vector<u64> badc(1, 0);
+    std::mutex m;
+    u64 bad = 0;
+    par_for(n, [&](u64 i) {
+        u64 a = name_off[i], b = name_off[i + 1];
+        u64 k = 0;
+        int st = (b - a > 24) ? 1 : decode_int_name(names + a, (int)(b - a), &k);
+        keys[i] = k;
+        status[i] = (u8)st;
+        if (st) { std::lock_guard<std::mutex> g(m); bad++; }
+    });
+    return (int64_t)bad;
+}
+
+int64_t kd_pack_hash_keys(const uint8_t* paths, const uint64_t* path_off, uint64_t n, int levels, int hex,
+                          uint64_t* keys, uint8_t* status) {
+    if (!paths || !path_off || !keys || !status || levels <= 0) { set_error("kd_pack_hash_keys: bad args"); return KD_EINVAL; }
+    std::mutex m;
+    u64 bad = 0;
+    par_for(n, [&](u64 i) {
+        const u8* s = paths + path_off[i];
+        u64 len = path_off[i + 1] - path_off[i];
+        u64 bucket = 0, pos = 0;
+        int bits = 0, st = 0;
+        for (int l = 0; l < levels && !st; l++) {
+            int seg = hex ? 2 : 1;
+            for (int c = 0; c < seg && !st; c++) {
+                if (pos >= len) { st = 1; break; }
+                u8 ch = s[pos++];
+                int v;
+                if (hex) {
+                    v = (ch >= '0' && ch <= '9') ? ch - '0' : (ch >= 'a' && ch <= 'f') ? ch - 'a' + 10 : -1;
+                    if (v < 0) { st = 1; break; }
+                    bucket = (bucket << 4) | (u64)v; bits += 4;
+                } else {
+                    v = b64v(ch);
+                    if (v < 0) { st = 1; break; }
+                    bucket = (bucket << 6) | (u64)v; bits += 6;
+                }
+            }
+            if (!st && (pos >= len || s[pos] != '/')) st = 1;
+            pos++;
+        }
+        u64 k = 0;
+        if (!st) {
+            int low = 64 - bits;
+            u64 h = fnv1a64(s + pos, len - pos);
+            k = (bucket << low) | (h >> (64 - low));
+        }
+        keys[i] = k;
+        status[i] = (u8)st;
+        if (st) { std::lock_guard<std::mutex> g(m); bad++; }
+    });
+    return (int64_t)bad;
+}
+
+int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks) {
+    KD_CHECK(keys && pks, "kd_int_keys_to_pks: NULL");
+    par_for(n, [&](u64 i) {
+        u64 key = keys[i];
+        i64 bucket = (i64)(key >> 40);
+        i64 k = (i64)((key >> 6) & ((1ull << 34) - 1)) - ((i64)1 << 33);
+        i64 r = (i64)(key & 63);
+        // ((k * 2^24 + bucket) * 64 + r), computed in unsigned arithmetic (wraps exactly to int64)
+        u64 v = (((u64)k << 24) + (u64)bucket) * 64u + (u64)r;
+        pks[i] = (i64)v;
+    });
+    return KD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// kd_internal.h — shared internals of libkartdiff (gfx950 / MI355X).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kartdiff.h"
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int64_t i64;
+typedef int16_t i16;
+typedef int8_t i8;
+
+namespace kd {
+
+void set_error(const char* fmt, ...);
+
+#define KD_HIP(call)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            ::kd::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+            return KD_EHIP;                                                                 \
+        }                                                                                   \
+    } while (0)
+
+#define KD_CHECK(cond, ...)            \
+    do {                               \
+        if (!(cond)) {                 \
+            ::kd::set_error(__VA_ARGS__); \
+            return KD_EINVAL;          \
+        }                              \
+    } while (0)
+
+// grow-only device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct ProfStat {
+    u64 launches = 0;
+    double ms = 0;
+};
+
+struct PendingEv {
+    std::string name;
+    hipEvent_t a, b;
+};
+
+}  // namespace kd
+
+struct kd_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::map<std::string, kd::DevBuf> bufs;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<kd::PendingEv> pending;
+    std::map<std::string, kd::ProfStat> stats;
+};
+
+namespace kd {
+
+// device scratch slot, grown as needed (never shrinks).  Not called inside timed regions once
+// kd_reserve() has sized it.
+int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out);
+
+// profiling wrappers around a launch on ctx->stream
+void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a);
+void prof_end(kd_ctx* ctx, const char* name, hipEvent_t a);
+int prof_flush(kd_ctx* ctx);
+
+template <typename F>
+inline int launch(kd_ctx* ctx, const char* name, F&& f) {
+    hipEvent_t a = nullptr;
+    if (ctx->prof) prof_begin(ctx, name, &a);
+    f();
+    hipError_t e = hipGetLastError();
+    if (ctx->prof) prof_end(ctx, name, a);
+    if (e != hipSuccess) {
+        set_error("launch %s: %s", name, hipGetErrorString(e));
+        return KD_EHIP;
+    }
+    return KD_OK;
+}
+
+// copy a host/device side array to device (returns device pointer; device input is passed through)
+int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem, const void** dev);
+
+// ---- classify2 (device form), kd_classify.hip ----
+int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
+                 u32* d_upd, u64* d_counts, u32* d_err);
+constexpr int C2_NT = 256;
+constexpr int C2_IPT = 8;
+constexpr int C2_TILE = C2_NT * C2_IPT;
+
+}  // namespace kd

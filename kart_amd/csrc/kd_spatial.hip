@@ -1,0 +1,311 @@
+// kd_spatial.hip — GPKG envelope extraction, bbox prefilter, identity-CRS index envelope,
+// EnvelopeEncoder quantisation and encoded-envelope overlap, all in FP64 on gfx950.
+//
+// Reference (file:line under /root/reference):
+//   geom_envelope ................ kart/geometry.py:638-700   (GPKG flags / envelope indicator)
+//   SpatialFilter.matches ........ kart/spatial_filter/__init__.py:534-590 (stored env, else OGR
+//                                   GetEnvelope: point -> (x,x,y,y), empty -> (0,0,0,0))
+//   bbox_intersects_fast ......... kart/spatial_filter/__init__.py:709-734
+//   get_envelope_for_indexing .... kart/spatial_filter/index.py:551-579 + transform_minmax_envelope
+//                                   :639-707 (identity CRS), _buffer_minmax_envelope :783-793,
+//                                   _wrap_lon :811-813 (Python float %)
+//   EnvelopeEncoder .............. index.py:485-548 == vendor/spatial-filter/spatial_filter.cpp:30-152
+//   cyclic_range_overlaps ........ spatial_filter.cpp:170-208
+// Built with -ffp-contract=off: `a - 0.1*b`, `n*(max-min)+min` must not fuse into FMAs.
+// One lane per geometry; each lane reads the 8-byte header + 32-byte envelope (or the 21-byte
+// point WKB) of its blob; HBM-bound.
+#include "kd_internal.h"
+
+namespace kd {
+
+__device__ __forceinline__ double ld_f64(const u8* p, bool le) {
+    u64 b = 0;
+    if (le) {
+#pragma unroll
+        for (int i = 7; i >= 0; i--) b = (b << 8) | p[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) b = (b << 8) | p[i];
+    }
+    return __longlong_as_double((i64)b);
+}
+
+__device__ __forceinline__ u32 ld_u32(const u8* p, bool le) {
+    return le ? (u32)p[0] | (u32)p[1] << 8 | (u32)p[2] << 16 | (u32)p[3] << 24
+              : (u32)p[3] | (u32)p[2] << 8 | (u32)p[1] << 16 | (u32)p[0] << 24;
+}
+
+__device__ __forceinline__ int env_size(int et) { return et == 0 ? 0 : et == 1 ? 32 : et <= 3 ? 48 : 64; }
+
+// 1 stored env, 0 None (empty / NaN), 2 no stored env, -1 malformed/unsupported
+__device__ int gpkg_env(const u8* g, u64 n, double e[4]) {
+    if (n < 8 || g[0] != 'G' || g[1] != 'P' || g[2] != 0) return -1;
+    const u8 f = g[3];
+    if (f & 0x20) return -1;
+    if (f & 0x10) return 0;
+    const int et = (f >> 1) & 7;
+    if (et > 4) return -1;
+    if (et == 0) return 2;
+    if (n < (u64)(8 + env_size(et))) return -1;
+    const bool le = f & 1;
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { e[i] = ld_f64(g + 8 + 8 * i, le); nan |= e[i] != e[i]; }
+    return nan ? 0 : 1;
+}
+
+// point WKB after the header: 1 ok (x,x,y,y), 0 empty point (NaN coords), -1 not a point
+__device__ int point_env(const u8* g, u64 n, double e[4]) {
+    const int et = (g[3] >> 1) & 7;
+    if (et > 4) return -1;
+    const u64 off = 8 + env_size(et);
+    if (n < off + 5) return -1;
+    const bool le = g[off] == 1;
+    u32 typ = ld_u32(g + off + 1, le) & 0x0fffffffu;
+    if (typ >= 1000) typ %= 1000;
+    if (typ != 1 || n < off + 21) return -1;
+    const double x = ld_f64(g + off + 5, le), y = ld_f64(g + off + 13, le);
+    if (x != x && y != y) { e[0] = e[1] = e[2] = e[3] = 0.0; return 0; }
+    e[0] = x; e[1] = x; e[2] = y; e[3] = y;
+    return 1;
+}
+
+// _range_overlaps: 1 / 0, -1 inverted range (reference raises)
+__device__ __forceinline__ int range_ov(double a1, double a2, double b1, double b2) {
+    if (a1 > a2 || b1 > b2) return -1;
+    if (b1 < a1) return b2 > a1;
+    if (a1 < b1) return a2 > b1;
+    return (b2 != b1) && (a2 != a1);
+}
+
+__device__ __forceinline__ double py_mod360(double a) {
+    double m = fmod(a, 360.0);
+    if (m != 0.0) {
+        if (m < 0) m += 360.0;  // b > 0: result takes the sign of b
+    } else {
+        m = 0.0;  // copysign(0, 360)
+    }
+    return m;
+}
+
+__device__ __forceinline__ double wrap_lon(double x) { return py_mod360(x + 180.0) - 180.0; }
+
+// encode one value (EnvelopeEncoder._encode_value); false if out of range (reference asserts)
+__device__ __forceinline__ bool enc_val(double v, double lo, double hi, double vmax, bool up, u64* out) {
+    if (!(lo <= v && v <= hi)) return false;
+    double norm = (v - lo) / (hi - lo);
+    double sc = norm * vmax;
+    double r = up ? ceil(sc) : floor(sc);
+    if (!(r >= 0 && r <= vmax)) return false;
+    *out = (u64)r;
+    return true;
+}
+
+struct EnvArgs {
+    const u8* data;
+    const u64* off;
+    u64 n;
+    double f0, f1, f2, f3;  // filter env (minx, maxx, miny, maxy)
+    int bits;
+    u8* match;
+    u8* enc;
+    u8* enc_ok;
+    unsigned long long* n_cand;
+};
+
+__global__ __launch_bounds__(256) void k_envelopes(EnvArgs a) {
+    const int nb = a.bits / 2;
+    const double vmax = (double)((1ull << a.bits) - 1);
+    u32 cand = 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (u64)gridDim.x * blockDim.x) {
+        const u64 o = a.off[i], len = a.off[i + 1] - o;
+        const u8* g = a.data + o;
+        u8 m;
+        u8 ok = 0;
+        u8 out[16] = {0};
+        if (len == 0) {
+            m = 2;
+        } else {
+            double e[4];
+            int r = gpkg_env(g, len, e);
+            bool have = false;
+            if (r == 1) have = true;
+            else if (r >= 0) {
+                if (g[3] & 0x10) { e[0] = e[1] = e[2] = e[3] = 0.0; have = true; }
+                else have = point_env(g, len, e) >= 0;
+            }
+            if (!have) m = 3;
+            else {
+                int x = range_ov(a.f0, a.f1, e[0], e[1]);
+                if (x > 0) x = range_ov(a.f2, a.f3, e[2], e[3]);
+                m = x < 0 ? 3 : (u8)x;
+                cand += x > 0;
+            }
+            // ---- index envelope (skip empties: index.py:346) ----
+            if (!(g[3] & 0x10) && r >= 0) {
+                double s[4];
+                bool src = false;
+                if (r == 1) { s[0] = e[0]; s[1] = e[1]; s[2] = e[2]; s[3] = e[3]; src = true; }
+                else if (r == 2) src = point_env(g, len, s) == 1;
+                if (src) {
+                    // transpose -> (minx, miny, maxx, maxy)
+                    const double e0 = s[0], e1 = s[2], e2 = s[1], e3 = s[3];
+                    double w, so, ea, no;
+                    bool valid = true;
+                    if (e0 == e2 && e1 == e3) {
+                        w = wrap_lon(e0); so = e1; ea = w; no = e1;
+                    } else {
+                        const double width = e2 - e0, height = e3 - e1;
+                        if (width >= 180) valid = false;
+                        double big = width;
+                        if (height > big) big = height;
+                        const double buf = big < 1.0 ? 0.1 * big : 0.1;
+                        double t1 = e1 - buf; if (-90.0 > t1) t1 = -90.0;
+                        double t3 = e3 + buf; if (90.0 < t3) t3 = 90.0;
+                        w = wrap_lon(e0 - buf); so = t1; ea = wrap_lon(e2 + buf); no = t3;
+                    }
+                    if (valid) {
+                        u64 q0, q1, q2, q3;
+                        if (enc_val(w, -180, 180, vmax, false, &q0) && enc_val(so, -90, 90, vmax, false, &q1) &&
+                            enc_val(ea, -180, 180, vmax, true, &q2) && enc_val(no, -90, 90, vmax, true, &q3)) {
+                            // 4*bits big-endian bits -> nb bytes
+                            unsigned __int128 acc = ((unsigned __int128)q0 << (3 * a.bits)) |
+                                                    ((unsigned __int128)q1 << (2 * a.bits)) |
+                                                    ((unsigned __int128)q2 << a.bits) | (unsigned __int128)q3;
+                            for (int k = nb - 1; k >= 0; k--) { out[k] = (u8)(acc & 0xFF); acc >>= 8; }
+                            ok = 1;
+                        }
+                    }
+                }
+            }
+        }
+        a.match[i] = m;
+        a.enc_ok[i] = ok;
+        u8* eo = a.enc + i * nb;
+        for (int k = 0; k < nb; k++) eo[k] = out[k];
+    }
+    // candidate count: wave reduce then one atomic per wave
+    u64 c = cand;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(a.n_cand, (unsigned long long)c);
+}
+
+__global__ __launch_bounds__(256) void k_env_overlap(const u8* __restrict__ enc, u64 n, int bits, double qw, double qs,
+                                                     double qe, double qn, u8* __restrict__ out) {
+    const int nb = bits / 2;
+    const double vmax = (double)((1ull << bits) - 1);
+    const u64 mask = (1ull << bits) - 1;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const u8* p = enc + i * nb;
+        unsigned __int128 acc = 0;
+        for (int k = 0; k < nb; k++) acc = (acc << 8) | p[k];
+        double v[4];
+        const double mins[4] = {-180, -90, -180, -90}, maxs[4] = {180, 90, 180, 90};
+        for (int k = 3; k >= 0; k--) {
+            u64 q = (u64)(acc & mask);
+            acc >>= bits;
+            double norm = (double)q / vmax;
+            v[k] = norm * (maxs[k] - mins[k]) + mins[k];
+        }
+        // cyclic_range_overlaps(w, e, qw, qe) && range_overlaps(s, n, qs, qn)
+        double a1 = v[0], a2 = v[2], b1 = qw, b2 = qe;
+        if (a1 > a2) a2 += 360;
+        if (b1 > b2) b2 += 360;
+        int r = range_ov(a1, a2, b1, b2);
+        if (r == 0) {
+            if (a1 < b1) { a1 += 360; a2 += 360; } else { b1 += 360; b2 += 360; }
+            r = range_ov(a1, a2, b1, b2);
+        }
+        if (r > 0) r = range_ov(v[1], v[3], qs, qn);
+        out[i] = r < 0 ? 2 : (u8)r;
+    }
+}
+
+}  // namespace kd
+
+using namespace kd;
+
+extern "C" {
+
+int kd_envelopes(kd_ctx* ctx, const kd_blobs* geoms, const double filt_env[4], int bits, uint8_t* match, uint8_t* enc,
+                 uint8_t* enc_ok, uint32_t out_mem, uint64_t* n_candidates) {
+    KD_CHECK(ctx && geoms && filt_env && match && enc && enc_ok, "kd_envelopes: NULL argument");
+    KD_CHECK(bits >= 2 && bits <= 32 && bits % 2 == 0, "kd_envelopes: bits must be even and <= 32");
+    KD_CHECK(filt_env[0] <= filt_env[1] && filt_env[2] <= filt_env[3], "kd_envelopes: inverted filter envelope");
+    KD_HIP(hipSetDevice(ctx->device));
+    const u64 n = geoms->n;
+    const int nb = bits / 2;
+    int rc;
+    const void *d_data, *d_off;
+    u64 bytes = geoms->mem == KD_MEM_HOST ? geoms->off[n] : 0;
+    if ((rc = stage_in(ctx, "sp.off", geoms->off, (n + 1) * 8, geoms->mem, &d_off))) return rc;
+    if ((rc = stage_in(ctx, "sp.data", geoms->data, bytes ? bytes : 1, geoms->mem, &d_data))) return rc;
+    u8 *dm = match, *de = enc, *dk = enc_ok;
+    if (out_mem == KD_MEM_HOST) {
+        void *a, *b, *c;
+        if ((rc = ensure(ctx, "sp.match", n + 1, &a)) || (rc = ensure(ctx, "sp.enc", n * nb + 1, &b)) ||
+            (rc = ensure(ctx, "sp.ok", n + 1, &c)))
+            return rc;
+        dm = (u8*)a; de = (u8*)b; dk = (u8*)c;
+    }
+    void* dc;
+    if ((rc = ensure(ctx, "sp.cnt", 8, &dc))) return rc;
+    KD_HIP(hipMemsetAsync(dc, 0, 8, ctx->stream));
+    if (n) {
+        EnvArgs a;
+        a.data = (const u8*)d_data; a.off = (const u64*)d_off; a.n = n;
+        a.f0 = filt_env[0]; a.f1 = filt_env[1]; a.f2 = filt_env[2]; a.f3 = filt_env[3];
+        a.bits = bits; a.match = dm; a.enc = de; a.enc_ok = dk; a.n_cand = (unsigned long long*)dc;
+        unsigned blocks = (unsigned)std::min<u64>((n + 255) / 256, 256ull * 32);
+        rc = launch(ctx, "k_envelopes", [&] {
+            hipLaunchKernelGGL(k_envelopes, dim3(blocks), dim3(256), 0, ctx->stream, a);
+        });
+        if (rc) return rc;
+    }
+    if (out_mem == KD_MEM_HOST || n_candidates) {
+        u64 hc = 0;
+        KD_HIP(hipMemcpyAsync(&hc, dc, 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out_mem == KD_MEM_HOST && n) {
+            KD_HIP(hipMemcpyAsync(match, dm, n, hipMemcpyDeviceToHost, ctx->stream));
+            KD_HIP(hipMemcpyAsync(enc, de, n * nb, hipMemcpyDeviceToHost, ctx->stream));
+            KD_HIP(hipMemcpyAsync(enc_ok, dk, n, hipMemcpyDeviceToHost, ctx->stream));
+        }
+        KD_HIP(hipStreamSynchronize(ctx->stream));
+        if (n_candidates) *n_candidates = hc;
+        prof_flush(ctx);
+    }
+    return KD_OK;
+}
+
+int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const double q[4], uint8_t* out, uint32_t mem) {
+    KD_CHECK(ctx && enc && q && out, "kd_env_overlap: NULL argument");
+    KD_CHECK(bits >= 2 && bits <= 32 && bits % 2 == 0, "kd_env_overlap: bad bits");
+    KD_HIP(hipSetDevice(ctx->device));
+    const int nb = bits / 2;
+    int rc;
+    const void* d_enc;
+    if ((rc = stage_in(ctx, "ov.enc", enc, n * nb + 1, mem, &d_enc))) return rc;
+    u8* d_out = out;
+    if (mem == KD_MEM_HOST) {
+        void* p;
+        if ((rc = ensure(ctx, "ov.out", n + 1, &p))) return rc;
+        d_out = (u8*)p;
+    }
+    if (n) {
+        unsigned blocks = (unsigned)std::min<u64>((n + 255) / 256, 256ull * 32);
+        rc = launch(ctx, "k_env_overlap", [&] {
+            hipLaunchKernelGGL(k_env_overlap, dim3(blocks), dim3(256), 0, ctx->stream, (const u8*)d_enc, n, bits, q[0],
+                               q[1], q[2], q[3], d_out);
+        });
+        if (rc) return rc;
+    }
+    if (mem == KD_MEM_HOST) {
+        if (n) KD_HIP(hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, ctx->stream));
+        KD_HIP(hipStreamSynchronize(ctx->stream));
+        prof_flush(ctx);
+    }
+    return KD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+"""Engine: one libkartdiff context per GPU, with numpy-in / numpy-out calls.
+
+Every method goes through the HIP library; there is no CPU implementation here.  Device-resident
+pipelines (bench.py) use ``libkartdiff`` through torch-allocated device buffers instead
+(see ``kart_amd.device``).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+
+@dataclass
+class Diff2Result:
+    n_insert: int
+    n_update: int
+    n_delete: int
+    delta: np.ndarray  # uint32 [n_delta, 2] (base sorted index | NONE, target sorted index | NONE)
+    upd: np.ndarray  # uint32 [n_update, 2]
+
+    def type_counts(self):
+        out = {}
+        for name, v in (("inserts", self.n_insert), ("updates", self.n_update), ("deletes", self.n_delete)):
+            if v:
+                out[name] = v
+        return out
+
+
+@dataclass
+class Merge3Result:
+    n_clean: int
+    conflict: np.ndarray  # uint32 [n, 3] (ancestor, ours, theirs) sorted indices | NONE
+    mdelta: np.ndarray  # uint32 [n, 2] (ours | NONE, theirs | NONE): take theirs
+
+
+class Engine:
+    def __init__(self, device=0):
+        self.L = N.lib()
+        self.ctx = ctypes.c_void_p()
+        N.check(self.L.kd_init(int(device), ctypes.byref(self.ctx)), "kd_init")
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            self.L.kd_fini(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---------------------------------------------------------------------------------------
+    def set_stream(self, stream_handle):
+        N.check(self.L.kd_set_stream(self.ctx, stream_handle), "kd_set_stream")
+
+    def sync(self):
+        N.check(self.L.kd_sync(self.ctx), "kd_sync")
+
+    def reserve(self, max_entries, max_updates=0):
+        N.check(self.L.kd_reserve(self.ctx, int(max_entries), int(max_updates)), "kd_reserve")
+
+    def prof_enable(self, on=True):
+        N.check(self.L.kd_prof_enable(self.ctx, 1 if on else 0), "kd_prof_enable")
+
+    def prof_reset(self):
+        N.check(self.L.kd_prof_reset(self.ctx), "kd_prof_reset")
+
+    def prof_get(self, name):
+        launches = ctypes.c_uint64()
+        ms = ctypes.c_double()
+        N.check(self.L.kd_prof_get(self.ctx, name.encode(), ctypes.byref(launches), ctypes.byref(ms)), "kd_prof_get")
+        return int(launches.value), float(ms.value)
+
+    # ---------------------------------------------------------------------------------------
+    def diff2(self, base, target, flags=0) -> Diff2Result:
+        """base/target: PackedSide (host) -> key-ordered delta set (kd_diff2)."""
+        sa, sb = base.kd_side(), target.kd_side()
+        res = ctypes.POINTER(N.KdDiffResult)()
+        N.check(self.L.kd_diff2(self.ctx, ctypes.byref(sa), ctypes.byref(sb), flags, ctypes.byref(res)), "kd_diff2")
+        try:
+            r = res.contents
+            nd, nu = int(r.n_delta), int(r.n_update)
+            delta = np.ctypeslib.as_array(r.delta, (nd * 2,)).reshape(nd, 2).copy() if nd else np.zeros((0, 2), np.uint32)
+            upd = np.ctypeslib.as_array(r.upd, (nu * 2,)).reshape(nu, 2).copy() if nu else np.zeros((0, 2), np.uint32)
+            return Diff2Result(int(r.n_insert), nu, int(r.n_delete), delta, upd)
+        finally:
+            self.L.kd_free(res)
+
+    def fielddiff(self, old_data, old_off, new_data, new_off, pairs, maps):
+        """Blob arenas (uint8 data, uint64 off[n+1]) per side; pairs uint32 [n, 2] (old blob,
+        new blob) or None (blob u on both sides); maps: schema.FieldMaps.
+        Returns (masks uint64 [n, words], status uint8 [n])."""
+        old_data = np.ascontiguousarray(old_data, np.uint8)
+        new_data = np.ascontiguousarray(new_data, np.uint8)
+        old_off = np.ascontiguousarray(old_off, np.uint64)
+        new_off = np.ascontiguousarray(new_off, np.uint64)
+        n = int(pairs.shape[0]) if pairs is not None else int(old_off.shape[0]) - 1
+        if pairs is not None:
+            pairs = np.ascontiguousarray(pairs, np.uint32)
+        ob, nb = N.KdBlobs(), N.KdBlobs()
+        for b, d, o in ((ob, old_data, old_off), (nb, new_data, new_off)):
+            b.n = int(o.shape[0]) - 1
+            b.data = N.ptr(d) if d.size else N.ptr(np.zeros(1, np.uint8))
+            b.off = N.ptr(o)
+            b.mem = N.KD_MEM_HOST
+        masks = np.zeros((max(n, 1), maps.words), np.uint64)
+        status = np.zeros(max(n, 1), np.uint8)
+        km = maps.kd_maps()
+        N.check(
+            self.L.kd_fielddiff(self.ctx, ctypes.byref(ob), ctypes.byref(nb), N.ptr(pairs), n, None, N.KD_MEM_HOST,
+                                ctypes.byref(km), N.ptr(masks), N.ptr(status), N.KD_MEM_HOST),
+            "kd_fielddiff",
+        )
+        return masks[:n], status[:n]
+
+    def merge3(self, ancestor, ours, theirs, flags=0) -> Merge3Result:
+        sa, so, st = ancestor.kd_side(), ours.kd_side(), theirs.kd_side()
+        res = ctypes.POINTER(N.KdMergeResult)()
+        N.check(self.L.kd_merge3(self.ctx, ctypes.byref(sa), ctypes.byref(so), ctypes.byref(st), flags,
+                                 ctypes.byref(res)), "kd_merge3")
+        try:
+            r = res.contents
+            nc, nm = int(r.n_conflict), int(r.n_mdelta)
+            conf = np.ctypeslib.as_array(r.conflict, (nc * 3,)).reshape(nc, 3).copy() if nc else np.zeros((0, 3), np.uint32)
+            md = np.ctypeslib.as_array(r.mdelta, (nm * 2,)).reshape(nm, 2).copy() if nm else np.zeros((0, 2), np.uint32)
+            return Merge3Result(int(r.n_clean), conf, md)
+        finally:
+            self.L.kd_free(res)
+
+    def envelopes(self, data, off, filt_env, bits=20):
+        """GPKG geometry blobs -> (match u8[n], enc u8[n, bits/2], enc_ok u8[n], n_candidates)."""
+        data = np.ascontiguousarray(data, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        n = int(off.shape[0]) - 1
+        g = N.KdBlobs()
+        g.n = n
+        g.data = N.ptr(data) if data.size else N.ptr(np.zeros(1, np.uint8))
+        g.off = N.ptr(off)
+        g.mem = N.KD_MEM_HOST
+        nb = bits // 2
+        match = np.zeros(max(n, 1), np.uint8)
+        enc = np.zeros((max(n, 1), nb), np.uint8)
+        ok = np.zeros(max(n, 1), np.uint8)
+        fe = (ctypes.c_double * 4)(*[float(x) for x in filt_env])
+        ncand = ctypes.c_uint64()
+        N.check(self.L.kd_envelopes(self.ctx, ctypes.byref(g), fe, int(bits), N.ptr(match), N.ptr(enc), N.ptr(ok),
+                                    N.KD_MEM_HOST, ctypes.byref(ncand)), "kd_envelopes")
+        return match[:n], enc[:n], ok[:n], int(ncand.value)
+
+    def env_overlap(self, enc, bits, q):
+        enc = np.ascontiguousarray(enc, np.uint8)
+        n = enc.shape[0]
+        out = np.zeros(max(n, 1), np.uint8)
+        qq = (ctypes.c_double * 4)(*[float(x) for x in q])
+        N.check(self.L.kd_env_overlap(self.ctx, N.ptr(enc) if enc.size else N.ptr(np.zeros(1, np.uint8)), n, int(bits),
+                                      qq, N.ptr(out), N.KD_MEM_HOST), "kd_env_overlap")
+        return out[:n]

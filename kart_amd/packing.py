@@ -1,0 +1,185 @@
+"""Packing one commit's dataset feature tree into the engine's flat, key-sorted side arrays.
+
+A *side* is what ``RichBaseDataset.diff_feature`` hands to libgit2 implicitly: the leaves under
+``<ds>/.table-dataset/feature/`` of one commit (kart/rich_base_dataset.py:212-232).  Here they
+become SoA arrays in join-key order (DESIGN.md "join key"):
+
+* ``KD_KEY_INT`` (IntPathEncoder, kart/dataset3_paths.py:283-299): the filename is
+  ``b64(msgpack([pk]))``; key = bucket24 | wrap34 | pk%64 — bijective with the pk, so equal keys
+  are equal paths and the pk is recovered from the key without touching the filename again.
+* ``KD_KEY_HASH`` (MsgpackHashPathEncoder, :202-215, and the 2x256 hex legacy layout): key = the
+  tree levels as a bucket number | FNV-1a bits of the filename; the GPU verifies filenames of
+  matched keys, a collision returns KD_EUNSUPPORTED.
+
+Packing runs on the CPU in the native library (kd_pack_*), multithreaded.
+"""
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+
+
+@dataclass
+class PathEncoding:
+    """The dataset's path-structure.json (kart/dataset3_paths.py:121-130,474-486)."""
+
+    scheme: str = "int"  # "int" | "msgpack/hash"
+    levels: int = 4
+    branches: int = 64
+    encoding: str = "base64"  # "base64" | "hex"
+
+    @classmethod
+    def from_dict(cls, d):
+        if d is None:  # no path-structure.json -> LEGACY_ENCODER (kart/dataset3.py:233-248)
+            return cls("msgpack/hash", 2, 256, "hex")
+        return cls(d["scheme"], int(d["levels"]), int(d["branches"]), d["encoding"])
+
+    @property
+    def key_mode(self):
+        return N.KD_KEY_INT if self.scheme == "int" else N.KD_KEY_HASH
+
+    def to_dict(self):
+        return {"scheme": self.scheme, "branches": self.branches, "levels": self.levels, "encoding": self.encoding}
+
+
+INT_PK_ENCODING = PathEncoding("int", 4, 64, "base64")
+GENERAL_ENCODING = PathEncoding("msgpack/hash", 4, 64, "base64")
+LEGACY_ENCODING = PathEncoding("msgpack/hash", 2, 256, "hex")
+
+
+def _arena(strings):
+    """list[bytes|str] -> (uint8 arena, int64 offsets[n+1])"""
+    bs = [s.encode() if isinstance(s, str) else s for s in strings]
+    off = np.zeros(len(bs) + 1, np.uint64)
+    if bs:
+        off[1:] = np.cumsum(np.fromiter((len(b) for b in bs), np.uint64, len(bs)))
+    data = np.frombuffer(b"".join(bs), np.uint8) if bs else np.zeros(0, np.uint8)
+    return data, off
+
+
+def basenames(paths, path_off):
+    """Filename start offsets inside a relative-path arena ('c/c/c/c/<name>')."""
+    n = len(path_off) - 1
+    starts = np.empty(n, np.uint64)
+    for i in range(n):
+        a, b = int(path_off[i]), int(path_off[i + 1])
+        j = paths[a:b].tobytes().rfind(b"/")
+        starts[i] = a + j + 1
+    return starts
+
+
+@dataclass
+class PackedSide:
+    """Key-sorted side arrays (host memory).  ``order[k]`` = index of sorted entry k in the
+    caller's original entry order, so results map back to the caller's paths/blobs."""
+
+    key: np.ndarray  # uint64 [n], strictly ascending
+    oid: np.ndarray  # uint8 [n, 20]
+    key_mode: int
+    order: np.ndarray  # int64 [n]
+    name: Optional[np.ndarray] = None  # uint8 arena (KD_KEY_HASH: relative paths, sorted order)
+    name_off: Optional[np.ndarray] = None  # uint64 [n+1]
+    encoding: PathEncoding = field(default_factory=lambda: INT_PK_ENCODING)
+
+    @property
+    def n(self):
+        return int(self.key.shape[0])
+
+    def kd_side(self):
+        s = N.KdSide()
+        s.n = self.n
+        s.key = N.ptr(self.key)
+        s.oid = N.ptr(self.oid)
+        s.name = N.ptr(self.name) if self.name is not None and self.name.size else None
+        s.name_off = N.ptr(self.name_off) if self.name_off is not None else None
+        s.mem = N.KD_MEM_HOST
+        s.key_mode = self.key_mode
+        return s
+
+    def rel_path(self, k):
+        """relative path ('c/c/c/c/<filename>') of sorted entry k (KD_KEY_HASH sides)"""
+        a, b = int(self.name_off[k]), int(self.name_off[k + 1])
+        return self.name[a:b].tobytes().decode()
+
+
+class PackError(ValueError):
+    pass
+
+
+def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None):
+    """Pack leaves: rel_paths = list[str] (relative to feature/) or a uint8 arena with
+    ``rel_off``; oids = uint8 [n, 20].  Returns PackedSide.  Raises PackError on paths that are
+    not valid for the encoding (the caller falls back to the reference path)."""
+    if rel_off is None:
+        paths, off = _arena(rel_paths)
+    else:
+        paths, off = np.ascontiguousarray(rel_paths, np.uint8), np.ascontiguousarray(rel_off, np.uint64)
+    n = len(off) - 1
+    oids = np.ascontiguousarray(oids, np.uint8).reshape(n, 20)
+    keys = np.empty(n, np.uint64)
+    status = np.empty(n, np.uint8)
+    L = N.lib()
+    if encoding.key_mode == N.KD_KEY_INT:
+        starts = basenames(paths, off)
+        # contiguous filename arena for the native packer
+        names = [paths[int(starts[i]):int(off[i + 1])].tobytes() for i in range(n)]
+        nd, noff = _arena(names)
+        bad = L.kd_pack_int_keys(N.ptr(nd) if nd.size else None, N.ptr(noff), n, N.ptr(keys), N.ptr(status))
+    else:
+        hex_ = 1 if encoding.encoding == "hex" else 0
+        glen = 2 if hex_ else 1
+        levels = encoding.levels if encoding.branches in (64, 256) else encoding.levels
+        if (hex_ and encoding.branches != 256) or (not hex_ and encoding.branches != 64):
+            raise PackError(f"unsupported path structure {encoding}")
+        del glen
+        bad = L.kd_pack_hash_keys(N.ptr(paths) if paths.size else None, N.ptr(off), n, levels, hex_,
+                                  N.ptr(keys), N.ptr(status))
+    if bad < 0:
+        N.check(int(bad), "pack")
+    if bad:
+        i = int(np.nonzero(status)[0][0])
+        raise PackError(f"{bad} feature paths not packable, first: {paths[int(off[i]):int(off[i+1])].tobytes()!r}")
+    order = np.argsort(keys, kind="stable")
+    keys = keys[order]
+    if n > 1 and not np.all(keys[1:] > keys[:-1]):
+        raise PackError("duplicate join keys within one side")
+    side = PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(oids[order]),
+                      key_mode=encoding.key_mode, order=order.astype(np.int64), encoding=encoding)
+    if encoding.key_mode == N.KD_KEY_HASH:
+        # sorted relative-path arena (needed for collision verification + pk decode)
+        lens = (off[1:] - off[:-1])[order]
+        noff = np.zeros(n + 1, np.uint64)
+        noff[1:] = np.cumsum(lens)
+        idx = np.concatenate([np.arange(int(off[i]), int(off[i + 1])) for i in order]) if n else np.zeros(0, np.int64)
+        side.name = np.ascontiguousarray(paths[idx]) if n else np.zeros(0, np.uint8)
+        side.name_off = noff
+    return side
+
+
+def empty_side(encoding: PathEncoding):
+    s = PackedSide(key=np.zeros(0, np.uint64), oid=np.zeros((0, 20), np.uint8), key_mode=encoding.key_mode,
+                   order=np.zeros(0, np.int64), encoding=encoding)
+    if encoding.key_mode == N.KD_KEY_HASH:
+        s.name = np.zeros(0, np.uint8)
+        s.name_off = np.zeros(1, np.uint64)
+    return s
+
+
+def int_keys_to_pks(keys):
+    keys = np.ascontiguousarray(keys, np.uint64)
+    out = np.empty(keys.shape[0], np.int64)
+    N.check(N.lib().kd_int_keys_to_pks(N.ptr(keys), keys.shape[0], N.ptr(out)), "int_keys_to_pks")
+    return out
+
+
+def pk_to_int_key(pk):
+    """Python-int pk -> KD_KEY_INT key (same formula as the native packer)."""
+    q = pk // 64
+    r = pk - q * 64
+    bucket = q % (1 << 24)
+    k = pk // (1 << 30) + (1 << 33)
+    if not 0 <= k < (1 << 34):
+        raise PackError(f"pk {pk} outside [-2**63, 2**63)")
+    return (bucket << 40) | (k << 6) | r
