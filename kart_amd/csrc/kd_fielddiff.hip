@@ -311,7 +311,10 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     std::memcpy(&h[o_nv], nvo.data(), (size_t)nlo * 4);
     void* dt;
     if ((rc = ensure(ctx, "fd.tab", o_end, &dt))) return rc;
-    KD_HIP(hipMemcpyAsync(dt, h.data(), o_end, hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->fd_tab != h) {
+        ctx->fd_tab.swap(h);  // keep the source alive until the stream has consumed it
+        KD_HIP(hipMemcpyAsync(dt, ctx->fd_tab.data(), o_end, hipMemcpyHostToDevice, ctx->stream));
+    }
     FdTab tb;
     tb.n_keys = nk; tb.words = W; tb.n_lo = nlo; tb.n_ln = nln; tb.maxv = maxv;
     const u8* base = (const u8*)dt;

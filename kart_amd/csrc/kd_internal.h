@@ -68,6 +68,9 @@ struct kd_ctx {
     std::vector<hipEvent_t> ev_pool;
     std::vector<kd::PendingEv> pending;
     std::map<std::string, kd::ProfStat> stats;
+    // last uploaded kd_fielddiff table (host copy kept alive for the async upload, and reused
+    // when the next call's tables are identical)
+    std::vector<uint8_t> fd_tab;
 };
 
 namespace kd {

@@ -1,0 +1,236 @@
+"""HIP path (libkartdiff on an MI355X) vs the reference's golden outputs and the CPU oracle.
+
+Every comparison is bit-exact: delta sets, update lists, changed-field masks, conflict sets,
+encoded envelopes and match flags are integer / byte results.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from checks import check_diff_case, check_merge_case
+from fixtures import DIFF_FIXTURES, GOLDEN, MERGE_FIXTURES, load
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _g_classify(engine):
+    def f(A, B):
+        r = engine.diff2(A, B)
+        return r.delta, r.upd, r.type_counts()
+
+    return f
+
+
+@pytest.mark.parametrize("name", DIFF_FIXTURES)
+def test_gpu_diff2_golden(engine, name):
+    fx = load(name)
+    for case in fx.cases("diff2"):
+        check_diff_case(fx, case, _g_classify(engine), engine.fielddiff)
+
+
+@pytest.mark.parametrize("name", MERGE_FIXTURES)
+def test_gpu_merge3_golden(engine, name):
+    fx = load(name)
+    (case,) = fx.cases("merge3")
+
+    def m(A, O_, T):
+        r = engine.merge3(A, O_, T)
+        return r.conflict, r.mdelta, r.n_clean
+
+    check_merge_case(fx, case, m)
+
+
+def test_gpu_spatial_points_golden(engine):
+    from test_oracle_golden import _arena, _geoms_of_side
+
+    fx = load("repo_points")
+    sp = fx.meta["spatial"]
+    geoms, names = _geoms_of_side(fx, sp["side"])
+    data, off = _arena(geoms)
+    match, enc, ok, ncand = engine.envelopes(data, off, sp["filter_env"], 20)
+    assert sorted(n for n, m in zip(names, match) if m == 1) == sorted(sp["matching_names"])
+    assert ncand == 13
+    om, oe, ook, _ = O.envelope_batch(data, off, sp["filter_env"], 20)
+    assert np.array_equal(match, om) and np.array_equal(ok, ook) and np.array_equal(enc, oe)
+
+
+# ------------------------------------------------------------------------------------------
+# size-scaled parity vs the oracle on seeded synthetic layers
+@pytest.mark.parametrize("n,seed", [(0, 1), (1, 2), (5000, 3), (300_000, 4), (2_000_000, 5)])
+def test_gpu_diff2_synthetic_vs_oracle(engine, n, seed):
+    from kart_amd import synth
+
+    L = synth.points_layer(n, seed=seed)
+    r = engine.diff2(L.base, L.target)
+    od, counts = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
+    assert np.array_equal(r.delta, od)
+    assert (r.n_insert, r.n_update, r.n_delete) == (counts["inserts"], counts["updates"], counts["deletes"])
+    assert (r.n_insert, r.n_update, r.n_delete) == (L.n_insert, L.n_update, L.n_delete)
+    if r.upd.shape[0]:
+        from kart_amd.schema import FieldMaps
+
+        maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+        gm, gs = engine.fielddiff(*L.base_blobs, *L.target_blobs, r.upd, maps)
+        om, os_ = O.fielddiff(*L.base_blobs, *L.target_blobs, r.upd, maps)
+        assert np.array_equal(gm, om) and np.array_equal(gs, os_)
+        assert not gs.any()
+
+
+def _edge_sides(rng, nA, nB, overlap, change):
+    """random strictly-ascending key sets with controlled overlap / OID changes"""
+    universe = np.unique(rng.integers(0, 2**63, size=int((nA + nB) * 1.5) + 10, dtype=np.uint64))
+    rng.shuffle(universe)
+    common = universe[: int(min(nA, nB) * overlap)]
+    onlyA = universe[len(common): len(common) + nA - len(common)]
+    onlyB = universe[len(common) + len(onlyA): len(common) + len(onlyA) + nB - len(common)]
+    kA = np.sort(np.concatenate([common, onlyA]))
+    kB = np.sort(np.concatenate([common, onlyB]))
+    oA = rng.integers(0, 256, size=(kA.size, 20), dtype=np.uint8)
+    oB = np.zeros((kB.size, 20), np.uint8)
+    # same OID for common keys unless changed
+    posA = {int(k): i for i, k in enumerate(kA)}
+    oB[:] = rng.integers(0, 256, size=oB.shape, dtype=np.uint8)
+    for j, k in enumerate(kB):
+        i = posA.get(int(k))
+        if i is not None and rng.random() >= change:
+            oB[j] = oA[i]
+    return kA, oA, kB, oB
+
+
+@pytest.mark.parametrize("nA,nB,overlap,change", [(10, 0, 0, 0), (0, 10, 0, 0), (3000, 3000, 1.0, 0.0),
+                                                  (3000, 3000, 1.0, 1.0), (5000, 200, 0.5, 0.3),
+                                                  (200, 5000, 0.5, 0.3), (40000, 40000, 0.0, 0.0),
+                                                  (60000, 50000, 0.9, 0.05)])
+def test_gpu_diff2_edges_vs_oracle(engine, nA, nB, overlap, change):
+    """merge-path tile seams: long one-sided runs, all-equal, all-changed, disjoint sets"""
+    from kart_amd import packing
+
+    rng = np.random.default_rng(nA * 7 + nB)
+    kA, oA, kB, oB = _edge_sides(rng, nA, nB, overlap, change)
+    A = packing.PackedSide(kA, oA, 0, np.arange(kA.size))
+    B = packing.PackedSide(kB, oB, 0, np.arange(kB.size))
+    r = engine.diff2(A, B)
+    od, counts = O.classify2(kA, oA, kB, oB)
+    assert np.array_equal(r.delta, od)
+    assert r.n_update == counts["updates"]
+
+
+def test_gpu_diff2_rejects_unsorted(engine):
+    from kart_amd import _native as N
+    from kart_amd import packing
+
+    k = np.array([5, 3, 9], np.uint64)
+    A = packing.PackedSide(k, np.zeros((3, 20), np.uint8), 0, np.arange(3))
+    B = packing.PackedSide(np.array([1, 2], np.uint64), np.zeros((2, 20), np.uint8), 0, np.arange(2))
+    with pytest.raises(N.Unsupported):
+        engine.diff2(A, B)
+
+
+@pytest.mark.parametrize("n", [1000, 200_000])
+def test_gpu_merge3_synthetic_vs_oracle(engine, n):
+    from kart_amd import packing
+
+    rng = np.random.default_rng(n)
+    kA = np.unique(rng.integers(0, 2**62, size=n, dtype=np.uint64))
+    oA = rng.integers(0, 256, size=(kA.size, 20), dtype=np.uint8)
+
+    def edit(seed):
+        r = np.random.default_rng(seed)
+        keep = r.random(kA.size) > 0.005
+        k = kA[keep]
+        o = oA[keep].copy()
+        ch = r.random(k.size) < 0.05
+        o[ch] = r.integers(0, 256, size=(int(ch.sum()), 20), dtype=np.uint8)
+        ins = r.integers(0, 2**62, size=kA.size // 200, dtype=np.uint64)
+        k2 = np.concatenate([k, ins])
+        o2 = np.concatenate([o, r.integers(0, 256, size=(ins.size, 20), dtype=np.uint8)])
+        k2, idx = np.unique(k2, return_index=True)
+        return k2, np.ascontiguousarray(o2[idx])
+
+    kO, oO = edit(1)
+    kT, oT = edit(2)
+    # overlapping edits: same keys changed identically on both sides (clean) and differently (conflict)
+    common = np.intersect1d(kO, kT)
+    pick = rng.choice(common, size=min(50, common.size), replace=False)
+    iO, iT = np.searchsorted(kO, pick), np.searchsorted(kT, pick)
+    same = rng.integers(0, 256, size=(pick.size, 20), dtype=np.uint8)
+    oO[iO] = same
+    oT[iT[: pick.size // 2]] = same[: pick.size // 2]
+    sides = [packing.PackedSide(k, o, 0, np.arange(k.size)) for k, o in ((kA, oA), (kO, oO), (kT, oT))]
+    r = engine.merge3(*sides)
+    oc, om, oclean = O.classify3(kA, oA, kO, oO, kT, oT)
+    key = lambda rows: sorted(map(tuple, rows.tolist()))
+    assert key(r.conflict) == key(oc)
+    assert key(r.mdelta) == key(om)
+    assert r.n_clean == oclean
+
+
+def _gpkg_blobs(rng, n):
+    """mixed GPKG geometries: XY/XYZ envelopes (LE/BE), points without envelope, empties,
+    NaN envelopes, antimeridian/wide envelopes, null geometries, one malformed blob"""
+    import struct
+
+    out = []
+    for i in range(n):
+        r = rng.random()
+        if r < 0.02:
+            out.append(b"")
+            continue
+        if r < 0.35:
+            le = rng.random() < 0.9
+            bo = "<" if le else ">"
+            x, y = rng.uniform(-200, 200), rng.uniform(-95, 95)
+            if rng.random() < 0.02:
+                x = y = float("nan")
+            flags = 1 if le else 0
+            if rng.random() < 0.02:
+                flags |= 0x10
+            out.append(b"GP\x00" + bytes([flags]) + struct.pack(bo + "i", 4326) + struct.pack(bo + "bI", 1 if le else 0, 1)
+                       + struct.pack(bo + "dd", x, y))
+            continue
+        le = rng.random() < 0.85
+        bo = "<" if le else ">"
+        et = 1 if rng.random() < 0.8 else 2
+        minx = rng.uniform(-180, 180)
+        w = 10 ** rng.uniform(-7, 2.6)
+        miny = rng.uniform(-90, 90)
+        h = 10 ** rng.uniform(-7, 1.5)
+        env = [minx, minx + w, miny, miny + h] + ([0.0, 1.0] if et == 2 else [])
+        if rng.random() < 0.01:
+            env[1] = float("nan")
+        flags = (1 if le else 0) | (et << 1)
+        if rng.random() < 0.01:
+            flags |= 0x10
+        body = struct.pack(bo + "bI", 1 if le else 0, 6) + b"\x00" * 16
+        out.append(b"GP\x00" + bytes([flags]) + struct.pack(bo + "i", 4326) + struct.pack(bo + "d" * len(env), *env) + body)
+    out.append(b"GX\x00\x01")  # malformed
+    return out
+
+
+@pytest.mark.parametrize("bits", [20, 16, 32, 8])
+def test_gpu_envelopes_vs_oracle(engine, bits):
+    from test_oracle_golden import _arena
+
+    rng = np.random.default_rng(bits)
+    geoms = _gpkg_blobs(rng, 20000)
+    data, off = _arena(geoms)
+    for filt in [(175.8, 175.9, -37.1, -36.9), (-10.0, 10.0, -5.0, 5.0), (-180.0, 180.0, -90.0, 90.0), (0.0, 0.0, 0.0, 0.0)]:
+        gm, ge, gk, gc = engine.envelopes(data, off, filt, bits)
+        om, oe, ok, oc = O.envelope_batch(data, off, filt, bits)
+        assert np.array_equal(gm, om)
+        assert np.array_equal(gk, ok)
+        assert np.array_equal(ge, oe)
+        assert gc == oc
+
+
+def test_gpu_env_overlap_vs_oracle(engine):
+    with open(os.path.join(GOLDEN, "envelopes.json")) as f:
+        E = json.load(f)
+    enc = np.array([list(bytes.fromhex(h)) for h, _ in E["decode"]], np.uint8)
+    for q in E["queries"]:
+        g = engine.env_overlap(enc, 20, q)
+        o = O.envelope_overlap(enc, 20, q)
+        assert np.array_equal(g, o)
