@@ -60,7 +60,7 @@ class KdBlobs(ctypes.Structure):
         ("data", ctypes.c_void_p),
         ("off", ctypes.c_void_p),
         ("mem", ctypes.c_uint32),
-        ("_pad", ctypes.c_uint32),
+        ("size_hint", ctypes.c_uint32),
     ]
 
 

@@ -1,371 +1,19 @@
-// kd_classify.hip — classify2 (two-way tree diff) and classify3 (three-way merge) on gfx950.
+// kd_classify.hip — classify3 (three-way merge) on gfx950 + the host-form C API of both joins.
+// (classify2's kernels live in kd_classify2.hip.)
 //
 // classify2 replaces libgit2's tree-to-tree diff as consumed by RichBaseDataset.diff_feature
 // (/root/reference/kart/rich_base_dataset.py:205-300): both commits' feature leaves arrive as
 // strictly ascending join keys + 20-byte blob OIDs; a pair present on one side only is an
 // insert/delete, a pair present on both with different OIDs is an update.
 //
-// Kernels (one pass over the inputs, HBM-bound; no MFMA):
-//   k_partition2  merge-path split points of the union sequence, one thread per tile boundary
-//   k_join2       per 2048-item tile: keys -> LDS, per-thread merge path, striped OID compare
-//                 (consecutive lanes read consecutive 20-B OIDs), ordered compaction of the
-//                 tile's deltas + updates into a tile-local staging slot
-//   k_scan_tiles  exclusive scan of the per-tile counts (one workgroup)
-//   k_scatter2    tile-local staging -> final key-ordered delta / update lists
+// (kernels: kd_classify2.hip)
 //
 // classify3 replaces libgit2 git_merge_trees (kart/merge.py:99-100): key-range tiles cut on the
 // ancestor∪ours merge path, theirs split by lower_bound; per item LDS binary searches find the
 // (ancestor, ours, theirs) triple and the libgit2 OID rule classifies it.
-#include "kd_internal.h"
+#include "kd_join.h"
 
 namespace kd {
-
-__device__ __forceinline__ bool oid_ne(const u32* __restrict__ x, const u32* __restrict__ y) {
-    return ((x[0] ^ y[0]) | (x[1] ^ y[1]) | (x[2] ^ y[2]) | (x[3] ^ y[3]) | (x[4] ^ y[4])) != 0;
-}
-
-__device__ bool names_eq(const u8* __restrict__ na, const u64* __restrict__ oa, u64 i, const u8* __restrict__ nb,
-                         const u64* __restrict__ ob, u64 j) {
-    u64 a0 = oa[i], a1 = oa[i + 1], b0 = ob[j], b1 = ob[j + 1];
-    if (a1 - a0 != b1 - b0) return false;
-    for (u64 k = 0; k < a1 - a0; k++)
-        if (na[a0 + k] != nb[b0 + k]) return false;
-    return true;
-}
-
-// --------------------------------------------------------------------------------------------
-// merge-path partition: part[t] = number of A items among the first min(t*TILE, nA+nB) items of
-// the union order (ties: A first).
-__global__ void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B, u64 nB,
-                             u64 ntiles, u64* __restrict__ part) {
-    u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    u64 total = nA + nB;
-    u64 d = t * (u64)C2_TILE;
-    if (d > total) d = total;
-    u64 lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
-    while (lo < hi) {
-        u64 mid = (lo + hi) >> 1;
-        if (A[mid] <= B[d - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    part[t] = lo;
-}
-
-// block-wide exclusive scan of one u32 per thread; returns the block total via *total
-template <int NT>
-__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* s_wave, u32* total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    u32 x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        u32 y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wave[wid] = x;
-    __syncthreads();
-    u32 wpre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; w++) {
-        u32 s = s_wave[w];
-        if (w < wid) wpre += s;
-        tot += s;
-    }
-    __syncthreads();
-    *total = tot;
-    return wpre + x - v;
-}
-
-template <int NT>
-__device__ __forceinline__ u32 block_sum(u32 v, u32* s_wave) {
-    u32 tot;
-    block_excl_scan<NT>(v, s_wave, &tot);
-    return tot;
-}
-
-struct Join2Args {
-    const u64* A;
-    const u32* oidA;
-    u64 nA;
-    const u64* B;
-    const u32* oidB;
-    u64 nB;
-    const u64* part;
-    const u8* nameA;
-    const u64* nameOffA;
-    const u8* nameB;
-    const u64* nameOffB;
-    int hash_mode;
-    uint2* stage_delta;
-    uint2* stage_upd;
-    u32* tile_cnt;  // [ntiles*4]: inserts, updates, deletes, deltas
-    u32* err;
-};
-
-template <int NT, int IPT>
-__global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
-    constexpr int TILE = NT * IPT;
-    constexpr u16 NOP = 0xFFFF;
-    __shared__ u64 sk[TILE];
-    __shared__ u16 s_partner[TILE];
-    __shared__ u8 s_chg[TILE];
-    __shared__ u32 s_wave[NT / 64];
-
-    const int tid = threadIdx.x;
-    const u64 tile = blockIdx.x;
-    const u64 total = g.nA + g.nB;
-    const u64 d0 = tile * (u64)TILE;
-    const u64 d1 = d0 + TILE < total ? d0 + TILE : total;
-    const u64 i0 = g.part[tile], i1 = g.part[tile + 1];
-    if (i1 < i0 || d1 - i1 < d0 - i0 || i1 - i0 > d1 - d0) {  // only on unsorted input
-        if (tid == 0) atomicOr(g.err, 1u);
-        if (tid == 0) { u32* c = g.tile_cnt + 4 * tile; c[0] = c[1] = c[2] = c[3] = 0; }
-        return;
-    }
-    const u64 j0 = d0 - i0, j1 = d1 - i1;
-    const int na = (int)(i1 - i0), nb = (int)(j1 - j0);
-    const bool has_lbA = i0 > 0, has_lbB = j0 > 0, has_la = j1 < g.nB;
-    const u64 lbA = has_lbA ? g.A[i0 - 1] : 0;
-    const u64 lbB = has_lbB ? g.B[j0 - 1] : 0;
-    const u64 la = has_la ? g.B[j1] : 0;
-
-    for (int x = tid; x < na + nb; x += NT) sk[x] = x < na ? g.A[i0 + x] : g.B[j0 + (x - na)];
-    __syncthreads();
-    const u64* sA = sk;
-    const u64* sB = sk + na;
-
-    // ---- phase A: per-thread merge path; record each A item's partner --------------------------
-    const int nitems = na + nb;
-    const int dd = tid * IPT < nitems ? tid * IPT : nitems;
-    const int cnt = (dd + IPT < nitems ? dd + IPT : nitems) - dd;
-    int lo = dd - nb > 0 ? dd - nb : 0, hi = dd < na ? dd : na;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (sA[mid] <= sB[dd - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    const int ia0 = lo, jb0 = dd - lo;
-    bool bad = false;
-    {
-        int ia = ia0, jb = jb0;
-        for (int k = 0; k < IPT; k++) {
-            if (k >= cnt) break;
-            if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
-                u64 ka = sA[ia];
-                if (ia > 0 ? sA[ia - 1] >= ka : (has_lbA && lbA >= ka)) bad = true;
-                bool hb = jb < nb ? true : has_la;
-                u64 kb = jb < nb ? sB[jb] : la;
-                s_partner[ia] = (hb && kb == ka) ? (u16)jb : NOP;
-                ia++;
-            } else {
-                u64 kb = sB[jb];
-                if (jb > 0 ? sB[jb - 1] >= kb : (has_lbB && lbB >= kb)) bad = true;
-                jb++;
-            }
-        }
-    }
-    if (bad) atomicOr(g.err, 1u);
-    __syncthreads();
-
-    // ---- phase B: striped OID compare of matched pairs (coalesced 20-B records) -----------------
-    for (int a = tid; a < na; a += NT) {
-        u16 p = s_partner[a];
-        u8 chg = 0;
-        if (p != NOP) {
-            const u64 ia = i0 + a, jb = j0 + p;
-            chg = oid_ne(g.oidA + ia * 5, g.oidB + jb * 5) ? 1 : 0;
-            if (g.hash_mode && !names_eq(g.nameA, g.nameOffA, ia, g.nameB, g.nameOffB, jb)) atomicOr(g.err, 2u);
-        }
-        s_chg[a] = chg;
-    }
-    __syncthreads();
-
-    // ---- phase C: ordered compaction ------------------------------------------------------------
-    u32 nd = 0, nu = 0, ndel = 0;
-    {
-        int ia = ia0, jb = jb0;
-        for (int k = 0; k < IPT; k++) {
-            if (k >= cnt) break;
-            if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
-                u16 p = s_partner[ia];
-                if (p == NOP) { nd++; ndel++; }
-                else if (s_chg[ia]) { nd++; nu++; }
-                ia++;
-            } else {
-                u64 kb = sB[jb];
-                bool partner = ia > 0 ? sA[ia - 1] == kb : (has_lbA && lbA == kb);
-                if (!partner) nd++;
-                jb++;
-            }
-        }
-    }
-    u32 tot_packed;
-    const u32 off_packed = block_excl_scan<NT>(nd | (nu << 16), s_wave, &tot_packed);
-    const u32 tot_del = block_sum<NT>(ndel, s_wave);
-    u32 od = off_packed & 0xFFFF, ou = off_packed >> 16;
-    uint2* sd = g.stage_delta + tile * (u64)TILE;
-    uint2* su = g.stage_upd + tile * (u64)TILE;
-    {
-        int ia = ia0, jb = jb0;
-        for (int k = 0; k < IPT; k++) {
-            if (k >= cnt) break;
-            if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
-                u16 p = s_partner[ia];
-                if (p == NOP) sd[od++] = make_uint2((u32)(i0 + ia), KD_NONE);
-                else if (s_chg[ia]) {
-                    uint2 v = make_uint2((u32)(i0 + ia), (u32)(j0 + p));
-                    sd[od++] = v;
-                    su[ou++] = v;
-                }
-                ia++;
-            } else {
-                u64 kb = sB[jb];
-                bool partner = ia > 0 ? sA[ia - 1] == kb : (has_lbA && lbA == kb);
-                if (!partner) sd[od++] = make_uint2(KD_NONE, (u32)(j0 + jb));
-                jb++;
-            }
-        }
-    }
-    if (tid == 0) {
-        u32 tnd = tot_packed & 0xFFFF, tnu = tot_packed >> 16;
-        u32* c = g.tile_cnt + 4 * tile;
-        c[0] = tnd - tnu - tot_del;
-        c[1] = tnu;
-        c[2] = tot_del;
-        c[3] = tnd;
-    }
-}
-
-// exclusive scan of per-tile (deltas, updates) -> tile_off[2*t]; totals -> counts[0..3]
-template <int NT>
-__global__ __launch_bounds__(NT) void k_scan_tiles(const u32* __restrict__ tile_cnt, u64 ntiles,
-                                                   u64* __restrict__ tile_off, u64* __restrict__ counts) {
-    __shared__ u64 s_w[2][NT / 64];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    u64 carry_d = 0, carry_u = 0, tins = 0, tdel = 0;
-    for (u64 base = 0; base < ntiles; base += NT) {
-        u64 t = base + threadIdx.x;
-        u64 vd = 0, vu = 0, vi = 0, vx = 0;
-        if (t < ntiles) {
-            vi = tile_cnt[4 * t + 0];
-            vu = tile_cnt[4 * t + 1];
-            vx = tile_cnt[4 * t + 2];
-            vd = tile_cnt[4 * t + 3];
-        }
-        u64 xd = vd, xu = vu;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            u64 yd = __shfl_up(xd, o, 64), yu = __shfl_up(xu, o, 64);
-            if (lane >= o) { xd += yd; xu += yu; }
-        }
-        if (lane == 63) { s_w[0][wid] = xd; s_w[1][wid] = xu; }
-        // per-chunk sums of inserts / deletes via atomics-free reduction
-        u64 ri = vi, rx = vx;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { ri += __shfl_xor(ri, o, 64); rx += __shfl_xor(rx, o, 64); }
-        __syncthreads();
-        u64 pd = 0, pu = 0, sd = 0, su = 0;
-#pragma unroll
-        for (int w = 0; w < NT / 64; w++) {
-            if (w < wid) { pd += s_w[0][w]; pu += s_w[1][w]; }
-            sd += s_w[0][w];
-            su += s_w[1][w];
-        }
-        if (t < ntiles) {
-            tile_off[2 * t] = carry_d + pd + xd - vd;
-            tile_off[2 * t + 1] = carry_u + pu + xu - vu;
-        }
-        __syncthreads();
-        if (lane == 0) { s_w[0][wid] = ri; s_w[1][wid] = rx; }
-        __syncthreads();
-        u64 ci = 0, cx = 0;
-#pragma unroll
-        for (int w = 0; w < NT / 64; w++) { ci += s_w[0][w]; cx += s_w[1][w]; }
-        __syncthreads();
-        carry_d += sd;
-        carry_u += su;
-        tins += ci;
-        tdel += cx;
-    }
-    if (threadIdx.x == 0) {
-        counts[0] = tins;
-        counts[1] = carry_u;
-        counts[2] = tdel;
-        counts[3] = carry_d;
-    }
-}
-
-template <int NT, int TILE>
-__global__ __launch_bounds__(NT) void k_scatter2(const uint2* __restrict__ stage_delta,
-                                                 const uint2* __restrict__ stage_upd,
-                                                 const u32* __restrict__ tile_cnt, const u64* __restrict__ tile_off,
-                                                 uint2* __restrict__ out_delta, uint2* __restrict__ out_upd) {
-    const u64 tile = blockIdx.x;
-    const u32 nd = tile_cnt[4 * tile + 3], nu = tile_cnt[4 * tile + 1];
-    const u64 od = tile_off[2 * tile], ou = tile_off[2 * tile + 1];
-    const uint2* sd = stage_delta + tile * (u64)TILE;
-    const uint2* su = stage_upd + tile * (u64)TILE;
-    for (u32 k = threadIdx.x; k < nd; k += NT) out_delta[od + k] = sd[k];
-    if (out_upd)
-        for (u32 k = threadIdx.x; k < nu; k += NT) out_upd[ou + k] = su[k];
-}
-
-// --------------------------------------------------------------------------------------------
-int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
-                 u64* d_counts, u32* d_err) {
-    (void)flags;
-    const u64 nA = A->n, nB = B->n, total = nA + nB;
-    KD_CHECK(nA < 0xFFFFFFFFull && nB < 0xFFFFFFFFull, "diff2: side too large for uint32 indices");
-    const bool hash = A->key_mode == KD_KEY_HASH || B->key_mode == KD_KEY_HASH;
-    KD_CHECK(A->key_mode == B->key_mode, "diff2: key modes differ");
-    if (hash) KD_CHECK((nA == 0 || (A->name && A->name_off)) && (nB == 0 || (B->name && B->name_off)),
-                       "diff2: KD_KEY_HASH needs filenames");
-    const u64 ntiles = (total + C2_TILE - 1) / C2_TILE;
-    KD_HIP(hipMemsetAsync(d_err, 0, sizeof(u32), ctx->stream));
-    if (ntiles == 0) {
-        KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
-        return KD_OK;
-    }
-    void *part, *tcnt, *toff, *sdel, *supd;
-    int rc;
-    if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
-    if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
-    if ((rc = ensure(ctx, "c2.toff", ntiles * 2 * sizeof(u64), &toff))) return rc;
-    if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_TILE * sizeof(uint2), &sdel))) return rc;
-    if ((rc = ensure(ctx, "c2.supd", ntiles * C2_TILE * sizeof(uint2), &supd))) return rc;
-
-    const u64 empty = 0;
-    const u64* kA = nA ? A->key : &empty;  // never dereferenced when n == 0
-    const u64* kB = nB ? B->key : &empty;
-    rc = launch(ctx, "k_partition2", [&] {
-        unsigned nb = (unsigned)((ntiles + 1 + 255) / 256);
-        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(256), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part);
-    });
-    if (rc) return rc;
-    Join2Args g;
-    g.A = kA; g.oidA = (const u32*)A->oid; g.nA = nA;
-    g.B = kB; g.oidB = (const u32*)B->oid; g.nB = nB;
-    g.part = (const u64*)part;
-    g.nameA = A->name; g.nameOffA = A->name_off; g.nameB = B->name; g.nameOffB = B->name_off;
-    g.hash_mode = hash ? 1 : 0;
-    g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
-    g.tile_cnt = (u32*)tcnt; g.err = d_err;
-    rc = launch(ctx, "k_join2", [&] {
-        hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
-    });
-    if (rc) return rc;
-    rc = launch(ctx, "k_scan_tiles", [&] {
-        hipLaunchKernelGGL((k_scan_tiles<1024>), dim3(1), dim3(1024), 0, ctx->stream, (const u32*)tcnt, ntiles,
-                           (u64*)toff, d_counts);
-    });
-    if (rc) return rc;
-    rc = launch(ctx, "k_scatter2", [&] {
-        hipLaunchKernelGGL((k_scatter2<256, C2_TILE>), dim3((unsigned)ntiles), dim3(256), 0, ctx->stream,
-                           (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)toff,
-                           (uint2*)d_delta, (uint2*)d_upd);
-    });
-    return rc;
-}
 
 // ============================================================================================
 // classify3
@@ -634,10 +282,7 @@ int kd_reserve(kd_ctx* ctx, uint64_t max_entries_per_side, uint64_t max_updates)
     void* p;
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * 8, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.tcnt", ntiles * 16, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.toff", ntiles * 16, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_TILE * 8, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.supd", ntiles * C2_TILE * 8, &p))) return rc;
+    if ((rc = lookback_state(ctx, ntiles, &p))) return rc;
     (void)max_updates;
     return KD_OK;
 }

@@ -178,28 +178,64 @@ __device__ __forceinline__ int find_legend(const u8* tab, int n, const u8* hex) 
 }
 
 constexpr int FD_MAXV = 128;
+constexpr int FD_NT = 64;  // one wave per block: each lane owns one update and two LDS slots
 
-__global__ __launch_bounds__(256) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
-                                                   const u8* __restrict__ nd, const u64* __restrict__ noff,
-                                                   const uint2* __restrict__ pairs, u64 n_upd_host,
-                                                   const u64* __restrict__ n_upd_dev, FdTab tb,
-                                                   u64* __restrict__ masks, u8* __restrict__ status) {
+// Stage [p, p+len) into an LDS slot with 16-B loads from the 16-B aligned-down address, all issued
+// before any use (one HBM latency instead of one per byte).  Returns the LDS pointer of byte p, or
+// nullptr when the blob does not fit (the lane then parses straight from global memory).
+template <int SLOT>
+__device__ __forceinline__ const u8* stage_blob(const u8* __restrict__ data, u64 start, u32 len, u64 arena_end,
+                                                uint4* slot) {
+    const u64 base = start & ~(u64)15;
+    const u32 delta = (u32)(start - base);
+    const u32 nch = (delta + len + 15) >> 4;
+    if (nch * 16 > (u32)SLOT || base + (u64)nch * 16 > arena_end) return nullptr;
+    const uint4* src = (const uint4*)(data + base);
+#pragma unroll
+    for (int c = 0; c < SLOT / 16; c++)
+        if (c < (int)nch) slot[c] = src[c];
+    return (const u8*)slot + delta;
+}
+
+template <int SLOT>
+__global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff, u64 on_blobs,
+                                                     const u8* __restrict__ nd, const u64* __restrict__ noff, u64 nn_blobs,
+                                                     const uint2* __restrict__ pairs, u64 n_upd_host,
+                                                     const u64* __restrict__ n_upd_dev, FdTab tb,
+                                                     u64* __restrict__ masks, u8* __restrict__ status) {
+    __shared__ uint4 s_slots[SLOT > 0 ? FD_NT * 2 * (SLOT / 16) : 1];
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
-    for (u64 u = (u64)blockIdx.x * blockDim.x + threadIdx.x; u < n_upd; u += (u64)gridDim.x * blockDim.x) {
+    const u64 o_end = ooff[on_blobs], n_end = noff[nn_blobs];
+    const int lane = threadIdx.x;
+    for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < n_upd; u0 += (u64)gridDim.x * FD_NT) {
+        const u64 u = u0 + lane;
+        if (u >= n_upd) break;
         u64 oi = pairs ? pairs[u].x : u, ni = pairs ? pairs[u].y : u;
-        const u8* ob = od + ooff[oi];
-        const u32 on = (u32)(ooff[oi + 1] - ooff[oi]);
-        const u8* nb = nd + noff[ni];
-        const u32 nn = (u32)(noff[ni + 1] - noff[ni]);
+        const u64 os = ooff[oi], ns = noff[ni];
+        const u32 on = (u32)(ooff[oi + 1] - os);
+        const u32 nn = (u32)(noff[ni + 1] - ns);
+        const u8* ob = nullptr;
+        const u8* nb = nullptr;
+        if constexpr (SLOT > 0) {
+            uint4* my = s_slots + (size_t)lane * 2 * (SLOT / 16);
+            ob = stage_blob<SLOT>(od, os, on, o_end, my);
+            nb = stage_blob<SLOT>(nd, ns, nn, n_end, my + SLOT / 16);
+        }
+        if (!ob) ob = od + os;
+        if (!nb) nb = nd + ns;
         u64* m = masks + u * tb.words;
-        for (int w = 0; w < tb.words; w++) m[w] = 0;
+        u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
         u8 st = 0;
         const u8 *lo, *ln;
         u32 cvo, cvn, po, pn;
-        if (parse_header(ob, on, &lo, &cvo, &po) || parse_header(nb, nn, &ln, &cvn, &pn)) { status[u] = 1; continue; }
-        const int li_o = find_legend(tb.leg_o, tb.n_lo, lo), li_n = find_legend(tb.leg_n, tb.n_ln, ln);
-        if (li_o < 0 || li_n < 0) { status[u] = 2; continue; }
-        if (tb.aligned[li_o * tb.n_ln + li_n] && cvo == cvn) {
+        int li_o = -1, li_n = -1;
+        if (parse_header(ob, on, &lo, &cvo, &po) || parse_header(nb, nn, &ln, &cvn, &pn)) st = 1;
+        else {
+            li_o = find_legend(tb.leg_o, tb.n_lo, lo);
+            li_n = find_legend(tb.leg_n, tb.n_ln, ln);
+            if (li_o < 0 || li_n < 0) st = 2;
+        }
+        if (!st && tb.aligned[li_o * tb.n_ln + li_n] && cvo == cvn) {
             // ---- lockstep: value v of both blobs belongs to the same union key ----
             const i16* kov = tb.key_of_val + (u64)li_o * tb.maxv;
             u32 pa = po, pb = pn;
@@ -209,12 +245,15 @@ __global__ __launch_bounds__(256) void k_fielddiff(const u8* __restrict__ od, co
                 if (!ca || !cb) { st = 4; break; }
                 pa += ca; pb += cb;
                 int k = v < (u32)tb.maxv ? kov[v] : -1;
-                if (k >= 0 && !py_eq(a, b)) m[k >> 6] |= 1ull << (k & 63);
+                if (k >= 0 && !py_eq(a, b)) {
+                    if (k < 256) mk[k >> 6] |= 1ull << (k & 63);
+                    else m[k >> 6] |= 1ull << (k & 63);
+                }
             }
             if (!st && (pa != on || pb != nn)) st = 4;  // trailing bytes: unpackb raises ExtraData
-        } else {
+        } else if (!st) {
             // ---- general: resolve each union key through both maps ----
-            if (cvo > FD_MAXV || cvn > FD_MAXV) { status[u] = 3; continue; }
+            if (cvo > FD_MAXV || cvn > FD_MAXV) st = 3;
             u32 vo[FD_MAXV], vn[FD_MAXV];
             u32 p = po;
             for (u32 v = 0; v < cvo && !st; v++) { DVal x; u32 c = dv_decode(ob + p, ob + on, x); if (!c) st = 4; vo[v] = p; p += c; }
@@ -222,8 +261,8 @@ __global__ __launch_bounds__(256) void k_fielddiff(const u8* __restrict__ od, co
             p = pn;
             for (u32 v = 0; v < cvn && !st; v++) { DVal x; u32 c = dv_decode(nb + p, nb + nn, x); if (!c) st = 4; vn[v] = p; p += c; }
             if (!st && p != nn) st = 4;
-            const i16* mo = tb.map_o + (u64)li_o * tb.n_keys;
-            const i16* mn = tb.map_n + (u64)li_n * tb.n_keys;
+            const i16* mo = tb.map_o + (u64)(li_o < 0 ? 0 : li_o) * tb.n_keys;
+            const i16* mn = tb.map_n + (u64)(li_n < 0 ? 0 : li_n) * tb.n_keys;
             for (int k = 0; k < tb.n_keys && !st; k++) {
                 if (!((tb.cmp[k >> 6] >> (k & 63)) & 1)) continue;
                 const int so = mo[k], sn = mn[k];
@@ -242,8 +281,16 @@ __global__ __launch_bounds__(256) void k_fielddiff(const u8* __restrict__ od, co
                     else dv_decode(nb + vn[sn], nb + nn, b);
                     changed = !py_eq(a, b);
                 }
-                if (changed) m[k >> 6] |= 1ull << (k & 63);
+                if (changed) {
+                    if (k < 256) mk[k >> 6] |= 1ull << (k & 63);
+                    else m[k >> 6] |= 1ull << (k & 63);
+                }
             }
+        }
+        if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+        for (int w = 0; w < tb.words; w++) {
+            if (w < 4) m[w] = mk[w];
+            else if (st) m[w] = 0;
         }
         status[u] = st;
     }
@@ -347,12 +394,30 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
         d_status = (u8*)b;
     }
     if (n_upd == 0 && d_n_upd == nullptr) return KD_OK;
-    u64 work = d_n_upd ? (u64)1 << 22 : n_upd;  // device count: size grid for the capacity
-    unsigned blocks = (unsigned)std::min<u64>((work + 255) / 256, 256ull * 16);
+    u64 work = d_n_upd ? (u64)1 << 22 : n_upd;  // device count: size the grid for the capacity
+    unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, 256ull * 32);
     if (blocks == 0) blocks = 1;
+    // LDS slot per blob, from the largest typical blob (kd_blobs.size_hint; host arenas: measured).
+    // Blobs that do not fit a slot are parsed from global memory by their lane.
+    auto max_len = [](const kd_blobs* b) -> u64 {
+        if (b->size_hint) return b->size_hint;
+        u64 m = 0;
+        if (b->mem == KD_MEM_HOST)
+            for (u64 i = 0; i < b->n; i++) m = std::max<u64>(m, b->off[i + 1] - b->off[i]);
+        return m ? m : 256;
+    };
+    const u64 need = std::max(max_len(ob), max_len(nb)) + 15;
+    const int slot = need <= 160 ? 160 : need <= 256 ? 256 : need <= 512 ? 512 : 0;
     rc = launch(ctx, "k_fielddiff", [&] {
-        hipLaunchKernelGGL(k_fielddiff, dim3(blocks), dim3(256), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
-                           (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks, d_status);
+        auto args = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
+                               ob->n, (const u8*)d_nd, (const u64*)d_noff, nb->n, (const uint2*)d_pu, n_upd, d_n_upd,
+                               tb, d_masks, d_status);
+        };
+        if (slot == 160) args(k_fielddiff<160>);
+        else if (slot == 256) args(k_fielddiff<256>);
+        else if (slot == 512) args(k_fielddiff<512>);
+        else args(k_fielddiff<0>);
     });
     if (rc) return rc;
     if (out_mem == KD_MEM_HOST) {

@@ -71,6 +71,9 @@ struct kd_ctx {
     // last uploaded kd_fielddiff table (host copy kept alive for the async upload, and reused
     // when the next call's tables are identical)
     std::vector<uint8_t> fd_tab;
+    // classify2 decoupled look-back bookkeeping (kd_classify2.hip)
+    uint64_t c2_tile_base = 0;
+    uint32_t c2_epoch = 0;
 };
 
 namespace kd {
@@ -102,6 +105,7 @@ inline int launch(kd_ctx* ctx, const char* name, F&& f) {
 int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem, const void** dev);
 
 // ---- classify2 (device form), kd_classify.hip ----
+int lookback_state(kd_ctx* ctx, u64 ntiles, void** out);
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
                  u32* d_upd, u64* d_counts, u32* d_err);
 constexpr int C2_NT = 256;

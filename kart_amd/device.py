@@ -53,6 +53,7 @@ class DevBlobs:
         self.data = to_dev(data if data.size else np.zeros(1, np.uint8), device)
         self.off = to_dev(off, device)
         self.nbytes = int(data.size)
+        self.max_len = int((off[1:] - off[:-1]).max()) if self.n else 0
 
     def kd_blobs(self):
         b = N.KdBlobs()
@@ -60,6 +61,7 @@ class DevBlobs:
         b.data = self.data.data_ptr()
         b.off = self.off.data_ptr()
         b.mem = N.KD_MEM_DEVICE
+        b.size_hint = min(self.max_len, 0xFFFFFFFF)
         return b
 
 

@@ -1,0 +1,200 @@
+"""The drop-in boundary: get_dataset_diff / diff_feature / field_diff return the reference's
+delta sets, values, changed fields and streaming behaviour (tests/golden, from the reference).
+
+Each test runs twice: against the HIP engine (-m gpu) and, on CPU, against a test-only engine
+whose diff2/fielddiff are the oracle — that CPU run checks the host adaptor logic (swap/reverse,
+pk decoding, lazy values, key filter), never the kernels.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from checks import NONE
+from fixtures import DIFF_FIXTURES, load, pk_of
+from kart_amd import dataset as D
+from kart_amd.engine import Diff2Result
+
+
+class OracleEngine:
+    """test-only stand-in with the Engine interface, computed by the CPU oracle"""
+
+    def diff2(self, A, B):
+        from oracle import oracle as O
+
+        delta, c = O.classify2(A.key, A.oid, B.key, B.oid)
+        upd = delta[(delta[:, 0] != NONE) & (delta[:, 1] != NONE)]
+        return Diff2Result(c["inserts"], c["updates"], c["deletes"], delta, upd)
+
+    def fielddiff(self, od, oo, nd, no, pairs, maps):
+        from oracle import oracle as O
+
+        return O.fielddiff(od, oo, nd, no, pairs, maps)
+
+
+@pytest.fixture(params=["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+def eng(request):
+    if request.param == "oracle":
+        yield OracleEngine()
+    else:
+        yield request.getfixturevalue("engine")
+
+
+def version(fx, key):
+    if fx.n(key) == 0:
+        return None
+    idx = fx.a[f"{key}_blob"]
+    return D.DatasetVersion(fx.meta["ds_path"], fx.schema(key), fx.legends, fx.encoding(key), fx.a[f"{key}_names"],
+                            fx.a[f"{key}_name_off"].astype(np.uint64), fx.oids(key), lambda i: fx.blob(int(idx[i])),
+                            meta={"schema.json": fx.meta["sides"][key]["schema"]})
+
+
+def _jv(v):
+    """engine value -> golden json_safe form"""
+    if v is None:
+        return None
+    if isinstance(v, bool):
+        return {"bool": v}
+    if isinstance(v, int):
+        return {"int": str(v)}
+    if isinstance(v, float):
+        return {"float": v.hex()}
+    if isinstance(v, str):
+        return {"str": v}
+    if isinstance(v, (bytes, bytearray)):
+        return {"bytes": bytes(v).hex(), "geom": isinstance(v, D.Geometry)}
+    return {"repr": repr(v)}
+
+
+@pytest.mark.parametrize("name", DIFF_FIXTURES)
+def test_get_dataset_diff_golden(eng, name):
+    fx = load(name)
+    for case in fx.cases("diff2"):
+        base, target = version(fx, case["base"]), version(fx, case["target"])
+        ds = D.get_dataset_diff(eng, base, target)
+        fd = ds.get("feature", {})
+        got = {(d.type, d.old_key, d.new_key) for d in fd.values()}
+        want = {(d["type"], pk_of(d["old_pk"]), pk_of(d["new_pk"])) for d in case["deltas"]}
+        assert got == want
+        assert fd.type_counts() if fd else {} == {k: v for k, v in case["counts"].items() if v}
+        # sorted_items order == the golden (reference DeltaDiff.sorted_items) order
+        assert [k for k, _ in fd.sorted_items()] == [pk_of(d["old_pk"]) if d["old_pk"] is not None
+                                                     else pk_of(d["new_pk"]) for d in case["deltas"]]
+        if any("old" in d for d in case["deltas"]):
+            for (k, delta), gd in zip(fd.sorted_items(), case["deltas"]):
+                if "old" in gd:
+                    assert {a: _jv(b) for a, b in delta.old_value.items()} == gd["old"]
+                    assert {a: _jv(b) for a, b in delta.new_value.items()} == gd["new"]
+        # field diff attached in one batch equals the reference text writer's decision
+        n = D.field_diff(eng, fd, base or target, target or base) if fd else 0
+        for (k, delta), gd in zip(fd.sorted_items() if fd else [], case["deltas"]):
+            if gd["type"] == "update":
+                assert delta.changed_fields == gd["changed"]
+        assert n == sum(1 for d in case["deltas"] if d["type"] == "update")
+
+
+def test_diff_streaming_contract(eng):
+    """tests/test_diff.py:1656-1685: diffing calls get_feature zero times; each value access once."""
+    fx = load("repo_points")
+    old, new = version(fx, "head1"), version(fx, "head")
+    calls = {"n": 0}
+    for v in (old, new):
+        orig = v.get_feature
+
+        def counted(*a, _orig=orig, **k):
+            calls["n"] += 1
+            return _orig(*a, **k)
+
+        v.get_feature = counted
+    reads = {"n": 0}
+    for v in (old, new):
+        rb = v.read_blob
+
+        def counted_read(i, _rb=rb):
+            reads["n"] += 1
+            return _rb(i)
+
+        v.read_blob = counted_read
+    fd = D.dataset_diff(eng, old, new)["feature"]
+    assert calls["n"] == 0 and reads["n"] == 0
+    expected = 0
+    for key, delta in sorted(fd.items()):
+        delta.old_value
+        delta.new_value
+        expected += 2
+        assert calls["n"] == expected
+        delta.old_value  # cached
+        assert calls["n"] == expected
+    # DeltaFetcher reads the blob id from the promise (base_diff_writer.py:505-507)
+    d = next(iter(fd.values()))
+    assert len(d.old.value.args[0].id.hex) == 40
+
+
+def test_key_filter(eng):
+    fx = load("repo_points")
+    old, new = version(fx, "head1"), version(fx, "head")
+
+    class F(set):
+        match_all = False
+
+    fd = D.DeltaDiff(D.diff_feature(eng, old, new, F({"1166", "1182", "999999"})))
+    assert sorted(fd.keys()) == [1166, 1182]
+
+
+def test_reverse_and_missing_dataset(eng):
+    fx = load("repo_points")
+    head = version(fx, "head")
+    ins = D.get_dataset_diff(eng, None, head)["feature"]
+    dels = D.get_dataset_diff(eng, head, None)["feature"]
+    assert ins.type_counts() == {"inserts": 2143}
+    assert dels.type_counts() == {"deletes": 2143}
+    inv = ~ins
+    assert {k: (d.type, d.old_key, d.new_key) for k, d in inv.items()} == \
+        {k: (d.type, d.old_key, d.new_key) for k, d in dels.items()}
+
+
+def test_gitsource_walk(eng, tmp_path):
+    """host tree walker over a real git repository built from the fixture's own blobs"""
+    fx = load("repo_points")
+    gitdir = str(tmp_path / "repo.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    ds = fx.meta["ds_path"]
+    inner = f"{ds}/.table-dataset"
+    lines = []
+    mark = 0
+    for ci, key in enumerate(("head1", "head")):
+        files = {}
+        idx = fx.a[f"{key}_blob"]
+        for name, bi in zip(fx.names(key), idx):
+            files[f"{inner}/feature/{name}"] = fx.blob(int(bi))
+        files[f"{inner}/meta/schema.json"] = json.dumps(fx.meta["sides"][key]["schema"]).encode()
+        files[f"{inner}/meta/path-structure.json"] = json.dumps(fx.meta["sides"][key]["path_structure"]).encode()
+        for h, lg in fx.legends.items():
+            files[f"{inner}/meta/legend/{h}"] = lg.dumps()
+        marks = {}
+        for p, data in files.items():
+            mark += 1
+            marks[p] = mark
+            lines.append(b"blob\nmark :%d\ndata %d\n" % (mark, len(data)) + data + b"\n")
+        lines.append(b"commit refs/heads/c%d\ncommitter t <t@t> %d +0000\ndata 1\nx\n" % (ci, 1600000000 + ci))
+        if ci:
+            lines.append(b"from refs/heads/c0\n")
+        lines.append(b"deleteall\n")
+        for p in files:
+            lines.append(b"M 100644 :%d %s\n" % (marks[p], p.encode()))
+        lines.append(b"\n")
+    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
+                   check=True)
+    from kart_amd.gitsource import GitRepo
+
+    repo = GitRepo(gitdir)
+    assert repo.dataset_paths("refs/heads/c1") == [ds]
+    old = repo.dataset_version("refs/heads/c0", ds)
+    new = repo.dataset_version("refs/heads/c1", ds)
+    fd = D.get_dataset_diff(eng, old, new)["feature"]
+    assert sorted(fd.keys()) == [1095, 1166, 1168, 1181, 1182]
+    D.field_diff(eng, fd, old, new)
+    assert sum(len(d.changed_fields) for d in fd.values()) == 13
+    repo.close()
