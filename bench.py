@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU (C2: 10M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ordered", action="store_true",
+                    help="key-ordered delta list (adds the scan + scatter kernels); default: tile-grouped")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     return ap.parse_args()
@@ -75,7 +77,7 @@ def main():
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     eng = Engine(torch.cuda.current_device())
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, dev)
+    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, dev, ordered=args.ordered)
     torch.cuda.synchronize()
 
     # ---- warmup + correctness of the resident pipeline against the generator's own counts ----
@@ -117,7 +119,7 @@ def main():
         total_pairs, total_deltas = n_pairs, counts["deltas"]
 
     kern = {}
-    for name in ("k_partition2", "k_join2", "k_scan_tiles", "k_scatter2", "k_fielddiff"):
+    for name in ("k_partition2", "k_join2", "k_scan_tiles", "k_scatter2", "k_fielddiff"):  # kernels of a step
         launches, ms = eng.prof_get(name)
         if launches:
             kern[name] = (launches, ms / launches)
@@ -169,6 +171,7 @@ def main():
             "data": "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
             "config": {"workload": "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
                        "points_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
+                       "delta_order": "key" if args.ordered else "tile-grouped (same delta set)",
                        "parallelism": f"bucket-range shards x{world}"},
             "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
             "roofline": roof,

@@ -124,6 +124,11 @@ void kd_free(void* p); /* frees kd_diff_result / kd_merge_result and their array
 /* Host-convenience form: sides may be host or device; results are host memory (kd_free). */
 int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags,
              kd_diff_result** out);
+/* flags for kd_diff2 / kd_diff2_device */
+#define KD_DIFF_UNORDERED 0x1u /* device form only: deltas/updates grouped per 2048-pair tile, tiles in
+                                  completion order (each tile key-ordered) — skips the ordering
+                                  scan + scatter; the delta SET is identical                      */
+
 /* Device form: everything device-resident, asynchronous on the context stream.
  * d_delta / d_upd capacity must cover the worst case (base.n + target.n pairs).
  * d_counts[4] <- inserts, updates, deletes, deltas.  d_err <- nonzero if a side is not strictly

@@ -19,6 +19,7 @@ KD_MEM_HOST = 0
 KD_MEM_DEVICE = 1
 KD_KEY_INT = 0
 KD_KEY_HASH = 1
+KD_DIFF_UNORDERED = 0x1
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -165,6 +166,14 @@ def lib():
     """Load libkartdiff.so once; raise NativeUnavailable (never silently fall back)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64/libhsa-runtime64 with the
+        # same sonames as /opt/rocm's.  Whichever loads first serves both, so load torch's first
+        # when it is installed — the device pipeline hands torch-allocated HBM and torch's stream
+        # to this library.  (Without torch, /opt/rocm's runtime is used.)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise NativeUnavailable(
                 f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"

@@ -282,7 +282,10 @@ int kd_reserve(kd_ctx* ctx, uint64_t max_entries_per_side, uint64_t max_updates)
     void* p;
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * 8, &p))) return rc;
-    if ((rc = lookback_state(ctx, ntiles, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.tcnt", ntiles * 16, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.toff", ntiles * 8, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_TILE * 8, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.supd", ntiles * C2_TILE * 8, &p))) return rc;
     (void)max_updates;
     return KD_OK;
 }
@@ -371,10 +374,11 @@ int kd_merge3(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_sid
     u64* counts = (u64*)dc;
     u32* derr = (u32*)(counts + 4);
     KD_HIP(hipMemsetAsync(dc, 0, 64, ctx->stream));
-    const u64 empty = 0;
-    const u64* kA = nA ? A.key : &empty;
-    const u64* kO = nO ? O.key : &empty;
-    const u64* kT = nT ? T.key : &empty;
+    void* dz;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    const u64* kA = nA ? A.key : (const u64*)dz;  // an empty side points at device zeros
+    const u64* kO = nO ? O.key : (const u64*)dz;
+    const u64* kT = nT ? T.key : (const u64*)dz;
     rc = launch(ctx, "k_partition3", [&] {
         hipLaunchKernelGGL(k_partition3, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0, ctx->stream, kA, nA,
                            kO, nO, kT, nT, ntiles, (u64*)bounds);

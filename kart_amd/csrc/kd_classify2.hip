@@ -5,58 +5,68 @@
 // strictly ascending join keys + 20-byte blob OIDs; a key on one side only is an insert/delete, a
 // key on both sides with different OIDs is an update (GIT_DELTA_ADDED/DELETED/MODIFIED).
 //
-//   k_partition2  merge-path split points of the union sequence: one wave per tile boundary,
-//                 64-ary search (4-6 dependent HBM round trips instead of ~24 for binary search)
-//   k_join2       per 2048-item tile (dynamic tile id):
-//                   A. keys -> LDS; per-thread merge path over 8 items; partner of every A item
-//                   B. striped OID compare of matched pairs (consecutive lanes read consecutive
-//                      20-B records: every fetched line is fully used)
-//                   C. ordered compaction: per-thread counts -> block scan -> decoupled look-back
-//                      across tiles (8-byte {epoch, inclusive/aggregate, value} granules written by
-//                      one agent-scope atomic store each, polled with agent-scope atomic loads —
-//                      the data is the flag, so no fences are needed) -> deltas and updates are
-//                      written straight to their final key-ordered positions.
-// Inputs are read once; outputs written once; no staging, no scan/scatter kernels.
+//   k_partition2  merge-path split points of the union sequence: 8 lanes per tile boundary,
+//                 8-ary search (8 dependent HBM round trips instead of ~24 for binary search)
+//   k_join2       per 2048-item tile:
+//                   0. the tile's key and OID byte ranges (both sides) -> LDS as 16-B chunks, every
+//                      load issued before any use (~56 KB in flight per workgroup)
+//                   A. per-thread merge path over 8 items in LDS; partner of every A item
+//                   B. OID compare of matched pairs from LDS
+//                   C. ordered compaction (block scan) of the tile's deltas and updates into a
+//                      tile-local staging slot + per-tile counts
+//   k_scatter2    each block reduces the counts of all preceding tiles (L2-resident) to find its
+//                 offsets, then copies its tiles' staged records to their final key-ordered
+//                 positions; the last block writes the totals.
+// Inputs are read once; the staging round trip costs 16 B per delta.
 #include "kd_join.h"
 
 namespace kd {
 
-// ---- merge-path partition, wave-cooperative 64-ary search --------------------------------------
+// ---- merge-path partition: PW lanes per tile boundary, PW-ary search ------------------------------
 // part[t] = number of A items among the first min(t*TILE, nA+nB) union items (ties: A first).
+// A binary search is ~24 dependent HBM round trips at 10M keys; a 64-ary one needs 4 but fetches
+// 128 random lines per round per boundary.  PW = 8 lanes: 8 round trips, 16 lines per round.
+constexpr int PW = 8;
+
 __global__ __launch_bounds__(256) void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B,
-                                                    u64 nB, u64 ntiles, u64* __restrict__ part) {
-    const u64 t = (u64)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                    u64 nB, u64 ntiles, u64* __restrict__ part,
+                                                    u64* __restrict__ zero_counts, u32* __restrict__ zero_err) {
+    // the join's counters start at zero: cleared here (stream-ordered before k_join2) instead of
+    // by separate memset launches
+    if (blockIdx.x == 0 && threadIdx.x < 4) zero_counts[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 4) *zero_err = 0;
+    const u64 t = ((u64)blockIdx.x * 256 + threadIdx.x) / PW;
+    const int sub = threadIdx.x % PW;
     const int lane = threadIdx.x & 63;
-    if (t > ntiles) return;
+    const int grp = lane / PW;  // group within the wave
+    if (t > ntiles) return;  // whole groups exit together (group = PW consecutive lanes)
     const u64 total = nA + nB;
     u64 d = t * (u64)C2_TILE;
     if (d > total) d = total;
     // smallest i in [lo, hi] with pred(i) = (i == hi) || A[i] > B[d-1-i]
     u64 lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
-    while (hi - lo > 0) {
-        const u64 span = hi - lo;
-        const u64 step = (span + 63) / 64;  // probe lo + step*(l+1) - 1
-        u64 probe = lo + step * (u64)(lane + 1) - 1;
+    while (hi > lo) {
+        const u64 step = (hi - lo + PW - 1) / PW;  // lane s probes lo + step*(s+1) - 1
+        const u64 probe = lo + step * (u64)(sub + 1) - 1;
         bool p = true;
         if (probe < hi) p = A[probe] > B[d - 1 - probe];
-        const unsigned long long bal = __ballot(p);
-        if (bal == 0) { lo = hi; break; }  // every probe (the last is hi-1) false -> answer is hi
+        const unsigned long long bal = (__ballot(p) >> (grp * PW)) & ((1ull << PW) - 1);
+        if (bal == 0) { lo = hi; break; }  // all probes (the last is hi-1) false -> answer is hi
         const int f = __ffsll(bal) - 1;
-        const u64 new_hi = lo + step * (u64)(f + 1) - 1;
-        const u64 new_lo = f == 0 ? lo : lo + step * (u64)f;
-        lo = new_lo;
-        hi = new_hi < hi ? new_hi : hi;
+        const u64 nh = lo + step * (u64)(f + 1) - 1;
+        lo = lo + step * (u64)f;
+        hi = nh < hi ? nh : hi;
         if (step == 1) { lo = hi; break; }
     }
-    if (lane == 0) part[t] = lo;
+    if (sub == 0) part[t] = lo;
 }
 
 struct Join2Args {
     const u64* A;
-    const u32* oidA;
+    const u8* oidA;
     u64 nA;
     const u64* B;
-    const u32* oidB;
+    const u8* oidB;
     u64 nB;
     const u64* part;
     const u8* nameA;
@@ -64,61 +74,109 @@ struct Join2Args {
     const u8* nameB;
     const u64* nameOffB;
     int hash_mode;
-    u64 ntiles;
-    u64 tile_base;       // dynamic tile ids: atomicAdd(tile_ctr) - tile_base
-    u64* tile_ctr;
-    u64* st_d;           // look-back granules per tile: deltas
-    u64* st_u;           //                              updates
-    u64* st_x;           //                              deletes
-    u32 epoch;           // 15-bit tag of this call's granules
-    uint2* out_delta;
+    const u8* dummy;     // >= 64 readable device bytes (target of masked-off lanes' loads)
+    uint2* stage_delta;  // ordered mode: tile-local slots of TILE records
+    uint2* stage_upd;
+    u32* tile_cnt;       // ordered mode: [ntiles*4] inserts, updates, deletes, deltas
+    uint2* out_delta;    // unordered mode: final lists, appended per tile
     uint2* out_upd;
-    u64* counts;         // [4] inserts, updates, deletes, deltas (written by the last tile)
+    u64* counts;         // unordered mode: [4] inserts, updates, deletes, deltas (atomic)
     u32* err;
 };
 
-// granule: [epoch:15][inclusive:1][value:48]
-__device__ __forceinline__ u64 gran(u32 epoch, bool inc, u64 v) {
-    return ((u64)epoch << 49) | ((u64)(inc ? 1 : 0) << 48) | (v & ((1ull << 48) - 1));
+// The tile's four input byte ranges (A keys, B keys, A OIDs, B OIDs) are copied to LDS as
+// 16-byte chunks of their 16-byte-aligned *absolute* addresses: a 16-byte-aligned chunk holding
+// any valid byte lies inside one mapped page, so the over-read at either end can never fault, and
+// every chunk load is a full-width, fully used global_load_dwordx4 issued before any use.
+struct Range {
+    u64 base;  // aligned-down absolute address
+    u32 nch;   // 16-byte chunks
+    u32 skew;  // byte offset of the first element inside chunk 0
+};
+
+__device__ __forceinline__ Range mk_range(const void* p, u64 first_byte, u64 end_byte) {
+    Range r;
+    const u64 a0 = (u64)p + first_byte, a1 = (u64)p + end_byte;
+    r.base = a0 & ~(u64)15;
+    r.skew = (u32)(a0 - r.base);
+    r.nch = end_byte > first_byte ? (u32)((a1 - r.base + 15) >> 4) : 0;
+    return r;
 }
 
 template <int NT, int IPT>
+struct Join2Lds {
+    static constexpr int TILE = NT * IPT;
+    static constexpr int CH = TILE / 2 + 4;  // 16-B chunks holding the 8-B keys of both ranges
+    static constexpr int UNR = (CH + NT - 1) / NT;
+    static constexpr int KB = (TILE + NT - 1) / NT;  // A items per thread in the OID phase
+};
+
+// UNORD: each tile reserves its output ranges with one atomic add per counter and writes its
+// (key-ordered) records straight to the final lists — tiles land in completion order, no staging,
+// no scan, no scatter.  Ordered (default): tile-local staging + k_scan_tiles + k_scatter2.
+template <int NT, int IPT, bool UNORD>
 __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
-    constexpr int TILE = NT * IPT;
+    using LD = Join2Lds<NT, IPT>;
+    constexpr int TILE = LD::TILE;
+    static_assert(TILE <= 4095, "per-item records hold 12-bit local indices");
     constexpr u16 NOP = 0xFFFF;
-    __shared__ u64 sk[TILE];
+    __shared__ u32x4 s_ch[LD::CH];
     __shared__ u16 s_partner[TILE];
     __shared__ u8 s_chg[TILE];
     __shared__ u32 s_wave[NT / 64];
-    __shared__ u64 s_bcast[4];
+    __shared__ u64 s_base[2];
 
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) s_bcast[0] = atomicAdd((unsigned long long*)g.tile_ctr, 1ull) - g.tile_base;
-    __syncthreads();
-    const u64 tile = s_bcast[0];
-    if (tile >= g.ntiles) return;  // cannot happen (grid == ntiles); guard only
+    const int tid = threadIdx.x;
+    const u64 tile = blockIdx.x;
     const u64 total = g.nA + g.nB;
     const u64 d0 = tile * (u64)TILE;
     const u64 d1 = d0 + TILE < total ? d0 + TILE : total;
     u64 i0 = g.part[tile], i1 = g.part[tile + 1];
-    bool broken = i1 < i0 || d1 - i1 < d0 - i0 || i1 - i0 > d1 - d0;
-    if (broken) {  // only on unsorted input: still publish an empty aggregate so successors progress
-        if (tid == 0) atomicOr(g.err, 1u);
-        i1 = i0;
+    if (i1 < i0 || d1 - i1 < d0 - i0 || i1 - i0 > d1 - d0) {  // only on unsorted input
+        if (tid == 0) {
+            atomicOr(g.err, 1u);
+            if (!UNORD) {
+                u32* c = g.tile_cnt + 4 * tile;
+                c[0] = c[1] = c[2] = c[3] = 0;
+            }
+        }
+        return;
     }
-    const u64 j0 = d0 - i0, j1 = broken ? j0 : d1 - i1;
+    const u64 j0 = d0 - i0, j1 = d1 - i1;
     const int na = (int)(i1 - i0), nb = (int)(j1 - j0);
+
+    // ---- the tile's keys (both ranges) -> LDS as 16-B chunks, all loads in flight together --------
+    const Range rka = mk_range(g.A, 8 * i0, 8 * i1), rkb = mk_range(g.B, 8 * j0, 8 * j1);
+    const u32 c1 = rka.nch, c2 = c1 + rkb.nch;
+    {
+        // branch-free issue (out-of-range lanes re-load chunk 0), then the LDS stores
+        u32x4 v[LD::UNR];
+#pragma unroll
+        for (int k = 0; k < LD::UNR; k++) {
+            const u32 c0 = tid + k * NT;
+            const u32 c = c0 < c2 ? c0 : 0;
+            const u64 addr = c < c1 ? rka.base + 16ull * c : rkb.base + 16ull * (c - c1);
+            v[k] = *(const __attribute__((address_space(1))) u32x4*)addr;  // global_, not flat_
+        }
+#pragma unroll
+        for (int k = 0; k < LD::UNR; k++) {
+            const u32 c = tid + k * NT;
+            if (c < c2) s_ch[c] = v[k];
+        }
+    }
+    // lookbehind / lookahead keys (tiny, scalar)
     const bool has_lbA = i0 > 0, has_lbB = j0 > 0, has_la = j1 < g.nB;
     const u64 lbA = has_lbA ? g.A[i0 - 1] : 0;
     const u64 lbB = has_lbB ? g.B[j0 - 1] : 0;
     const u64 la = has_la ? g.B[j1] : 0;
-
-    for (int x = tid; x < na + nb; x += NT) sk[x] = x < na ? g.A[i0 + x] : g.B[j0 + (x - na)];
     __syncthreads();
-    const u64* sA = sk;
-    const u64* sB = sk + na;
+    const u64* sA = (const u64*)((const u8*)s_ch + rka.skew);
+    const u64* sB = (const u64*)((const u8*)(s_ch + c1) + rkb.skew);
 
-    // ---- A: per-thread merge path; partner of each A item -------------------------------------
+    // ---- A: per-thread merge path over IPT items (one walk); each item's outcome is kept in a
+    //         register: rec = kind << 25 | changed << 24 | jb << 12 | ia  (local 12-bit indices; jb
+    //         may be nb = the lookahead B[j1])
+    enum : u32 { R_NONE = 0, R_DEL = 1, R_MATCH = 2, R_INS = 3 };
     const int nitems = na + nb;
     const int dd = tid * IPT < nitems ? tid * IPT : nitems;
     const int cnt = (dd + IPT < nitems ? dd + IPT : nitems) - dd;
@@ -128,183 +186,202 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         if (sA[mid] <= sB[dd - 1 - mid]) lo = mid + 1;
         else hi = mid;
     }
-    const int ia0 = lo, jb0 = dd - lo;
+    u32 rec[IPT];
     bool bad = false;
     {
-        int ia = ia0, jb = jb0;
+        int ia = lo, jb = dd - lo;
+#pragma unroll
         for (int k = 0; k < IPT; k++) {
-            if (k >= cnt) break;
-            if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
-                u64 ka = sA[ia];
-                if (ia > 0 ? sA[ia - 1] >= ka : (has_lbA && lbA >= ka)) bad = true;
-                bool hb = jb < nb ? true : has_la;
-                u64 kb = jb < nb ? sB[jb] : la;
-                s_partner[ia] = (hb && kb == ka) ? (u16)jb : NOP;
-                ia++;
-            } else {
-                u64 kb = sB[jb];
-                if (jb > 0 ? sB[jb - 1] >= kb : (has_lbB && lbB >= kb)) bad = true;
-                jb++;
+            rec[k] = R_NONE << 25;
+            if (k < cnt) {
+                if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
+                    const u64 ka = sA[ia];
+                    if (ia > 0 ? sA[ia - 1] >= ka : (has_lbA && lbA >= ka)) bad = true;
+                    const bool hb = jb < nb ? true : has_la;
+                    const u64 kb = jb < nb ? sB[jb] : la;
+                    const bool m = hb && kb == ka;
+                    s_partner[ia] = m ? (u16)jb : NOP;
+                    rec[k] = ((m ? R_MATCH : R_DEL) << 25) | ((u32)jb << 12) | (u32)ia;
+                    ia++;
+                } else {
+                    const u64 kb = sB[jb];
+                    if (jb > 0 ? sB[jb - 1] >= kb : (has_lbB && lbB >= kb)) bad = true;
+                    const bool partner = ia > 0 ? sA[ia - 1] == kb : (has_lbA && lbA == kb);
+                    rec[k] = ((partner ? R_NONE : R_INS) << 25) | ((u32)jb << 12) | (u32)ia;
+                    jb++;
+                }
             }
         }
     }
     if (bad) atomicOr(g.err, 1u);
     __syncthreads();
 
-    // ---- B: striped OID compare ------------------------------------------------------------------
-    for (int a = tid; a < na; a += NT) {
-        u16 p = s_partner[a];
-        u8 chg = 0;
-        if (p != NOP) {
-            const u64 ia = i0 + a, jb = j0 + p;
-            chg = oid_ne(g.oidA + ia * 5, g.oidB + jb * 5) ? 1 : 0;
-            if (g.hash_mode && !names_eq(g.nameA, g.nameOffA, ia, g.nameB, g.nameOffB, jb)) atomicOr(g.err, 2u);
+    // ---- B: OID compare of matched pairs.  Lane l takes A items l, l+NT, ...: consecutive lanes
+    //         read consecutive 20-B records of both sides (every fetched line fully used); all of a
+    //         batch's loads are issued branch-free before the compares ------------------------------
+    typedef const __attribute__((address_space(1))) u32* gp32;
+    constexpr int BATCH = 4;
+#pragma unroll
+    for (int k0 = 0; k0 < LD::KB; k0 += BATCH) {
+        u32 xa[BATCH][5], xb[BATCH][5];
+        bool m[BATCH];
+#pragma unroll
+        for (int k = 0; k < BATCH; k++) {
+            const int a = tid + (k0 + k) * NT;
+            const bool in = a < na;
+            const u16 p = in ? s_partner[a] : NOP;
+            m[k] = p != NOP;
+            gp32 pa = in ? (gp32)(g.oidA + 20 * (i0 + a)) : (gp32)g.dummy;
+            gp32 pb = m[k] ? (gp32)(g.oidB + 20 * (j0 + p)) : pa;
+#pragma unroll
+            for (int w = 0; w < 5; w++) { xa[k][w] = pa[w]; xb[k][w] = pb[w]; }
         }
-        s_chg[a] = chg;
+#pragma unroll
+        for (int k = 0; k < BATCH; k++) {
+            const int a = tid + (k0 + k) * NT;
+            if (a < na) {
+                u32 d = 0;
+#pragma unroll
+                for (int w = 0; w < 5; w++) d |= xa[k][w] ^ xb[k][w];
+                s_chg[a] = (m[k] && d) ? 1 : 0;
+                if (m[k] && g.hash_mode &&
+                    !names_eq(g.nameA, g.nameOffA, i0 + a, g.nameB, g.nameOffB, j0 + s_partner[a]))
+                    atomicOr(g.err, 2u);
+            }
+        }
     }
     __syncthreads();
 
-    // ---- C: counts, block scan, look-back, final writes ------------------------------------------
+    // ---- C: counts from the registers, block scan, ordered writes ----------------------------------
     u32 nd = 0, nu = 0, ndel = 0;
-    {
-        int ia = ia0, jb = jb0;
-        for (int k = 0; k < IPT; k++) {
-            if (k >= cnt) break;
-            if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
-                u16 p = s_partner[ia];
-                if (p == NOP) { nd++; ndel++; }
-                else if (s_chg[ia]) { nd++; nu++; }
-                ia++;
-            } else {
-                u64 kb = sB[jb];
-                bool partner = ia > 0 ? sA[ia - 1] == kb : (has_lbA && lbA == kb);
-                if (!partner) nd++;
-                jb++;
-            }
-        }
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF;
+        if (kind == R_MATCH) {
+            if (s_chg[ia]) { nd++; nu++; rec[k] |= 1u << 24; }  // bit 24: OIDs differ
+        } else if (kind == R_DEL) { nd++; ndel++; }
+        else if (kind == R_INS) nd++;
     }
     u32 tot_packed;
     const u32 off_packed = block_excl_scan<NT>(nd | (nu << 16), s_wave, &tot_packed);
     const u32 tot_del = block_sum<NT>(ndel, s_wave);
-    const u64 agg_d = tot_packed & 0xFFFF, agg_u = tot_packed >> 16, agg_x = tot_del;
-
-    if (tid < 64) {
-        // decoupled look-back by wave 0: publish aggregate, then walk predecessors 64 at a time
-        u64 pre_d = 0, pre_u = 0, pre_x = 0;
-        if (tile > 0 && lane == 0) {
-            __hip_atomic_store(g.st_d + tile, gran(g.epoch, false, agg_d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g.st_u + tile, gran(g.epoch, false, agg_u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g.st_x + tile, gran(g.epoch, false, agg_x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 tnd = tot_packed & 0xFFFF, tnu = tot_packed >> 16;
+    u32 od = off_packed & 0xFFFF, ou = off_packed >> 16;
+    uint2* sd;
+    uint2* su;
+    if (UNORD) {
+        // four lanes of wave 0 reserve in parallel: deltas, updates (offsets) + inserts, deletes
+        if (tid < 4) {
+            const u64 v = tid == 0 ? tnd : tid == 1 ? tnu : tid == 2 ? tnd - tnu - tot_del : tot_del;
+            const int slot = tid == 0 ? 3 : tid == 1 ? 1 : tid == 2 ? 0 : 2;
+            const u64 old = v ? atomicAdd((unsigned long long*)(g.counts + slot), (unsigned long long)v) : 0;
+            if (tid < 2) s_base[tid] = old;
         }
-        i64 base = (i64)tile - 1;
-        u32 spins = 0;
-        while (base >= 0) {
-            const i64 t = base - lane;
-            u64 wd = 0, wu = 0, wx = 0;
-            bool ready = true, inc = false;
-            if (t >= 0) {
-                wd = __hip_atomic_load(g.st_d + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wu = __hip_atomic_load(g.st_u + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wx = __hip_atomic_load(g.st_x + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const u32 ep = g.epoch;
-                const u64 fd = (wd >> 48) & 1, fu = (wu >> 48) & 1, fx = (wx >> 48) & 1;
-                // a tile's three granules are separate stores: use them only once all three carry
-                // this call's epoch and the same kind (aggregate or inclusive)
-                ready = (u32)(wd >> 49) == ep && (u32)(wu >> 49) == ep && (u32)(wx >> 49) == ep && fd == fu && fu == fx;
-                inc = ready && fd;
-            } else {
-                inc = true;  // virtual inclusive 0 before tile 0
-            }
-            const unsigned long long m_inc = __ballot(inc);
-            const int first_inc = m_inc ? __ffsll(m_inc) - 1 : 64;  // nearest inclusive predecessor
-            // all lanes up to first_inc must be ready
-            const unsigned long long m_notready = __ballot(!ready);
-            const unsigned long long need = first_inc >= 63 ? ~0ull : ((1ull << (first_inc + 1)) - 1);
-            if (m_notready & need) {
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(g.err, 16u); break; }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            const u64 mask48 = (1ull << 48) - 1;
-            u64 vd = (lane <= first_inc && t >= 0) ? (wd & mask48) : 0;
-            u64 vu = (lane <= first_inc && t >= 0) ? (wu & mask48) : 0;
-            u64 vx = (lane <= first_inc && t >= 0) ? (wx & mask48) : 0;
+        __syncthreads();
+        sd = g.out_delta + s_base[0];
+        su = g.out_upd ? g.out_upd + s_base[1] : nullptr;
+    } else {
+        sd = g.stage_delta + tile * (u64)TILE;
+        su = g.stage_upd + tile * (u64)TILE;
+    }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                vd += __shfl_xor(vd, o, 64);
-                vu += __shfl_xor(vu, o, 64);
-                vx += __shfl_xor(vx, o, 64);
-            }
-            pre_d += vd; pre_u += vu; pre_x += vx;
-            if (first_inc < 64) break;
-            base -= 64;
-        }
-        if (lane == 0) {
-            __hip_atomic_store(g.st_d + tile, gran(g.epoch, true, pre_d + agg_d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g.st_u + tile, gran(g.epoch, true, pre_u + agg_u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g.st_x + tile, gran(g.epoch, true, pre_x + agg_x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_bcast[1] = pre_d;
-            s_bcast[2] = pre_u;
-            if (tile == g.ntiles - 1) {
-                const u64 td = pre_d + agg_d, tu = pre_u + agg_u, tx = pre_x + agg_x;
-                g.counts[0] = td - tu - tx;
-                g.counts[1] = tu;
-                g.counts[2] = tx;
-                g.counts[3] = td;
-            }
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
+        if (kind == R_DEL) sd[od++] = make_uint2((u32)(i0 + ia), KD_NONE);
+        else if (kind == R_INS) sd[od++] = make_uint2(KD_NONE, (u32)(j0 + jb));
+        else if (kind == R_MATCH && ((rec[k] >> 24) & 1)) {
+            const uint2 v = make_uint2((u32)(i0 + ia), (u32)(j0 + jb));
+            sd[od++] = v;
+            if (su) su[ou++] = v;
         }
     }
-    __syncthreads();
-    u64 od = s_bcast[1] + (off_packed & 0xFFFF), ou = s_bcast[2] + (off_packed >> 16);
-    {
-        int ia = ia0, jb = jb0;
-        for (int k = 0; k < IPT; k++) {
-            if (k >= cnt) break;
-            if (jb >= nb || (ia < na && sA[ia] <= sB[jb])) {
-                u16 p = s_partner[ia];
-                if (p == NOP) g.out_delta[od++] = make_uint2((u32)(i0 + ia), KD_NONE);
-                else if (s_chg[ia]) {
-                    uint2 v = make_uint2((u32)(i0 + ia), (u32)(j0 + p));
-                    g.out_delta[od++] = v;
-                    if (g.out_upd) g.out_upd[ou++] = v;
-                }
-                ia++;
-            } else {
-                u64 kb = sB[jb];
-                bool partner = ia > 0 ? sA[ia - 1] == kb : (has_lbA && lbA == kb);
-                if (!partner) g.out_delta[od++] = make_uint2(KD_NONE, (u32)(j0 + jb));
-                jb++;
-            }
-        }
+    if (!UNORD && tid == 0) {
+        u32* c = g.tile_cnt + 4 * tile;
+        c[0] = tnd - tnu - tot_del;
+        c[1] = tnu;
+        c[2] = tot_del;
+        c[3] = tnd;
     }
 }
 
-// look-back state: [tile counter | 3 granule arrays of ntiles].  Zeroed when (re)allocated and
-// whenever the 15-bit epoch wraps; otherwise every call tags its granules with a fresh epoch and
-// takes tile ids from the monotonic counter (tile = counter - tile_base).
-int lookback_state(kd_ctx* ctx, u64 ntiles, void** out) {
-    const size_t bytes = 64 + 3 * ntiles * sizeof(u64);
-    kd::DevBuf& b = ctx->bufs["c2.lb"];
-    const bool fresh = b.bytes < bytes;
-    int rc;
-    if ((rc = ensure(ctx, "c2.lb", bytes, out))) return rc;
-    if (fresh) {
-        KD_HIP(hipMemsetAsync(*out, 0, ctx->bufs["c2.lb"].bytes, ctx->stream));
-        ctx->c2_tile_base = 0;
-        ctx->c2_epoch = 0;
+// Exclusive scan of the per-tile (deltas, updates) counts -> tile_off; totals -> counts[0..3].
+// One block of NT threads; thread t owns tiles [t*PER, t*PER+PER) of each CHUNK = NT*PER tiles;
+// its PER 16-byte count loads are issued together (one memory round trip per chunk).
+template <int NT, int PER>
+__global__ __launch_bounds__(NT) void k_scan_tiles(const u32* __restrict__ tile_cnt, u64 ntiles,
+                                                   uint2* __restrict__ tile_off, u64* __restrict__ counts) {
+    __shared__ u64 s_w[4][NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    u64 carry_d = 0, carry_u = 0, ti = 0, tx = 0;
+    for (u64 base = 0; base < ntiles; base += (u64)NT * PER) {
+        const u64 b = base + (u64)tid * PER;
+        uint4 c[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const u64 t = b + k < ntiles ? b + k : 0;
+            c[k] = *(const uint4*)(tile_cnt + 4 * t);
+        }
+        u64 sd = 0, su = 0, si = 0, sx = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (b + k < ntiles) { si += c[k].x; su += c[k].y; sx += c[k].z; sd += c[k].w; }
+        u64 xd = sd, xu = su;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            u64 yd = __shfl_up(xd, o, 64), yu = __shfl_up(xu, o, 64);
+            if (lane >= o) { xd += yd; xu += yu; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { si += __shfl_xor(si, o, 64); sx += __shfl_xor(sx, o, 64); }
+        if (lane == 63) { s_w[0][wid] = xd; s_w[1][wid] = xu; }
+        if (lane == 0) { s_w[2][wid] = si; s_w[3][wid] = sx; }
+        __syncthreads();
+        u64 pd = 0, pu = 0, td = 0, tu = 0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; w++) {
+            if (w < wid) { pd += s_w[0][w]; pu += s_w[1][w]; }
+            td += s_w[0][w]; tu += s_w[1][w]; ti += s_w[2][w]; tx += s_w[3][w];
+        }
+        __syncthreads();
+        u64 od = carry_d + pd + xd - sd, ou = carry_u + pu + xu - su;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            if (b + k < ntiles) {
+                tile_off[b + k] = make_uint2((u32)od, (u32)ou);  // one GPU's deltas fit uint32 indices
+                od += c[k].w;
+                ou += c[k].y;
+            }
+        }
+        carry_d += td;
+        carry_u += tu;
     }
-    ctx->c2_epoch = (ctx->c2_epoch + 1) & 0x7FFF;
-    if (ctx->c2_epoch == 0) {
-        KD_HIP(hipMemsetAsync(*out, 0, ctx->bufs["c2.lb"].bytes, ctx->stream));
-        ctx->c2_tile_base = 0;
-        ctx->c2_epoch = 1;
+    if (tid == 0) {
+        counts[0] = ti;
+        counts[1] = carry_u;
+        counts[2] = tx;
+        counts[3] = carry_d;
     }
-    return KD_OK;
+}
+
+// Tile-local staging -> final key-ordered positions; one tile per block.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scatter2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
+                                                 const u32* __restrict__ tile_cnt, const uint2* __restrict__ tile_off,
+                                                 int tile_items, uint2* __restrict__ out_delta,
+                                                 uint2* __restrict__ out_upd) {
+    const u64 t = blockIdx.x;
+    const uint4 c = *(const uint4*)(tile_cnt + 4 * t);
+    const uint2 o = tile_off[t];
+    const uint2* sdp = stage_delta + t * (u64)tile_items;
+    const uint2* sup = stage_upd + t * (u64)tile_items;
+    for (u32 k = threadIdx.x; k < c.w; k += NT) out_delta[o.x + k] = sdp[k];
+    if (out_upd)
+        for (u32 k = threadIdx.x; k < c.y; k += NT) out_upd[o.y + k] = sup[k];
 }
 
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
                  u64* d_counts, u32* d_err) {
-    (void)flags;
+    const bool unord = (flags & KD_DIFF_UNORDERED) != 0;
     const u64 nA = A->n, nB = B->n, total = nA + nB;
     KD_CHECK(nA < 0xFFFFFFFFull && nB < 0xFFFFFFFFull, "diff2: side too large for uint32 indices");
     const bool hash = A->key_mode == KD_KEY_HASH || B->key_mode == KD_KEY_HASH;
@@ -312,42 +389,62 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     if (hash) KD_CHECK((nA == 0 || (A->name && A->name_off)) && (nB == 0 || (B->name && B->name_off)),
                        "diff2: KD_KEY_HASH needs filenames");
     const u64 ntiles = (total + C2_TILE - 1) / C2_TILE;
-    KD_HIP(hipMemsetAsync(d_err, 0, sizeof(u32), ctx->stream));
     if (ntiles == 0) {
+        KD_HIP(hipMemsetAsync(d_err, 0, sizeof(u32), ctx->stream));
         KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
         return KD_OK;
     }
-    void *part, *lb;
+    void *part, *tcnt, *toff, *sdel, *supd;
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
-    if ((rc = lookback_state(ctx, ntiles, &lb))) return rc;
-    u64* tile_ctr = (u64*)lb;
-    u64* st = (u64*)((u8*)lb + 64);
-    const u64 empty = 0;
-    const u64* kA = nA ? A->key : &empty;  // never dereferenced when n == 0
-    const u64* kB = nB ? B->key : &empty;
+    if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
+    if ((rc = ensure(ctx, "c2.toff", ntiles * sizeof(uint2), &toff))) return rc;
+    if (!unord) {
+        if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_TILE * sizeof(uint2), &sdel))) return rc;
+        if ((rc = ensure(ctx, "c2.supd", ntiles * C2_TILE * sizeof(uint2), &supd))) return rc;
+    } else {
+        sdel = supd = nullptr;
+    }
+    void* dz;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    const u64* kA = nA ? A->key : (const u64*)dz;  // an empty side points at device zeros
+    const u64* kB = nB ? B->key : (const u64*)dz;
+    const u8* empty_oid = (const u8*)dz;
     rc = launch(ctx, "k_partition2", [&] {
-        unsigned nb = (unsigned)((ntiles + 1 + 3) / 4);
-        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(256), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part);
+        unsigned nb = (unsigned)(((ntiles + 1) * PW + 255) / 256);
+        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(256), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part,
+                           d_counts, d_err);
     });
     if (rc) return rc;
     Join2Args g;
-    g.A = kA; g.oidA = (const u32*)A->oid; g.nA = nA;
-    g.B = kB; g.oidB = (const u32*)B->oid; g.nB = nB;
+    g.A = kA; g.oidA = nA ? A->oid : empty_oid; g.nA = nA;
+    g.B = kB; g.oidB = nB ? B->oid : empty_oid; g.nB = nB;
     g.part = (const u64*)part;
     g.nameA = A->name; g.nameOffA = A->name_off; g.nameB = B->name; g.nameOffB = B->name_off;
     g.hash_mode = hash ? 1 : 0;
-    g.ntiles = ntiles;
-    g.tile_base = ctx->c2_tile_base;
-    g.tile_ctr = tile_ctr;
-    g.st_d = st; g.st_u = st + ntiles; g.st_x = st + 2 * ntiles;
-    g.epoch = ctx->c2_epoch;
-    g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd;
-    g.counts = d_counts; g.err = d_err;
+    g.dummy = (const u8*)dz;
+    g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
+    g.tile_cnt = (u32*)tcnt; g.err = d_err;
+    g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd; g.counts = d_counts;
+    if (unord) {
+        return launch(ctx, "k_join2", [&] {
+            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+        });
+    }
     rc = launch(ctx, "k_join2", [&] {
-        hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+        hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
     });
-    ctx->c2_tile_base += ntiles;
+    if (rc) return rc;
+    rc = launch(ctx, "k_scan_tiles", [&] {
+        hipLaunchKernelGGL((k_scan_tiles<1024, 4>), dim3(1), dim3(1024), 0, ctx->stream, (const u32*)tcnt, ntiles,
+                           (uint2*)toff, d_counts);
+    });
+    if (rc) return rc;
+    rc = launch(ctx, "k_scatter2", [&] {
+        hipLaunchKernelGGL((k_scatter2<64>), dim3((unsigned)ntiles), dim3(64), 0, ctx->stream, (const uint2*)sdel,
+                           (const uint2*)supd, (const u32*)tcnt, (const uint2*)toff, C2_TILE, (uint2*)d_delta,
+                           (uint2*)d_upd);
+    });
     return rc;
 }
 

@@ -36,6 +36,15 @@ int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out) {
     return KD_OK;
 }
 
+int device_zeros(kd_ctx* ctx, void** out) {
+    kd::DevBuf& b = ctx->bufs["zeros"];
+    const bool fresh = b.p == nullptr;
+    int rc = ensure(ctx, "zeros", 256, out);
+    if (rc) return rc;
+    if (fresh) KD_HIP(hipMemsetAsync(*out, 0, 256, ctx->stream));
+    return KD_OK;
+}
+
 int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem, const void** dev) {
     if (p == nullptr || bytes == 0 || mem == KD_MEM_DEVICE) {
         *dev = p;

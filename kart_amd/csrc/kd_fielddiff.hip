@@ -185,15 +185,30 @@ constexpr int FD_NT = 64;  // one wave per block: each lane owns one update and 
 // nullptr when the blob does not fit (the lane then parses straight from global memory).
 template <int SLOT>
 __device__ __forceinline__ const u8* stage_blob(const u8* __restrict__ data, u64 start, u32 len, u64 arena_end,
-                                                uint4* slot) {
-    const u64 base = start & ~(u64)15;
-    const u32 delta = (u32)(start - base);
+                                                u32x4* slot) {
+    (void)arena_end;
+    // 16-byte chunks of the aligned-down *absolute* address: an aligned chunk that holds a valid
+    // byte lies in one mapped page, so reading the whole chunk cannot fault.
+    const u64 a0 = (u64)data + start;
+    const u64 base = a0 & ~(u64)15;
+    const u32 delta = (u32)(a0 - base);
     const u32 nch = (delta + len + 15) >> 4;
-    if (nch * 16 > (u32)SLOT || base + (u64)nch * 16 > arena_end) return nullptr;
-    const uint4* src = (const uint4*)(data + base);
+    if (nch * 16 > (u32)SLOT) return nullptr;
+    typedef const __attribute__((address_space(1))) u32x4* gp;
+    constexpr int B = 8;  // chunks in flight per batch (branch-free issue, then LDS stores)
 #pragma unroll
-    for (int c = 0; c < SLOT / 16; c++)
-        if (c < (int)nch) slot[c] = src[c];
+    for (int c0 = 0; c0 < SLOT / 16; c0 += B) {
+        if (c0 >= (int)nch) break;
+        u32x4 v[B];
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            const int c = c0 + k < (int)nch ? c0 + k : c0;
+            v[k] = *(gp)(base + 16ull * c);
+        }
+#pragma unroll
+        for (int k = 0; k < B; k++)
+            if (c0 + k < (int)nch) slot[c0 + k] = v[k];
+    }
     return (const u8*)slot + delta;
 }
 
@@ -203,7 +218,7 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
                                                      const u64* __restrict__ n_upd_dev, FdTab tb,
                                                      u64* __restrict__ masks, u8* __restrict__ status) {
-    __shared__ uint4 s_slots[SLOT > 0 ? FD_NT * 2 * (SLOT / 16) : 1];
+    __shared__ u32x4 s_slots[SLOT > 0 ? FD_NT * 2 * (SLOT / 16) : 1];
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 o_end = ooff[on_blobs], n_end = noff[nn_blobs];
     const int lane = threadIdx.x;
@@ -217,7 +232,7 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         const u8* ob = nullptr;
         const u8* nb = nullptr;
         if constexpr (SLOT > 0) {
-            uint4* my = s_slots + (size_t)lane * 2 * (SLOT / 16);
+            u32x4* my = s_slots + (size_t)lane * 2 * (SLOT / 16);
             ob = stage_blob<SLOT>(od, os, on, o_end, my);
             nb = stage_blob<SLOT>(nd, ns, nn, n_end, my + SLOT / 16);
         }

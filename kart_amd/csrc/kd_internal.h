@@ -18,6 +18,7 @@ typedef uint64_t u64;
 typedef int64_t i64;
 typedef int16_t i16;
 typedef int8_t i8;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector (SROA-friendly)
 
 namespace kd {
 
@@ -82,6 +83,10 @@ namespace kd {
 // kd_reserve() has sized it.
 int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out);
 
+// 256 zero bytes of device memory: what empty inputs point at, and the target of loads issued by
+// masked-off lanes in branch-free load batches (never a host address)
+int device_zeros(kd_ctx* ctx, void** out);
+
 // profiling wrappers around a launch on ctx->stream
 void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a);
 void prof_end(kd_ctx* ctx, const char* name, hipEvent_t a);
@@ -105,7 +110,6 @@ inline int launch(kd_ctx* ctx, const char* name, F&& f) {
 int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem, const void** dev);
 
 // ---- classify2 (device form), kd_classify.hip ----
-int lookback_state(kd_ctx* ctx, u64 ntiles, void** out);
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
                  u32* d_upd, u64* d_counts, u32* d_err);
 constexpr int C2_NT = 256;

@@ -68,8 +68,9 @@ class DevBlobs:
 class DiffPipeline:
     """classify2 + fused-by-stream fielddiff over device-resident sides (one GPU)."""
 
-    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, device):
+    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, device, ordered=True):
         self.eng = engine
+        self.flags = 0 if ordered else N.KD_DIFF_UNORDERED
         self.device = device
         self.A = DevSide(base, device)
         self.B = DevSide(target, device)
@@ -90,7 +91,7 @@ class DiffPipeline:
     def step(self):
         L, ctx = self.eng.L, self.eng.ctx
         err_ptr = self.counts.data_ptr() + 4 * 8
-        N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), 0, self.delta.data_ptr(),
+        N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.data_ptr(),
                                   self.upd.data_ptr(), self.counts.data_ptr(), err_ptr), "kd_diff2_device")
         N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.data_ptr(), 0,
                                ctypes.cast(self.counts.data_ptr() + 8, N.c_u64p), N.KD_MEM_DEVICE,

@@ -234,3 +234,32 @@ def test_gpu_env_overlap_vs_oracle(engine):
         g = engine.env_overlap(enc, 20, q)
         o = O.envelope_overlap(enc, 20, q)
         assert np.array_equal(g, o)
+
+
+@pytest.mark.parametrize("ordered", [True, False])
+@pytest.mark.parametrize("n", [1000, 3_000_000])
+def test_gpu_device_pipeline_vs_oracle(engine, n, ordered):
+    """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes)"""
+    import torch
+
+    from kart_amd import synth
+    from kart_amd.device import DiffPipeline
+    from kart_amd.schema import FieldMaps
+
+    L = synth.points_layer(n, seed=11)
+    maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, torch.device("cuda", 0),
+                        ordered=ordered)
+    for _ in range(3):  # repeated steps reuse the workspaces and counters
+        pipe.step()
+    engine.sync()
+    counts, delta, upd, masks, status = pipe.results()
+    od, oc = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
+    if ordered:
+        assert np.array_equal(delta, od)
+    else:
+        key = lambda a: sorted(map(tuple, a.tolist()))
+        assert key(delta) == key(od)
+    assert (counts["inserts"], counts["updates"], counts["deletes"]) == (oc["inserts"], oc["updates"], oc["deletes"])
+    om, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
+    assert np.array_equal(masks, om) and np.array_equal(status, ost)
