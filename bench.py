@@ -4,8 +4,8 @@
 Workload (BASELINE.json configs[1], "C2"): a synthetic 10M-point int-PK layer per GPU with seeded
 1% updates / 1% deletes / 1% inserts (kart_amd.synth.points_layer; the reference's feature blob
 and path encodings, synthetic OIDs).  One *step* = one full pass of the hot path over that layer:
-merge-path join + OID compare + ordered compaction of the delta set (k_partition2, k_join2,
-k_scan_tiles, k_scatter2), then the msgpack field decode + Python-== column compare of every
+merge-path join + OID compare + key-ordered compaction of the delta set (k_partition2, k_join2,
+k_place2), then the msgpack field decode + Python-== column compare of every
 update (k_fielddiff) — all on the device, inputs resident in HBM before the timed region.
 
 Multi-GPU (torch.distributed, one process per GPU, RCCL): each rank owns a disjoint dataset3
@@ -36,8 +36,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU (C2: 10M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--ordered", action="store_true",
-                    help="key-ordered delta list (adds the scan + scatter kernels); default: tile-grouped")
+    ap.add_argument("--unordered", action="store_true",
+                    help="tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
     return ap.parse_args()
@@ -77,7 +77,7 @@ def main():
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     eng = Engine(torch.cuda.current_device())
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, dev, ordered=args.ordered)
+    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, dev, ordered=not args.unordered)
     torch.cuda.synchronize()
 
     # ---- warmup + correctness of the resident pipeline against the generator's own counts ----
@@ -119,7 +119,7 @@ def main():
         total_pairs, total_deltas = n_pairs, counts["deltas"]
 
     kern = {}
-    for name in ("k_partition2", "k_join2", "k_scan_tiles", "k_scatter2", "k_fielddiff"):  # kernels of a step
+    for name in ("k_partition2", "k_join2", "k_place2", "k_fielddiff"):  # kernels of a step
         launches, ms = eng.prof_get(name)
         if launches:
             kern[name] = (launches, ms / launches)
@@ -171,7 +171,7 @@ def main():
             "data": "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
             "config": {"workload": "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
                        "points_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
-                       "delta_order": "key" if args.ordered else "tile-grouped (same delta set)",
+                       "delta_order": "tile-grouped (same delta set)" if args.unordered else "key",
                        "parallelism": f"bucket-range shards x{world}"},
             "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
             "roofline": roof,

@@ -142,8 +142,10 @@ int kd_diff2_device(kd_ctx* ctx, const kd_side* base, const kd_side* target, uin
  * bit k set iff union key k changed under Python `==`.  status[u]: 0 ok, 1 malformed blob,
  * 2 unknown legend, 3 too many values, 4 unsupported value (nested container, invalid ext 'G'):
  * nonzero -> the caller recomputes that update on the CPU path.
- * pairs_mem / out_mem say where pu and masks/status live; n_upd may be read from a device
- * counter (d_n_upd != NULL, device form) so no host sync is needed between classify and diff. */
+ * pairs_mem / out_mem say where pu and masks/status live.  Device form: with d_n_upd != NULL the
+ * update count is read from that device counter (no host sync between classify and diff), pu
+ * and the outputs must be device memory, and n_upd is the capacity — an upper bound of *d_n_upd
+ * used to size the grid (0 = unknown). */
 int kd_fielddiff(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_blobs* new_blobs,
                  const uint32_t* pu, uint64_t n_upd, const uint64_t* d_n_upd, uint32_t pairs_mem,
                  const kd_legend_maps* maps, uint64_t* masks, uint8_t* status, uint32_t out_mem);

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g) {
     const int tid = threadIdx.x;
     const u64 a0 = g.bounds[3 * tile], o0 = g.bounds[3 * tile + 1], t0 = g.bounds[3 * tile + 2];
     const u64 a1 = g.bounds[3 * tile + 3], o1 = g.bounds[3 * tile + 4], t1 = g.bounds[3 * tile + 5];
-    u32 clean = 0, nconf = 0, nmd = 0;
+    u32 clean = 0;
     u32 base_c = 0, base_m = 0;  // running output offsets within the tile slot
     if (a1 < a0 || o1 < o0 || t1 < t0) {
         if (tid == 0) atomicOr(g.err, 1u);
@@ -283,9 +283,9 @@ int kd_reserve(kd_ctx* ctx, uint64_t max_entries_per_side, uint64_t max_updates)
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * 8, &p))) return rc;
     if ((rc = ensure(ctx, "c2.tcnt", ntiles * 16, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.toff", ntiles * 8, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_TILE * 8, &p))) return rc;
-    if ((rc = ensure(ctx, "c2.supd", ntiles * C2_TILE * 8, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.gsum", 2 * (ntiles / 64 + 1) * 8, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.sdel", ntiles * (C2_TILE + 64) * 8, &p))) return rc;
+    if ((rc = ensure(ctx, "c2.supd", ntiles * (C2_TILE + 64) * 8, &p))) return rc;
     (void)max_updates;
     return KD_OK;
 }

@@ -7,16 +7,17 @@
 //
 //   k_partition2  merge-path split points of the union sequence: 8 lanes per tile boundary,
 //                 8-ary search (8 dependent HBM round trips instead of ~24 for binary search)
-//   k_join2       per 2048-item tile:
-//                   0. the tile's key and OID byte ranges (both sides) -> LDS as 16-B chunks, every
-//                      load issued before any use (~56 KB in flight per workgroup)
-//                   A. per-thread merge path over 8 items in LDS; partner of every A item
-//                   B. OID compare of matched pairs from LDS
-//                   C. ordered compaction (block scan) of the tile's deltas and updates into a
-//                      tile-local staging slot + per-tile counts
-//   k_scatter2    each block reduces the counts of all preceding tiles (L2-resident) to find its
-//                 offsets, then copies its tiles' staged records to their final key-ordered
-//                 positions; the last block writes the totals.
+//   k_join2       per 2048-item tile (256 threads x 8 items):
+//                   0. the tile's key ranges (both sides) -> LDS as 16-B chunks, every load issued
+//                      before any use
+//                   A. per-thread merge path over 8 items in LDS; each item's outcome (kind, local
+//                      indices) kept in a register record
+//                   B. OID compare of matched pairs: 20-B OIDs loaded in batches straight from HBM
+//                   C. block scan of the tile's delta/update counts; records written key-ordered
+//                      into a tile-local staging slot (ordered) or appended per tile (unordered)
+//   k_place2      one tile per block: output offset from 64-tile group sums (accumulated by the
+//                 join) + the earlier tiles of its group; staged records -> final key-ordered
+//                 positions; totals from the last block.
 // Inputs are read once; the staging round trip costs 16 B per delta.
 #include "kd_join.h"
 
@@ -27,14 +28,26 @@ namespace kd {
 // A binary search is ~24 dependent HBM round trips at 10M keys; a 64-ary one needs 4 but fetches
 // 128 random lines per round per boundary.  PW = 8 lanes: 8 round trips, 16 lines per round.
 constexpr int PW = 8;
+constexpr u64 C2_GROUP = 64;  // tiles per group sum (k_place2 offsets)
+#ifndef KD_C2_STAGE_PAD
+#define KD_C2_STAGE_PAD 32
+#endif
+// staging slot stride in records: one tile plus a pad, so the slots' hot first lines do not all
+// fall on the same HBM channels (a 16 KB power-of-two stride would)
+constexpr u64 C2_STAGE = C2_TILE + KD_C2_STAGE_PAD;
+#ifndef KD_PLACE_NT
+#define KD_PLACE_NT 64  // one wave per tile: up to 32 staged records per lane, all loads in flight
+#endif
 
 __global__ __launch_bounds__(256) void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B,
                                                     u64 nB, u64 ntiles, u64* __restrict__ part,
-                                                    u64* __restrict__ zero_counts, u32* __restrict__ zero_err) {
+                                                    u64* __restrict__ zero_counts, u32* __restrict__ zero_err,
+                                                    u64* __restrict__ zero_gsum, u64 n_gsum) {
     // the join's counters start at zero: cleared here (stream-ordered before k_join2) instead of
     // by separate memset launches
     if (blockIdx.x == 0 && threadIdx.x < 4) zero_counts[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 4) *zero_err = 0;
+    for (u64 k = (u64)blockIdx.x * 256 + threadIdx.x; k < n_gsum; k += (u64)gridDim.x * 256) zero_gsum[k] = 0;
     const u64 t = ((u64)blockIdx.x * 256 + threadIdx.x) / PW;
     const int sub = threadIdx.x % PW;
     const int lane = threadIdx.x & 63;
@@ -78,6 +91,7 @@ struct Join2Args {
     uint2* stage_delta;  // ordered mode: tile-local slots of TILE records
     uint2* stage_upd;
     u32* tile_cnt;       // ordered mode: [ntiles*4] inserts, updates, deletes, deltas
+    u64* gsum;           // ordered mode: [2*ngroups] per C2_GROUP tiles: deltas | updates<<32, inserts | deletes<<32
     uint2* out_delta;    // unordered mode: final lists, appended per tile
     uint2* out_upd;
     u64* counts;         // unordered mode: [4] inserts, updates, deletes, deltas (atomic)
@@ -281,8 +295,8 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         sd = g.out_delta + s_base[0];
         su = g.out_upd ? g.out_upd + s_base[1] : nullptr;
     } else {
-        sd = g.stage_delta + tile * (u64)TILE;
-        su = g.stage_upd + tile * (u64)TILE;
+        sd = g.stage_delta + tile * (u64)C2_STAGE;
+        su = g.stage_upd + tile * (u64)C2_STAGE;
     }
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
@@ -297,86 +311,104 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     }
     if (!UNORD && tid == 0) {
         u32* c = g.tile_cnt + 4 * tile;
-        c[0] = tnd - tnu - tot_del;
+        const u32 tins = tnd - tnu - tot_del;
+        c[0] = tins;
         c[1] = tnu;
         c[2] = tot_del;
         c[3] = tnd;
+        // group sums (<= 64 tiles x 2048 per 32-bit half: no carry between halves); a handful of
+        // atomics per address
+        u64* gs = g.gsum + 2 * (tile / C2_GROUP);
+        atomicAdd((unsigned long long*)gs, (unsigned long long)(tnd | (u64)tnu << 32));
+        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)tot_del << 32));
     }
 }
 
-// Exclusive scan of the per-tile (deltas, updates) counts -> tile_off; totals -> counts[0..3].
-// One block of NT threads; thread t owns tiles [t*PER, t*PER+PER) of each CHUNK = NT*PER tiles;
-// its PER 16-byte count loads are issued together (one memory round trip per chunk).
-template <int NT, int PER>
-__global__ __launch_bounds__(NT) void k_scan_tiles(const u32* __restrict__ tile_cnt, u64 ntiles,
-                                                   uint2* __restrict__ tile_off, u64* __restrict__ counts) {
-    __shared__ u64 s_w[4][NT / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    u64 carry_d = 0, carry_u = 0, ti = 0, tx = 0;
-    for (u64 base = 0; base < ntiles; base += (u64)NT * PER) {
-        const u64 b = base + (u64)tid * PER;
-        uint4 c[PER];
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const u64 t = b + k < ntiles ? b + k : 0;
-            c[k] = *(const uint4*)(tile_cnt + 4 * t);
-        }
-        u64 sd = 0, su = 0, si = 0, sx = 0;
-#pragma unroll
-        for (int k = 0; k < PER; k++)
-            if (b + k < ntiles) { si += c[k].x; su += c[k].y; sx += c[k].z; sd += c[k].w; }
-        u64 xd = sd, xu = su;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            u64 yd = __shfl_up(xd, o, 64), yu = __shfl_up(xu, o, 64);
-            if (lane >= o) { xd += yd; xu += yu; }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { si += __shfl_xor(si, o, 64); sx += __shfl_xor(sx, o, 64); }
-        if (lane == 63) { s_w[0][wid] = xd; s_w[1][wid] = xu; }
-        if (lane == 0) { s_w[2][wid] = si; s_w[3][wid] = sx; }
-        __syncthreads();
-        u64 pd = 0, pu = 0, td = 0, tu = 0;
-#pragma unroll
-        for (int w = 0; w < NT / 64; w++) {
-            if (w < wid) { pd += s_w[0][w]; pu += s_w[1][w]; }
-            td += s_w[0][w]; tu += s_w[1][w]; ti += s_w[2][w]; tx += s_w[3][w];
-        }
-        __syncthreads();
-        u64 od = carry_d + pd + xd - sd, ou = carry_u + pu + xu - su;
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            if (b + k < ntiles) {
-                tile_off[b + k] = make_uint2((u32)od, (u32)ou);  // one GPU's deltas fit uint32 indices
-                od += c[k].w;
-                ou += c[k].y;
-            }
-        }
-        carry_d += td;
-        carry_u += tu;
-    }
-    if (tid == 0) {
-        counts[0] = ti;
-        counts[1] = carry_u;
-        counts[2] = tx;
-        counts[3] = carry_d;
-    }
-}
-
-// Tile-local staging -> final key-ordered positions; one tile per block.
+// Tile-local staging -> final key-ordered positions; one tile per block.  The tile's output
+// offset = the group sums of all earlier C2_GROUP-tile groups + the counts of the earlier tiles of
+// its own group (at most ngroups + C2_GROUP - 1 loads, issued together); the last block also
+// writes the totals.  Work per block is bounded by one tile, so insert-dense regions do not
+// serialise.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_scatter2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
-                                                 const u32* __restrict__ tile_cnt, const uint2* __restrict__ tile_off,
-                                                 int tile_items, uint2* __restrict__ out_delta,
-                                                 uint2* __restrict__ out_upd) {
+__global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
+                                               const u32* __restrict__ tile_cnt, const u64* __restrict__ gsum,
+                                               u64 ntiles, int tile_items, uint2* __restrict__ out_delta,
+                                               uint2* __restrict__ out_upd, u64* __restrict__ counts) {
+    __shared__ u64 s_red[4][NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const u64 t = blockIdx.x;
-    const uint4 c = *(const uint4*)(tile_cnt + 4 * t);
-    const uint2 o = tile_off[t];
+    const u64 grp = t / C2_GROUP, ngroups = (ntiles + C2_GROUP - 1) / C2_GROUP;
+    const bool last = t == ntiles - 1;
+    const u64 g_end = last ? ngroups : grp;  // the last block sums every group for the totals
+    u64 pd = 0, pu = 0, si = 0, sx = 0;
+    for (u64 k = tid; k < g_end; k += NT) {
+        const u64 a = gsum[2 * k];
+        if (k < grp) { pd += a & 0xFFFFFFFFu; pu += a >> 32; }
+        if (last) {
+            const u64 b = gsum[2 * k + 1];
+            si += b & 0xFFFFFFFFu; sx += b >> 32;
+            if (k >= grp) { pd += a & 0xFFFFFFFFu; pu += a >> 32; }  // totals: all groups
+        }
+    }
+    // counts of the earlier tiles of this group (the last block already has them in the totals)
+    const u64 t_lo = grp * C2_GROUP;
+    if (!last && tid < (int)(t - t_lo)) {
+        const uint4 c = *(const uint4*)(tile_cnt + 4 * (t_lo + tid));
+        pd += c.w;
+        pu += c.y;
+    }
+    const uint4 own = *(const uint4*)(tile_cnt + 4 * t);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        pd += __shfl_xor(pd, o, 64); pu += __shfl_xor(pu, o, 64);
+        si += __shfl_xor(si, o, 64); sx += __shfl_xor(sx, o, 64);
+    }
+    if (lane == 0) { s_red[0][wid] = pd; s_red[1][wid] = pu; s_red[2][wid] = si; s_red[3][wid] = sx; }
+    __syncthreads();
+    pd = pu = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) { pd += s_red[0][w]; pu += s_red[1][w]; }
+    if (last) {
+        // pd/pu are the totals here; this tile's records start at total - own count
+        if (tid == 0) {
+            u64 ti = 0, tx = 0;
+#pragma unroll
+            for (int w = 0; w < NT / 64; w++) { ti += s_red[2][w]; tx += s_red[3][w]; }
+            counts[0] = ti;
+            counts[1] = pu;
+            counts[2] = tx;
+            counts[3] = pd;
+        }
+        pd -= own.w;
+        pu -= own.y;
+    }
     const uint2* sdp = stage_delta + t * (u64)tile_items;
     const uint2* sup = stage_upd + t * (u64)tile_items;
-    for (u32 k = threadIdx.x; k < c.w; k += NT) out_delta[o.x + k] = sdp[k];
-    if (out_upd)
-        for (u32 k = threadIdx.x; k < c.y; k += NT) out_upd[o.y + k] = sup[k];
+    // C2_TILE / NT records per thread at most: every load before any store
+    constexpr int UC = C2_TILE / NT;
+    uint2 v[UC];
+#pragma unroll
+    for (int j = 0; j < UC; j++) {
+        const u32 r = j * NT + tid;
+        if (r < own.w) v[j] = sdp[r];
+    }
+#pragma unroll
+    for (int j = 0; j < UC; j++) {
+        const u32 r = j * NT + tid;
+        if (r < own.w) out_delta[pd + r] = v[j];
+    }
+    if (out_upd) {
+#pragma unroll
+        for (int j = 0; j < UC; j++) {
+            const u32 r = j * NT + tid;
+            if (r < own.y) v[j] = sup[r];
+        }
+#pragma unroll
+        for (int j = 0; j < UC; j++) {
+            const u32 r = j * NT + tid;
+            if (r < own.y) out_upd[pu + r] = v[j];
+        }
+    }
 }
 
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
@@ -394,14 +426,15 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
         return KD_OK;
     }
-    void *part, *tcnt, *toff, *sdel, *supd;
+    void *part, *tcnt, *sdel, *supd, *gsum = nullptr;
+    const u64 n_gsum = unord ? 0 : 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
     if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
-    if ((rc = ensure(ctx, "c2.toff", ntiles * sizeof(uint2), &toff))) return rc;
+    if (n_gsum && (rc = ensure(ctx, "c2.gsum", n_gsum * sizeof(u64), &gsum))) return rc;
     if (!unord) {
-        if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_TILE * sizeof(uint2), &sdel))) return rc;
-        if ((rc = ensure(ctx, "c2.supd", ntiles * C2_TILE * sizeof(uint2), &supd))) return rc;
+        if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_STAGE * sizeof(uint2), &sdel))) return rc;
+        if ((rc = ensure(ctx, "c2.supd", ntiles * C2_STAGE * sizeof(uint2), &supd))) return rc;
     } else {
         sdel = supd = nullptr;
     }
@@ -413,7 +446,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     rc = launch(ctx, "k_partition2", [&] {
         unsigned nb = (unsigned)(((ntiles + 1) * PW + 255) / 256);
         hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(256), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part,
-                           d_counts, d_err);
+                           d_counts, d_err, (u64*)gsum, n_gsum);
     });
     if (rc) return rc;
     Join2Args g;
@@ -424,7 +457,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.hash_mode = hash ? 1 : 0;
     g.dummy = (const u8*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
-    g.tile_cnt = (u32*)tcnt; g.err = d_err;
+    g.tile_cnt = (u32*)tcnt; g.gsum = (u64*)gsum; g.err = d_err;
     g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd; g.counts = d_counts;
     if (unord) {
         return launch(ctx, "k_join2", [&] {
@@ -435,15 +468,10 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
     });
     if (rc) return rc;
-    rc = launch(ctx, "k_scan_tiles", [&] {
-        hipLaunchKernelGGL((k_scan_tiles<1024, 4>), dim3(1), dim3(1024), 0, ctx->stream, (const u32*)tcnt, ntiles,
-                           (uint2*)toff, d_counts);
-    });
-    if (rc) return rc;
-    rc = launch(ctx, "k_scatter2", [&] {
-        hipLaunchKernelGGL((k_scatter2<64>), dim3((unsigned)ntiles), dim3(64), 0, ctx->stream, (const uint2*)sdel,
-                           (const uint2*)supd, (const u32*)tcnt, (const uint2*)toff, C2_TILE, (uint2*)d_delta,
-                           (uint2*)d_upd);
+    rc = launch(ctx, "k_place2", [&] {
+        hipLaunchKernelGGL((k_place2<KD_PLACE_NT>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream, (const uint2*)sdel,
+                           (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles, C2_STAGE, (uint2*)d_delta,
+                           (uint2*)d_upd, d_counts);
     });
     return rc;
 }

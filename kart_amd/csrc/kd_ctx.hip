@@ -205,6 +205,9 @@ int kd_init(int device_ordinal, kd_ctx** out) {
         return KD_EHIP;
     }
     c->stream = c->own_stream;
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) == hipSuccess && cu > 0)
+        c->n_cu = cu;
     *out = c;
     return KD_OK;
 }

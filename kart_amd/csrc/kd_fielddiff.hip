@@ -18,34 +18,55 @@
 
 namespace kd {
 
+// Blob bytes are read through address-space-qualified pointers: LDS-staged blobs as
+// address_space(3) (ds_read, word-wide compares), blobs too large for a slot as address_space(1)
+// (global loads).  A generic pointer would turn every byte access into a flat load.
+typedef const __attribute__((address_space(3))) u8* lp8;
+typedef const __attribute__((address_space(3))) u32* lp32;
+typedef const __attribute__((address_space(1))) u8* gp8;
+
 enum : u8 { V_NIL = 0, V_INT = 1, V_FLOAT = 2, V_STR = 3, V_BYTES = 4, V_EXT = 5 };
 
+template <class P>
 struct DVal {
     u8 cls;
     u8 big;     // V_INT: value in [2^63, 2^64) held in bits as uint64
     i8 ext;
     u64 bits;   // V_INT: int64 (or uint64 if big); V_FLOAT: double bits
-    const u8* p;
+    P p;
     u32 len;
 };
 
-__device__ __forceinline__ u64 ld_be(const u8* p, int w) {
+// big-endian W-byte integer: the W loads are independent (issued together)
+template <int W, class P>
+__device__ __forceinline__ u64 ld_be(P p) {
     u64 v = 0;
-    for (int i = 0; i < w; i++) v = (v << 8) | p[i];
+#pragma unroll
+    for (int i = 0; i < W; i++) v = (v << 8) | p[i];
     return v;
 }
 
+template <class P>
+__device__ __forceinline__ u64 ld_be_w(P p, int w) {
+    switch (w) {
+    case 1: return ld_be<1>(p);
+    case 2: return ld_be<2>(p);
+    case 4: return ld_be<4>(p);
+    default: return ld_be<8>(p);
+    }
+}
+
 // decode one value; returns bytes consumed, 0 on malformed / unsupported
-__device__ u32 dv_decode(const u8* __restrict__ p, const u8* end, DVal& v) {
-    if (p >= end) return 0;
-    const u64 avail = (u64)(end - p);
+template <class P>
+__device__ __forceinline__ u32 dv_decode(P p, u32 avail, DVal<P>& v) {
+    if (avail == 0) return 0;
     const u8 t = p[0];
     v.big = 0;
     if (t <= 0x7f) { v.cls = V_INT; v.bits = t; return 1; }
     if (t >= 0xe0) { v.cls = V_INT; v.bits = (u64)(i64)(int8_t)t; return 1; }
     if (t >= 0xa0 && t <= 0xbf) {
         u32 n = t & 31;
-        if (1 + (u64)n > avail) return 0;
+        if (1 + n > avail) return 0;
         v.cls = V_STR; v.p = p + 1; v.len = n; return 1 + n;
     }
     switch (t) {
@@ -54,101 +75,129 @@ __device__ u32 dv_decode(const u8* __restrict__ p, const u8* end, DVal& v) {
     case 0xc3: v.cls = V_INT; v.bits = 1; return 1;
     case 0xcc: case 0xcd: case 0xce: case 0xcf: {
         int w = 1 << (t - 0xcc);
-        if ((u64)(1 + w) > avail) return 0;
-        v.cls = V_INT; v.bits = ld_be(p + 1, w); v.big = (w == 8 && (v.bits >> 63)) ? 1 : 0;
+        if ((u32)(1 + w) > avail) return 0;
+        v.cls = V_INT; v.bits = ld_be_w(p + 1, w); v.big = (w == 8 && (v.bits >> 63)) ? 1 : 0;
         return 1 + w;
     }
     case 0xd0: case 0xd1: case 0xd2: case 0xd3: {
         int w = 1 << (t - 0xd0);
-        if ((u64)(1 + w) > avail) return 0;
+        if ((u32)(1 + w) > avail) return 0;
         int sh = 64 - 8 * w;
-        v.cls = V_INT; v.bits = (u64)(((i64)(ld_be(p + 1, w) << sh)) >> sh);
+        v.cls = V_INT; v.bits = (u64)(((i64)(ld_be_w(p + 1, w) << sh)) >> sh);
         return 1 + w;
     }
     case 0xca: {
         if (5 > avail) return 0;
-        u32 b = (u32)ld_be(p + 1, 4);
+        u32 b = (u32)ld_be<4>(p + 1);
         v.cls = V_FLOAT; v.bits = (u64)__double_as_longlong((double)__uint_as_float(b));
         return 5;
     }
     case 0xcb: {
         if (9 > avail) return 0;
-        v.cls = V_FLOAT; v.bits = ld_be(p + 1, 8);
+        v.cls = V_FLOAT; v.bits = ld_be<8>(p + 1);
         return 9;
     }
     case 0xd9: case 0xda: case 0xdb: case 0xc4: case 0xc5: case 0xc6: {
         int w = (t == 0xd9 || t == 0xc4) ? 1 : (t == 0xda || t == 0xc5) ? 2 : 4;
-        if ((u64)(1 + w) > avail) return 0;
-        u32 n = (u32)ld_be(p + 1, w);
+        if ((u32)(1 + w) > avail) return 0;
+        u64 n = ld_be_w(p + 1, w);
         if ((u64)1 + w + n > avail) return 0;
-        v.cls = t >= 0xd9 ? V_STR : V_BYTES; v.p = p + 1 + w; v.len = n;
-        return 1 + w + n;
+        v.cls = t >= 0xd9 ? V_STR : V_BYTES; v.p = p + 1 + w; v.len = (u32)n;
+        return 1 + w + (u32)n;
     }
     case 0xd4: case 0xd5: case 0xd6: case 0xd7: case 0xd8: case 0xc7: case 0xc8: case 0xc9: {
-        u32 n, hdr;
+        u64 n;
+        u32 hdr;
         if (t <= 0xd8 && t >= 0xd4) { n = 1u << (t - 0xd4); hdr = 2; }
         else {
             int w = 1 << (t - 0xc7);
-            if ((u64)(2 + w) > avail) return 0;
-            n = (u32)ld_be(p + 1, w); hdr = 2 + w;
+            if ((u32)(2 + w) > avail) return 0;
+            n = ld_be_w(p + 1, w); hdr = 2 + w;
         }
         if ((u64)hdr + n > avail) return 0;
-        v.ext = (i8)p[hdr - 1]; v.p = p + hdr; v.len = n;
+        v.ext = (i8)p[hdr - 1]; v.p = p + hdr; v.len = (u32)n;
         if (v.ext == 'G') {
-            if (n == 0) { v.cls = V_NIL; return hdr; }           // Geometry.of(b"") -> None
-            if (n < 2 || v.p[0] != 'G' || v.p[1] != 'P') return 0; // Geometry() raises
+            if (n == 0) { v.cls = V_NIL; return hdr; }               // Geometry.of(b"") -> None
+            if (n < 2 || v.p[0] != 'G' || v.p[1] != 'P') return 0;  // Geometry() raises
             v.cls = V_BYTES;
         } else {
             v.cls = V_EXT;
         }
-        return hdr + n;
+        return hdr + (u32)n;
     }
     default: return 0;  // arrays / maps / 0xc1: not field values Kart writes
     }
 }
 
-__device__ __forceinline__ bool int_eq_float(const DVal& i, double d) {
+__device__ __forceinline__ bool int_eq_float(u8 big, u64 bits, double d) {
     if (!(d == d)) return false;
     if (floor(d) != d) return false;
-    if (i.big) {
+    if (big) {
         // value in [2^63, 2^64)
         if (!(d >= 9223372036854775808.0 && d < 18446744073709551616.0)) return false;
-        return (u64)d == i.bits;
+        return (u64)d == bits;
     }
     if (!(d >= -9223372036854775808.0 && d < 9223372036854775808.0)) return false;
-    return (i64)d == (i64)i.bits;
+    return (i64)d == (i64)bits;
 }
 
-__device__ bool bytes_eq(const u8* a, const u8* b, u32 n) {
+template <class P>
+__device__ bool bytes_eq(P a, P b, u32 n) {
     for (u32 k = 0; k < n; k++)
         if (a[k] != b[k]) return false;
     return true;
 }
 
-__device__ bool py_eq(const DVal& a, const DVal& b) {
+// LDS: four bytes at a time from aligned words, realigned with v_alignbyte; the aligned reads
+// may run up to 4 bytes past either range (still inside the workgroup's LDS allocation, or
+// returning 0 past its end) and those bytes are masked off.
+__device__ __forceinline__ u32 lds_word(lp32 w, u32 k, u32 s) {
+    return __builtin_amdgcn_alignbyte(w[k + 1], w[k], s);
+}
+
+template <>
+__device__ bool bytes_eq<lp8>(lp8 a, lp8 b, u32 n) {
+    const u32 sa = (u32)(size_t)a & 3, sb = (u32)(size_t)b & 3;
+    const lp32 wa = (lp32)(a - sa), wb = (lp32)(b - sb);
+    const u32 nw = n >> 2;
+    u32 k = 0;
+    for (; k + 4 <= nw; k += 4) {
+        u32 x = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) x |= lds_word(wa, k + j, sa) ^ lds_word(wb, k + j, sb);
+        if (x) return false;
+    }
+    u32 x = 0;
+    for (; k < nw; k++) x |= lds_word(wa, k, sa) ^ lds_word(wb, k, sb);
+    if (n & 3) x |= (lds_word(wa, nw, sa) ^ lds_word(wb, nw, sb)) & ((1u << (8 * (n & 3))) - 1);
+    return x == 0;
+}
+
+template <class P>
+__device__ __forceinline__ bool py_eq(const DVal<P>& a, const DVal<P>& b) {
     if (a.cls == V_NIL || b.cls == V_NIL) return a.cls == b.cls;
     if (a.cls == V_INT && b.cls == V_INT) return a.big == b.big && a.bits == b.bits;
     if (a.cls == V_FLOAT && b.cls == V_FLOAT) return __longlong_as_double((i64)a.bits) == __longlong_as_double((i64)b.bits);
-    if (a.cls == V_INT && b.cls == V_FLOAT) return int_eq_float(a, __longlong_as_double((i64)b.bits));
-    if (a.cls == V_FLOAT && b.cls == V_INT) return int_eq_float(b, __longlong_as_double((i64)a.bits));
+    if (a.cls == V_INT && b.cls == V_FLOAT) return int_eq_float(a.big, a.bits, __longlong_as_double((i64)b.bits));
+    if (a.cls == V_FLOAT && b.cls == V_INT) return int_eq_float(b.big, b.bits, __longlong_as_double((i64)a.bits));
     if (a.cls != b.cls) return false;
     if (a.cls == V_EXT && a.ext != b.ext) return false;
     return a.len == b.len && bytes_eq(a.p, b.p, a.len);
 }
 
 // header: 0x92, str(40) legend hex, array header -> returns 0 ok
-__device__ int parse_header(const u8* b, u32 n, const u8** leg, u32* nvals, u32* off) {
+template <class P>
+__device__ __forceinline__ int parse_header(P b, u32 n, u32* nvals, u32* off) {
     if (n < 3 || b[0] != 0x92) return 1;
-    DVal lv;
-    u32 c = dv_decode(b + 1, b + n, lv);
+    DVal<P> lv;
+    u32 c = dv_decode(b + 1, n - 1, lv);
     if (!c || lv.cls != V_STR || lv.len != 40) return 1;
-    *leg = lv.p;
     u32 o = 1 + c;
     if (o >= n) return 1;
     u8 t = b[o];
     if (t >= 0x90 && t <= 0x9f) { *nvals = t & 15; o += 1; }
-    else if (t == 0xdc) { if (o + 3 > n) return 1; *nvals = (u32)ld_be(b + o + 1, 2); o += 3; }
-    else if (t == 0xdd) { if (o + 5 > n) return 1; *nvals = (u32)ld_be(b + o + 1, 4); o += 5; }
+    else if (t == 0xdc) { if (o + 3 > n) return 1; *nvals = (u32)ld_be<2>(b + o + 1); o += 3; }
+    else if (t == 0xdd) { if (o + 5 > n) return 1; *nvals = (u32)ld_be<4>(b + o + 1); o += 5; }
     else return 1;
     *off = o;
     return 0;
@@ -157,36 +206,136 @@ __device__ int parse_header(const u8* b, u32 n, const u8** leg, u32* nvals, u32*
 // device-side tables (built by the host per call)
 struct FdTab {
     int n_keys, words, n_lo, n_ln, maxv;
-    const u8* leg_o;        // [n_lo*40]
-    const u8* leg_n;        // [n_ln*40]
+    const u32* leg_o;       // [n_lo*10]: 40-byte legend hex strings as words
+    const u32* leg_n;       // [n_ln*10]
     const i16* map_o;       // [n_lo*n_keys]
     const i16* map_n;       // [n_ln*n_keys]
     const u64* cmp;         // [words]
     const u8* aligned;      // [n_lo*n_ln]: maps identical on every compared key
     const i16* key_of_val;  // [n_lo*maxv]: union key of value v of legend lo (-1 none / not compared)
-    const u32* nv_o;        // [n_lo] value count of each old legend (number of non-pk columns)
 };
 
-__device__ __forceinline__ int find_legend(const u8* tab, int n, const u8* hex) {
+// the 40 hex bytes at p (after the 3 header bytes 0x92 0xd9 0x28) as 10 little-endian words
+template <class P>
+__device__ __forceinline__ void hex_words(P p, u32 w[10]) {
+#pragma unroll
+    for (int i = 0; i < 10; i++)
+        w[i] = (u32)p[4 * i] | (u32)p[4 * i + 1] << 8 | (u32)p[4 * i + 2] << 16 | (u32)p[4 * i + 3] << 24;
+}
+template <>
+__device__ __forceinline__ void hex_words<lp8>(lp8 p, u32 w[10]) {
+    const u32 s = (u32)(size_t)p & 3;
+    const lp32 a = (lp32)(p - s);
+#pragma unroll
+    for (int i = 0; i < 10; i++) w[i] = lds_word(a, i, s);
+}
+
+template <class P>
+__device__ __forceinline__ int find_legend(const u32* __restrict__ tab, int n, P hex) {
+    u32 h[10];
+    hex_words(hex, h);
     for (int l = 0; l < n; l++) {
-        const u8* t = tab + 40 * l;
-        bool eq = true;
-        for (int k = 0; k < 40 && eq; k++) eq = t[k] == hex[k];
-        if (eq) return l;
+        u32 x = 0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) x |= tab[10 * l + i] ^ h[i];
+        if (x == 0) return l;
     }
     return -1;
 }
 
-constexpr int FD_MAXV = 128;
-constexpr int FD_NT = 64;  // one wave per block: each lane owns one update and two LDS slots
+constexpr u32 FD_MAXV = 4096;  // oracle limit (status 3 above it)
+constexpr int FD_NT = 64;      // one wave per block: each lane owns one update and two LDS slots
+
+__device__ __forceinline__ void set_bit(u64 mk[4], u64* m, int k) {
+    const u64 bit = 1ull << (k & 63);
+    const int w = k >> 6;  // selects, not a dynamic index: mk stays in registers
+    mk[0] |= w == 0 ? bit : 0;
+    mk[1] |= w == 1 ? bit : 0;
+    mk[2] |= w == 2 ? bit : 0;
+    mk[3] |= w == 3 ? bit : 0;
+    if (w >= 4) m[w] |= bit;
+}
+
+// Value `want` of a blob, walking forward from a cursor (idx, pos); a backward request restarts
+// at the first value.  Maps are near-monotone, so a key loop costs about one walk per blob.
+template <class P>
+__device__ __forceinline__ bool seek_value(P b, u32 n, u32 first, u32 want, u32& idx, u32& pos, DVal<P>& out) {
+    if (want < idx) { idx = 0; pos = first; }
+    for (;;) {
+        u32 c = dv_decode(b + pos, n - pos, out);
+        if (!c) return false;
+        if (idx == want) return true;
+        pos += c;
+        idx++;
+    }
+}
+
+// one update: returns the status; mask bits (k < 256) in mk, the rest straight into m
+template <class P>
+__device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const FdTab& tb, u64 mk[4], u64* m) {
+    u32 cvo, cvn, po, pn;
+    if (parse_header(ob, on, &cvo, &po) || parse_header(nb, nn, &cvn, &pn)) return 1;
+    const int li_o = find_legend(tb.leg_o, tb.n_lo, ob + 3);
+    const int li_n = find_legend(tb.leg_n, tb.n_ln, nb + 3);
+    if (li_o < 0 || li_n < 0) return 2;
+    if (cvo > FD_MAXV || cvn > FD_MAXV) return 3;
+    if (tb.aligned[li_o * tb.n_ln + li_n] && cvo == cvn) {
+        // ---- lockstep: value v of both blobs belongs to the same union key ----
+        const i16* kov = tb.key_of_val + (u64)li_o * tb.maxv;
+        u32 pa = po, pb = pn;
+        for (u32 v = 0; v < cvo; v++) {
+            DVal<P> a, b;
+            const u32 ca = dv_decode(ob + pa, on - pa, a), cb = dv_decode(nb + pb, nn - pb, b);
+            if (!ca || !cb) return 4;
+            pa += ca;
+            pb += cb;
+            const int k = v < (u32)tb.maxv ? kov[v] : -1;
+            if (k >= 0 && !py_eq(a, b)) set_bit(mk, m, k);
+        }
+        if (pa != on || pb != nn) return 4;  // trailing bytes: unpackb raises ExtraData
+        return 0;
+    }
+    // ---- general: validate both blobs (msgpack.unpackb decodes everything first), then
+    //      resolve each union key through both maps ----
+    u32 p = po;
+    for (u32 v = 0; v < cvo; v++) { DVal<P> x; u32 c = dv_decode(ob + p, on - p, x); if (!c) return 4; p += c; }
+    if (p != on) return 4;
+    p = pn;
+    for (u32 v = 0; v < cvn; v++) { DVal<P> x; u32 c = dv_decode(nb + p, nn - p, x); if (!c) return 4; p += c; }
+    if (p != nn) return 4;
+    const i16* mo = tb.map_o + (u64)li_o * tb.n_keys;
+    const i16* mn = tb.map_n + (u64)li_n * tb.n_keys;
+    u32 io = 0, ipo = po, in = 0, ipn = pn;
+    for (int k = 0; k < tb.n_keys; k++) {
+        if (!((tb.cmp[k >> 6] >> (k & 63)) & 1)) continue;
+        const int so = mo[k], sn = mn[k];
+        bool changed;
+        if (so == -1 || sn == -1) changed = !(so == -1 && sn == -1);
+        else if (so == -3 || sn == -3) {
+            if (so == -3 && sn == -3) changed = false;
+            else return 4;
+        } else {
+            DVal<P> a, b;
+            if (so == -2) a.cls = V_NIL;
+            else if ((u32)so >= cvo) return 1;
+            else seek_value(ob, on, po, (u32)so, io, ipo, a);
+            if (sn == -2) b.cls = V_NIL;
+            else if ((u32)sn >= cvn) return 1;
+            else seek_value(nb, nn, pn, (u32)sn, in, ipn, b);
+            changed = !py_eq(a, b);
+        }
+        if (changed) set_bit(mk, m, k);
+    }
+    return 0;
+}
 
 // Stage [p, p+len) into an LDS slot with 16-B loads from the 16-B aligned-down address, all issued
 // before any use (one HBM latency instead of one per byte).  Returns the LDS pointer of byte p, or
 // nullptr when the blob does not fit (the lane then parses straight from global memory).
+// Slots are 8-byte granular and a lane's two slots are (2*SLOT + 8) bytes apart: an odd multiple
+// of 8 bytes, so same-offset byte reads of the 64 lanes spread over 32 banks instead of 4.
 template <int SLOT>
-__device__ __forceinline__ const u8* stage_blob(const u8* __restrict__ data, u64 start, u32 len, u64 arena_end,
-                                                u32x4* slot) {
-    (void)arena_end;
+__device__ __forceinline__ lp8 stage_blob(const u8* __restrict__ data, u64 start, u32 len, u64* slot) {
     // 16-byte chunks of the aligned-down *absolute* address: an aligned chunk that holds a valid
     // byte lies in one mapped page, so reading the whole chunk cannot fault.
     const u64 a0 = (u64)data + start;
@@ -207,101 +356,79 @@ __device__ __forceinline__ const u8* stage_blob(const u8* __restrict__ data, u64
         }
 #pragma unroll
         for (int k = 0; k < B; k++)
-            if (c0 + k < (int)nch) slot[c0 + k] = v[k];
+            if (c0 + k < (int)nch) {
+                slot[2 * (c0 + k)] = (u64)v[k].x | (u64)v[k].y << 32;
+                slot[2 * (c0 + k) + 1] = (u64)v[k].z | (u64)v[k].w << 32;
+            }
     }
-    return (const u8*)slot + delta;
+    return (lp8)((const u8*)slot + delta);
 }
 
+#ifndef KD_FD_EXPERIMENT
+#define KD_FD_EXPERIMENT 0  // profiling builds only: 1 = offsets only, 2 = + staging (no parse)
+#endif
+
 template <int SLOT>
-__global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff, u64 on_blobs,
-                                                     const u8* __restrict__ nd, const u64* __restrict__ noff, u64 nn_blobs,
+__global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
+                                                     const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
                                                      const u64* __restrict__ n_upd_dev, FdTab tb,
                                                      u64* __restrict__ masks, u8* __restrict__ status) {
-    __shared__ u32x4 s_slots[SLOT > 0 ? FD_NT * 2 * (SLOT / 16) : 1];
+    constexpr int LS = SLOT > 0 ? 2 * SLOT / 8 + 1 : 1;  // u64 words per lane (odd)
+    __shared__ u64 s_slots[FD_NT * LS];
+    // device count: n_upd_host is the capacity of pairs, so pairs[u] (u < capacity) is loaded
+    // before the count arrives; capacity 0 = unknown -> wait for the count first
+    const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
-    const u64 o_end = ooff[on_blobs], n_end = noff[nn_blobs];
+    const u64 lim = spec ? n_upd_host : n_upd;
     const int lane = threadIdx.x;
-    for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < n_upd; u0 += (u64)gridDim.x * FD_NT) {
+    for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < lim; u0 += (u64)gridDim.x * FD_NT) {
         const u64 u = u0 + lane;
+        uint2 pr = make_uint2((u32)u, (u32)u);
+        if (pairs && u < lim) pr = pairs[u];
+        if (u0 >= n_upd) break;
         if (u >= n_upd) break;
-        u64 oi = pairs ? pairs[u].x : u, ni = pairs ? pairs[u].y : u;
+#if KD_FD_EXPERIMENT == 3  // no offset loads: fake blob positions from the pair indices
+        const u64 os = (u64)pr.x * 96, ns = (u64)pr.y * 96;
+        const u32 on = 90, nn = 90;
+#elif KD_FD_EXPERIMENT == 4  // offsets of blob u (sequential), no pairs use
+        const u64 oi = u, ni = u + (pr.x & 0);
         const u64 os = ooff[oi], ns = noff[ni];
         const u32 on = (u32)(ooff[oi + 1] - os);
         const u32 nn = (u32)(noff[ni + 1] - ns);
-        const u8* ob = nullptr;
-        const u8* nb = nullptr;
-        if constexpr (SLOT > 0) {
-            u32x4* my = s_slots + (size_t)lane * 2 * (SLOT / 16);
-            ob = stage_blob<SLOT>(od, os, on, o_end, my);
-            nb = stage_blob<SLOT>(nd, ns, nn, n_end, my + SLOT / 16);
-        }
-        if (!ob) ob = od + os;
-        if (!nb) nb = nd + ns;
+#else
+        const u64 oi = pr.x, ni = pr.y;
+        const u64 os = ooff[oi], ns = noff[ni];
+        const u32 on = (u32)(ooff[oi + 1] - os);
+        const u32 nn = (u32)(noff[ni + 1] - ns);
+#endif
         u64* m = masks + u * tb.words;
         u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
-        u8 st = 0;
-        const u8 *lo, *ln;
-        u32 cvo, cvn, po, pn;
-        int li_o = -1, li_n = -1;
-        if (parse_header(ob, on, &lo, &cvo, &po) || parse_header(nb, nn, &ln, &cvn, &pn)) st = 1;
-        else {
-            li_o = find_legend(tb.leg_o, tb.n_lo, lo);
-            li_n = find_legend(tb.leg_n, tb.n_ln, ln);
-            if (li_o < 0 || li_n < 0) st = 2;
+        u8 st;
+        lp8 ol = nullptr, nl = nullptr;
+#if KD_FD_EXPERIMENT == 1 || KD_FD_EXPERIMENT == 3 || KD_FD_EXPERIMENT == 4
+        mk[0] = on ^ nn ^ os ^ ns;
+        (void)ol; (void)nl;
+        st = 0;
+        if (false) {}
+#elif KD_FD_EXPERIMENT == 2
+        if constexpr (SLOT > 0) {
+            u64* my = s_slots + (size_t)lane * LS;
+            ol = stage_blob<SLOT>(od, os, on, my);
+            nl = stage_blob<SLOT>(nd, ns, nn, my + SLOT / 8);
         }
-        if (!st && tb.aligned[li_o * tb.n_ln + li_n] && cvo == cvn) {
-            // ---- lockstep: value v of both blobs belongs to the same union key ----
-            const i16* kov = tb.key_of_val + (u64)li_o * tb.maxv;
-            u32 pa = po, pb = pn;
-            for (u32 v = 0; v < cvo; v++) {
-                DVal a, b;
-                u32 ca = dv_decode(ob + pa, ob + on, a), cb = dv_decode(nb + pb, nb + nn, b);
-                if (!ca || !cb) { st = 4; break; }
-                pa += ca; pb += cb;
-                int k = v < (u32)tb.maxv ? kov[v] : -1;
-                if (k >= 0 && !py_eq(a, b)) {
-                    if (k < 256) mk[k >> 6] |= 1ull << (k & 63);
-                    else m[k >> 6] |= 1ull << (k & 63);
-                }
-            }
-            if (!st && (pa != on || pb != nn)) st = 4;  // trailing bytes: unpackb raises ExtraData
-        } else if (!st) {
-            // ---- general: resolve each union key through both maps ----
-            if (cvo > FD_MAXV || cvn > FD_MAXV) st = 3;
-            u32 vo[FD_MAXV], vn[FD_MAXV];
-            u32 p = po;
-            for (u32 v = 0; v < cvo && !st; v++) { DVal x; u32 c = dv_decode(ob + p, ob + on, x); if (!c) st = 4; vo[v] = p; p += c; }
-            if (!st && p != on) st = 4;
-            p = pn;
-            for (u32 v = 0; v < cvn && !st; v++) { DVal x; u32 c = dv_decode(nb + p, nb + nn, x); if (!c) st = 4; vn[v] = p; p += c; }
-            if (!st && p != nn) st = 4;
-            const i16* mo = tb.map_o + (u64)(li_o < 0 ? 0 : li_o) * tb.n_keys;
-            const i16* mn = tb.map_n + (u64)(li_n < 0 ? 0 : li_n) * tb.n_keys;
-            for (int k = 0; k < tb.n_keys && !st; k++) {
-                if (!((tb.cmp[k >> 6] >> (k & 63)) & 1)) continue;
-                const int so = mo[k], sn = mn[k];
-                bool changed;
-                if (so == -1 || sn == -1) changed = !(so == -1 && sn == -1);
-                else if (so == -3 || sn == -3) {
-                    if (so == -3 && sn == -3) changed = false;
-                    else { st = 4; break; }
-                } else {
-                    DVal a, b;
-                    if (so == -2) a.cls = V_NIL;
-                    else if ((u32)so >= cvo) { st = 1; break; }
-                    else dv_decode(ob + vo[so], ob + on, a);
-                    if (sn == -2) b.cls = V_NIL;
-                    else if ((u32)sn >= cvn) { st = 1; break; }
-                    else dv_decode(nb + vn[sn], nb + nn, b);
-                    changed = !py_eq(a, b);
-                }
-                if (changed) {
-                    if (k < 256) mk[k >> 6] |= 1ull << (k & 63);
-                    else m[k >> 6] |= 1ull << (k & 63);
-                }
-            }
+        mk[0] = (ol ? ol[on - 1] : 0) ^ (nl ? nl[nn - 1] : 0);
+        st = 0;
+        if (false) {}
+#else
+        if constexpr (SLOT > 0) {
+            u64* my = s_slots + (size_t)lane * LS;
+            ol = stage_blob<SLOT>(od, os, on, my);
+            nl = stage_blob<SLOT>(nd, ns, nn, my + SLOT / 8);
         }
+        if (ol && nl) st = diff_one(ol, on, nl, nn, tb, mk, m);
+#endif
+        else st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
         if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
         for (int w = 0; w < tb.words; w++) {
             if (w < 4) m[w] = mk[w];
@@ -380,10 +507,10 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     FdTab tb;
     tb.n_keys = nk; tb.words = W; tb.n_lo = nlo; tb.n_ln = nln; tb.maxv = maxv;
     const u8* base = (const u8*)dt;
-    tb.leg_o = base + o_lo; tb.leg_n = base + o_ln;
+    tb.leg_o = (const u32*)(base + o_lo); tb.leg_n = (const u32*)(base + o_ln);
     tb.map_o = (const i16*)(base + o_mo); tb.map_n = (const i16*)(base + o_mn);
     tb.cmp = (const u64*)(base + o_cmp); tb.aligned = base + o_al;
-    tb.key_of_val = (const i16*)(base + o_kov); tb.nv_o = (const u32*)(base + o_nv);
+    tb.key_of_val = (const i16*)(base + o_kov);
 
     // ---- inputs ----
     const void *d_od, *d_ooff, *d_nd, *d_noff, *d_pu = nullptr;
@@ -394,14 +521,15 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     if ((rc = stage_in(ctx, "fd.od", ob->data, ob_bytes ? ob_bytes : 1, ob->mem, &d_od))) return rc;
     if ((rc = stage_in(ctx, "fd.noff", nb->off, (nb->n + 1) * 8, nb->mem, &d_noff))) return rc;
     if ((rc = stage_in(ctx, "fd.nd", nb->data, nb_bytes ? nb_bytes : 1, nb->mem, &d_nd))) return rc;
-    if (pu && n_upd) {
+    if (d_n_upd) {
+        KD_CHECK(pu == nullptr || pairs_mem == KD_MEM_DEVICE, "kd_fielddiff: device count needs device pairs");
+        d_pu = pu;  // device pairs with a device count; n_upd is then the capacity (0 = unknown)
+    } else if (pu && n_upd) {
         if ((rc = stage_in(ctx, "fd.pu", pu, n_upd * 8, pairs_mem, &d_pu))) return rc;
-    } else if (pu) {
-        d_pu = pu;  // device pairs with a device count
     }
     u64 *d_masks = masks;
     u8* d_status = status;
-    if (out_mem == KD_MEM_HOST && n_upd) {
+    if (out_mem == KD_MEM_HOST && n_upd && !d_n_upd) {
         void *a, *b;
         if ((rc = ensure(ctx, "fd.masks", n_upd * W * 8, &a))) return rc;
         if ((rc = ensure(ctx, "fd.status", n_upd, &b))) return rc;
@@ -409,9 +537,8 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
         d_status = (u8*)b;
     }
     if (n_upd == 0 && d_n_upd == nullptr) return KD_OK;
-    u64 work = d_n_upd ? (u64)1 << 22 : n_upd;  // device count: size the grid for the capacity
-    unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, 256ull * 32);
-    if (blocks == 0) blocks = 1;
+    // grid-stride: at most one resident wave per LDS-slot set (8 single-wave blocks per CU)
+    u64 work = d_n_upd ? (n_upd ? n_upd : (u64)1 << 22) : n_upd;
     // LDS slot per blob, from the largest typical blob (kd_blobs.size_hint; host arenas: measured).
     // Blobs that do not fit a slot are parsed from global memory by their lane.
     auto max_len = [](const kd_blobs* b) -> u64 {
@@ -423,10 +550,14 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     };
     const u64 need = std::max(max_len(ob), max_len(nb)) + 15;
     const int slot = need <= 160 ? 160 : need <= 256 ? 256 : need <= 512 ? 512 : 0;
+    // one resident round: single-wave blocks per CU allowed by the 160 KB LDS (8 without slots)
+    const u64 per_cu = slot ? std::min<u64>(8, (160 * 1024) / (u64)(FD_NT * (2 * slot + 8))) : 8;
+    unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, (u64)ctx->n_cu * per_cu);
+    if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
         auto args = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
-                               ob->n, (const u8*)d_nd, (const u64*)d_noff, nb->n, (const uint2*)d_pu, n_upd, d_n_upd,
+                               (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
                                tb, d_masks, d_status);
         };
         if (slot == 160) args(k_fielddiff<160>);

@@ -72,9 +72,7 @@ struct kd_ctx {
     // last uploaded kd_fielddiff table (host copy kept alive for the async upload, and reused
     // when the next call's tables are identical)
     std::vector<uint8_t> fd_tab;
-    // classify2 decoupled look-back bookkeeping (kd_classify2.hip)
-    uint64_t c2_tile_base = 0;
-    uint32_t c2_epoch = 0;
+    int n_cu = 256;  // compute units (grid sizing of grid-stride kernels)
 };
 
 namespace kd {

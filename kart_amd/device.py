@@ -78,6 +78,7 @@ class DiffPipeline:
         self.NB = DevBlobs(*target_blobs, device)
         self.maps = maps
         cap = base.n + target.n + 1
+        self.cap_upd = min(base.n, target.n)  # updates <= matched keys
         self.delta = torch.empty(2 * cap, dtype=torch.int32, device=device)
         self.upd = torch.empty(2 * cap, dtype=torch.int32, device=device)
         self.counts = torch.zeros(8, dtype=torch.int64, device=device)  # [0..3] counts, [4] err
@@ -93,7 +94,7 @@ class DiffPipeline:
         err_ptr = self.counts.data_ptr() + 4 * 8
         N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.data_ptr(),
                                   self.upd.data_ptr(), self.counts.data_ptr(), err_ptr), "kd_diff2_device")
-        N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.data_ptr(), 0,
+        N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.data_ptr(), self.cap_upd,
                                ctypes.cast(self.counts.data_ptr() + 8, N.c_u64p), N.KD_MEM_DEVICE,
                                ctypes.byref(self._km), self.masks.data_ptr(), self.status.data_ptr(),
                                N.KD_MEM_DEVICE), "kd_fielddiff")

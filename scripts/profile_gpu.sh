@@ -18,5 +18,7 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format c
     python3 $R/bench.py $ARGS > $OUT/fetch_bench.json 2> $OUT/fetch_bench.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d $OUT/write -o run -- \
     python3 $R/bench.py $ARGS > $OUT/write_bench.json 2> $OUT/write_bench.err
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -T --output-format csv -d $OUT/sq -o run -- \
+    python3 $R/bench.py $ARGS > $OUT/sq_bench.json 2> $OUT/sq_bench.err
 echo "profile done"
-find $OUT -name "*.csv" | head -20
+cd $R && python3 scripts/pmc_summary.py $OUT --write-traffic $OUT/traffic_c2.json
