@@ -125,7 +125,7 @@ void kd_free(void* p); /* frees kd_diff_result / kd_merge_result and their array
 int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags,
              kd_diff_result** out);
 /* flags for kd_diff2 / kd_diff2_device */
-#define KD_DIFF_UNORDERED 0x1u /* device form only: deltas/updates grouped per 2048-pair tile, tiles in
+#define KD_DIFF_UNORDERED 0x1u /* device form only: deltas/updates grouped per 1024-pair tile, tiles in
                                   completion order (each tile key-ordered) — skips the ordering
                                   scan + scatter; the delta SET is identical                      */
 
@@ -182,6 +182,9 @@ int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks);
 
 /* -------- profiling (hipEvents around every launch on the context stream) -------- */
 int kd_prof_enable(kd_ctx* ctx, int on);
+/* Time only the named kernels ("k_join2,k_fielddiff"; NULL or "" = every kernel): each timed
+ * launch adds two events to the stream, so a bench times just the kernels it reports. */
+int kd_prof_select(kd_ctx* ctx, const char* names);
 /* name = kernel name; returns launches and summed milliseconds since the last reset. */
 int kd_prof_get(kd_ctx* ctx, const char* name, uint64_t* launches, double* total_ms);
 int kd_prof_reset(kd_ctx* ctx);

@@ -152,6 +152,7 @@ SIGNATURES = {
     ),
     "kd_int_keys_to_pks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "kd_prof_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "kd_prof_select": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "kd_prof_get": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_char_p, c_u64p, c_dblp],

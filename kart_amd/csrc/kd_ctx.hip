@@ -251,6 +251,12 @@ int kd_prof_enable(kd_ctx* ctx, int on) {
     return KD_OK;
 }
 
+int kd_prof_select(kd_ctx* ctx, const char* names) {
+    KD_CHECK(ctx, "kd_prof_select: ctx is NULL");
+    ctx->prof_only = names && *names ? "," + std::string(names) + "," : std::string();
+    return KD_OK;
+}
+
 int kd_prof_get(kd_ctx* ctx, const char* name, uint64_t* launches, double* total_ms) {
     KD_CHECK(ctx && name, "kd_prof_get: bad args");
     int rc = prof_flush(ctx);

@@ -129,6 +129,81 @@ __device__ __forceinline__ u32 dv_decode(P p, u32 avail, DVal<P>& v) {
     }
 }
 
+// ---- LDS-staged blobs: branch-free header decode -------------------------------------------------
+// Every msgpack type byte maps to one table entry (built at compile time, copied to LDS per block):
+//   bits 0-2 class (7 = not a field value), 3-5 header bytes, 6-10 fixed payload bytes (numbers: their
+//   width), 11-13 width of a big-endian length field, 14-17 number width (0 = immediate), 18 signed,
+//   19 float32, 24-31 immediate value.
+// A value is then decoded from one 12-byte window read (two ds_read2_b32 + v_alignbyte) with selects
+// and shifts instead of a divergent switch: lanes holding different types (fixint vs uint16, fixstr vs
+// str8) stay converged.
+struct MpTab {
+    u32 e[256];
+    static constexpr u32 mk(u32 cls, u32 hdr, u32 plen, u32 lenw, u32 numw, u32 sgn, u32 f32, u32 imm) {
+        return cls | hdr << 3 | plen << 6 | lenw << 11 | numw << 14 | sgn << 18 | f32 << 19 | imm << 24;
+    }
+    constexpr MpTab() : e() {
+        for (u32 t = 0; t < 256; t++) {
+            u32 v = mk(7, 1, 0, 0, 0, 0, 0, 0);
+            if (t <= 0x7f) v = mk(V_INT, 1, 0, 0, 0, 0, 0, t);
+            else if (t >= 0xe0) v = mk(V_INT, 1, 0, 0, 0, 1, 0, t);
+            else if (t >= 0xa0 && t <= 0xbf) v = mk(V_STR, 1, t & 31, 0, 0, 0, 0, 0);
+            else if (t == 0xc0) v = mk(V_NIL, 1, 0, 0, 0, 0, 0, 0);
+            else if (t == 0xc2 || t == 0xc3) v = mk(V_INT, 1, 0, 0, 0, 0, 0, t & 1);
+            else if (t >= 0xc4 && t <= 0xc6) { u32 w = 1u << (t - 0xc4); v = mk(V_BYTES, 1 + w, 0, w, 0, 0, 0, 0); }
+            else if (t >= 0xc7 && t <= 0xc9) { u32 w = 1u << (t - 0xc7); v = mk(V_EXT, 2 + w, 0, w, 0, 0, 0, 0); }
+            else if (t == 0xca) v = mk(V_FLOAT, 1, 4, 0, 4, 0, 1, 0);
+            else if (t == 0xcb) v = mk(V_FLOAT, 1, 8, 0, 8, 0, 0, 0);
+            else if (t >= 0xcc && t <= 0xcf) { u32 w = 1u << (t - 0xcc); v = mk(V_INT, 1, w, 0, w, 0, 0, 0); }
+            else if (t >= 0xd0 && t <= 0xd3) { u32 w = 1u << (t - 0xd0); v = mk(V_INT, 1, w, 0, w, 1, 0, 0); }
+            else if (t >= 0xd4 && t <= 0xd8) v = mk(V_EXT, 2, 1u << (t - 0xd4), 0, 0, 0, 0, 0);
+            else if (t >= 0xd9 && t <= 0xdb) { u32 w = 1u << (t - 0xd9); v = mk(V_STR, 1 + w, 0, w, 0, 0, 0, 0); }
+            e[t] = v;
+        }
+    }
+};
+__shared__ u32 s_mp[256];
+
+__device__ __forceinline__ void mp_tab_to_lds() {
+    constexpr MpTab T{};
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_mp[i] = T.e[i];
+}
+
+template <>
+__device__ __forceinline__ u32 dv_decode<lp8>(lp8 p, u32 avail, DVal<lp8>& v) {
+    const u32 s = (u32)(size_t)p & 3;
+    const lp32 a = (lp32)(p - s);
+    const u32 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+    const u32 x0 = __builtin_amdgcn_alignbyte(a1, a0, s), x1 = __builtin_amdgcn_alignbyte(a2, a1, s),
+              x2 = __builtin_amdgcn_alignbyte(a3, a2, s);
+    const u64 lo = (u64)x0 | (u64)x1 << 32;
+    const u32 t = x0 & 0xff;
+    const u32 e = s_mp[t];
+    u32 cls = e & 7;
+    const u32 hdr = (e >> 3) & 7, plen = (e >> 6) & 31, lenw = (e >> 11) & 7, numw = (e >> 14) & 15;
+    const u64 be = __builtin_bswap64((lo >> 8) | (u64)x2 << 56);  // bytes 1..8, big-endian
+    const u64 lenv = lenw ? be >> (64 - 8 * lenw) : plen;
+    u64 nv = numw ? be >> (64 - 8 * numw) : (u64)(e >> 24);
+    const u32 sh = 64 - 8 * (numw ? numw : 1);
+    if ((e >> 18) & 1) nv = (u64)((i64)(nv << sh) >> sh);
+    if ((e >> 19) & 1) nv = (u64)__double_as_longlong((double)__uint_as_float((u32)nv));
+    v.bits = nv;
+    v.big = (cls == V_INT && !((e >> 18) & 1) && numw == 8 && (nv >> 63)) ? 1 : 0;
+    const u32 et = (u32)(lo >> (8 * (hdr - 1))) & 0xff;  // ext type byte (hdr <= 6)
+    v.ext = (i8)et;
+    const u64 used = hdr + lenv;
+    bool ok = cls != 7 && used <= avail;
+    if (cls == V_EXT && et == 'G') {  // Geometry: b"" -> None; else must start "GP" (Geometry())
+        const u32 g0 = (u32)(lo >> (8 * hdr)) & 0xff, g1 = (u32)(lo >> (8 * hdr + 8)) & 0xff;
+        ok = ok && (lenv == 0 || (lenv >= 2 && g0 == 'G' && g1 == 'P'));
+        cls = lenv == 0 ? V_NIL : V_BYTES;
+    }
+    v.cls = (u8)cls;
+    v.p = p + hdr;
+    v.len = (u32)lenv;
+    return ok ? (u32)used : 0;
+}
+
 __device__ __forceinline__ bool int_eq_float(u8 big, u64 bits, double d) {
     if (!(d == d)) return false;
     if (floor(d) != d) return false;
@@ -204,15 +279,25 @@ __device__ __forceinline__ int parse_header(P b, u32 n, u32* nvals, u32* off) {
 }
 
 // device-side tables (built by the host per call)
-struct FdTab {
+// AS = -1: generic pointers into the device copy; AS = 3: the block's LDS copy (small tables)
+template <int AS, class T>
+struct ASP { typedef const __attribute__((address_space(AS))) T* type; };
+template <class T>
+struct ASP<-1, T> { typedef const T* type; };
+template <int AS>
+struct FdTabT {
     int n_keys, words, n_lo, n_ln, maxv;
-    const u32* leg_o;       // [n_lo*10]: 40-byte legend hex strings as words
-    const u32* leg_n;       // [n_ln*10]
-    const i16* map_o;       // [n_lo*n_keys]
-    const i16* map_n;       // [n_ln*n_keys]
-    const u64* cmp;         // [words]
-    const u8* aligned;      // [n_lo*n_ln]: maps identical on every compared key
-    const i16* key_of_val;  // [n_lo*maxv]: union key of value v of legend lo (-1 none / not compared)
+    typename ASP<AS, u32>::type leg_o;       // [n_lo*10]: 40-byte legend hex strings as words
+    typename ASP<AS, u32>::type leg_n;       // [n_ln*10]
+    typename ASP<AS, i16>::type map_o;       // [n_lo*n_keys]
+    typename ASP<AS, i16>::type map_n;       // [n_ln*n_keys]
+    typename ASP<AS, u64>::type cmp;         // [words]
+    typename ASP<AS, u8>::type aligned;      // [n_lo*n_ln]: maps identical on every compared key
+    typename ASP<AS, i16>::type key_of_val;  // [n_lo*maxv]: union key of value v of legend lo (-1 none)
+};
+typedef FdTabT<-1> FdTab;
+struct FdTabOff {  // byte offsets of the tables inside the packed upload (what an LDS copy rebases)
+    u32 leg_o, leg_n, map_o, map_n, cmp, aligned, key_of_val, bytes;
 };
 
 // the 40 hex bytes at p (after the 3 header bytes 0x92 0xd9 0x28) as 10 little-endian words
@@ -230,8 +315,8 @@ __device__ __forceinline__ void hex_words<lp8>(lp8 p, u32 w[10]) {
     for (int i = 0; i < 10; i++) w[i] = lds_word(a, i, s);
 }
 
-template <class P>
-__device__ __forceinline__ int find_legend(const u32* __restrict__ tab, int n, P hex) {
+template <class P, class TP>
+__device__ __forceinline__ int find_legend(TP tab, int n, P hex) {
     u32 h[10];
     hex_words(hex, h);
     for (int l = 0; l < n; l++) {
@@ -271,17 +356,18 @@ __device__ __forceinline__ bool seek_value(P b, u32 n, u32 first, u32 want, u32&
 }
 
 // one update: returns the status; mask bits (k < 256) in mk, the rest straight into m
-template <class P>
-__device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const FdTab& tb, u64 mk[4], u64* m) {
+template <class P, class TB>
+__device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const TB& tb, u64 mk[4], u64* m) {
     u32 cvo, cvn, po, pn;
     if (parse_header(ob, on, &cvo, &po) || parse_header(nb, nn, &cvn, &pn)) return 1;
     const int li_o = find_legend(tb.leg_o, tb.n_lo, ob + 3);
     const int li_n = find_legend(tb.leg_n, tb.n_ln, nb + 3);
     if (li_o < 0 || li_n < 0) return 2;
     if (cvo > FD_MAXV || cvn > FD_MAXV) return 3;
-    if (tb.aligned[li_o * tb.n_ln + li_n] && cvo == cvn) {
+    const bool al = tb.aligned[li_o * tb.n_ln + li_n];
+    if (al && cvo == cvn) {
         // ---- lockstep: value v of both blobs belongs to the same union key ----
-        const i16* kov = tb.key_of_val + (u64)li_o * tb.maxv;
+        const auto kov = tb.key_of_val + (u64)li_o * tb.maxv;
         u32 pa = po, pb = pn;
         for (u32 v = 0; v < cvo; v++) {
             DVal<P> a, b;
@@ -303,8 +389,8 @@ __device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const FdTab& 
     p = pn;
     for (u32 v = 0; v < cvn; v++) { DVal<P> x; u32 c = dv_decode(nb + p, nn - p, x); if (!c) return 4; p += c; }
     if (p != nn) return 4;
-    const i16* mo = tb.map_o + (u64)li_o * tb.n_keys;
-    const i16* mn = tb.map_n + (u64)li_n * tb.n_keys;
+    const auto mo = tb.map_o + (u64)li_o * tb.n_keys;
+    const auto mn = tb.map_n + (u64)li_n * tb.n_keys;
     u32 io = 0, ipo = po, in = 0, ipn = pn;
     for (int k = 0; k < tb.n_keys; k++) {
         if (!((tb.cmp[k >> 6] >> (k & 63)) & 1)) continue;
@@ -329,106 +415,144 @@ __device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const FdTab& 
     return 0;
 }
 
-// Stage [p, p+len) into an LDS slot with 16-B loads from the 16-B aligned-down address, all issued
-// before any use (one HBM latency instead of one per byte).  Returns the LDS pointer of byte p, or
-// nullptr when the blob does not fit (the lane then parses straight from global memory).
-// Slots are 8-byte granular and a lane's two slots are (2*SLOT + 8) bytes apart: an odd multiple
-// of 8 bytes, so same-offset byte reads of the 64 lanes spread over 32 banks instead of 4.
-template <int SLOT>
-__device__ __forceinline__ lp8 stage_blob(const u8* __restrict__ data, u64 start, u32 len, u64* slot) {
-    // 16-byte chunks of the aligned-down *absolute* address: an aligned chunk that holds a valid
-    // byte lies in one mapped page, so reading the whole chunk cannot fault.
-    const u64 a0 = (u64)data + start;
-    const u64 base = a0 & ~(u64)15;
-    const u32 delta = (u32)(a0 - base);
-    const u32 nch = (delta + len + 15) >> 4;
-    if (nch * 16 > (u32)SLOT) return nullptr;
-    typedef const __attribute__((address_space(1))) u32x4* gp;
-    constexpr int B = 8;  // chunks in flight per batch (branch-free issue, then LDS stores)
-#pragma unroll
-    for (int c0 = 0; c0 < SLOT / 16; c0 += B) {
-        if (c0 >= (int)nch) break;
-        u32x4 v[B];
-#pragma unroll
-        for (int k = 0; k < B; k++) {
-            const int c = c0 + k < (int)nch ? c0 + k : c0;
-            v[k] = *(gp)(base + 16ull * c);
-        }
-#pragma unroll
-        for (int k = 0; k < B; k++)
-            if (c0 + k < (int)nch) {
-                slot[2 * (c0 + k)] = (u64)v[k].x | (u64)v[k].y << 32;
-                slot[2 * (c0 + k) + 1] = (u64)v[k].z | (u64)v[k].w << 32;
-            }
-    }
-    return (lp8)((const u8*)slot + delta);
-}
+constexpr u32 FD_TAB_LDS_MAX = 16384;  // tables up to this size are copied into each block's LDS
 
-#ifndef KD_FD_EXPERIMENT
-#define KD_FD_EXPERIMENT 0  // profiling builds only: 1 = offsets only, 2 = + staging (no parse)
-#endif
-
+// One wave per block, one update per lane.  Per round of 64 updates:
+//   1. pair + blob offsets (coalesced pair loads; offset loads per lane);
+//   2. cooperative staging: the 64 updates' 2x64 blobs are cut into 16-B chunks and dealt to the lanes
+//      so that one wave-instruction reads consecutive chunks of a few blobs (a handful of cache lines)
+//      instead of 64 scattered lines — per-lane staging of its own blobs made every load instruction
+//      touch 64 lines and the staging dominated the kernel;
+//   3. each lane walks its two blobs from LDS (table-driven decoder, tables in LDS).
 template <int SLOT>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
-                                                     const u64* __restrict__ n_upd_dev, FdTab tb,
-                                                     u64* __restrict__ masks, u8* __restrict__ status) {
-    constexpr int LS = SLOT > 0 ? 2 * SLOT / 8 + 1 : 1;  // u64 words per lane (odd)
+                                                     const u64* __restrict__ n_upd_dev, FdTab tg, FdTabOff to,
+                                                     const u8* __restrict__ tab_base, u64* __restrict__ masks,
+                                                     u8* __restrict__ status) {
+    static_assert(SLOT > 0 && SLOT % 16 == 0, "LDS slots");
+    constexpr int NC = SLOT / 16;          // chunks per blob slot
+    constexpr int LS = 2 * SLOT / 8 + 1;   // u64 words per lane (odd: the lanes' slots spread over banks)
+    constexpr int NR = 2 * NC;             // chunk rounds per 64 updates
+    constexpr int BATCH = NR <= 20 ? NR : 16;
     __shared__ u64 s_slots[FD_NT * LS];
+    __shared__ u64 s_ab[FD_NT], s_bb[FD_NT];
+    __shared__ u32 s_n[FD_NT];
+    extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
+    const int lane = threadIdx.x;
+    typedef const __attribute__((address_space(1))) u32x4* gp;
+    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp)(tab_base + i);
+    mp_tab_to_lds();
+    FdTabT<3> tb;
+    tb.n_keys = tg.n_keys; tb.words = tg.words; tb.n_lo = tg.n_lo; tb.n_ln = tg.n_ln; tb.maxv = tg.maxv;
+    typedef __attribute__((address_space(3))) u8* l8;
+    const l8 lt = (l8)s_tab;
+    tb.leg_o = (typename ASP<3, u32>::type)(lt + to.leg_o);
+    tb.leg_n = (typename ASP<3, u32>::type)(lt + to.leg_n);
+    tb.map_o = (typename ASP<3, i16>::type)(lt + to.map_o);
+    tb.map_n = (typename ASP<3, i16>::type)(lt + to.map_n);
+    tb.cmp = (typename ASP<3, u64>::type)(lt + to.cmp);
+    tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
+    tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
+    __syncthreads();
     // device count: n_upd_host is the capacity of pairs, so pairs[u] (u < capacity) is loaded
     // before the count arrives; capacity 0 = unknown -> wait for the count first
     const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 lim = spec ? n_upd_host : n_upd;
-    const int lane = threadIdx.x;
+    const u64 safe = (u64)od & ~(u64)15;  // a mapped chunk for masked-off lanes' loads
     for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < lim; u0 += (u64)gridDim.x * FD_NT) {
         const u64 u = u0 + lane;
         uint2 pr = make_uint2((u32)u, (u32)u);
         if (pairs && u < lim) pr = pairs[u];
-        if (u0 >= n_upd) break;
-        if (u >= n_upd) break;
-#if KD_FD_EXPERIMENT == 3  // no offset loads: fake blob positions from the pair indices
-        const u64 os = (u64)pr.x * 96, ns = (u64)pr.y * 96;
-        const u32 on = 90, nn = 90;
-#elif KD_FD_EXPERIMENT == 4  // offsets of blob u (sequential), no pairs use
-        const u64 oi = u, ni = u + (pr.x & 0);
-        const u64 os = ooff[oi], ns = noff[ni];
-        const u32 on = (u32)(ooff[oi + 1] - os);
-        const u32 nn = (u32)(noff[ni + 1] - ns);
-#else
-        const u64 oi = pr.x, ni = pr.y;
-        const u64 os = ooff[oi], ns = noff[ni];
-        const u32 on = (u32)(ooff[oi + 1] - os);
-        const u32 nn = (u32)(noff[ni + 1] - ns);
-#endif
+        if (u0 >= n_upd) break;  // wave-uniform
+        const bool act = u < n_upd;
+        u64 os = 0, ns = 0;
+        u32 on = 0, nn = 0;
+        if (act) {
+            os = ooff[pr.x];
+            ns = noff[pr.y];
+            on = (u32)(ooff[pr.x + 1] - os);
+            nn = (u32)(noff[pr.y + 1] - ns);
+        }
+        const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
+        const u64 ab = a0 & ~(u64)15, bb = b0 & ~(u64)15;
+        const u32 ad = (u32)(a0 - ab), bd = (u32)(b0 - bb);
+        const u32 na = (ad + on + 15) >> 4, nb = (bd + nn + 15) >> 4;
+        const bool fa = act && na <= (u32)NC, fb = act && nb <= (u32)NC;
+        s_ab[lane] = ab;
+        s_bb[lane] = bb;
+        s_n[lane] = (fa ? na : 0) | (fb ? nb : 0) << 16;
+        __syncthreads();
+#pragma unroll
+        for (int r0 = 0; r0 < NR; r0 += BATCH) {
+            u32x4 v[BATCH];
+            u32 dst[BATCH];
+            bool ok[BATCH];
+#pragma unroll
+            for (int k = 0; k < BATCH; k++) {
+                const u32 q = (u32)(r0 + k) * FD_NT + lane;
+                const u32 uu = q / (2 * NC), rem = q - uu * (2 * NC);
+                const bool bs = rem >= (u32)NC;
+                const u32 c = bs ? rem - NC : rem;
+                const u32 nw = s_n[uu];
+                const u32 n = bs ? nw >> 16 : nw & 0xFFFF;
+                ok[k] = r0 + k < NR && c < n;
+                const u64 base = bs ? s_bb[uu] : s_ab[uu];
+                v[k] = *(gp)(ok[k] ? base + 16ull * c : safe);
+                dst[k] = uu * LS + (bs ? SLOT / 8 : 0) + 2 * c;
+            }
+#pragma unroll
+            for (int k = 0; k < BATCH; k++)
+                if (ok[k]) {
+                    s_slots[dst[k]] = (u64)v[k].x | (u64)v[k].y << 32;
+                    s_slots[dst[k] + 1] = (u64)v[k].z | (u64)v[k].w << 32;
+                }
+        }
+        __syncthreads();
+        if (act) {
+            u64* m = masks + u * tb.words;
+            u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
+            u64* my = s_slots + (size_t)lane * LS;
+            u8 st;
+            if (fa && fb) st = diff_one((lp8)((const u8*)my + ad), on, (lp8)((const u8*)(my + SLOT / 8) + bd), nn, tb, mk, m);
+            else st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
+            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+            for (int w = 0; w < tb.words; w++) {
+                if (w < 4) m[w] = mk[w];
+                else if (st) m[w] = 0;
+            }
+            status[u] = st;
+        }
+        __syncthreads();  // slots and descriptors are rewritten by the next round
+    }
+}
+
+// Fallback for blobs larger than the biggest slot or tables too large for LDS: one lane per update,
+// blobs parsed straight from global memory.
+__global__ __launch_bounds__(FD_NT) void k_fielddiff_g(const u8* __restrict__ od, const u64* __restrict__ ooff,
+                                                       const u8* __restrict__ nd, const u64* __restrict__ noff,
+                                                       const uint2* __restrict__ pairs, u64 n_upd_host,
+                                                       const u64* __restrict__ n_upd_dev, FdTab tb,
+                                                       u64* __restrict__ masks, u8* __restrict__ status) {
+    const int lane = threadIdx.x;
+    mp_tab_to_lds();
+    __syncthreads();
+    const bool spec = n_upd_dev && n_upd_host;
+    const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
+    const u64 lim = spec ? n_upd_host : n_upd;
+    for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < lim; u0 += (u64)gridDim.x * FD_NT) {
+        const u64 u = u0 + lane;
+        uint2 pr = make_uint2((u32)u, (u32)u);
+        if (pairs && u < lim) pr = pairs[u];
+        if (u0 >= n_upd || u >= n_upd) break;
+        const u64 os = ooff[pr.x], ns = noff[pr.y];
+        const u32 on = (u32)(ooff[pr.x + 1] - os);
+        const u32 nn = (u32)(noff[pr.y + 1] - ns);
         u64* m = masks + u * tb.words;
-        u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
-        u8 st;
-        lp8 ol = nullptr, nl = nullptr;
-#if KD_FD_EXPERIMENT == 1 || KD_FD_EXPERIMENT == 3 || KD_FD_EXPERIMENT == 4
-        mk[0] = on ^ nn ^ os ^ ns;
-        (void)ol; (void)nl;
-        st = 0;
-        if (false) {}
-#elif KD_FD_EXPERIMENT == 2
-        if constexpr (SLOT > 0) {
-            u64* my = s_slots + (size_t)lane * LS;
-            ol = stage_blob<SLOT>(od, os, on, my);
-            nl = stage_blob<SLOT>(nd, ns, nn, my + SLOT / 8);
-        }
-        mk[0] = (ol ? ol[on - 1] : 0) ^ (nl ? nl[nn - 1] : 0);
-        st = 0;
-        if (false) {}
-#else
-        if constexpr (SLOT > 0) {
-            u64* my = s_slots + (size_t)lane * LS;
-            ol = stage_blob<SLOT>(od, os, on, my);
-            nl = stage_blob<SLOT>(nd, ns, nn, my + SLOT / 8);
-        }
-        if (ol && nl) st = diff_one(ol, on, nl, nn, tb, mk, m);
-#endif
-        else st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
+        u64 mk[4] = {0, 0, 0, 0};
+        const u8 st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
         if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
         for (int w = 0; w < tb.words; w++) {
             if (w < 4) m[w] = mk[w];
@@ -549,21 +673,29 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
         return m ? m : 256;
     };
     const u64 need = std::max(max_len(ob), max_len(nb)) + 15;
-    const int slot = need <= 160 ? 160 : need <= 256 ? 256 : need <= 512 ? 512 : 0;
+    FdTabOff to;
+    to.leg_o = (u32)o_lo; to.leg_n = (u32)o_ln; to.map_o = (u32)o_mo; to.map_n = (u32)o_mn; to.cmp = (u32)o_cmp;
+    to.aligned = (u32)o_al; to.key_of_val = (u32)o_kov; to.bytes = (u32)o_end;
+    const bool lds_tab = o_end <= FD_TAB_LDS_MAX;
+    const int slot = !lds_tab ? 0 : need <= 160 ? 160 : need <= 256 ? 256 : need <= 512 ? 512 : 0;
     // one resident round: single-wave blocks per CU allowed by the 160 KB LDS (8 without slots)
-    const u64 per_cu = slot ? std::min<u64>(8, (160 * 1024) / (u64)(FD_NT * (2 * slot + 8))) : 8;
+    const u64 lds_blk = slot ? (u64)FD_NT * (2 * slot + 8) + FD_NT * 20 + 1024 + o_end : 1024;
+    const u64 per_cu = std::min<u64>(8, (160 * 1024) / lds_blk);
     unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, (u64)ctx->n_cu * per_cu);
     if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
         auto args = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
-                               tb, d_masks, d_status);
+                               tb, to, (const u8*)dt, d_masks, d_status);
         };
         if (slot == 160) args(k_fielddiff<160>);
         else if (slot == 256) args(k_fielddiff<256>);
         else if (slot == 512) args(k_fielddiff<512>);
-        else args(k_fielddiff<0>);
+        else
+            hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
+                               (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks,
+                               d_status);
     });
     if (rc) return rc;
     if (out_mem == KD_MEM_HOST) {

@@ -66,6 +66,7 @@ struct kd_ctx {
     std::map<std::string, kd::DevBuf> bufs;
     // profiling
     bool prof = false;
+    std::string prof_only;  // ",name,name," selection (empty = every kernel)
     std::vector<hipEvent_t> ev_pool;
     std::vector<kd::PendingEv> pending;
     std::map<std::string, kd::ProfStat> stats;
@@ -90,13 +91,18 @@ void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a);
 void prof_end(kd_ctx* ctx, const char* name, hipEvent_t a);
 int prof_flush(kd_ctx* ctx);
 
+inline bool prof_on(const kd_ctx* ctx, const char* name) {
+    return ctx->prof && (ctx->prof_only.empty() || ctx->prof_only.find("," + std::string(name) + ",") != std::string::npos);
+}
+
 template <typename F>
 inline int launch(kd_ctx* ctx, const char* name, F&& f) {
     hipEvent_t a = nullptr;
-    if (ctx->prof) prof_begin(ctx, name, &a);
+    const bool prof = prof_on(ctx, name);
+    if (prof) prof_begin(ctx, name, &a);
     f();
     hipError_t e = hipGetLastError();
-    if (ctx->prof) prof_end(ctx, name, a);
+    if (prof) prof_end(ctx, name, a);
     if (e != hipSuccess) {
         set_error("launch %s: %s", name, hipGetErrorString(e));
         return KD_EHIP;
@@ -110,8 +116,14 @@ int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem
 // ---- classify2 (device form), kd_classify.hip ----
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
                  u32* d_upd, u64* d_counts, u32* d_err);
-constexpr int C2_NT = 256;
-constexpr int C2_IPT = 8;
+#ifndef KD_C2_NT
+#define KD_C2_NT 256
+#endif
+constexpr int C2_NT = KD_C2_NT;
+#ifndef KD_C2_IPT
+#define KD_C2_IPT 4
+#endif
+constexpr int C2_IPT = KD_C2_IPT;
 constexpr int C2_TILE = C2_NT * C2_IPT;
 
 }  // namespace kd

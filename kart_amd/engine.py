@@ -72,6 +72,11 @@ class Engine:
     def prof_enable(self, on=True):
         N.check(self.L.kd_prof_enable(self.ctx, 1 if on else 0), "kd_prof_enable")
 
+    def prof_select(self, names=None):
+        """time only these kernels (iterable of names; None = all)"""
+        arg = ",".join(names).encode() if names else None
+        N.check(self.L.kd_prof_select(self.ctx, arg), "kd_prof_select")
+
     def prof_reset(self):
         N.check(self.L.kd_prof_reset(self.ctx), "kd_prof_reset")
 
