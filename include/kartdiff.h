@@ -73,7 +73,7 @@ typedef struct kd_blobs {
     const uint8_t* data;
     const uint64_t* off; /* [n+1] */
     uint32_t mem;
-    uint32_t size_hint; /* typical blob size in bytes (0 = unknown); sizes the LDS staging slots */
+    uint32_t size_hint; /* typical (mean) blob size in bytes (0 = unknown); sizes the LDS staging pool */
 } kd_blobs;
 
 /* Legend -> union-key maps for kd_fielddiff (host memory).  Union keys are the old schema's

@@ -232,20 +232,26 @@ __device__ __forceinline__ u32 lds_word(lp32 w, u32 k, u32 s) {
 
 template <>
 __device__ bool bytes_eq<lp8>(lp8 a, lp8 b, u32 n) {
+    // 32-byte blocks: the 9 aligned words of each side are read together (one LDS round trip per
+    // block, no per-word early exit), realigned with v_alignbyte and compared; bytes past n masked
     const u32 sa = (u32)(size_t)a & 3, sb = (u32)(size_t)b & 3;
-    const lp32 wa = (lp32)(a - sa), wb = (lp32)(b - sb);
-    const u32 nw = n >> 2;
-    u32 k = 0;
-    for (; k + 4 <= nw; k += 4) {
-        u32 x = 0;
+    lp32 wa = (lp32)(a - sa), wb = (lp32)(b - sb);
+    u32 rem = n, diff = 0;
+    while (rem > 0 && diff == 0) {
+        u32 xa[9], xb[9];
 #pragma unroll
-        for (int j = 0; j < 4; j++) x |= lds_word(wa, k + j, sa) ^ lds_word(wb, k + j, sb);
-        if (x) return false;
+        for (int j = 0; j < 9; j++) { xa[j] = wa[j]; xb[j] = wb[j]; }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const u32 d = __builtin_amdgcn_alignbyte(xa[j + 1], xa[j], sa) ^ __builtin_amdgcn_alignbyte(xb[j + 1], xb[j], sb);
+            const u32 valid = rem >= 4u * j + 4 ? 0xFFFFFFFFu : rem > 4u * j ? (1u << (8 * (rem - 4 * j))) - 1 : 0u;
+            diff |= d & valid;
+        }
+        wa += 8;
+        wb += 8;
+        rem = rem > 32 ? rem - 32 : 0;
     }
-    u32 x = 0;
-    for (; k < nw; k++) x |= lds_word(wa, k, sa) ^ lds_word(wb, k, sb);
-    if (n & 3) x |= (lds_word(wa, nw, sa) ^ lds_word(wb, nw, sb)) & ((1u << (8 * (n & 3))) - 1);
-    return x == 0;
+    return diff == 0;
 }
 
 template <class P>
@@ -258,6 +264,34 @@ __device__ __forceinline__ bool py_eq(const DVal<P>& a, const DVal<P>& b) {
     if (a.cls != b.cls) return false;
     if (a.cls == V_EXT && a.ext != b.ext) return false;
     return a.len == b.len && bytes_eq(a.p, b.p, a.len);
+}
+
+// LDS values: Python == with the scalar cases as selects; only a same-class, same-length byte
+// payload pair reaches the (LDS) byte compare.  The branchy generic form cost most of the parse.
+__device__ __forceinline__ bool int_eq_float_sel(u8 big, u64 bits, double d) {
+    const bool whole = d == d && floor(d) == d;
+    const bool in_big = d >= 9223372036854775808.0 && d < 18446744073709551616.0;
+    const bool in_small = d >= -9223372036854775808.0 && d < 9223372036854775808.0;
+    const double dc_b = in_big ? d : 9223372036854775808.0, dc_s = in_small ? d : 0.0;
+    const bool eq_b = in_big && (u64)dc_b == bits, eq_s = in_small && (i64)dc_s == (i64)bits;
+    return whole && (big ? eq_b : eq_s);
+}
+
+template <>
+__device__ __forceinline__ bool py_eq<lp8>(const DVal<lp8>& a, const DVal<lp8>& b) {
+    const bool an = a.cls == V_NIL, bn = b.cls == V_NIL;
+    const bool ai = a.cls == V_INT, bi = b.cls == V_INT, af = a.cls == V_FLOAT, bf = b.cls == V_FLOAT;
+    const double da = __longlong_as_double((i64)a.bits), db = __longlong_as_double((i64)b.bits);
+    const bool ii = ai && bi, ff = af && bf, mixed = (ai && bf) || (af && bi);
+    const bool r_ii = a.big == b.big && a.bits == b.bits;
+    const bool r_ff = da == db;
+    const bool r_mx = int_eq_float_sel(ai ? a.big : b.big, ai ? a.bits : b.bits, ai ? db : da);
+    const bool num = (ai || af) && (bi || bf);
+    const bool r_num = ii ? r_ii : ff ? r_ff : mixed && r_mx;
+    const bool byt = !an && !bn && !(ai || af) && a.cls == b.cls && (a.cls != V_EXT || a.ext == b.ext) && a.len == b.len;
+    bool eqb = false;
+    if (byt) eqb = bytes_eq(a.p, b.p, a.len);
+    return (an || bn) ? (an && bn) : num ? r_num : eqb;
 }
 
 // header: 0x92, str(40) legend hex, array header -> returns 0 ok
@@ -311,8 +345,11 @@ template <>
 __device__ __forceinline__ void hex_words<lp8>(lp8 p, u32 w[10]) {
     const u32 s = (u32)(size_t)p & 3;
     const lp32 a = (lp32)(p - s);
+    u32 x[11];
 #pragma unroll
-    for (int i = 0; i < 10; i++) w[i] = lds_word(a, i, s);
+    for (int i = 0; i < 11; i++) x[i] = a[i];  // one LDS round trip
+#pragma unroll
+    for (int i = 0; i < 10; i++) w[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], s);
 }
 
 template <class P, class TP>
@@ -356,8 +393,19 @@ __device__ __forceinline__ bool seek_value(P b, u32 n, u32 first, u32 want, u32&
 }
 
 // one update: returns the status; mask bits (k < 256) in mk, the rest straight into m
+#ifndef KD_FD_CLOCK
+#define KD_FD_CLOCK 0  // profiling builds only: per-phase clock64 printf of sampled waves
+#endif
+#if KD_FD_CLOCK
+__device__ u64 g_fd_dbg[4 * 8192 * 64];
+#define FD_DBG(i) g_fd_dbg[4 * ((blockIdx.x % 8192) * 64 + threadIdx.x) + (i)]
+#endif
 template <class P, class TB>
 __device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const TB& tb, u64 mk[4], u64* m) {
+#if KD_FD_CLOCK
+    const u64 D0 = clock64();
+    u64 tdec = 0, teq = 0;
+#endif
     u32 cvo, cvn, po, pn;
     if (parse_header(ob, on, &cvo, &po) || parse_header(nb, nn, &cvn, &pn)) return 1;
     const int li_o = find_legend(tb.leg_o, tb.n_lo, ob + 3);
@@ -369,15 +417,35 @@ __device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const TB& tb,
         // ---- lockstep: value v of both blobs belongs to the same union key ----
         const auto kov = tb.key_of_val + (u64)li_o * tb.maxv;
         u32 pa = po, pb = pn;
+#if KD_FD_CLOCK
+        FD_DBG(0) = clock64() - D0;
+#endif
         for (u32 v = 0; v < cvo; v++) {
             DVal<P> a, b;
+#if KD_FD_CLOCK
+            u64 E0 = clock64();
+#endif
             const u32 ca = dv_decode(ob + pa, on - pa, a), cb = dv_decode(nb + pb, nn - pb, b);
             if (!ca || !cb) return 4;
             pa += ca;
             pb += cb;
             const int k = v < (u32)tb.maxv ? kov[v] : -1;
+#if KD_FD_CLOCK
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            u64 E1 = clock64();
+            tdec += E1 - E0;
+#endif
             if (k >= 0 && !py_eq(a, b)) set_bit(mk, m, k);
+#if KD_FD_CLOCK
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            teq += clock64() - E1;
+#endif
         }
+#if KD_FD_CLOCK
+        FD_DBG(1) = tdec;
+        FD_DBG(2) = teq;
+        FD_DBG(3) = cvo;
+#endif
         if (pa != on || pb != nn) return 4;  // trailing bytes: unpackb raises ExtraData
         return 0;
     }
@@ -424,23 +492,23 @@ constexpr u32 FD_TAB_LDS_MAX = 16384;  // tables up to this size are copied into
 //      instead of 64 scattered lines — per-lane staging of its own blobs made every load instruction
 //      touch 64 lines and the staging dominated the kernel;
 //   3. each lane walks its two blobs from LDS (table-driven decoder, tables in LDS).
-template <int SLOT>
+template <int POOL>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
                                                      const u64* __restrict__ n_upd_dev, FdTab tg, FdTabOff to,
                                                      const u8* __restrict__ tab_base, u64* __restrict__ masks,
                                                      u8* __restrict__ status) {
-    static_assert(SLOT > 0 && SLOT % 16 == 0, "LDS slots");
-    constexpr int NC = SLOT / 16;          // chunks per blob slot
-    constexpr int LS = 2 * SLOT / 8 + 1;   // u64 words per lane (odd: the lanes' slots spread over banks)
-    constexpr int NR = 2 * NC;             // chunk rounds per 64 updates
-    constexpr int BATCH = NR <= 20 ? NR : 16;
-    __shared__ u64 s_slots[FD_NT * LS];
+    constexpr int BATCH = 8;  // chunk loads in flight per lane
+    __shared__ u32x4 s_pool[POOL];  // the round's blobs, packed back to back in 16-B chunks
+    __shared__ u8 s_own[POOL];      // lane owning each pool chunk
     __shared__ u64 s_ab[FD_NT], s_bb[FD_NT];
-    __shared__ u32 s_n[FD_NT];
+    __shared__ u32 s_cnt[FD_NT], s_off[FD_NT];
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
     const int lane = threadIdx.x;
+#if KD_FD_CLOCK
+    const u64 WE = wall_clock64();
+#endif
     typedef const __attribute__((address_space(1))) u32x4* gp;
     for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp)(tab_base + i);
     mp_tab_to_lds();
@@ -461,9 +529,11 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 lim = spec ? n_upd_host : n_upd;
-    const u64 safe = (u64)od & ~(u64)15;  // a mapped chunk for masked-off lanes' loads
     for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < lim; u0 += (u64)gridDim.x * FD_NT) {
         const u64 u = u0 + lane;
+#if KD_FD_CLOCK
+        const u64 T0 = clock64(), W0 = wall_clock64();
+#endif
         uint2 pr = make_uint2((u32)u, (u32)u);
         if (pairs && u < lim) pr = pairs[u];
         if (u0 >= n_upd) break;  // wave-uniform
@@ -476,47 +546,62 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             on = (u32)(ooff[pr.x + 1] - os);
             nn = (u32)(noff[pr.y + 1] - ns);
         }
+        // ---- pool allocation: exclusive wave scan of the lanes' chunk counts ----
         const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
         const u64 ab = a0 & ~(u64)15, bb = b0 & ~(u64)15;
         const u32 ad = (u32)(a0 - ab), bd = (u32)(b0 - bb);
-        const u32 na = (ad + on + 15) >> 4, nb = (bd + nn + 15) >> 4;
-        const bool fa = act && na <= (u32)NC, fb = act && nb <= (u32)NC;
+        const u32 na = act ? (ad + on + 15) >> 4 : 0, nb = act ? (bd + nn + 15) >> 4 : 0;
+        const u32 need = na + nb;
+        u32 x = need;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        const u32 off = x - need;
+        const bool fit = act && x <= (u32)POOL;  // lanes past the pool parse from global memory
+        const u64 bal = __ballot(fit);
+        const u32 used = bal ? __shfl(x, 63 - __clzll((long long)bal), 64) : 0;  // end of the last fitting lane
         s_ab[lane] = ab;
         s_bb[lane] = bb;
-        s_n[lane] = (fa ? na : 0) | (fb ? nb : 0) << 16;
+        s_cnt[lane] = na;
+        s_off[lane] = off;
+        if (fit)
+            for (u32 c = 0; c < need; c++) s_own[off + c] = (u8)lane;
         __syncthreads();
-#pragma unroll
-        for (int r0 = 0; r0 < NR; r0 += BATCH) {
+#if KD_FD_CLOCK
+        const u64 T1 = clock64();
+#endif
+        // ---- cooperative staging: chunk q of the pool is loaded by lane q % 64 (consecutive lanes
+        //      read consecutive chunks of the same blob) ----
+        for (u32 q0 = 0; q0 < used; q0 += BATCH * FD_NT) {
             u32x4 v[BATCH];
-            u32 dst[BATCH];
-            bool ok[BATCH];
 #pragma unroll
             for (int k = 0; k < BATCH; k++) {
-                const u32 q = (u32)(r0 + k) * FD_NT + lane;
-                const u32 uu = q / (2 * NC), rem = q - uu * (2 * NC);
-                const bool bs = rem >= (u32)NC;
-                const u32 c = bs ? rem - NC : rem;
-                const u32 nw = s_n[uu];
-                const u32 n = bs ? nw >> 16 : nw & 0xFFFF;
-                ok[k] = r0 + k < NR && c < n;
-                const u64 base = bs ? s_bb[uu] : s_ab[uu];
-                v[k] = *(gp)(ok[k] ? base + 16ull * c : safe);
-                dst[k] = uu * LS + (bs ? SLOT / 8 : 0) + 2 * c;
+                const u32 q = q0 + k * FD_NT + lane;
+                u64 src = ab;  // own blob: a mapped chunk for masked-off lanes
+                if (q < used) {
+                    const u32 w = s_own[q];
+                    const u32 c = q - s_off[w], n0 = s_cnt[w];
+                    src = c < n0 ? s_ab[w] + 16ull * c : s_bb[w] + 16ull * (c - n0);
+                }
+                v[k] = *(gp)src;
             }
 #pragma unroll
-            for (int k = 0; k < BATCH; k++)
-                if (ok[k]) {
-                    s_slots[dst[k]] = (u64)v[k].x | (u64)v[k].y << 32;
-                    s_slots[dst[k] + 1] = (u64)v[k].z | (u64)v[k].w << 32;
-                }
+            for (int k = 0; k < BATCH; k++) {
+                const u32 q = q0 + k * FD_NT + lane;
+                if (q < used) s_pool[q] = v[k];
+            }
         }
         __syncthreads();
+#if KD_FD_CLOCK
+        const u64 T2 = clock64();
+#endif
         if (act) {
             u64* m = masks + u * tb.words;
             u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
-            u64* my = s_slots + (size_t)lane * LS;
             u8 st;
-            if (fa && fb) st = diff_one((lp8)((const u8*)my + ad), on, (lp8)((const u8*)(my + SLOT / 8) + bd), nn, tb, mk, m);
+            if (fit) st = diff_one((lp8)((const u8*)(s_pool + off) + ad), on, (lp8)((const u8*)(s_pool + off + na) + bd), nn, tb, mk, m);
             else st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
             if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
             for (int w = 0; w < tb.words; w++) {
@@ -525,7 +610,17 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             }
             status[u] = st;
         }
-        __syncthreads();  // slots and descriptors are rewritten by the next round
+        __syncthreads();  // the pool and descriptors are rewritten by the next round
+#if KD_FD_CLOCK
+        if (lane == 0) printf("FB %u %llu %llu\n", blockIdx.x, (unsigned long long)WE, (unsigned long long)wall_clock64());
+        if (lane == 0 && blockIdx.x % 97 == 0) {
+            const u64 T3 = clock64(), W3 = wall_clock64();
+            printf("FD entry->start %llu entry->end %llu wall %llu (x10ns) start %llu | blk %u offsets %llu staging %llu parse %llu total %llu used %u | hdr %llu dec %llu eq %llu nv %llu\n",
+                   (unsigned long long)(W0 - WE), (unsigned long long)(W3 - WE), (unsigned long long)(W3 - W0), (unsigned long long)W0 % 100000000, blockIdx.x, (unsigned long long)(T1 - T0), (unsigned long long)(T2 - T1), (unsigned long long)(T3 - T2),
+                   (unsigned long long)(T3 - T0), used, (unsigned long long)FD_DBG(0), (unsigned long long)FD_DBG(1),
+                   (unsigned long long)FD_DBG(2), (unsigned long long)FD_DBG(3));
+        }
+#endif
     }
 }
 
@@ -663,23 +758,24 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     if (n_upd == 0 && d_n_upd == nullptr) return KD_OK;
     // grid-stride: at most one resident wave per LDS-slot set (8 single-wave blocks per CU)
     u64 work = d_n_upd ? (n_upd ? n_upd : (u64)1 << 22) : n_upd;
-    // LDS slot per blob, from the largest typical blob (kd_blobs.size_hint; host arenas: measured).
-    // Blobs that do not fit a slot are parsed from global memory by their lane.
-    auto max_len = [](const kd_blobs* b) -> u64 {
+    // typical blob size: kd_blobs.size_hint, or the mean of host arenas
+    auto typical = [](const kd_blobs* b) -> u64 {
         if (b->size_hint) return b->size_hint;
-        u64 m = 0;
-        if (b->mem == KD_MEM_HOST)
-            for (u64 i = 0; i < b->n; i++) m = std::max<u64>(m, b->off[i + 1] - b->off[i]);
-        return m ? m : 256;
+        if (b->mem == KD_MEM_HOST && b->n) return (b->off[b->n] - b->off[0] + b->n - 1) / b->n;
+        return 256;
     };
-    const u64 need = std::max(max_len(ob), max_len(nb)) + 15;
+    const u64 typ = std::max(typical(ob), typical(nb));
     FdTabOff to;
     to.leg_o = (u32)o_lo; to.leg_n = (u32)o_ln; to.map_o = (u32)o_mo; to.map_n = (u32)o_mn; to.cmp = (u32)o_cmp;
     to.aligned = (u32)o_al; to.key_of_val = (u32)o_kov; to.bytes = (u32)o_end;
     const bool lds_tab = o_end <= FD_TAB_LDS_MAX;
-    const int slot = !lds_tab ? 0 : need <= 160 ? 160 : need <= 256 ? 256 : need <= 512 ? 512 : 0;
-    // one resident round: single-wave blocks per CU allowed by the 160 KB LDS (8 without slots)
-    const u64 lds_blk = slot ? (u64)FD_NT * (2 * slot + 8) + FD_NT * 20 + 1024 + o_end : 1024;
+    // LDS pool for one round of 64 updates: both blobs of every lane packed back to back, sized from
+    // the typical (mean) blob — ~(len + 15) / 16 chunks with the 16-B alignment skew — with 10 %
+    // headroom (1152 chunks: seven 64-update blocks per CU for ~110-B point features); a lane whose blobs do not fit the round's pool parses them from global memory.
+    const u64 per_round = (u64)FD_NT * 2 * (typ + 15) / 16 * 110 / 100;
+    const int pool = !lds_tab ? 0 : per_round <= 1152 ? 1152 : per_round <= 1536 ? 1536 : per_round <= 2048 ? 2048
+                   : per_round <= 3072 ? 3072 : per_round <= 4096 ? 4096 : 0;
+    const u64 lds_blk = pool ? (u64)pool * 17 + FD_NT * 24 + 1024 + o_end : 1024;
     const u64 per_cu = std::min<u64>(8, (160 * 1024) / lds_blk);
     unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, (u64)ctx->n_cu * per_cu);
     if (blocks == 0) blocks = 1;
@@ -689,9 +785,11 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
                                tb, to, (const u8*)dt, d_masks, d_status);
         };
-        if (slot == 160) args(k_fielddiff<160>);
-        else if (slot == 256) args(k_fielddiff<256>);
-        else if (slot == 512) args(k_fielddiff<512>);
+        if (pool == 1152) args(k_fielddiff<1152>);
+        else if (pool == 1536) args(k_fielddiff<1536>);
+        else if (pool == 2048) args(k_fielddiff<2048>);
+        else if (pool == 3072) args(k_fielddiff<3072>);
+        else if (pool == 4096) args(k_fielddiff<4096>);
         else
             hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks,

@@ -54,6 +54,7 @@ class DevBlobs:
         self.off = to_dev(off, device)
         self.nbytes = int(data.size)
         self.max_len = int((off[1:] - off[:-1]).max()) if self.n else 0
+        self.mean_len = int((int(off[-1]) - int(off[0]) + self.n - 1) // self.n) if self.n else 0
 
     def kd_blobs(self):
         b = N.KdBlobs()
@@ -61,7 +62,7 @@ class DevBlobs:
         b.data = self.data.data_ptr()
         b.off = self.off.data_ptr()
         b.mem = N.KD_MEM_DEVICE
-        b.size_hint = min(self.max_len, 0xFFFFFFFF)
+        b.size_hint = min(self.mean_len, 0xFFFFFFFF)  # typical (mean) blob size: sizes the LDS pool
         return b
 
 

@@ -7,5 +7,5 @@ cat gpurun_out/bench_e9.json
 bash scripts/probe_variants.sh 2>&1 | grep -v "Traceback\|File \|raise\|obj, end\|JSONDecodeError\|json.load\|return \|^ *\^"
 for v in; do
 KART_AMD_LIB=$(pwd)/build/probe/libkartdiff_$v.so timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check > gpurun_out/$v.txt 2> gpurun_out/$v.err || exit 1
-grep "^JT\|^FD" gpurun_out/$v.txt | tail -12
+grep "^JT\|^FD" gpurun_out/$v.txt | tail -30
 done
