@@ -1,18 +1,24 @@
 #!/usr/bin/env python3
-"""Bench: device-resident two-way feature diff (classify2 + field diff) on MI355X.
+"""Bench: device-resident bulk feature diff on MI355X (one JSON line on rank 0).
 
-Workload (BASELINE.json configs[1], "C2"): a synthetic 10M-point int-PK layer per GPU with seeded
-1% updates / 1% deletes / 1% inserts (kart_amd.synth.points_layer; the reference's feature blob
-and path encodings, synthetic OIDs).  One *step* = one full pass of the hot path over that layer:
-merge-path join + OID compare + key-ordered compaction of the delta set (k_partition2, k_join2,
-k_place2), then the msgpack field decode + Python-== column compare of every
-update (k_fielddiff) — all on the device, inputs resident in HBM before the timed region.
+Default workload (BASELINE.json configs[1], "C2"): a synthetic 10M-point int-PK layer per GPU with
+seeded 1% updates / 1% deletes / 1% inserts (kart_amd.synth.points_layer; the reference's feature
+blob and path encodings, synthetic OIDs).  One *step* = one full pass of the hot path over that
+layer: merge-path join + OID compare + key-ordered compaction of the delta set (k_partition2,
+k_join2, k_place2), then the msgpack field decode + Python-== column compare of every update
+(k_fielddiff) — all on the device, inputs resident in HBM before the timed region.
+
+--workload c5 (BASELINE configs[4], scaled: --n geometries per GPU, default 20M): GPKG geometry
+blobs of a spatially filtered layer (synth.geometry_layer); one step = k_envelopes (header /
+stored envelope or point WKB -> SpatialFilter bbox test + identity-CRS index envelope +
+EnvelopeEncoder bytes) + k_env_overlap (decode + cyclic overlap of the encoded envelopes).
 
 Multi-GPU (torch.distributed, one process per GPU, RCCL): each rank owns a disjoint dataset3
-path-bucket range (its own 10M-point shard; weak scaling); the only collective is the all-gather
-of per-rank delta counts each step.  value = feature pairs (union PKs) of all ranks / max-rank time.
+path-bucket range (its own shard; weak scaling); the only collective is the all-gather of per-rank
+counts each step.  value = units of all ranks / max-rank time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n POINTS] [--no-cpu-baseline]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c5] [--n UNITS]
+                       [--no-cpu-baseline]
 """
 import argparse
 import json
@@ -34,40 +40,110 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU (C2: 10M)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"])
+    ap.add_argument("--n", type=int, default=0, help="units per GPU (c2: points, default 10M; c5: geometries, 20M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unordered", action="store_true",
-                    help="tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
+                    help="c2: tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the count check")
+    ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
+    ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--time-all", action="store_true",
-                    help="HIP events around every kernel of a step (default: only the dominant k_join2, "
+                    help="HIP events around every kernel of a step (default: only the dominant kernel, "
                          "so the events do not inflate the step time)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    if not a.n:
+        a.n = 10_000_000 if a.workload == "c2" else 20_000_000
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
+    return a
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+class Dist:
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", rank=self.rank, world_size=self.world, device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(0)
+        self.dev = torch.device("cuda", torch.cuda.current_device())
 
+    def timed(self, step, steps, exchange=None):
+        """barrier + sync, K steps, sync + barrier; returns the max-over-ranks seconds"""
+        torch, dist = self.torch, self.dist
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+            if exchange is not None and self.world > 1:
+                exchange()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if self.world > 1:
+            e = torch.tensor([el], device=self.dev, dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el
+
+    def total(self, *vals):
+        if self.world == 1:
+            return vals
+        t = self.torch.tensor(list(vals), device=self.dev, dtype=self.torch.int64)
+        self.dist.all_reduce(t)
+        return tuple(int(x) for x in t.tolist())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def roofline(kern, dom, alg_bytes, traffic_json, units_tag, n_units):
+    """roofline object of the dominant kernel: algorithmic bytes per launch / its average launch time"""
+    if dom not in kern:
+        return None
+    achieved = alg_bytes / (kern[dom][1] * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("kernel") == dom and int(tj.get(units_tag, -1)) == n_units:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_bytes_per_launch": int(alg_bytes),
+            "avg_launch_ms": round(kern[dom][1], 5)}
+
+
+def kernel_times(eng, names):
+    kern = {}
+    for name in names:
+        launches, ms = eng.prof_get(name)
+        if launches:
+            kern[name] = (launches, ms / launches)
+    return kern
+
+
+# ---------------------------------------------------------------------------------------------
+def run_c2(args, D):
+    torch = D.torch
     from kart_amd import shard, synth
     from kart_amd.device import DiffPipeline
     from kart_amd.engine import Engine
@@ -75,14 +151,13 @@ def main():
 
     n = args.n
     t0 = time.time()
-    pk0 = shard.rank_pk_base(rank, n)
-    L = synth.points_layer(n, seed=synth.SEED + rank, pk0=pk0)
-    log(f"[rank {rank}] generated {n} points in {time.time() - t0:.1f}s "
+    L = synth.points_layer(n, seed=synth.SEED + D.rank, pk0=shard.rank_pk_base(D.rank, n))
+    log(f"[rank {D.rank}] generated {n} points in {time.time() - t0:.1f}s "
         f"(+{L.n_insert} ins, ~{L.n_update} upd, -{L.n_delete} del)")
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     eng = Engine(torch.cuda.current_device())
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, dev, ordered=not args.unordered)
+    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, D.dev, ordered=not args.unordered)
     torch.cuda.synchronize()
 
     # ---- warmup + correctness of the resident pipeline against the generator's own counts ----
@@ -94,46 +169,18 @@ def main():
         assert (counts["inserts"], counts["updates"], counts["deletes"]) == (L.n_insert, L.n_update, L.n_delete), counts
         assert not status.any(), "fielddiff status flags set"
     n_pairs = L.base.n + L.n_insert
-    counts_t = torch.tensor([counts["inserts"], counts["updates"], counts["deletes"]], device=dev, dtype=torch.int64)
+    counts_t = torch.tensor([counts["inserts"], counts["updates"], counts["deletes"]], device=D.dev, dtype=torch.int64)
+    gathered = [torch.empty_like(counts_t) for _ in range(D.world)]
 
-    # ---- timed region ----
     eng.prof_reset()
     eng.prof_select(None if args.time_all else ["k_join2"])
     eng.prof_enable(not args.no_events)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    gathered = None
-    for _ in range(args.steps):
-        pipe.step()
-        if world > 1:
-            gathered = [torch.empty_like(counts_t) for _ in range(world)]
-            dist.all_gather(gathered, counts_t)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    elapsed = D.timed(pipe.step, args.steps, lambda: D.dist.all_gather(gathered, counts_t))
     eng.prof_enable(False)
-    if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-        tot = torch.tensor([n_pairs, counts["deltas"]], device=dev, dtype=torch.int64)
-        dist.all_reduce(tot)
-        total_pairs, total_deltas = int(tot[0].item()), int(tot[1].item())
-    else:
-        total_pairs, total_deltas = n_pairs, counts["deltas"]
+    total_pairs, total_deltas = D.total(n_pairs, counts["deltas"])
+    kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_fielddiff"))
 
-    kern = {}
-    for name in ("k_partition2", "k_join2", "k_place2", "k_fielddiff"):  # kernels of a step
-        launches, ms = eng.prof_get(name)
-        if launches:
-            kern[name] = (launches, ms / launches)
-    ms_per_step = elapsed / args.steps * 1e3
-    value = total_pairs * args.steps / elapsed / 1e6
-
-    # ---- roofline of the dominant kernel (algorithmic bytes per launch, DESIGN.md §roofline) ----
+    # ---- roofline of the dominant kernel (algorithmic bytes per launch, DESIGN.md §3.1) ----
     nA, nB = L.base.n, L.target.n
     ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
     upd_bytes = int((ob_off[upd[:, 0] + 1] - ob_off[upd[:, 0]]).sum() + (nb_off[upd[:, 1] + 1] - nb_off[upd[:, 1]]).sum())
@@ -142,55 +189,35 @@ def main():
         "k_fielddiff": upd_bytes + counts["updates"] * (8 + 8 * maps.words + 1),
     }
     dom = max(kern, key=lambda k: kern[k][1]) if kern else None
-    roof = None
-    if dom in alg:
-        achieved = alg[dom] / (kern[dom][1] * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("kernel") == dom and int(tj.get("n_points", -1)) == n:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": alg[dom], "avg_launch_ms": round(kern[dom][1], 5)}
-
-    # ---- CPU baseline: the oracle (C port, 1 thread) on a bounded sample of the same workload ----
+    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, "n_points", n) if dom in alg else None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(L, maps, args.cpu_seconds)
-
-    if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "M feature-pairs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8/u64 (integer + fp64 compare)",
-            "data": "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
-            "config": {"workload": "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
-                       "points_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
-                       "delta_order": "tile-grouped (same delta set)" if args.unordered else "key",
-                       "parallelism": f"bucket-range shards x{world}"},
-            "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_c2(L, maps, args.cpu_seconds)
     eng.close()
+    return {
+        "metric": METRIC,
+        "value": round(total_pairs * args.steps / elapsed / 1e6, 2),
+        "unit": "M feature-pairs/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u64 (integer + fp64 compare)",
+        "data": "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
+        "config": {"workload": "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
+                   "points_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
+                   "delta_order": "tile-grouped (same delta set)" if args.unordered else "key",
+                   "parallelism": f"bucket-range shards x{D.world}"},
+        "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
 
 
-def cpu_baseline(L, maps, seconds):
+def cpu_baseline_c2(L, maps, seconds):
     """oracle classify2 + fielddiff (sequential C, 1 core) on the same layer, repeated for ~N s"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle as O
@@ -210,6 +237,115 @@ def cpu_baseline(L, maps, seconds):
     return {"value": round(pairs / dt / 1e6, 3), "unit": "M feature-pairs/s", "cores": 1, "kind": "port",
             "sample": f"full C2 layer ({A.n + L.n_insert} pairs) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
                       f"classify2 + fielddiff, 1 thread"}
+
+
+# ---------------------------------------------------------------------------------------------
+def run_c5(args, D):
+    import ctypes
+
+    torch = D.torch
+    from kart_amd import _native as N
+    from kart_amd import synth
+    from kart_amd.device import to_dev
+    from kart_amd.engine import Engine
+
+    n, bits = args.n, 20
+    nb = bits // 2
+    t0 = time.time()
+    data, off, is_pt = synth.geometry_layer(n, seed=synth.SEED + D.rank)
+    log(f"[rank {D.rank}] generated {n} geometries ({data.size / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
+    eng = Engine(torch.cuda.current_device())
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    d_data, d_off = to_dev(data, D.dev), to_dev(off, D.dev)
+    g = N.KdBlobs()
+    g.n, g.data, g.off, g.mem, g.size_hint = n, d_data.data_ptr(), d_off.data_ptr(), N.KD_MEM_DEVICE, 0
+    match = torch.empty(n, dtype=torch.uint8, device=D.dev)
+    enc = torch.empty(n * nb, dtype=torch.uint8, device=D.dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=D.dev)
+    ovl = torch.empty(n, dtype=torch.uint8, device=D.dev)
+    fe = (ctypes.c_double * 4)(*synth.C5_FILTER)
+    q = (ctypes.c_double * 4)(synth.C5_FILTER[0], synth.C5_FILTER[2], synth.C5_FILTER[1], synth.C5_FILTER[3])
+    L, ctx = eng.L, eng.ctx
+
+    def step():
+        N.check(L.kd_envelopes(ctx, ctypes.byref(g), fe, bits, match.data_ptr(), enc.data_ptr(), ok.data_ptr(),
+                               N.KD_MEM_DEVICE, None), "kd_envelopes")
+        N.check(L.kd_env_overlap(ctx, enc.data_ptr(), n, bits, q, ovl.data_ptr(), N.KD_MEM_DEVICE), "kd_env_overlap")
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_check:  # the first 1M geometries against the CPU oracle (bit-exact)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle import oracle as O
+
+        m = min(n, 1_000_000)
+        om, oe, okk, _ = O.envelope_batch(data[: int(off[m])], off[: m + 1], synth.C5_FILTER, bits)
+        assert np.array_equal(match[:m].cpu().numpy(), om), "k_envelopes match flags differ from the oracle"
+        assert np.array_equal(ok[:m].cpu().numpy(), okk), "k_envelopes enc_ok differs from the oracle"
+        assert np.array_equal(enc[: m * nb].cpu().numpy().reshape(m, nb), oe), "EnvelopeEncoder bytes differ"
+    eng.prof_reset()
+    eng.prof_select(None if args.time_all else ["k_envelopes"])
+    eng.prof_enable(not args.no_events)
+    cnt = torch.zeros(1, dtype=torch.int64, device=D.dev)
+    gathered = [torch.empty_like(cnt) for _ in range(D.world)]
+    elapsed = D.timed(step, args.steps, lambda: D.dist.all_gather(gathered, cnt))
+    eng.prof_enable(False)
+    (total,) = D.total(n)
+    kern = kernel_times(eng, ("k_envelopes", "k_env_overlap"))
+    npt = int(is_pt.sum())
+    # algorithmic bytes per k_envelopes launch: offsets (8 B) + GPKG header (8 B) + stored envelope
+    # (32 B, polygons) or point WKB (21 B) read; match + enc_ok flags (2 B) + encoded envelope written
+    alg = n * (8 + 8 + 2 + nb) + npt * 21 + (n - npt) * 32
+    roof = roofline(kern, "k_envelopes", alg, args.traffic_json, "n_geoms", n)
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle import oracle as O
+
+        m = min(n, 2_000_000)
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            O.envelope_batch(data[: int(off[m])], off[: m + 1], synth.C5_FILTER, bits)
+            reps += 1
+            if time.perf_counter() - t0 >= min(args.cpu_seconds, 5.0):
+                break
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(m * reps / dt / 1e6, 3), "unit": "M geometries/s", "cores": 1, "kind": "port",
+               "sample": f"first {m} geometries of the same layer x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
+                         f"envelope batch (bbox test + index envelope + EnvelopeEncoder), 1 thread"}
+    eng.close()
+    return {
+        "metric": METRIC,
+        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "unit": "M geometries/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64 (envelopes, EnvelopeEncoder) + u8",
+        "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
+        "config": {"workload": f"C5 (scaled to {n} geometries per GPU): spatial-filter envelopes + "
+                               "EnvelopeEncoder + encoded-envelope overlap",
+                   "geoms_per_gpu": n, "points": npt, "bits": bits, "filter": list(synth.C5_FILTER),
+                   "parallelism": f"independent shards x{D.world}"},
+        "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+
+
+def main():
+    args = parse()
+    D = Dist()
+    out = run_c2(args, D) if args.workload == "c2" else run_c5(args, D)
+    if D.rank == 0:
+        print(json.dumps(out), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

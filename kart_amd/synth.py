@@ -186,3 +186,65 @@ def _int_keys(pk):
     bucket = (q & ((1 << 24) - 1)).astype(np.uint64)
     k = ((pk >> 30) + (1 << 33)).astype(np.uint64)
     return np.ascontiguousarray((bucket << np.uint64(40)) | (k << np.uint64(6)) | r)
+
+
+# ---------------------------------------------------------------------------------------------
+# C5: GPKG geometry blobs of a spatially filtered layer
+C5_FILTER = (170.0, 180.0, -50.0, -30.0)  # (min-x, max-x, min-y, max-y) of the spatial filter
+
+
+def geometry_layer(n, seed=SEED, frac_point=0.3):
+    """n GPKG geometry blobs, EPSG:4326, as one arena (uint8 data, uint64 off[n+1]).
+
+    30 % points (8-B header + 21-B WKB, no stored envelope), 70 % MULTIPOLYGONs (8-B header + 32-B
+    XY envelope + WKB body, 245-582 B in total: polygon bodies are zero-filled — only the header,
+    envelope and WKB type are ever read on this path).  lon U[-180, 180), lat U[-85, 85]; polygon
+    widths log-U[1e-6, 10] degrees; 1 % straddle +180; 0.1 % >= 180 degrees wide (no index
+    envelope); 0.1 % EMPTY points; 1 % of polygons start exactly on the filter's east edge."""
+    rng = np.random.default_rng(seed)
+    is_pt = rng.random(n) < frac_point
+    npt, npoly = int(is_pt.sum()), int(n - is_pt.sum())
+    size = np.where(is_pt, 29, rng.integers(245, 583, size=n)).astype(np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(size, out=off[1:])
+    data = np.zeros(int(off[-1]), np.uint8)
+    start = off[:-1]
+    lon = rng.uniform(-180.0, 180.0, n)
+    lat = rng.uniform(-85.0, 85.0, n)
+
+    # points: GP 00 flags srs | 01 01000000 x y
+    pi = np.nonzero(is_pt)[0]
+    rec = np.zeros((npt, 29), np.uint8)
+    rec[:, 0], rec[:, 1], rec[:, 2] = ord("G"), ord("P"), 0
+    empty = rng.random(npt) < 0.001
+    rec[:, 3] = np.where(empty, 0x11, 0x01)
+    rec[:, 4:8] = np.array([4326], "<i4").view(np.uint8)
+    rec[:, 8] = 1
+    rec[:, 9:13] = np.array([1], "<u4").view(np.uint8)
+    xy = np.stack([lon[pi], lat[pi]], 1)
+    xy[empty] = np.nan
+    rec[:, 13:29] = xy.astype("<f8").view(np.uint8).reshape(npt, 16)
+    data[(start[pi, None] + np.arange(29, dtype=np.uint64)[None, :]).ravel()] = rec.ravel()
+
+    # polygons: GP 00 03 srs | minx maxx miny maxy | 01 06000000 01000000 ...
+    qi = np.nonzero(~is_pt)[0]
+    w = 10.0 ** rng.uniform(-6, 1, npoly)
+    h = 10.0 ** rng.uniform(-6, 1, npoly)
+    minx, miny = lon[qi], lat[qi]
+    u = rng.random(npoly)
+    straddle = u < 0.01
+    minx = np.where(straddle, 180.0 - w / 2, minx)
+    wide = (u >= 0.01) & (u < 0.011)
+    w = np.where(wide, 180.0 + 10.0 * rng.random(npoly), w)
+    edge = (u >= 0.011) & (u < 0.021)
+    minx = np.where(edge, C5_FILTER[1], minx)
+    env = np.stack([minx, minx + w, miny, np.minimum(miny + h, 90.0)], 1)
+    rec = np.zeros((npoly, 49), np.uint8)
+    rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3] = ord("G"), ord("P"), 0, 0x03
+    rec[:, 4:8] = np.array([4326], "<i4").view(np.uint8)
+    rec[:, 8:40] = env.astype("<f8").view(np.uint8).reshape(npoly, 32)
+    rec[:, 40] = 1
+    rec[:, 41:45] = np.array([6], "<u4").view(np.uint8)
+    rec[:, 45:49] = np.array([1], "<u4").view(np.uint8)
+    data[(start[qi, None] + np.arange(49, dtype=np.uint64)[None, :]).ravel()] = rec.ravel()
+    return data, off, is_pt

@@ -263,3 +263,16 @@ def test_gpu_device_pipeline_vs_oracle(engine, n, ordered):
     assert (counts["inserts"], counts["updates"], counts["deletes"]) == (oc["inserts"], oc["updates"], oc["deletes"])
     om, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
     assert np.array_equal(masks, om) and np.array_equal(status, ost)
+
+
+@pytest.mark.parametrize("n,seed", [(1000, 1), (2_000_000, 2)])
+def test_gpu_envelopes_c5_layer_vs_oracle(engine, n, seed):
+    """the C5 bench layer (points, multipolygons, straddles, >=180-degree widths, empties, filter-edge
+    envelopes) at scale: flags, EnvelopeEncoder bytes and candidate counts bit-exact"""
+    from kart_amd import synth
+
+    data, off, _ = synth.geometry_layer(n, seed=seed)
+    gm, ge, gk, gc = engine.envelopes(data, off, synth.C5_FILTER, 20)
+    om, oe, ok, oc = O.envelope_batch(data, off, synth.C5_FILTER, 20)
+    assert np.array_equal(gm, om) and np.array_equal(gk, ok) and np.array_equal(ge, oe) and gc == oc
+    assert 0 < gc < n
