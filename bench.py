@@ -183,7 +183,9 @@ def run_c2(args, D):
     # ---- roofline of the dominant kernel (algorithmic bytes per launch) ----
     nA, nB = L.base.n, L.target.n
     ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
-    upd_bytes = int((ob_off[upd[:, 0] + 1] - ob_off[upd[:, 0]]).sum() + (nb_off[upd[:, 1] + 1] - nb_off[upd[:, 1]]).sum())
+    ok_u = (upd[:, 0] < nA) & (upd[:, 1] < nB)  # (profiling variants with --no-check may emit junk)
+    u0, u1 = upd[ok_u, 0], upd[ok_u, 1]
+    upd_bytes = int((ob_off[u0 + 1] - ob_off[u0]).sum() + (nb_off[u1 + 1] - nb_off[u1]).sum())
     alg = {
         "k_join2": 28 * (nA + nB) + 8 * counts["deltas"] + 8 * counts["updates"],
         "k_fielddiff": upd_bytes + counts["updates"] * (8 + 8 * maps.words + 1),

@@ -1,37 +1,55 @@
-// kd_classify2.hip — classify2: the two-way tree diff as one single-pass HIP kernel on gfx950.
+// kd_classify2.hip — classify2: the two-way tree diff on gfx950.
 //
 // Replaces libgit2's tree-to-tree diff as consumed by RichBaseDataset.diff_feature
 // (/root/reference/kart/rich_base_dataset.py:205-300): both commits' feature leaves arrive as
 // strictly ascending join keys + 20-byte blob OIDs; a key on one side only is an insert/delete, a
 // key on both sides with different OIDs is an update (GIT_DELTA_ADDED/DELETED/MODIFIED).
 //
-//   k_partition2  merge-path split points of the union sequence: 8 lanes per tile boundary,
-//                 8-ary search (8 dependent HBM round trips instead of ~24 for binary search)
-//   k_join2       per 1024-item tile (256 threads x 4 items):
-//                   0. the tile's keys AND OIDs (both sides) -> LDS by LDS-DMA 16-B chunks, every
-//                      load issued before any use: one HBM round trip per tile
-//                   A. per-thread merge path over 4 items in LDS; matched pairs' OIDs compared
-//                      from LDS; each item's outcome (kind, local indices) kept in a register
-//                   B. block scan of the tile's delta/update counts; records written key-ordered
-//                      into a tile-local staging slot (ordered) or appended per tile (unordered)
-//   k_place2      one tile per block: output offset from 64-tile group sums (accumulated by the
-//                 join) + the earlier tiles of its group; staged records -> final key-ordered
-//                 positions; totals from the last block.
-// Inputs are read once; the staging round trip costs 16 B per delta.
+// The key union is cut into 1024-item merge-path tiles (k_partition2).  Default (key-ordered) path:
+//   k_join2p   persistent: a few workgroups per CU walk the tiles round-robin.  Per tile:
+//                0. keys + OIDs of both sides (plus the B entry after the tile) arrive in registers
+//                   as 16-B chunks — issued one tile AHEAD, while the previous tile computes — and go
+//                   to LDS once that tile is done (one LDS buffer per workgroup, loads always in
+//                   flight);
+//                1. merge path (4-ary search + register walk), OID compare in LDS;
+//                2. per-item-slot ballots -> tile-local offsets; decoupled look-back over earlier
+//                   tiles' descriptors -> the tile's global offsets; records written straight to
+//                   their final key-ordered positions (no staging, no second pass).
+// KD_DIFF_UNORDERED: k_join2 (one tile per workgroup, LDS-DMA staging) appends each tile's records
+// at an atomically reserved offset (tiles in completion order, key order inside each tile).
+// KD_C2_MODE (profiling builds): 1 = the per-tile k_join2 (LDS-DMA staging) for the ordered path;
+// 2 = k_join2p with a decoupled look-back instead of k_place2 (slow: with ~1000 tiles in flight the
+// look-back walks ~30 descriptor windows per tile).
 #include "kd_join.h"
 
 namespace kd {
 
-constexpr u64 C2_GROUP = 64;  // tiles per group sum (k_place2 offsets)
+constexpr u64 C2_GROUP = 64;  // tiles per group sum (staged path: k_place2 offsets)
 #ifndef KD_C2_STAGE_PAD
 #define KD_C2_STAGE_PAD 32
 #endif
 // staging slot stride in records: one tile plus a pad, so the slots' hot first lines do not all
-// fall on the same HBM channels (a 16 KB power-of-two stride would)
+// fall on the same HBM channels (a power-of-two stride would)
 constexpr u64 C2_STAGE = C2_TILE + KD_C2_STAGE_PAD;
 #ifndef KD_PLACE_NT
-#define KD_PLACE_NT 64  // one wave per tile: up to 32 staged records per lane, all loads in flight
+#define KD_PLACE_NT 64  // one wave per tile: up to 16 staged records per lane, all loads in flight
 #endif
+#ifndef KD_C2_MODE
+#define KD_C2_MODE 1  // ordered path: 1 per-tile k_join2 + k_place2, 0 persistent k_join2p + k_place2, 2 look-back
+#endif
+#ifndef KD_J_EXP
+#define KD_J_EXP 0  // profiling builds only: 1 = staging only (k_join2)
+#endif
+#ifndef KD_J_OIDG
+#define KD_J_OIDG 1  // k_join2: keys-only LDS image, OIDs compared straight from HBM (more tiles per CU)
+#endif
+#ifndef KD_J2P_WAVES
+#define KD_J2P_WAVES 4  // k_join2p waves per SIMD to fit (VGPR cap): 4 four-wave workgroups per CU, no spills
+#endif
+
+// ---------------------------------------------------------------------------------------------
+// merge-path partition
+// ---------------------------------------------------------------------------------------------
 
 // One merge-path split by a group of PW consecutive lanes (PW-ary search, all PW lanes call it
 // together): smallest i in [lo, hi] with i == hi || A[i] > B[d-1-i]  (ties: A first).
@@ -58,18 +76,17 @@ __device__ __forceinline__ u64 mp_search(const u64* __restrict__ A, const u64* _
 // levels: one block per group of C2_PG tiles.  The group's two end splits are searched over the
 // whole arrays (16 lanes each, 16-ary: ~6 rounds of random HBM reads); every inner split then lies
 // inside the box the end splits span (i and d-i are both monotone in d), at most C2_PG tiles wide,
-// and is found there by 8 lanes (8-ary) whose probes land in that small, cache-warm region.  This
-// replaced one full-array 8-ary search per tile (~8 rounds x 16 random lines for every boundary).
+// and is found there by 8 lanes (8-ary) whose probes land in that small, cache-warm region.
+// The kernel also clears the counters and look-back descriptors the join needs (stream-ordered
+// before it), instead of separate memset launches.
 constexpr int C2_PG = 32;
 __global__ __launch_bounds__(256) void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B,
                                                     u64 nB, u64 ntiles, u64* __restrict__ part,
                                                     u64* __restrict__ zero_counts, u32* __restrict__ zero_err,
-                                                    u64* __restrict__ zero_gsum, u64 n_gsum) {
-    // the join's counters start at zero: cleared here (stream-ordered before k_join2) instead of
-    // by separate memset launches
+                                                    u64* __restrict__ zero_buf, u64 n_zero) {
     if (blockIdx.x == 0 && threadIdx.x < 4) zero_counts[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 4) *zero_err = 0;
-    for (u64 k = (u64)blockIdx.x * 256 + threadIdx.x; k < n_gsum; k += (u64)gridDim.x * 256) zero_gsum[k] = 0;
+    for (u64 k = (u64)blockIdx.x * 256 + threadIdx.x; k < n_zero; k += (u64)gridDim.x * 256) zero_buf[k] = 0;
     __shared__ u64 s_end[2];
     const int tid = threadIdx.x;
     const u64 total = nA + nB;
@@ -96,6 +113,9 @@ __global__ __launch_bounds__(256) void k_partition2(const u64* __restrict__ A, u
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// shared tile machinery
+// ---------------------------------------------------------------------------------------------
 struct Join2Args {
     const u64* A;
     const u8* oidA;
@@ -109,14 +129,17 @@ struct Join2Args {
     const u8* nameB;
     const u64* nameOffB;
     int hash_mode;
-    uint2* stage_delta;  // ordered mode: tile-local slots of TILE records
+    const u8* dummy;     // >= 16 readable device bytes: source of masked-off chunk loads
+    uint2* stage_delta;  // staged path: tile-local slots of TILE records
     uint2* stage_upd;
-    u32* tile_cnt;       // ordered mode: [ntiles*4] inserts, updates, deletes, deltas
-    u64* gsum;           // ordered mode: [2*ngroups] per C2_GROUP tiles: deltas | updates<<32, inserts | deletes<<32
-    uint2* out_delta;    // unordered mode: final lists, appended per tile
+    u32* tile_cnt;       // staged path: [ntiles*4] inserts, updates, deletes, deltas
+    u64* gsum;           // staged path: [2*ngroups] deltas | updates<<32, inserts | deletes<<32
+    uint2* out_delta;    // final lists
     uint2* out_upd;
-    u64* counts;         // unordered mode: [4] inserts, updates, deletes, deltas (atomic)
+    u64* counts;         // [4] inserts, updates, deletes, deltas
     u32* err;
+    u64* desc;           // persistent path: [2*ntiles] look-back descriptors
+    u64 ntiles;
 };
 
 // A byte range of one input array, copied to LDS as 16-byte chunks of its 16-byte-aligned
@@ -140,115 +163,94 @@ __device__ __forceinline__ Range mk_range(const void* p, u64 first_byte, u64 end
 template <int NT, int IPT>
 struct Join2Lds {
     static constexpr int TILE = NT * IPT;
-    // na + nb <= TILE items; keys 8 B and OIDs 20 B per item, +1 lookahead entry on B, and at most
-    // two extra (partial) chunks per range
-    static constexpr int CH = (28 * (TILE + 1) + 15) / 16 + 8;
+    // na + nb <= TILE items; keys 8 B and OIDs 20 B per item, +1 lookahead entry on B, +1 lookbehind
+    // key per side, and at most two extra (partial) chunks per range
+    static constexpr int CH = (28 * (TILE + 1) + 16 + 15) / 16 + 8;  // + the two lookbehind keys
     static constexpr int ROUNDS = (CH + NT - 1) / NT;
     // 4-ary search rounds until a width of TILE shrinks to 0 (w -> ceil(w/4) - 1)
     static constexpr int rounds(int w) { return w <= 0 ? 0 : 1 + rounds((w + 3) / 4 - 1); }
     static constexpr int SEARCH_ROUNDS = rounds(TILE);
 };
 
-#ifndef KD_J_EXP
-#define KD_J_EXP 0  // profiling builds only: 1 = DMA staging only, 9 = per-phase clock64 printf
-#endif
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef const __attribute__((address_space(1))) void* glb_vp;
+typedef const __attribute__((address_space(1))) u32x4* gp_x4;
 
-// The tile (merge-path items [d0, d1): A entries [i0, i1), B entries [j0, j1)) is staged in ONE
-// HBM round trip: keys and OIDs of both sides, plus the B entry after the tile (a tile's last A
-// item may match it), go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, 16 B
-// per lane, the wave's 64 chunks land contiguously), all issued before any use.  Everything after
-// that — merge path, OID compare, compaction — reads LDS.
-//
-// UNORD: each tile reserves its output ranges with one atomic add per counter and writes its
-// (key-ordered) records straight to the final lists.  Ordered (default): tile-local staging +
-// k_place2.
-template <int NT, int IPT, bool UNORD>
-__global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
-    using LD = Join2Lds<NT, IPT>;
-    constexpr int TILE = LD::TILE;
-    static_assert(TILE <= 4095, "per-item records hold 12-bit local indices");
-    __shared__ u32x4 s_ch[LD::CH];  // lanes past the tile's chunks are masked off
-    __shared__ u32 s_wave[3 * NT / 64];
-    __shared__ u64 s_base[2];
+// Tile t's place in both sides: merge-path items [d0, d1), A entries [i0, i1), B entries [j0, j1)
+// (+ the lookahead B[j1] when it exists), and the keys just before it on each side.
+struct TileGeo {
+    u64 i0, i1, j0, j1, j1e, lbA, lbB;
+    int na, nb;
+    bool ok, has_lbA, has_lbB, has_la;
+};
 
-    const int tid = threadIdx.x;
-    const u64 tile = blockIdx.x;
-#if KD_J_EXP == 9
-    const u64 T0 = clock64();
-    u64 T1 = 0, T2 = 0, T3 = 0;
-#endif
+// wave-uniform 64-bit value into SGPRs: the tile geometry is loaded through the vector path (the
+// compiler cannot prove part[] read-only for s_load), and without this every derived address would
+// sit in VGPRs — for the current AND the prefetched tile
+__device__ __forceinline__ u64 uni64(u64 x) {
+    // (readfirstlane returns int: widen through u32, or bit 31 of the low half would sign-extend)
+    return (u64)(u32)__builtin_amdgcn_readfirstlane((u32)x) | (u64)(u32)__builtin_amdgcn_readfirstlane((u32)(x >> 32)) << 32;
+}
+
+// geometry of tile t from its two split points (p0 = part[t], p1 = part[t + 1])
+__device__ __forceinline__ TileGeo tile_geo_from(const Join2Args& g, u64 t, int TILE, u64 p0, u64 p1) {
+    TileGeo q;
     const u64 total = g.nA + g.nB;
-    const u64 d0 = tile * (u64)TILE;
-    const u64 d1 = d0 + TILE < total ? d0 + TILE : total;
-    const u64 i0 = g.part[tile], i1 = g.part[tile + 1];
-    if (i1 < i0 || d1 - i1 < d0 - i0 || i1 - i0 > d1 - d0) {  // only on unsorted input
-        if (tid == 0) {
-            atomicOr(g.err, 1u);
-            if (!UNORD) {
-                u32* c = g.tile_cnt + 4 * tile;
-                c[0] = c[1] = c[2] = c[3] = 0;
-            }
-        }
-        return;
-    }
-    const u64 j0 = d0 - i0, j1 = d1 - i1;
-    const u64 j1e = j1 < g.nB ? j1 + 1 : j1;  // + the lookahead entry B[j1]
-    const int na = (int)(i1 - i0), nb = (int)(j1 - j0);
+    const u64 d0 = t * (u64)TILE, d1 = d0 + TILE < total ? d0 + TILE : total;
+    q.i0 = uni64(p0);
+    q.i1 = uni64(p1);
+    q.ok = !(q.i1 < q.i0 || d1 - q.i1 < d0 - q.i0 || q.i1 - q.i0 > d1 - d0);  // fails only on unsorted input
+    if (!q.ok) q.i1 = q.i0 = d0 < g.nA ? d0 : g.nA;
+    q.j0 = d0 - q.i0;
+    q.j1 = q.ok ? d1 - q.i1 : q.j0;
+    if (q.j1 > g.nB) q.j1 = q.j0 = g.nB;
+    q.j1e = q.j1 < g.nB ? q.j1 + 1 : q.j1;
+    q.na = (int)(q.i1 - q.i0);
+    q.nb = (int)(q.j1 - q.j0);
+    q.has_lbA = q.i0 > 0;
+    q.has_lbB = q.j0 > 0;
+    q.has_la = q.j1 < g.nB;
+    q.lbA = q.lbB = 0;  // read from LDS: the key ranges start one entry early (the lookbehind keys)
+    return q;
+}
 
-    // ---- stage: four byte ranges -> LDS, chunk c at LDS byte 16c ------------------------------------
-    const Range rka = mk_range(g.A, 8 * i0, 8 * i1), rkb = mk_range(g.B, 8 * j0, 8 * j1e);
-    const Range roa = mk_range(g.oidA, 20 * i0, 20 * i1), rob = mk_range(g.oidB, 20 * j0, 20 * j1e);
-    const u32 c1 = rka.nch, c2 = c1 + rkb.nch, c3 = c2 + roa.nch;
-    // 64-chunk pieces (one wave-instruction each: wave-uniform source base and LDS base, lane l takes
-    // chunk 64p + l), dealt round-robin to the waves across the four ranges: scalar address math
-    {
-        constexpr int NW = NT / 64;
-        const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-        u32 q0 = 0;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const Range& R = r == 0 ? rka : r == 1 ? rkb : r == 2 ? roa : rob;
-            const u32 off = r == 0 ? 0 : r == 1 ? c1 : r == 2 ? c2 : c3;
-            const u32 np = (R.nch + 63) >> 6;
-            for (u32 p = (u32)(wid + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
-                const u32 c = 64 * p + lane;
-                if (c < R.nch)
-                    __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(s_ch + off + 64 * p), 16, 0, 0);
-            }
-            q0 += np;
-        }
-    }
-    // lookbehind keys (tiny, scalar; in flight with the DMA)
-    const bool has_lbA = i0 > 0, has_lbB = j0 > 0, has_la = j1 < g.nB;
-    const u64 lbA = has_lbA ? g.A[i0 - 1] : 0;
-    const u64 lbB = has_lbB ? g.B[j0 - 1] : 0;
-    __syncthreads();  // vmcnt(0) + barrier: the DMA has landed
-#if KD_J_EXP == 9
-    T1 = clock64();
-#endif
-    const u64* sA = (const u64*)((const u8*)s_ch + rka.skew);
-    const u64* sB = (const u64*)((const u8*)(s_ch + c1) + rkb.skew);
-    const u32* oA = (const u32*)((const u8*)(s_ch + c2) + roa.skew);  // 4-B aligned: 20*i is
-    const u32* oB = (const u32*)((const u8*)(s_ch + c3) + rob.skew);  // and allocations are
-#if KD_J_EXP == 1  // staging only (profiling builds)
-    if (tid == 0 && !UNORD) {
-        u32* c = g.tile_cnt + 4 * tile;
-        c[0] = c[1] = c[2] = c[3] = ((const u32*)s_ch)[tid] == 0x12345678u ? (u32)(lbA ^ lbB) : 0;
-    }
-    return;
-#endif
+__device__ __forceinline__ TileGeo tile_geo(const Join2Args& g, u64 t, int TILE) {
+    return tile_geo_from(g, t, TILE, g.part[t], g.part[t + 1]);
+}
 
-    // ---- merge path, branch-free (selects instead of divergent branches: SALU exec-mask traffic was
-    //      the join's largest instruction stream).  4-ary search for the thread's split: 3 independent
-    //      probes per round, a fixed round count (5 for a 1024-item tile); then a walk over IPT items with
-    //      the current and previous keys in registers (one LDS round trip per item; the strictly-
-    //      ascending check compares registers).  Outcome per item in a register:
-    //      rec = kind << 25 | changed << 24 | jb << 12 | ia
-    enum : u32 { R_NONE = 0, R_DEL = 1, R_MATCH = 2, R_INS = 3 };
+struct TileRanges {
+    Range ka, kb, oa, ob;
+    u32 c1, c2, c3, c4;  // chunk offsets of the four ranges in the LDS image
+};
+
+__device__ __forceinline__ TileRanges tile_ranges(const Join2Args& g, const TileGeo& q) {
+    TileRanges r;
+    r.ka = mk_range(g.A, 8 * (q.i0 - q.has_lbA), 8 * q.i1);  // + A[i0-1], B[j0-1]: the lookbehind keys
+    r.kb = mk_range(g.B, 8 * (q.j0 - q.has_lbB), 8 * q.j1e);
+    r.oa = mk_range(g.oidA, 20 * q.i0, 20 * q.i1);
+    r.ob = mk_range(g.oidB, 20 * q.j0, 20 * q.j1e);
+    r.c1 = r.ka.nch;
+    r.c2 = r.c1 + r.kb.nch;
+    r.c3 = r.c2 + r.oa.nch;
+    r.c4 = r.c3 + r.ob.nch;
+    return r;
+}
+
+enum : u32 { R_NONE = 0, R_DEL = 1, R_MATCH = 2, R_INS = 3 };
+
+// Merge path of one tile out of LDS, branch-free (selects instead of divergent branches: SALU
+// exec-mask traffic was the join's largest instruction stream).  4-ary search for the thread's
+// split — 3 independent probes per round, a fixed round count (5 for a 1024-item tile) — then a
+// walk over IPT items with the current and previous keys in registers (one LDS round trip per item;
+// the strictly-ascending check compares registers), then the OID compare of the matched pairs with
+// every LDS read issued before any compare.  Outcome per item:
+//   rec = kind << 25 | changed << 24 | jb << 12 | ia          (tile-local indices)
+template <int NT, int IPT>
+__device__ __forceinline__ void tile_walk(const u64* sA, const u64* sB, const TileGeo& q, u32 rec[IPT], bool& bad) {
+    using LD = Join2Lds<NT, IPT>;
+    const int tid = threadIdx.x, na = q.na, nb = q.nb;
     const int nitems = na + nb;
-    const int nbx = nb + (has_la ? 1 : 0);  // B keys in LDS, including the lookahead
+    const int nbx = nb + (q.has_la ? 1 : 0);  // B keys in LDS, including the lookahead
     const int dd = tid * IPT < nitems ? tid * IPT : nitems;
     const int cnt = (dd + IPT < nitems ? dd + IPT : nitems) - dd;
     int lo = dd - nb > 0 ? dd - nb : 0, hi = dd < na ? dd : na;
@@ -276,15 +278,13 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         lo = w > 0 ? nlo : lo;
         hi = w > 0 ? nhi : hi;
     }
-    u32 rec[IPT];
-    bool bad = false;
     {
         int ia = lo, jb = dd - lo;
         const int amax = na > 0 ? na - 1 : 0, bmax = nbx > 0 ? nbx - 1 : 0;
         u64 ka = sA[ia < amax ? ia : amax], kb = sB[jb < bmax ? jb : bmax];
-        bool ap_ok = ia > 0 || has_lbA, bp_ok = jb > 0 || has_lbB;
-        u64 ap = ia > 0 ? sA[ia - 1] : lbA;  // the A / B keys before the walk position
-        u64 bp = jb > 0 ? sB[jb - 1] : lbB;
+        bool ap_ok = ia > 0 || q.has_lbA, bp_ok = jb > 0 || q.has_lbB;
+        u64 ap = sA[ia - 1];  // the A / B keys before the walk position (sA[-1] / sB[-1]: the
+        u64 bp = sB[jb - 1];  // lookbehind keys, staged with the tile; garbage when absent, unused)
 #pragma unroll
         for (int k = 0; k < IPT; k++) {
             const bool act = k < cnt;
@@ -305,47 +305,104 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
             kb = sB[jb < bmax ? jb : bmax];
         }
     }
-    // ---- OID compare of the matched pairs: every LDS read issued before any compare ------------------
-    {
-        u32 x[IPT][5], y[IPT][5];
+}
+
+// OID compare of the matched pairs out of the tile's LDS image, in batches of OB items: every LDS read
+// of a batch issued before its compares (OB bounds the registers held while the persistent kernel
+// also carries the next tile's prefetch)
+template <int IPT>
+__device__ __forceinline__ void tile_oid_lds(const u32* oA, const u32* oB, u32 rec[IPT]) {
+    constexpr int OB = IPT < 2 ? IPT : 2;
 #pragma unroll
-        for (int k = 0; k < IPT; k++) {
-            const bool m = (rec[k] >> 25) == R_MATCH;
-            const u32 ia = m ? rec[k] & 0xFFF : 0, jb = m ? (rec[k] >> 12) & 0xFFF : 0;
+    for (int k0 = 0; k0 < IPT; k0 += OB) {
+        u32 x[OB][5], y[OB][5];
+#pragma unroll
+        for (int k = 0; k < OB; k++) {
+            const bool m = (rec[k0 + k] >> 25) == R_MATCH;
+            const u32 ia = m ? rec[k0 + k] & 0xFFF : 0, jb = m ? (rec[k0 + k] >> 12) & 0xFFF : 0;
 #pragma unroll
             for (int w = 0; w < 5; w++) { x[k][w] = oA[5 * ia + w]; y[k][w] = oB[5 * jb + w]; }
         }
 #pragma unroll
-        for (int k = 0; k < IPT; k++) {
+        for (int k = 0; k < OB; k++) {
             u32 d = 0;
 #pragma unroll
             for (int w = 0; w < 5; w++) d |= x[k][w] ^ y[k][w];
-            if ((rec[k] >> 25) == R_MATCH && d) rec[k] |= 1u << 24;
+            if ((rec[k0 + k] >> 25) == R_MATCH && d) rec[k0 + k] |= 1u << 24;
         }
     }
-    if (g.hash_mode) {
-#pragma unroll
-        for (int k = 0; k < IPT; k++)
-            if ((rec[k] >> 25) == R_MATCH &&
-                !names_eq(g.nameA, g.nameOffA, i0 + (rec[k] & 0xFFF), g.nameB, g.nameOffB, j0 + ((rec[k] >> 12) & 0xFFF)))
-                atomicOr(g.err, 2u);
-    }
-    if (bad) atomicOr(g.err, 1u);
-#if KD_J_EXP == 9
-    T2 = clock64();
-#endif
+}
 
-    // ---- compaction: per item-slot ballots give the wave-local exclusive offsets (thread-major item
-    //      order) with mbcnt — no LDS round trips; one barrier for the wave totals ---------------------
-    const int lane = tid & 63, wid = tid >> 6;
+// OID compare straight from HBM (keys-only LDS image): each thread loads the two 20-B OIDs of its own
+// matched pairs (consecutive items -> neighbouring entries across lanes), all loads issued before any
+// compare
+template <int IPT>
+__device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGeo& q, u32 rec[IPT]) {
+    typedef const __attribute__((address_space(1))) u32* gp32;
+    u32 x[IPT][5], y[IPT][5];
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const bool m = (rec[k] >> 25) == R_MATCH;
+        const gp32 pa = m ? (gp32)(g.oidA + 20 * (q.i0 + (rec[k] & 0xFFF))) : (gp32)g.dummy;
+        const gp32 pb = m ? (gp32)(g.oidB + 20 * (q.j0 + ((rec[k] >> 12) & 0xFFF))) : (gp32)g.dummy;
+#pragma unroll
+        for (int w = 0; w < 5; w++) { x[k][w] = pa[w]; y[k][w] = pb[w]; }
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        u32 d = 0;
+#pragma unroll
+        for (int w = 0; w < 5; w++) d |= x[k][w] ^ y[k][w];
+        if ((rec[k] >> 25) == R_MATCH && d) rec[k] |= 1u << 24;
+    }
+}
+
+template <int NT, int IPT>
+__device__ __forceinline__ void tile_merge(const u64* sA, const u64* sB, const u32* oA, const u32* oB, const TileGeo& q,
+                                           u32 rec[IPT], bool& bad) {
+    tile_walk<NT, IPT>(sA, sB, q, rec, bad);
+    tile_oid_lds<IPT>(oA, oB, rec);
+}
+
+// KD_KEY_HASH: a matched key must also match the full filename (a 64-bit key collision between two
+// different names would otherwise be read as an update)
+template <int IPT>
+__device__ __forceinline__ void tile_names(const Join2Args& g, const TileGeo& q, const u32 rec[IPT]) {
+#pragma unroll
+    for (int k = 0; k < IPT; k++)
+        if ((rec[k] >> 25) == R_MATCH &&
+            !names_eq(g.nameA, g.nameOffA, q.i0 + (rec[k] & 0xFFF), g.nameB, g.nameOffB, q.j0 + ((rec[k] >> 12) & 0xFFF)))
+            atomicOr(g.err, 2u);
+}
+
+// Per-item flag bits (bitwise, not short-circuit: no exec-mask branches), then per item-slot ballots:
+// the wave-local exclusive offsets in thread-major item order come from mbcnt — no LDS round trips —
+// and one barrier exchanges the wave totals.
+struct TileCounts {
+    u32 fd, fu;          // item k is a delta / an update
+    u32 od, ou;          // this thread's first delta / update slot inside the tile
+    u32 tnd, tnu, tdel;  // tile totals: deltas, updates, deletes
+};
+
+template <int NT, int IPT>
+__device__ __forceinline__ TileCounts tile_counts(const u32 rec[IPT], u32* s_wave) {
+    TileCounts c;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    u32 fd = 0, fu = 0, fx = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1;
+        const u32 isx = (u32)(kind == R_DEL), isi = (u32)(kind == R_INS), isu = (u32)(kind == R_MATCH) & chg;
+        fd |= (isx | isi | isu) << k;
+        fu |= isu << k;
+        fx |= isx << k;
+    }
     u32 od = 0, ou = 0, wd = 0, wu = 0, wx = 0;
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
-        const u32 kind = rec[k] >> 25;
-        const bool chg = (rec[k] >> 24) & 1;
-        const u64 bd = __ballot(kind == R_DEL || kind == R_INS || (kind == R_MATCH && chg));
-        const u64 bu = __ballot(kind == R_MATCH && chg);
-        const u64 bx = __ballot(kind == R_DEL);
+        const u64 bd = __ballot((fd >> k) & 1);
+        const u64 bu = __ballot((fu >> k) & 1);
+        const u64 bx = __ballot((fx >> k) & 1);
         od += __builtin_amdgcn_mbcnt_hi((u32)(bd >> 32), __builtin_amdgcn_mbcnt_lo((u32)bd, 0));
         ou += __builtin_amdgcn_mbcnt_hi((u32)(bu >> 32), __builtin_amdgcn_mbcnt_lo((u32)bu, 0));
         wd += __popcll(bd);
@@ -354,24 +411,108 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     }
     if (lane == 0) { s_wave[wid] = wd; s_wave[NT / 64 + wid] = wu; s_wave[2 * NT / 64 + wid] = wx; }
     __syncthreads();
-    u32 tnd = 0, tnu = 0, tot_del = 0;
+    u32 tnd = 0, tnu = 0, tdel = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) {
         const u32 a = s_wave[w], b = s_wave[NT / 64 + w];
         if (w < wid) { od += a; ou += b; }
         tnd += a;
         tnu += b;
-        tot_del += s_wave[2 * NT / 64 + w];
+        tdel += s_wave[2 * NT / 64 + w];
     }
-#if KD_J_EXP == 9
-    T3 = clock64();
+    c.fd = fd; c.fu = fu; c.od = od; c.ou = ou; c.tnd = tnd; c.tnu = tnu; c.tdel = tdel;
+    return c;
+}
+
+template <int IPT>
+__device__ __forceinline__ void tile_write(const u32 rec[IPT], const TileCounts& c, u64 i0, u64 j0,
+                                           uint2* __restrict__ sd, uint2* __restrict__ su) {
+    u32 od = c.od, ou = c.ou;
+    const u32 has_su = su != nullptr;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
+        const u32 isd = (c.fd >> k) & 1, isu = (c.fu >> k) & 1;
+        const uint2 v = make_uint2(kind == R_INS ? KD_NONE : (u32)(i0 + ia), kind == R_DEL ? KD_NONE : (u32)(j0 + jb));
+        if (isd) sd[od] = v;
+        od += isd;
+        if (isu & has_su) su[ou] = v;
+        ou += isu;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_join2: one tile per workgroup (unordered appends, or the staged ordered path)
+// ---------------------------------------------------------------------------------------------
+// The tile is staged in ONE HBM round trip: keys and OIDs of both sides go global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: 16 B per lane, the wave's 64 chunks land contiguously), all issued
+// before any use.
+template <int NT, int IPT, bool UNORD>
+__global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
+    using LD = Join2Lds<NT, IPT>;
+    static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
+    constexpr int NRANGE = KD_J_OIDG ? 2 : 4;  // keys only, or keys + OIDs
+    constexpr int CHK = (8 * (LD::TILE + 1) + 16 + 15) / 16 + 4;  // chunks of the two key ranges
+    __shared__ u32x4 s_ch[KD_J_OIDG ? CHK : LD::CH];  // lanes past the tile's chunks are masked off
+    __shared__ u32 s_wave[3 * NT / 64];
+    __shared__ u64 s_base[2];
+    const int tid = threadIdx.x;
+    const u64 tile = blockIdx.x;
+    const TileGeo q = tile_geo(g, tile, LD::TILE);
+    if (!q.ok && tid == 0) atomicOr(g.err, 1u);
+    const TileRanges r = tile_ranges(g, q);
+    // 64-chunk pieces (one wave-instruction each: wave-uniform source base and LDS base, lane l takes
+    // chunk 64p + l), dealt round-robin to the waves across the four ranges: scalar address math
+    {
+        constexpr int NW = NT / 64;
+        const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+        u32 q0 = 0;
+#pragma unroll
+        for (int k = 0; k < NRANGE; k++) {
+            const Range& R = k == 0 ? r.ka : k == 1 ? r.kb : k == 2 ? r.oa : r.ob;
+            const u32 off = k == 0 ? 0 : k == 1 ? r.c1 : k == 2 ? r.c2 : r.c3;
+            const u32 np = (R.nch + 63) >> 6;
+            for (u32 p = (u32)(wid + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
+                const u32 c = 64 * p + lane;
+                if (c < R.nch)
+                    __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(s_ch + off + 64 * p), 16, 0, 0);
+            }
+            q0 += np;
+        }
+    }
+    __syncthreads();  // vmcnt(0) + barrier: the DMA has landed
+    const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
+    const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
+    const u32* oA = (const u32*)((const u8*)(s_ch + r.c2) + r.oa.skew);  // 4-B aligned: 20*i is
+    const u32* oB = (const u32*)((const u8*)(s_ch + r.c3) + r.ob.skew);  // and allocations are
+#if KD_J_EXP == 1
+    if (tid == 0 && !UNORD) {
+        u32* c = g.tile_cnt + 4 * tile;
+        c[0] = c[1] = c[2] = c[3] = ((const u32*)s_ch)[tid] == 0x12345678u ? 1u : 0u;
+    }
+    return;
 #endif
-    uint2* sd;
-    uint2* su;
+    u32 rec[IPT];
+    bool bad = false;
+#if KD_J_EXP == 2  // profiling: no merge path (records from the item index), OID loads kept
+#pragma unroll
+    for (int k = 0; k < IPT; k++) rec[k] = (R_MATCH << 25) | ((u32)((tid * IPT + k) / 2) << 12) | (u32)((tid * IPT + k) / 2);
+    bad = sA[tid] == 0x123456789ull && sB[tid] == 7;
+#else
+    tile_walk<NT, IPT>(sA, sB, q, rec, bad);
+#endif
+#if KD_J_EXP != 3  // 3: profiling, no OID compare
+    if (KD_J_OIDG) tile_oid_global<IPT>(g, q, rec);
+    else tile_oid_lds<IPT>(oA, oB, rec);
+#endif
+    if (g.hash_mode) tile_names<IPT>(g, q, rec);
+    if (bad) atomicOr(g.err, 1u);
+    const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
+    uint2 *sd, *su;
     if (UNORD) {
         // four lanes of wave 0 reserve in parallel: deltas, updates (offsets) + inserts, deletes
         if (tid < 4) {
-            const u64 v = tid == 0 ? tnd : tid == 1 ? tnu : tid == 2 ? tnd - tnu - tot_del : tot_del;
+            const u64 v = tid == 0 ? c.tnd : tid == 1 ? c.tnu : tid == 2 ? c.tnd - c.tnu - c.tdel : c.tdel;
             const int slot = tid == 0 ? 3 : tid == 1 ? 1 : tid == 2 ? 0 : 2;
             const u64 old = v ? atomicAdd((unsigned long long*)(g.counts + slot), (unsigned long long)v) : 0;
             if (tid < 2) s_base[tid] = old;
@@ -383,46 +524,289 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         sd = g.stage_delta + tile * (u64)C2_STAGE;
         su = g.stage_upd + tile * (u64)C2_STAGE;
     }
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
-        const bool upd = kind == R_MATCH && ((rec[k] >> 24) & 1);
-        const bool del = kind == R_DEL, ins = kind == R_INS;
-        const uint2 v = make_uint2(ins ? KD_NONE : (u32)(i0 + ia), del ? KD_NONE : (u32)(j0 + jb));
-        if (del | ins | upd) sd[od] = v;
-        od += del | ins | upd;
-        if (su && upd) su[ou] = v;
-        ou += upd;
-    }
+    tile_write<IPT>(rec, c, q.i0, q.j0, sd, su);
     if (!UNORD && tid == 0) {
-        u32* c = g.tile_cnt + 4 * tile;
-        const u32 tins = tnd - tnu - tot_del;
-        c[0] = tins;
-        c[1] = tnu;
-        c[2] = tot_del;
-        c[3] = tnd;
-        // group sums (<= 64 tiles x TILE per 32-bit half: no carry between halves); a handful of
-        // atomics per address
+        u32* cc = g.tile_cnt + 4 * tile;
+        const u32 tins = c.tnd - c.tnu - c.tdel;
+        cc[0] = tins;
+        cc[1] = c.tnu;
+        cc[2] = c.tdel;
+        cc[3] = c.tnd;
+        // group sums (<= 64 tiles x TILE per 32-bit half: no carry between halves)
         u64* gs = g.gsum + 2 * (tile / C2_GROUP);
-        atomicAdd((unsigned long long*)gs, (unsigned long long)(tnd | (u64)tnu << 32));
-        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)tot_del << 32));
+        atomicAdd((unsigned long long*)gs, (unsigned long long)(c.tnd | (u64)c.tnu << 32));
+        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)c.tdel << 32));
     }
-#if KD_J_EXP == 9
-    if (tid == 0 && tile % 1009 == 0) {
-        const u64 T4 = clock64();
-        printf("JT tile %llu stage %llu merge %llu scan %llu write %llu total %llu\n", (unsigned long long)tile,
-               (unsigned long long)(T1 - T0), (unsigned long long)(T2 - T1), (unsigned long long)(T3 - T2),
-               (unsigned long long)(T4 - T3), (unsigned long long)(T4 - T0));
-    }
-#endif
 }
 
-// Tile-local staging -> final key-ordered positions; one tile per block.  The tile's output
-// offset = the group sums of all earlier C2_GROUP-tile groups + the counts of the earlier tiles of
-// its own group (at most ngroups + C2_GROUP - 1 loads, issued together); the last block also
-// writes the totals.  Work per block is bounded by one tile, so insert-dense regions do not
-// serialise.
+// ---------------------------------------------------------------------------------------------
+// k_join2r: run merge — one tile per workgroup, each wave walks its own 256-item stretch in runs
+// ---------------------------------------------------------------------------------------------
+// The merge path of a diff is almost all matched pairs, broken by short runs of inserts or deletes.
+// A wave therefore does not search a split for every lane: it walks its stretch in rounds, lane l
+// looking at A[a+l] and B[b+l] at once —
+//   pair round: the leading lanes with equal keys are matched pairs (OIDs compared from LDS, changed
+//               ones emitted), a and b advance by that count;
+//   run round:  (first keys differ) the leading lanes of A below B[b] are deletes, or of B below A[a]
+//               inserts, emitted and skipped in one step.
+// A 1 %-edit stretch of 256 items takes ~6 rounds of one LDS read pair + ballots each.  A stretch
+// still unfinished after RMAX rounds (dense interleaved edits) is finished by the per-lane merge path
+// (search + walk) restricted to what is left.  Records go to the wave's own slot (256 records) of the
+// tile's staging area, in key order; k_place2 concatenates the four slots.
+constexpr int RW = 256;   // merge-path items per wave stretch
+#ifndef KD_RMAX
+#define KD_RMAX 24        // run rounds before the per-lane fallback
+#endif
+
+// 64-lane 64-ary merge-path search over the tile's LDS keys (2 rounds for a 1024-item tile)
+__device__ __forceinline__ int mp_search_lds64(const u64* sA, const u64* sB, int d, int lo, int hi) {
+    const int lane = threadIdx.x & 63;
+    while (hi > lo) {
+        const int step = (hi - lo + 63) >> 6;
+        const int probe = lo + step * (lane + 1) - 1;
+        const int pc = probe < hi ? probe : hi - 1;
+        const bool p = probe >= hi || sA[pc] > sB[d - 1 - pc];
+        const u64 bal = __ballot(p);
+        if (bal == 0) return hi;
+        const int f = __ffsll((long long)bal) - 1;
+        const int nh = lo + step * (f + 1) - 1;
+        lo = lo + step * f;
+        hi = nh < hi ? nh : hi;
+        if (step == 1) return hi;
+    }
+    return lo;
+}
+
+// Per-lane merge path (search + register walk) over what is left of a wave's stretch:
+// A [a, ae), B [b, be) (tile-local; B keys readable up to nbx, the tile's lookahead included).
+// Item outcome records as in tile_walk.
+template <int IPT>
+__device__ __forceinline__ void wave_walk(const u64* sA, const u64* sB, int a, int ae, int b, int be, int nbx,
+                                          bool has_lbA, u32 rec[IPT]) {
+    const int lane = threadIdx.x & 63;
+    const int na = ae - a, nb = be - b, nitems = na + nb;
+    const int dd = lane * IPT < nitems ? lane * IPT : nitems;
+    const int cnt = (dd + IPT < nitems ? dd + IPT : nitems) - dd;
+    int lo = dd - nb > 0 ? dd - nb : 0, hi = dd < na ? dd : na;
+    while (lo < hi) {  // binary search: this path only runs for dense-edit stretches
+        const int mid = (lo + hi) >> 1;
+        if (sA[a + mid] <= sB[b + dd - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    int ia = a + lo, jb = b + dd - lo;
+    const bool ap_ok0 = ia > 0 || has_lbA;
+    u64 ap = sA[ia - 1];
+    bool ap_ok = ap_ok0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        rec[k] = R_NONE << 25;
+        if (k < cnt) {
+            const u64 ka = ia < ae ? sA[ia] : ~0ull, kb = jb < nbx ? sB[jb] : ~0ull;
+            if (jb >= be || (ia < ae && ka <= kb)) {
+                const bool m = jb < nbx && kb == ka;
+                rec[k] = ((m ? R_MATCH : R_DEL) << 25) | ((u32)jb << 12) | (u32)ia;
+                ap = ka;
+                ap_ok = true;
+                ia++;
+            } else {
+                const bool partner = ap_ok && ap == kb;
+                rec[k] = ((partner ? R_NONE : R_INS) << 25) | ((u32)jb << 12) | (u32)ia;
+                jb++;
+            }
+        }
+    }
+}
+
 template <int NT>
+__global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
+    using LD = Join2Lds<NT, 4>;
+    constexpr int NW = NT / 64;
+    static_assert(LD::TILE == NW * RW, "one 256-item stretch per wave");
+    constexpr int NRANGE = KD_J_OIDG ? 2 : 4;  // keys only (OIDs compared from HBM), or keys + OIDs
+    constexpr int CHK = (8 * (LD::TILE + 1) + 16 + 15) / 16 + 4;
+    __shared__ u32x4 s_ch[KD_J_OIDG ? CHK : LD::CH];
+    __shared__ int s_split[NW + 1];
+    __shared__ u32 s_cnt[NW][4];  // per wave: deltas, updates, deletes, inserts
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 tile = blockIdx.x;
+    const TileGeo q = tile_geo(g, tile, LD::TILE);
+    if (!q.ok && tid == 0) atomicOr(g.err, 1u);
+    const TileRanges r = tile_ranges(g, q);
+    {  // LDS-DMA staging: 64-chunk pieces dealt round-robin to the waves (see k_join2)
+        const int w = __builtin_amdgcn_readfirstlane(wid);
+        u32 q0 = 0;
+#pragma unroll
+        for (int k = 0; k < NRANGE; k++) {
+            const Range& R = k == 0 ? r.ka : k == 1 ? r.kb : k == 2 ? r.oa : r.ob;
+            const u32 off = k == 0 ? 0 : k == 1 ? r.c1 : k == 2 ? r.c2 : r.c3;
+            const u32 np = (R.nch + 63) >> 6;
+            for (u32 p = (u32)(w + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
+                const u32 c = 64 * p + lane;
+                if (c < R.nch)
+                    __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(s_ch + off + 64 * p), 16, 0, 0);
+            }
+            q0 += np;
+        }
+    }
+    __syncthreads();
+    const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
+    const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
+    const u32* oA = (const u32*)((const u8*)(s_ch + r.c2) + r.oa.skew);
+    const u32* oB = (const u32*)((const u8*)(s_ch + r.c3) + r.ob.skew);
+    const int na = q.na, nb = q.nb, nitems = na + nb, nbx = nb + (q.has_la ? 1 : 0);
+
+    // ---- strictly ascending keys (independent reads, off every chain) ----
+    bool bad = false;
+    for (int c = tid; c < na; c += NT) bad |= (c > 0 || q.has_lbA) && sA[c - 1] >= sA[c];
+    for (int c = tid; c < nb; c += NT) bad |= (c > 0 || q.has_lbB) && sB[c - 1] >= sB[c];
+    if (bad) atomicOr(g.err, 1u);
+
+    // ---- the stretch splits: wave w >= 1 finds the split at item w*RW ----
+    if (tid == 0) { s_split[0] = 0; s_split[NW] = na; }
+    if (wid >= 1) {
+        const int d = wid * RW < nitems ? wid * RW : nitems;
+        const int sp = mp_search_lds64(sA, sB, d, d - nb > 0 ? d - nb : 0, d < na ? d : na);
+        if (lane == 0) s_split[wid] = sp;
+    }
+    __syncthreads();
+    int a = __builtin_amdgcn_readfirstlane(s_split[wid]);  // wave-uniform walk state: SGPRs
+    const int ae = __builtin_amdgcn_readfirstlane(s_split[wid + 1]);
+    const int d0 = wid * RW < nitems ? wid * RW : nitems, d1 = (wid + 1) * RW < nitems ? (wid + 1) * RW : nitems;
+    int b = d0 - a;
+    const int be = d1 - ae;
+    // the stretch's first B may be the partner of the A just before it (matched there)
+    if (b < be && (a > 0 || q.has_lbA) && sA[a - 1] == sB[b]) b++;
+
+    uint2* sd = g.stage_delta + tile * (u64)C2_STAGE + wid * RW;
+    uint2* su = g.stage_upd + tile * (u64)C2_STAGE + wid * RW;
+    const u32 i0 = (u32)q.i0, j0 = (u32)q.j0;
+    const u64 lt = (1ull << lane) - 1;  // lanes below this one
+    u32 cd = 0, cu = 0, cx = 0, ci = 0;
+    const int amax = na > 0 ? na - 1 : 0, bmax = nbx > 0 ? nbx - 1 : 0;
+    for (int round = 0; round < KD_RMAX && (a < ae || b < be); round++) {
+        const int la = a + lane, lb = b + lane;
+        const bool ina = la < ae, inb = lb < nbx;
+        const u64 ka = sA[la < amax ? la : amax], kb = sB[lb < bmax ? lb : bmax];
+        const u64 ne = __ballot(!(ina && inb && ka == kb));
+        const int f = ne ? __ffsll((long long)ne) - 1 : 64;  // leading matched pairs
+        if (f > 0) {
+            u32 d = 0;
+            if (lane < f) {
+                if (KD_J_OIDG) {
+                    typedef const __attribute__((address_space(1))) u32* gp32;
+                    const gp32 pa = (gp32)(g.oidA + 20 * (q.i0 + la)), pb = (gp32)(g.oidB + 20 * (q.j0 + lb));
+                    u32 x[5], y[5];
+#pragma unroll
+                    for (int w = 0; w < 5; w++) { x[w] = pa[w]; y[w] = pb[w]; }
+#pragma unroll
+                    for (int w = 0; w < 5; w++) d |= x[w] ^ y[w];
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 5; w++) d |= oA[5 * la + w] ^ oB[5 * lb + w];
+                }
+            }
+            if (g.hash_mode && lane < f &&
+                !names_eq(g.nameA, g.nameOffA, q.i0 + la, g.nameB, g.nameOffB, q.j0 + lb))
+                atomicOr(g.err, 2u);
+            const bool chg = lane < f && d != 0;
+            const u64 bc = __ballot(chg);
+            if (chg) {
+                const u32 pos = (u32)__popcll(bc & lt);
+                const uint2 v = make_uint2(i0 + la, j0 + lb);
+                sd[cd + pos] = v;
+                su[cu + pos] = v;
+            }
+            cd += (u32)__popcll(bc);
+            cu += (u32)__popcll(bc);
+            a += f;
+            b += f;
+            continue;
+        }
+        // lane 0 differs: a run of deletes (A below B[b]) or of inserts (B below A[a])
+        const u64 kb0 = b < nbx ? sB[b] : ~0ull;  // B[be] is the lookahead: an A below it is a delete
+        if (a < ae && sA[a] < kb0) {
+            const u64 nd = __ballot(!(ina && ka < kb0));
+            const int run = nd ? __ffsll((long long)nd) - 1 : 64;
+            if (lane < run) sd[cd + lane] = make_uint2(i0 + la, KD_NONE);
+            cd += run;
+            cx += run;
+            a += run;
+        } else {
+            const u64 ka0 = a < ae ? sA[a] : ~0ull;
+            const u64 ni = __ballot(!(lb < be && kb < ka0));
+            const int run = ni ? __ffsll((long long)ni) - 1 : 64;
+            if (lane < run) sd[cd + lane] = make_uint2(KD_NONE, j0 + lb);
+            cd += run;
+            ci += run;
+            b += run;
+        }
+    }
+    if (a < ae || b < be) {  // dense edits: the per-lane merge path finishes the stretch
+        if (b > be) b = be;    // (only on unsorted input, already flagged: keeps the walk in bounds)
+        u32 rec[4];
+        wave_walk<4>(sA, sB, a, ae, b, be, nbx, q.has_lbA, rec);
+        if (KD_J_OIDG) tile_oid_global<4>(g, q, rec);
+        else tile_oid_lds<4>(oA, oB, rec);
+        if (g.hash_mode) tile_names<4>(g, q, rec);
+        TileCounts c;
+        c.fd = c.fu = 0;
+        u32 fx = 0, fi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1;
+            const u32 isx = (u32)(kind == R_DEL), isi = (u32)(kind == R_INS), isu = (u32)(kind == R_MATCH) & chg;
+            c.fd |= (isx | isi | isu) << k;
+            c.fu |= isu << k;
+            fx |= isx << k;
+            fi |= isi << k;
+        }
+        // thread-major item order: this lane's records follow every record of the lanes below it
+        u32 od = 0, ou = 0, wd = 0, wu = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u64 bd = __ballot((c.fd >> k) & 1), bu = __ballot((c.fu >> k) & 1);
+            od += (u32)__popcll(bd & lt);
+            ou += (u32)__popcll(bu & lt);
+            wd += (u32)__popcll(bd);
+            wu += (u32)__popcll(bu);
+            cx += (u32)__popcll(__ballot((fx >> k) & 1));
+            ci += (u32)__popcll(__ballot((fi >> k) & 1));
+        }
+        c.od = cd + od;
+        c.ou = cu + ou;
+        tile_write<4>(rec, c, i0, j0, sd, su);
+        cd += wd;
+        cu += wu;
+    }
+    if (lane == 0) { s_cnt[wid][0] = cd; s_cnt[wid][1] = cu; s_cnt[wid][2] = cx; s_cnt[wid][3] = ci; }
+    __syncthreads();
+    if (tid == 0) {
+        u32 td = 0, tu = 0, tx = 0, tn = 0, packed[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            td += s_cnt[w][0]; tu += s_cnt[w][1]; tx += s_cnt[w][2]; tn += s_cnt[w][3];
+            packed[w] = s_cnt[w][0] | s_cnt[w][1] << 16;
+        }
+        *(uint4*)(g.tile_cnt + 4 * tile) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+        u64* gs = g.gsum + 2 * (tile / C2_GROUP);
+        atomicAdd((unsigned long long*)gs, (unsigned long long)(td | (u64)tu << 32));
+        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tn | (u64)tx << 32));
+    }
+}
+
+// Staged path: tile-local staging -> final key-ordered positions; one tile per block.  The tile's
+// output offset = the group sums of all earlier C2_GROUP-tile groups + the counts of the earlier
+// tiles of its own group; the last block also writes the totals.
+// WS (k_join2r): a tile's records sit in NW wave slots of RW records, tile_cnt holds per wave
+// deltas | updates << 16; otherwise one contiguous slot and tile_cnt = inserts, updates, deletes, deltas.
+template <bool WS>
+__device__ __forceinline__ uint2 tile_du(const uint4 c) {  // (deltas, updates) of one tile
+    if (!WS) return make_uint2(c.w, c.y);
+    const u32 s = c.x + c.y + c.z + c.w;  // <= 1024 per half: no carry
+    return make_uint2(s & 0xFFFF, s >> 16);
+}
+
+template <int NT, bool WS>
 __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
                                                const u32* __restrict__ tile_cnt, const u64* __restrict__ gsum,
                                                u64 ntiles, int tile_items, uint2* __restrict__ out_delta,
@@ -443,14 +827,14 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
             if (k >= grp) { pd += a & 0xFFFFFFFFu; pu += a >> 32; }  // totals: all groups
         }
     }
-    // counts of the earlier tiles of this group (the last block already has them in the totals)
     const u64 t_lo = grp * C2_GROUP;
     if (!last && tid < (int)(t - t_lo)) {
-        const uint4 c = *(const uint4*)(tile_cnt + 4 * (t_lo + tid));
-        pd += c.w;
+        const uint2 c = tile_du<WS>(*(const uint4*)(tile_cnt + 4 * (t_lo + tid)));
+        pd += c.x;
         pu += c.y;
     }
-    const uint4 own = *(const uint4*)(tile_cnt + 4 * t);
+    const uint4 ownc = *(const uint4*)(tile_cnt + 4 * t);
+    const uint2 own = tile_du<WS>(ownc);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         pd += __shfl_xor(pd, o, 64); pu += __shfl_xor(pu, o, 64);
@@ -462,7 +846,6 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) { pd += s_red[0][w]; pu += s_red[1][w]; }
     if (last) {
-        // pd/pu are the totals here; this tile's records start at total - own count
         if (tid == 0) {
             u64 ti = 0, tx = 0;
 #pragma unroll
@@ -472,29 +855,40 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
             counts[2] = tx;
             counts[3] = pd;
         }
-        pd -= own.w;
+        pd -= own.x;
         pu -= own.y;
     }
     const uint2* sdp = stage_delta + t * (u64)tile_items;
     const uint2* sup = stage_upd + t * (u64)tile_items;
-    // C2_TILE / NT records per thread at most: every load before any store
+    // record r of the tile -> its staging slot (WS: the wave slot holding it)
+    u32 d1 = 0, d2 = 0, d3 = 0, u1 = 0, u2 = 0, u3 = 0;
+    if (WS) {
+        d1 = ownc.x & 0xFFFF; d2 = d1 + (ownc.y & 0xFFFF); d3 = d2 + (ownc.z & 0xFFFF);
+        u1 = ownc.x >> 16; u2 = u1 + (ownc.y >> 16); u3 = u2 + (ownc.z >> 16);
+    }
+    auto slot = [&](u32 r, u32 p1, u32 p2, u32 p3) -> u32 {
+        if (!WS) return r;
+        const u32 w = (u32)(r >= p1) + (u32)(r >= p2) + (u32)(r >= p3);
+        const u32 base = w == 0 ? 0 : w == 1 ? p1 : w == 2 ? p2 : p3;
+        return w * RW + (r - base);
+    };
     constexpr int UC = C2_TILE / NT;
     uint2 v[UC];
 #pragma unroll
     for (int j = 0; j < UC; j++) {
         const u32 r = j * NT + tid;
-        if (r < own.w) v[j] = sdp[r];
+        if (r < own.x) v[j] = sdp[slot(r, d1, d2, d3)];
     }
 #pragma unroll
     for (int j = 0; j < UC; j++) {
         const u32 r = j * NT + tid;
-        if (r < own.w) out_delta[pd + r] = v[j];
+        if (r < own.x) out_delta[pd + r] = v[j];
     }
     if (out_upd) {
 #pragma unroll
         for (int j = 0; j < UC; j++) {
             const u32 r = j * NT + tid;
-            if (r < own.y) v[j] = sup[r];
+            if (r < own.y) v[j] = sup[slot(r, u1, u2, u3)];
         }
 #pragma unroll
         for (int j = 0; j < UC; j++) {
@@ -504,11 +898,171 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_join2p: persistent, register-prefetched tiles, decoupled look-back
+// ---------------------------------------------------------------------------------------------
+// Look-back descriptors, two words per tile (own flag each, looked back independently):
+//   word 0 = flag << 62 | deltas << 31 | updates,   word 1 = flag << 62 | deletes
+// flag 0 = not yet, 1 = the tile's own counts (aggregate), 2 = inclusive prefix through the tile.
+// Fields are 31 bits (side sizes are checked on the host), so payloads add without carries.
+constexpr u64 LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_PAY = (1ull << 62) - 1;
+
+__device__ __forceinline__ void lb_store(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ u64 lb_load(u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Wave 0 of the tile's workgroup: publish the aggregates, walk back over earlier tiles' descriptors
+// (32 at a time per word, lanes 0-31 word 0 and lanes 32-63 word 1) until an inclusive prefix is
+// found, publish the tile's own inclusive prefix; returns the exclusive payload of this lane's word.
+// Every workgroup is resident (the grid is sized by occupancy) and tiles are taken in increasing
+// order, so every predecessor's descriptor is eventually published.
+__device__ __forceinline__ u64 lookback(u64* __restrict__ desc, u64 ntiles, u64 t, u64 agg0, u64 agg1) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
+    u64* D = desc + (u64)h * ntiles;
+    const u64 agg = h ? agg1 : agg0;
+    if (l == 0) lb_store(D + t, (t == 0 ? LB_INC : LB_AGG) | agg);
+    u64 excl = 0;
+    bool done = t == 0;
+    i64 pos = (i64)t - 1;
+    while (true) {
+        const bool act = !done;
+        if (__ballot(act) == 0) break;
+        u64 v = LB_INC;  // before tile 0: an inclusive prefix of zero
+        const i64 idx = pos - l;
+        if (act && idx >= 0) v = lb_load(D + idx);
+        const u32 f = (u32)(v >> 62);
+        const u32 mx = (u32)(__ballot(act && f == 0) >> (32 * h));
+        const u32 mp = (u32)(__ballot(act && f == 2) >> (32 * h));
+        const int fp = mp ? __ffs(mp) - 1 : 32, fx = mx ? __ffs(mx) - 1 : 32;
+        const bool take_all = mp == 0 && mx == 0;  // 32 aggregates: add them and look further back
+        const bool finish = mp != 0 && fp < fx;    // aggregates up to an inclusive prefix
+        u64 s = (act && (take_all || (finish && l <= fp))) ? (v & LB_PAY) : 0;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);  // sum within the 32-lane half
+        if (act && (take_all || finish)) excl += s;
+        if (act && finish) done = true;
+        if (act && take_all) pos -= 32;
+        if (act && !take_all && !finish) __builtin_amdgcn_s_sleep(1);  // a predecessor not published yet
+    }
+    if (l == 0) lb_store(D + t, LB_INC | (excl + agg));
+    return excl;
+}
+
+template <int NT, int IPT, bool LOOKBACK>
+__global__ __launch_bounds__(NT, KD_J2P_WAVES) void k_join2p(Join2Args g) {
+    using LD = Join2Lds<NT, IPT>;
+    static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
+    constexpr int R = LD::ROUNDS;
+    __shared__ u32x4 s_ch[LD::CH];
+    __shared__ u32 s_wave[3 * NT / 64];
+    __shared__ u64 s_excl[2];
+    const int tid = threadIdx.x;
+    const u64 ntiles = g.ntiles, stride = gridDim.x;
+    u64 t = blockIdx.x;
+    if (t >= ntiles) return;
+
+    // chunk k*NT + tid of the tile's LDS image -> its source address (per-range origin by selects)
+    u32x4 v[R];
+    auto issue = [&](const TileRanges& r) {
+        const u64 ob = r.kb.base - 16ull * r.c1, oa2 = r.oa.base - 16ull * r.c2, ob2 = r.ob.base - 16ull * r.c3;
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const u32 c = k * NT + tid;
+            const u64 org = c < r.c1 ? r.ka.base : c < r.c2 ? ob : c < r.c3 ? oa2 : ob2;
+            const u64 src = c < r.c4 ? org + 16ull * c : (u64)g.dummy;
+            v[k] = *(gp_x4)src;
+        }
+    };
+    auto land = [&](const TileRanges& r) {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const u32 c = k * NT + tid;
+            if (c < r.c4) s_ch[c] = v[k];
+        }
+    };
+    TileGeo q = tile_geo(g, t, LD::TILE);
+    TileRanges r = tile_ranges(g, q);
+    issue(r);
+    land(r);
+    __syncthreads();
+    // split points of the tile after next: loaded one iteration early, consumed after a tile's work
+    typedef const __attribute__((address_space(1))) u64* gp64;
+    u64 pn0 = 0, pn1 = 0;
+    if (t + stride < ntiles) { pn0 = ((gp64)g.part)[t + stride]; pn1 = ((gp64)g.part)[t + stride + 1]; }
+    for (;;) {
+        // ---- prefetch the next tile into registers (in flight during this tile's work) ----
+        const u64 tn = t + stride;
+        TileGeo qn = q;
+        TileRanges rn = r;
+        if (tn < ntiles) {
+            qn = tile_geo_from(g, tn, LD::TILE, pn0, pn1);
+            rn = tile_ranges(g, qn);
+            issue(rn);
+            const u64 tnn = tn + stride;
+            if (tnn < ntiles) { pn0 = ((gp64)g.part)[tnn]; pn1 = ((gp64)g.part)[tnn + 1]; }
+        }
+        // ---- this tile, out of LDS ----
+        const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
+        const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
+        const u32* oA = (const u32*)((const u8*)(s_ch + r.c2) + r.oa.skew);
+        const u32* oB = (const u32*)((const u8*)(s_ch + r.c3) + r.ob.skew);
+        u32 rec[IPT];
+        bool bad = !q.ok;
+        tile_merge<NT, IPT>(sA, sB, oA, oB, q, rec, bad);
+        if (g.hash_mode) tile_names<IPT>(g, q, rec);
+        if (bad) atomicOr(g.err, 1u);
+        const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
+        if (LOOKBACK) {
+            // ---- global offsets: decoupled look-back (wave 0) ----
+            if (tid < 64) {
+                const u64 ex = lookback(g.desc, ntiles, t, ((u64)c.tnd << 31) | c.tnu, (u64)c.tdel);
+                if ((tid & 31) == 0) s_excl[tid >> 5] = ex;
+                const u64 ex1 = __shfl(ex, 32, 64);
+                if (t == ntiles - 1 && tid == 0) {  // the last tile knows the totals
+                    const u64 nd = (ex >> 31) + c.tnd, nu = (ex & 0x7FFFFFFFull) + c.tnu, nx = ex1 + c.tdel;
+                    g.counts[0] = nd - nu - nx;
+                    g.counts[1] = nu;
+                    g.counts[2] = nx;
+                    g.counts[3] = nd;
+                }
+            }
+            __syncthreads();
+            const u64 e0 = s_excl[0];
+            tile_write<IPT>(rec, c, q.i0, q.j0, g.out_delta + (e0 >> 31),
+                            g.out_upd ? g.out_upd + (e0 & 0x7FFFFFFFull) : nullptr);
+        } else {
+            // ---- tile-local staging slots + counts; k_place2 moves them to their final positions ----
+            tile_write<IPT>(rec, c, q.i0, q.j0, g.stage_delta + t * (u64)C2_STAGE, g.stage_upd + t * (u64)C2_STAGE);
+            if (tid == 0) {
+                u32* cc = g.tile_cnt + 4 * t;
+                const u32 tins = c.tnd - c.tnu - c.tdel;
+                cc[0] = tins;
+                cc[1] = c.tnu;
+                cc[2] = c.tdel;
+                cc[3] = c.tnd;
+                u64* gs = g.gsum + 2 * (t / C2_GROUP);
+                atomicAdd((unsigned long long*)gs, (unsigned long long)(c.tnd | (u64)c.tnu << 32));
+                atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)c.tdel << 32));
+            }
+        }
+        if (tn >= ntiles) break;
+        // ---- the prefetched tile -> LDS (after every wave is done with this one) ----
+        __syncthreads();
+        land(rn);
+        __syncthreads();
+        t = tn;
+        q = qn;
+        r = rn;
+    }
+}
+
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
                  u64* d_counts, u32* d_err) {
     const bool unord = (flags & KD_DIFF_UNORDERED) != 0;
+    const bool lookb = !unord && KD_C2_MODE == 2;  // persistent + decoupled look-back (profiling)
+    const bool staged = !unord && !lookb;         // tile-local staging + k_place2 (default)
     const u64 nA = A->n, nB = B->n, total = nA + nB;
     KD_CHECK(nA < 0xFFFFFFFFull && nB < 0xFFFFFFFFull, "diff2: side too large for uint32 indices");
+    KD_CHECK(!lookb || total < (1ull << 31), "diff2: look-back mode needs base.n + target.n < 2^31");
     const bool hash = A->key_mode == KD_KEY_HASH || B->key_mode == KD_KEY_HASH;
     KD_CHECK(A->key_mode == B->key_mode, "diff2: key modes differ");
     if (hash) KD_CHECK((nA == 0 || (A->name && A->name_off)) && (nB == 0 || (B->name && B->name_off)),
@@ -519,17 +1073,22 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
         return KD_OK;
     }
-    void *part, *tcnt, *sdel, *supd, *gsum = nullptr;
-    const u64 n_gsum = unord ? 0 : 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
+    void *part, *tcnt = nullptr, *sdel = nullptr, *supd = nullptr, *gsum = nullptr, *desc = nullptr;
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
-    if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
-    if (n_gsum && (rc = ensure(ctx, "c2.gsum", n_gsum * sizeof(u64), &gsum))) return rc;
-    if (!unord) {
+    u64* zero = nullptr;
+    u64 n_zero = 0;
+    if (staged) {
+        n_zero = 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
+        if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
+        if ((rc = ensure(ctx, "c2.gsum", n_zero * sizeof(u64), &gsum))) return rc;
         if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_STAGE * sizeof(uint2), &sdel))) return rc;
         if ((rc = ensure(ctx, "c2.supd", ntiles * C2_STAGE * sizeof(uint2), &supd))) return rc;
-    } else {
-        sdel = supd = nullptr;
+        zero = (u64*)gsum;
+    } else if (lookb) {
+        n_zero = 2 * ntiles;
+        if ((rc = ensure(ctx, "c2.desc", n_zero * sizeof(u64), &desc))) return rc;
+        zero = (u64*)desc;
     }
     void* dz;
     if ((rc = device_zeros(ctx, &dz))) return rc;
@@ -539,7 +1098,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     rc = launch(ctx, "k_partition2", [&] {
         unsigned nb = (unsigned)((ntiles + C2_PG - 1) / C2_PG);
         hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(256), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part,
-                           d_counts, d_err, (u64*)gsum, n_gsum);
+                           d_counts, d_err, zero, n_zero);
     });
     if (rc) return rc;
     Join2Args g;
@@ -548,24 +1107,53 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.part = (const u64*)part;
     g.nameA = A->name; g.nameOffA = A->name_off; g.nameB = B->name; g.nameOffB = B->name_off;
     g.hash_mode = hash ? 1 : 0;
+    g.dummy = (const u8*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
     g.tile_cnt = (u32*)tcnt; g.gsum = (u64*)gsum; g.err = d_err;
     g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd; g.counts = d_counts;
+    g.desc = (u64*)desc;
+    g.ntiles = ntiles;
     if (unord) {
         return launch(ctx, "k_join2", [&] {
             hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
         });
     }
-    rc = launch(ctx, "k_join2", [&] {
-        hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+    const bool ws = KD_C2_MODE == 3;
+    if (ws) {  // run merge, per-wave slots
+        rc = launch(ctx, "k_join2", [&] {
+            hipLaunchKernelGGL((k_join2r<C2_NT>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+        });
+    } else if (KD_C2_MODE == 1) {  // one tile per workgroup, LDS-DMA staging
+        rc = launch(ctx, "k_join2", [&] {
+            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+        });
+    } else {
+        // persistent: every workgroup resident at once (grid from the occupancy of this kernel)
+        const void* kern = lookb ? (const void*)k_join2p<C2_NT, C2_IPT, true> : (const void*)k_join2p<C2_NT, C2_IPT, false>;
+        if (ctx->occ_join2p <= 0) {
+            int nb = 0;
+            KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, C2_NT, 0));
+            ctx->occ_join2p = nb > 0 ? nb : 1;
+        }
+        const u64 grid = std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)ctx->occ_join2p);
+        rc = launch(ctx, "k_join2", [&] {
+            if (lookb)
+                hipLaunchKernelGGL((k_join2p<C2_NT, C2_IPT, true>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
+            else
+                hipLaunchKernelGGL((k_join2p<C2_NT, C2_IPT, false>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
+        });
+    }
+    if (rc || lookb) return rc;
+    return launch(ctx, "k_place2", [&] {
+        if (ws)
+            hipLaunchKernelGGL((k_place2<KD_PLACE_NT, true>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
+                               (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles,
+                               (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, d_counts);
+        else
+            hipLaunchKernelGGL((k_place2<KD_PLACE_NT, false>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
+                               (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles,
+                               (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, d_counts);
     });
-    if (rc) return rc;
-    rc = launch(ctx, "k_place2", [&] {
-        hipLaunchKernelGGL((k_place2<KD_PLACE_NT>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream, (const uint2*)sdel,
-                           (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles, C2_STAGE, (uint2*)d_delta,
-                           (uint2*)d_upd, d_counts);
-    });
-    return rc;
 }
 
 }  // namespace kd
