@@ -37,6 +37,9 @@ constexpr u64 C2_STAGE = C2_TILE + KD_C2_STAGE_PAD;
 #ifndef KD_C2_MODE
 #define KD_C2_MODE 1  // ordered path: 1 per-tile k_join2 + k_place2, 0 persistent k_join2p + k_place2, 2 look-back
 #endif
+#ifndef KD_J_CLOCK
+#define KD_J_CLOCK 0  // profiling builds: run-merge phase stamps in the staging pad + one report line
+#endif
 #ifndef KD_J_EXP
 #define KD_J_EXP 0  // profiling builds only: 1 = staging only (k_join2)
 #endif
@@ -310,8 +313,8 @@ __device__ __forceinline__ void tile_walk(const u64* sA, const u64* sB, const Ti
 // OID compare of the matched pairs out of the tile's LDS image, in batches of OB items: every LDS read
 // of a batch issued before its compares (OB bounds the registers held while the persistent kernel
 // also carries the next tile's prefetch)
-template <int IPT>
-__device__ __forceinline__ void tile_oid_lds(const u32* oA, const u32* oB, u32 rec[IPT]) {
+template <int IPT, typename P = const u32*>
+__device__ __forceinline__ void tile_oid_lds(P oA, P oB, u32 rec[IPT]) {
     constexpr int OB = IPT < 2 ? IPT : 2;
 #pragma unroll
     for (int k0 = 0; k0 < IPT; k0 += OB) {
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
 // still unfinished after RMAX rounds (dense interleaved edits) is finished by the per-lane merge path
 // (search + walk) restricted to what is left.  Records go to the wave's own slot (256 records) of the
 // tile's staging area, in key order; k_place2 concatenates the four slots.
-constexpr int RW = 256;   // merge-path items per wave stretch
+constexpr int RW = 64 * C2_IPT;  // merge-path items per wave stretch (one tile: NT/64 stretches)
 #ifndef KD_RMAX
 #define KD_RMAX 24        // run rounds before the per-lane fallback
 #endif
@@ -617,49 +620,104 @@ __device__ __forceinline__ void wave_walk(const u64* sA, const u64* sB, int a, i
     }
 }
 
+// Run-merge LDS image: keys and OIDs in separate arrays (distinct alias scopes: the waitcnt pass then
+// knows a key read cannot overlap an OID LDS-DMA still in flight, and inserts no vmcnt wait for it)
 template <int NT>
-__global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
-    using LD = Join2Lds<NT, 4>;
+struct RunLds {
+    static constexpr int TILE = NT * C2_IPT;
+    static constexpr int CHK = (8 * (TILE + 3) + 15) / 16 + 4;   // A + lookbehind, B + lookbehind + lookahead
+    static constexpr int CHO = (20 * (TILE + 1) + 15) / 16 + 4;  // A, B + lookahead
+};
+
+// LDS-DMA staging of one tile: wave 0 issues the key pieces (then waits for them alone), waves 1.. the
+// OID pieces, dealt round-robin.  Issue only.
+template <int NT>
+__device__ __forceinline__ void run_stage(const TileRanges& r, u32x4* s_key, u32x4* s_oid) {
     constexpr int NW = NT / 64;
-    static_assert(LD::TILE == NW * RW, "one 256-item stretch per wave");
-    constexpr int NRANGE = KD_J_OIDG ? 2 : 4;  // keys only (OIDs compared from HBM), or keys + OIDs
-    constexpr int CHK = (8 * (LD::TILE + 1) + 16 + 15) / 16 + 4;
-    __shared__ u32x4 s_ch[KD_J_OIDG ? CHK : LD::CH];
-    __shared__ int s_split[NW + 1];
-    __shared__ u32 s_cnt[NW][4];  // per wave: deltas, updates, deletes, inserts
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const u64 tile = blockIdx.x;
-    const TileGeo q = tile_geo(g, tile, LD::TILE);
-    if (!q.ok && tid == 0) atomicOr(g.err, 1u);
-    const TileRanges r = tile_ranges(g, q);
-    {  // LDS-DMA staging: 64-chunk pieces dealt round-robin to the waves (see k_join2)
-        const int w = __builtin_amdgcn_readfirstlane(wid);
-        u32 q0 = 0;
+    static_assert(NW >= 2, "one key wave + at least one OID wave");
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w == 0) {
 #pragma unroll
-        for (int k = 0; k < NRANGE; k++) {
-            const Range& R = k == 0 ? r.ka : k == 1 ? r.kb : k == 2 ? r.oa : r.ob;
-            const u32 off = k == 0 ? 0 : k == 1 ? r.c1 : k == 2 ? r.c2 : r.c3;
-            const u32 np = (R.nch + 63) >> 6;
-            for (u32 p = (u32)(w + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
+        for (int k = 0; k < 2; k++) {
+            const Range& R = k == 0 ? r.ka : r.kb;
+            u32x4* dst = s_key + (k == 0 ? 0 : r.c1);
+            for (u32 p = 0; 64 * p < R.nch; p++) {
                 const u32 c = 64 * p + lane;
-                if (c < R.nch)
-                    __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(s_ch + off + 64 * p), 16, 0, 0);
+                if (c < R.nch) __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(dst + 64 * p), 16, 0, 0);
             }
-            q0 += np;
+        }
+    } else {
+        const u32 npa = (r.oa.nch + 63) >> 6, np = npa + ((r.ob.nch + 63) >> 6);
+        for (u32 p = (u32)(w - 1); p < np; p += NW - 1) {
+            const bool onA = p < npa;
+            const Range& R = onA ? r.oa : r.ob;
+            const u32 pp = onA ? p : p - npa;
+            u32x4* dst = s_oid + (onA ? 0 : r.c3 - r.c2) + 64 * pp;
+            const u32 c = 64 * pp + lane;
+            if (c < R.nch) __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)dst, 16, 0, 0);
         }
     }
-    __syncthreads();
-    const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
-    const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
-    const u32* oA = (const u32*)((const u8*)(s_ch + r.c2) + r.oa.skew);
-    const u32* oB = (const u32*)((const u8*)(s_ch + r.c3) + r.ob.skew);
-    const int na = q.na, nb = q.nb, nitems = na + nb, nbx = nb + (q.has_la ? 1 : 0);
+}
 
-    // ---- strictly ascending keys (independent reads, off every chain) ----
+// workgroup barrier that waits for LDS traffic only: an LDS-DMA still in flight stays in flight
+// across it (__syncthreads would also drain vmcnt)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// 64-bit value of lane 0 (wave-uniform: SGPRs)
+__device__ __forceinline__ u64 lane0_64(u64 x) {
+    return (u64)(u32)__builtin_amdgcn_readlane((u32)x, 0) | (u64)(u32)__builtin_amdgcn_readlane((u32)(x >> 32), 0) << 32;
+}
+
+// run descriptor: kind << 30 | length << 23 | a << 11 | b   (tile-local a, b < 2048; length <= 64)
+enum : u32 { RUN_PAIR = 0, RUN_DEL = 1, RUN_INS = 2 };
+static_assert(C2_TILE <= 2048, "run descriptors hold 11-bit tile-local indices");
+
+// Run merge of one tile, in two phases so that the OIDs land while the keys are walked.
+//   phase 1 (keys only — wave 0 waited for its key DMA, the OID DMA is still in flight): key order
+//     check, per-wave stretch splits, then the run rounds: lane l looks at A[a+l] and B[b+l]; the
+//     leading equal lanes are matched pairs, or (first keys differ) the leading A below B[b] are
+//     deletes or the leading B below A[a] inserts.  A round only records its run (one descriptor per
+//     round, in lane `round` of a VGPR); the walk state stays in SGPRs (scalar branches only).
+//   phase 2 (after the OID DMA has landed): the runs in order — OIDs of each pair run compared out of
+//     LDS, changed pairs, deletes and inserts written to the wave's slot in key order.
+// A stretch still unfinished after RMAX rounds (dense interleaved edits) is finished by the per-lane
+// merge path (search + walk) over what is left.
+template <int NT, bool HASH, typename LandOids>
+__device__ __forceinline__ void run_tile(const Join2Args& g, const TileGeo& q, const TileRanges& r, const u32x4* s_key,
+                                         const u32x4* s_oid, int* s_split, u32 (*s_cnt)[4], u64 tile,
+                                         LandOids land_oids) {
+    constexpr int NW = NT / 64, TILE = NW * RW, IPL = RW / 64;  // IPL: items per lane (fallback walk)
+    static_assert(KD_RMAX <= 64, "one run descriptor per lane");
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64* sA = (const u64*)((const u8*)s_key + r.ka.skew) + q.has_lbA;
+    const u64* sB = (const u64*)((const u8*)(s_key + r.c1) + r.kb.skew) + q.has_lbB;
+    // address space 3 + volatile: single ds_read_b32s (merged ds_read2s lose the alias scope)
+    typedef const volatile __attribute__((address_space(3))) u32* lds_vu32;
+    const lds_vu32 oA = (lds_vu32)((const u8*)s_oid + r.oa.skew);
+    const lds_vu32 oB = (lds_vu32)((const u8*)(s_oid + (r.c3 - r.c2)) + r.ob.skew);
+    const int na = q.na, nb = q.nb, nitems = na + nb, nbx = nb + (q.has_la ? 1 : 0);
+#if KD_J_CLOCK
+    u64* clk = (u64*)(g.stage_delta + tile * (u64)C2_STAGE + TILE);
+#endif
+
+    // ---- strictly ascending keys: item c of the tile checks its key against the one before it ----
     bool bad = false;
-    for (int c = tid; c < na; c += NT) bad |= (c > 0 || q.has_lbA) && sA[c - 1] >= sA[c];
-    for (int c = tid; c < nb; c += NT) bad |= (c > 0 || q.has_lbB) && sB[c - 1] >= sB[c];
-    if (bad) atomicOr(g.err, 1u);
+#pragma unroll
+    for (int k = 0; k < TILE / NT; k++) {
+        const int c = k * NT + tid;
+        const bool onA = c < na;
+        const int ci = onA ? c : c - na;
+        const bool chk = (c < nitems) & (ci > 0 || (onA ? q.has_lbA : q.has_lbB));
+        const u64* s = onA ? sA : sB;
+        const int cc = chk ? ci : 1;
+        const u64 k0 = s[cc - 1], k1 = s[cc];
+        bad |= chk & (k0 >= k1);
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(g.err, 1u);
+#if KD_J_CLOCK
+    if (tid == 0) clk[2] = wall_clock64();
+#endif
 
     // ---- the stretch splits: wave w >= 1 finds the split at item w*RW ----
     if (tid == 0) { s_split[0] = 0; s_split[NW] = na; }
@@ -668,91 +726,108 @@ __global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
         const int sp = mp_search_lds64(sA, sB, d, d - nb > 0 ? d - nb : 0, d < na ? d : na);
         if (lane == 0) s_split[wid] = sp;
     }
-    __syncthreads();
-    int a = __builtin_amdgcn_readfirstlane(s_split[wid]);  // wave-uniform walk state: SGPRs
+    lds_barrier();
+#if KD_J_CLOCK
+    if (tid == 0) clk[3] = wall_clock64();
+#endif
+    int a = __builtin_amdgcn_readfirstlane(s_split[wid]);
     const int ae = __builtin_amdgcn_readfirstlane(s_split[wid + 1]);
     const int d0 = wid * RW < nitems ? wid * RW : nitems, d1 = (wid + 1) * RW < nitems ? (wid + 1) * RW : nitems;
-    int b = d0 - a;
-    const int be = d1 - ae;
+    int b = __builtin_amdgcn_readfirstlane(d0 - a);
+    const int be = __builtin_amdgcn_readfirstlane(d1 - ae);
     // the stretch's first B may be the partner of the A just before it (matched there)
-    if (b < be && (a > 0 || q.has_lbA) && sA[a - 1] == sB[b]) b++;
+    if (b < be && (a > 0 || q.has_lbA) && uni64(sA[a - 1]) == uni64(sB[b])) b++;
 
+    // ---- phase 1: the run rounds over the keys ----
+    const int amax = na > 0 ? na - 1 : 0, bmax = nbx > 0 ? nbx - 1 : 0;
+    u32 runs = 0;  // lane k: descriptor of round k
+    int nr = 0;
+    for (; nr < KD_RMAX && a + b < ae + be; nr++) {
+        const int la = a + lane, lb = b + lane;
+        const u64 ka = sA[la < amax ? la : amax], kb = sB[lb < bmax ? lb : bmax];
+        const bool ina = la < ae;
+        const u64 ne = __ballot(!(ina && lb < nbx && ka == kb));
+        const int f = ne ? __ffsll((long long)ne) - 1 : 64;  // leading matched pairs
+        u32 desc;
+        if (f > 0) {
+            desc = RUN_PAIR << 30 | (u32)f << 23 | (u32)a << 11 | (u32)b;
+            a += f;
+            b += f;
+        } else {
+            // lane 0 holds A[a] and B[b] (B[be] is the lookahead: an A below it is a delete)
+            const u64 ka0 = a < ae ? lane0_64(ka) : ~0ull, kb0 = b < nbx ? lane0_64(kb) : ~0ull;
+            if (ka0 < kb0) {
+                const u64 nd = __ballot(!(ina && ka < kb0));
+                const int run = nd ? __ffsll((long long)nd) - 1 : 64;
+                desc = RUN_DEL << 30 | (u32)run << 23 | (u32)a << 11 | (u32)b;
+                a += run;
+            } else {
+                const u64 ni = __ballot(!(lb < be && kb < ka0));
+                const int run = ni ? __ffsll((long long)ni) - 1 : 64;
+                desc = RUN_INS << 30 | (u32)run << 23 | (u32)a << 11 | (u32)b;
+                b += run;
+            }
+        }
+        runs = lane == nr ? desc : runs;
+    }
+#if KD_J_CLOCK
+    if (lane == 0) { clk[4 + wid] = wall_clock64(); clk[8 + wid] = nr + ((a < ae || b < be) ? 1000 : 0); }
+#endif
+
+    // ---- the OIDs land in LDS (and a barrier publishes them) ----
+    land_oids();
+#if KD_J_CLOCK
+    if (tid == 0) clk[14] = wall_clock64();
+#endif
+
+    // ---- phase 2: the runs in key order ----
     uint2* sd = g.stage_delta + tile * (u64)C2_STAGE + wid * RW;
     uint2* su = g.stage_upd + tile * (u64)C2_STAGE + wid * RW;
     const u32 i0 = (u32)q.i0, j0 = (u32)q.j0;
     const u64 lt = (1ull << lane) - 1;  // lanes below this one
     u32 cd = 0, cu = 0, cx = 0, ci = 0;
-    const int amax = na > 0 ? na - 1 : 0, bmax = nbx > 0 ? nbx - 1 : 0;
-    for (int round = 0; round < KD_RMAX && (a < ae || b < be); round++) {
-        const int la = a + lane, lb = b + lane;
-        const bool ina = la < ae, inb = lb < nbx;
-        const u64 ka = sA[la < amax ? la : amax], kb = sB[lb < bmax ? lb : bmax];
-        const u64 ne = __ballot(!(ina && inb && ka == kb));
-        const int f = ne ? __ffsll((long long)ne) - 1 : 64;  // leading matched pairs
-        if (f > 0) {
+    for (int k = 0; k < nr; k++) {
+        const u32 desc = __builtin_amdgcn_readlane(runs, k);
+        const u32 kind = desc >> 30, len = (desc >> 23) & 127, ra = (desc >> 11) & 2047, rb = desc & 2047;
+        const u32 la = ra + lane, lb = rb + lane;
+        if (kind == RUN_PAIR) {
+            const u32 ia = lane < len ? la : ra, jb = lane < len ? lb : rb;
             u32 d = 0;
-            if (lane < f) {
-                if (KD_J_OIDG) {
-                    typedef const __attribute__((address_space(1))) u32* gp32;
-                    const gp32 pa = (gp32)(g.oidA + 20 * (q.i0 + la)), pb = (gp32)(g.oidB + 20 * (q.j0 + lb));
-                    u32 x[5], y[5];
 #pragma unroll
-                    for (int w = 0; w < 5; w++) { x[w] = pa[w]; y[w] = pb[w]; }
-#pragma unroll
-                    for (int w = 0; w < 5; w++) d |= x[w] ^ y[w];
-                } else {
-#pragma unroll
-                    for (int w = 0; w < 5; w++) d |= oA[5 * la + w] ^ oB[5 * lb + w];
-                }
-            }
-            if (g.hash_mode && lane < f &&
-                !names_eq(g.nameA, g.nameOffA, q.i0 + la, g.nameB, g.nameOffB, q.j0 + lb))
+            for (int w = 0; w < 5; w++) d |= oA[5 * ia + w] ^ oB[5 * jb + w];
+            if (HASH && lane < len && !names_eq(g.nameA, g.nameOffA, q.i0 + la, g.nameB, g.nameOffB, q.j0 + lb))
                 atomicOr(g.err, 2u);
-            const bool chg = lane < f && d != 0;
+            const bool chg = (lane < len) & (d != 0);
             const u64 bc = __ballot(chg);
-            if (chg) {
-                const u32 pos = (u32)__popcll(bc & lt);
-                const uint2 v = make_uint2(i0 + la, j0 + lb);
-                sd[cd + pos] = v;
-                su[cu + pos] = v;
+            if (bc) {
+                if (chg) {
+                    const u32 pos = (u32)__popcll(bc & lt);
+                    const uint2 v = make_uint2(i0 + la, j0 + lb);
+                    sd[cd + pos] = v;
+                    su[cu + pos] = v;
+                }
+                cd += (u32)__popcll(bc);
+                cu += (u32)__popcll(bc);
             }
-            cd += (u32)__popcll(bc);
-            cu += (u32)__popcll(bc);
-            a += f;
-            b += f;
-            continue;
-        }
-        // lane 0 differs: a run of deletes (A below B[b]) or of inserts (B below A[a])
-        const u64 kb0 = b < nbx ? sB[b] : ~0ull;  // B[be] is the lookahead: an A below it is a delete
-        if (a < ae && sA[a] < kb0) {
-            const u64 nd = __ballot(!(ina && ka < kb0));
-            const int run = nd ? __ffsll((long long)nd) - 1 : 64;
-            if (lane < run) sd[cd + lane] = make_uint2(i0 + la, KD_NONE);
-            cd += run;
-            cx += run;
-            a += run;
         } else {
-            const u64 ka0 = a < ae ? sA[a] : ~0ull;
-            const u64 ni = __ballot(!(lb < be && kb < ka0));
-            const int run = ni ? __ffsll((long long)ni) - 1 : 64;
-            if (lane < run) sd[cd + lane] = make_uint2(KD_NONE, j0 + lb);
-            cd += run;
-            ci += run;
-            b += run;
+            const bool del = kind == RUN_DEL;
+            if (lane < len) sd[cd + lane] = del ? make_uint2(i0 + la, KD_NONE) : make_uint2(KD_NONE, j0 + lb);
+            cd += len;
+            if (del) cx += len;
+            else ci += len;
         }
     }
     if (a < ae || b < be) {  // dense edits: the per-lane merge path finishes the stretch
         if (b > be) b = be;    // (only on unsorted input, already flagged: keeps the walk in bounds)
-        u32 rec[4];
-        wave_walk<4>(sA, sB, a, ae, b, be, nbx, q.has_lbA, rec);
-        if (KD_J_OIDG) tile_oid_global<4>(g, q, rec);
-        else tile_oid_lds<4>(oA, oB, rec);
-        if (g.hash_mode) tile_names<4>(g, q, rec);
+        u32 rec[IPL];
+        wave_walk<IPL>(sA, sB, a, ae, b, be, nbx, q.has_lbA, rec);
+        tile_oid_lds<IPL, lds_vu32>(oA, oB, rec);
+        if (HASH) tile_names<IPL>(g, q, rec);
         TileCounts c;
         c.fd = c.fu = 0;
         u32 fx = 0, fi = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < IPL; k++) {
             const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1;
             const u32 isx = (u32)(kind == R_DEL), isi = (u32)(kind == R_INS), isu = (u32)(kind == R_MATCH) & chg;
             c.fd |= (isx | isi | isu) << k;
@@ -763,7 +838,7 @@ __global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
         // thread-major item order: this lane's records follow every record of the lanes below it
         u32 od = 0, ou = 0, wd = 0, wu = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < IPL; k++) {
             const u64 bd = __ballot((c.fd >> k) & 1), bu = __ballot((c.fu >> k) & 1);
             od += (u32)__popcll(bd & lt);
             ou += (u32)__popcll(bu & lt);
@@ -774,13 +849,20 @@ __global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
         }
         c.od = cd + od;
         c.ou = cu + ou;
-        tile_write<4>(rec, c, i0, j0, sd, su);
+        tile_write<IPL>(rec, c, i0, j0, sd, su);
         cd += wd;
         cu += wu;
     }
+#if KD_J_CLOCK
+    if (lane == 0) clk[16 + wid] = wall_clock64();
+#endif
     if (lane == 0) { s_cnt[wid][0] = cd; s_cnt[wid][1] = cu; s_cnt[wid][2] = cx; s_cnt[wid][3] = ci; }
-    __syncthreads();
+    lds_barrier();
+#if KD_J_CLOCK
+    if (tid == 0) clk[12] = wall_clock64();
+#endif
     if (tid == 0) {
+        static_assert(NW <= 4, "tile_cnt packs at most four wave slots");
         u32 td = 0, tu = 0, tx = 0, tn = 0, packed[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int w = 0; w < NW; w++) {
@@ -791,6 +873,153 @@ __global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
         u64* gs = g.gsum + 2 * (tile / C2_GROUP);
         atomicAdd((unsigned long long*)gs, (unsigned long long)(td | (u64)tu << 32));
         atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tn | (u64)tx << 32));
+    }
+}
+
+#if KD_J_CLOCK
+// stamps per tile (u64, in the staging pad): 13 before staging, 0 keys landed, 2 after the key check,
+// 3 after the split barrier, 4+w wave w's rounds done, 8+w its rounds (+1000 = fell back), 14 OIDs
+// landed, 16+w its records written, 12 after the final barrier
+__global__ void k_jclk_report(const uint2* stage, u64 ntiles) {
+    constexpr int NS = 11;
+    __shared__ double s_sum[NS][256];
+    double sm[NS] = {};
+    for (u64 t = threadIdx.x; t < ntiles; t += 256) {
+        const u64* p = (const u64*)(stage + t * (u64)C2_STAGE + C2_TILE);
+        double r = 0, fb = 0, wr = 0, wl = 0;
+        for (int w = 0; w < C2_NT / 64; w++) {
+            r += (double)(p[8 + w] % 1000); fb += p[8 + w] >= 1000;
+            wr += (double)(p[4 + w] - p[3]); wl += (double)(p[16 + w] - p[14]);
+            sm[10] += (double)(p[20 + w] - p[4 + w]) / (C2_NT / 64);
+        }
+        const double nw = C2_NT / 64;
+        sm[0] += (double)(p[0] - p[13]); sm[1] += (double)(p[2] - p[0]); sm[2] += (double)(p[3] - p[2]);
+        sm[3] += wr / nw; sm[4] += (double)(p[14] - p[3]); sm[5] += wl / nw; sm[6] += (double)(p[12] - p[14]);
+        sm[7] += r / nw; sm[8] += fb; sm[9] += (double)(p[12] - p[13]);
+    }
+    for (int k = 0; k < NS; k++) s_sum[k][threadIdx.x] = sm[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 256; i++)
+            for (int k = 0; k < NS; k++) sm[k] += s_sum[k][i];
+        const double n = (double)ntiles, us = 0.01 / n;
+        printf("JCLK tiles %llu mean_us keys %.3f check %.3f split %.3f rounds %.3f oids_landed %.3f emit %.3f "
+               "tail %.3f total %.3f | rounds/wave %.2f fallbacks %.0f own_oid_wait %.3f\n",
+               (unsigned long long)ntiles, sm[0] * us, sm[1] * us, sm[2] * us, sm[3] * us, sm[4] * us, sm[5] * us,
+               sm[6] * us, sm[9] * us, sm[7] / n, sm[8], sm[10] * us);
+    }
+}
+#endif
+
+// Register staging of one tile: every thread loads a fixed number of 16-byte chunks of the key ranges
+// (KP) and of the OID ranges (OP) — all loads issued up front, lanes past a range reload its first chunk
+// (fixed counts: the compiler's vmcnt waits stay exact) — the keys are written to LDS at once, the OIDs
+// only after the key phase (their loads stay in flight meanwhile).  Plain loads, not LDS-DMA: DMA
+// writes into LDS lose arbitration to the co-resident workgroups' ds_reads and landed several µs late.
+template <int NT>
+struct RunRegs {
+    static constexpr int KP = (RunLds<NT>::CHK + NT - 1) / NT, OP = (RunLds<NT>::CHO + NT - 1) / NT;
+    u32x4 k[KP], o[OP];
+};
+
+template <int NT>
+__device__ __forceinline__ void run_load(const TileRanges& r, RunRegs<NT>& v) {
+    typedef const __attribute__((address_space(1))) u32x4* gx4;
+    const u32 tid = threadIdx.x, nk = r.c2, no = r.c4 - r.c2;
+#pragma unroll
+    for (int k = 0; k < RunRegs<NT>::KP; k++) {
+        const u32 c = k * NT + tid;
+        const bool onA = c < r.c1;
+        const Range& R = onA ? r.ka : r.kb;
+        const u32 cc = c < nk ? (onA ? c : c - r.c1) : 0;
+        v.k[k] = *(gx4)(R.base + 16ull * cc);
+    }
+#pragma unroll
+    for (int k = 0; k < RunRegs<NT>::OP; k++) {
+        const u32 c = k * NT + tid;
+        const bool onA = c < r.c3 - r.c2;
+        const Range& R = onA ? r.oa : r.ob;
+        const u32 cc = c < no ? (onA ? c : c - (r.c3 - r.c2)) : 0;
+        v.o[k] = *(gx4)(R.base + 16ull * cc);
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void run_put_keys(const TileRanges& r, const RunRegs<NT>& v, u32x4* s_key) {
+#pragma unroll
+    for (int k = 0; k < RunRegs<NT>::KP; k++) {
+        const u32 c = k * NT + threadIdx.x;
+        if (c < r.c2) s_key[c] = v.k[k];
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void run_put_oids(const TileRanges& r, const RunRegs<NT>& v, u32x4* s_oid) {
+#pragma unroll
+    for (int k = 0; k < RunRegs<NT>::OP; k++) {
+        const u32 c = k * NT + threadIdx.x;
+        if (c < r.c4 - r.c2) s_oid[c] = v.o[k];
+    }
+}
+
+// Persistent and software-pipelined: workgroup b merges tiles b, b + G, b + 2G, ... (G = the grid,
+// sized so that every workgroup is resident).  As soon as a tile's OIDs are in LDS (after its key
+// phase), the loads of the next tile are issued into the same registers: they fly during the current
+// tile's emit phase, and the next tile's split points one tile further ahead.
+template <int NT, bool HASH>
+__global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
+    using LD = RunLds<NT>;
+    static_assert(LD::TILE == (NT / 64) * RW, "one RW-item stretch per wave");
+    __shared__ u32x4 s_key[LD::CHK];
+    __shared__ u32x4 s_oid[LD::CHO];
+    __shared__ int s_split[NT / 64 + 1];
+    __shared__ u32 s_cnt[NT / 64][4];  // per wave: deltas, updates, deletes, inserts
+    u64 tile = blockIdx.x;
+    if (tile >= g.ntiles) return;
+    TileGeo q = tile_geo(g, tile, LD::TILE);
+    if (!q.ok && threadIdx.x == 0) atomicOr(g.err, 1u);
+    TileRanges r = tile_ranges(g, q);
+    RunRegs<NT> v;
+    run_load<NT>(r, v);
+    u64 tn = tile + gridDim.x, p0 = 0, p1 = 0;
+    if (tn < g.ntiles) { p0 = g.part[tn]; p1 = g.part[tn + 1]; }
+    run_put_keys<NT>(r, v, s_key);
+    lds_barrier();
+    for (;;) {
+#if KD_J_CLOCK
+        if (threadIdx.x == 0) {
+            u64* clk = (u64*)(g.stage_delta + tile * (u64)C2_STAGE + LD::TILE);
+            clk[0] = clk[13] = wall_clock64();
+        }
+#endif
+        const bool more = tn < g.ntiles;
+        TileGeo qn = q;
+        TileRanges rn = r;
+        u64 tnn = tn;
+        run_tile<NT, HASH>(g, q, r, s_key, s_oid, s_split, s_cnt, tile, [&] {
+#if KD_J_CLOCK
+            vm_drain();
+            if ((threadIdx.x & 63) == 0)
+                ((u64*)(g.stage_delta + tile * (u64)C2_STAGE + LD::TILE))[20 + (threadIdx.x >> 6)] = wall_clock64();
+#endif
+            run_put_oids<NT>(r, v, s_oid);
+            lds_barrier();
+            if (more) {  // the next tile's loads fly during this tile's emit phase
+                qn = tile_geo_from(g, tn, LD::TILE, p0, p1);
+                if (!qn.ok && threadIdx.x == 0) atomicOr(g.err, 1u);
+                rn = tile_ranges(g, qn);
+                run_load<NT>(rn, v);
+                tnn = tn + gridDim.x;
+                if (tnn < g.ntiles) { p0 = g.part[tnn]; p1 = g.part[tnn + 1]; }
+            }
+        });  // ends with a barrier: LDS free for the next tile
+        if (!more) break;
+        run_put_keys<NT>(rn, v, s_key);
+        lds_barrier();
+        tile = tn;
+        q = qn;
+        r = rn;
+        tn = tnn;
     }
 }
 
@@ -1119,9 +1348,18 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         });
     }
     const bool ws = KD_C2_MODE == 3;
-    if (ws) {  // run merge, per-wave slots
+    if (KD_C2_MODE == 3) {  // run merge, persistent, per-wave slots
+        if (ctx->occ_join2r <= 0) {
+            int nb = 0;
+            KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_join2r<C2_NT, false>, C2_NT, 0));
+            ctx->occ_join2r = nb > 0 ? nb : 1;
+        }
+        const u64 grid = std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)ctx->occ_join2r);
         rc = launch(ctx, "k_join2", [&] {
-            hipLaunchKernelGGL((k_join2r<C2_NT>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+            if (hash)
+                hipLaunchKernelGGL((k_join2r<C2_NT, true>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
+            else
+                hipLaunchKernelGGL((k_join2r<C2_NT, false>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
         });
     } else if (KD_C2_MODE == 1) {  // one tile per workgroup, LDS-DMA staging
         rc = launch(ctx, "k_join2", [&] {
@@ -1144,6 +1382,9 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         });
     }
     if (rc || lookb) return rc;
+#if KD_J_CLOCK
+    if (ws) hipLaunchKernelGGL(k_jclk_report, dim3(1), dim3(256), 0, ctx->stream, (const uint2*)sdel, ntiles);
+#endif
     return launch(ctx, "k_place2", [&] {
         if (ws)
             hipLaunchKernelGGL((k_place2<KD_PLACE_NT, true>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
