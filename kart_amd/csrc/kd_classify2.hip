@@ -75,6 +75,30 @@ __device__ __forceinline__ u64 mp_search(const u64* __restrict__ A, const u64* _
     return lo;
 }
 
+// The same split, starting from a guess: one round of PW probes spaced `step` apart around `guess`
+// brackets the answer (or cuts the range down to one side of the probes), then mp_search finishes
+// inside the bracket.  A 1 %-edit diff keeps each split within a few hundred entries of the
+// proportional guess, so the first round almost always brackets it: ~3 dependent rounds instead of
+// ~6 over the whole arrays.  Correct for any guess (the predicate is monotone; probes are clamped).
+template <int PW>
+__device__ __forceinline__ u64 mp_search_guided(const u64* __restrict__ A, const u64* __restrict__ B, u64 d, u64 lo,
+                                                u64 hi, u64 guess, u64 step) {
+    if (hi <= lo) return lo;
+    const int lane = threadIdx.x & 63, sub = lane % PW, grp = lane / PW;
+    const u64 span = step * (PW / 2);
+    const u64 g0 = guess > lo + span ? guess - span : lo;  // probe k at g0 + k*step, clamped to [lo, hi]
+    u64 probe = g0 + step * (u64)sub;
+    if (probe > hi) probe = hi;
+    bool p = true;
+    if (probe < hi) p = A[probe] > B[d - 1 - probe];
+    const unsigned long long bal = (__ballot(p) >> (grp * PW)) & ((PW == 64) ? ~0ull : ((1ull << PW) - 1));
+    const int f = bal ? __ffsll(bal) - 1 : PW;  // first true probe (PW: none)
+    const u64 pf = f < PW ? (g0 + step * (u64)f < hi ? g0 + step * (u64)f : hi) : hi;
+    const u64 pl = f > 0 ? (g0 + step * (u64)(f - 1) < hi ? g0 + step * (u64)(f - 1) : hi) : lo;
+    const u64 nlo = f > 0 ? pl + 1 : lo, nhi = pf;
+    return mp_search<PW>(A, B, d, nlo < nhi ? nlo : nhi, nhi);
+}
+
 // Merge-path split points part[t] (A items among the first min(t*TILE, nA+nB) union items), two
 // levels: one block per group of C2_PG tiles.  The group's two end splits are searched over the
 // whole arrays (16 lanes each, 16-ary: ~6 rounds of random HBM reads); every inner split then lies
@@ -82,24 +106,28 @@ __device__ __forceinline__ u64 mp_search(const u64* __restrict__ A, const u64* _
 // and is found there by 8 lanes (8-ary) whose probes land in that small, cache-warm region.
 // The kernel also clears the counters and look-back descriptors the join needs (stream-ordered
 // before it), instead of separate memset launches.
-constexpr int C2_PG = 32;
-__global__ __launch_bounds__(256) void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B,
-                                                    u64 nB, u64 ntiles, u64* __restrict__ part,
-                                                    u64* __restrict__ zero_counts, u32* __restrict__ zero_err,
-                                                    u64* __restrict__ zero_buf, u64 n_zero) {
+#ifndef KD_PTOP
+#define KD_PTOP 16  // lanes per top-level split search
+#endif
+constexpr int C2_PG = 32, C2_PNT = 256;  // tiles per group; threads (8 lanes per inner split)
+__global__ __launch_bounds__(C2_PNT) void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B,
+                                                       u64 nB, u64 ntiles, u64* __restrict__ part,
+                                                       u64* __restrict__ zero_counts, u32* __restrict__ zero_err,
+                                                       u64* __restrict__ zero_buf, u64 n_zero) {
     if (blockIdx.x == 0 && threadIdx.x < 4) zero_counts[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 4) *zero_err = 0;
-    for (u64 k = (u64)blockIdx.x * 256 + threadIdx.x; k < n_zero; k += (u64)gridDim.x * 256) zero_buf[k] = 0;
+    for (u64 k = (u64)blockIdx.x * C2_PNT + threadIdx.x; k < n_zero; k += (u64)gridDim.x * C2_PNT) zero_buf[k] = 0;
     __shared__ u64 s_end[2];
     const int tid = threadIdx.x;
     const u64 total = nA + nB;
     const u64 t0 = (u64)blockIdx.x * C2_PG, t1 = t0 + C2_PG < ntiles ? t0 + C2_PG : ntiles;
-    if (tid < 32) {  // wave 0: lanes 0-15 -> split t0, lanes 16-31 -> split t1
-        const u64 t = tid < 16 ? t0 : t1;
+    if (tid < 2 * KD_PTOP) {  // wave 0: the group's end splits t0 and t1 (guided: ~3 rounds)
+        const u64 t = tid < KD_PTOP ? t0 : t1;
         u64 d = t * (u64)C2_TILE;
         if (d > total) d = total;
-        const u64 i = mp_search<16>(A, B, d, d > nB ? d - nB : 0, d < nA ? d : nA);
-        if ((tid & 15) == 0) s_end[tid >> 4] = i;
+        const u64 guess = (u64)((double)d * (double)nA / (double)(total ? total : 1));
+        const u64 i = mp_search_guided<KD_PTOP>(A, B, d, d > nB ? d - nB : 0, d < nA ? d : nA, guess, 2048 / KD_PTOP);
+        if ((tid & (KD_PTOP - 1)) == 0) s_end[tid / KD_PTOP] = i;
     }
     __syncthreads();
     const u64 i0 = s_end[0], i1 = s_end[1];
@@ -111,7 +139,9 @@ __global__ __launch_bounds__(256) void k_partition2(const u64* __restrict__ A, u
     if (t < t1) {
         const u64 d = t * (u64)C2_TILE;
         const u64 lo = (d > j1 && d - j1 > i0) ? d - j1 : i0, hi = i1 < d - j0 ? i1 : d - j0;
-        const u64 i = mp_search<8>(A, B, d, lo, hi);
+        // proportional guess inside the group's box
+        const u64 guess = d1 > d0 ? i0 + (u64)((double)(d - d0) * (double)(i1 - i0) / (double)(d1 - d0)) : lo;
+        const u64 i = mp_search_guided<8>(A, B, d, lo, hi, guess, 16);
         if ((tid & 7) == 0) part[t] = i;
     }
 }
@@ -1326,7 +1356,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     const u8* empty_oid = (const u8*)dz;
     rc = launch(ctx, "k_partition2", [&] {
         unsigned nb = (unsigned)((ntiles + C2_PG - 1) / C2_PG);
-        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(256), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part,
+        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part,
                            d_counts, d_err, zero, n_zero);
     });
     if (rc) return rc;

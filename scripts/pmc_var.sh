@@ -12,5 +12,5 @@ for lib in $LIBS; do
        -d $R/gpurun_out/pmcv/$name/p$i -o run -- python3 $R/bench.py $ARGS > $R/gpurun_out/pmcv/$name/p$i.json \
        2> $R/gpurun_out/pmcv/$name/p$i.err) || { echo "$name pass $i failed"; tail -3 gpurun_out/pmcv/$name/p$i.err; exit 1; }
   done
-  echo "== $name"; python3 scripts/pmc_summary.py gpurun_out/pmcv/$name 2>&1 | grep -E "k_join2" || true
+  echo "== $name"; python3 scripts/pmc_summary.py gpurun_out/pmcv/$name 2>&1 | grep -E "k_join2|k_place2" || true
 done
