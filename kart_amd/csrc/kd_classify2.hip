@@ -5,21 +5,19 @@
 // strictly ascending join keys + 20-byte blob OIDs; a key on one side only is an insert/delete, a
 // key on both sides with different OIDs is an update (GIT_DELTA_ADDED/DELETED/MODIFIED).
 //
-// The key union is cut into 1024-item merge-path tiles (k_partition2).  Default (key-ordered) path:
-//   k_join2p   persistent: a few workgroups per CU walk the tiles round-robin.  Per tile:
-//                0. keys + OIDs of both sides (plus the B entry after the tile) arrive in registers
-//                   as 16-B chunks — issued one tile AHEAD, while the previous tile computes — and go
-//                   to LDS once that tile is done (one LDS buffer per workgroup, loads always in
-//                   flight);
-//                1. merge path (4-ary search + register walk), OID compare in LDS;
-//                2. per-item-slot ballots -> tile-local offsets; decoupled look-back over earlier
-//                   tiles' descriptors -> the tile's global offsets; records written straight to
-//                   their final key-ordered positions (no staging, no second pass).
-// KD_DIFF_UNORDERED: k_join2 (one tile per workgroup, LDS-DMA staging) appends each tile's records
-// at an atomically reserved offset (tiles in completion order, key order inside each tile).
-// KD_C2_MODE (profiling builds): 1 = the per-tile k_join2 (LDS-DMA staging) for the ordered path;
-// 2 = k_join2p with a decoupled look-back instead of k_place2 (slow: with ~1000 tiles in flight the
-// look-back walks ~30 descriptor windows per tile).
+// The key union is cut into 1024-item merge-path tiles (k_partition2, guided two-level search).
+// Default (key-ordered) path, KD_C2_MODE 1:
+//   k_join2    one tile per 256-thread workgroup: keys by LDS-DMA into LDS, branch-free 4-ary split
+//              search + register walk, OIDs of matched pairs compared straight from HBM, ballot
+//              compaction into the tile's staging slot + tile counts + 64-tile group sums;
+//   k_place2   one wave per tile: earlier groups' sums + earlier tiles of its group -> offset, staged
+//              records -> final key-ordered positions; the last tile writes the totals.
+// KD_DIFF_UNORDERED: k_join2 appends each tile's records at an atomically reserved offset (tiles in
+// completion order, key order inside each tile); no k_place2.
+// Profiling builds (KD_C2_MODE): 0 = persistent register-prefetched k_join2p + k_place2;
+// 2 = k_join2p with a decoupled look-back (slow: ~1000 tiles in flight -> long look-back walks);
+// 3 = run merge k_join2r (persistent, per-wave run rounds, see its comment) + k_place2 over wave
+// slots.  Measurements of each are in DESIGN.md §3.1.
 #include "kd_join.h"
 
 namespace kd {
