@@ -78,7 +78,7 @@ __device__ __forceinline__ int range_ov(double a1, double a2, double b1, double 
     return (b2 != b1) && (a2 != a1);
 }
 
-__device__ __forceinline__ double py_mod360(double a) {
+__device__ __attribute__((noinline)) double py_mod360_slow(double a) {
     double m = fmod(a, 360.0);
     if (m != 0.0) {
         if (m < 0) m += 360.0;  // b > 0: result takes the sign of b
@@ -86,6 +86,17 @@ __device__ __forceinline__ double py_mod360(double a) {
         m = 0.0;  // copysign(0, 360)
     }
     return m;
+}
+
+// Python float a % 360.  On (-360, 720) fmod is exact and needs at most one +-360 (Sterbenz: a - 360
+// is exact for a in [360, 720)), so the common cases are plain selects; the rest call fmod.
+__device__ __forceinline__ double py_mod360(double a) {
+    double m;
+    if (a >= 0.0 && a < 360.0) m = a;
+    else if (a >= 360.0 && a < 720.0) m = a - 360.0;
+    else if (a < 0.0 && a > -360.0) m = a + 360.0;
+    else return py_mod360_slow(a);
+    return m == 0.0 ? 0.0 : m;
 }
 
 __device__ __forceinline__ double wrap_lon(double x) { return py_mod360(x + 180.0) - 180.0; }
@@ -113,76 +124,173 @@ struct EnvArgs {
     unsigned long long* n_cand;
 };
 
+// Fast header decode from registers.  The lane loads the 48 bytes from its blob start rounded down
+// to 4 B (three dword-aligned 16-B loads instead of ~60 byte loads), realigns them with v_alignbyte
+// (>= 45 valid bytes from the blob start), and decodes the GPKG header, a 32-B envelope (type 1) or
+// a point WKB right after the header (type 0) at fixed byte positions — exactly gpkg_env /
+// point_env.  Returns false (byte-wise slow path) where a field may lie past the window: envelope
+// types 2-4, and a NaN type-1 envelope (whose point WKB would follow it).
+__device__ __forceinline__ u64 f64_bits(u32 lo, u32 hi, bool le) {
+    const u64 x = (u64)hi << 32 | lo;
+    return le ? x : __builtin_bswap64(x);
+}
+__device__ __forceinline__ bool env_fast(const u32 r[11], u64 len, int& rc, double e[4], int& pc, double pe[4]) {
+    const u32 h = r[0];
+    const u32 f = h >> 24;
+    pc = -1;
+    if ((h & 0xFFFFFFu) != 0x005047u || (f & 0x20)) { rc = -1; return true; }  // 'G' 'P' version 0
+    if (f & 0x10) { rc = 0; return true; }  // empty: no envelope or point read
+    const int et = (f >> 1) & 7;
+    if (et > 1) return false;
+    const bool le = f & 1;
+    if (et == 1) {
+        if (len < 40) { rc = -1; return true; }
+        bool nan = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            e[i] = __longlong_as_double((i64)f64_bits(r[2 + 2 * i], r[3 + 2 * i], le));
+            nan |= e[i] != e[i];
+        }
+        rc = 1;
+        return !nan;
+    }
+    rc = 2;  // no stored envelope: point WKB at byte 8, its fields 1 byte past dword boundaries
+    if (len >= 13) {
+        const bool wle = (r[2] & 0xFF) == 1;
+        u32 typ = __builtin_amdgcn_alignbyte(r[3], r[2], 1);
+        if (!wle) typ = __builtin_bswap32(typ);
+        typ &= 0x0fffffffu;
+        if (typ >= 1000) typ %= 1000;
+        if (typ == 1 && len >= 29) {
+            const double x = __longlong_as_double((i64)f64_bits(__builtin_amdgcn_alignbyte(r[4], r[3], 1),
+                                                                __builtin_amdgcn_alignbyte(r[5], r[4], 1), wle));
+            const double y = __longlong_as_double((i64)f64_bits(__builtin_amdgcn_alignbyte(r[6], r[5], 1),
+                                                                __builtin_amdgcn_alignbyte(r[7], r[6], 1), wle));
+            if (x != x && y != y) { pe[0] = pe[1] = pe[2] = pe[3] = 0.0; pc = 0; }
+            else { pe[0] = x; pe[1] = x; pe[2] = y; pe[3] = y; pc = 1; }
+        }
+    }
+    return true;
+}
+
+// One lane per geometry, 256 consecutive geometries per workgroup iteration; the outputs (match
+// byte, encoded envelope, ok byte) are assembled in LDS and written as contiguous dwords.
 __global__ __launch_bounds__(256) void k_envelopes(EnvArgs a) {
+    typedef const __attribute__((address_space(1))) u32x4* gx4;
+    __shared__ u8 s_enc[256 * 16];
+    __shared__ u8 s_m[256], s_ok[256];
     const int nb = a.bits / 2;
     const double vmax = (double)((1ull << a.bits) - 1);
+    const int tid = threadIdx.x;
+    const u64 arena_end = (u64)a.data + a.off[a.n];
     u32 cand = 0;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (u64)gridDim.x * blockDim.x) {
-        const u64 o = a.off[i], len = a.off[i + 1] - o;
-        const u8* g = a.data + o;
-        u8 m;
-        u8 ok = 0;
-        u8 out[16] = {0};
-        if (len == 0) {
-            m = 2;
-        } else {
-            double e[4];
-            int r = gpkg_env(g, len, e);
-            bool have = false;
-            if (r == 1) have = true;
-            else if (r >= 0) {
-                if (g[3] & 0x10) { e[0] = e[1] = e[2] = e[3] = 0.0; have = true; }
-                else have = point_env(g, len, e) >= 0;
+    for (u64 i0 = (u64)blockIdx.x * 256; i0 < a.n; i0 += (u64)gridDim.x * 256) {
+        const u64 i = i0 + tid;
+        u8 m = 0, ok = 0;
+        for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
+        if (i < a.n) {
+            const u64 o = a.off[i], len = a.off[i + 1] - o;
+            const u8* g = a.data + o;
+            double e[4] = {0, 0, 0, 0}, pe[4] = {0, 0, 0, 0};
+            int r = -1, pc = -1;
+            u32 hflags = 0;
+            bool fast = false;
+            const u64 a0 = (u64)g, a4 = a0 & ~(u64)3;
+            if (len >= 8 && a4 + 48 <= arena_end) {
+                u32 w[12];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const u32x4 v = *(gx4)(a4 + 16 * k);
+                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                }
+                const u32 sh = (u32)(a0 - a4);
+                u32 rr[11];
+#pragma unroll
+                for (int j = 0; j < 11; j++) rr[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+                fast = env_fast(rr, len, r, e, pc, pe);
+                hflags = rr[0] >> 24;
             }
-            if (!have) m = 3;
-            else {
-                int x = range_ov(a.f0, a.f1, e[0], e[1]);
-                if (x > 0) x = range_ov(a.f2, a.f3, e[2], e[3]);
-                m = x < 0 ? 3 : (u8)x;
-                cand += x > 0;
+            if (!fast && len > 0) {  // byte-wise reference decode (short or unusual blobs)
+                r = gpkg_env(g, len, e);
+                pc = -1;
+                if (r == 0 || r == 2) pc = point_env(g, len, pe);
+                if (r >= 0) hflags = g[3];
             }
-            // ---- index envelope (skip empties: index.py:346) ----
-            if (!(g[3] & 0x10) && r >= 0) {
-                double s[4];
-                bool src = false;
-                if (r == 1) { s[0] = e[0]; s[1] = e[1]; s[2] = e[2]; s[3] = e[3]; src = true; }
-                else if (r == 2) src = point_env(g, len, s) == 1;
-                if (src) {
-                    // transpose -> (minx, miny, maxx, maxy)
-                    const double e0 = s[0], e1 = s[2], e2 = s[1], e3 = s[3];
-                    double w, so, ea, no;
-                    bool valid = true;
-                    if (e0 == e2 && e1 == e3) {
-                        w = wrap_lon(e0); so = e1; ea = w; no = e1;
-                    } else {
-                        const double width = e2 - e0, height = e3 - e1;
-                        if (width >= 180) valid = false;
-                        double big = width;
-                        if (height > big) big = height;
-                        const double buf = big < 1.0 ? 0.1 * big : 0.1;
-                        double t1 = e1 - buf; if (-90.0 > t1) t1 = -90.0;
-                        double t3 = e3 + buf; if (90.0 < t3) t3 = 90.0;
-                        w = wrap_lon(e0 - buf); so = t1; ea = wrap_lon(e2 + buf); no = t3;
-                    }
-                    if (valid) {
-                        u64 q0, q1, q2, q3;
-                        if (enc_val(w, -180, 180, vmax, false, &q0) && enc_val(so, -90, 90, vmax, false, &q1) &&
-                            enc_val(ea, -180, 180, vmax, true, &q2) && enc_val(no, -90, 90, vmax, true, &q3)) {
-                            // 4*bits big-endian bits -> nb bytes
-                            unsigned __int128 acc = ((unsigned __int128)q0 << (3 * a.bits)) |
-                                                    ((unsigned __int128)q1 << (2 * a.bits)) |
-                                                    ((unsigned __int128)q2 << a.bits) | (unsigned __int128)q3;
-                            for (int k = nb - 1; k >= 0; k--) { out[k] = (u8)(acc & 0xFF); acc >>= 8; }
-                            ok = 1;
+            if (len == 0) {
+                m = 2;
+            } else {
+                // the GPKG empty bit (r == 0 may also mean a NaN envelope); r >= 0 implies len >= 8
+                const bool is_empty = r >= 0 && (hflags & 0x10);
+                bool have = false;
+                if (r == 1) have = true;
+                else if (r >= 0) {
+                    if (is_empty) { e[0] = e[1] = e[2] = e[3] = 0.0; have = true; }
+                    else if (pc >= 0) { e[0] = pe[0]; e[1] = pe[1]; e[2] = pe[2]; e[3] = pe[3]; have = true; }
+                }
+                if (!have) m = 3;
+                else {
+                    int x = range_ov(a.f0, a.f1, e[0], e[1]);
+                    if (x > 0) x = range_ov(a.f2, a.f3, e[2], e[3]);
+                    m = x < 0 ? 3 : (u8)x;
+                    cand += x > 0;
+                }
+                // ---- index envelope (skip empties: index.py:346) ----
+                if (!is_empty && r >= 0) {
+                    double sv[4];
+                    bool src = false;
+                    if (r == 1) { sv[0] = e[0]; sv[1] = e[1]; sv[2] = e[2]; sv[3] = e[3]; src = true; }
+                    else if (r == 2 && pc == 1) { sv[0] = pe[0]; sv[1] = pe[1]; sv[2] = pe[2]; sv[3] = pe[3]; src = true; }
+                    if (src) {
+                        // transpose -> (minx, miny, maxx, maxy)
+                        const double e0 = sv[0], e1 = sv[2], e2 = sv[1], e3 = sv[3];
+                        double wv, so, ea, no;
+                        bool valid = true;
+                        if (e0 == e2 && e1 == e3) {
+                            wv = wrap_lon(e0); so = e1; ea = wv; no = e1;
+                        } else {
+                            const double width = e2 - e0, height = e3 - e1;
+                            if (width >= 180) valid = false;
+                            double big = width;
+                            if (height > big) big = height;
+                            const double buf = big < 1.0 ? 0.1 * big : 0.1;
+                            double t1 = e1 - buf; if (-90.0 > t1) t1 = -90.0;
+                            double t3 = e3 + buf; if (90.0 < t3) t3 = 90.0;
+                            wv = wrap_lon(e0 - buf); so = t1; ea = wrap_lon(e2 + buf); no = t3;
+                        }
+                        if (valid) {
+                            u64 q0, q1, q2, q3;
+                            if (enc_val(wv, -180, 180, vmax, false, &q0) && enc_val(so, -90, 90, vmax, false, &q1) &&
+                                enc_val(ea, -180, 180, vmax, true, &q2) && enc_val(no, -90, 90, vmax, true, &q3)) {
+                                // 4*bits big-endian bits -> nb bytes
+                                unsigned __int128 acc = ((unsigned __int128)q0 << (3 * a.bits)) |
+                                                        ((unsigned __int128)q1 << (2 * a.bits)) |
+                                                        ((unsigned __int128)q2 << a.bits) | (unsigned __int128)q3;
+                                for (int k = nb - 1; k >= 0; k--) { s_enc[tid * nb + k] = (u8)(acc & 0xFF); acc >>= 8; }
+                                ok = 1;
+                            }
                         }
                     }
                 }
             }
         }
-        a.match[i] = m;
-        a.enc_ok[i] = ok;
-        u8* eo = a.enc + i * nb;
-        for (int k = 0; k < nb; k++) eo[k] = out[k];
+        // ---- outputs through LDS: contiguous dword stores ----
+        s_m[tid] = m;
+        s_ok[tid] = ok;
+        __syncthreads();
+        const u32 cnt = (u32)(a.n - i0 < 256 ? a.n - i0 : 256);
+        auto copy = [&](u8* dst, const u8* src, u32 bytes) {
+            if ((((u64)dst) & 3) == 0) {
+                const u32 nw = bytes >> 2;
+                for (u32 k = tid; k < nw; k += 256) ((u32*)dst)[k] = ((const u32*)src)[k];
+                for (u32 k = 4 * nw + tid; k < bytes; k += 256) dst[k] = src[k];
+            } else {
+                for (u32 k = tid; k < bytes; k += 256) dst[k] = src[k];
+            }
+        };
+        copy(a.match + i0, s_m, cnt);
+        copy(a.enc_ok + i0, s_ok, cnt);
+        copy(a.enc + i0 * nb, s_enc, cnt * nb);
+        __syncthreads();
     }
     // candidate count: wave reduce then one atomic per wave
     u64 c = cand;
