@@ -299,34 +299,65 @@ __global__ __launch_bounds__(256) void k_envelopes(EnvArgs a) {
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(a.n_cand, (unsigned long long)c);
 }
 
-__global__ __launch_bounds__(256) void k_env_overlap(const u8* __restrict__ enc, u64 n, int bits, double qw, double qs,
+// 1024 consecutive encoded envelopes per workgroup iteration are moved HBM <-> LDS as contiguous
+// 16-B (or 4-B) chunks — 10 KB in flight per workgroup; the per-lane byte loads of nb-byte records
+// were the bound — and each lane decodes four of them.  BITS > 0: compile-time bit width (the shifts
+// of the 4*bits-bit record fold to constants).
+template <int BITS>
+__global__ __launch_bounds__(256) void k_env_overlap(const u8* __restrict__ enc, u64 n, int bits_rt, double qw, double qs,
                                                      double qe, double qn, u8* __restrict__ out) {
-    const int nb = bits / 2;
+    constexpr int CH = 1024;
+    __shared__ __attribute__((aligned(16))) u8 s_in[CH * 16];
+    __shared__ __attribute__((aligned(16))) u8 s_out[CH];
+    const int bits = BITS > 0 ? BITS : bits_rt;
+    const int nb = bits / 2, tid = threadIdx.x;
     const double vmax = (double)((1ull << bits) - 1);
     const u64 mask = (1ull << bits) - 1;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        const u8* p = enc + i * nb;
-        unsigned __int128 acc = 0;
-        for (int k = 0; k < nb; k++) acc = (acc << 8) | p[k];
-        double v[4];
-        const double mins[4] = {-180, -90, -180, -90}, maxs[4] = {180, 90, 180, 90};
-        for (int k = 3; k >= 0; k--) {
-            u64 q = (u64)(acc & mask);
-            acc >>= bits;
-            double norm = (double)q / vmax;
-            v[k] = norm * (maxs[k] - mins[k]) + mins[k];
+    auto copy = [&](u8* dst, const u8* src, u32 bytes) {
+        const u64 al = ((u64)dst) | ((u64)src);
+        if ((al & 15) == 0) {
+            const u32 nq = bytes >> 4;
+            for (u32 k = tid; k < nq; k += 256) ((u32x4*)dst)[k] = ((const u32x4*)src)[k];
+            for (u32 k = 16 * nq + tid; k < bytes; k += 256) dst[k] = src[k];
+        } else if ((al & 3) == 0) {
+            const u32 nw = bytes >> 2;
+            for (u32 k = tid; k < nw; k += 256) ((u32*)dst)[k] = ((const u32*)src)[k];
+            for (u32 k = 4 * nw + tid; k < bytes; k += 256) dst[k] = src[k];
+        } else {
+            for (u32 k = tid; k < bytes; k += 256) dst[k] = src[k];
         }
-        // cyclic_range_overlaps(w, e, qw, qe) && range_overlaps(s, n, qs, qn)
-        double a1 = v[0], a2 = v[2], b1 = qw, b2 = qe;
-        if (a1 > a2) a2 += 360;
-        if (b1 > b2) b2 += 360;
-        int r = range_ov(a1, a2, b1, b2);
-        if (r == 0) {
-            if (a1 < b1) { a1 += 360; a2 += 360; } else { b1 += 360; b2 += 360; }
-            r = range_ov(a1, a2, b1, b2);
+    };
+    for (u64 i0 = (u64)blockIdx.x * CH; i0 < n; i0 += (u64)gridDim.x * CH) {
+        const u32 cnt = (u32)(n - i0 < CH ? n - i0 : CH);
+        copy(s_in, enc + i0 * nb, cnt * nb);
+        __syncthreads();
+        for (u32 e = tid; e < cnt; e += 256) {
+            const u8* p = s_in + e * nb;
+            unsigned __int128 acc = 0;
+            for (int k = 0; k < nb; k++) acc = (acc << 8) | p[k];
+            double v[4];
+            const double mins[4] = {-180, -90, -180, -90}, maxs[4] = {180, 90, 180, 90};
+            for (int k = 3; k >= 0; k--) {
+                u64 q = (u64)(acc & mask);
+                acc >>= bits;
+                double norm = (double)q / vmax;
+                v[k] = norm * (maxs[k] - mins[k]) + mins[k];
+            }
+            // cyclic_range_overlaps(w, e, qw, qe) && range_overlaps(s, n, qs, qn)
+            double a1 = v[0], a2 = v[2], b1 = qw, b2 = qe;
+            if (a1 > a2) a2 += 360;
+            if (b1 > b2) b2 += 360;
+            int r = range_ov(a1, a2, b1, b2);
+            if (r == 0) {
+                if (a1 < b1) { a1 += 360; a2 += 360; } else { b1 += 360; b2 += 360; }
+                r = range_ov(a1, a2, b1, b2);
+            }
+            if (r > 0) r = range_ov(v[1], v[3], qs, qn);
+            s_out[e] = r < 0 ? 2 : (u8)r;
         }
-        if (r > 0) r = range_ov(v[1], v[3], qs, qn);
-        out[i] = r < 0 ? 2 : (u8)r;
+        __syncthreads();
+        copy(out + i0, s_out, cnt);
+        __syncthreads();
     }
 }
 
@@ -401,9 +432,11 @@ int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const 
         d_out = (u8*)p;
     }
     if (n) {
-        unsigned blocks = (unsigned)std::min<u64>((n + 255) / 256, 256ull * 32);
+        unsigned blocks = (unsigned)std::min<u64>((n + 1023) / 1024, 256ull * 32);
         rc = launch(ctx, "k_env_overlap", [&] {
-            hipLaunchKernelGGL(k_env_overlap, dim3(blocks), dim3(256), 0, ctx->stream, (const u8*)d_enc, n, bits, q[0],
+            if (bits == 20) hipLaunchKernelGGL(k_env_overlap<20>, dim3(blocks), dim3(256), 0, ctx->stream, (const u8*)d_enc, n, bits, q[0],
+                               q[1], q[2], q[3], d_out);
+            else hipLaunchKernelGGL(k_env_overlap<0>, dim3(blocks), dim3(256), 0, ctx->stream, (const u8*)d_enc, n, bits, q[0],
                                q[1], q[2], q[3], d_out);
         });
         if (rc) return rc;

@@ -7,7 +7,9 @@
 set -e
 R=$(pwd)
 TAG=${1:-r01}
-ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline"}
+WL=${WL:-c2}
+KERN=${KERN:-k_join2}
+ARGS=${BENCH_ARGS:-"--workload $WL --steps 10 --warmup 2 --no-cpu-baseline"}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -21,4 +23,4 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format c
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -T --output-format csv -d $OUT/sq -o run -- \
     python3 $R/bench.py $ARGS > $OUT/sq_bench.json 2> $OUT/sq_bench.err
 echo "profile done"
-cd $R && python3 scripts/pmc_summary.py $OUT --write-traffic $OUT/traffic_c2.json
+cd $R && python3 scripts/pmc_summary.py $OUT --n ${NPTS:-10000000} --kernel $KERN --write-traffic $OUT/traffic_$WL.json
