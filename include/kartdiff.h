@@ -153,6 +153,13 @@ int kd_fielddiff(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_blobs* new_blo
 /* -------- three-way merge classification -------- */
 int kd_merge3(kd_ctx* ctx, const kd_side* ancestor, const kd_side* ours, const kd_side* theirs,
               uint32_t flags, kd_merge_result** out);
+/* Device form of kd_merge3 (no host sync): all three sides in device memory; d_conflict
+ * [(a.n + o.n + t.n) * 3] <- conflict triples (ancestor, ours, theirs index, 0xFFFFFFFF = absent)
+ * in path order, d_mdelta [(o.n + t.n) * 2] <- merge deltas, d_counts[4] <- clean entries,
+ * conflicts, merge deltas, 0; d_err <- 1 unsorted side, 2 hash key collision, 8 tile overflow. */
+int kd_merge3_device(kd_ctx* ctx, const kd_side* ancestor, const kd_side* ours, const kd_side* theirs,
+                     uint32_t flags, uint32_t* d_conflict, uint32_t* d_mdelta, uint64_t* d_counts,
+                     uint32_t* d_err);
 
 /* -------- spatial -------- */
 /* Per geometry blob (GPKG; length 0 = null geometry):

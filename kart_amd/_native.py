@@ -131,6 +131,11 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
          ctypes.c_uint32, ctypes.POINTER(ctypes.POINTER(KdMergeResult))],
     ),
+    "kd_merge3_device": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
+         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+    ),
     "kd_envelopes": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.POINTER(KdBlobs), c_dblp, ctypes.c_int, ctypes.c_void_p,

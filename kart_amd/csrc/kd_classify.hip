@@ -272,6 +272,59 @@ static int check_side(const kd_side* s, const char* which) {
     return KD_OK;
 }
 
+// classify3 on device-resident sides: conflicts (a, o, t index triples, path order) -> d_conf,
+// merge deltas -> d_md, counts[4] <- clean, conflicts, mdeltas, 0 (zeroed by the caller, with
+// *derr).
+static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
+                         u64* counts, u32* derr) {
+    int rc;
+    const u64 nA = A.n, nO = O.n, nT = T.n;
+    u64 ntiles = (nA + nO + C3_TILE - 1) / C3_TILE;
+    if (ntiles == 0) ntiles = 1;
+    // worst case per tile: everything in theirs lands in one tile -> slot capacity must cover
+    // the tile's own items; we bound by (C3_TILE + 1) * 2 + nT/ntiles*4 and flag overflow (err 8)
+    u64 slot_cap = 2 * (C3_TILE + 2) + (nT / ntiles) * 4 + 64;
+    if (slot_cap > nA + nO + nT + 1) slot_cap = nA + nO + nT + 1;
+    void *bounds, *tcnt, *toff, *sc, *sm;
+    if ((rc = ensure(ctx, "c3.bounds", 3 * (ntiles + 1) * 8, &bounds))) return rc;
+    if ((rc = ensure(ctx, "c3.tcnt", ntiles * 16, &tcnt))) return rc;
+    if ((rc = ensure(ctx, "c3.toff", ntiles * 16, &toff))) return rc;
+    if ((rc = ensure(ctx, "c3.sc", ntiles * slot_cap * 16, &sc))) return rc;
+    if ((rc = ensure(ctx, "c3.sm", ntiles * slot_cap * 8, &sm))) return rc;
+    void* dz;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    const u64* kA = nA ? A.key : (const u64*)dz;  // an empty side points at device zeros
+    const u64* kO = nO ? O.key : (const u64*)dz;
+    const u64* kT = nT ? T.key : (const u64*)dz;
+    rc = launch(ctx, "k_partition3", [&] {
+        hipLaunchKernelGGL(k_partition3, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0, ctx->stream, kA, nA,
+                           kO, nO, kT, nT, ntiles, (u64*)bounds);
+    });
+    if (rc) return rc;
+    Join3Args g;
+    g.A = kA; g.O = kO; g.T = kT;
+    g.oA = (const u32*)A.oid; g.oO = (const u32*)O.oid; g.oT = (const u32*)T.oid;
+    g.nA = nA; g.nO = nO; g.nT = nT;
+    g.nmA = A.name; g.nmO = O.name; g.nmT = T.name;
+    g.noA = A.name_off; g.noO = O.name_off; g.noT = T.name_off;
+    g.hash_mode = A.key_mode == KD_KEY_HASH;
+    g.bounds = (const u64*)bounds;
+    g.stage_conf = (uint4*)sc; g.stage_md = (uint2*)sm; g.slot_cap = slot_cap;
+    g.tile_cnt = (u32*)tcnt; g.err = derr;
+    rc = launch(ctx, "k_join3", [&] {
+        hipLaunchKernelGGL((k_join3<C3_NT>), dim3((unsigned)ntiles), dim3(C3_NT), 0, ctx->stream, g);
+    });
+    if (rc) return rc;
+    rc = launch(ctx, "k_scan3", [&] {
+        hipLaunchKernelGGL((k_scan3<256>), dim3(1), dim3(256), 0, ctx->stream, (const u32*)tcnt, ntiles, (u64*)toff, counts);
+    });
+    if (rc) return rc;
+    return launch(ctx, "k_scatter3", [&] {
+        hipLaunchKernelGGL(k_scatter3, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, (const uint4*)sc,
+                           (const uint2*)sm, slot_cap, (const u32*)tcnt, (const u64*)toff, d_conf, d_md);
+    });
+}
+
 extern "C" {
 
 int kd_reserve(kd_ctx* ctx, uint64_t max_entries_per_side, uint64_t max_updates) {
@@ -356,57 +409,14 @@ int kd_merge3(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_sid
         (rc = stage_side(ctx, theirs, "in.c", &T)))
         return rc;
     const u64 nA = A.n, nO = O.n, nT = T.n;
-    u64 ntiles = (nA + nO + C3_TILE - 1) / C3_TILE;
-    if (ntiles == 0) ntiles = 1;
-    // worst case per tile: everything in theirs lands in one tile -> slot capacity must cover
-    // the tile's own items; we bound by (C3_TILE + 1) * 2 + nT/ntiles*4 and flag overflow (err 8)
-    u64 slot_cap = 2 * (C3_TILE + 2) + (nT / ntiles) * 4 + 64;
-    if (slot_cap > nA + nO + nT + 1) slot_cap = nA + nO + nT + 1;
-    void *bounds, *tcnt, *toff, *sc, *sm, *oc, *om, *dc;
-    if ((rc = ensure(ctx, "c3.bounds", 3 * (ntiles + 1) * 8, &bounds))) return rc;
-    if ((rc = ensure(ctx, "c3.tcnt", ntiles * 16, &tcnt))) return rc;
-    if ((rc = ensure(ctx, "c3.toff", ntiles * 16, &toff))) return rc;
-    if ((rc = ensure(ctx, "c3.sc", ntiles * slot_cap * 16, &sc))) return rc;
-    if ((rc = ensure(ctx, "c3.sm", ntiles * slot_cap * 8, &sm))) return rc;
+    void *oc, *om, *dc;
     if ((rc = ensure(ctx, "c3.oc", (nA + nO + nT + 1) * 12, &oc))) return rc;
     if ((rc = ensure(ctx, "c3.om", (nO + nT + 1) * 8, &om))) return rc;
     if ((rc = ensure(ctx, "c3.counts", 64, &dc))) return rc;
     u64* counts = (u64*)dc;
     u32* derr = (u32*)(counts + 4);
     KD_HIP(hipMemsetAsync(dc, 0, 64, ctx->stream));
-    void* dz;
-    if ((rc = device_zeros(ctx, &dz))) return rc;
-    const u64* kA = nA ? A.key : (const u64*)dz;  // an empty side points at device zeros
-    const u64* kO = nO ? O.key : (const u64*)dz;
-    const u64* kT = nT ? T.key : (const u64*)dz;
-    rc = launch(ctx, "k_partition3", [&] {
-        hipLaunchKernelGGL(k_partition3, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0, ctx->stream, kA, nA,
-                           kO, nO, kT, nT, ntiles, (u64*)bounds);
-    });
-    if (rc) return rc;
-    Join3Args g;
-    g.A = kA; g.O = kO; g.T = kT;
-    g.oA = (const u32*)A.oid; g.oO = (const u32*)O.oid; g.oT = (const u32*)T.oid;
-    g.nA = nA; g.nO = nO; g.nT = nT;
-    g.nmA = A.name; g.nmO = O.name; g.nmT = T.name;
-    g.noA = A.name_off; g.noO = O.name_off; g.noT = T.name_off;
-    g.hash_mode = A.key_mode == KD_KEY_HASH;
-    g.bounds = (const u64*)bounds;
-    g.stage_conf = (uint4*)sc; g.stage_md = (uint2*)sm; g.slot_cap = slot_cap;
-    g.tile_cnt = (u32*)tcnt; g.err = derr;
-    rc = launch(ctx, "k_join3", [&] {
-        hipLaunchKernelGGL((k_join3<C3_NT>), dim3((unsigned)ntiles), dim3(C3_NT), 0, ctx->stream, g);
-    });
-    if (rc) return rc;
-    rc = launch(ctx, "k_scan3", [&] {
-        hipLaunchKernelGGL((k_scan3<256>), dim3(1), dim3(256), 0, ctx->stream, (const u32*)tcnt, ntiles, (u64*)toff, counts);
-    });
-    if (rc) return rc;
-    rc = launch(ctx, "k_scatter3", [&] {
-        hipLaunchKernelGGL(k_scatter3, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, (const uint4*)sc,
-                           (const uint2*)sm, slot_cap, (const u32*)tcnt, (const u64*)toff, (u32*)oc, (uint2*)om);
-    });
-    if (rc) return rc;
+    if ((rc = merge3_device(ctx, A, O, T, (u32*)oc, (uint2*)om, counts, derr))) return rc;
     u64 hc[5];
     KD_HIP(hipMemcpyAsync(hc, dc, 40, hipMemcpyDeviceToHost, ctx->stream));
     KD_HIP(hipStreamSynchronize(ctx->stream));
@@ -430,6 +440,23 @@ int kd_merge3(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_sid
     prof_flush(ctx);
     *out = r;
     return KD_OK;
+}
+
+int kd_merge3_device(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_side* theirs, uint32_t flags,
+                     uint32_t* d_conflict, uint32_t* d_mdelta, uint64_t* d_counts, uint32_t* d_err) {
+    (void)flags;
+    KD_CHECK(ctx && d_conflict && d_mdelta && d_counts && d_err, "kd_merge3_device: NULL");
+    int rc;
+    if ((rc = check_side(anc, "ancestor")) || (rc = check_side(ours, "ours")) || (rc = check_side(theirs, "theirs"))) return rc;
+    KD_CHECK(anc->mem == KD_MEM_DEVICE && ours->mem == KD_MEM_DEVICE && theirs->mem == KD_MEM_DEVICE,
+             "kd_merge3_device: sides must be device memory");
+    KD_CHECK(anc->key_mode == ours->key_mode && ours->key_mode == theirs->key_mode, "kd_merge3_device: key modes differ");
+    KD_CHECK(anc->n < 0xFFFFFFFFull && ours->n < 0xFFFFFFFFull && theirs->n < 0xFFFFFFFFull,
+             "kd_merge3_device: side too large");
+    KD_HIP(hipSetDevice(ctx->device));
+    KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
+    KD_HIP(hipMemsetAsync(d_err, 0, sizeof(u32), ctx->stream));
+    return merge3_device(ctx, *anc, *ours, *theirs, d_conflict, (uint2*)d_mdelta, d_counts, d_err);
 }
 
 }  // extern "C"

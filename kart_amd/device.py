@@ -111,3 +111,32 @@ class DiffPipeline:
         masks = self.masks[: nu * self.maps.words].cpu().numpy().view(np.uint64).reshape(nu, self.maps.words)
         status = self.status[:nu].cpu().numpy()
         return {"inserts": int(c[0]), "updates": nu, "deletes": int(c[2]), "deltas": nd}, delta, upd, masks, status
+
+
+class MergePipeline:
+    """classify3 (three-way merge classification) over device-resident sides (one GPU)."""
+
+    def __init__(self, engine, ancestor, ours, theirs, device):
+        self.eng = engine
+        self.S = [DevSide(x, device) for x in (ancestor, ours, theirs)]
+        self._s = [x.kd_side() for x in self.S]
+        na, no, nt = ancestor.n, ours.n, theirs.n
+        self.conf = torch.empty(3 * (na + no + nt + 1), dtype=torch.int32, device=device)
+        self.md = torch.empty(2 * (no + nt + 1), dtype=torch.int32, device=device)
+        self.counts = torch.zeros(8, dtype=torch.int64, device=device)  # [0..3] counts, [4] err
+
+    def step(self):
+        L, ctx = self.eng.L, self.eng.ctx
+        N.check(L.kd_merge3_device(ctx, ctypes.byref(self._s[0]), ctypes.byref(self._s[1]), ctypes.byref(self._s[2]), 0,
+                                   self.conf.data_ptr(), self.md.data_ptr(), self.counts.data_ptr(),
+                                   self.counts.data_ptr() + 4 * 8), "kd_merge3_device")
+
+    def results(self):
+        """host copies (after a sync): n_clean, conflicts [n,3], merge deltas [m,2]"""
+        c = self.counts.cpu().numpy()
+        if c[4]:
+            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flag {int(c[4])}")
+        nc, nm = int(c[1]), int(c[2])
+        conf = self.conf[: 3 * nc].cpu().numpy().view(np.uint32).reshape(nc, 3)
+        md = self.md[: 2 * nm].cpu().numpy().view(np.uint32).reshape(nm, 2)
+        return int(c[0]), conf, md

@@ -248,3 +248,109 @@ def geometry_layer(n, seed=SEED, frac_point=0.3):
     rec[:, 45:49] = np.array([1], "<u4").view(np.uint8)
     data[(start[qi, None] + np.arange(49, dtype=np.uint64)[None, :]).ravel()] = rec.ravel()
     return data, off, is_pt
+
+
+# ---------------------------------------------------------------------------------------------
+# C4: string-PK attribute table, three-way merge (ancestor / ours / theirs)
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class Merge3Layer:
+    ancestor: packing.PackedSide
+    ours: packing.PackedSide
+    theirs: packing.PackedSide
+    n_conflict: int  # libgit2 rule over the generator's plan (o == t -> o; a == o -> t; a == t -> o)
+
+
+def _hash_paths(ids):
+    """MsgpackHashPathEncoder paths (dataset3_paths.py:202-215, 4 levels x 64 branches, base64) of the
+    string pks 'R%09d' % id: 'c/c/c/c/' + urlsafe_b64(msgpack([pk])) — 24 bytes each, [n, 24] uint8."""
+    import base64
+    import hashlib
+
+    ids = np.asarray(ids, np.int64)
+    n = ids.size
+    digits = np.char.zfill(ids.astype("U9"), 9)
+    packed = np.zeros((n, 12), np.uint8)  # 91 aa 'R' + 9 digits  == msgpack(['R%09d'])
+    packed[:, 0], packed[:, 1], packed[:, 2] = 0x91, 0xAA, ord("R")
+    packed[:, 3:] = np.frombuffer("".join(digits.tolist()).encode(), np.uint8).reshape(n, 9)
+    alpha = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_", np.uint8)
+    # filename: urlsafe base64 of 12 bytes = 16 chars, vectorised (4 groups of 3 bytes)
+    g = packed.reshape(n, 4, 3).astype(np.uint32)
+    v = g[:, :, 0] << 16 | g[:, :, 1] << 8 | g[:, :, 2]
+    fn = np.stack([(v >> 18) & 63, (v >> 12) & 63, (v >> 6) & 63, v & 63], 2).reshape(n, 16)
+    out = np.empty((n, 24), np.uint8)
+    out[:, 8:] = alpha[fn]
+    # tree: first 24 bits of sha256(packed) as 4 base64 chars (b64hash, serialise_util.py:82-85)
+    rows = packed.tobytes()
+    h = np.frombuffer(b"".join(hashlib.sha256(rows[12 * i:12 * i + 12]).digest()[:3] for i in range(n)),
+                      np.uint8).reshape(n, 3).astype(np.uint32)
+    hv = h[:, 0] << 16 | h[:, 1] << 8 | h[:, 2]
+    for k in range(4):
+        out[:, 2 * k] = alpha[(hv >> (18 - 6 * k)) & 63]
+        out[:, 2 * k + 1] = ord("/")
+    return out
+
+
+def _pack_fixed(paths, oids):
+    """PackedSide (KD_KEY_HASH) of fixed-width relative paths [n, w] + OIDs [n, 20], vectorised"""
+    from . import _native as N
+
+    n, w = paths.shape
+    flat = np.ascontiguousarray(paths).reshape(-1)
+    off = np.arange(n + 1, dtype=np.uint64) * np.uint64(w)
+    keys = np.empty(n, np.uint64)
+    status = np.empty(n, np.uint8)
+    bad = N.lib().kd_pack_hash_keys(N.ptr(flat), N.ptr(off), n, 4, 0, N.ptr(keys), N.ptr(status))
+    if bad:
+        raise packing.PackError(f"{bad} synthetic paths not packable")
+    order = np.argsort(keys, kind="stable")
+    keys = keys[order]
+    if n > 1 and not np.all(keys[1:] > keys[:-1]):
+        raise packing.PackError("synthetic key collision")
+    s = packing.PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(oids[order]),
+                           key_mode=N.KD_KEY_HASH, order=order.astype(np.int64), encoding=packing.GENERAL_ENCODING)
+    s.name = np.ascontiguousarray(paths[order]).reshape(-1)
+    s.name_off = off
+    return s
+
+
+def table3_layers(n, seed=SEED, p_mod=0.02, p_del=0.005, p_ins=0.005, p_same=0.001, p_addadd=0.0005):
+    """Ancestor of n string-PK rows and two independently edited descendants.  Per ancestor row each
+    side keeps / modifies / deletes it; a fraction is modified identically on both (clean); both
+    sides insert new rows, some with the same pk on both (add/add, half identical)."""
+    rng = np.random.default_rng(seed)
+    ids = np.arange(n, dtype=np.int64)
+    act = []  # per side: 0 keep, 1 modify, 2 delete
+    for _ in range(2):
+        u = rng.random(n)
+        act.append(np.where(u < p_mod, 1, np.where(u < p_mod + p_del, 2, 0)).astype(np.int8))
+    same = rng.random(n) < p_same  # both modify to the same new content
+    act[0][same] = 1
+    act[1][same] = 1
+    n_ins = int(n * p_ins)
+    n_aa = int(n * p_addadd)
+    ins_o = n + np.arange(n_ins)
+    ins_t = n + n_ins + np.arange(n_ins)
+    aa = n + 2 * n_ins + np.arange(n_aa)  # inserted on both sides
+    aa_same = rng.random(n_aa) < 0.5
+    paths_all = _hash_paths(np.concatenate([ids, ins_o, ins_t, aa]))
+    P = lambda x: paths_all[x]  # ids are 0..total-1 in that order
+    anc = _pack_fixed(P(ids), synth_oids(ids, 0))
+
+    def side(k, ins, ver):
+        keep = act[k] != 2
+        v = np.where(act[k] == 1, ver, 0).astype(np.uint64)
+        v[same] = 3
+        rows = ids[keep]
+        oid = synth_oids(rows, v[keep])
+        aav = np.where(aa_same, 3, ver).astype(np.uint64)
+        sel = np.concatenate([rows, ins, aa])
+        oids = np.concatenate([oid, synth_oids(ins, ver), synth_oids(aa, aav)])
+        return _pack_fixed(P(sel), oids)
+
+    ours = side(0, ins_o, 1)
+    theirs = side(1, ins_t, 2)
+    a0, a1 = act
+    conflict_rows = ((a0 == 1) & (a1 == 1) & ~same) | ((a0 == 1) & (a1 == 2)) | ((a0 == 2) & (a1 == 1))
+    n_conflict = int(conflict_rows.sum()) + int((~aa_same).sum())
+    return Merge3Layer(anc, ours, theirs, n_conflict)

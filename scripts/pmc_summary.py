@@ -57,7 +57,7 @@ def main():
         fetch_kb, write_kb = cs.get("FETCH_SIZE"), cs.get("WRITE_SIZE")
         if fetch_kb is None or write_kb is None:
             sys.exit("FETCH_SIZE / WRITE_SIZE missing")
-        tj = {"kernel": a.kernel, "n_points": a.n, "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+        tj = {"kernel": a.kernel, "n_units": a.n, "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
               "hbm_bytes_per_launch": int(round((2 * fetch_kb + write_kb) * 1024)),
               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH doubled (gfx950)"}
         with open(a.write_traffic, "w") as f:

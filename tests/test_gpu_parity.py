@@ -276,3 +276,27 @@ def test_gpu_envelopes_c5_layer_vs_oracle(engine, n, seed):
     om, oe, ok, oc = O.envelope_batch(data, off, synth.C5_FILTER, 20)
     assert np.array_equal(gm, om) and np.array_equal(gk, ok) and np.array_equal(ge, oe) and gc == oc
     assert 0 < gc < n
+
+
+@pytest.mark.parametrize("n", [1000, 400_000])
+def test_gpu_merge3_device_c4_layer_vs_oracle(engine, n):
+    """the C4 bench layer (string PKs, MsgpackHashPathEncoder paths, mod/mod, mod/del, del/mod and
+    add/add edits) through the device-resident kd_merge3_device pipeline bench.py times, and the host
+    kd_merge3: conflicts and merge deltas bit-exact with the oracle, conflicts = the generator's plan"""
+    import torch
+
+    from kart_amd import synth
+    from kart_amd.device import MergePipeline
+
+    M = synth.table3_layers(n, seed=n)
+    pipe = MergePipeline(engine, M.ancestor, M.ours, M.theirs, torch.device("cuda", 0))
+    for _ in range(2):  # repeated steps reuse the workspaces and counters
+        pipe.step()
+    engine.sync()
+    n_clean, conf, md = pipe.results()
+    oc, om, ocl = O.classify3(M.ancestor.key, M.ancestor.oid, M.ours.key, M.ours.oid, M.theirs.key, M.theirs.oid)
+    key = lambda rows: sorted(map(tuple, np.asarray(rows).tolist()))
+    assert key(conf) == key(oc) and key(md) == key(om) and n_clean == ocl
+    assert conf.shape[0] == M.n_conflict
+    r = engine.merge3(M.ancestor, M.ours, M.theirs)
+    assert key(r.conflict) == key(oc) and key(r.mdelta) == key(om)
