@@ -9,7 +9,8 @@ k_join2, k_place2), then the msgpack field decode + Python-== column compare of 
 (k_fielddiff) — all on the device, inputs resident in HBM before the timed region.
 
 --workload c4 (BASELINE configs[3]): a 50M-row string-PK table per GPU (MsgpackHashPathEncoder paths)
-three-way merge classification: ancestor/ours/theirs join + the libgit2 conflict rule (k_join3).
+three-way merge classification: classify2(ours, theirs) + k_resolve3 (ancestor lookup + the libgit2
+conflict rule) over the paths where ours and theirs differ.
 
 --workload c5 (BASELINE configs[4], scaled: --n geometries per GPU, default 20M): GPKG geometry
 blobs of a spatially filtered layer (synth.geometry_layer); one step = k_envelopes (header /
@@ -365,19 +366,23 @@ def run_c4(args, D):
     if not args.no_check:  # the generator's own plan (libgit2 rule over planned edits)
         assert conf.shape[0] == M.n_conflict, (conf.shape[0], M.n_conflict)
     eng.prof_reset()
-    eng.prof_select(None if args.time_all else ["k_join3"])
+    eng.prof_select(None if args.time_all else ["k_join2"])
     eng.prof_enable(not args.no_events)
     cnt = torch.zeros(1, dtype=torch.int64, device=D.dev)
     gathered = [torch.empty_like(cnt) for _ in range(D.world)]
     elapsed = D.timed(pipe.step, args.steps, lambda: D.dist.all_gather(gathered, cnt))
     eng.prof_enable(False)
     (total,) = D.total(A.n + O_.n + T.n)
-    kern = kernel_times(eng, ("k_partition3", "k_join3", "k_scan3", "k_scatter3"))
+    kern = kernel_times(eng, ("k_sorted3", "k_partition2", "k_join2", "k_place2", "k_resolve3"))
     nall = A.n + O_.n + T.n
-    # algorithmic bytes per k_join3 launch: every key + OID once (28 B), every filename once (hash
-    # keys are verified against the names: 24 B here), conflict triples (12 B) and merge deltas (8 B)
-    alg = 28 * nall + int(A.name.size + O_.name.size + T.name.size) + 12 * conf.shape[0] + 8 * md.shape[0]
-    roof = roofline(kern, "k_join3", alg, args.traffic_json, "n_rows", n)
+    # classify3 = classify2(ours, theirs) + k_resolve3 over the paths where they differ.
+    # Dominant kernel k_join2, algorithmic bytes per launch: every ours/theirs key + OID once (28 B),
+    # every ours/theirs filename once (hash keys are verified against the names) and one 8-B record
+    # per differing path
+    _, io, it = np.intersect1d(O_.key, T.key, assume_unique=True, return_indices=True)
+    n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((O_.oid[io] != T.oid[it]).any(axis=1)))
+    alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand
+    roof = roofline(kern, "k_join2", alg, args.traffic_json, "n_rows", n)
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -416,7 +421,8 @@ def run_c4(args, D):
         "config": {"workload": f"C4: {n}-row string-PK table per GPU, three-way merge classification "
                                "(ancestor/ours/theirs join + libgit2 conflict rule)",
                    "rows_per_gpu": n, "entries_per_step": total, "conflicts": int(conf.shape[0]),
-                   "merge_deltas": int(md.shape[0]), "parallelism": f"independent shards x{D.world}"},
+                   "merge_deltas": int(md.shape[0]), "differing_paths": n_cand,
+                   "parallelism": f"independent shards x{D.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
         "roofline": roof,
         "cpu_baseline": cpu,

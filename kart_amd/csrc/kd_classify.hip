@@ -16,227 +16,248 @@
 namespace kd {
 
 // ============================================================================================
-// classify3
+// classify3 = classify2(ours, theirs) + k_resolve3 over the ours/theirs deltas
 // ============================================================================================
+// libgit2's per-path rule (o == t -> o; a == o -> t; a == t -> o; else conflict) only needs the
+// ancestor where ours and theirs differ: every path with o == t is clean and takes ours.  So the
+// three-way merge is (1) the two-way join of ours against theirs (k_partition2/k_join2/k_place2,
+// which also verify hash-mode filenames of every matched pair), giving the key-ordered list of
+// paths where they differ (~2 x the edit rate of the entries), then (2) k_resolve3: per differing
+// path, look the key up in the ancestor, compare the OIDs, apply the rule and compact conflicts and
+// merge deltas in key order with a decoupled look-back.  The ancestor's keys are read only along
+// the lookups' paths and its OIDs only where a path differs; k_sorted3 checks it is strictly
+// ascending (one streaming pass over its keys).
 constexpr int C3_NT = 256;
-constexpr int C3_TILE = 2048;   // ancestor∪ours items per tile (before equal-key adjustment)
-constexpr int C3_CAP = 3072;    // LDS keys per array chunk
+constexpr int C3_CH = 1024;  // differing paths per resolve chunk (4 per thread, contiguous)
+constexpr int C3_SAMPLE_BITS = 10;
+constexpr int C3_SAMPLES = 1 << C3_SAMPLE_BITS;  // ancestor keys sampled per chunk bracket (LDS)
 
-// tile boundary keys: bkey[t] = key at union position t*C3_TILE of ancestor∪ours (0 for t=0,
-// UINT64_MAX sentinel for t=ntiles); then lower_bound of bkey in each array.
-__global__ void k_partition3(const u64* __restrict__ A, u64 nA, const u64* __restrict__ O, u64 nO,
-                             const u64* __restrict__ T, u64 nT, u64 ntiles, u64* __restrict__ bounds /*[3*(ntiles+1)]*/) {
-    u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    u64 ba, bo, bt;
-    if (t == 0) { ba = bo = bt = 0; }
-    else if (t == ntiles) { ba = nA; bo = nO; bt = nT; }
-    else {
-        u64 total = nA + nO, d = t * (u64)C3_TILE;
-        if (d > total) d = total;
-        u64 lo = d > nO ? d - nO : 0, hi = d < nA ? d : nA;
-        while (lo < hi) {
-            u64 mid = (lo + hi) >> 1;
-            if (A[mid] <= O[d - 1 - mid]) lo = mid + 1;
-            else hi = mid;
-        }
-        u64 i = lo, j = d - lo;
-        // boundary key = smallest key not yet consumed
-        u64 key = UINT64_MAX;
-        if (i < nA && A[i] < key) key = A[i];
-        if (j < nO && O[j] < key) key = O[j];
-        // lower bounds of key in each array
-        auto lb = [key](const u64* X, u64 n) {
-            u64 l = 0, h = n;
-            while (l < h) { u64 m = (l + h) >> 1; if (X[m] < key) l = m + 1; else h = m; }
-            return l;
-        };
-        ba = key == UINT64_MAX ? nA : lb(A, nA);
-        bo = key == UINT64_MAX ? nO : lb(O, nO);
-        bt = key == UINT64_MAX ? nT : lb(T, nT);
-    }
-    bounds[3 * t + 0] = ba;
-    bounds[3 * t + 1] = bo;
-    bounds[3 * t + 2] = bt;
-}
-
-__device__ __forceinline__ int lds_find(const u64* s, int n, u64 key) {
-    int l = 0, h = n;
-    while (l < h) { int m = (l + h) >> 1; if (s[m] < key) l = m + 1; else h = m; }
-    return (l < n && s[l] == key) ? l : -1;
-}
-
-struct Join3Args {
+struct Resolve3Args {
     const u64 *A, *O, *T;
     const u32 *oA, *oO, *oT;
-    u64 nA, nO, nT;
+    u64 nA, nO;
     const u8 *nmA, *nmO, *nmT;
     const u64 *noA, *noO, *noT;
     int hash_mode;
-    const u64* bounds;
-    uint4* stage_conf;   // (a, o, t, 0) per conflict, tile slot capacity = slot_cap
-    uint2* stage_md;     // (o, t) per merge delta
-    u64 slot_cap;
-    u32* tile_cnt;       // [ntiles*4]: clean, conflicts, mdeltas, overflow
+    const uint2* cand;      // classify2(ours, theirs) delta list: (ours | NONE, theirs | NONE)
+    const u64* c2;          // its counts: inserts, updates, deletes, deltas
+    u64* desc;              // look-back descriptors [2][nchunk]
+    u64 nchunk;
+    u32* aux;               // [0] chunk ticket, [1] ancestor-order error (k_sorted3)
+    u32* out_conf;          // (a, o, t) per conflict
+    uint2* out_md;          // (o, t) per merge delta
+    u64* counts;            // clean, conflicts, mdeltas, 0
     u32* err;
 };
 
-// rule: 0 ours, 1 theirs, 2 conflict.  x==y includes both absent.
-__device__ __forceinline__ int merge_rule(const u32* a, const u32* o, const u32* t) {
-    auto eq = [](const u32* x, const u32* y) { return (!x && !y) || (x && y && !oid_ne(x, y)); };
-    if (eq(o, t)) return 0;
-    if (eq(a, o)) return 1;
-    if (eq(a, t)) return 0;
-    return 2;
+// ancestor strictly ascending (-> aux[1]), and the resolve's counters zeroed
+__global__ __launch_bounds__(256) void k_sorted3(const u64* __restrict__ A, u64 nA, u64* __restrict__ desc, u64 ndesc,
+                                                 u32* __restrict__ aux, u64* __restrict__ counts) {
+    const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x, stride = (u64)gridDim.x * blockDim.x;
+    if (tid == 0) {
+        aux[0] = 0;  // (aux[1] is cleared by the k_resolve3 that consumes it)
+        counts[0] = counts[1] = counts[2] = counts[3] = 0;
+    }
+    for (u64 k = tid; k < ndesc; k += stride) desc[k] = 0;
+    u32 bad = 0;
+    // pairs (2i, 2i+1), and (2i+1, 2i+2) with the next pair's first key
+    const u64 np = nA / 2;
+    for (u64 p = tid; p < np; p += stride) {
+        const u64 x = A[2 * p], y = A[2 * p + 1];  // (the side may start at any 8-B offset)
+        bad |= x >= y;
+        if (2 * p + 2 < nA) bad |= y >= A[2 * p + 2];
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(aux + 1, 1u);
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void k_join3(Join3Args g) {
-    __shared__ u64 sA[C3_CAP], sO[C3_CAP], sT[C3_CAP];
-    __shared__ u32 s_wave[NT / 64];
-    const u64 tile = blockIdx.x;
-    const int tid = threadIdx.x;
-    const u64 a0 = g.bounds[3 * tile], o0 = g.bounds[3 * tile + 1], t0 = g.bounds[3 * tile + 2];
-    const u64 a1 = g.bounds[3 * tile + 3], o1 = g.bounds[3 * tile + 4], t1 = g.bounds[3 * tile + 5];
-    u32 clean = 0;
-    u32 base_c = 0, base_m = 0;  // running output offsets within the tile slot
-    if (a1 < a0 || o1 < o0 || t1 < t0) {
-        if (tid == 0) atomicOr(g.err, 1u);
-        if (tid == 0) { u32* c = g.tile_cnt + 4 * tile; c[0] = c[1] = c[2] = 0; c[3] = 0; }
-        return;
-    }
-    // process the tile's key range in sub-ranges that fit LDS: walk by key windows cut on the
-    // array with most items left.
-    u64 ca = a0, co = o0, ct = t0;
-    u32 overflow = 0;
-    uint4* sc = g.stage_conf + tile * g.slot_cap;
-    uint2* sm = g.stage_md + tile * g.slot_cap;
-    while (ca < a1 || co < o1 || ct < t1) {
-        // window end key: min over arrays of the key at position cur + CAP (exclusive bound)
-        u64 wend = UINT64_MAX;
-        bool bounded = false;
-        if (a1 - ca > C3_CAP) { u64 k = g.A[ca + C3_CAP]; if (k < wend) wend = k; bounded = true; }
-        if (o1 - co > C3_CAP) { u64 k = g.O[co + C3_CAP]; if (k < wend) wend = k; bounded = true; }
-        if (t1 - ct > C3_CAP) { u64 k = g.T[ct + C3_CAP]; if (k < wend) wend = k; bounded = true; }
-        // counts of items < wend in each array (items within the first CAP of each array)
-        __syncthreads();
-        auto load = [&](const u64* X, u64 cur, u64 end, u64* s) -> int {
-            u64 lim = end - cur < (u64)C3_CAP ? end - cur : (u64)C3_CAP;
-            for (u64 x = tid; x < lim; x += NT) s[x] = X[cur + x];
-            return (int)lim;
-        };
-        int la = load(g.A, ca, a1, sA), lo_ = load(g.O, co, o1, sO), lt = load(g.T, ct, t1, sT);
-        __syncthreads();
-        auto cut = [&](const u64* s, int n) {
-            if (!bounded) return n;
-            int l = 0, h = n;
-            while (l < h) { int m = (l + h) >> 1; if (s[m] < wend) l = m + 1; else h = m; }
-            return l;
-        };
-        const int na = cut(sA, la), no = cut(sO, lo_), nt = cut(sT, lt);
-        // strict ascending check (within window; window seams are checked via the next window's
-        // first item against the last consumed one by the partition kernel's sortedness)
-        for (int x = tid + 1; x < na; x += NT) if (sA[x - 1] >= sA[x]) atomicOr(g.err, 1u);
-        for (int x = tid + 1; x < no; x += NT) if (sO[x - 1] >= sO[x]) atomicOr(g.err, 1u);
-        for (int x = tid + 1; x < nt; x += NT) if (sT[x - 1] >= sT[x]) atomicOr(g.err, 1u);
-
-        // three passes (ancestor-anchored, ours-only, theirs-only), each an ordered compaction
-        for (int pass = 0; pass < 3; pass++) {
-            const int n = pass == 0 ? na : pass == 1 ? no : nt;
-            for (int base = 0; base < n; base += NT) {
-                int x = base + tid;
-                int res = -1;  // -1 nothing; 0 ours (clean) ; 1 theirs (mdelta) ; 2 conflict
-                u32 ia = KD_NONE, io = KD_NONE, it = KD_NONE;
-                bool present_clean = false;
-                if (x < n) {
-                    u64 key = pass == 0 ? sA[x] : pass == 1 ? sO[x] : sT[x];
-                    int pa = pass == 0 ? x : lds_find(sA, na, key);
-                    int po = pass == 1 ? x : lds_find(sO, no, key);
-                    int pt = pass == 2 ? x : lds_find(sT, nt, key);
-                    bool owner = pass == 0 || (pass == 1 && pa < 0) || (pass == 2 && pa < 0 && po < 0);
-                    if (owner) {
-                        if (pa >= 0) ia = (u32)(ca + pa);
-                        if (po >= 0) io = (u32)(co + po);
-                        if (pt >= 0) it = (u32)(ct + pt);
-                        const u32* xa = pa >= 0 ? g.oA + (u64)ia * 5 : nullptr;
-                        const u32* xo = po >= 0 ? g.oO + (u64)io * 5 : nullptr;
-                        const u32* xt = pt >= 0 ? g.oT + (u64)it * 5 : nullptr;
-                        if (g.hash_mode) {
-                            if (xa && xo && !names_eq(g.nmA, g.noA, ia, g.nmO, g.noO, io)) atomicOr(g.err, 2u);
-                            if (xa && xt && !names_eq(g.nmA, g.noA, ia, g.nmT, g.noT, it)) atomicOr(g.err, 2u);
-                            if (xo && xt && !names_eq(g.nmO, g.noO, io, g.nmT, g.noT, it)) atomicOr(g.err, 2u);
-                        }
-                        res = merge_rule(xa, xo, xt);
-                        present_clean = (res == 0 && xo) || (res == 1 && xt);
-                    }
-                }
-                clean += present_clean ? 1 : 0;
-                u32 fc = res == 2 ? 1 : 0, fm = res == 1 ? 1 : 0;
-                u32 totp;
-                u32 offp = block_excl_scan<NT>(fc | (fm << 16), s_wave, &totp);
-                u32 oc = base_c + (offp & 0xFFFF), om = base_m + (offp >> 16);
-                if (fc) { if (oc < g.slot_cap) sc[oc] = make_uint4(ia, io, it, 0); else overflow = 1; }
-                if (fm) { if (om < g.slot_cap) sm[om] = make_uint2(io, it); else overflow = 1; }
-                base_c += totp & 0xFFFF;
-                base_m += totp >> 16;
+// smallest index in [0, n) with X[index] >= key (n if none), for one key per 32-lane half-wave:
+// 32 probes per round, ~6 rounds for 50M keys
+__device__ __forceinline__ u64 half_lower_bound(const u64* __restrict__ X, u64 n, u64 key) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
+    u64 lo = 0, hi = n;  // answer in [lo, hi]
+    while (__ballot(lo < hi)) {
+        const u64 span = hi - lo, step = (span + 31) / 32;
+        const u64 p = lo + (u64)l * step;
+        const bool probe = lo < hi && p < hi;
+        const bool below = probe && X[p] < key;
+        const u32 c = __popc((u32)(__ballot(below) >> (32 * h)));
+        if (lo < hi) {
+            if (c == 0) hi = lo;
+            else {
+                const u64 nlo = lo + (u64)(c - 1) * step + 1, nhi = lo + (u64)c * step;
+                lo = nlo;
+                hi = nhi < hi ? nhi : hi;
             }
         }
-        ca += na; co += no; ct += nt;
-        if (na == 0 && no == 0 && nt == 0) { if (tid == 0) atomicOr(g.err, 4u); break; }  // no progress
     }
-    u32 tclean = block_sum<NT>(clean, s_wave);
-    u32 tov = block_sum<NT>(overflow, s_wave);
-    if (tid == 0) {
-        u32* c = g.tile_cnt + 4 * tile;
-        c[0] = tclean;
-        c[1] = base_c;
-        c[2] = base_m;
-        c[3] = tov;
-        if (tov) atomicOr(g.err, 8u);
-    }
+    return lo;
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_scan3(const u32* __restrict__ tile_cnt, u64 ntiles,
-                                              u64* __restrict__ tile_off, u64* __restrict__ counts) {
-    // single thread per lane-chunk serial scan is enough here (ntiles ~ 1e4..1e5)
-    __shared__ u64 s_sum[3][NT];
-    u64 per = (ntiles + NT - 1) / NT;
-    u64 b = threadIdx.x * per, e = b + per < ntiles ? b + per : ntiles;
-    u64 c0 = 0, c1 = 0, c2 = 0;
-    for (u64 t = b; t < e; t++) { c0 += tile_cnt[4 * t]; c1 += tile_cnt[4 * t + 1]; c2 += tile_cnt[4 * t + 2]; }
-    s_sum[0][threadIdx.x] = c0; s_sum[1][threadIdx.x] = c1; s_sum[2][threadIdx.x] = c2;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        u64 r0 = 0, r1 = 0, r2 = 0;
-        for (int i = 0; i < NT; i++) {
-            u64 x0 = s_sum[0][i], x1 = s_sum[1][i], x2 = s_sum[2][i];
-            s_sum[0][i] = r0; s_sum[1][i] = r1; s_sum[2][i] = r2;
-            r0 += x0; r1 += x1; r2 += x2;
+__global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
+    constexpr int PT = C3_CH / NT;
+    constexpr int NS = C3_SAMPLES;
+    __shared__ u32 s_wave[NT / 64];
+    __shared__ u64 s_b[4];  // ticket, bracket lo, bracket hi, -
+    __shared__ u64 s_ex[2];
+    __shared__ u64 s_smp[NS];  // ancestor keys at NS evenly spaced bracket positions
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 n = g.c2[3];
+    while (true) {
+        if (tid == 0) s_b[0] = atomicAdd(g.aux, 1u);
+        __syncthreads();
+        const u64 t = s_b[0];
+        if (t == 0 && tid == 0) {  // paths where ours == theirs: clean, and the ancestor-order check
+            atomicAdd((unsigned long long*)g.counts, (unsigned long long)(g.nO - g.c2[1] - g.c2[2]));
+            if (g.aux[1]) { atomicOr(g.err, 1u); g.aux[1] = 0; }  // consumed: k_sorted3 only sets it
         }
-        counts[0] = r0; counts[1] = r1; counts[2] = r2;
+        const u64 base = t * C3_CH;
+        if (base >= n) break;
+        const u32 cnt = (u32)(n - base < (u64)C3_CH ? n - base : (u64)C3_CH);
+        auto key_of = [&](uint2 r) { return *(r.x != KD_NONE ? g.O + r.x : g.T + r.y); };  // one load
+        // the chunk's ancestor bracket: [lower_bound(first key), lower_bound(last key) + 1)
+        if (wid == 0) {
+            const u64 k = key_of(g.cand[base + (lane < 32 ? 0 : cnt - 1)]);
+            const u64 p = half_lower_bound(g.A, g.nA, k);
+            if (lane == 0) s_b[1] = p;
+            if (lane == 32) s_b[2] = p < g.nA ? p + 1 : g.nA;
+        }
+        uint2 rec[PT];
+        u64 key[PT];
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const u32 r = tid * PT + j;
+            rec[j] = r < cnt ? g.cand[base + r] : make_uint2(KD_NONE, KD_NONE);
+        }
+#pragma unroll
+        for (int j = 0; j < PT; j++) key[j] = (tid * PT + j < cnt) ? key_of(rec[j]) : 0;
+        __syncthreads();
+        const u32 blo = (u32)s_b[1], bhi = (u32)s_b[2];
+        const u32 span = bhi - blo;
+        // sample level: NS keys at positions blo + s*span/NS in LDS (one gather), each key's
+        // sub-bracket from an LDS search, then the global search inside it (~log2(span/NS) rounds)
+        for (int x = tid; x < NS; x += NT) {
+            const u32 pos = blo + (u32)(((u64)x * span) / NS);
+            s_smp[x] = pos < bhi ? g.A[pos] : ~0ull;
+        }
+        __syncthreads();
+        u32 lo[PT], hi[PT];
+        bool found[PT];
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            // c = number of samples < key: lower_bound lies in (pos(c-1), pos(c)]
+            int l = 0, h = NS;
+#pragma unroll
+            for (int r = 0; r < C3_SAMPLE_BITS + 1; r++) {
+                const int m = (l + h) >> 1;
+                const bool act = l < h;
+                const bool lt = s_smp[m < NS ? m : NS - 1] < key[j];
+                l = act && lt ? m + 1 : l;
+                h = act && !lt ? m : h;
+            }
+            lo[j] = l == 0 ? blo : blo + (u32)(((u64)(l - 1) * span) / NS) + 1;
+            hi[j] = l == NS ? bhi : blo + (u32)(((u64)l * span) / NS);
+            found[j] = l < NS && s_smp[l] == key[j];
+            if (found[j]) lo[j] = hi[j];  // the sample itself is the match
+        }
+        u32 sub = 0;
+#pragma unroll
+        for (int j = 0; j < PT; j++) sub = max(sub, hi[j] - lo[j]);
+        const int rounds = sub ? 32 - __clz(sub) : 0;
+        for (int it = 0; it < rounds; it++) {
+            u64 v[PT];
+            u32 m[PT];
+#pragma unroll
+            for (int j = 0; j < PT; j++) {
+                m[j] = (lo[j] + hi[j]) >> 1;
+                v[j] = g.A[m[j] < g.nA ? m[j] : 0];
+            }
+#pragma unroll
+            for (int j = 0; j < PT; j++) {
+                const bool act = lo[j] < hi[j];
+                const bool lt = v[j] < key[j];
+                found[j] |= act && v[j] == key[j];
+                lo[j] = act && lt ? m[j] + 1 : lo[j];
+                hi[j] = act && !lt ? m[j] : hi[j];
+            }
+        }
+        // every OID of the chunk's paths loaded before any compare
+        u32 ia[PT], io[PT], itt[PT];
+        u32 xa[PT][5], xo[PT][5], xt[PT][5];
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            ia[j] = found[j] ? lo[j] : KD_NONE;
+            io[j] = rec[j].x;
+            itt[j] = rec[j].y;
+            const u32* qa = g.oA + (u64)(ia[j] != KD_NONE ? ia[j] : 0) * 5;
+            const u32* qo = g.oO + (u64)(io[j] != KD_NONE ? io[j] : 0) * 5;
+            const u32* qt = g.oT + (u64)(itt[j] != KD_NONE ? itt[j] : 0) * 5;
+#pragma unroll
+            for (int w = 0; w < 5; w++) { xa[j][w] = qa[w]; xo[j][w] = qo[w]; xt[j][w] = qt[w]; }
+        }
+        if (g.hash_mode) {  // a matched ancestor path must carry the same filename
+            u32 act_o = 0, act_t = 0;
+#pragma unroll
+            for (int j = 0; j < PT; j++) {
+                act_o |= (u32)(ia[j] != KD_NONE && io[j] != KD_NONE) << j;
+                // with ours present, theirs' name = ours' (classify2 checked the matched pair) = the
+                // ancestor's (checked here): only ancestor-and-theirs-without-ours needs its own check
+                act_t |= (u32)(ia[j] != KD_NONE && itt[j] != KD_NONE && io[j] == KD_NONE) << j;
+            }
+            if (names_ne_batch<PT, 8>(g.nmA, g.noA, ia, g.nmO, g.noO, io, act_o) |
+                names_ne_batch<PT, 8>(g.nmA, g.noA, ia, g.nmT, g.noT, itt, act_t))
+                atomicOr(g.err, 2u);
+        }
+        u32 fc = 0, fm = 0, clean = 0;
+        u32 cls[PT];
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const bool valid = tid * PT + j < cnt;
+            const bool pa = ia[j] != KD_NONE, po = io[j] != KD_NONE, pt = itt[j] != KD_NONE;
+            auto same = [](const u32* x, const u32* y) {
+                return ((x[0] ^ y[0]) | (x[1] ^ y[1]) | (x[2] ^ y[2]) | (x[3] ^ y[3]) | (x[4] ^ y[4])) == 0;
+            };
+            // ours != theirs here (classify2 emitted the path), so the rule reduces to two tests
+            const bool a_eq_o = pa == po && (!pa || same(xa[j], xo[j]));
+            const bool a_eq_t = pa == pt && (!pa || same(xa[j], xt[j]));
+            u32 c = a_eq_o ? 1u : a_eq_t ? 0u : 2u;  // 0 ours (clean), 1 theirs (merge delta), 2 conflict
+            if (!valid) c = 3;
+            cls[j] = c;
+            fc += c == 2;
+            fm += c == 1;
+            clean += (c == 0 && po) || (c == 1 && pt);
+        }
+        u32 tot;
+        const u32 off = block_excl_scan<NT>(fc | (fm << 16), s_wave, &tot);
+        const u32 tc = tot & 0xFFFF, tm = tot >> 16;
+        const u32 tclean = block_sum<NT>(clean, s_wave);
+        if (wid == 0) {
+            const u64 ex = lookback(g.desc, g.nchunk, t, tc, tm);
+            if (lane == 0) s_ex[0] = ex;
+            if (lane == 32) s_ex[1] = ex;
+        }
+        __syncthreads();
+        const u64 exc = s_ex[0], exm = s_ex[1];
+        if (tid == 0) {
+            if (tclean) atomicAdd((unsigned long long*)g.counts, (unsigned long long)tclean);
+            if (base + cnt == n) {
+                g.counts[1] = exc + tc;
+                g.counts[2] = exm + tm;
+            }
+        }
+        u64 pc = exc + (off & 0xFFFF), pm = exm + (off >> 16);
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            if (cls[j] == 2) {
+                u32* o = g.out_conf + 3 * pc;
+                o[0] = ia[j]; o[1] = io[j]; o[2] = itt[j];
+                pc++;
+            } else if (cls[j] == 1) {
+                g.out_md[pm] = rec[j];
+                pm++;
+            }
+        }
     }
-    __syncthreads();
-    u64 o1 = s_sum[1][threadIdx.x], o2 = s_sum[2][threadIdx.x];
-    for (u64 t = b; t < e; t++) {
-        tile_off[2 * t] = o1; tile_off[2 * t + 1] = o2;
-        o1 += tile_cnt[4 * t + 1]; o2 += tile_cnt[4 * t + 2];
-    }
-}
-
-__global__ void k_scatter3(const uint4* __restrict__ sc, const uint2* __restrict__ sm, u64 slot_cap,
-                           const u32* __restrict__ tile_cnt, const u64* __restrict__ tile_off,
-                           u32* __restrict__ out_conf, uint2* __restrict__ out_md) {
-    const u64 tile = blockIdx.x;
-    const u32 nc = tile_cnt[4 * tile + 1], nm = tile_cnt[4 * tile + 2];
-    const u64 oc = tile_off[2 * tile], om = tile_off[2 * tile + 1];
-    for (u32 k = threadIdx.x; k < nc && k < slot_cap; k += blockDim.x) {
-        uint4 v = sc[tile * slot_cap + k];
-        out_conf[3 * (oc + k) + 0] = v.x;
-        out_conf[3 * (oc + k) + 1] = v.y;
-        out_conf[3 * (oc + k) + 2] = v.z;
-    }
-    for (u32 k = threadIdx.x; k < nm && k < slot_cap; k += blockDim.x) out_md[om + k] = sm[tile * slot_cap + k];
 }
 
 }  // namespace kd
@@ -273,55 +294,54 @@ static int check_side(const kd_side* s, const char* which) {
 }
 
 // classify3 on device-resident sides: conflicts (a, o, t index triples, path order) -> d_conf,
-// merge deltas -> d_md, counts[4] <- clean, conflicts, mdeltas, 0 (zeroed by the caller, with
-// *derr).
+// merge deltas -> d_md, counts[4] <- clean, conflicts, mdeltas, 0; *derr <- error bits.  Nothing
+// needs zeroing by the caller.
 static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
                          u64* counts, u32* derr) {
     int rc;
     const u64 nA = A.n, nO = O.n, nT = T.n;
-    u64 ntiles = (nA + nO + C3_TILE - 1) / C3_TILE;
-    if (ntiles == 0) ntiles = 1;
-    // worst case per tile: everything in theirs lands in one tile -> slot capacity must cover
-    // the tile's own items; we bound by (C3_TILE + 1) * 2 + nT/ntiles*4 and flag overflow (err 8)
-    u64 slot_cap = 2 * (C3_TILE + 2) + (nT / ntiles) * 4 + 64;
-    if (slot_cap > nA + nO + nT + 1) slot_cap = nA + nO + nT + 1;
-    void *bounds, *tcnt, *toff, *sc, *sm;
-    if ((rc = ensure(ctx, "c3.bounds", 3 * (ntiles + 1) * 8, &bounds))) return rc;
-    if ((rc = ensure(ctx, "c3.tcnt", ntiles * 16, &tcnt))) return rc;
-    if ((rc = ensure(ctx, "c3.toff", ntiles * 16, &toff))) return rc;
-    if ((rc = ensure(ctx, "c3.sc", ntiles * slot_cap * 16, &sc))) return rc;
-    if ((rc = ensure(ctx, "c3.sm", ntiles * slot_cap * 8, &sm))) return rc;
-    void* dz;
+    const u64 nchunk = (nO + nT) / C3_CH + 2;
+    void *cand, *c2, *desc, *aux, *dz;
+    if ((rc = ensure(ctx, "c3.cand", (nO + nT + 1) * 8, &cand))) return rc;
+    if ((rc = ensure(ctx, "c3.c2", 64, &c2))) return rc;
+    if ((rc = ensure(ctx, "c3.desc", 2 * nchunk * 8, &desc))) return rc;
+    const bool fresh_aux = ctx->bufs["c3.aux"].p == nullptr;
+    if ((rc = ensure(ctx, "c3.aux", 64, &aux))) return rc;
+    if (fresh_aux) KD_HIP(hipMemsetAsync(aux, 0, 64, ctx->stream));
     if ((rc = device_zeros(ctx, &dz))) return rc;
-    const u64* kA = nA ? A.key : (const u64*)dz;  // an empty side points at device zeros
-    const u64* kO = nO ? O.key : (const u64*)dz;
-    const u64* kT = nT ? T.key : (const u64*)dz;
-    rc = launch(ctx, "k_partition3", [&] {
-        hipLaunchKernelGGL(k_partition3, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0, ctx->stream, kA, nA,
-                           kO, nO, kT, nT, ntiles, (u64*)bounds);
+    const u64* kA = nA ? A.key : (const u64*)dz;
+    rc = launch(ctx, "k_sorted3", [&] {
+        const u64 work = std::max<u64>(nA / 2, 2 * nchunk);
+        const u64 blocks = std::min<u64>((work + 255) / 256, (u64)ctx->n_cu * 8);
+        hipLaunchKernelGGL(k_sorted3, dim3((unsigned)std::max<u64>(blocks, 1)), dim3(256), 0, ctx->stream, kA, nA,
+                           (u64*)desc, 2 * nchunk, (u32*)aux, counts);
     });
     if (rc) return rc;
-    Join3Args g;
-    g.A = kA; g.O = kO; g.T = kT;
-    g.oA = (const u32*)A.oid; g.oO = (const u32*)O.oid; g.oT = (const u32*)T.oid;
-    g.nA = nA; g.nO = nO; g.nT = nT;
-    g.nmA = A.name; g.nmO = O.name; g.nmT = T.name;
-    g.noA = A.name_off; g.noO = O.name_off; g.noT = T.name_off;
+    // ours vs theirs: key-ordered differing paths (+ filename checks, order check, error bits)
+    if ((rc = diff2_device(ctx, &O, &T, 0, (u32*)cand, nullptr, (u64*)c2, derr))) return rc;
+    if (ctx->occ_resolve3 <= 0) {
+        int nb = 0;
+        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_resolve3<C3_NT>, C3_NT, 0));
+        ctx->occ_resolve3 = nb > 0 ? nb : 1;
+    }
+    // an empty side (or an absent filename arena) points at device zeros: lanes without an entry
+    // load from index 0 of every array instead of branching, so each array must be readable
+    auto ptr = [&](const void* p, u64 n) { return n && p ? p : (const void*)dz; };
+    Resolve3Args g;
+    g.A = kA; g.O = (const u64*)ptr(O.key, nO); g.T = (const u64*)ptr(T.key, nT);
+    g.oA = (const u32*)ptr(A.oid, nA); g.oO = (const u32*)ptr(O.oid, nO); g.oT = (const u32*)ptr(T.oid, nT);
+    g.nA = nA; g.nO = nO;
+    g.nmA = (const u8*)ptr(A.name, nA); g.nmO = (const u8*)ptr(O.name, nO); g.nmT = (const u8*)ptr(T.name, nT);
+    g.noA = (const u64*)ptr(A.name_off, nA); g.noO = (const u64*)ptr(O.name_off, nO); g.noT = (const u64*)ptr(T.name_off, nT);
     g.hash_mode = A.key_mode == KD_KEY_HASH;
-    g.bounds = (const u64*)bounds;
-    g.stage_conf = (uint4*)sc; g.stage_md = (uint2*)sm; g.slot_cap = slot_cap;
-    g.tile_cnt = (u32*)tcnt; g.err = derr;
-    rc = launch(ctx, "k_join3", [&] {
-        hipLaunchKernelGGL((k_join3<C3_NT>), dim3((unsigned)ntiles), dim3(C3_NT), 0, ctx->stream, g);
-    });
-    if (rc) return rc;
-    rc = launch(ctx, "k_scan3", [&] {
-        hipLaunchKernelGGL((k_scan3<256>), dim3(1), dim3(256), 0, ctx->stream, (const u32*)tcnt, ntiles, (u64*)toff, counts);
-    });
-    if (rc) return rc;
-    return launch(ctx, "k_scatter3", [&] {
-        hipLaunchKernelGGL(k_scatter3, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, (const uint4*)sc,
-                           (const uint2*)sm, slot_cap, (const u32*)tcnt, (const u64*)toff, d_conf, d_md);
+    g.cand = (const uint2*)cand; g.c2 = (const u64*)c2;
+    g.desc = (u64*)desc; g.nchunk = nchunk; g.aux = (u32*)aux;
+    g.out_conf = d_conf; g.out_md = d_md; g.counts = counts; g.err = derr;
+    // persistent: at most every resident workgroup, at most one per chunk (+1 so someone adds the
+    // clean count when there are no differing paths)
+    const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)ctx->occ_resolve3);
+    return launch(ctx, "k_resolve3", [&] {
+        hipLaunchKernelGGL((k_resolve3<C3_NT>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
     });
 }
 
@@ -415,7 +435,6 @@ int kd_merge3(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_sid
     if ((rc = ensure(ctx, "c3.counts", 64, &dc))) return rc;
     u64* counts = (u64*)dc;
     u32* derr = (u32*)(counts + 4);
-    KD_HIP(hipMemsetAsync(dc, 0, 64, ctx->stream));
     if ((rc = merge3_device(ctx, A, O, T, (u32*)oc, (uint2*)om, counts, derr))) return rc;
     u64 hc[5];
     KD_HIP(hipMemcpyAsync(hc, dc, 40, hipMemcpyDeviceToHost, ctx->stream));
@@ -454,8 +473,6 @@ int kd_merge3_device(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const
     KD_CHECK(anc->n < 0xFFFFFFFFull && ours->n < 0xFFFFFFFFull && theirs->n < 0xFFFFFFFFull,
              "kd_merge3_device: side too large");
     KD_HIP(hipSetDevice(ctx->device));
-    KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
-    KD_HIP(hipMemsetAsync(d_err, 0, sizeof(u32), ctx->stream));
     return merge3_device(ctx, *anc, *ours, *theirs, d_conflict, (uint2*)d_mdelta, d_counts, d_err);
 }
 

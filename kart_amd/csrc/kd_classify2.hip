@@ -399,11 +399,14 @@ __device__ __forceinline__ void tile_merge(const u64* sA, const u64* sB, const u
 // different names would otherwise be read as an update)
 template <int IPT>
 __device__ __forceinline__ void tile_names(const Join2Args& g, const TileGeo& q, const u32 rec[IPT]) {
+    u32 ia[IPT], jb[IPT], act = 0;
 #pragma unroll
-    for (int k = 0; k < IPT; k++)
-        if ((rec[k] >> 25) == R_MATCH &&
-            !names_eq(g.nameA, g.nameOffA, q.i0 + (rec[k] & 0xFFF), g.nameB, g.nameOffB, q.j0 + ((rec[k] >> 12) & 0xFFF)))
-            atomicOr(g.err, 2u);
+    for (int k = 0; k < IPT; k++) {
+        ia[k] = (u32)q.i0 + (rec[k] & 0xFFF);
+        jb[k] = (u32)q.j0 + ((rec[k] >> 12) & 0xFFF);
+        act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
+    }
+    if (names_ne_batch<IPT, 8>(g.nameA, g.nameOffA, ia, g.nameB, g.nameOffB, jb, act)) atomicOr(g.err, 2u);
 }
 
 // Per-item flag bits (bitwise, not short-circuit: no exec-mask branches), then per item-slot ballots:
@@ -478,8 +481,9 @@ __device__ __forceinline__ void tile_write(const u32 rec[IPT], const TileCounts&
 // The tile is staged in ONE HBM round trip: keys and OIDs of both sides go global -> LDS by LDS-DMA
 // (global_load_lds_dwordx4: 16 B per lane, the wave's 64 chunks land contiguously), all issued
 // before any use.
-template <int NT, int IPT, bool UNORD>
+template <int NT, int IPT, bool UNORD, bool HASH>
 __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
+    // (HASH: filename checks compiled in; the int-key instantiation carries none of their registers)
     using LD = Join2Lds<NT, IPT>;
     static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
     constexpr int NRANGE = KD_J_OIDG ? 2 : 4;  // keys only, or keys + OIDs
@@ -532,11 +536,16 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
 #else
     tile_walk<NT, IPT>(sA, sB, q, rec, bad);
 #endif
+    // complete order check: the walk only compares the keys it consumes, and on unsorted input the
+    // per-thread merge-path splits can skip keys, so every adjacent pair of the tile's two ranges
+    // (the first against the lookbehind key) is checked here as well
+    for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
+    for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
 #if KD_J_EXP != 3  // 3: profiling, no OID compare
     if (KD_J_OIDG) tile_oid_global<IPT>(g, q, rec);
     else tile_oid_lds<IPT>(oA, oB, rec);
 #endif
-    if (g.hash_mode) tile_names<IPT>(g, q, rec);
+    if (HASH) tile_names<IPT>(g, q, rec);
     if (bad) atomicOr(g.err, 1u);
     const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
     uint2 *sd, *su;
@@ -1158,51 +1167,7 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
 // ---------------------------------------------------------------------------------------------
 // k_join2p: persistent, register-prefetched tiles, decoupled look-back
 // ---------------------------------------------------------------------------------------------
-// Look-back descriptors, two words per tile (own flag each, looked back independently):
-//   word 0 = flag << 62 | deltas << 31 | updates,   word 1 = flag << 62 | deletes
-// flag 0 = not yet, 1 = the tile's own counts (aggregate), 2 = inclusive prefix through the tile.
-// Fields are 31 bits (side sizes are checked on the host), so payloads add without carries.
-constexpr u64 LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_PAY = (1ull << 62) - 1;
-
-__device__ __forceinline__ void lb_store(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ u64 lb_load(u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// Wave 0 of the tile's workgroup: publish the aggregates, walk back over earlier tiles' descriptors
-// (32 at a time per word, lanes 0-31 word 0 and lanes 32-63 word 1) until an inclusive prefix is
-// found, publish the tile's own inclusive prefix; returns the exclusive payload of this lane's word.
-// Every workgroup is resident (the grid is sized by occupancy) and tiles are taken in increasing
-// order, so every predecessor's descriptor is eventually published.
-__device__ __forceinline__ u64 lookback(u64* __restrict__ desc, u64 ntiles, u64 t, u64 agg0, u64 agg1) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
-    u64* D = desc + (u64)h * ntiles;
-    const u64 agg = h ? agg1 : agg0;
-    if (l == 0) lb_store(D + t, (t == 0 ? LB_INC : LB_AGG) | agg);
-    u64 excl = 0;
-    bool done = t == 0;
-    i64 pos = (i64)t - 1;
-    while (true) {
-        const bool act = !done;
-        if (__ballot(act) == 0) break;
-        u64 v = LB_INC;  // before tile 0: an inclusive prefix of zero
-        const i64 idx = pos - l;
-        if (act && idx >= 0) v = lb_load(D + idx);
-        const u32 f = (u32)(v >> 62);
-        const u32 mx = (u32)(__ballot(act && f == 0) >> (32 * h));
-        const u32 mp = (u32)(__ballot(act && f == 2) >> (32 * h));
-        const int fp = mp ? __ffs(mp) - 1 : 32, fx = mx ? __ffs(mx) - 1 : 32;
-        const bool take_all = mp == 0 && mx == 0;  // 32 aggregates: add them and look further back
-        const bool finish = mp != 0 && fp < fx;    // aggregates up to an inclusive prefix
-        u64 s = (act && (take_all || (finish && l <= fp))) ? (v & LB_PAY) : 0;
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);  // sum within the 32-lane half
-        if (act && (take_all || finish)) excl += s;
-        if (act && finish) done = true;
-        if (act && take_all) pos -= 32;
-        if (act && !take_all && !finish) __builtin_amdgcn_s_sleep(1);  // a predecessor not published yet
-    }
-    if (l == 0) lb_store(D + t, LB_INC | (excl + agg));
-    return excl;
-}
+// (look-back descriptors and lookback(): kd_join.h)
 
 template <int NT, int IPT, bool LOOKBACK>
 __global__ __launch_bounds__(NT, KD_J2P_WAVES) void k_join2p(Join2Args g) {
@@ -1362,7 +1327,12 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.A = kA; g.oidA = nA ? A->oid : empty_oid; g.nA = nA;
     g.B = kB; g.oidB = nB ? B->oid : empty_oid; g.nB = nB;
     g.part = (const u64*)part;
-    g.nameA = A->name; g.nameOffA = A->name_off; g.nameB = B->name; g.nameOffB = B->name_off;
+    // filename arenas of an empty side point at device zeros (the batched compare loads index 0 of
+    // the offsets of lanes without a matched pair)
+    g.nameA = nA && A->name ? A->name : (const u8*)dz;
+    g.nameOffA = nA && A->name_off ? A->name_off : (const u64*)dz;
+    g.nameB = nB && B->name ? B->name : (const u8*)dz;
+    g.nameOffB = nB && B->name_off ? B->name_off : (const u64*)dz;
     g.hash_mode = hash ? 1 : 0;
     g.dummy = (const u8*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
@@ -1372,7 +1342,10 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.ntiles = ntiles;
     if (unord) {
         return launch(ctx, "k_join2", [&] {
-            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+            if (hash)
+                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+            else
+                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
         });
     }
     const bool ws = KD_C2_MODE == 3;
@@ -1391,7 +1364,10 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         });
     } else if (KD_C2_MODE == 1) {  // one tile per workgroup, LDS-DMA staging
         rc = launch(ctx, "k_join2", [&] {
-            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+            if (hash)
+                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+            else
+                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
         });
     } else {
         // persistent: every workgroup resident at once (grid from the occupancy of this kernel)

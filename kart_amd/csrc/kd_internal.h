@@ -19,6 +19,7 @@ typedef int64_t i64;
 typedef int16_t i16;
 typedef int8_t i8;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector (SROA-friendly)
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 namespace kd {
 
@@ -76,6 +77,7 @@ struct kd_ctx {
     int n_cu = 256;  // compute units (grid sizing of grid-stride kernels)
     int occ_join2p = 0;  // resident k_join2p workgroups per CU (persistent grid size), 0 = not queried
     int occ_join2r = 0;  // resident k_join2r workgroups per CU
+    int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
 };
 
 namespace kd {

@@ -300,3 +300,127 @@ def test_gpu_merge3_device_c4_layer_vs_oracle(engine, n):
     assert conf.shape[0] == M.n_conflict
     r = engine.merge3(M.ancestor, M.ours, M.theirs)
     assert key(r.conflict) == key(oc) and key(r.mdelta) == key(om)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nA,nO,nT,mode", [(0, 0, 0, "x"), (0, 500, 700, "add"), (3000, 0, 0, "del"),
+                                          (3000, 3000, 0, "x"), (3000, 0, 3000, "x"), (5000, 5000, 5000, "same"),
+                                          (4000, 4100, 3900, "rand"), (70_000, 70_000, 70_000, "all")])
+def test_gpu_merge3_edges_vs_oracle(engine, nA, nO, nT, mode):
+    """one-sided and empty merges, all paths identical, every path edited on both sides, random
+    overlaps: conflicts / merge deltas bit-exact with the oracle and in key (path) order"""
+    from kart_amd import packing
+
+    rng = np.random.default_rng(nA * 7 + nO * 3 + nT)
+    pool = np.unique(rng.integers(0, 2**63, size=max(nA, nO, nT) * 2 + 8, dtype=np.uint64))
+    oid_of = rng.integers(0, 256, size=(pool.size, 20), dtype=np.uint8)
+
+    def side(n, salt):
+        if mode == "same" or mode == "all":
+            idx = np.arange(min(n, pool.size))
+        else:
+            idx = np.sort(rng.choice(pool.size, size=n, replace=False))
+        o = oid_of[idx].copy()
+        if mode == "all" and salt:
+            o[:, 0] ^= salt  # every path edited, differently on ours and theirs -> all conflicts
+        elif mode == "rand" and salt:
+            ch = rng.random(idx.size) < 0.3
+            o[ch] = rng.integers(0, 256, size=(int(ch.sum()), 20), dtype=np.uint8)
+        return pool[idx].copy(), o
+
+    kA, oA = side(nA, 0)
+    kO, oO = side(nO, 1)
+    kT, oT = side(nT, 2)
+    sides = [packing.PackedSide(k, o, 0, np.arange(k.size)) for k, o in ((kA, oA), (kO, oO), (kT, oT))]
+    r = engine.merge3(*sides)
+    oc, om, oclean = O.classify3(kA, oA, kO, oO, kT, oT)
+    assert np.array_equal(np.asarray(r.conflict).reshape(-1, 3), np.asarray(oc).reshape(-1, 3))
+    assert np.array_equal(np.asarray(r.mdelta).reshape(-1, 2), np.asarray(om).reshape(-1, 2))
+    assert r.n_clean == oclean
+    if mode == "all":
+        assert len(r.conflict) == nA
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_gpu_merge3_rejects_unsorted(engine, which):
+    from kart_amd import _native as N
+    from kart_amd import packing
+
+    ks = [np.array([1, 4, 9, 12], np.uint64) for _ in range(3)]
+    ks[which] = np.array([1, 9, 4, 12], np.uint64)
+    sides = [packing.PackedSide(k, np.zeros((4, 20), np.uint8), 0, np.arange(4)) for k in ks]
+    with pytest.raises(N.Unsupported):
+        engine.merge3(*sides)
+    # the error flag is consumed: the next, valid merge succeeds
+    ok = [packing.PackedSide(np.array([1, 4, 9, 12], np.uint64), np.zeros((4, 20), np.uint8), 0, np.arange(4))
+          for _ in range(3)]
+    assert engine.merge3(*ok).n_clean == 4
+
+
+def _hash_sides(rng, n, lens):
+    """hash-key sides sharing keys and filenames: names of the given lengths (random bytes, so every
+    byte offset mod 4 occurs), three sides = ancestor / ours / theirs with ~10% per-side edits"""
+    from kart_amd import packing
+    from kart_amd import _native as N
+
+    keys = np.unique(rng.integers(0, 2**63, size=n, dtype=np.uint64))
+    ln = rng.choice(lens, size=keys.size)
+    names = [rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes() for k in ln]
+    oids = rng.integers(0, 256, size=(keys.size, 20), dtype=np.uint8)
+
+    def side(sel, oid, nm):
+        idx = np.flatnonzero(sel)
+        arena = b"".join(nm[i] for i in idx)
+        off = np.zeros(idx.size + 1, np.uint64)
+        off[1:] = np.cumsum([len(nm[i]) for i in idx])
+        return packing.PackedSide(keys[idx].copy(), np.ascontiguousarray(oid[idx]), N.KD_KEY_HASH,
+                                  np.arange(idx.size), np.frombuffer(arena, np.uint8).copy(), off)
+
+    return keys, names, oids, side
+
+
+@pytest.mark.parametrize("lens", [[24], [1, 2, 3, 5, 7, 13, 29, 30, 31, 33, 64, 100]])
+def test_gpu_hash_names_verified(engine, lens):
+    """KD_KEY_HASH: matched keys with equal filenames classify normally (the batched 32-B window and
+    the long-name loop both); one differing byte in one matched filename (first, middle or last
+    byte, or a length change) is a key collision -> Unsupported, for diff2 and for merge3 (ancestor
+    vs ours and ancestor vs theirs-without-ours)"""
+    from kart_amd import _native as N
+
+    rng = np.random.default_rng(len(lens))
+    keys, names, oids, side = _hash_sides(rng, 3000, lens)
+    m = keys.size
+    selA = rng.random(m) > 0.1
+    selO = rng.random(m) > 0.1
+    selT = rng.random(m) > 0.1
+    oO = oids.copy(); oO[rng.random(m) < 0.1, 0] ^= 1
+    oT = oids.copy(); oT[rng.random(m) < 0.1, 1] ^= 1
+    A, O_, T = side(selA, oids, names), side(selO, oO, names), side(selT, oT, names)
+    r = engine.diff2(A, O_)
+    od, _ = O.classify2(A.key, A.oid, O_.key, O_.oid)
+    assert np.array_equal(r.delta, od)
+    r3 = engine.merge3(A, O_, T)
+    oc, om, ocl = O.classify3(A.key, A.oid, O_.key, O_.oid, T.key, T.oid)
+    assert np.array_equal(np.asarray(r3.conflict).reshape(-1, 3), oc.reshape(-1, 3))
+    assert np.array_equal(np.asarray(r3.mdelta).reshape(-1, 2), om.reshape(-1, 2)) and r3.n_clean == ocl
+
+    both = np.flatnonzero(selA & selO & selT)
+    for pick, where in ((both[5], 0), (both[len(both) // 2], -1), (both[-3], "len")):
+        bad = list(names)
+        b = bytearray(bad[pick])
+        if where == "len":
+            b += b"x"
+        else:
+            b[where] ^= 0x20
+        bad[pick] = bytes(b)
+        with pytest.raises(N.Unsupported):
+            engine.diff2(A, side(selO, oO, bad))
+        with pytest.raises(N.Unsupported):
+            engine.merge3(A, side(selO, oO, bad), T)
+    # ancestor and theirs matched, ours absent: the ancestor/theirs filenames are checked directly
+    only_at = np.flatnonzero(selA & ~selO & selT)
+    bad = list(names)
+    b = bytearray(bad[only_at[0]]); b[-1] ^= 1; bad[only_at[0]] = bytes(b)
+    with pytest.raises(N.Unsupported):
+        engine.merge3(A, O_, side(selT, oT, bad))
