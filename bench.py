@@ -8,6 +8,10 @@ layer: merge-path join + OID compare + key-ordered compaction of the delta set (
 k_join2, k_place2), then the msgpack field decode + Python-== column compare of every update
 (k_fielddiff) — all on the device, inputs resident in HBM before the timed region.
 
+--workload c3 (BASELINE configs[2]): a 100M-polygon int-PK layer per GPU (--n), 10% edits: 4% geometry
+updates, 4% attribute updates, 1% deletes, 1% inserts; same step as C2 (blobs materialised only for the
+updated features: nothing else is read).
+
 --workload c4 (BASELINE configs[3]): a 50M-row string-PK table per GPU (MsgpackHashPathEncoder paths)
 three-way merge classification: classify2(ours, theirs) + k_resolve3 (ancestor lookup + the libgit2
 conflict rule) over the paths where ours and theirs differ.
@@ -44,8 +48,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"])
-    ap.add_argument("--n", type=int, default=0, help="units per GPU (c2: points, default 10M; c4: rows, 50M; c5: geometries, 20M)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--n", type=int, default=0, help="units per GPU (c2: points, default 10M; c3: polygons, 100M; c4: rows, 50M; c5: geometries, 20M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unordered", action="store_true",
                     help="c2: tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
@@ -58,7 +62,7 @@ def parse():
                          "so the events do not inflate the step time)")
     a = ap.parse_args()
     if not a.n:
-        a.n = {"c2": 10_000_000, "c4": 50_000_000, "c5": 20_000_000}[a.workload]
+        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c4": 50_000_000, "c5": 20_000_000}[a.workload]
     if a.traffic_json is None:
         a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
     return a
@@ -146,7 +150,7 @@ def kernel_times(eng, names):
 
 
 # ---------------------------------------------------------------------------------------------
-def run_c2(args, D):
+def run_c2(args, D, polygons=False):
     torch = D.torch
     from kart_amd import shard, synth
     from kart_amd.device import DiffPipeline
@@ -155,8 +159,11 @@ def run_c2(args, D):
 
     n = args.n
     t0 = time.time()
-    L = synth.points_layer(n, seed=synth.SEED + D.rank, pk0=shard.rank_pk_base(D.rank, n))
-    log(f"[rank {D.rank}] generated {n} points in {time.time() - t0:.1f}s "
+    if polygons:  # C3: 10 % edits (4 % geometry + 4 % attribute updates, 1 % del, 1 % ins)
+        L = synth.polygons_layer(n, seed=synth.SEED + D.rank, pk0=shard.rank_pk_base(D.rank, n))
+    else:
+        L = synth.points_layer(n, seed=synth.SEED + D.rank, pk0=shard.rank_pk_base(D.rank, n))
+    log(f"[rank {D.rank}] generated {n} {'polygons' if polygons else 'points'} in {time.time() - t0:.1f}s "
         f"(+{L.n_insert} ins, ~{L.n_update} upd, -{L.n_delete} del)")
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     eng = Engine(torch.cuda.current_device())
@@ -212,9 +219,14 @@ def run_c2(args, D):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/u64 (integer + fp64 compare)",
-        "data": "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
-        "config": {"workload": "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
-                   "points_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
+        "data": ("synthetic (seeded MULTIPOLYGON layer: reference blob/path encodings, synthetic OIDs; "
+                 "blobs materialised for updated features only)") if polygons else
+                "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
+        "config": {"workload": (f"C3: {n}-polygon int-PK layer per GPU, 10% edits (4% geometry + 4% attribute "
+                                "updates, 1% del, 1% ins), two-commit diff + field diff") if polygons else
+                               "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
+                   "features_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
+                   "updates_per_step": counts["updates"],
                    "delta_order": "tile-grouped (same delta set)" if args.unordered else "key",
                    "parallelism": f"bucket-range shards x{D.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
@@ -432,7 +444,8 @@ def run_c4(args, D):
 def main():
     args = parse()
     D = Dist()
-    out = {"c2": run_c2, "c4": run_c4, "c5": run_c5}[args.workload](args, D)
+    out = {"c2": run_c2, "c3": lambda a, d: run_c2(a, d, polygons=True), "c4": run_c4,
+           "c5": run_c5}[args.workload](args, D)
     if D.rank == 0:
         print(json.dumps(out), flush=True)
     D.close()

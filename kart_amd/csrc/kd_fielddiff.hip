@@ -492,6 +492,9 @@ constexpr u32 FD_TAB_LDS_MAX = 16384;  // tables up to this size are copied into
 //      instead of 64 scattered lines — per-lane staging of its own blobs made every load instruction
 //      touch 64 lines and the staging dominated the kernel;
 //   3. each lane walks its two blobs from LDS (table-driven decoder, tables in LDS).
+typedef __attribute__((address_space(3))) void* fd_lds_vp;
+typedef const __attribute__((address_space(1))) void* fd_glb_vp;
+
 template <int POOL>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
@@ -499,11 +502,7 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
                                                      const u64* __restrict__ n_upd_dev, FdTab tg, FdTabOff to,
                                                      const u8* __restrict__ tab_base, u64* __restrict__ masks,
                                                      u8* __restrict__ status) {
-    constexpr int BATCH = 8;  // chunk loads in flight per lane
     __shared__ u32x4 s_pool[POOL];  // the round's blobs, packed back to back in 16-B chunks
-    __shared__ u8 s_own[POOL];      // lane owning each pool chunk
-    __shared__ u64 s_ab[FD_NT], s_bb[FD_NT];
-    __shared__ u32 s_cnt[FD_NT], s_off[FD_NT];
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
     const int lane = threadIdx.x;
 #if KD_FD_CLOCK
@@ -562,35 +561,31 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         const bool fit = act && x <= (u32)POOL;  // lanes past the pool parse from global memory
         const u64 bal = __ballot(fit);
         const u32 used = bal ? __shfl(x, 63 - __clzll((long long)bal), 64) : 0;  // end of the last fitting lane
-        s_ab[lane] = ab;
-        s_bb[lane] = bb;
-        s_cnt[lane] = na;
-        s_off[lane] = off;
-        if (fit)
-            for (u32 c = 0; c < need; c++) s_own[off + c] = (u8)lane;
-        __syncthreads();
+        (void)used;
 #if KD_FD_CLOCK
         const u64 T1 = clock64();
 #endif
-        // ---- cooperative staging: chunk q of the pool is loaded by lane q % 64 (consecutive lanes
-        //      read consecutive chunks of the same blob) ----
-        for (u32 q0 = 0; q0 < used; q0 += BATCH * FD_NT) {
-            u32x4 v[BATCH];
-#pragma unroll
-            for (int k = 0; k < BATCH; k++) {
-                const u32 q = q0 + k * FD_NT + lane;
-                u64 src = ab;  // own blob: a mapped chunk for masked-off lanes
-                if (q < used) {
-                    const u32 w = s_own[q];
-                    const u32 c = q - s_off[w], n0 = s_cnt[w];
-                    src = c < n0 ? s_ab[w] + 16ull * c : s_bb[w] + 16ull * (c - n0);
+        // ---- staging, global -> LDS directly (LDS-DMA): owner lane by owner lane (a wave-uniform
+        //      loop, its descriptors read with readlane into SGPRs), lane l loads chunk c0 + l of the
+        //      owner's two blobs into pool chunk off + c0 + l (wave-uniform LDS base + 16 l), so
+        //      consecutive lanes read consecutive 16-B chunks and every load of the round is in
+        //      flight at once, without registers and without LDS reads between the loads ----
+        const u32 need_fit = fit ? need : 0u;
+        for (int w = 0; w < FD_NT; w++) {
+            const u32 need_w = (u32)__builtin_amdgcn_readlane((int)need_fit, w);
+            if (need_w == 0) continue;
+            const u32 off_w = (u32)__builtin_amdgcn_readlane((int)off, w);
+            const u32 na_w = (u32)__builtin_amdgcn_readlane((int)na, w);
+            const u64 ab_w = (u64)(u32)__builtin_amdgcn_readlane((int)(u32)ab, w) |
+                             (u64)(u32)__builtin_amdgcn_readlane((int)(u32)(ab >> 32), w) << 32;
+            const u64 bb_w = (u64)(u32)__builtin_amdgcn_readlane((int)(u32)bb, w) |
+                             (u64)(u32)__builtin_amdgcn_readlane((int)(u32)(bb >> 32), w) << 32;
+            for (u32 c0 = 0; c0 < need_w; c0 += FD_NT) {
+                const u32 c = c0 + lane;
+                if (c < need_w) {
+                    const u64 src = c < na_w ? ab_w + 16ull * c : bb_w + 16ull * (c - na_w);
+                    __builtin_amdgcn_global_load_lds((fd_glb_vp)src, (fd_lds_vp)(s_pool + off_w + c0), 16, 0, 0);
                 }
-                v[k] = *(gp)src;
-            }
-#pragma unroll
-            for (int k = 0; k < BATCH; k++) {
-                const u32 q = q0 + k * FD_NT + lane;
-                if (q < used) s_pool[q] = v[k];
             }
         }
         __syncthreads();
@@ -775,7 +770,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     const u64 per_round = (u64)FD_NT * 2 * (typ + 15) / 16 * 110 / 100;
     const int pool = !lds_tab ? 0 : per_round <= 1152 ? 1152 : per_round <= 1536 ? 1536 : per_round <= 2048 ? 2048
                    : per_round <= 3072 ? 3072 : per_round <= 4096 ? 4096 : 0;
-    const u64 lds_blk = pool ? (u64)pool * 17 + FD_NT * 24 + 1024 + o_end : 1024;
+    const u64 lds_blk = pool ? (u64)pool * 16 + 1024 + o_end : 1024;
     const u64 per_cu = std::min<u64>(8, (160 * 1024) / lds_blk);
     unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, (u64)ctx->n_cu * per_cu);
     if (blocks == 0) blocks = 1;

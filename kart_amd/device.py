@@ -54,7 +54,9 @@ class DevBlobs:
         self.off = to_dev(off, device)
         self.nbytes = int(data.size)
         self.max_len = int((off[1:] - off[:-1]).max()) if self.n else 0
-        self.mean_len = int((int(off[-1]) - int(off[0]) + self.n - 1) // self.n) if self.n else 0
+        # typical blob = mean over the non-empty blobs (an arena may hold only the blobs a diff reads)
+        nz = int(np.count_nonzero(off[1:] != off[:-1])) if self.n else 0
+        self.mean_len = int((int(off[-1]) - int(off[0]) + nz - 1) // nz) if nz else 0
 
     def kd_blobs(self):
         b = N.KdBlobs()

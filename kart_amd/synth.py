@@ -178,6 +178,153 @@ def points_layer(n, frac_update=0.01, frac_delete=0.01, frac_insert=0.01, seed=S
     return Layer(base, target, bb, tb, schema, {lh: legend}, n_ins, n_upd, n_del)
 
 
+def polygon_blobs(pk, gver, aver, legend_hex, rng_seed=SEED):
+    """Polygons-layer feature blobs (the shape of tests/data/polygons: 245-582 B).
+
+    values = [geom MULTIPOLYGON (ext 'G': 8-B GPKG header, XY envelope, one ring of 5-24 points),
+              date_adjusted str (20-char timestamp), survey_reference str|None, adjusted_nodes int32].
+    The geometry is a function of (pk, gver), the attributes of (pk, aver), so a geometry edit and an
+    attribute edit change different fields.  Canonical (smallest-width) msgpack headers throughout."""
+    pk = np.asarray(pk, np.int64)
+    n = pk.shape[0]
+    u = pk.view(np.uint64)
+    hg = splitmix64(u ^ (np.asarray(gver, np.uint64) << np.uint64(48)) ^ np.uint64(rng_seed ^ 0x6706))
+    ha = splitmix64(u ^ (np.asarray(aver, np.uint64) << np.uint64(48)) ^ np.uint64(rng_seed ^ 0xA77A))
+    ha2 = splitmix64(ha)
+    npts = (5 + (hg >> np.uint64(58)) % np.uint64(20)).astype(np.int64)  # 5..24 ring points
+    glen = 8 + 32 + 22 + 16 * npts  # GPKG header + envelope + MULTIPOLYGON/POLYGON/ring headers + xy
+    ehdr = np.where(glen <= 255, 3, 4)  # c7 len 47 | c8 len16 47
+    has_ref = ((ha2 >> np.uint64(7)) & np.uint64(3)) != 0
+    rlen = (8 + (ha2 >> np.uint64(20)) % np.uint64(9)).astype(np.int64)  # 8..16 chars
+    reflen = np.where(has_ref, 1 + rlen, 1)
+    blen = 3 + 40 + 1 + ehdr + glen + 21 + reflen + 5
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(blen, out=off[1:])
+    if n == 0:
+        return np.zeros(0, np.uint8), off
+    W = int(blen.max())
+    mat = np.zeros((n, W), np.uint8)
+    lon = -180.0 + (hg & np.uint64(0xFFFFFF)).astype(np.float64) / float(1 << 24) * 359.0
+    lat = -85.0 + ((hg >> np.uint64(24)) & np.uint64(0xFFFFFF)).astype(np.float64) / float(1 << 24) * 169.0
+    w = 1e-4 * (1 + ((hg >> np.uint64(48)) & np.uint64(0x3FF)).astype(np.float64))
+    # date_adjusted: "20YY-MM-DDThh:mm:ssZ" from the attribute hash
+    yy = 2000 + (ha % np.uint64(25)).astype(np.int64)
+    mo = 1 + ((ha >> np.uint64(8)) % np.uint64(12)).astype(np.int64)
+    dd = 1 + ((ha >> np.uint64(16)) % np.uint64(28)).astype(np.int64)
+    hh = ((ha >> np.uint64(24)) % np.uint64(24)).astype(np.int64)
+    mi = ((ha >> np.uint64(32)) % np.uint64(60)).astype(np.int64)
+    ss = ((ha >> np.uint64(40)) % np.uint64(60)).astype(np.int64)
+    dig = lambda v, w_: [(v // 10 ** (w_ - 1 - j)) % 10 + 48 for j in range(w_)]
+    date = np.stack(dig(yy, 4) + [np.full(n, 45)] + dig(mo, 2) + [np.full(n, 45)] + dig(dd, 2) + [np.full(n, 84)] +
+                    dig(hh, 2) + [np.full(n, 58)] + dig(mi, 2) + [np.full(n, 58)] + dig(ss, 2) + [np.full(n, 90)],
+                    1).astype(np.uint8)
+    chars = (splitmix64(ha2[:, None] ^ np.arange(16, dtype=np.uint64)[None, :]) % np.uint64(26)).astype(np.uint8) + 65
+    nodes = ((ha2 >> np.uint64(32)) & np.uint64(0xFFFFF)).astype(">u4").view(np.uint8).reshape(n, 4)
+    legend_row = np.frombuffer(b"\x92\xd9\x28" + legend_hex.encode() + b"\x94", np.uint8)
+    wkb = np.frombuffer(b"GP\x00\x03" + np.array([4326], "<i4").tobytes(), np.uint8)
+    wkb2 = np.frombuffer(b"\x01\x06\x00\x00\x00\x01\x00\x00\x00\x01\x03\x00\x00\x00\x01\x00\x00\x00", np.uint8)
+    # fixed layout per ring size: slice writes per group, the variable tail (survey_reference,
+    # adjusted_nodes) by a 5-column gather
+    for npv in np.unique(npts):
+        sel = np.nonzero(npts == npv)[0]
+        m = sel.size
+        gl = 62 + 16 * int(npv)
+        eh = 3 if gl <= 255 else 4
+        g0 = 44 + eh
+        sub = np.zeros((m, W), np.uint8)
+        sub[:, 0:44] = legend_row
+        sub[:, 44] = 0xC7 if eh == 3 else 0xC8
+        if eh == 3:
+            sub[:, 45] = gl
+        else:
+            sub[:, 45], sub[:, 46] = gl >> 8, gl & 0xFF
+        sub[:, g0 - 1] = 0x47
+        sub[:, g0:g0 + 8] = wkb
+        lo, la, ww = lon[sel], lat[sel], w[sel]
+        sub[:, g0 + 8:g0 + 40] = np.stack([lo, lo + ww, la, la + ww], 1).astype("<f8").view(np.uint8).reshape(m, 32)
+        sub[:, g0 + 40:g0 + 58] = wkb2
+        sub[:, g0 + 58:g0 + 62] = np.array([npv], "<u4").view(np.uint8)
+        k = np.arange(2 * int(npv), dtype=np.float64)[None, :]
+        xy = np.where(k % 2 == 0, lo[:, None] + ww[:, None] * ((k * 0.37) % 1.0),
+                      la[:, None] + ww[:, None] * ((k * 0.61) % 1.0))
+        sub[:, g0 + 62:g0 + gl] = xy.astype("<f8").view(np.uint8).reshape(m, 16 * int(npv))
+        c = g0 + gl
+        sub[:, c] = 0xB4
+        sub[:, c + 1:c + 21] = date[sel]
+        c += 21
+        hr, rl = has_ref[sel], rlen[sel]
+        sub[:, c] = np.where(hr, 0xA0 | rl, 0xC0).astype(np.uint8)
+        sub[:, c + 1:c + 17] = chars[sel]
+        ci = c + np.where(hr, 1 + rl, 1)  # adjusted_nodes: ce <u32 BE>
+        cols = ci[:, None] + np.arange(5)[None, :]
+        vals = np.concatenate([np.full((m, 1), 0xCE, np.uint8), nodes[sel]], 1)
+        np.put_along_axis(sub, cols, vals, axis=1)
+        mat[sel] = sub
+    arena = mat[np.arange(W)[None, :] < blen[:, None]]
+    return arena, off
+
+
+def _sparse_arena(n, sel, data, off_sel):
+    """arena holding blobs only for entries `sel` (ascending); every other entry is zero-length"""
+    lens = np.zeros(n, np.uint64)
+    lens[sel] = off_sel[1:] - off_sel[:-1]
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    return data, off
+
+
+def polygons_layer(n, frac_geom=0.04, frac_attr=0.04, frac_delete=0.01, frac_insert=0.01, seed=SEED, pk0=0,
+                   batch=1 << 20):
+    """C3: n int-PK MULTIPOLYGON features, 10 % edits = 4 % geometry updates + 4 % attribute updates
+    + 1 % deletes + 1 % inserts.  Feature blobs are materialised for the updated
+    features only (both versions): the diff reads no other blob — classification needs only keys and
+    OIDs — so every other entry has a zero-length blob in the arena."""
+    rng = np.random.default_rng(seed)
+    schema = Schema.from_column_dicts(POLYGON_SCHEMA)
+    legend = Legend(["p-fid"], [c["id"] for c in POLYGON_SCHEMA[1:]])
+    lh = legend.hexhash()
+    pks = np.arange(pk0, pk0 + n, dtype=np.int64)
+    n_g, n_a = int(n * frac_geom), int(n * frac_attr)
+    n_del, n_ins = int(n * frac_delete), int(n * frac_insert)
+    perm = rng.permutation(n)
+    g_i, a_i = np.sort(perm[:n_g]), np.sort(perm[n_g:n_g + n_a])
+    del_i = np.sort(perm[n_g + n_a:n_g + n_a + n_del])
+    del perm
+    gver = np.zeros(n, np.uint8)
+    aver = np.zeros(n, np.uint8)
+    gver[g_i] = 1
+    aver[a_i] = 1
+    upd = np.zeros(n, bool)
+    upd[g_i] = upd[a_i] = True
+    keep = np.ones(n, bool)
+    keep[del_i] = False
+    ins_pk = np.arange(pk0 + n, pk0 + n + n_ins, dtype=np.int64)
+    t_pk = np.concatenate([pks[keep], ins_pk])
+    ver_b = np.zeros(n, np.uint64)
+    ver_t = np.concatenate([(gver.astype(np.uint64) | (aver.astype(np.uint64) << np.uint64(1)))[keep],
+                            np.full(n_ins, 4, np.uint64)])
+    base = packing.PackedSide(key=_int_keys(pks), oid=synth_oids(pks, ver_b), key_mode=0,
+                              order=np.arange(n, dtype=np.int64), encoding=packing.INT_PK_ENCODING)
+    target = packing.PackedSide(key=_int_keys(t_pk), oid=synth_oids(t_pk, ver_t), key_mode=0,
+                                order=np.arange(t_pk.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
+    ub = np.nonzero(upd)[0]  # updated entries: base index; target index = position among kept + 0
+    ut = np.searchsorted(t_pk, pks[ub])
+
+    def blobs(idx_pk, gv, av):
+        parts, offs = [], [np.zeros(1, np.uint64)]
+        for s in range(0, idx_pk.shape[0], batch):
+            d, o = polygon_blobs(idx_pk[s:s + batch], gv[s:s + batch], av[s:s + batch], lh, seed)
+            parts.append(d)
+            offs.append(o[1:] + offs[-1][-1])
+        return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), np.concatenate(offs)
+
+    bd, bo = blobs(pks[ub], np.zeros(ub.size, np.uint64), np.zeros(ub.size, np.uint64))
+    td, to = blobs(pks[ub], gver[ub].astype(np.uint64), aver[ub].astype(np.uint64))
+    bb = _sparse_arena(n, ub, bd, bo)
+    tb = _sparse_arena(t_pk.shape[0], ut, td, to)
+    return Layer(base, target, bb, tb, schema, {lh: legend}, n_ins, int(ub.size), n_del)
+
+
 def _int_keys(pk):
     """vectorised KD_KEY_INT (same formula as kd_pack_int_keys / packing.pk_to_int_key)"""
     pk = np.asarray(pk, np.int64)
