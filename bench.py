@@ -205,7 +205,7 @@ def run_c2(args, D, polygons=False):
     roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, "n_points", n) if dom in alg else None
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_c2(L, maps, args.cpu_seconds)
+        cpu = cpu_baseline_c2(L, maps, args.cpu_seconds, "C3" if polygons else "C2")
     eng.close()
     return {
         "metric": METRIC,
@@ -235,7 +235,7 @@ def run_c2(args, D, polygons=False):
     }
 
 
-def cpu_baseline_c2(L, maps, seconds):
+def cpu_baseline_c2(L, maps, seconds, tag="C2"):
     """oracle classify2 + fielddiff (sequential C, 1 core) on the same layer, repeated for ~N s"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle as O
@@ -253,7 +253,7 @@ def cpu_baseline_c2(L, maps, seconds):
     dt = time.perf_counter() - t0
     pairs = (A.n + L.n_insert) * reps
     return {"value": round(pairs / dt / 1e6, 3), "unit": "M feature-pairs/s", "cores": 1, "kind": "port",
-            "sample": f"full C2 layer ({A.n + L.n_insert} pairs) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
+            "sample": f"the full {tag} layer ({A.n + L.n_insert} pairs) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
                       f"classify2 + fielddiff, 1 thread"}
 
 

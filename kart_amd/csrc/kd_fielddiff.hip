@@ -230,8 +230,14 @@ __device__ __forceinline__ u32 lds_word(lp32 w, u32 k, u32 s) {
     return __builtin_amdgcn_alignbyte(w[k + 1], w[k], s);
 }
 
+#ifndef KD_FD_EXP
+#define KD_FD_EXP 0  // profiling builds only: 1 = no parse, 2 = no LDS byte-payload compare
+#endif
 template <>
 __device__ bool bytes_eq<lp8>(lp8 a, lp8 b, u32 n) {
+#if KD_FD_EXP == 2
+    return a[0] == b[0] || n > 0;
+#endif
     // 32-byte blocks: the 9 aligned words of each side are read together (one LDS round trip per
     // block, no per-word early exit), realigned with v_alignbyte and compared; bytes past n masked
     const u32 sa = (u32)(size_t)a & 3, sb = (u32)(size_t)b & 3;
@@ -528,23 +534,37 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 lim = spec ? n_upd_host : n_upd;
-    for (u64 u0 = (u64)blockIdx.x * FD_NT; u0 < lim; u0 += (u64)gridDim.x * FD_NT) {
+    // one round ahead: the next round's pair is loaded while this round stages, its blob offsets
+    // while this round parses, so a round waits on one HBM latency (the staging) instead of three
+    const u64 step = (u64)gridDim.x * FD_NT;
+    auto load_pair = [&](u64 uu) {
+        uint2 p = make_uint2((u32)uu, (u32)uu);
+        if (pairs && uu < lim) p = pairs[uu];
+        return p;
+    };
+    auto load_off = [&](uint2 p, bool a, u64& os_, u64& ns_, u32& on_, u32& nn_) {
+        os_ = ns_ = 0;
+        on_ = nn_ = 0;
+        if (a) {
+            os_ = ooff[p.x];
+            ns_ = noff[p.y];
+            on_ = (u32)(ooff[p.x + 1] - os_);
+            nn_ = (u32)(noff[p.y + 1] - ns_);
+        }
+    };
+    u64 u0 = (u64)blockIdx.x * FD_NT;
+    u64 os = 0, ns = 0;
+    u32 on = 0, nn = 0;
+    if (u0 < lim) load_off(load_pair(u0 + lane), u0 + lane < n_upd, os, ns, on, nn);
+    for (; u0 < lim; u0 += step) {
         const u64 u = u0 + lane;
 #if KD_FD_CLOCK
         const u64 T0 = clock64(), W0 = wall_clock64();
 #endif
-        uint2 pr = make_uint2((u32)u, (u32)u);
-        if (pairs && u < lim) pr = pairs[u];
         if (u0 >= n_upd) break;  // wave-uniform
         const bool act = u < n_upd;
-        u64 os = 0, ns = 0;
-        u32 on = 0, nn = 0;
-        if (act) {
-            os = ooff[pr.x];
-            ns = noff[pr.y];
-            on = (u32)(ooff[pr.x + 1] - os);
-            nn = (u32)(noff[pr.y + 1] - ns);
-        }
+        const u64 un = u + step;
+        const uint2 pr_n = load_pair(un);
         // ---- pool allocation: exclusive wave scan of the lanes' chunk counts ----
         const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
         const u64 ab = a0 & ~(u64)15, bb = b0 & ~(u64)15;
@@ -589,6 +609,9 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             }
         }
         __syncthreads();
+        u64 os_n, ns_n;
+        u32 on_n, nn_n;
+        load_off(pr_n, un < n_upd, os_n, ns_n, on_n, nn_n);
 #if KD_FD_CLOCK
         const u64 T2 = clock64();
 #endif
@@ -596,7 +619,11 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             u64* m = masks + u * tb.words;
             u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
             u8 st;
+#if KD_FD_EXP == 1
+            if (fit) st = ((const u8*)(s_pool + off))[ad] == 7 ? 9 : 0;
+#else
             if (fit) st = diff_one((lp8)((const u8*)(s_pool + off) + ad), on, (lp8)((const u8*)(s_pool + off + na) + bd), nn, tb, mk, m);
+#endif
             else st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
             if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
             for (int w = 0; w < tb.words; w++) {
@@ -605,7 +632,8 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             }
             status[u] = st;
         }
-        __syncthreads();  // the pool and descriptors are rewritten by the next round
+        __syncthreads();  // the pool is rewritten by the next round
+        os = os_n; ns = ns_n; on = on_n; nn = nn_n;
 #if KD_FD_CLOCK
         if (lane == 0) printf("FB %u %llu %llu\n", blockIdx.x, (unsigned long long)WE, (unsigned long long)wall_clock64());
         if (lane == 0 && blockIdx.x % 97 == 0) {
@@ -768,10 +796,17 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     // the typical (mean) blob — ~(len + 15) / 16 chunks with the 16-B alignment skew — with 10 %
     // headroom (1152 chunks: seven 64-update blocks per CU for ~110-B point features); a lane whose blobs do not fit the round's pool parses them from global memory.
     const u64 per_round = (u64)FD_NT * 2 * (typ + 15) / 16 * 110 / 100;
-    const int pool = !lds_tab ? 0 : per_round <= 1152 ? 1152 : per_round <= 1536 ? 1536 : per_round <= 2048 ? 2048
+    int pool = !lds_tab ? 0 : per_round <= 1152 ? 1152 : per_round <= 1536 ? 1536 : per_round <= 2048 ? 2048
                    : per_round <= 3072 ? 3072 : per_round <= 4096 ? 4096 : 0;
+#ifndef KD_FD_FORCE_G
+#define KD_FD_FORCE_G 0  // profiling builds: 1 = always the global-memory kernel
+#endif
+#ifndef KD_FD_G_PER_CU
+#define KD_FD_G_PER_CU 8  // resident single-wave blocks per CU for the global-memory kernel
+#endif
+    if (KD_FD_FORCE_G) pool = 0;
     const u64 lds_blk = pool ? (u64)pool * 16 + 1024 + o_end : 1024;
-    const u64 per_cu = std::min<u64>(8, (160 * 1024) / lds_blk);
+    const u64 per_cu = pool ? std::min<u64>(8, (160 * 1024) / lds_blk) : (u64)KD_FD_G_PER_CU;
     unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, (u64)ctx->n_cu * per_cu);
     if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
