@@ -237,16 +237,18 @@ def test_gpu_env_overlap_vs_oracle(engine):
 
 
 @pytest.mark.parametrize("ordered", [True, False])
-@pytest.mark.parametrize("n", [1000, 3_000_000])
-def test_gpu_device_pipeline_vs_oracle(engine, n, ordered):
-    """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes)"""
+@pytest.mark.parametrize("n,layer", [(1000, "points"), (3_000_000, "points"), (1000, "polygons"),
+                                     (2_000_000, "polygons")])
+def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered):
+    """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes),
+    on the C2 points layer and the C3 polygon layer (~370-B blobs: the large LDS pool)"""
     import torch
 
     from kart_amd import synth
     from kart_amd.device import DiffPipeline
     from kart_amd.schema import FieldMaps
 
-    L = synth.points_layer(n, seed=11)
+    L = synth.points_layer(n, seed=11) if layer == "points" else synth.polygons_layer(n, seed=12)
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, torch.device("cuda", 0),
                         ordered=ordered)
