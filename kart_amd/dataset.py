@@ -255,6 +255,44 @@ def get_dataset_diff(engine, base, target, ds_filter=None):
     return ds
 
 
+# ---------------------------------------------------------------------------------------------
+# diff_estimation: exact counts straight from classify2
+# ---------------------------------------------------------------------------------------------
+ACCURACY_CHOICES = ("veryfast", "fast", "medium", "good", "exact")  # kart/diff_estimation.py:50
+
+
+def get_exact_diff_blob_count(engine, base, target):
+    """diff_estimation.get_exact_diff_blob_count (kart/diff_estimation.py:51-76) for one dataset's
+    feature trees: the number of paths `git diff --name-only --no-renames` lists = inserts +
+    updates + deletes of classify2, with no blob read and no git subprocess.
+
+    base / target: DatasetVersion or None (the empty tree)."""
+    present = base if base is not None else target
+    if present is None:
+        return 0
+    empty = packing.empty_side(present.encoding)
+    A = base.packed if base is not None else empty
+    B = target.packed if target is not None else empty
+    r = engine.diff2(A, B)
+    return int(r.n_insert + r.n_update + r.n_delete)
+
+
+def estimate_diff_feature_counts(engine, base_datasets, target_datasets, *, accuracy):
+    """diff_estimation.estimate_diff_feature_counts (kart/diff_estimation.py:96-184) without a
+    working copy: {dataset path: changed feature count}, datasets with no change left out.
+
+    base_datasets / target_datasets: {path: DatasetVersion} of the two commits.  Every accuracy
+    is answered with the exact count: the join costs less than the reference's subtree sampling,
+    so "veryfast".."good" (estimates by contract) return the exact value too."""
+    assert accuracy in ACCURACY_CHOICES
+    counts = {}
+    for path in sorted(set(base_datasets) | set(target_datasets)):
+        n = get_exact_diff_blob_count(engine, base_datasets.get(path), target_datasets.get(path))
+        if n:
+            counts[path] = n
+    return counts
+
+
 def field_diff(engine, feature_diff, old_version, new_version):
     """Attach ``changed_fields`` (names, in _all_feature_keys order) to every update delta of
     ``feature_diff``, computed by kd_fielddiff in one batch.  Updates the GPU cannot handle

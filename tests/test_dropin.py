@@ -198,3 +198,21 @@ def test_gitsource_walk(eng, tmp_path):
     D.field_diff(eng, fd, old, new)
     assert sum(len(d.changed_fields) for d in fd.values()) == 13
     repo.close()
+
+
+@pytest.mark.parametrize("name", DIFF_FIXTURES)
+def test_exact_feature_counts(eng, name):
+    """get_exact_diff_blob_count / estimate_diff_feature_counts (kart/diff_estimation.py:51-184):
+    the changed-path count of every golden diff (reference counts), and of one-sided diffs"""
+    fx = load(name)
+    for case in fx.cases("diff2"):
+        base, target = version(fx, case["base"]), version(fx, case["target"])
+        want = sum(case["counts"].values())
+        assert D.get_exact_diff_blob_count(eng, base, target) == want
+        path = fx.meta["ds_path"]
+        got = D.estimate_diff_feature_counts(eng, {path: base} if base else {}, {path: target} if target else {},
+                                             accuracy="exact")
+        assert got == ({path: want} if want else {})
+        if base is not None:  # dataset deleted in the target: every feature is a changed path
+            assert D.get_exact_diff_blob_count(eng, base, None) == base.n
+    assert D.get_exact_diff_blob_count(eng, None, None) == 0
