@@ -62,7 +62,7 @@ void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a) {
     (void)name;
     if (ctx->ev_pool.empty()) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) { *a = nullptr; return; }
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) { *a = nullptr; return; }
         ctx->ev_pool.push_back(e);
     }
     *a = ctx->ev_pool.back();
@@ -74,7 +74,7 @@ void prof_end(kd_ctx* ctx, const char* name, hipEvent_t a) {
     if (!a) return;
     hipEvent_t b;
     if (ctx->ev_pool.empty()) {
-        if (hipEventCreate(&b) != hipSuccess) return;
+        if (hipEventCreateWithFlags(&b, hipEventDisableSystemFence) != hipSuccess) return;
     } else {
         b = ctx->ev_pool.back();
         ctx->ev_pool.pop_back();
