@@ -555,21 +555,6 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
 #if KD_FD_CLOCK
     const u64 WE = wall_clock64();
 #endif
-    typedef const __attribute__((address_space(1))) u32x4* gp;
-    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp)(tab_base + i);
-    mp_tab_to_lds();
-    FdTabT<3> tb;
-    tb.n_keys = tg.n_keys; tb.words = tg.words; tb.n_lo = tg.n_lo; tb.n_ln = tg.n_ln; tb.maxv = tg.maxv;
-    typedef __attribute__((address_space(3))) u8* l8;
-    const l8 lt = (l8)s_tab;
-    tb.leg_o = (typename ASP<3, u32>::type)(lt + to.leg_o);
-    tb.leg_n = (typename ASP<3, u32>::type)(lt + to.leg_n);
-    tb.map_o = (typename ASP<3, i16>::type)(lt + to.map_o);
-    tb.map_n = (typename ASP<3, i16>::type)(lt + to.map_n);
-    tb.cmp = (typename ASP<3, u64>::type)(lt + to.cmp);
-    tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
-    tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
-    __syncthreads();
     // device count: n_upd_host is the capacity of pairs, so pairs[u] (u < capacity) is loaded
     // before the count arrives; capacity 0 = unknown -> wait for the count first
     const bool spec = n_upd_dev && n_upd_host;
@@ -596,7 +581,23 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     u64 u0 = (u64)blockIdx.x * FD_NT;
     u64 os = 0, ns = 0;
     u32 on = 0, nn = 0;
+    // (the first round's pair and offsets are in flight while the tables are copied to LDS)
     if (u0 < lim) load_off(load_pair(u0 + lane), u0 + lane < n_upd, os, ns, on, nn);
+    typedef const __attribute__((address_space(1))) u32x4* gp;
+    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp)(tab_base + i);
+    mp_tab_to_lds();
+    FdTabT<3> tb;
+    tb.n_keys = tg.n_keys; tb.words = tg.words; tb.n_lo = tg.n_lo; tb.n_ln = tg.n_ln; tb.maxv = tg.maxv;
+    typedef __attribute__((address_space(3))) u8* l8;
+    const l8 lt = (l8)s_tab;
+    tb.leg_o = (typename ASP<3, u32>::type)(lt + to.leg_o);
+    tb.leg_n = (typename ASP<3, u32>::type)(lt + to.leg_n);
+    tb.map_o = (typename ASP<3, i16>::type)(lt + to.map_o);
+    tb.map_n = (typename ASP<3, i16>::type)(lt + to.map_n);
+    tb.cmp = (typename ASP<3, u64>::type)(lt + to.cmp);
+    tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
+    tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
+    __syncthreads();
     for (; u0 < lim; u0 += step) {
         const u64 u = u0 + lane;
 #if KD_FD_CLOCK
