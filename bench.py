@@ -21,11 +21,15 @@ blobs of a spatially filtered layer (synth.geometry_layer); one step = k_envelop
 stored envelope or point WKB -> SpatialFilter bbox test + identity-CRS index envelope +
 EnvelopeEncoder bytes) + k_env_overlap (decode + cyclic overlap of the encoded envelopes).
 
+--workload c6 (--n geometries per GPU, default 20M): the C5 geometry arena hex-encoded
+as `kart diff -o json` formats geometries (kd_hex_encode: k_wkb_start WKB offsets + k_hex
+streaming 16 B -> 32 B hex per lane).
+
 Multi-GPU (torch.distributed, one process per GPU, RCCL): each rank owns a disjoint dataset3
 path-bucket range (its own shard; weak scaling); the only collective is the all-gather of per-rank
 counts each step.  value = units of all ranks / max-rank time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c5] [--n UNITS]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|c6] [--n UNITS]
                        [--no-cpu-baseline]
 """
 import argparse
@@ -48,7 +52,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "c6"])
     ap.add_argument("--n", type=int, default=0, help="units per GPU (c2: points, default 10M; c3: polygons, 100M; c4: rows, 50M; c5: geometries, 20M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unordered", action="store_true",
@@ -62,7 +66,7 @@ def parse():
                          "so the events do not inflate the step time)")
     a = ap.parse_args()
     if not a.n:
-        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c4": 50_000_000, "c5": 20_000_000}[a.workload]
+        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c4": 50_000_000, "c5": 20_000_000, "c6": 20_000_000}[a.workload]
     if a.traffic_json is None:
         a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
     return a
@@ -356,6 +360,102 @@ def run_c5(args, D):
 
 
 # ---------------------------------------------------------------------------------------------
+def run_c6(args, D):
+    """Writer formatting: hex WKB of every geometry of the C5 layer (kd_hex_encode,
+    KD_HEX_GPKG_WKB), the formatting `kart diff -o json` applies per geometry value."""
+    import ctypes
+
+    torch = D.torch
+    from kart_amd import _native as N
+    from kart_amd import synth
+    from kart_amd.device import to_dev
+    from kart_amd.engine import Engine
+
+    n = args.n
+    t0 = time.time()
+    data, off, is_pt = synth.geometry_layer(n, seed=synth.SEED + D.rank)
+    nbytes = int(off[-1])
+    log(f"[rank {D.rank}] generated {n} geometries ({nbytes / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
+    eng = Engine(torch.cuda.current_device())
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    d_data, d_off = to_dev(data, D.dev), to_dev(off, D.dev)
+    g = N.KdBlobs()
+    g.n, g.data, g.off, g.mem, g.size_hint = n, d_data.data_ptr(), d_off.data_ptr(), N.KD_MEM_DEVICE, 0
+    hexbuf = torch.empty(2 * nbytes, dtype=torch.uint8, device=D.dev)
+    start = torch.empty(n, dtype=torch.int32, device=D.dev)
+    status = torch.empty(n, dtype=torch.uint8, device=D.dev)
+    L, ctx = eng.L, eng.ctx
+
+    def step():
+        N.check(L.kd_hex_encode(ctx, ctypes.byref(g), N.KD_HEX_GPKG_WKB, hexbuf.data_ptr(), start.data_ptr(),
+                                status.data_ptr(), N.KD_MEM_DEVICE), "kd_hex_encode")
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+
+    if not args.no_check:  # every geometry is valid LE GPKG; sampled strings equal the oracle's
+        assert int(status.max().item()) == 0, "kd_hex_encode flagged a valid geometry"
+        st = start.cpu().numpy()
+        for i in list(range(0, n, max(1, n // 2000))) + [n - 1]:
+            o, e = int(off[i]), int(off[i + 1])
+            got = hexbuf[2 * (o + int(st[i])): 2 * e].cpu().numpy().tobytes().decode()
+            assert got == O.hex_wkb(data[o:e].tobytes()), f"hex WKB of geometry {i} differs from the oracle"
+    eng.prof_reset()
+    eng.prof_select(None if args.time_all else ["k_hex"])
+    eng.prof_enable(not args.no_events)
+    cnt = torch.zeros(1, dtype=torch.int64, device=D.dev)
+    gathered = [torch.empty_like(cnt) for _ in range(D.world)]
+    elapsed = D.timed(step, args.steps, lambda: D.dist.all_gather(gathered, cnt))
+    eng.prof_enable(False)
+    (total,) = D.total(n)
+    kern = kernel_times(eng, ("k_hex", "k_wkb_start"))
+    # algorithmic bytes per k_hex launch: the geometry arena read once, two hex chars written per byte
+    alg = 3 * nbytes
+    roof = roofline(kern, "k_hex", alg, args.traffic_json, "n_geoms", n)
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        m = min(n, 200_000)
+        blobs = [data[int(off[i]):int(off[i + 1])].tobytes() for i in range(m)]
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            for b in blobs:
+                O.hex_wkb(b)
+            reps += 1
+            if time.perf_counter() - t0 >= min(args.cpu_seconds, 5.0):
+                break
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(m * reps / dt / 1e6, 3), "unit": "M geometries/s", "cores": 1, "kind": "port",
+               "sample": f"first {m} geometries of the same layer x {reps} reps in {dt:.1f}s: oracle.hex_wkb "
+                         f"(the reference's gpkg_geom_to_hex_wkb restated: slice + hexlify + upper), 1 thread"}
+    eng.close()
+    return {
+        "metric": METRIC,
+        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "unit": "M geometries/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
+        "config": {"workload": f"C6 (SURVEY 8f #2, {n} geometries per GPU): hex WKB of every geometry "
+                               "(Geometry.to_hex_wkb for kart diff -o json)",
+                   "geoms_per_gpu": n, "points": int(is_pt.sum()), "arena_bytes": nbytes,
+                   "parallelism": f"independent shards x{D.world}"},
+        "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+
+
+# ---------------------------------------------------------------------------------------------
 def run_c4(args, D):
     torch = D.torch
     from kart_amd import synth
@@ -445,7 +545,7 @@ def main():
     args = parse()
     D = Dist()
     out = {"c2": run_c2, "c3": lambda a, d: run_c2(a, d, polygons=True), "c4": run_c4,
-           "c5": run_c5}[args.workload](args, D)
+           "c5": run_c5, "c6": run_c6}[args.workload](args, D)
     if D.rank == 0:
         print(json.dumps(out), flush=True)
     D.close()

@@ -16,6 +16,8 @@
  *                     CRS (kart/spatial_filter/index.py:485-579,639-707).
  *   kd_env_overlap <- sf_filter_blob decode + cyclic_range_overlaps
  *                     (vendor/spatial-filter/spatial_filter.cpp:170-260).
+ *   kd_hex_encode  <- Geometry.to_hex_wkb / gpkg_geom_to_hex_wkb (kart/geometry.py:346-375) and
+ *                     bytes.hex(v), as feature_as_json formats them (kart/feature_output.py:34-56).
  *   kd_pack_*      <- Dataset3.decode_path_to_1pk / PathEncoder (kart/dataset3.py:250-259,
  *                     kart/dataset3_paths.py:202-215,292-299): host-side key packing.
  *
@@ -175,6 +177,18 @@ int kd_envelopes(kd_ctx* ctx, const kd_blobs* geoms, const double filt_env[4], i
  * out[i] = cyclic(w,e) && range(s,n) overlap (spatial_filter.cpp:187-260). */
 int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const double q[4],
                    uint8_t* out, uint32_t mem);
+
+/* -------- writer formatting -------- */
+#define KD_HEX_BYTES 0u    /* bytes.hex(v): lowercase hex of every byte of every blob                */
+#define KD_HEX_GPKG_WKB 1u /* gpkg_geom_to_hex_wkb: uppercase hex of the WKB after the GPKG header   */
+/* hex[2*off[n]]: the hex of arena byte p lands at hex[2p], so blob i's string is
+ * hex[2*(off[i] + start[i]) .. 2*off[i+1]) (start = 0 in KD_HEX_BYTES mode; start/status may then
+ * be NULL).  KD_HEX_GPKG_WKB: start[i] = WKB offset in blob i (8 + envelope size), status[i] =
+ * 0 ok, 1 null geometry (length 0: the reference returns None), 3 needs the CPU path (invalid
+ * GPKG or empty WKB: the reference raises; big-endian WKB: the reference re-encodes via OGR).
+ * blobs->mem says where the arena lives, out_mem where hex/start/status live. */
+int kd_hex_encode(kd_ctx* ctx, const kd_blobs* blobs, uint32_t mode, uint8_t* hex, uint32_t* start,
+                  uint8_t* status, uint32_t out_mem);
 
 /* -------- host-side key packing (CPU, multithreaded) -------- */
 /* KD_KEY_INT: filenames b64(msgpack([pk])) -> keys.  status[i] = 0 ok / 1 not an int pk /

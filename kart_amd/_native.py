@@ -20,6 +20,8 @@ KD_MEM_DEVICE = 1
 KD_KEY_INT = 0
 KD_KEY_HASH = 1
 KD_DIFF_UNORDERED = 0x1
+KD_HEX_BYTES = 0
+KD_HEX_GPKG_WKB = 1
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -145,6 +147,11 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_dblp, ctypes.c_void_p,
          ctypes.c_uint32],
+    ),
+    "kd_hex_encode": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(KdBlobs), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_uint32],
     ),
     "kd_pack_int_keys": (
         ctypes.c_int64,

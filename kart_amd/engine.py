@@ -162,6 +162,25 @@ class Engine:
                                     N.KD_MEM_HOST, ctypes.byref(ncand)), "kd_envelopes")
         return match[:n], enc[:n], ok[:n], int(ncand.value)
 
+    def hex_encode(self, data, off, mode):
+        """Blob arena -> (hex u8[2*off[n]], start u32[n], status u8[n]) via kd_hex_encode (host buffers).
+        Blob i's string is hex[2*(off[i] + start[i]) : 2*off[i+1]]."""
+        data = np.ascontiguousarray(data, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        n = int(off.shape[0]) - 1
+        g = N.KdBlobs()
+        g.n = n
+        g.data = N.ptr(data) if data.size else N.ptr(np.zeros(1, np.uint8))
+        g.off = N.ptr(off)
+        g.mem = N.KD_MEM_HOST
+        nbytes = int(off[-1]) if n >= 0 and off.size else 0
+        hexbuf = np.zeros(max(2 * nbytes, 1), np.uint8)
+        start = np.zeros(max(n, 1), np.uint32)
+        status = np.zeros(max(n, 1), np.uint8)
+        N.check(self.L.kd_hex_encode(self.ctx, ctypes.byref(g), int(mode), N.ptr(hexbuf), N.ptr(start), N.ptr(status),
+                                     N.KD_MEM_HOST), "kd_hex_encode")
+        return hexbuf[: 2 * nbytes], start[:n], status[:n]
+
     def env_overlap(self, enc, bits, q):
         enc = np.ascontiguousarray(enc, np.uint8)
         n = enc.shape[0]

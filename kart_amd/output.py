@@ -1,0 +1,79 @@
+"""Writer formatting on the GPU: hex WKB of geometries and hex of bytes values.
+
+Mirrors the reference's per-value formatting, batched:
+  * ``hex_wkb_batch``     <- ``gpkg_geom_to_hex_wkb`` / ``Geometry.to_hex_wkb``
+                             (kart/geometry.py:346-375, :142-143)
+  * ``bytes_hex_batch``   <- ``bytes.hex(v)`` as ``feature_as_json`` applies it (kart/feature_output.py:54-55)
+  * ``features_as_json``  <- ``feature_as_json(row, pk_value)`` with no geometry transform
+                             (kart/feature_output.py:34-56), for a list of rows at once.
+
+Every hex string is produced by ``kd_hex_encode`` (kd_output.hip).  Geometries the kernel flags
+as needing the CPU path (big-endian WKB, which the reference re-encodes through OGR, or invalid
+GPKG, for which the reference raises) are returned in ``fallback`` for the caller's own path;
+nothing here computes a hex string on the CPU.
+"""
+import numpy as np
+
+from . import _native as N
+
+
+def _arena(values):
+    lens = np.fromiter((len(v) for v in values), np.uint64, len(values))
+    off = np.zeros(len(values) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = np.frombuffer(b"".join(values), np.uint8) if values else np.zeros(0, np.uint8)
+    return data, off
+
+
+def hex_wkb_batch(engine, geoms):
+    """geoms: sequence of GPKG geometry bytes or None.  Returns (hex_list, fallback_indices):
+    hex_list[i] is the uppercase hex WKB (str), None for a None/empty-bytes geometry, or None with
+    i in fallback_indices when the reference would go through OGR or raise."""
+    vals = [b"" if g is None else bytes(g) for g in geoms]
+    data, off = _arena(vals)
+    hexbuf, start, status = engine.hex_encode(data, off, N.KD_HEX_GPKG_WKB)
+    raw = hexbuf.tobytes()
+    out, fallback = [], []
+    for i in range(len(vals)):
+        st = int(status[i])
+        if st == 0:
+            out.append(raw[2 * (int(off[i]) + int(start[i])): 2 * int(off[i + 1])].decode("ascii"))
+        else:
+            out.append(None)
+            if st == 3:
+                fallback.append(i)
+    return out, fallback
+
+
+def bytes_hex_batch(engine, values):
+    """bytes.hex(v) for each bytes value (lowercase)."""
+    vals = [bytes(v) for v in values]
+    data, off = _arena(vals)
+    hexbuf, _, _ = engine.hex_encode(data, off, N.KD_HEX_BYTES)
+    raw = hexbuf.tobytes()
+    return [raw[2 * int(off[i]): 2 * int(off[i + 1])].decode("ascii") for i in range(len(vals))]
+
+
+def features_as_json(engine, rows, geometry_type=bytes):
+    """feature_as_json for many rows (dicts): geometries (instances of ``geometry_type``, Kart's
+    ``Geometry`` bytes subclass) -> hex WKB, other bytes -> bytes.hex, everything else unchanged.
+    Raises NotImplementedError naming the first geometry that needs the CPU (OGR) path."""
+    geo_at, geoms, byt_at, byts = [], [], [], []
+    for r, row in enumerate(rows):
+        for k, v in row.items():
+            if isinstance(v, geometry_type) and geometry_type is not bytes:
+                geo_at.append((r, k)); geoms.append(v)
+            elif isinstance(v, (bytes, bytearray)):
+                byt_at.append((r, k)); byts.append(v)
+    out = [dict(row) for row in rows]
+    if geoms:
+        hexes, fb = hex_wkb_batch(engine, geoms)
+        if fb:
+            r, k = geo_at[fb[0]]
+            raise NotImplementedError(f"geometry {k!r} of row {r} needs the OGR path (big-endian or invalid WKB)")
+        for (r, k), h in zip(geo_at, hexes):
+            out[r][k] = h
+    if byts:
+        for (r, k), h in zip(byt_at, bytes_hex_batch(engine, byts)):
+            out[r][k] = h
+    return out

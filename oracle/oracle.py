@@ -184,3 +184,24 @@ def decode_pk_from_filename(name):
     if len(pks) != 1:
         raise ValueError(f"Expected a single pk_value, got {pks}")
     return pks[0]
+
+
+# ------------------------------------------------------------------------------------------
+# writer formatting restated (kart/geometry.py:227-252,346-375; kart/feature_output.py:54-55)
+_ENV_SIZES = {0: 0, 1: 32, 2: 48, 3: 48, 4: 64}
+
+
+def hex_wkb(gpkg):
+    """gpkg_geom_to_hex_wkb restated: None -> None; 'fallback' where the reference uses OGR
+    (big-endian WKB) or raises (invalid GPKG / empty WKB)."""
+    if gpkg is None or len(gpkg) == 0:
+        return None
+    if len(gpkg) < 8 or gpkg[0:2] != b"GP" or gpkg[2] != 0 or gpkg[3] & 0x20:
+        return "fallback"
+    size = _ENV_SIZES.get((gpkg[3] & 0b1110) >> 1)
+    if size is None:
+        return "fallback"
+    wkb = gpkg[8 + size:]
+    if len(wkb) == 0 or wkb[0] == 0:
+        return "fallback"
+    return wkb.hex().upper()

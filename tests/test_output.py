@@ -1,0 +1,180 @@
+"""Writer formatting: hex WKB (kart/geometry.py:346-375) and bytes.hex
+(kart/feature_output.py:54-55) through kd_hex_encode, against the reference's own `kart diff -o json`
+golden values (tests/golden/hexwkb.json, extracted from the reference's tests/test_diff.py by
+tests/golden/gen_hexwkb.py) and the oracle restatement (oracle.hex_wkb).  Bit-exact strings.
+"""
+import json
+import os
+import struct
+
+import msgpack
+import numpy as np
+import pytest
+
+from fixtures import GOLDEN, load
+from oracle import oracle as O
+
+
+def _golden():
+    with open(os.path.join(GOLDEN, "hexwkb.json")) as f:
+        return json.load(f)
+
+
+def _geometry(fixture, side, pk):
+    """the GPKG geometry value of feature `pk` on `side` of a golden fixture repo (None when the
+    golden value comes from a working-copy edit that no fixture commit holds)"""
+    fx = load(fixture)
+    if f"{side}_names" not in fx.a:
+        return None
+    names = fx.names(side)
+    for i, name in enumerate(names):
+        if O.decode_pk_from_filename(name.rsplit("/", 1)[-1]) == pk:
+            blob = fx.blob(int(fx.a[f"{side}_blob"][i]))
+            _, vals = msgpack.unpackb(blob, raw=False, ext_hook=O._ext_hook)
+            (g,) = [v for v in vals if isinstance(v, O._Geometry)]
+            return bytes(g)
+    return None
+
+
+def _golden_geoms():
+    """(gpkg, expected hex) pairs: the fixture repos' own feature blobs where they hold the feature,
+    and for every golden value GPKG wrappings of its WKB with envelope types 0 and 1"""
+    pairs = []
+    for r in _golden():
+        g = _geometry(r["fixture"], r["side"], r["pk"])
+        if g is not None:
+            pairs.append((g, r["hex"]))
+        wkb = bytes.fromhex(r["hex"])
+        pairs.append((b"GP\x00\x01" + struct.pack("<i", 4326) + wkb, r["hex"]))
+        pairs.append((b"GP\x00\x03" + struct.pack("<i", 0) + struct.pack("<4d", 1, 2, 3, 4) + wkb, r["hex"]))
+    return pairs
+
+
+def _mixed_geoms(rng, n):
+    """LE points / polygons with every envelope type, null geometries, big-endian WKB, empty WKB,
+    extended-GPKG and bad-envelope-indicator blobs, truncated headers"""
+    out = []
+    for i in range(n):
+        r = rng.random()
+        if r < 0.03:
+            out.append(None)
+        elif r < 0.05:
+            out.append(b"GP\x00\x00" + struct.pack(">i", 4326) + struct.pack(">bIdd", 0, 1, 1.5, -2.5))  # BE WKB
+        elif r < 0.06:
+            out.append(b"GP\x00" + bytes([rng.choice([0x21, 0x0B, 0x0F])]) + b"\x00" * 60)  # extended / et 5,7
+        elif r < 0.07:
+            out.append(b"GP\x00\x01" + b"\x00\x00"[: int(rng.integers(0, 3))])  # truncated / empty WKB
+        else:
+            et = int(rng.integers(0, 5))
+            env = struct.pack("<" + "d" * {0: 0, 1: 4, 2: 6, 3: 6, 4: 8}[et], *rng.uniform(-90, 90, {0: 0, 1: 4, 2: 6, 3: 6, 4: 8}[et]))
+            body = struct.pack("<bI", 1, 1) + rng.bytes(int(rng.integers(0, 200)))
+            out.append(b"GP\x00" + bytes([1 | (et << 1) | (0x10 if rng.random() < 0.02 else 0)]) + struct.pack("<i", 4326)
+                       + env + body)
+    return out
+
+
+# ---------------------------------------------------------------- CPU: oracle vs golden
+def test_oracle_hexwkb_golden():
+    assert len(_golden()) == 12
+    pairs = _golden_geoms()
+    assert len(pairs) >= 24 + 5  # >= 5 golden features held by the fixture commits themselves
+    for g, h in pairs:
+        assert O.hex_wkb(g) == h
+
+
+def test_oracle_hexwkb_edges():
+    assert O.hex_wkb(None) is None
+    le = b"GP\x00\x01" + b"\x00" * 4 + struct.pack("<bIdd", 1, 1, 1.0, 2.0)
+    assert O.hex_wkb(le) == struct.pack("<bIdd", 1, 1, 1.0, 2.0).hex().upper()
+    assert O.hex_wkb(b"GP\x00\x00" + b"\x00" * 4 + struct.pack(">bIdd", 0, 1, 1.0, 2.0)) == "fallback"
+    assert O.hex_wkb(b"GP\x00\x21" + b"\x00" * 30) == "fallback"
+    assert O.hex_wkb(b"GP\x00\x01\x00\x00\x00\x00") == "fallback"
+
+
+# ---------------------------------------------------------------- GPU: kd_hex_encode
+@pytest.mark.gpu
+def test_gpu_hexwkb_golden(engine):
+    from kart_amd.output import hex_wkb_batch
+
+    pairs = _golden_geoms()
+    hexes, fb = hex_wkb_batch(engine, [g for g, _ in pairs])
+    assert fb == []
+    assert hexes == [h for _, h in pairs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(0, 1), (1, 2), (17, 3), (5000, 4), (200_000, 5)])
+def test_gpu_hexwkb_vs_oracle(engine, n, seed):
+    from kart_amd.output import hex_wkb_batch
+
+    geoms = _mixed_geoms(np.random.default_rng(seed), n)
+    hexes, fb = hex_wkb_batch(engine, geoms)
+    want = [O.hex_wkb(g) for g in geoms]
+    assert fb == [i for i, w in enumerate(want) if w == "fallback"]
+    assert hexes == [None if w == "fallback" else w for w in want]
+
+
+@pytest.mark.gpu
+def test_gpu_hexwkb_synthetic_layer(engine):
+    from kart_amd import _native as N
+    from kart_amd import synth
+
+    data, off, _ = synth.geometry_layer(300_000, seed=11)
+    hexbuf, start, status = engine.hex_encode(data, off, N.KD_HEX_GPKG_WKB)
+    assert not status.any()
+    raw, d = hexbuf.tobytes(), data.tobytes()
+    for i in list(range(0, 300_000, 997)) + [299_999]:
+        o, e = int(off[i]), int(off[i + 1])
+        assert raw[2 * (o + int(start[i])): 2 * e].decode() == O.hex_wkb(d[o:e])
+    # size-independent: the whole hex arena decodes back to the input bytes
+    assert bytes.fromhex(raw.decode()) == d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(0, 1), (3, 2), (1000, 3), (100_000, 4)])
+def test_gpu_bytes_hex(engine, n, seed):
+    from kart_amd.output import bytes_hex_batch
+
+    rng = np.random.default_rng(seed)
+    vals = [rng.bytes(int(rng.integers(0, 70))) for _ in range(n)]
+    assert bytes_hex_batch(engine, vals) == [v.hex() for v in vals]
+
+
+@pytest.mark.gpu
+def test_gpu_hex_device_unaligned(engine):
+    """device-resident arena off the 16-B grid takes the byte-wise kernel; same strings"""
+    import ctypes
+
+    import torch
+    from kart_amd import _native as N
+
+    rng = np.random.default_rng(9)
+    vals = [rng.bytes(int(rng.integers(0, 50))) for _ in range(3000)]
+    data = np.frombuffer(b"".join(vals), np.uint8)
+    off = np.zeros(len(vals) + 1, np.uint64)
+    np.cumsum([len(v) for v in vals], out=off[1:])
+    dev = torch.device("cuda", 0)
+    d_data = torch.zeros(data.size + 3, dtype=torch.uint8, device=dev)
+    d_data[3:] = torch.from_numpy(data.copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64).copy()).to(dev)
+    d_hex = torch.zeros(2 * data.size + 5, dtype=torch.uint8, device=dev)
+    g = N.KdBlobs()
+    g.n, g.data, g.off, g.mem, g.size_hint = len(vals), d_data.data_ptr() + 3, d_off.data_ptr(), N.KD_MEM_DEVICE, 0
+    N.check(engine.L.kd_hex_encode(engine.ctx, ctypes.byref(g), N.KD_HEX_BYTES, d_hex.data_ptr() + 1, None, None,
+                                   N.KD_MEM_DEVICE), "kd_hex_encode")
+    torch.cuda.synchronize()
+    assert d_hex[1:1 + 2 * data.size].cpu().numpy().tobytes() == data.tobytes().hex().encode()
+
+
+@pytest.mark.gpu
+def test_gpu_features_as_json(engine):
+    from kart_amd.dataset import Geometry
+    from kart_amd.output import features_as_json
+
+    g = _geometry("repo_points", "head", 2)
+    rows = [{"fid": 2, "geom": Geometry(g), "name": "test", "raw": b"\x00\xffA"},
+            {"fid": 1, "geom": None, "name": None, "raw": b""}]
+    out = features_as_json(engine, rows, geometry_type=Geometry)
+    assert out[0] == {"fid": 2, "geom": "0101000000E702F16784226640ADE666D77CFE42C0", "name": "test",
+                      "raw": "00ff41"}
+    assert out[1] == {"fid": 1, "geom": None, "name": None, "raw": ""}
