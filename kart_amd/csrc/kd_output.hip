@@ -31,19 +31,46 @@ __device__ __forceinline__ u32 hex2b(u32 x, u32 alpha) {
 }
 
 // Streaming hex encode of bytes [0, nbytes) of `src` into `dst` (2 chars per byte).  Aligned form:
-// src 16-B and dst 32-B aligned; 16 B per lane per iteration; the ragged tail byte-wise.
+// src 16-B and dst 32-B aligned.  Each lane issues U independent 16-B loads (units t, t+G, ..,
+// t+(U-1)G for G lanes in the grid: every load instruction stays fully coalesced) before its 2U
+// 16-B stores; NT selects nontemporal loads/stores (streamed once, no reuse).  Ragged tail
+// byte-wise by block 0.
+// Default: plain loads/stores, U = 4 (C6 measured: NT x1 3.48 ms, plain x1 3.48, NT x4 4.42,
+// plain x4 3.37 per 5.96-GB arena).
+#ifndef KD_HEX_VARIANT
+#define KD_HEX_VARIANT 3
+#endif
+template <bool NT, int U>
 __global__ __launch_bounds__(256) void k_hex(const u8* __restrict__ src, u64 nbytes, u8* __restrict__ dst, u32 alpha) {
     const u64 n16 = nbytes >> 4;
-    const u64 stride = (u64)gridDim.x * 256;
-    for (u64 t = (u64)blockIdx.x * 256 + threadIdx.x; t < n16; t += stride) {
-        const u32x4 v = __builtin_nontemporal_load((const u32x4*)src + t);
-        u32x4 o0, o1;
-        o0.x = hex2b(v.x, alpha); o0.y = hex2b(v.x >> 16, alpha);
-        o0.z = hex2b(v.y, alpha); o0.w = hex2b(v.y >> 16, alpha);
-        o1.x = hex2b(v.z, alpha); o1.y = hex2b(v.z >> 16, alpha);
-        o1.z = hex2b(v.w, alpha); o1.w = hex2b(v.w >> 16, alpha);
-        __builtin_nontemporal_store(o0, (u32x4*)dst + 2 * t);
-        __builtin_nontemporal_store(o1, (u32x4*)dst + 2 * t + 1);
+    const u64 G = (u64)gridDim.x * 256;
+    const u32x4* s4 = (const u32x4*)src;
+    u32x4* d4 = (u32x4*)dst;
+    for (u64 t = (u64)blockIdx.x * 256 + threadIdx.x; t < n16; t += U * G) {
+        u32x4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const u64 q = t + k * G;
+            if (q < n16) v[k] = NT ? __builtin_nontemporal_load(s4 + q) : s4[q];
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const u64 q = t + k * G;
+            if (q < n16) {
+                u32x4 o0, o1;
+                o0.x = hex2b(v[k].x, alpha); o0.y = hex2b(v[k].x >> 16, alpha);
+                o0.z = hex2b(v[k].y, alpha); o0.w = hex2b(v[k].y >> 16, alpha);
+                o1.x = hex2b(v[k].z, alpha); o1.y = hex2b(v[k].z >> 16, alpha);
+                o1.z = hex2b(v[k].w, alpha); o1.w = hex2b(v[k].w >> 16, alpha);
+                if (NT) {
+                    __builtin_nontemporal_store(o0, d4 + 2 * q);
+                    __builtin_nontemporal_store(o1, d4 + 2 * q + 1);
+                } else {
+                    d4[2 * q] = o0;
+                    d4[2 * q + 1] = o1;
+                }
+            }
+        }
     }
     if (blockIdx.x == 0) {
         for (u64 p = 16 * n16 + threadIdx.x; p < nbytes; p += 256) {
@@ -53,6 +80,19 @@ __global__ __launch_bounds__(256) void k_hex(const u8* __restrict__ src, u64 nby
         }
     }
 }
+#if KD_HEX_VARIANT == 1
+#define K_HEX k_hex<false, 1>
+#elif KD_HEX_VARIANT == 2
+#define K_HEX k_hex<true, 4>
+#elif KD_HEX_VARIANT == 3
+#define K_HEX k_hex<false, 4>
+#elif KD_HEX_VARIANT == 4
+#define K_HEX k_hex<false, 8>
+#elif KD_HEX_VARIANT == 5
+#define K_HEX k_hex<false, 2>
+#else
+#define K_HEX k_hex<true, 1>
+#endif
 
 // Unaligned form (caller-provided device pointers off the 16/32-B grid): one byte per lane.
 __global__ __launch_bounds__(256) void k_hex_bytes(const u8* __restrict__ src, u64 nbytes, u8* __restrict__ dst, u32 alpha) {
@@ -139,7 +179,7 @@ int kd_hex_encode(kd_ctx* ctx, const kd_blobs* blobs, uint32_t mode, uint8_t* he
         const bool aligned = ((u64)d_data & 15) == 0 && ((u64)d_hex & 31) == 0;
         rc = launch(ctx, "k_hex", [&] {
             if (aligned)
-                hipLaunchKernelGGL(k_hex, dim3(grid_for(bytes >> 4)), dim3(256), 0, ctx->stream, (const u8*)d_data, bytes,
+                hipLaunchKernelGGL(K_HEX, dim3(grid_for(bytes >> 4)), dim3(256), 0, ctx->stream, (const u8*)d_data, bytes,
                                    d_hex, alpha);
             else
                 hipLaunchKernelGGL(k_hex_bytes, dim3(grid_for(bytes)), dim3(256), 0, ctx->stream, (const u8*)d_data, bytes,
