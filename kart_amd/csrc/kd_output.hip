@@ -108,6 +108,8 @@ __global__ __launch_bounds__(256) void k_hex_bytes(const u8* __restrict__ src, u
 //   0 ok, 1 null geometry (length 0 -> None), 3 needs the CPU path (not GPKG v0 / extended /
 //   bad envelope indicator / truncated / empty WKB — the reference raises — or big-endian WKB,
 //   which the reference re-encodes through OGR).
+// All candidate WKB first bytes (offsets 8, 40, 56, 72 for envelope types 0, 1, 2-3, 4) are loaded
+// together with the header, so no load depends on the flags byte (one memory round trip per blob).
 __global__ __launch_bounds__(256) void k_wkb_start(const u8* __restrict__ data, const u64* __restrict__ off, u64 n,
                                                    u32* __restrict__ start, u8* __restrict__ status) {
     const u64 stride = (u64)gridDim.x * 256;
@@ -119,11 +121,14 @@ __global__ __launch_bounds__(256) void k_wkb_start(const u8* __restrict__ data, 
             st = 1;
         } else if (len >= 8) {
             const u8* g = data + o;
-            const u8 f = g[3];
+            const u8 g0 = g[0], g1 = g[1], g2 = g[2], f = g[3];
+            const u8 w8 = len > 8 ? g[8] : 0, w40 = len > 40 ? g[40] : 0, w56 = len > 56 ? g[56] : 0,
+                     w72 = len > 72 ? g[72] : 0;
             const int et = (f >> 1) & 7;
-            if (g[0] == 'G' && g[1] == 'P' && g[2] == 0 && !(f & 0x20) && et <= 4) {
+            if (g0 == 'G' && g1 == 'P' && g2 == 0 && !(f & 0x20) && et <= 4) {
                 s = 8 + (et == 0 ? 0 : et == 1 ? 32 : et <= 3 ? 48 : 64);
-                if (len > s && g[s] != 0) st = 0;
+                const u8 w = et == 0 ? w8 : et == 1 ? w40 : et <= 3 ? w56 : w72;
+                if (len > s && w != 0) st = 0;
             }
         }
         start[i] = s;
