@@ -178,3 +178,46 @@ def test_gpu_features_as_json(engine):
     assert out[0] == {"fid": 2, "geom": "0101000000E702F16784226640ADE666D77CFE42C0", "name": "test",
                       "raw": "00ff41"}
     assert out[1] == {"fid": 1, "geom": None, "name": None, "raw": ""}
+
+
+# ---------------------------------------------------------------- CPU: host-side slicing logic
+class _ArenaEngine:
+    """test double for Engine.hex_encode with the kernel's output contract (hex of byte p at 2p;
+    start / status from the oracle restatement) — exercises kart_amd.output's slicing on CPU"""
+
+    def hex_encode(self, data, off, mode):
+        from kart_amd import _native as N
+
+        raw = data.tobytes()
+        h = raw.hex().upper() if mode == N.KD_HEX_GPKG_WKB else raw.hex()
+        n = len(off) - 1
+        start = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint8)
+        if mode == N.KD_HEX_GPKG_WKB:
+            for i in range(n):
+                g = raw[int(off[i]):int(off[i + 1])]
+                w = O.hex_wkb(g)
+                status[i] = 1 if w is None else 3 if w == "fallback" else 0
+                if status[i] == 0:
+                    start[i] = len(g) - len(w) // 2
+        return np.frombuffer(h.encode(), np.uint8), start, status
+
+
+def test_output_host_slicing():
+    from kart_amd.output import bytes_hex_batch, features_as_json, hex_wkb_batch
+
+    eng = _ArenaEngine()
+    geoms = _mixed_geoms(np.random.default_rng(21), 400)
+    hexes, fb = hex_wkb_batch(eng, geoms)
+    want = [O.hex_wkb(g) for g in geoms]
+    assert fb == [i for i, w in enumerate(want) if w == "fallback"]
+    assert hexes == [None if w == "fallback" else w for w in want]
+    assert bytes_hex_batch(eng, [b"", b"\x01\xab", b"xyz"]) == ["", "01ab", "78797a"]
+    assert bytes_hex_batch(eng, []) == []
+
+    class G(bytes):
+        pass
+
+    be = G(b"GP\x00\x00" + struct.pack(">i", 4326) + struct.pack(">bIdd", 0, 1, 1.5, -2.5))
+    with pytest.raises(NotImplementedError):
+        features_as_json(eng, [{"g": be}], geometry_type=G)
