@@ -6,7 +6,7 @@
 // key on both sides with different OIDs is an update (GIT_DELTA_ADDED/DELETED/MODIFIED).
 //
 // The key union is cut into 1024-item merge-path tiles (k_partition2, guided two-level search).
-// Default (key-ordered) path, KD_C2_MODE 1:
+// Default (key-ordered) path:
 //   k_join2    one tile per 256-thread workgroup: keys by LDS-DMA into LDS, branch-free 4-ary split
 //              search + register walk, OIDs of matched pairs compared straight from HBM, ballot
 //              compaction into the tile's staging slot + tile counts + 64-tile group sums;
@@ -14,10 +14,8 @@
 //              records -> final key-ordered positions; the last tile writes the totals.
 // KD_DIFF_UNORDERED: k_join2 appends each tile's records at an atomically reserved offset (tiles in
 // completion order, key order inside each tile); no k_place2.
-// Profiling builds (KD_C2_MODE): 0 = persistent register-prefetched k_join2p + k_place2;
-// 2 = k_join2p with a decoupled look-back (slow: ~1000 tiles in flight -> long look-back walks);
-// 3 = run merge k_join2r (persistent, per-wave run rounds, see its comment) + k_place2 over wave
-// slots.  Measurements of each are in DESIGN.md §3.1.
+// (Earlier variants — a persistent register-prefetched join, a decoupled look-back and a per-wave
+// run merge — were measured slower and removed; their numbers are in DESIGN.md §3.1.)
 #include "kd_join.h"
 
 namespace kd {
@@ -31,21 +29,6 @@ constexpr u64 C2_GROUP = 64;  // tiles per group sum (staged path: k_place2 offs
 constexpr u64 C2_STAGE = C2_TILE + KD_C2_STAGE_PAD;
 #ifndef KD_PLACE_NT
 #define KD_PLACE_NT 64  // one wave per tile: up to 16 staged records per lane, all loads in flight
-#endif
-#ifndef KD_C2_MODE
-#define KD_C2_MODE 1  // ordered path: 1 per-tile k_join2 + k_place2, 0 persistent k_join2p + k_place2, 2 look-back
-#endif
-#ifndef KD_J_CLOCK
-#define KD_J_CLOCK 0  // profiling builds: run-merge phase stamps in the staging pad + one report line
-#endif
-#ifndef KD_J_EXP
-#define KD_J_EXP 0  // profiling builds only: 1 = staging only (k_join2)
-#endif
-#ifndef KD_J_OIDG
-#define KD_J_OIDG 1  // k_join2: keys-only LDS image, OIDs compared straight from HBM (more tiles per CU)
-#endif
-#ifndef KD_J2P_WAVES
-#define KD_J2P_WAVES 4  // k_join2p waves per SIMD to fit (VGPR cap): 4 four-wave workgroups per CU, no spills
 #endif
 
 // ---------------------------------------------------------------------------------------------
@@ -102,7 +85,7 @@ __device__ __forceinline__ u64 mp_search_guided(const u64* __restrict__ A, const
 // whole arrays (16 lanes each, 16-ary: ~6 rounds of random HBM reads); every inner split then lies
 // inside the box the end splits span (i and d-i are both monotone in d), at most C2_PG tiles wide,
 // and is found there by 8 lanes (8-ary) whose probes land in that small, cache-warm region.
-// The kernel also clears the counters and look-back descriptors the join needs (stream-ordered
+// The kernel also clears the counters and group sums the join needs (stream-ordered
 // before it), instead of separate memset launches.
 #ifndef KD_PTOP
 #define KD_PTOP 16  // lanes per top-level split search
@@ -169,7 +152,6 @@ struct Join2Args {
     uint2* out_upd;
     u64* counts;         // [4] inserts, updates, deletes, deltas
     u32* err;
-    u64* desc;           // persistent path: [2*ntiles] look-back descriptors
     u64 ntiles;
 };
 
@@ -194,10 +176,9 @@ __device__ __forceinline__ Range mk_range(const void* p, u64 first_byte, u64 end
 template <int NT, int IPT>
 struct Join2Lds {
     static constexpr int TILE = NT * IPT;
-    // na + nb <= TILE items; keys 8 B and OIDs 20 B per item, +1 lookahead entry on B, +1 lookbehind
-    // key per side, and at most two extra (partial) chunks per range
-    static constexpr int CH = (28 * (TILE + 1) + 16 + 15) / 16 + 8;  // + the two lookbehind keys
-    static constexpr int ROUNDS = (CH + NT - 1) / NT;
+    // keys of both sides (8 B per item, +1 lookahead key on B, +1 lookbehind key per side) and at
+    // most two extra (partial) chunks per range
+    static constexpr int CHK = (8 * (TILE + 1) + 16 + 15) / 16 + 4;
     // 4-ary search rounds until a width of TILE shrinks to 0 (w -> ceil(w/4) - 1)
     static constexpr int rounds(int w) { return w <= 0 ? 0 : 1 + rounds((w + 3) / 4 - 1); }
     static constexpr int SEARCH_ROUNDS = rounds(TILE);
@@ -205,7 +186,6 @@ struct Join2Lds {
 
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef const __attribute__((address_space(1))) void* glb_vp;
-typedef const __attribute__((address_space(1))) u32x4* gp_x4;
 
 // Tile t's place in both sides: merge-path items [d0, d1), A entries [i0, i1), B entries [j0, j1)
 // (+ the lookahead B[j1] when it exists), and the keys just before it on each side.
@@ -250,20 +230,15 @@ __device__ __forceinline__ TileGeo tile_geo(const Join2Args& g, u64 t, int TILE)
 }
 
 struct TileRanges {
-    Range ka, kb, oa, ob;
-    u32 c1, c2, c3, c4;  // chunk offsets of the four ranges in the LDS image
+    Range ka, kb;
+    u32 c1;  // chunk offset of the B key range in the LDS image
 };
 
 __device__ __forceinline__ TileRanges tile_ranges(const Join2Args& g, const TileGeo& q) {
     TileRanges r;
     r.ka = mk_range(g.A, 8 * (q.i0 - q.has_lbA), 8 * q.i1);  // + A[i0-1], B[j0-1]: the lookbehind keys
     r.kb = mk_range(g.B, 8 * (q.j0 - q.has_lbB), 8 * q.j1e);
-    r.oa = mk_range(g.oidA, 20 * q.i0, 20 * q.i1);
-    r.ob = mk_range(g.oidB, 20 * q.j0, 20 * q.j1e);
     r.c1 = r.ka.nch;
-    r.c2 = r.c1 + r.kb.nch;
-    r.c3 = r.c2 + r.oa.nch;
-    r.c4 = r.c3 + r.ob.nch;
     return r;
 }
 
@@ -338,32 +313,6 @@ __device__ __forceinline__ void tile_walk(const u64* sA, const u64* sB, const Ti
     }
 }
 
-// OID compare of the matched pairs out of the tile's LDS image, in batches of OB items: every LDS read
-// of a batch issued before its compares (OB bounds the registers held while the persistent kernel
-// also carries the next tile's prefetch)
-template <int IPT, typename P = const u32*>
-__device__ __forceinline__ void tile_oid_lds(P oA, P oB, u32 rec[IPT]) {
-    constexpr int OB = IPT < 2 ? IPT : 2;
-#pragma unroll
-    for (int k0 = 0; k0 < IPT; k0 += OB) {
-        u32 x[OB][5], y[OB][5];
-#pragma unroll
-        for (int k = 0; k < OB; k++) {
-            const bool m = (rec[k0 + k] >> 25) == R_MATCH;
-            const u32 ia = m ? rec[k0 + k] & 0xFFF : 0, jb = m ? (rec[k0 + k] >> 12) & 0xFFF : 0;
-#pragma unroll
-            for (int w = 0; w < 5; w++) { x[k][w] = oA[5 * ia + w]; y[k][w] = oB[5 * jb + w]; }
-        }
-#pragma unroll
-        for (int k = 0; k < OB; k++) {
-            u32 d = 0;
-#pragma unroll
-            for (int w = 0; w < 5; w++) d |= x[k][w] ^ y[k][w];
-            if ((rec[k0 + k] >> 25) == R_MATCH && d) rec[k0 + k] |= 1u << 24;
-        }
-    }
-}
-
 // OID compare straight from HBM (keys-only LDS image): each thread loads the two 20-B OIDs of its own
 // matched pairs (consecutive items -> neighbouring entries across lanes), all loads issued before any
 // compare
@@ -386,13 +335,6 @@ __device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGe
         for (int w = 0; w < 5; w++) d |= x[k][w] ^ y[k][w];
         if ((rec[k] >> 25) == R_MATCH && d) rec[k] |= 1u << 24;
     }
-}
-
-template <int NT, int IPT>
-__device__ __forceinline__ void tile_merge(const u64* sA, const u64* sB, const u32* oA, const u32* oB, const TileGeo& q,
-                                           u32 rec[IPT], bool& bad) {
-    tile_walk<NT, IPT>(sA, sB, q, rec, bad);
-    tile_oid_lds<IPT>(oA, oB, rec);
 }
 
 // KD_KEY_HASH: a matched key must also match the full filename (a 64-bit key collision between two
@@ -486,9 +428,7 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // (HASH: filename checks compiled in; the int-key instantiation carries none of their registers)
     using LD = Join2Lds<NT, IPT>;
     static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
-    constexpr int NRANGE = KD_J_OIDG ? 2 : 4;  // keys only, or keys + OIDs
-    constexpr int CHK = (8 * (LD::TILE + 1) + 16 + 15) / 16 + 4;  // chunks of the two key ranges
-    __shared__ u32x4 s_ch[KD_J_OIDG ? CHK : LD::CH];  // lanes past the tile's chunks are masked off
+    __shared__ u32x4 s_ch[LD::CHK];  // the two key ranges; lanes past the tile's chunks are masked off
     __shared__ u32 s_wave[3 * NT / 64];
     __shared__ u64 s_base[2];
     const int tid = threadIdx.x;
@@ -497,15 +437,15 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     if (!q.ok && tid == 0) atomicOr(g.err, 1u);
     const TileRanges r = tile_ranges(g, q);
     // 64-chunk pieces (one wave-instruction each: wave-uniform source base and LDS base, lane l takes
-    // chunk 64p + l), dealt round-robin to the waves across the four ranges: scalar address math
+    // chunk 64p + l), dealt round-robin to the waves across the two ranges: scalar address math
     {
         constexpr int NW = NT / 64;
         const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
         u32 q0 = 0;
 #pragma unroll
-        for (int k = 0; k < NRANGE; k++) {
-            const Range& R = k == 0 ? r.ka : k == 1 ? r.kb : k == 2 ? r.oa : r.ob;
-            const u32 off = k == 0 ? 0 : k == 1 ? r.c1 : k == 2 ? r.c2 : r.c3;
+        for (int k = 0; k < 2; k++) {
+            const Range& R = k == 0 ? r.ka : r.kb;
+            const u32 off = k == 0 ? 0 : r.c1;
             const u32 np = (R.nch + 63) >> 6;
             for (u32 p = (u32)(wid + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
                 const u32 c = 64 * p + lane;
@@ -518,33 +458,15 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     __syncthreads();  // vmcnt(0) + barrier: the DMA has landed
     const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
     const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
-    const u32* oA = (const u32*)((const u8*)(s_ch + r.c2) + r.oa.skew);  // 4-B aligned: 20*i is
-    const u32* oB = (const u32*)((const u8*)(s_ch + r.c3) + r.ob.skew);  // and allocations are
-#if KD_J_EXP == 1
-    if (tid == 0 && !UNORD) {
-        u32* c = g.tile_cnt + 4 * tile;
-        c[0] = c[1] = c[2] = c[3] = ((const u32*)s_ch)[tid] == 0x12345678u ? 1u : 0u;
-    }
-    return;
-#endif
     u32 rec[IPT];
     bool bad = false;
-#if KD_J_EXP == 2  // profiling: no merge path (records from the item index), OID loads kept
-#pragma unroll
-    for (int k = 0; k < IPT; k++) rec[k] = (R_MATCH << 25) | ((u32)((tid * IPT + k) / 2) << 12) | (u32)((tid * IPT + k) / 2);
-    bad = sA[tid] == 0x123456789ull && sB[tid] == 7;
-#else
     tile_walk<NT, IPT>(sA, sB, q, rec, bad);
-#endif
     // complete order check: the walk only compares the keys it consumes, and on unsorted input the
     // per-thread merge-path splits can skip keys, so every adjacent pair of the tile's two ranges
     // (the first against the lookbehind key) is checked here as well
     for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
     for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
-#if KD_J_EXP != 3  // 3: profiling, no OID compare
-    if (KD_J_OIDG) tile_oid_global<IPT>(g, q, rec);
-    else tile_oid_lds<IPT>(oA, oB, rec);
-#endif
+    tile_oid_global<IPT>(g, q, rec);
     if (HASH) tile_names<IPT>(g, q, rec);
     if (bad) atomicOr(g.err, 1u);
     const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
@@ -579,500 +501,11 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_join2r: run merge — one tile per workgroup, each wave walks its own 256-item stretch in runs
-// ---------------------------------------------------------------------------------------------
-// The merge path of a diff is almost all matched pairs, broken by short runs of inserts or deletes.
-// A wave therefore does not search a split for every lane: it walks its stretch in rounds, lane l
-// looking at A[a+l] and B[b+l] at once —
-//   pair round: the leading lanes with equal keys are matched pairs (OIDs compared from LDS, changed
-//               ones emitted), a and b advance by that count;
-//   run round:  (first keys differ) the leading lanes of A below B[b] are deletes, or of B below A[a]
-//               inserts, emitted and skipped in one step.
-// A 1 %-edit stretch of 256 items takes ~6 rounds of one LDS read pair + ballots each.  A stretch
-// still unfinished after RMAX rounds (dense interleaved edits) is finished by the per-lane merge path
-// (search + walk) restricted to what is left.  Records go to the wave's own slot (256 records) of the
-// tile's staging area, in key order; k_place2 concatenates the four slots.
-constexpr int RW = 64 * C2_IPT;  // merge-path items per wave stretch (one tile: NT/64 stretches)
-#ifndef KD_RMAX
-#define KD_RMAX 24        // run rounds before the per-lane fallback
-#endif
-
-// 64-lane 64-ary merge-path search over the tile's LDS keys (2 rounds for a 1024-item tile)
-__device__ __forceinline__ int mp_search_lds64(const u64* sA, const u64* sB, int d, int lo, int hi) {
-    const int lane = threadIdx.x & 63;
-    while (hi > lo) {
-        const int step = (hi - lo + 63) >> 6;
-        const int probe = lo + step * (lane + 1) - 1;
-        const int pc = probe < hi ? probe : hi - 1;
-        const bool p = probe >= hi || sA[pc] > sB[d - 1 - pc];
-        const u64 bal = __ballot(p);
-        if (bal == 0) return hi;
-        const int f = __ffsll((long long)bal) - 1;
-        const int nh = lo + step * (f + 1) - 1;
-        lo = lo + step * f;
-        hi = nh < hi ? nh : hi;
-        if (step == 1) return hi;
-    }
-    return lo;
-}
-
-// Per-lane merge path (search + register walk) over what is left of a wave's stretch:
-// A [a, ae), B [b, be) (tile-local; B keys readable up to nbx, the tile's lookahead included).
-// Item outcome records as in tile_walk.
-template <int IPT>
-__device__ __forceinline__ void wave_walk(const u64* sA, const u64* sB, int a, int ae, int b, int be, int nbx,
-                                          bool has_lbA, u32 rec[IPT]) {
-    const int lane = threadIdx.x & 63;
-    const int na = ae - a, nb = be - b, nitems = na + nb;
-    const int dd = lane * IPT < nitems ? lane * IPT : nitems;
-    const int cnt = (dd + IPT < nitems ? dd + IPT : nitems) - dd;
-    int lo = dd - nb > 0 ? dd - nb : 0, hi = dd < na ? dd : na;
-    while (lo < hi) {  // binary search: this path only runs for dense-edit stretches
-        const int mid = (lo + hi) >> 1;
-        if (sA[a + mid] <= sB[b + dd - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    int ia = a + lo, jb = b + dd - lo;
-    const bool ap_ok0 = ia > 0 || has_lbA;
-    u64 ap = sA[ia - 1];
-    bool ap_ok = ap_ok0;
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        rec[k] = R_NONE << 25;
-        if (k < cnt) {
-            const u64 ka = ia < ae ? sA[ia] : ~0ull, kb = jb < nbx ? sB[jb] : ~0ull;
-            if (jb >= be || (ia < ae && ka <= kb)) {
-                const bool m = jb < nbx && kb == ka;
-                rec[k] = ((m ? R_MATCH : R_DEL) << 25) | ((u32)jb << 12) | (u32)ia;
-                ap = ka;
-                ap_ok = true;
-                ia++;
-            } else {
-                const bool partner = ap_ok && ap == kb;
-                rec[k] = ((partner ? R_NONE : R_INS) << 25) | ((u32)jb << 12) | (u32)ia;
-                jb++;
-            }
-        }
-    }
-}
-
-// Run-merge LDS image: keys and OIDs in separate arrays (distinct alias scopes: the waitcnt pass then
-// knows a key read cannot overlap an OID LDS-DMA still in flight, and inserts no vmcnt wait for it)
-template <int NT>
-struct RunLds {
-    static constexpr int TILE = NT * C2_IPT;
-    static constexpr int CHK = (8 * (TILE + 3) + 15) / 16 + 4;   // A + lookbehind, B + lookbehind + lookahead
-    static constexpr int CHO = (20 * (TILE + 1) + 15) / 16 + 4;  // A, B + lookahead
-};
-
-// LDS-DMA staging of one tile: wave 0 issues the key pieces (then waits for them alone), waves 1.. the
-// OID pieces, dealt round-robin.  Issue only.
-template <int NT>
-__device__ __forceinline__ void run_stage(const TileRanges& r, u32x4* s_key, u32x4* s_oid) {
-    constexpr int NW = NT / 64;
-    static_assert(NW >= 2, "one key wave + at least one OID wave");
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (w == 0) {
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const Range& R = k == 0 ? r.ka : r.kb;
-            u32x4* dst = s_key + (k == 0 ? 0 : r.c1);
-            for (u32 p = 0; 64 * p < R.nch; p++) {
-                const u32 c = 64 * p + lane;
-                if (c < R.nch) __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(dst + 64 * p), 16, 0, 0);
-            }
-        }
-    } else {
-        const u32 npa = (r.oa.nch + 63) >> 6, np = npa + ((r.ob.nch + 63) >> 6);
-        for (u32 p = (u32)(w - 1); p < np; p += NW - 1) {
-            const bool onA = p < npa;
-            const Range& R = onA ? r.oa : r.ob;
-            const u32 pp = onA ? p : p - npa;
-            u32x4* dst = s_oid + (onA ? 0 : r.c3 - r.c2) + 64 * pp;
-            const u32 c = 64 * pp + lane;
-            if (c < R.nch) __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)dst, 16, 0, 0);
-        }
-    }
-}
-
-// workgroup barrier that waits for LDS traffic only: an LDS-DMA still in flight stays in flight
-// across it (__syncthreads would also drain vmcnt)
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// 64-bit value of lane 0 (wave-uniform: SGPRs)
-__device__ __forceinline__ u64 lane0_64(u64 x) {
-    return (u64)(u32)__builtin_amdgcn_readlane((u32)x, 0) | (u64)(u32)__builtin_amdgcn_readlane((u32)(x >> 32), 0) << 32;
-}
-
-// run descriptor: kind << 30 | length << 23 | a << 11 | b   (tile-local a, b < 2048; length <= 64)
-enum : u32 { RUN_PAIR = 0, RUN_DEL = 1, RUN_INS = 2 };
-static_assert(C2_TILE <= 2048, "run descriptors hold 11-bit tile-local indices");
-
-// Run merge of one tile, in two phases so that the OIDs land while the keys are walked.
-//   phase 1 (keys only — wave 0 waited for its key DMA, the OID DMA is still in flight): key order
-//     check, per-wave stretch splits, then the run rounds: lane l looks at A[a+l] and B[b+l]; the
-//     leading equal lanes are matched pairs, or (first keys differ) the leading A below B[b] are
-//     deletes or the leading B below A[a] inserts.  A round only records its run (one descriptor per
-//     round, in lane `round` of a VGPR); the walk state stays in SGPRs (scalar branches only).
-//   phase 2 (after the OID DMA has landed): the runs in order — OIDs of each pair run compared out of
-//     LDS, changed pairs, deletes and inserts written to the wave's slot in key order.
-// A stretch still unfinished after RMAX rounds (dense interleaved edits) is finished by the per-lane
-// merge path (search + walk) over what is left.
-template <int NT, bool HASH, typename LandOids>
-__device__ __forceinline__ void run_tile(const Join2Args& g, const TileGeo& q, const TileRanges& r, const u32x4* s_key,
-                                         const u32x4* s_oid, int* s_split, u32 (*s_cnt)[4], u64 tile,
-                                         LandOids land_oids) {
-    constexpr int NW = NT / 64, TILE = NW * RW, IPL = RW / 64;  // IPL: items per lane (fallback walk)
-    static_assert(KD_RMAX <= 64, "one run descriptor per lane");
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const u64* sA = (const u64*)((const u8*)s_key + r.ka.skew) + q.has_lbA;
-    const u64* sB = (const u64*)((const u8*)(s_key + r.c1) + r.kb.skew) + q.has_lbB;
-    // address space 3 + volatile: single ds_read_b32s (merged ds_read2s lose the alias scope)
-    typedef const volatile __attribute__((address_space(3))) u32* lds_vu32;
-    const lds_vu32 oA = (lds_vu32)((const u8*)s_oid + r.oa.skew);
-    const lds_vu32 oB = (lds_vu32)((const u8*)(s_oid + (r.c3 - r.c2)) + r.ob.skew);
-    const int na = q.na, nb = q.nb, nitems = na + nb, nbx = nb + (q.has_la ? 1 : 0);
-#if KD_J_CLOCK
-    u64* clk = (u64*)(g.stage_delta + tile * (u64)C2_STAGE + TILE);
-#endif
-
-    // ---- strictly ascending keys: item c of the tile checks its key against the one before it ----
-    bool bad = false;
-#pragma unroll
-    for (int k = 0; k < TILE / NT; k++) {
-        const int c = k * NT + tid;
-        const bool onA = c < na;
-        const int ci = onA ? c : c - na;
-        const bool chk = (c < nitems) & (ci > 0 || (onA ? q.has_lbA : q.has_lbB));
-        const u64* s = onA ? sA : sB;
-        const int cc = chk ? ci : 1;
-        const u64 k0 = s[cc - 1], k1 = s[cc];
-        bad |= chk & (k0 >= k1);
-    }
-    if (__ballot(bad) && lane == 0) atomicOr(g.err, 1u);
-#if KD_J_CLOCK
-    if (tid == 0) clk[2] = wall_clock64();
-#endif
-
-    // ---- the stretch splits: wave w >= 1 finds the split at item w*RW ----
-    if (tid == 0) { s_split[0] = 0; s_split[NW] = na; }
-    if (wid >= 1) {
-        const int d = wid * RW < nitems ? wid * RW : nitems;
-        const int sp = mp_search_lds64(sA, sB, d, d - nb > 0 ? d - nb : 0, d < na ? d : na);
-        if (lane == 0) s_split[wid] = sp;
-    }
-    lds_barrier();
-#if KD_J_CLOCK
-    if (tid == 0) clk[3] = wall_clock64();
-#endif
-    int a = __builtin_amdgcn_readfirstlane(s_split[wid]);
-    const int ae = __builtin_amdgcn_readfirstlane(s_split[wid + 1]);
-    const int d0 = wid * RW < nitems ? wid * RW : nitems, d1 = (wid + 1) * RW < nitems ? (wid + 1) * RW : nitems;
-    int b = __builtin_amdgcn_readfirstlane(d0 - a);
-    const int be = __builtin_amdgcn_readfirstlane(d1 - ae);
-    // the stretch's first B may be the partner of the A just before it (matched there)
-    if (b < be && (a > 0 || q.has_lbA) && uni64(sA[a - 1]) == uni64(sB[b])) b++;
-
-    // ---- phase 1: the run rounds over the keys ----
-    const int amax = na > 0 ? na - 1 : 0, bmax = nbx > 0 ? nbx - 1 : 0;
-    u32 runs = 0;  // lane k: descriptor of round k
-    int nr = 0;
-    for (; nr < KD_RMAX && a + b < ae + be; nr++) {
-        const int la = a + lane, lb = b + lane;
-        const u64 ka = sA[la < amax ? la : amax], kb = sB[lb < bmax ? lb : bmax];
-        const bool ina = la < ae;
-        const u64 ne = __ballot(!(ina && lb < nbx && ka == kb));
-        const int f = ne ? __ffsll((long long)ne) - 1 : 64;  // leading matched pairs
-        u32 desc;
-        if (f > 0) {
-            desc = RUN_PAIR << 30 | (u32)f << 23 | (u32)a << 11 | (u32)b;
-            a += f;
-            b += f;
-        } else {
-            // lane 0 holds A[a] and B[b] (B[be] is the lookahead: an A below it is a delete)
-            const u64 ka0 = a < ae ? lane0_64(ka) : ~0ull, kb0 = b < nbx ? lane0_64(kb) : ~0ull;
-            if (ka0 < kb0) {
-                const u64 nd = __ballot(!(ina && ka < kb0));
-                const int run = nd ? __ffsll((long long)nd) - 1 : 64;
-                desc = RUN_DEL << 30 | (u32)run << 23 | (u32)a << 11 | (u32)b;
-                a += run;
-            } else {
-                const u64 ni = __ballot(!(lb < be && kb < ka0));
-                const int run = ni ? __ffsll((long long)ni) - 1 : 64;
-                desc = RUN_INS << 30 | (u32)run << 23 | (u32)a << 11 | (u32)b;
-                b += run;
-            }
-        }
-        runs = lane == nr ? desc : runs;
-    }
-#if KD_J_CLOCK
-    if (lane == 0) { clk[4 + wid] = wall_clock64(); clk[8 + wid] = nr + ((a < ae || b < be) ? 1000 : 0); }
-#endif
-
-    // ---- the OIDs land in LDS (and a barrier publishes them) ----
-    land_oids();
-#if KD_J_CLOCK
-    if (tid == 0) clk[14] = wall_clock64();
-#endif
-
-    // ---- phase 2: the runs in key order ----
-    uint2* sd = g.stage_delta + tile * (u64)C2_STAGE + wid * RW;
-    uint2* su = g.stage_upd + tile * (u64)C2_STAGE + wid * RW;
-    const u32 i0 = (u32)q.i0, j0 = (u32)q.j0;
-    const u64 lt = (1ull << lane) - 1;  // lanes below this one
-    u32 cd = 0, cu = 0, cx = 0, ci = 0;
-    for (int k = 0; k < nr; k++) {
-        const u32 desc = __builtin_amdgcn_readlane(runs, k);
-        const u32 kind = desc >> 30, len = (desc >> 23) & 127, ra = (desc >> 11) & 2047, rb = desc & 2047;
-        const u32 la = ra + lane, lb = rb + lane;
-        if (kind == RUN_PAIR) {
-            const u32 ia = lane < len ? la : ra, jb = lane < len ? lb : rb;
-            u32 d = 0;
-#pragma unroll
-            for (int w = 0; w < 5; w++) d |= oA[5 * ia + w] ^ oB[5 * jb + w];
-            if (HASH && lane < len && !names_eq(g.nameA, g.nameOffA, q.i0 + la, g.nameB, g.nameOffB, q.j0 + lb))
-                atomicOr(g.err, 2u);
-            const bool chg = (lane < len) & (d != 0);
-            const u64 bc = __ballot(chg);
-            if (bc) {
-                if (chg) {
-                    const u32 pos = (u32)__popcll(bc & lt);
-                    const uint2 v = make_uint2(i0 + la, j0 + lb);
-                    sd[cd + pos] = v;
-                    su[cu + pos] = v;
-                }
-                cd += (u32)__popcll(bc);
-                cu += (u32)__popcll(bc);
-            }
-        } else {
-            const bool del = kind == RUN_DEL;
-            if (lane < len) sd[cd + lane] = del ? make_uint2(i0 + la, KD_NONE) : make_uint2(KD_NONE, j0 + lb);
-            cd += len;
-            if (del) cx += len;
-            else ci += len;
-        }
-    }
-    if (a < ae || b < be) {  // dense edits: the per-lane merge path finishes the stretch
-        if (b > be) b = be;    // (only on unsorted input, already flagged: keeps the walk in bounds)
-        u32 rec[IPL];
-        wave_walk<IPL>(sA, sB, a, ae, b, be, nbx, q.has_lbA, rec);
-        tile_oid_lds<IPL, lds_vu32>(oA, oB, rec);
-        if (HASH) tile_names<IPL>(g, q, rec);
-        TileCounts c;
-        c.fd = c.fu = 0;
-        u32 fx = 0, fi = 0;
-#pragma unroll
-        for (int k = 0; k < IPL; k++) {
-            const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1;
-            const u32 isx = (u32)(kind == R_DEL), isi = (u32)(kind == R_INS), isu = (u32)(kind == R_MATCH) & chg;
-            c.fd |= (isx | isi | isu) << k;
-            c.fu |= isu << k;
-            fx |= isx << k;
-            fi |= isi << k;
-        }
-        // thread-major item order: this lane's records follow every record of the lanes below it
-        u32 od = 0, ou = 0, wd = 0, wu = 0;
-#pragma unroll
-        for (int k = 0; k < IPL; k++) {
-            const u64 bd = __ballot((c.fd >> k) & 1), bu = __ballot((c.fu >> k) & 1);
-            od += (u32)__popcll(bd & lt);
-            ou += (u32)__popcll(bu & lt);
-            wd += (u32)__popcll(bd);
-            wu += (u32)__popcll(bu);
-            cx += (u32)__popcll(__ballot((fx >> k) & 1));
-            ci += (u32)__popcll(__ballot((fi >> k) & 1));
-        }
-        c.od = cd + od;
-        c.ou = cu + ou;
-        tile_write<IPL>(rec, c, i0, j0, sd, su);
-        cd += wd;
-        cu += wu;
-    }
-#if KD_J_CLOCK
-    if (lane == 0) clk[16 + wid] = wall_clock64();
-#endif
-    if (lane == 0) { s_cnt[wid][0] = cd; s_cnt[wid][1] = cu; s_cnt[wid][2] = cx; s_cnt[wid][3] = ci; }
-    lds_barrier();
-#if KD_J_CLOCK
-    if (tid == 0) clk[12] = wall_clock64();
-#endif
-    if (tid == 0) {
-        static_assert(NW <= 4, "tile_cnt packs at most four wave slots");
-        u32 td = 0, tu = 0, tx = 0, tn = 0, packed[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int w = 0; w < NW; w++) {
-            td += s_cnt[w][0]; tu += s_cnt[w][1]; tx += s_cnt[w][2]; tn += s_cnt[w][3];
-            packed[w] = s_cnt[w][0] | s_cnt[w][1] << 16;
-        }
-        *(uint4*)(g.tile_cnt + 4 * tile) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
-        u64* gs = g.gsum + 2 * (tile / C2_GROUP);
-        atomicAdd((unsigned long long*)gs, (unsigned long long)(td | (u64)tu << 32));
-        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tn | (u64)tx << 32));
-    }
-}
-
-#if KD_J_CLOCK
-// stamps per tile (u64, in the staging pad): 13 before staging, 0 keys landed, 2 after the key check,
-// 3 after the split barrier, 4+w wave w's rounds done, 8+w its rounds (+1000 = fell back), 14 OIDs
-// landed, 16+w its records written, 12 after the final barrier
-__global__ void k_jclk_report(const uint2* stage, u64 ntiles) {
-    constexpr int NS = 11;
-    __shared__ double s_sum[NS][256];
-    double sm[NS] = {};
-    for (u64 t = threadIdx.x; t < ntiles; t += 256) {
-        const u64* p = (const u64*)(stage + t * (u64)C2_STAGE + C2_TILE);
-        double r = 0, fb = 0, wr = 0, wl = 0;
-        for (int w = 0; w < C2_NT / 64; w++) {
-            r += (double)(p[8 + w] % 1000); fb += p[8 + w] >= 1000;
-            wr += (double)(p[4 + w] - p[3]); wl += (double)(p[16 + w] - p[14]);
-            sm[10] += (double)(p[20 + w] - p[4 + w]) / (C2_NT / 64);
-        }
-        const double nw = C2_NT / 64;
-        sm[0] += (double)(p[0] - p[13]); sm[1] += (double)(p[2] - p[0]); sm[2] += (double)(p[3] - p[2]);
-        sm[3] += wr / nw; sm[4] += (double)(p[14] - p[3]); sm[5] += wl / nw; sm[6] += (double)(p[12] - p[14]);
-        sm[7] += r / nw; sm[8] += fb; sm[9] += (double)(p[12] - p[13]);
-    }
-    for (int k = 0; k < NS; k++) s_sum[k][threadIdx.x] = sm[k];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int i = 1; i < 256; i++)
-            for (int k = 0; k < NS; k++) sm[k] += s_sum[k][i];
-        const double n = (double)ntiles, us = 0.01 / n;
-        printf("JCLK tiles %llu mean_us keys %.3f check %.3f split %.3f rounds %.3f oids_landed %.3f emit %.3f "
-               "tail %.3f total %.3f | rounds/wave %.2f fallbacks %.0f own_oid_wait %.3f\n",
-               (unsigned long long)ntiles, sm[0] * us, sm[1] * us, sm[2] * us, sm[3] * us, sm[4] * us, sm[5] * us,
-               sm[6] * us, sm[9] * us, sm[7] / n, sm[8], sm[10] * us);
-    }
-}
-#endif
-
-// Register staging of one tile: every thread loads a fixed number of 16-byte chunks of the key ranges
-// (KP) and of the OID ranges (OP) — all loads issued up front, lanes past a range reload its first chunk
-// (fixed counts: the compiler's vmcnt waits stay exact) — the keys are written to LDS at once, the OIDs
-// only after the key phase (their loads stay in flight meanwhile).  Plain loads, not LDS-DMA: DMA
-// writes into LDS lose arbitration to the co-resident workgroups' ds_reads and landed several µs late.
-template <int NT>
-struct RunRegs {
-    static constexpr int KP = (RunLds<NT>::CHK + NT - 1) / NT, OP = (RunLds<NT>::CHO + NT - 1) / NT;
-    u32x4 k[KP], o[OP];
-};
-
-template <int NT>
-__device__ __forceinline__ void run_load(const TileRanges& r, RunRegs<NT>& v) {
-    typedef const __attribute__((address_space(1))) u32x4* gx4;
-    const u32 tid = threadIdx.x, nk = r.c2, no = r.c4 - r.c2;
-#pragma unroll
-    for (int k = 0; k < RunRegs<NT>::KP; k++) {
-        const u32 c = k * NT + tid;
-        const bool onA = c < r.c1;
-        const Range& R = onA ? r.ka : r.kb;
-        const u32 cc = c < nk ? (onA ? c : c - r.c1) : 0;
-        v.k[k] = *(gx4)(R.base + 16ull * cc);
-    }
-#pragma unroll
-    for (int k = 0; k < RunRegs<NT>::OP; k++) {
-        const u32 c = k * NT + tid;
-        const bool onA = c < r.c3 - r.c2;
-        const Range& R = onA ? r.oa : r.ob;
-        const u32 cc = c < no ? (onA ? c : c - (r.c3 - r.c2)) : 0;
-        v.o[k] = *(gx4)(R.base + 16ull * cc);
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void run_put_keys(const TileRanges& r, const RunRegs<NT>& v, u32x4* s_key) {
-#pragma unroll
-    for (int k = 0; k < RunRegs<NT>::KP; k++) {
-        const u32 c = k * NT + threadIdx.x;
-        if (c < r.c2) s_key[c] = v.k[k];
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void run_put_oids(const TileRanges& r, const RunRegs<NT>& v, u32x4* s_oid) {
-#pragma unroll
-    for (int k = 0; k < RunRegs<NT>::OP; k++) {
-        const u32 c = k * NT + threadIdx.x;
-        if (c < r.c4 - r.c2) s_oid[c] = v.o[k];
-    }
-}
-
-// Persistent and software-pipelined: workgroup b merges tiles b, b + G, b + 2G, ... (G = the grid,
-// sized so that every workgroup is resident).  As soon as a tile's OIDs are in LDS (after its key
-// phase), the loads of the next tile are issued into the same registers: they fly during the current
-// tile's emit phase, and the next tile's split points one tile further ahead.
-template <int NT, bool HASH>
-__global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
-    using LD = RunLds<NT>;
-    static_assert(LD::TILE == (NT / 64) * RW, "one RW-item stretch per wave");
-    __shared__ u32x4 s_key[LD::CHK];
-    __shared__ u32x4 s_oid[LD::CHO];
-    __shared__ int s_split[NT / 64 + 1];
-    __shared__ u32 s_cnt[NT / 64][4];  // per wave: deltas, updates, deletes, inserts
-    u64 tile = blockIdx.x;
-    if (tile >= g.ntiles) return;
-    TileGeo q = tile_geo(g, tile, LD::TILE);
-    if (!q.ok && threadIdx.x == 0) atomicOr(g.err, 1u);
-    TileRanges r = tile_ranges(g, q);
-    RunRegs<NT> v;
-    run_load<NT>(r, v);
-    u64 tn = tile + gridDim.x, p0 = 0, p1 = 0;
-    if (tn < g.ntiles) { p0 = g.part[tn]; p1 = g.part[tn + 1]; }
-    run_put_keys<NT>(r, v, s_key);
-    lds_barrier();
-    for (;;) {
-#if KD_J_CLOCK
-        if (threadIdx.x == 0) {
-            u64* clk = (u64*)(g.stage_delta + tile * (u64)C2_STAGE + LD::TILE);
-            clk[0] = clk[13] = wall_clock64();
-        }
-#endif
-        const bool more = tn < g.ntiles;
-        TileGeo qn = q;
-        TileRanges rn = r;
-        u64 tnn = tn;
-        run_tile<NT, HASH>(g, q, r, s_key, s_oid, s_split, s_cnt, tile, [&] {
-#if KD_J_CLOCK
-            vm_drain();
-            if ((threadIdx.x & 63) == 0)
-                ((u64*)(g.stage_delta + tile * (u64)C2_STAGE + LD::TILE))[20 + (threadIdx.x >> 6)] = wall_clock64();
-#endif
-            run_put_oids<NT>(r, v, s_oid);
-            lds_barrier();
-            if (more) {  // the next tile's loads fly during this tile's emit phase
-                qn = tile_geo_from(g, tn, LD::TILE, p0, p1);
-                if (!qn.ok && threadIdx.x == 0) atomicOr(g.err, 1u);
-                rn = tile_ranges(g, qn);
-                run_load<NT>(rn, v);
-                tnn = tn + gridDim.x;
-                if (tnn < g.ntiles) { p0 = g.part[tnn]; p1 = g.part[tnn + 1]; }
-            }
-        });  // ends with a barrier: LDS free for the next tile
-        if (!more) break;
-        run_put_keys<NT>(rn, v, s_key);
-        lds_barrier();
-        tile = tn;
-        q = qn;
-        r = rn;
-        tn = tnn;
-    }
-}
-
 // Staged path: tile-local staging -> final key-ordered positions; one tile per block.  The tile's
 // output offset = the group sums of all earlier C2_GROUP-tile groups + the counts of the earlier
-// tiles of its own group; the last block also writes the totals.
-// WS (k_join2r): a tile's records sit in NW wave slots of RW records, tile_cnt holds per wave
-// deltas | updates << 16; otherwise one contiguous slot and tile_cnt = inserts, updates, deletes, deltas.
-template <bool WS>
-__device__ __forceinline__ uint2 tile_du(const uint4 c) {  // (deltas, updates) of one tile
-    if (!WS) return make_uint2(c.w, c.y);
-    const u32 s = c.x + c.y + c.z + c.w;  // <= 1024 per half: no carry
-    return make_uint2(s & 0xFFFF, s >> 16);
-}
-
-template <int NT, bool WS>
+// tiles of its own group; the last block also writes the totals.  tile_cnt = inserts, updates,
+// deletes, deltas per tile.
+template <int NT>
 __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
                                                const u32* __restrict__ tile_cnt, const u64* __restrict__ gsum,
                                                u64 ntiles, int tile_items, uint2* __restrict__ out_delta,
@@ -1095,12 +528,12 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
     }
     const u64 t_lo = grp * C2_GROUP;
     if (!last && tid < (int)(t - t_lo)) {
-        const uint2 c = tile_du<WS>(*(const uint4*)(tile_cnt + 4 * (t_lo + tid)));
-        pd += c.x;
+        const uint4 c = *(const uint4*)(tile_cnt + 4 * (t_lo + tid));
+        pd += c.w;
         pu += c.y;
     }
     const uint4 ownc = *(const uint4*)(tile_cnt + 4 * t);
-    const uint2 own = tile_du<WS>(ownc);
+    const uint2 own = make_uint2(ownc.w, ownc.y);  // (deltas, updates) of this tile
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         pd += __shfl_xor(pd, o, 64); pu += __shfl_xor(pu, o, 64);
@@ -1126,24 +559,12 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
     }
     const uint2* sdp = stage_delta + t * (u64)tile_items;
     const uint2* sup = stage_upd + t * (u64)tile_items;
-    // record r of the tile -> its staging slot (WS: the wave slot holding it)
-    u32 d1 = 0, d2 = 0, d3 = 0, u1 = 0, u2 = 0, u3 = 0;
-    if (WS) {
-        d1 = ownc.x & 0xFFFF; d2 = d1 + (ownc.y & 0xFFFF); d3 = d2 + (ownc.z & 0xFFFF);
-        u1 = ownc.x >> 16; u2 = u1 + (ownc.y >> 16); u3 = u2 + (ownc.z >> 16);
-    }
-    auto slot = [&](u32 r, u32 p1, u32 p2, u32 p3) -> u32 {
-        if (!WS) return r;
-        const u32 w = (u32)(r >= p1) + (u32)(r >= p2) + (u32)(r >= p3);
-        const u32 base = w == 0 ? 0 : w == 1 ? p1 : w == 2 ? p2 : p3;
-        return w * RW + (r - base);
-    };
     constexpr int UC = C2_TILE / NT;
     uint2 v[UC];
 #pragma unroll
     for (int j = 0; j < UC; j++) {
         const u32 r = j * NT + tid;
-        if (r < own.x) v[j] = sdp[slot(r, d1, d2, d3)];
+        if (r < own.x) v[j] = sdp[r];
     }
 #pragma unroll
     for (int j = 0; j < UC; j++) {
@@ -1154,7 +575,7 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
 #pragma unroll
         for (int j = 0; j < UC; j++) {
             const u32 r = j * NT + tid;
-            if (r < own.y) v[j] = sup[slot(r, u1, u2, u3)];
+            if (r < own.y) v[j] = sup[r];
         }
 #pragma unroll
         for (int j = 0; j < UC; j++) {
@@ -1164,127 +585,11 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_join2p: persistent, register-prefetched tiles, decoupled look-back
-// ---------------------------------------------------------------------------------------------
-// (look-back descriptors and lookback(): kd_join.h)
-
-template <int NT, int IPT, bool LOOKBACK>
-__global__ __launch_bounds__(NT, KD_J2P_WAVES) void k_join2p(Join2Args g) {
-    using LD = Join2Lds<NT, IPT>;
-    static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
-    constexpr int R = LD::ROUNDS;
-    __shared__ u32x4 s_ch[LD::CH];
-    __shared__ u32 s_wave[3 * NT / 64];
-    __shared__ u64 s_excl[2];
-    const int tid = threadIdx.x;
-    const u64 ntiles = g.ntiles, stride = gridDim.x;
-    u64 t = blockIdx.x;
-    if (t >= ntiles) return;
-
-    // chunk k*NT + tid of the tile's LDS image -> its source address (per-range origin by selects)
-    u32x4 v[R];
-    auto issue = [&](const TileRanges& r) {
-        const u64 ob = r.kb.base - 16ull * r.c1, oa2 = r.oa.base - 16ull * r.c2, ob2 = r.ob.base - 16ull * r.c3;
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-            const u32 c = k * NT + tid;
-            const u64 org = c < r.c1 ? r.ka.base : c < r.c2 ? ob : c < r.c3 ? oa2 : ob2;
-            const u64 src = c < r.c4 ? org + 16ull * c : (u64)g.dummy;
-            v[k] = *(gp_x4)src;
-        }
-    };
-    auto land = [&](const TileRanges& r) {
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-            const u32 c = k * NT + tid;
-            if (c < r.c4) s_ch[c] = v[k];
-        }
-    };
-    TileGeo q = tile_geo(g, t, LD::TILE);
-    TileRanges r = tile_ranges(g, q);
-    issue(r);
-    land(r);
-    __syncthreads();
-    // split points of the tile after next: loaded one iteration early, consumed after a tile's work
-    typedef const __attribute__((address_space(1))) u64* gp64;
-    u64 pn0 = 0, pn1 = 0;
-    if (t + stride < ntiles) { pn0 = ((gp64)g.part)[t + stride]; pn1 = ((gp64)g.part)[t + stride + 1]; }
-    for (;;) {
-        // ---- prefetch the next tile into registers (in flight during this tile's work) ----
-        const u64 tn = t + stride;
-        TileGeo qn = q;
-        TileRanges rn = r;
-        if (tn < ntiles) {
-            qn = tile_geo_from(g, tn, LD::TILE, pn0, pn1);
-            rn = tile_ranges(g, qn);
-            issue(rn);
-            const u64 tnn = tn + stride;
-            if (tnn < ntiles) { pn0 = ((gp64)g.part)[tnn]; pn1 = ((gp64)g.part)[tnn + 1]; }
-        }
-        // ---- this tile, out of LDS ----
-        const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
-        const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
-        const u32* oA = (const u32*)((const u8*)(s_ch + r.c2) + r.oa.skew);
-        const u32* oB = (const u32*)((const u8*)(s_ch + r.c3) + r.ob.skew);
-        u32 rec[IPT];
-        bool bad = !q.ok;
-        tile_merge<NT, IPT>(sA, sB, oA, oB, q, rec, bad);
-        if (g.hash_mode) tile_names<IPT>(g, q, rec);
-        if (bad) atomicOr(g.err, 1u);
-        const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
-        if (LOOKBACK) {
-            // ---- global offsets: decoupled look-back (wave 0) ----
-            if (tid < 64) {
-                const u64 ex = lookback(g.desc, ntiles, t, ((u64)c.tnd << 31) | c.tnu, (u64)c.tdel);
-                if ((tid & 31) == 0) s_excl[tid >> 5] = ex;
-                const u64 ex1 = __shfl(ex, 32, 64);
-                if (t == ntiles - 1 && tid == 0) {  // the last tile knows the totals
-                    const u64 nd = (ex >> 31) + c.tnd, nu = (ex & 0x7FFFFFFFull) + c.tnu, nx = ex1 + c.tdel;
-                    g.counts[0] = nd - nu - nx;
-                    g.counts[1] = nu;
-                    g.counts[2] = nx;
-                    g.counts[3] = nd;
-                }
-            }
-            __syncthreads();
-            const u64 e0 = s_excl[0];
-            tile_write<IPT>(rec, c, q.i0, q.j0, g.out_delta + (e0 >> 31),
-                            g.out_upd ? g.out_upd + (e0 & 0x7FFFFFFFull) : nullptr);
-        } else {
-            // ---- tile-local staging slots + counts; k_place2 moves them to their final positions ----
-            tile_write<IPT>(rec, c, q.i0, q.j0, g.stage_delta + t * (u64)C2_STAGE, g.stage_upd + t * (u64)C2_STAGE);
-            if (tid == 0) {
-                u32* cc = g.tile_cnt + 4 * t;
-                const u32 tins = c.tnd - c.tnu - c.tdel;
-                cc[0] = tins;
-                cc[1] = c.tnu;
-                cc[2] = c.tdel;
-                cc[3] = c.tnd;
-                u64* gs = g.gsum + 2 * (t / C2_GROUP);
-                atomicAdd((unsigned long long*)gs, (unsigned long long)(c.tnd | (u64)c.tnu << 32));
-                atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)c.tdel << 32));
-            }
-        }
-        if (tn >= ntiles) break;
-        // ---- the prefetched tile -> LDS (after every wave is done with this one) ----
-        __syncthreads();
-        land(rn);
-        __syncthreads();
-        t = tn;
-        q = qn;
-        r = rn;
-    }
-}
-
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
                  u64* d_counts, u32* d_err) {
     const bool unord = (flags & KD_DIFF_UNORDERED) != 0;
-    const bool lookb = !unord && KD_C2_MODE == 2;  // persistent + decoupled look-back (profiling)
-    const bool staged = !unord && !lookb;         // tile-local staging + k_place2 (default)
     const u64 nA = A->n, nB = B->n, total = nA + nB;
     KD_CHECK(nA < 0xFFFFFFFFull && nB < 0xFFFFFFFFull, "diff2: side too large for uint32 indices");
-    KD_CHECK(!lookb || total < (1ull << 31), "diff2: look-back mode needs base.n + target.n < 2^31");
     const bool hash = A->key_mode == KD_KEY_HASH || B->key_mode == KD_KEY_HASH;
     KD_CHECK(A->key_mode == B->key_mode, "diff2: key modes differ");
     if (hash) KD_CHECK((nA == 0 || (A->name && A->name_off)) && (nB == 0 || (B->name && B->name_off)),
@@ -1295,22 +600,18 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
         return KD_OK;
     }
-    void *part, *tcnt = nullptr, *sdel = nullptr, *supd = nullptr, *gsum = nullptr, *desc = nullptr;
+    void *part, *tcnt = nullptr, *sdel = nullptr, *supd = nullptr, *gsum = nullptr;
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
     u64* zero = nullptr;
     u64 n_zero = 0;
-    if (staged) {
+    if (!unord) {
         n_zero = 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
         if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
         if ((rc = ensure(ctx, "c2.gsum", n_zero * sizeof(u64), &gsum))) return rc;
         if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_STAGE * sizeof(uint2), &sdel))) return rc;
         if ((rc = ensure(ctx, "c2.supd", ntiles * C2_STAGE * sizeof(uint2), &supd))) return rc;
         zero = (u64*)gsum;
-    } else if (lookb) {
-        n_zero = 2 * ntiles;
-        if ((rc = ensure(ctx, "c2.desc", n_zero * sizeof(u64), &desc))) return rc;
-        zero = (u64*)desc;
     }
     void* dz;
     if ((rc = device_zeros(ctx, &dz))) return rc;
@@ -1338,66 +639,24 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
     g.tile_cnt = (u32*)tcnt; g.gsum = (u64*)gsum; g.err = d_err;
     g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd; g.counts = d_counts;
-    g.desc = (u64*)desc;
     g.ntiles = ntiles;
-    if (unord) {
-        return launch(ctx, "k_join2", [&] {
+    rc = launch(ctx, "k_join2", [&] {
+        if (unord) {
             if (hash)
                 hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
             else
                 hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
-        });
-    }
-    const bool ws = KD_C2_MODE == 3;
-    if (KD_C2_MODE == 3) {  // run merge, persistent, per-wave slots
-        if (ctx->occ_join2r <= 0) {
-            int nb = 0;
-            KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_join2r<C2_NT, false>, C2_NT, 0));
-            ctx->occ_join2r = nb > 0 ? nb : 1;
+        } else if (hash) {
+            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+        } else {
+            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
         }
-        const u64 grid = std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)ctx->occ_join2r);
-        rc = launch(ctx, "k_join2", [&] {
-            if (hash)
-                hipLaunchKernelGGL((k_join2r<C2_NT, true>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
-            else
-                hipLaunchKernelGGL((k_join2r<C2_NT, false>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
-        });
-    } else if (KD_C2_MODE == 1) {  // one tile per workgroup, LDS-DMA staging
-        rc = launch(ctx, "k_join2", [&] {
-            if (hash)
-                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
-            else
-                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
-        });
-    } else {
-        // persistent: every workgroup resident at once (grid from the occupancy of this kernel)
-        const void* kern = lookb ? (const void*)k_join2p<C2_NT, C2_IPT, true> : (const void*)k_join2p<C2_NT, C2_IPT, false>;
-        if (ctx->occ_join2p <= 0) {
-            int nb = 0;
-            KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, C2_NT, 0));
-            ctx->occ_join2p = nb > 0 ? nb : 1;
-        }
-        const u64 grid = std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)ctx->occ_join2p);
-        rc = launch(ctx, "k_join2", [&] {
-            if (lookb)
-                hipLaunchKernelGGL((k_join2p<C2_NT, C2_IPT, true>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
-            else
-                hipLaunchKernelGGL((k_join2p<C2_NT, C2_IPT, false>), dim3((unsigned)grid), dim3(C2_NT), 0, ctx->stream, g);
-        });
-    }
-    if (rc || lookb) return rc;
-#if KD_J_CLOCK
-    if (ws) hipLaunchKernelGGL(k_jclk_report, dim3(1), dim3(256), 0, ctx->stream, (const uint2*)sdel, ntiles);
-#endif
+    });
+    if (rc || unord) return rc;
     return launch(ctx, "k_place2", [&] {
-        if (ws)
-            hipLaunchKernelGGL((k_place2<KD_PLACE_NT, true>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
-                               (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles,
-                               (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, d_counts);
-        else
-            hipLaunchKernelGGL((k_place2<KD_PLACE_NT, false>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
-                               (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles,
-                               (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, d_counts);
+        hipLaunchKernelGGL((k_place2<KD_PLACE_NT>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
+                           (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles,
+                           (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, d_counts);
     });
 }
 

@@ -5,29 +5,43 @@
 // sides, Schema.feature_from_raw_dict (schema.py:288-293) and the field loop of
 // TextDiffWriter.write_feature_delta (kart/text_diff_writer.py:135-145):
 //     changed(k) = old.get(k, _NULL) != new.get(k, _NULL)   for k in old keys ∪ new-only keys.
-// The host turns both schemas + every legend into per-legend maps (kartdiff.h kd_legend_maps);
-// here one lane walks one update's two blobs.  Value semantics follow msgpack.unpackb(raw=False)
-// with the ext hook of kart/serialise_util.py:26-31 and Python's ==:
-// ints of any width by value, bool == int, exact int/float compare, IEEE float ==, str/bytes by
-// payload, bin == ext 'G' payload, None only == None, empty ext 'G' -> None.
+// The host turns both schemas + every legend into per-legend maps (kartdiff.h kd_legend_maps).
+// Value semantics follow msgpack.unpackb(raw=False) with the ext hook of
+// kart/serialise_util.py:26-31 and Python's ==: ints of any width by value,
+// bool == int, exact int/float compare, IEEE float ==, str/bytes by payload, bin == ext 'G'
+// payload, None only == None, empty ext 'G' -> None.
 //
-// Fast path: when the old and new legend maps are identical (the common case: no schema change)
-// both blobs are walked in lockstep with no per-value storage.  Otherwise value offsets go to a
-// small per-lane array and keys are resolved through the maps.
+// k_fielddiff (one wave per workgroup, UPR updates per round, one lane per update):
+//   1. LDS windows.  Per blob only a head window (NH 16-B chunks from the blob's aligned start) and a
+//      tail window (the NTL-1 aligned chunks ending with the blob's last byte + one pad chunk) are
+//      copied to LDS by LDS-DMA — the msgpack headers, the legend, and the short values that follow
+//      a long one.  Long payloads (geometries) never enter LDS, so ~10 KiB per 32 updates keeps
+//      ~10 waves per CU resident.
+//   2. Parse: each lane walks its two blobs value by value from the windows (table-driven header
+//      decode from a 12-byte window; bytes outside both windows come from global memory), compares
+//      scalars and short payloads in registers or LDS, and queues every byte payload it cannot see
+//      whole in LDS as a compare task (old address, new address, length, lane, key).
+//   3. Tasks: the wave compares the queued payloads cooperatively, 16 lanes x 16 B per step straight
+//      from HBM (coalesced; the new side realigned to the old side's byte offset with a funnel
+//      shift), and ORs the changed keys into the owners' masks in LDS.
+// Payloads of unequal length are "changed" without reading them.  Tables too large for LDS take
+// k_fielddiff_g (one lane per update, everything from global memory).
+#include <type_traits>
+
 #include "kd_internal.h"
 
 namespace kd {
 
-// Blob bytes are read through address-space-qualified pointers: LDS-staged blobs as
-// address_space(3) (ds_read, word-wide compares), blobs too large for a slot as address_space(1)
-// (global loads).  A generic pointer would turn every byte access into a flat load.
-typedef const __attribute__((address_space(3))) u8* lp8;
 typedef const __attribute__((address_space(3))) u32* lp32;
-typedef const __attribute__((address_space(3))) u32x4* lp128;
 typedef const __attribute__((address_space(1))) u8* gp8;
+typedef const __attribute__((address_space(1))) u32* gp32;
+typedef const __attribute__((address_space(1))) u32x4* gp128;
 
 enum : u8 { V_NIL = 0, V_INT = 1, V_FLOAT = 2, V_STR = 3, V_BYTES = 4, V_EXT = 5 };
 
+// ================================================================================================
+// generic decoder (global-memory pointers): the large-table fallback kernel k_fielddiff_g
+// ================================================================================================
 template <class P>
 struct DVal {
     u8 cls;
@@ -130,81 +144,6 @@ __device__ __forceinline__ u32 dv_decode(P p, u32 avail, DVal<P>& v) {
     }
 }
 
-// ---- LDS-staged blobs: branch-free header decode -------------------------------------------------
-// Every msgpack type byte maps to one table entry (built at compile time, copied to LDS per block):
-//   bits 0-2 class (7 = not a field value), 3-5 header bytes, 6-10 fixed payload bytes (numbers: their
-//   width), 11-13 width of a big-endian length field, 14-17 number width (0 = immediate), 18 signed,
-//   19 float32, 24-31 immediate value.
-// A value is then decoded from one 12-byte window read (two ds_read2_b32 + v_alignbyte) with selects
-// and shifts instead of a divergent switch: lanes holding different types (fixint vs uint16, fixstr vs
-// str8) stay converged.
-struct MpTab {
-    u32 e[256];
-    static constexpr u32 mk(u32 cls, u32 hdr, u32 plen, u32 lenw, u32 numw, u32 sgn, u32 f32, u32 imm) {
-        return cls | hdr << 3 | plen << 6 | lenw << 11 | numw << 14 | sgn << 18 | f32 << 19 | imm << 24;
-    }
-    constexpr MpTab() : e() {
-        for (u32 t = 0; t < 256; t++) {
-            u32 v = mk(7, 1, 0, 0, 0, 0, 0, 0);
-            if (t <= 0x7f) v = mk(V_INT, 1, 0, 0, 0, 0, 0, t);
-            else if (t >= 0xe0) v = mk(V_INT, 1, 0, 0, 0, 1, 0, t);
-            else if (t >= 0xa0 && t <= 0xbf) v = mk(V_STR, 1, t & 31, 0, 0, 0, 0, 0);
-            else if (t == 0xc0) v = mk(V_NIL, 1, 0, 0, 0, 0, 0, 0);
-            else if (t == 0xc2 || t == 0xc3) v = mk(V_INT, 1, 0, 0, 0, 0, 0, t & 1);
-            else if (t >= 0xc4 && t <= 0xc6) { u32 w = 1u << (t - 0xc4); v = mk(V_BYTES, 1 + w, 0, w, 0, 0, 0, 0); }
-            else if (t >= 0xc7 && t <= 0xc9) { u32 w = 1u << (t - 0xc7); v = mk(V_EXT, 2 + w, 0, w, 0, 0, 0, 0); }
-            else if (t == 0xca) v = mk(V_FLOAT, 1, 4, 0, 4, 0, 1, 0);
-            else if (t == 0xcb) v = mk(V_FLOAT, 1, 8, 0, 8, 0, 0, 0);
-            else if (t >= 0xcc && t <= 0xcf) { u32 w = 1u << (t - 0xcc); v = mk(V_INT, 1, w, 0, w, 0, 0, 0); }
-            else if (t >= 0xd0 && t <= 0xd3) { u32 w = 1u << (t - 0xd0); v = mk(V_INT, 1, w, 0, w, 1, 0, 0); }
-            else if (t >= 0xd4 && t <= 0xd8) v = mk(V_EXT, 2, 1u << (t - 0xd4), 0, 0, 0, 0, 0);
-            else if (t >= 0xd9 && t <= 0xdb) { u32 w = 1u << (t - 0xd9); v = mk(V_STR, 1 + w, 0, w, 0, 0, 0, 0); }
-            e[t] = v;
-        }
-    }
-};
-__shared__ u32 s_mp[256];
-
-__device__ __forceinline__ void mp_tab_to_lds() {
-    constexpr MpTab T{};
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_mp[i] = T.e[i];
-}
-
-template <>
-__device__ __forceinline__ u32 dv_decode<lp8>(lp8 p, u32 avail, DVal<lp8>& v) {
-    const u32 s = (u32)(size_t)p & 3;
-    const lp32 a = (lp32)(p - s);
-    const u32 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
-    const u32 x0 = __builtin_amdgcn_alignbyte(a1, a0, s), x1 = __builtin_amdgcn_alignbyte(a2, a1, s),
-              x2 = __builtin_amdgcn_alignbyte(a3, a2, s);
-    const u64 lo = (u64)x0 | (u64)x1 << 32;
-    const u32 t = x0 & 0xff;
-    const u32 e = s_mp[t];
-    u32 cls = e & 7;
-    const u32 hdr = (e >> 3) & 7, plen = (e >> 6) & 31, lenw = (e >> 11) & 7, numw = (e >> 14) & 15;
-    const u64 be = __builtin_bswap64((lo >> 8) | (u64)x2 << 56);  // bytes 1..8, big-endian
-    const u64 lenv = lenw ? be >> (64 - 8 * lenw) : plen;
-    u64 nv = numw ? be >> (64 - 8 * numw) : (u64)(e >> 24);
-    const u32 sh = 64 - 8 * (numw ? numw : 1);
-    if ((e >> 18) & 1) nv = (u64)((i64)(nv << sh) >> sh);
-    if ((e >> 19) & 1) nv = (u64)__double_as_longlong((double)__uint_as_float((u32)nv));
-    v.bits = nv;
-    v.big = (cls == V_INT && !((e >> 18) & 1) && numw == 8 && (nv >> 63)) ? 1 : 0;
-    const u32 et = (u32)(lo >> (8 * (hdr - 1))) & 0xff;  // ext type byte (hdr <= 6)
-    v.ext = (i8)et;
-    const u64 used = hdr + lenv;
-    bool ok = cls != 7 && used <= avail;
-    if (cls == V_EXT && et == 'G') {  // Geometry: b"" -> None; else must start "GP" (Geometry())
-        const u32 g0 = (u32)(lo >> (8 * hdr)) & 0xff, g1 = (u32)(lo >> (8 * hdr + 8)) & 0xff;
-        ok = ok && (lenv == 0 || (lenv >= 2 && g0 == 'G' && g1 == 'P'));
-        cls = lenv == 0 ? V_NIL : V_BYTES;
-    }
-    v.cls = (u8)cls;
-    v.p = p + hdr;
-    v.len = (u32)lenv;
-    return ok ? (u32)used : 0;
-}
-
 __device__ __forceinline__ bool int_eq_float(u8 big, u64 bits, double d) {
     if (!(d == d)) return false;
     if (floor(d) != d) return false;
@@ -224,83 +163,6 @@ __device__ bool bytes_eq(P a, P b, u32 n) {
     return true;
 }
 
-// LDS: four bytes at a time from aligned words, realigned with v_alignbyte; the aligned reads
-// may run up to 4 bytes past either range (still inside the workgroup's LDS allocation, or
-// returning 0 past its end) and those bytes are masked off.
-__device__ __forceinline__ u32 lds_word(lp32 w, u32 k, u32 s) {
-    return __builtin_amdgcn_alignbyte(w[k + 1], w[k], s);
-}
-
-#ifndef KD_FD_EXP
-#define KD_FD_EXP 0  // profiling builds only: 1 = no parse, 2 = no LDS byte-payload compare
-#endif
-#ifndef KD_FD_B128
-#define KD_FD_B128 0  // 1: 32-B blocks from three 16-B LDS reads per side (measured 2x slower on C3)
-#endif
-// the 8 dwords starting at byte s (0..15) of a 48-B aligned window: dword shift by selects, byte
-// shift by v_alignbyte
-__device__ __forceinline__ void window8(const u32x4 w0, const u32x4 w1, const u32x4 w2, u32 s, u32 out[8]) {
-    const u32 x[12] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w};
-    const u32 d = s >> 2, sb = s & 3;
-    u32 t1[11], t2[9];
-#pragma unroll
-    for (int i = 0; i < 11; i++) t1[i] = (d & 1) ? x[i + 1] : x[i];
-#pragma unroll
-    for (int i = 0; i < 9; i++) t2[i] = (d & 2) ? t1[i + 2] : t1[i];
-#pragma unroll
-    for (int i = 0; i < 8; i++) out[i] = __builtin_amdgcn_alignbyte(t2[i + 1], t2[i], sb);
-}
-
-template <>
-__device__ bool bytes_eq<lp8>(lp8 a, lp8 b, u32 n) {
-#if KD_FD_EXP == 2
-    return a[0] == b[0] || n > 0;
-#endif
-#if KD_FD_B128
-    // 32-byte blocks, each side's 48-B aligned window read as three ds_read_b128 (a third of the
-    // LDS instructions of dword reads); reads past the pool return 0 or stay in the allocation
-    const u32 sa = (u32)(size_t)a & 15, sb = (u32)(size_t)b & 15;
-    lp128 wa = (lp128)(a - sa), wb = (lp128)(b - sb);
-    u32 rem = n, diff = 0;
-    while (rem > 0 && diff == 0) {
-        const u32x4 a0 = wa[0], a1 = wa[1], a2 = wa[2], b0 = wb[0], b1 = wb[1], b2 = wb[2];
-        u32 xa[8], xb[8];
-        window8(a0, a1, a2, sa, xa);
-        window8(b0, b1, b2, sb, xb);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const u32 valid = rem >= 4u * j + 4 ? 0xFFFFFFFFu : rem > 4u * j ? (1u << (8 * (rem - 4 * j))) - 1 : 0u;
-            diff |= (xa[j] ^ xb[j]) & valid;
-        }
-        wa += 2;
-        wb += 2;
-        rem = rem > 32 ? rem - 32 : 0;
-    }
-    return diff == 0;
-#else
-    // 32-byte blocks: the 9 aligned words of each side are read together (one LDS round trip per
-    // block, no per-word early exit), realigned with v_alignbyte and compared; bytes past n masked
-    const u32 sa = (u32)(size_t)a & 3, sb = (u32)(size_t)b & 3;
-    lp32 wa = (lp32)(a - sa), wb = (lp32)(b - sb);
-    u32 rem = n, diff = 0;
-    while (rem > 0 && diff == 0) {
-        u32 xa[9], xb[9];
-#pragma unroll
-        for (int j = 0; j < 9; j++) { xa[j] = wa[j]; xb[j] = wb[j]; }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const u32 d = __builtin_amdgcn_alignbyte(xa[j + 1], xa[j], sa) ^ __builtin_amdgcn_alignbyte(xb[j + 1], xb[j], sb);
-            const u32 valid = rem >= 4u * j + 4 ? 0xFFFFFFFFu : rem > 4u * j ? (1u << (8 * (rem - 4 * j))) - 1 : 0u;
-            diff |= d & valid;
-        }
-        wa += 8;
-        wb += 8;
-        rem = rem > 32 ? rem - 32 : 0;
-    }
-    return diff == 0;
-#endif
-}
-
 template <class P>
 __device__ __forceinline__ bool py_eq(const DVal<P>& a, const DVal<P>& b) {
     if (a.cls == V_NIL || b.cls == V_NIL) return a.cls == b.cls;
@@ -313,41 +175,14 @@ __device__ __forceinline__ bool py_eq(const DVal<P>& a, const DVal<P>& b) {
     return a.len == b.len && bytes_eq(a.p, b.p, a.len);
 }
 
-// LDS values: Python == with the scalar cases as selects; only a same-class, same-length byte
-// payload pair reaches the (LDS) byte compare.  The branchy generic form cost most of the parse.
-__device__ __forceinline__ bool int_eq_float_sel(u8 big, u64 bits, double d) {
-    const bool whole = d == d && floor(d) == d;
-    const bool in_big = d >= 9223372036854775808.0 && d < 18446744073709551616.0;
-    const bool in_small = d >= -9223372036854775808.0 && d < 9223372036854775808.0;
-    const double dc_b = in_big ? d : 9223372036854775808.0, dc_s = in_small ? d : 0.0;
-    const bool eq_b = in_big && (u64)dc_b == bits, eq_s = in_small && (i64)dc_s == (i64)bits;
-    return whole && (big ? eq_b : eq_s);
-}
-
-template <>
-__device__ __forceinline__ bool py_eq<lp8>(const DVal<lp8>& a, const DVal<lp8>& b) {
-    const bool an = a.cls == V_NIL, bn = b.cls == V_NIL;
-    const bool ai = a.cls == V_INT, bi = b.cls == V_INT, af = a.cls == V_FLOAT, bf = b.cls == V_FLOAT;
-    const double da = __longlong_as_double((i64)a.bits), db = __longlong_as_double((i64)b.bits);
-    const bool ii = ai && bi, ff = af && bf, mixed = (ai && bf) || (af && bi);
-    const bool r_ii = a.big == b.big && a.bits == b.bits;
-    const bool r_ff = da == db;
-    const bool r_mx = int_eq_float_sel(ai ? a.big : b.big, ai ? a.bits : b.bits, ai ? db : da);
-    const bool num = (ai || af) && (bi || bf);
-    const bool r_num = ii ? r_ii : ff ? r_ff : mixed && r_mx;
-    const bool byt = !an && !bn && !(ai || af) && a.cls == b.cls && (a.cls != V_EXT || a.ext == b.ext) && a.len == b.len;
-    bool eqb = false;
-    if (byt) eqb = bytes_eq(a.p, b.p, a.len);
-    return (an || bn) ? (an && bn) : num ? r_num : eqb;
-}
-
 // header: 0x92, str(40) legend hex, array header -> returns 0 ok
 template <class P>
-__device__ __forceinline__ int parse_header(P b, u32 n, u32* nvals, u32* off) {
+__device__ __forceinline__ int parse_header(P b, u32 n, u32* nvals, u32* off, u32* lp) {
     if (n < 3 || b[0] != 0x92) return 1;
     DVal<P> lv;
     u32 c = dv_decode(b + 1, n - 1, lv);
     if (!c || lv.cls != V_STR || lv.len != 40) return 1;
+    *lp = 1 + c - 40;
     u32 o = 1 + c;
     if (o >= n) return 1;
     u8 t = b[o];
@@ -359,7 +194,9 @@ __device__ __forceinline__ int parse_header(P b, u32 n, u32* nvals, u32* off) {
     return 0;
 }
 
+// ================================================================================================
 // device-side tables (built by the host per call)
+// ================================================================================================
 // AS = -1: generic pointers into the device copy; AS = 3: the block's LDS copy (small tables)
 template <int AS, class T>
 struct ASP { typedef const __attribute__((address_space(AS))) T* type; };
@@ -388,21 +225,9 @@ __device__ __forceinline__ void hex_words(P p, u32 w[10]) {
     for (int i = 0; i < 10; i++)
         w[i] = (u32)p[4 * i] | (u32)p[4 * i + 1] << 8 | (u32)p[4 * i + 2] << 16 | (u32)p[4 * i + 3] << 24;
 }
-template <>
-__device__ __forceinline__ void hex_words<lp8>(lp8 p, u32 w[10]) {
-    const u32 s = (u32)(size_t)p & 3;
-    const lp32 a = (lp32)(p - s);
-    u32 x[11];
-#pragma unroll
-    for (int i = 0; i < 11; i++) x[i] = a[i];  // one LDS round trip
-#pragma unroll
-    for (int i = 0; i < 10; i++) w[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], s);
-}
 
-template <class P, class TP>
-__device__ __forceinline__ int find_legend(TP tab, int n, P hex) {
-    u32 h[10];
-    hex_words(hex, h);
+template <class TP>
+__device__ __forceinline__ int find_legend_w(TP tab, int n, const u32 h[10]) {
     for (int l = 0; l < n; l++) {
         u32 x = 0;
 #pragma unroll
@@ -412,8 +237,15 @@ __device__ __forceinline__ int find_legend(TP tab, int n, P hex) {
     return -1;
 }
 
+template <class P, class TP>
+__device__ __forceinline__ int find_legend(TP tab, int n, P hex) {
+    u32 h[10];
+    hex_words(hex, h);
+    return find_legend_w(tab, n, h);
+}
+
 constexpr u32 FD_MAXV = 4096;  // oracle limit (status 3 above it)
-constexpr int FD_NT = 64;      // one wave per block: each lane owns one update and two LDS slots
+constexpr int FD_NT = 64;      // one wave per block
 
 __device__ __forceinline__ void set_bit(u64 mk[4], u64* m, int k) {
     const u64 bit = 1ull << (k & 63);
@@ -423,6 +255,17 @@ __device__ __forceinline__ void set_bit(u64 mk[4], u64* m, int k) {
     mk[2] |= w == 2 ? bit : 0;
     mk[3] |= w == 3 ? bit : 0;
     if (w >= 4) m[w] |= bit;
+}
+
+// the update's mask words: the first four from registers (constant indices: mk stays in VGPRs), the
+// rest were ORed in place and are cleared when the update failed
+__device__ __forceinline__ void store_masks(u64* m, int words, const u64 mk[4], u8 st) {
+    m[0] = mk[0];
+    if (words > 1) m[1] = mk[1];
+    if (words > 2) m[2] = mk[2];
+    if (words > 3) m[3] = mk[3];
+    if (st)
+        for (int w = 4; w < words; w++) m[w] = 0;
 }
 
 // Value `want` of a blob, walking forward from a cursor (idx, pos); a backward request restarts
@@ -439,65 +282,32 @@ __device__ __forceinline__ bool seek_value(P b, u32 n, u32 first, u32 want, u32&
     }
 }
 
-// one update: returns the status; mask bits (k < 256) in mk, the rest straight into m
-#ifndef KD_FD_CLOCK
-#define KD_FD_CLOCK 0  // profiling builds only: per-phase clock64 printf of sampled waves
-#endif
-#if KD_FD_CLOCK
-__device__ u64 g_fd_dbg[4 * 8192 * 64];
-#define FD_DBG(i) g_fd_dbg[4 * ((blockIdx.x % 8192) * 64 + threadIdx.x) + (i)]
-#endif
+// one update from global memory (k_fielddiff_g): returns the status; mask bits (k < 256) in mk,
+// the rest straight into m
 template <class P, class TB>
 __device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const TB& tb, u64 mk[4], u64* m) {
-#if KD_FD_CLOCK
-    const u64 D0 = clock64();
-    u64 tdec = 0, teq = 0;
-#endif
-    u32 cvo, cvn, po, pn;
-    if (parse_header(ob, on, &cvo, &po) || parse_header(nb, nn, &cvn, &pn)) return 1;
-    const int li_o = find_legend(tb.leg_o, tb.n_lo, ob + 3);
-    const int li_n = find_legend(tb.leg_n, tb.n_ln, nb + 3);
+    u32 cvo, cvn, po, pn, lpo, lpn;
+    if (parse_header(ob, on, &cvo, &po, &lpo) || parse_header(nb, nn, &cvn, &pn, &lpn)) return 1;
+    const int li_o = find_legend(tb.leg_o, tb.n_lo, ob + lpo);
+    const int li_n = find_legend(tb.leg_n, tb.n_ln, nb + lpn);
     if (li_o < 0 || li_n < 0) return 2;
     if (cvo > FD_MAXV || cvn > FD_MAXV) return 3;
     const bool al = tb.aligned[li_o * tb.n_ln + li_n];
     if (al && cvo == cvn) {
-        // ---- lockstep: value v of both blobs belongs to the same union key ----
         const auto kov = tb.key_of_val + (u64)li_o * tb.maxv;
         u32 pa = po, pb = pn;
-#if KD_FD_CLOCK
-        FD_DBG(0) = clock64() - D0;
-#endif
         for (u32 v = 0; v < cvo; v++) {
             DVal<P> a, b;
-#if KD_FD_CLOCK
-            u64 E0 = clock64();
-#endif
             const u32 ca = dv_decode(ob + pa, on - pa, a), cb = dv_decode(nb + pb, nn - pb, b);
             if (!ca || !cb) return 4;
             pa += ca;
             pb += cb;
             const int k = v < (u32)tb.maxv ? kov[v] : -1;
-#if KD_FD_CLOCK
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            u64 E1 = clock64();
-            tdec += E1 - E0;
-#endif
             if (k >= 0 && !py_eq(a, b)) set_bit(mk, m, k);
-#if KD_FD_CLOCK
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            teq += clock64() - E1;
-#endif
         }
-#if KD_FD_CLOCK
-        FD_DBG(1) = tdec;
-        FD_DBG(2) = teq;
-        FD_DBG(3) = cvo;
-#endif
         if (pa != on || pb != nn) return 4;  // trailing bytes: unpackb raises ExtraData
         return 0;
     }
-    // ---- general: validate both blobs (msgpack.unpackb decodes everything first), then
-    //      resolve each union key through both maps ----
     u32 p = po;
     for (u32 v = 0; v < cvo; v++) { DVal<P> x; u32 c = dv_decode(ob + p, on - p, x); if (!c) return 4; p += c; }
     if (p != on) return 4;
@@ -530,42 +340,462 @@ __device__ __forceinline__ u8 diff_one(P ob, u32 on, P nb, u32 nn, const TB& tb,
     return 0;
 }
 
-constexpr u32 FD_TAB_LDS_MAX = 16384;  // tables up to this size are copied into each block's LDS
+// ================================================================================================
+// windowed decoder (k_fielddiff)
+// ================================================================================================
+// Every msgpack type byte maps to one table entry (built at compile time, copied to LDS per block):
+//   bits 0-2 class (7 = not a field value), 3-5 header bytes, 6-10 fixed payload bytes (numbers: their
+//   width), 11-13 width of a big-endian length field, 14-17 number width (0 = immediate), 18 signed,
+//   19 float32, 24-31 immediate value.
+// A value is decoded from one 12-byte window (three words) with selects and shifts instead of a
+// divergent switch: lanes holding different types (fixint vs uint16, fixstr vs str8) stay converged.
+struct MpTab {
+    u32 e[256];
+    static constexpr u32 mk(u32 cls, u32 hdr, u32 plen, u32 lenw, u32 numw, u32 sgn, u32 f32, u32 imm) {
+        return cls | hdr << 3 | plen << 6 | lenw << 11 | numw << 14 | sgn << 18 | f32 << 19 | imm << 24;
+    }
+    constexpr MpTab() : e() {
+        for (u32 t = 0; t < 256; t++) {
+            u32 v = mk(7, 1, 0, 0, 0, 0, 0, 0);
+            if (t <= 0x7f) v = mk(V_INT, 1, 0, 0, 0, 0, 0, t);
+            else if (t >= 0xe0) v = mk(V_INT, 1, 0, 0, 0, 1, 0, t);
+            else if (t >= 0xa0 && t <= 0xbf) v = mk(V_STR, 1, t & 31, 0, 0, 0, 0, 0);
+            else if (t == 0xc0) v = mk(V_NIL, 1, 0, 0, 0, 0, 0, 0);
+            else if (t == 0xc2 || t == 0xc3) v = mk(V_INT, 1, 0, 0, 0, 0, 0, t & 1);
+            else if (t >= 0xc4 && t <= 0xc6) { u32 w = 1u << (t - 0xc4); v = mk(V_BYTES, 1 + w, 0, w, 0, 0, 0, 0); }
+            else if (t >= 0xc7 && t <= 0xc9) { u32 w = 1u << (t - 0xc7); v = mk(V_EXT, 2 + w, 0, w, 0, 0, 0, 0); }
+            else if (t == 0xca) v = mk(V_FLOAT, 1, 4, 0, 4, 0, 1, 0);
+            else if (t == 0xcb) v = mk(V_FLOAT, 1, 8, 0, 8, 0, 0, 0);
+            else if (t >= 0xcc && t <= 0xcf) { u32 w = 1u << (t - 0xcc); v = mk(V_INT, 1, w, 0, w, 0, 0, 0); }
+            else if (t >= 0xd0 && t <= 0xd3) { u32 w = 1u << (t - 0xd0); v = mk(V_INT, 1, w, 0, w, 1, 0, 0); }
+            else if (t >= 0xd4 && t <= 0xd8) v = mk(V_EXT, 2, 1u << (t - 0xd4), 0, 0, 0, 0, 0);
+            else if (t >= 0xd9 && t <= 0xdb) { u32 w = 1u << (t - 0xd9); v = mk(V_STR, 1 + w, 0, w, 0, 0, 0, 0); }
+            e[t] = v;
+        }
+    }
+};
+__shared__ u32 s_mp[256];
 
-// One wave per block, one update per lane.  Per round of 64 updates:
-//   1. pair + blob offsets (coalesced pair loads; offset loads per lane);
-//   2. cooperative staging: the 64 updates' 2x64 blobs are cut into 16-B chunks and dealt to the lanes
-//      so that one wave-instruction reads consecutive chunks of a few blobs (a handful of cache lines)
-//      instead of 64 scattered lines — per-lane staging of its own blobs made every load instruction
-//      touch 64 lines and the staging dominated the kernel;
-//   3. each lane walks its two blobs from LDS (table-driven decoder, tables in LDS).
+__device__ __forceinline__ void mp_tab_to_lds() {
+    constexpr MpTab T{};
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_mp[i] = T.e[i];
+}
+
+// One blob of one lane: its bytes in HBM, and the LDS image of its head and tail windows.
+//   head: chunks [hb, hb + 16 NH)                      (hb = start rounded down to 16)
+//   tail: chunks [tb, tb + 16 NTL), tb = last chunk - 16 (NTL - 2): NTL-1 chunks ending with the
+//         chunk holding the last byte, then one pad chunk, so a window read at any valid position
+//         fits.
+// Chunks holding no byte of the blob are loaded from device zeros instead (never a possibly
+// unmapped address), so window bytes past the blob are zero; every decode bounds-checks anyway.
+template <int NH, int NTL>
+struct WBlob {
+    u64 start;  // device address of byte 0
+    u32 len;
+    u32 s0;     // start - hb (0..15): blob position p is at offset x = p + s0 from hb
+    int t0;     // tb - hb (negative for blobs shorter than the tail window)
+    u32 img;    // LDS byte address of the image (head chunks, then tail chunks)
+    // image offset of the bytes at hb offsets [x, x + n) when they lie in one window, else ~0u
+    __device__ __forceinline__ u32 win(u32 x, u32 n) const {
+        if (x + n <= 16 * NH) return x;
+        const int y = (int)x - t0;
+        if (y >= 0 && (u32)y + n <= 16 * NTL) return 16 * NH + (u32)y;
+        return ~0u;
+    }
+};
+
+__device__ __forceinline__ u32 lds_u32(u32 addr) { return *(lp32)(size_t)addr; }
+
+// bytes [p, p + 12) of a blob as three little-endian words (bytes past the blob: zero or garbage;
+// callers bound every access by the blob length)
+template <class BL>
+__device__ __forceinline__ void rd12(const BL& b, u32 p, u32& x0, u32& x1, u32& x2) {
+    const u32 x = p + b.s0, x4 = x & ~3u, s = x & 3;
+    u32 w0, w1, w2, w3;
+    const u32 o = b.win(x4, 16);
+    if (o != ~0u) {
+        const u32 q = b.img + o;
+        w0 = lds_u32(q); w1 = lds_u32(q + 4); w2 = lds_u32(q + 8); w3 = lds_u32(q + 12);
+    } else {  // outside both windows: aligned dwords holding a blob byte, from global memory
+        const u32 end = b.len + b.s0;
+        const gp32 g = (gp32)(b.start - b.s0 + x4);
+        w0 = x4 < end ? g[0] : 0;
+        w1 = x4 + 4 < end ? g[1] : 0;
+        w2 = x4 + 8 < end ? g[2] : 0;
+        w3 = x4 + 12 < end ? g[3] : 0;
+    }
+    x0 = __builtin_amdgcn_alignbyte(w1, w0, s);
+    x1 = __builtin_amdgcn_alignbyte(w2, w1, s);
+    x2 = __builtin_amdgcn_alignbyte(w3, w2, s);
+}
+
+// the 40 legend hex bytes at blob position lp as 10 words
+template <class BL>
+__device__ __forceinline__ void rd_legend(const BL& b, u32 lp, u32 h[10]) {
+    const u32 x = lp + b.s0, x4 = x & ~3u, s = x & 3;
+    u32 w[11];
+    const u32 o = b.win(x4, 44);
+    if (o != ~0u) {
+#pragma unroll
+        for (int i = 0; i < 11; i++) w[i] = lds_u32(b.img + o + 4 * i);
+    } else {
+        const u32 end = b.len + b.s0;
+        const gp32 g = (gp32)(b.start - b.s0 + x4);
+#pragma unroll
+        for (int i = 0; i < 11; i++) w[i] = x4 + 4 * i < end ? g[i] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; i++) h[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], s);
+}
+
+// a decoded value: class, header size and length, and either the number's bits or (byte classes)
+// the first 12 payload bytes as they sit in the decode window (short payloads compare from here)
+struct WVal {
+    u32 meta;  // cls | big << 3 | hdr << 4 | ext << 8
+    u32 len;
+    u64 bits;  // numbers: int64 (uint64 if big) / double bits; byte classes: payload bytes 0..7
+    u32 hi;    // byte classes: payload bytes 8..11
+    __device__ __forceinline__ u32 cls() const { return meta & 7; }
+    __device__ __forceinline__ u32 big() const { return (meta >> 3) & 1; }
+    __device__ __forceinline__ u32 hdr() const { return (meta >> 4) & 15; }
+    __device__ __forceinline__ u32 ext() const { return meta >> 8; }
+};
+
+__device__ __forceinline__ u32 decode_w(u32 x0, u32 x1, u32 x2, u32 avail, WVal& v) {
+    const u64 lo = (u64)x0 | (u64)x1 << 32;
+    const u32 t = x0 & 0xff;
+    const u32 e = s_mp[t];
+    u32 cls = e & 7;
+    const u32 hdr = (e >> 3) & 7, plen = (e >> 6) & 31, lenw = (e >> 11) & 7, numw = (e >> 14) & 15;
+    const u64 be = __builtin_bswap64((lo >> 8) | (u64)x2 << 56);  // bytes 1..8, big-endian
+    const u64 lenv = lenw ? be >> (64 - 8 * lenw) : plen;
+    u64 nv = numw ? be >> (64 - 8 * numw) : (u64)(e >> 24);
+    const u32 sh = 64 - 8 * (numw ? numw : 1);
+    if ((e >> 18) & 1) nv = (u64)((i64)(nv << sh) >> sh);
+    if ((e >> 19) & 1) nv = (u64)__double_as_longlong((double)__uint_as_float((u32)nv));
+    const u32 big = (cls == V_INT && !((e >> 18) & 1) && numw == 8 && (nv >> 63)) ? 1 : 0;
+    const u32 et = (u32)(lo >> (8 * (hdr - 1))) & 0xff;  // ext type byte (hdr <= 6)
+    const u64 used = hdr + lenv;
+    bool ok = cls != 7 && used <= avail;
+    if (cls == V_EXT && et == 'G') {  // Geometry: b"" -> None; else must start "GP" (Geometry())
+        const u32 g0 = (u32)(lo >> (8 * hdr)) & 0xff, g1 = (u32)(lo >> (8 * hdr + 8)) & 0xff;
+        ok = ok && (lenv == 0 || (lenv >= 2 && g0 == 'G' && g1 == 'P'));
+        cls = lenv == 0 ? V_NIL : V_BYTES;
+    }
+    const bool num = cls == V_INT || cls == V_FLOAT;
+    const unsigned __int128 w = ((unsigned __int128)lo | ((unsigned __int128)x2 << 64)) >> (8 * hdr);
+    v.meta = cls | big << 3 | hdr << 4 | et << 8;
+    v.len = (u32)lenv;
+    v.bits = num ? nv : (u64)w;
+    v.hi = (u32)(w >> 64);
+    return ok ? (u32)used : 0;
+}
+
+// Python == of two decoded values without their payload bytes: 0 equal, 1 changed, 2 the byte
+// payloads (same class, same ext code, same length >= 1) decide
+__device__ __forceinline__ u32 scalar_eq(const WVal& a, const WVal& b) {
+    const u32 ac = a.cls(), bc = b.cls();
+    const bool an = ac == V_NIL, bn = bc == V_NIL;
+    const bool ai = ac == V_INT, bi = bc == V_INT, af = ac == V_FLOAT, bf = bc == V_FLOAT;
+    const double da = __longlong_as_double((i64)a.bits), db = __longlong_as_double((i64)b.bits);
+    const bool ii = ai && bi, ff = af && bf, mixed = (ai && bf) || (af && bi);
+    const bool r_ii = a.big() == b.big() && a.bits == b.bits;
+    const bool r_ff = da == db;
+    const bool num = (ai || af) && (bi || bf);
+    bool r_num = ii ? r_ii : ff && r_ff;
+    if (mixed) r_num = int_eq_float(ai ? a.big() : b.big(), ai ? a.bits : b.bits, ai ? db : da);  // rare
+    const bool byt = !an && !bn && !(ai || af) && ac == bc && (ac != V_EXT || a.ext() == b.ext()) && a.len == b.len;
+    if (an || bn) return (an && bn) ? 0u : 1u;
+    if (num) return r_num ? 0u : 1u;
+    if (!byt) return 1u;
+    return a.len == 0 ? 0u : 2u;
+}
+
+// LDS byte compare: 32-byte blocks, the 9 aligned words of each side read together and realigned
+// with v_alignbyte; bytes past n masked (the aligned reads may run up to 4 bytes past either range,
+// still inside the block's LDS, or return 0 past its end)
+__device__ bool lds_bytes_eq(u32 a, u32 b, u32 n) {
+    const u32 sa = a & 3, sb = b & 3;
+    u32 wa = a - sa, wb = b - sb;
+    u32 rem = n, diff = 0;
+    while (rem > 0 && diff == 0) {  // 16-byte blocks: 5 aligned words per side, read together
+        u32 xa[5], xb[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) { xa[j] = lds_u32(wa + 4 * j); xb[j] = lds_u32(wb + 4 * j); }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32 d = __builtin_amdgcn_alignbyte(xa[j + 1], xa[j], sa) ^ __builtin_amdgcn_alignbyte(xb[j + 1], xb[j], sb);
+            const u32 valid = rem >= 4u * j + 4 ? 0xFFFFFFFFu : rem > 4u * j ? (1u << (8 * (rem - 4 * j))) - 1 : 0u;
+            diff |= d & valid;
+        }
+        wa += 16;
+        wb += 16;
+        rem = rem > 16 ? rem - 16 : 0;
+    }
+    return diff == 0;
+}
+
+// global byte compare by one lane (queue overflow, keys >= 256): aligned dword loads, realigned;
+// a dword is loaded only when it holds a byte of its range
+__device__ bool glb_bytes_eq(u64 a, u64 b, u32 n) {
+    const u32 sa = (u32)(a & 3), sb = (u32)(b & 3);
+    const u64 a4 = a - sa, b4 = b - sb, ae = a + n, bend = b + n;
+    u32 pa = ((gp32)a4)[0], pb = ((gp32)b4)[0];
+    for (u32 k = 0; 4 * k < n; k++) {
+        const u64 na = a4 + 4 * (k + 1), nb = b4 + 4 * (k + 1);
+        const u32 qa = na < ae ? ((gp32)na)[0] : 0, qb = nb < bend ? ((gp32)nb)[0] : 0;
+        const u32 d = __builtin_amdgcn_alignbyte(qa, pa, sa) ^ __builtin_amdgcn_alignbyte(qb, pb, sb);
+        const u32 r = n - 4 * k;
+        const u32 valid = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1;
+        if (d & valid) return false;
+        pa = qa;
+        pb = qb;
+    }
+    return true;
+}
+
+// Per-round queue of payloads compared cooperatively after the parse (in LDS).
+typedef __attribute__((address_space(3))) u64* lds_u64p;
+typedef __attribute__((address_space(3))) u32* lds_u32p;
+struct FdQueue {
+    lds_u64p task;  // [3 * cap] (old address, new address, len | lane << 32 | key << 48)
+    lds_u32p count;
+    u32 cap;
+};
+
+// byte payloads of a and b (same class, ext, length >= 1) at blob positions pa / pb:
+// 0 equal, 1 changed, 3 queued
+template <class BL>
+__device__ __forceinline__ u32 payload_eq(const WVal& a, const BL& A, u32 pa, const WVal& b, const BL& B, u32 pb,
+                                          int key, const FdQueue& q) {
+    const u32 n = a.len;
+    if (a.hdr() + n <= 12 && b.hdr() + n <= 12) {  // whole payload in the decode windows
+        const u64 m0 = n >= 8 ? ~0ull : (1ull << (8 * n)) - 1;
+        const u32 m1 = n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1;
+        return (((a.bits ^ b.bits) & m0) | ((a.hi ^ b.hi) & m1)) ? 1u : 0u;
+    }
+    const u32 ya = pa + a.hdr() + A.s0, yb = pb + b.hdr() + B.s0;  // payload offsets from hb
+    const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
+    if (oa != ~0u && ob != ~0u) return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
+    const u64 xa = A.start + pa + a.hdr(), xb = B.start + pb + b.hdr();
+    if (key < 64) {
+        const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t < q.cap) {
+            q.task[3 * t] = xa;
+            q.task[3 * t + 1] = xb;
+            q.task[3 * t + 2] = (u64)n | (u64)threadIdx.x << 32 | (u64)key << 48;
+            return 3;
+        }
+    }
+    return glb_bytes_eq(xa, xb, n) ? 0u : 1u;
+}
+
+template <class BL>
+__device__ __forceinline__ u32 rd_decode(const BL& b, u32 p, WVal& v) {
+    u32 x0, x1, x2;
+    rd12(b, p, x0, x1, x2);
+    return decode_w(x0, x1, x2, b.len - p, v);
+}
+
+// header of a windowed blob: 0x92, str(40) legend hex (str8, or a wider str header), array header
+// -> 0 ok; *lp = position of the legend hex
+template <class BL>
+__device__ __forceinline__ int parse_header_w(const BL& b, u32* nvals, u32* off, u32* lp) {
+    if (b.len < 44) return 1;
+    u32 x0, x1, x2;
+    rd12(b, 0, x0, x1, x2);
+    if ((x0 & 0xff) != 0x92) return 1;
+    const u32 t1 = (x0 >> 8) & 0xff;
+    if (t1 == 0xd9 && (x0 >> 16 & 0xff) == 40) *lp = 3;                       // d9 28
+    else if (t1 == 0xda && (x0 >> 16) == 0x2800) *lp = 4;                       // da 00 28
+    else if (t1 == 0xdb && (x0 >> 16) == 0 && (x1 & 0xffff) == 0x2800) *lp = 6;  // db 00 00 00 28
+    else return 1;
+    u32 o = *lp + 40;
+    if (o >= b.len) return 1;
+    rd12(b, o, x0, x1, x2);
+    const u32 t = x0 & 0xff;
+    const u32 be2 = ((x0 >> 8) & 0xff) << 8 | ((x0 >> 16) & 0xff);
+    const u32 be4 = ((x0 >> 8) & 0xff) << 24 | ((x0 >> 16) & 0xff) << 16 | (x0 >> 24) << 8 | (x1 & 0xff);
+    if (t >= 0x90 && t <= 0x9f) { *nvals = t & 15; o += 1; }
+    else if (t == 0xdc) { if (o + 3 > b.len) return 1; *nvals = be2; o += 3; }
+    else if (t == 0xdd) { if (o + 5 > b.len) return 1; *nvals = be4; o += 5; }
+    else return 1;
+    *off = o;
+    return 0;
+}
+
+template <class BL>
+__device__ __forceinline__ bool seek_value_w(const BL& b, u32 first, u32 want, u32& idx, u32& pos, WVal& out) {
+    if (want < idx) { idx = 0; pos = first; }
+    for (;;) {
+        const u32 c = rd_decode(b, pos, out);
+        if (!c) return false;
+        if (idx == want) return true;
+        pos += c;
+        idx++;
+    }
+}
+
+// one update from its windows: returns the status; mask bits (k < 256) in mk, the rest straight into m
+template <class BL, class TB>
+__device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb, u64 mk[4], u64* m, const FdQueue& q) {
+    u32 cvo, cvn, po, pn, lpo, lpn;
+    if (parse_header_w(A, &cvo, &po, &lpo) || parse_header_w(B, &cvn, &pn, &lpn)) return 1;
+    u32 h[10];
+    rd_legend(A, lpo, h);
+    const int li_o = find_legend_w(tb.leg_o, tb.n_lo, h);
+    rd_legend(B, lpn, h);
+    const int li_n = find_legend_w(tb.leg_n, tb.n_ln, h);
+    if (li_o < 0 || li_n < 0) return 2;
+    if (cvo > FD_MAXV || cvn > FD_MAXV) return 3;
+    const bool al = tb.aligned[li_o * tb.n_ln + li_n];
+    if (al && cvo == cvn) {
+        // ---- lockstep: value v of both blobs belongs to the same union key ----
+        const auto kov = tb.key_of_val + (u64)li_o * tb.maxv;
+        u32 pa = po, pb = pn;
+        for (u32 v = 0; v < cvo; v++) {
+            WVal a, b;
+            const u32 ca = rd_decode(A, pa, a), cb = rd_decode(B, pb, b);
+            if (!ca || !cb) return 4;
+            const int k = v < (u32)tb.maxv ? kov[v] : -1;
+            if (k >= 0) {
+                u32 r = scalar_eq(a, b);
+                if (r == 2) r = payload_eq(a, A, pa, b, B, pb, k, q);
+                if (r == 1) set_bit(mk, m, k);
+            }
+            pa += ca;
+            pb += cb;
+        }
+        if (pa != A.len || pb != B.len) return 4;  // trailing bytes: unpackb raises ExtraData
+        return 0;
+    }
+    // ---- general: validate both blobs (msgpack.unpackb decodes everything first), then resolve
+    //      each union key through both maps ----
+    u32 p = po;
+    for (u32 v = 0; v < cvo; v++) { WVal x; u32 c = rd_decode(A, p, x); if (!c) return 4; p += c; }
+    if (p != A.len) return 4;
+    p = pn;
+    for (u32 v = 0; v < cvn; v++) { WVal x; u32 c = rd_decode(B, p, x); if (!c) return 4; p += c; }
+    if (p != B.len) return 4;
+    const auto mo = tb.map_o + (u64)li_o * tb.n_keys;
+    const auto mn = tb.map_n + (u64)li_n * tb.n_keys;
+    u32 io = 0, ipo = po, in = 0, ipn = pn;
+    for (int k = 0; k < tb.n_keys; k++) {
+        if (!((tb.cmp[k >> 6] >> (k & 63)) & 1)) continue;
+        const int so = mo[k], sn = mn[k];
+        u32 r;
+        if (so == -1 || sn == -1) r = (so == -1 && sn == -1) ? 0u : 1u;
+        else if (so == -3 || sn == -3) {
+            if (so == -3 && sn == -3) r = 0;
+            else return 4;
+        } else {
+            WVal a, b;
+            a.meta = b.meta = V_NIL;
+            a.len = b.len = 0;
+            if (so != -2) {
+                if ((u32)so >= cvo) return 1;
+                seek_value_w(A, po, (u32)so, io, ipo, a);
+            }
+            if (sn != -2) {
+                if ((u32)sn >= cvn) return 1;
+                seek_value_w(B, pn, (u32)sn, in, ipn, b);
+            }
+            r = scalar_eq(a, b);
+            if (r == 2) r = payload_eq(a, A, ipo, b, B, ipn, k, q);
+        }
+        if (r == 1) set_bit(mk, m, k);
+    }
+    return 0;
+}
+
+// Cooperative compare of one queued payload by a 16-lane group: lane j of step s takes old chunk
+// c = 16 s + j of the payload's aligned range and the matching 16 new bytes (two aligned chunks,
+// funnel-shifted by the two sides' relative skew).  Returns "differs" on every lane of the group.
+// A chunk is loaded only if it holds a byte of its payload (else the device zeros).
+__device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n, const u8* dummy) {
+    const u32 j = threadIdx.x & 15, grp = (threadIdx.x >> 4) & 3;
+    const u32 sa = (u32)(a & 15);
+    const u64 abase = a - sa;
+    const u64 e = b - sa, ebase = e & ~(u64)15;
+    const u32 sd = (u32)(e & 15), q = sd >> 2, sb = sd & 3;
+    const u64 bend = b + n;
+    const u32 nch = (n + sa + 15) >> 4;
+    bool diff = false;
+    for (u32 c0 = 0; c0 < nch; c0 += 32) {
+        u32x4 O[2], N0[2], N1[2];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {  // both steps' loads issued before any compare
+            const u32 c = c0 + 16 * s + j;
+            const bool act = c < nch;
+            const u64 oa = abase + 16ull * c, na = ebase + 16ull * c;
+            const bool ok0 = act && na < bend && na + 16 > b;
+            const bool ok1 = act && sd != 0 && na + 16 < bend;
+            const u32x4 z = {0, 0, 0, 0};
+            O[s] = act ? *(gp128)oa : z;
+            N0[s] = ok0 ? *(gp128)na : z;
+            N1[s] = ok1 ? *(gp128)(na + 16) : z;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const u32 c = c0 + 16 * s + j;
+            // dwords q .. q+4 of the 8 new dwords (two select stages on named values: an array
+            // here was turned into a dynamically indexed scratch copy)
+            const bool s1 = q & 1, s2 = q & 2;
+            const u32 b0 = s1 ? N0[s].y : N0[s].x, b1 = s1 ? N0[s].z : N0[s].y, b2 = s1 ? N0[s].w : N0[s].z;
+            const u32 b3 = s1 ? N1[s].x : N0[s].w, b4 = s1 ? N1[s].y : N1[s].x, b5 = s1 ? N1[s].z : N1[s].y;
+            const u32 b6 = s1 ? N1[s].w : N1[s].z;
+            const u32 t2[5] = {s2 ? b2 : b0, s2 ? b3 : b1, s2 ? b4 : b2, s2 ? b5 : b3, s2 ? b6 : b4};
+            const u32 o[4] = {O[s].x, O[s].y, O[s].z, O[s].w};
+            // payload bytes of this chunk: t in [lo, hi)
+            const int lo = c == 0 ? (int)sa : 0;
+            const int hi = (int)n + (int)sa - 16 * (int)c;
+            u32 d = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const u32 nw = __builtin_amdgcn_alignbyte(t2[k + 1], t2[k], sb);
+                const u32 lm = lo >= 4 * k + 4 ? 0u : lo <= 4 * k ? ~0u : ~0u << (8 * (lo - 4 * k));
+                const u32 hm = hi <= 4 * k ? 0u : hi >= 4 * k + 4 ? ~0u : (1u << (8 * (hi - 4 * k))) - 1;
+                d |= (o[k] ^ nw) & lm & hm;
+            }
+            diff |= c < nch && d != 0;
+        }
+    }
+    const u64 bal = __ballot(diff);
+    return ((bal >> (16 * grp)) & 0xFFFF) != 0;
+}
+
+constexpr u32 FD_TAB_LDS_MAX = 16384;  // tables up to this size are copied into each block's LDS
 typedef __attribute__((address_space(3))) void* fd_lds_vp;
 typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 
-template <int POOL>
+template <int UPR, int NH, int NTL>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
                                                      const u64* __restrict__ n_upd_dev, FdTab tg, FdTabOff to,
-                                                     const u8* __restrict__ tab_base, u64* __restrict__ masks,
-                                                     u8* __restrict__ status) {
-    __shared__ u32x4 s_pool[POOL];  // the round's blobs, packed back to back in 16-B chunks
+                                                     const u8* __restrict__ tab_base, const u8* __restrict__ dummy,
+                                                     u64* __restrict__ masks, u8* __restrict__ status) {
+    constexpr int NC = NH + NTL;       // chunks per blob image
+    constexpr int LS = 2 * NC;         // a lane's two images
+    constexpr int NCH = (UPR * LS + 63) / 64 * 64;  // image chunks per round (whole instructions)
+    constexpr u32 TCAP = UPR;          // queued payload compares per round (then a lane compares alone)
+    static_assert(NTL >= 2, "window shape");
+    __shared__ u32x4 s_img[NCH];
+    __shared__ u64 s_desc[4 * UPR];    // per blob (lane l, side s at 2l + s): head base, last chunk
+    __shared__ u64 s_task[3 * TCAP];
+    __shared__ u64 s_res[UPR];         // mask bits (keys < 64) found by the cooperative compares
+    __shared__ u32 s_ntask;
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
+    using BL = WBlob<NH, NTL>;
     const int lane = threadIdx.x;
-#if KD_FD_CLOCK
-    const u64 WE = wall_clock64();
-#endif
-    // device count: n_upd_host is the capacity of pairs, so pairs[u] (u < capacity) is loaded
-    // before the count arrives; capacity 0 = unknown -> wait for the count first
+    const bool owner = lane < UPR;
     const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 lim = spec ? n_upd_host : n_upd;
-    // one round ahead: the next round's pair is loaded while this round stages, its blob offsets
-    // while this round parses, so a round waits on one HBM latency (the staging) instead of three
-    const u64 step = (u64)gridDim.x * FD_NT;
+    const u64 step = (u64)gridDim.x * UPR;
     auto load_pair = [&](u64 uu) {
         uint2 p = make_uint2((u32)uu, (u32)uu);
-        if (pairs && uu < lim) p = pairs[uu];
+        if (pairs && uu < lim && owner) p = pairs[uu];
         return p;
     };
     auto load_off = [&](uint2 p, bool a, u64& os_, u64& ns_, u32& on_, u32& nn_) {
@@ -578,14 +808,16 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             nn_ = (u32)(noff[p.y + 1] - ns_);
         }
     };
-    u64 u0 = (u64)blockIdx.x * FD_NT;
-    u64 os = 0, ns = 0;
-    u32 on = 0, nn = 0;
-    // (the first round's pair and offsets are in flight while the tables are copied to LDS)
-    if (u0 < lim) load_off(load_pair(u0 + lane), u0 + lane < n_upd, os, ns, on, nn);
-    typedef const __attribute__((address_space(1))) u32x4* gp;
-    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp)(tab_base + i);
+    u64 u0 = (u64)blockIdx.x * UPR;
+    if (u0 >= lim || u0 >= n_upd) return;  // wave-uniform: no round for this block
+    u64 os, ns;
+    u32 on, nn;
+    // the first round's pair and offsets are in flight while the tables are copied to LDS
+    load_off(load_pair(u0 + lane), owner && u0 + lane < n_upd, os, ns, on, nn);
+    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp128)(tab_base + i);
     mp_tab_to_lds();
+    if (owner) s_res[lane] = 0;
+    if (lane == 0) s_ntask = 0;
     FdTabT<3> tb;
     tb.n_keys = tg.n_keys; tb.words = tg.words; tb.n_lo = tg.n_lo; tb.n_ln = tg.n_ln; tb.maxv = tg.maxv;
     typedef __attribute__((address_space(3))) u8* l8;
@@ -597,108 +829,107 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     tb.cmp = (typename ASP<3, u64>::type)(lt + to.cmp);
     tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
     tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
+    const FdQueue queue{(lds_u64p)s_task, (lds_u32p)&s_ntask, TCAP};
+    const u32 img0 = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img;
+    // window descriptors of one round: head base and last chunk of both blobs (no chunk: last < head)
+    auto put_desc = [&](u64 a0, u32 an, u64 b0, u32 bn, bool a) {
+        if (owner) {
+            s_desc[4 * lane] = a0 & ~(u64)15;
+            s_desc[4 * lane + 1] = a && an ? (a0 + an - 1) & ~(u64)15 : 0;
+            s_desc[4 * lane + 2] = b0 & ~(u64)15;
+            s_desc[4 * lane + 3] = a && bn ? (b0 + bn - 1) & ~(u64)15 : 0;
+        }
+    };
+    // LDS-DMA of one round's windows: instruction k fills image chunks [64k, 64k + 64), lane l chunk
+    // 64k + l (its blob and window position from the descriptors)
+    auto stage = [&]() {
+#pragma unroll 2
+        for (int k = 0; k < NCH / 64; k++) {
+            const u32 c = 64 * k + lane;
+            const u32 ow = c / LS, r = c - ow * LS;  // (LS even: an odd stride measured 50 % slower)
+            const u32 bl = 2 * ow + (r >= (u32)NC), i = r >= (u32)NC ? r - NC : r;
+            const bool real = ow < (u32)UPR && r < 2u * NC;
+            const u64 hb = s_desc[2 * (real ? bl : 0)], lc = s_desc[2 * (real ? bl : 0) + 1];
+            const u64 addr = i < (u32)NH ? hb + 16ull * i : lc - 16ull * (NTL - 2) + 16ull * (i - NH);
+            const bool valid = real && addr >= hb && addr <= lc;
+            // chunks holding no blob byte are not loaded (their LDS bytes are never decoded: every
+            // read is bounded by the blob length)
+            if (valid) __builtin_amdgcn_global_load_lds((fd_glb_vp)addr, (fd_lds_vp)(s_img + 64 * k), 16, 0, 0);
+        }
+    };
+    // Software pipeline, one HBM round trip per round: round r's windows are parsed while nothing
+    // is in flight but the next offsets; then round r+1's windows (LDS-DMA into the freed image)
+    // and round r's queued payloads are loaded together.
+    put_desc((u64)od + os, on, (u64)nd + ns, nn, owner && u0 + lane < n_upd);
     __syncthreads();
-    for (; u0 < lim; u0 += step) {
+    stage();
+    uint2 pr_n = load_pair(u0 + step + lane);
+    __syncthreads();  // vmcnt(0) + barrier: round 0's windows have landed
+    for (;;) {
         const u64 u = u0 + lane;
-#if KD_FD_CLOCK
-        const u64 T0 = clock64(), W0 = wall_clock64();
-#endif
-        if (u0 >= n_upd) break;  // wave-uniform
-        const bool act = u < n_upd;
-        const u64 un = u + step;
-        const uint2 pr_n = load_pair(un);
-        // ---- pool allocation: exclusive wave scan of the lanes' chunk counts ----
-        const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
-        const u64 ab = a0 & ~(u64)15, bb = b0 & ~(u64)15;
-        const u32 ad = (u32)(a0 - ab), bd = (u32)(b0 - bb);
-        const u32 na = act ? (ad + on + 15) >> 4 : 0, nb = act ? (bd + nn + 15) >> 4 : 0;
-        const u32 need = na + nb;
-        u32 x = need;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const u32 y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        const u32 off = x - need;
-        const bool fit = act && x <= (u32)POOL;  // lanes past the pool parse from global memory
-        const u64 bal = __ballot(fit);
-        const u32 used = bal ? __shfl(x, 63 - __clzll((long long)bal), 64) : 0;  // end of the last fitting lane
-        (void)used;
-#if KD_FD_CLOCK
-        const u64 T1 = clock64();
-#endif
-        // ---- staging, global -> LDS directly (LDS-DMA): owner lane by owner lane (a wave-uniform
-        //      loop, its descriptors read with readlane into SGPRs), lane l loads chunk c0 + l of the
-        //      owner's two blobs into pool chunk off + c0 + l (wave-uniform LDS base + 16 l), so
-        //      consecutive lanes read consecutive 16-B chunks and every load of the round is in
-        //      flight at once, without registers and without LDS reads between the loads ----
-        const u32 need_fit = fit ? need : 0u;
-        for (int w = 0; w < FD_NT; w++) {
-            const u32 need_w = (u32)__builtin_amdgcn_readlane((int)need_fit, w);
-            if (need_w == 0) continue;
-            const u32 off_w = (u32)__builtin_amdgcn_readlane((int)off, w);
-            const u32 na_w = (u32)__builtin_amdgcn_readlane((int)na, w);
-            const u64 ab_w = (u64)(u32)__builtin_amdgcn_readlane((int)(u32)ab, w) |
-                             (u64)(u32)__builtin_amdgcn_readlane((int)(u32)(ab >> 32), w) << 32;
-            const u64 bb_w = (u64)(u32)__builtin_amdgcn_readlane((int)(u32)bb, w) |
-                             (u64)(u32)__builtin_amdgcn_readlane((int)(u32)(bb >> 32), w) << 32;
-            for (u32 c0 = 0; c0 < need_w; c0 += FD_NT) {
-                const u32 c = c0 + lane;
-                if (c < need_w) {
-                    const u64 src = c < na_w ? ab_w + 16ull * c : bb_w + 16ull * (c - na_w);
-                    __builtin_amdgcn_global_load_lds((fd_glb_vp)src, (fd_lds_vp)(s_pool + off_w + c0), 16, 0, 0);
-                }
-            }
-        }
-        __syncthreads();
-        u64 os_n, ns_n;
-        u32 on_n, nn_n;
-        load_off(pr_n, un < n_upd, os_n, ns_n, on_n, nn_n);
-#if KD_FD_CLOCK
-        const u64 T2 = clock64();
-#endif
+        const bool act = owner && u < n_upd;
+        const u64 u1 = u0 + step;
+        const bool more = u1 < lim && u1 < n_upd;  // wave-uniform
+        u64 os_n = 0, ns_n = 0;
+        u32 on_n = 0, nn_n = 0;
+        if (more) load_off(pr_n, owner && u1 + lane < n_upd, os_n, ns_n, on_n, nn_n);
+        // ---- parse ----
+        u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
+        u8 st = 0;
+        u64* m = masks + u * tb.words;
         if (act) {
-            u64* m = masks + u * tb.words;
-            u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
-            u8 st;
-#if KD_FD_EXP == 1
-            if (fit) st = ((const u8*)(s_pool + off))[ad] == 7 ? 9 : 0;
-#else
-            if (fit) st = diff_one((lp8)((const u8*)(s_pool + off) + ad), on, (lp8)((const u8*)(s_pool + off + na) + bd), nn, tb, mk, m);
-#endif
-            else st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
-            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
-            for (int w = 0; w < tb.words; w++) {
-                if (w < 4) m[w] = mk[w];
-                else if (st) m[w] = 0;
+            for (int w = 4; w < tb.words; w++) m[w] = 0;
+            const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
+            BL A, B;
+            A.start = a0; A.len = on; A.s0 = (u32)(a0 & 15);
+            A.t0 = (int)(((a0 + (on ? on - 1 : 0)) & ~(u64)15) - (a0 & ~(u64)15)) - 16 * (NTL - 2);
+            A.img = img0 + 16u * (u32)(lane * LS);
+            B.start = b0; B.len = nn; B.s0 = (u32)(b0 & 15);
+            B.t0 = (int)(((b0 + (nn ? nn - 1 : 0)) & ~(u64)15) - (b0 & ~(u64)15)) - 16 * (NTL - 2);
+            B.img = img0 + 16u * (u32)(lane * LS + NC);
+            st = diff_one_w(A, B, tb, mk, m, queue);
+        }
+        __syncthreads();  // parse done: the image is free, the queue complete
+        if (more) {
+            put_desc((u64)od + os_n, on_n, (u64)nd + ns_n, nn_n, owner && u1 + lane < n_upd);
+            __syncthreads();
+            stage();
+            pr_n = load_pair(u1 + step + lane);
+        }
+        // ---- the queued payloads, 16 lanes per payload ----
+        const u32 nt = min(s_ntask, TCAP);
+        for (u32 t = (u32)lane >> 4; t < nt; t += 4) {
+            const u64 x = s_task[3 * t + 2];
+            const bool d = coop_differs(s_task[3 * t], s_task[3 * t + 1], (u32)x, dummy);
+            if (d && (lane & 15) == 0) {
+                const u32 ow = (u32)(x >> 32) & 0xFFFF, key = (u32)(x >> 48);
+                atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
             }
+        }
+        __syncthreads();  // the compares are in s_res; vmcnt(0): the next windows have landed
+        if (act) {
+            mk[0] |= s_res[lane];
+            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+            store_masks(m, tb.words, mk, st);
             status[u] = st;
         }
-        __syncthreads();  // the pool is rewritten by the next round
+        if (owner) s_res[lane] = 0;
+        if (lane == 0) s_ntask = 0;
+        if (!more) break;
+        __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations stay in program order)
+        u0 = u1;
         os = os_n; ns = ns_n; on = on_n; nn = nn_n;
-#if KD_FD_CLOCK
-        if (lane == 0) printf("FB %u %llu %llu\n", blockIdx.x, (unsigned long long)WE, (unsigned long long)wall_clock64());
-        if (lane == 0 && blockIdx.x % 97 == 0) {
-            const u64 T3 = clock64(), W3 = wall_clock64();
-            printf("FD entry->start %llu entry->end %llu wall %llu (x10ns) start %llu | blk %u offsets %llu staging %llu parse %llu total %llu used %u | hdr %llu dec %llu eq %llu nv %llu\n",
-                   (unsigned long long)(W0 - WE), (unsigned long long)(W3 - WE), (unsigned long long)(W3 - W0), (unsigned long long)W0 % 100000000, blockIdx.x, (unsigned long long)(T1 - T0), (unsigned long long)(T2 - T1), (unsigned long long)(T3 - T2),
-                   (unsigned long long)(T3 - T0), used, (unsigned long long)FD_DBG(0), (unsigned long long)FD_DBG(1),
-                   (unsigned long long)FD_DBG(2), (unsigned long long)FD_DBG(3));
-        }
-#endif
     }
 }
 
-// Fallback for blobs larger than the biggest slot or tables too large for LDS: one lane per update,
-// blobs parsed straight from global memory.
+// Fallback for tables too large for LDS: one lane per update, blobs parsed straight from global
+// memory.
 __global__ __launch_bounds__(FD_NT) void k_fielddiff_g(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                        const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                        const uint2* __restrict__ pairs, u64 n_upd_host,
                                                        const u64* __restrict__ n_upd_dev, FdTab tb,
                                                        u64* __restrict__ masks, u8* __restrict__ status) {
     const int lane = threadIdx.x;
-    mp_tab_to_lds();
-    __syncthreads();
     const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 lim = spec ? n_upd_host : n_upd;
@@ -711,13 +942,11 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff_g(const u8* __restrict__ od
         const u32 on = (u32)(ooff[pr.x + 1] - os);
         const u32 nn = (u32)(noff[pr.y + 1] - ns);
         u64* m = masks + u * tb.words;
+        for (int w = 4; w < tb.words; w++) m[w] = 0;
         u64 mk[4] = {0, 0, 0, 0};
         const u8 st = diff_one((gp8)(od + os), on, (gp8)(nd + ns), nn, tb, mk, m);
         if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
-        for (int w = 0; w < tb.words; w++) {
-            if (w < 4) m[w] = mk[w];
-            else if (st) m[w] = 0;
-        }
+        store_masks(m, tb.words, mk, st);
         status[u] = st;
     }
 }
@@ -821,7 +1050,8 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
         d_status = (u8*)b;
     }
     if (n_upd == 0 && d_n_upd == nullptr) return KD_OK;
-    // grid-stride: at most one resident wave per LDS-slot set (8 single-wave blocks per CU)
+    void* dz;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
     u64 work = d_n_upd ? (n_upd ? n_upd : (u64)1 << 22) : n_upd;
     // typical blob size: kd_blobs.size_hint, or the mean of host arenas
     auto typical = [](const kd_blobs* b) -> u64 {
@@ -834,38 +1064,32 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     to.leg_o = (u32)o_lo; to.leg_n = (u32)o_ln; to.map_o = (u32)o_mo; to.map_n = (u32)o_mn; to.cmp = (u32)o_cmp;
     to.aligned = (u32)o_al; to.key_of_val = (u32)o_kov; to.bytes = (u32)o_end;
     const bool lds_tab = o_end <= FD_TAB_LDS_MAX;
-    // LDS pool for one round of 64 updates: both blobs of every lane packed back to back, sized from
-    // the typical (mean) blob — ~(len + 15) / 16 chunks with the 16-B alignment skew — with 10 %
-    // headroom (1152 chunks: seven 64-update blocks per CU for ~110-B point features); a lane whose blobs do not fit the round's pool parses them from global memory.
-    const u64 per_round = (u64)FD_NT * 2 * (typ + 15) / 16 * 110 / 100;
-    int pool = !lds_tab ? 0 : per_round <= 1152 ? 1152 : per_round <= 1536 ? 1536 : per_round <= 2048 ? 2048
-                   : per_round <= 3072 ? 3072 : per_round <= 4096 ? 4096 : 0;
-#ifndef KD_FD_FORCE_G
-#define KD_FD_FORCE_G 0  // profiling builds: 1 = always the global-memory kernel
-#endif
-#ifndef KD_FD_G_PER_CU
-#define KD_FD_G_PER_CU 8  // resident single-wave blocks per CU for the global-memory kernel
-#endif
-    if (KD_FD_FORCE_G) pool = 0;
-    const u64 lds_blk = pool ? (u64)pool * 16 + 1024 + o_end : 1024;
-    const u64 per_cu = pool ? std::min<u64>(8, (160 * 1024) / lds_blk) : (u64)KD_FD_G_PER_CU;
-    unsigned blocks = (unsigned)std::min<u64>((work + FD_NT - 1) / FD_NT, (u64)ctx->n_cu * per_cu);
+    // window shape from the typical blob: small features (points, ~90-150 B) fit a long head window
+    // whole; larger ones (polygons) get head + tail windows around their geometry
+    const bool small = typ <= 144;
+    // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
+    // calculator for this launch's LDS), capped at the measured optimum.
+    const void* kern = !lds_tab ? (const void*)k_fielddiff_g
+                       : small ? (const void*)k_fielddiff<32, 8, 3> : (const void*)k_fielddiff<32, 5, 5>;
+    int per_cu = 0;
+    KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FD_NT, lds_tab ? o_end : 0));
+    // measured on C3 (polygons, 1.6M updates): 9 / 10 / 11 blocks per CU = 0.45 / 0.42 / 0.53 ms
+    per_cu = std::max(1, std::min(per_cu, 10));
+    const u64 upr = lds_tab ? 32 : FD_NT;
+    unsigned blocks = (unsigned)std::min<u64>((work + upr - 1) / upr, (u64)ctx->n_cu * (u64)per_cu);
     if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
         auto args = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
-                               tb, to, (const u8*)dt, d_masks, d_status);
+                               tb, to, (const u8*)dt, (const u8*)dz, d_masks, d_status);
         };
-        if (pool == 1152) args(k_fielddiff<1152>);
-        else if (pool == 1536) args(k_fielddiff<1536>);
-        else if (pool == 2048) args(k_fielddiff<2048>);
-        else if (pool == 3072) args(k_fielddiff<3072>);
-        else if (pool == 4096) args(k_fielddiff<4096>);
-        else
+        if (!lds_tab)
             hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks,
                                d_status);
+        else if (small) args(k_fielddiff<32, 8, 3>);
+        else args(k_fielddiff<32, 5, 5>);
     });
     if (rc) return rc;
     if (out_mem == KD_MEM_HOST) {

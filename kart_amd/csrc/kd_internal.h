@@ -75,8 +75,6 @@ struct kd_ctx {
     // when the next call's tables are identical)
     std::vector<uint8_t> fd_tab;
     int n_cu = 256;  // compute units (grid sizing of grid-stride kernels)
-    int occ_join2p = 0;  // resident k_join2p workgroups per CU (persistent grid size), 0 = not queried
-    int occ_join2r = 0;  // resident k_join2r workgroups per CU
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
 };
 
