@@ -1,36 +1,28 @@
 #!/usr/bin/env python3
 """Bench: device-resident bulk feature diff on MI355X (one JSON line on rank 0).
 
-Default workload (BASELINE.json configs[1], "C2"): a synthetic 10M-point int-PK layer per GPU with
-seeded 1% updates / 1% deletes / 1% inserts (kart_amd.synth.points_layer; the reference's feature
-blob and path encodings, synthetic OIDs).  One *step* = one full pass of the hot path over that
-layer: merge-path join + OID compare + key-ordered compaction of the delta set (k_partition2,
-k_join2, k_place2), then the msgpack field decode + Python-== column compare of every update
-(k_fielddiff) — all on the device, inputs resident in HBM before the timed region.
+Default workload (BASELINE.json configs[2], "C3", the north-star config): ONE synthetic
+100M-MULTIPOLYGON int-PK layer, 10 % edits (4 % geometry + 4 % attribute updates, 1 % deletes, 1 %
+inserts; kart_amd.synth.polygons_layer: the reference's feature blob and path encodings, synthetic
+OIDs).  One *step* = one full pass of the hot path over that layer: merge-path join + OID compare +
+key-ordered compaction of the delta set (k_partition2, k_join2, k_place2), then the msgpack field
+decode + Python-== column compare of every update (k_fielddiff) — all on the device, inputs
+resident in HBM before the timed region.
 
---workload c3 (BASELINE configs[2]): a 100M-polygon int-PK layer per GPU (--n), 10% edits: 4% geometry
-updates, 4% attribute updates, 1% deletes, 1% inserts; same step as C2 (blobs materialised only for the
-updated features: nothing else is read).
+--gpus N (one process per GPU, launched by torch.distributed.run): the SAME layer split into N
+bucket ranges (whole 64-pk leaf buckets: synth.shard_pk_range); each rank generates and diffs its
+range, and every step all-gathers the per-rank counts and the compacted delta records (rebased to
+global indices) over RCCL inside libkartdiff (kd_diff2_gather) — strong scaling.  The harness
+(barrier, max-over-ranks time, the RCCL id broadcast) uses torch.distributed's gloo backend on the
+CPU; no device memory, stream or collective of the measured path goes through torch, and at N=1
+torch is not imported at all.
 
---workload c4 (BASELINE configs[3]): a 50M-row string-PK table per GPU (MsgpackHashPathEncoder paths)
-three-way merge classification: classify2(ours, theirs) + k_resolve3 (ancestor lookup + the libgit2
-conflict rule) over the paths where ours and theirs differ.
+--workload c2 (configs[1]): a 10M-point layer per GPU, 1 % upd/del/ins (weak scaling at N>1);
+c4 (configs[3]): 50M-row string-PK three-way merge classification; c5 (configs[4], scaled):
+spatial-filter envelopes + EnvelopeEncoder + overlap; c6: hex WKB of every geometry.
 
---workload c5 (BASELINE configs[4], scaled: --n geometries per GPU, default 20M): GPKG geometry
-blobs of a spatially filtered layer (synth.geometry_layer); one step = k_envelopes (header /
-stored envelope or point WKB -> SpatialFilter bbox test + identity-CRS index envelope +
-EnvelopeEncoder bytes) + k_env_overlap (decode + cyclic overlap of the encoded envelopes).
-
---workload c6 (--n geometries per GPU, default 20M): the C5 geometry arena hex-encoded
-as `kart diff -o json` formats geometries (kd_hex_encode: k_wkb_start WKB offsets + k_hex
-streaming 16 B -> 32 B hex per lane).
-
-Multi-GPU (torch.distributed, one process per GPU, RCCL): each rank owns a disjoint dataset3
-path-bucket range (its own shard; weak scaling); the only collective is the all-gather of per-rank
-counts each step.  value = units of all ranks / max-rank time.
-
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|c6] [--n UNITS]
-                       [--no-cpu-baseline]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c6] [--n UNITS]
+                       [--no-cpu-baseline] [--no-host-timing]
 """
 import argparse
 import json
@@ -45,6 +37,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "feature deltas classified+field-diffed/sec (M/s) at 1/2/4/8 GPUs; % HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# the reference's own hot path (kart's Python diff_feature + get_feature/== loop, git
+# diff-tree for libgit2) measured on 1 core in the build container on a 1M-feature 1 % layer
+REFERENCE_CPU_PATH = {"value": 0.54, "unit": "M feature-pairs/s", "cores": 1, "kind": "reference",
+                      "sample": "BASELINE.md: reference kart diff hot path (Python + git diff-tree), synthetic 1M "
+                                "points, 1 % U/I/D, build container (the reference cannot run on the GPU box)"}
 
 
 def parse():
@@ -52,12 +49,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "c6"])
-    ap.add_argument("--n", type=int, default=0, help="units per GPU (c2: points, default 10M; c3: polygons, 100M; c4: rows, 50M; c5: geometries, 20M)")
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "c6"])
+    ap.add_argument("--n", type=int, default=0,
+                    help="units (c3: polygons of the whole layer, 100M; c2: points per GPU, 10M; c4: rows, 50M; "
+                         "c5/c6: geometries, 20M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-timing", action="store_true", help="skip the host pack / H2D timings")
     ap.add_argument("--unordered", action="store_true",
-                    help="c2: tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+                    help="c2/c3: tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
@@ -76,57 +76,83 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-class Dist:
-    def __init__(self):
-        import torch
-        import torch.distributed as dist
+def host_cores():
+    try:
+        c = len(os.sched_getaffinity(0))
+    except AttributeError:
+        c = os.cpu_count() or 1
+    return max(1, min(c, 16))  # the GPU box's CPU share is 16 cores (nproc shows the whole host)
 
-        self.torch, self.dist = torch, dist
+
+class Harness:
+    """rank / world from the launcher's env; barrier, max and object exchange over gloo (CPU) when
+    world > 1.  Nothing of the measured path goes through it."""
+
+    def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
         if self.world > 1:
+            import torch.distributed as dist
+
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", rank=self.rank, world_size=self.world, device_id=torch.device("cuda", local))
-        else:
-            torch.cuda.set_device(0)
-        self.dev = torch.device("cuda", torch.cuda.current_device())
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
 
-    def timed(self, step, steps, exchange=None):
-        """barrier + sync, K steps, sync + barrier; returns the max-over-ranks seconds"""
-        torch, dist = self.torch, self.dist
-        if self.world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-            if exchange is not None and self.world > 1:
-                exchange()
-        torch.cuda.synchronize()
-        if self.world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if self.world > 1:
-            e = torch.tensor([el], device=self.dev, dtype=torch.float64)
-            dist.all_reduce(e, op=dist.ReduceOp.MAX)
-            el = float(e.item())
-        return el
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
 
-    def total(self, *vals):
-        if self.world == 1:
-            return vals
-        t = self.torch.tensor(list(vals), device=self.dev, dtype=self.torch.int64)
-        self.dist.all_reduce(t)
-        return tuple(int(x) for x in t.tolist())
+    def max(self, x):
+        if not self.dist:
+            return x
+        out = [None] * self.world
+        self.dist.all_gather_object(out, float(x))
+        return max(out)
+
+    def allgather(self, obj):
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def bcast(self, obj):
+        if not self.dist:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
 
     def close(self):
-        if self.world > 1:
+        if self.dist:
             self.dist.destroy_process_group()
 
 
-def roofline(kern, dom, alg_bytes, traffic_json, units_tag, n_units):
+def engine_for(H):
+    from kart_amd.engine import Engine
+
+    eng = Engine(H.local)
+    if H.world > 1:  # the library's own RCCL communicator; the id travels over the harness
+        uid = H.bcast(Engine.comm_unique_id() if H.rank == 0 else None)
+        eng.comm_init(H.world, H.rank, uid)
+    return eng
+
+
+def timed(H, eng, step, steps):
+    """barrier + device sync, K steps, device sync + barrier; the max-over-ranks seconds"""
+    H.barrier()
+    eng.device_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.device_sync()
+    H.barrier()
+    return H.max(time.perf_counter() - t0)
+
+
+def roofline(kern, dom, alg_bytes, traffic_json, n_units):
     """roofline object of the dominant kernel: algorithmic bytes per launch / its average launch time"""
     if dom not in kern:
         return None
@@ -153,49 +179,76 @@ def kernel_times(eng, names):
     return kern
 
 
+def oracle():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+
+    return O
+
+
 # ---------------------------------------------------------------------------------------------
-def run_c2(args, D, polygons=False):
-    torch = D.torch
+# c2 / c3: two-way diff + field diff
+def run_diff(args, H, polygons):
     from kart_amd import shard, synth
     from kart_amd.device import DiffPipeline
-    from kart_amd.engine import Engine
     from kart_amd.schema import FieldMaps
 
-    n = args.n
+    n, world, rank = args.n, H.world, H.rank
+    split = polygons and world > 1  # C3: one layer split by bucket range (strong scaling)
     t0 = time.time()
-    if polygons:  # C3: 10 % edits (4 % geometry + 4 % attribute updates, 1 % del, 1 % ins)
-        L = synth.polygons_layer(n, seed=synth.SEED + D.rank, pk0=shard.rank_pk_base(D.rank, n))
+    if polygons:
+        n_pks = n + n // 100
+        lo, hi = synth.shard_pk_range(rank, world, n_pks) if split else (0, n_pks)
+        L = synth.polygons_layer(n, lo=lo, hi=hi)
     else:
-        L = synth.points_layer(n, seed=synth.SEED + D.rank, pk0=shard.rank_pk_base(D.rank, n))
-    log(f"[rank {D.rank}] generated {n} {'polygons' if polygons else 'points'} in {time.time() - t0:.1f}s "
-        f"(+{L.n_insert} ins, ~{L.n_update} upd, -{L.n_delete} del)")
+        L = synth.points_layer(n, seed=synth.SEED + rank, pk0=shard.rank_pk_base(rank, n))
+    gen_s = time.time() - t0
+    log(f"[rank {rank}] generated {L.base.n}+{L.target.n} entries in {gen_s:.1f}s "
+        f"(+{L.n_insert} ins, {L.n_update} upd, -{L.n_delete} del)")
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
-    eng = Engine(torch.cuda.current_device())
-    eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, D.dev, ordered=not args.unordered)
-    torch.cuda.synchronize()
+    eng = engine_for(H)
+    gather = None
+    if split:  # global sorted index of this shard's first entry on each side
+        sizes = H.allgather((L.base.n, L.target.n))
+        gather = (sum(s[0] for s in sizes[:rank]), sum(s[1] for s in sizes[:rank]))
+    t0 = time.perf_counter()
+    pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=not args.unordered,
+                        gather=gather)
+    h2d_s = time.perf_counter() - t0
+    h2d_bytes = 28 * (L.base.n + L.target.n) + int(L.base_blobs[0].size + L.target_blobs[0].size) + \
+        8 * int(L.base_blobs[1].size + L.target_blobs[1].size)
 
     # ---- warmup + correctness of the resident pipeline against the generator's own counts ----
     for _ in range(max(1, args.warmup)):
         pipe.step()
-    torch.cuda.synchronize()
+    eng.sync()
     counts, delta, upd, masks, status = pipe.results()
+    plan = (L.n_insert, L.n_update, L.n_delete)
     if not args.no_check:
-        assert (counts["inserts"], counts["updates"], counts["deletes"]) == (L.n_insert, L.n_update, L.n_delete), counts
+        assert (counts["inserts"], counts["updates"], counts["deletes"]) == plan, (counts, plan)
         assert not status.any(), "fielddiff status flags set"
+    if split:
+        mx = max(x for x in H.allgather(counts["deltas"]))
+        pipe.reserve_gather(mx)
+        pipe.step()
+        eng.sync()
+        g_counts, g_delta = pipe.gathered()
+        tot = [sum(x) for x in zip(*H.allgather(plan))]
+        if not args.no_check:  # every rank holds the whole diff: counts of all ranks, global key order
+            assert (g_counts["inserts"], g_counts["updates"], g_counts["deletes"]) == tuple(tot), (g_counts, tot)
+            assert g_delta.shape[0] == g_counts["deltas"]
     n_pairs = L.base.n + L.n_insert
-    counts_t = torch.tensor([counts["inserts"], counts["updates"], counts["deletes"]], device=D.dev, dtype=torch.int64)
-    gathered = [torch.empty_like(counts_t) for _ in range(D.world)]
 
     eng.prof_reset()
-    eng.prof_select(None if args.time_all else ["k_join2"])
+    eng.prof_select(None if args.time_all else ["k_fielddiff" if polygons else "k_join2"])
     eng.prof_enable(not args.no_events)
-    elapsed = D.timed(pipe.step, args.steps, lambda: D.dist.all_gather(gathered, counts_t))
+    elapsed = timed(H, eng, pipe.step, args.steps)
     eng.prof_enable(False)
-    total_pairs, total_deltas = D.total(n_pairs, counts["deltas"])
-    kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_fielddiff"))
+    total_pairs = sum(H.allgather(n_pairs))
+    total_deltas = sum(H.allgather(counts["deltas"]))
+    kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_fielddiff", "k_rebase"))
 
-    # ---- roofline of the dominant kernel (algorithmic bytes per launch, DESIGN.md §3.1) ----
+    # ---- roofline of the dominant kernel (algorithmic bytes per launch, DESIGN.md §3) ----
     nA, nB = L.base.n, L.target.n
     ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
     ok_u = (upd[:, 0] < nA) & (upd[:, 1] < nB)  # (profiling variants with --no-check may emit junk)
@@ -205,128 +258,224 @@ def run_c2(args, D, polygons=False):
         "k_join2": 28 * (nA + nB) + 8 * counts["deltas"] + 8 * counts["updates"],
         "k_fielddiff": upd_bytes + counts["updates"] * (8 + 8 * maps.words + 1),
     }
-    dom = max(kern, key=lambda k: kern[k][1]) if kern else None
-    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, "n_points", n) if dom in alg else None
-    cpu = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_c2(L, maps, args.cpu_seconds, "C3" if polygons else "C2")
+    dom = max((k for k in kern if k in alg), key=lambda k: kern[k][1]) if kern else None
+    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, n) if dom else None
+    cpu = host = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_diff(L, maps, args.cpu_seconds, "C3" if polygons else "C2")
+    if rank == 0 and world == 1 and not args.no_host_timing:
+        host = host_timing(eng, L, h2d_s, h2d_bytes)
     eng.close()
-    return {
+    wl = (f"C3: ONE {n}-polygon int-PK layer{f' split into {world} bucket-range shards' if split else ''}, 10% edits "
+          "(4% geometry + 4% attribute updates, 1% del, 1% ins), two-commit diff + field diff") if polygons else \
+        f"C2: {n}-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff"
+    out = {
         "metric": METRIC,
         "value": round(total_pairs * args.steps / elapsed / 1e6, 2),
         "unit": "M feature-pairs/s",
-        "n_gpus": D.world,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if polygons else "weak",
         "vs_baseline": None,
         "dtype": "u8/u64 (integer + fp64 compare)",
         "data": ("synthetic (seeded MULTIPOLYGON layer: reference blob/path encodings, synthetic OIDs; "
                  "blobs materialised for updated features only)") if polygons else
                 "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
-        "config": {"workload": (f"C3: {n}-polygon int-PK layer per GPU, 10% edits (4% geometry + 4% attribute "
-                                "updates, 1% del, 1% ins), two-commit diff + field diff") if polygons else
-                               "C2: 10M-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff",
-                   "features_per_gpu": n, "pairs_per_step": total_pairs, "deltas_per_step": total_deltas,
-                   "updates_per_step": counts["updates"],
+        "config": {"workload": wl, "features": n if polygons else n * world, "pairs_per_step": total_pairs,
+                   "deltas_per_step": total_deltas, "updates_per_step": sum(H.allgather(counts["updates"])),
                    "delta_order": "tile-grouped (same delta set)" if args.unordered else "key",
-                   "parallelism": f"bucket-range shards x{D.world}"},
+                   "parallelism": f"bucket-range shards x{world}" + (", RCCL all-gather of counts + delta records"
+                                                                      if split else "")},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if host:
+        out["host"] = host
+    return out
 
 
-def cpu_baseline_c2(L, maps, seconds, tag="C2"):
-    """oracle classify2 + fielddiff (sequential C, 1 core) on the same layer, repeated for ~N s"""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle import oracle as O
+def _shard_bounds(L, parts):
+    from kart_amd import shard
 
+    bits = shard.bucket_bits(L.base.key_mode, L.base.encoding)
+    cuts = shard.cut_points([L.base.key, L.target.key], parts, bits)
+    return shard.slice_bounds(L.base.key, cuts, bits), shard.slice_bounds(L.target.key, cuts, bits)
+
+
+def _oracle_shard(O, L, maps, ba, bb, s):
+    """oracle classify2 + fielddiff of bucket-range shard s (the C restatement; ctypes drops the GIL)"""
     A, B = L.base, L.target
+    a0, a1, b0, b1 = int(ba[s]), int(ba[s + 1]), int(bb[s]), int(bb[s + 1])
+    delta, c = O.classify2(A.key[a0:a1], A.oid[a0:a1], B.key[b0:b1], B.oid[b0:b1])
+    upd = delta[(delta[:, 0] != O.NONE) & (delta[:, 1] != O.NONE)].astype(np.int64)
+    ob, oo = L.base_blobs
+    nb, no = L.target_blobs
+    O.fielddiff(ob, oo, nb, no, np.stack([upd[:, 0] + a0, upd[:, 1] + b0], 1).astype(np.uint32), maps)
+    return (a1 - a0) + c["inserts"]
+
+
+def cpu_baseline_diff(L, maps, seconds, tag):
+    """The C oracle's classify2 + fielddiff (test infrastructure, kd_oracle.c) on the host cores:
+    all cores over bucket-range shards of the whole layer, and one thread over one shard."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    O = oracle()
+    cores = host_cores()
+    parts = 4 * cores
+    ba, bb = _shard_bounds(L, parts)
+    with ThreadPoolExecutor(cores) as ex:
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            pairs = sum(ex.map(lambda s: _oracle_shard(O, L, maps, ba, bb, s), range(parts)))
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+    allc = pairs * reps / dt / 1e6
     t0 = time.perf_counter()
-    reps = 0
+    reps1 = 0
     while True:
-        delta, counts = O.classify2(A.key, A.oid, B.key, B.oid)
-        upd = delta[(delta[:, 0] != O.NONE) & (delta[:, 1] != O.NONE)]
-        O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
-        reps += 1
-        if time.perf_counter() - t0 >= seconds:
+        p1 = _oracle_shard(O, L, maps, ba, bb, 0)
+        reps1 += 1
+        if time.perf_counter() - t0 >= seconds / 2:
             break
-    dt = time.perf_counter() - t0
-    pairs = (A.n + L.n_insert) * reps
-    return {"value": round(pairs / dt / 1e6, 3), "unit": "M feature-pairs/s", "cores": 1, "kind": "port",
-            "sample": f"the full {tag} layer ({A.n + L.n_insert} pairs) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
-                      f"classify2 + fielddiff, 1 thread"}
+    dt1 = time.perf_counter() - t0
+    return {"value": round(allc, 2), "unit": "M feature-pairs/s", "cores": cores, "kind": "port",
+            "sample": f"the full {tag} layer ({pairs} pairs) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c classify2 + "
+                      f"fielddiff on {cores} threads over {parts} bucket-range shards",
+            "one_thread": {"value": round(p1 * reps1 / dt1 / 1e6, 3), "unit": "M feature-pairs/s", "cores": 1,
+                           "sample": f"one shard ({p1} pairs, 1/{parts} of the layer) x {reps1} reps in {dt1:.1f}s"},
+            "reference_path": REFERENCE_CPU_PATH}
+
+
+def host_timing(eng, L, h2d_s, h2d_bytes):
+    """What the drop-in path spends outside the timed device step, for the same layer:
+    * pack: the base side's relative leaf paths ('c/c/c/c/<b64(msgpack([pk]))>', as the tree walk
+      yields them) -> join keys (native, multithreaded) -> H2D of keys + OIDs from pinned staging ->
+      GPU radix sort (kd_sort_side) into a device-resident side;
+    * h2d: uploading both sides + the update blob arenas from pageable numpy arrays (the pipeline
+      setup above)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+
+    from kart_amd import _native as N
+    from kart_amd import packing, synth
+    from kart_amd.device import DevBuf
+
+    n = L.base.n
+    pks = (L.base.key >> np.uint64(40)).astype(np.int64) * 64 + (L.base.key & np.uint64(63)).astype(np.int64)
+    chunks = [(a, min(n, a + 4_000_000)) for a in range(0, n, 4_000_000)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(host_cores()) as ex:
+        parts = list(ex.map(lambda c: synth.int_pk_paths(pks[c[0]:c[1]]), chunks))
+    arena = np.concatenate([p[0] for p in parts])
+    off = np.zeros(n + 1, np.uint64)
+    pos = 0
+    for (a, b), (_, o) in zip(chunks, parts):
+        off[a + 1:b + 1] = o[1:] + np.uint64(pos)
+        pos += int(o[-1])
+    gen_paths_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    keys = packing.parse_keys(arena, off, packing.INT_PK_ENCODING)
+    parse_s = time.perf_counter() - t0
+    del arena, off
+    assert np.array_equal(keys, L.base.key)
+    # pinned staging -> HBM
+    nbytes = 28 * n
+    hp = ctypes.c_void_p()
+    N.check(N.lib().kd_host_alloc(nbytes, ctypes.byref(hp)), "kd_host_alloc")
+    try:
+        pinned = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_uint8)), (nbytes,))
+        pinned[:8 * n] = keys.view(np.uint8)
+        pinned[8 * n:] = L.base.oid.reshape(-1)
+        dk, do, dord = DevBuf(eng, 8 * n), DevBuf(eng, 20 * n), DevBuf(eng, 4 * n)
+        eng.sync()
+        t0 = time.perf_counter()
+        N.check(eng.L.kd_memcpy(eng.ctx, dk.ptr, hp.value, 8 * n, N.KD_COPY_H2D), "kd_memcpy")
+        N.check(eng.L.kd_memcpy(eng.ctx, do.ptr, hp.value + 8 * n, 20 * n, N.KD_COPY_H2D), "kd_memcpy")
+        eng.sync()
+        pinned_s = time.perf_counter() - t0
+    finally:
+        N.lib().kd_host_free(hp)
+    dup = ctypes.c_uint32(0)
+    t0 = time.perf_counter()
+    N.check(eng.L.kd_sort_side(eng.ctx, dk.ptr, do.ptr, dord.ptr, n, ctypes.byref(dup)), "kd_sort_side")
+    eng.sync()
+    sort_s = time.perf_counter() - t0
+    assert not dup.value and np.array_equal(dk.download(np.uint64, n), L.base.key)
+    return {"pack_entries": n, "host_pack_s": round(parse_s, 3), "gpu_sort_s": round(sort_s, 4),
+            "pack_h2d_pinned_s": round(pinned_s, 4), "pack_h2d_pinned_GBps": round(nbytes / pinned_s / 1e9, 1),
+            "h2d_s": round(h2d_s, 3), "h2d_bytes": h2d_bytes, "h2d_GBps": round(h2d_bytes / h2d_s / 1e9, 1),
+            "note": f"host_pack_s = native parse of {n} relative leaf paths ('c/c/c/c/<b64 msgpack pk>', "
+                    f"generated in {gen_paths_s:.1f}s, not counted) into join keys on {host_cores()} threads; then "
+                    "H2D of keys + OIDs from pinned memory and kd_sort_side (LDS-ranked LSD radix sort + OID "
+                    "permute) leave a device-resident sorted side. h2d_s = the pipeline setup's uploads of both "
+                    "sides + update blobs from pageable memory."}
 
 
 # ---------------------------------------------------------------------------------------------
-def run_c5(args, D):
+def run_c5(args, H):
     import ctypes
 
-    torch = D.torch
     from kart_amd import _native as N
     from kart_amd import synth
-    from kart_amd.device import to_dev
-    from kart_amd.engine import Engine
+    from kart_amd.device import DevBuf
 
     n, bits = args.n, 20
     nb = bits // 2
     t0 = time.time()
-    data, off, is_pt = synth.geometry_layer(n, seed=synth.SEED + D.rank)
-    log(f"[rank {D.rank}] generated {n} geometries ({data.size / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
-    eng = Engine(torch.cuda.current_device())
-    eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    d_data, d_off = to_dev(data, D.dev), to_dev(off, D.dev)
+    data, off, is_pt = synth.geometry_layer(n, seed=synth.SEED + H.rank)
+    log(f"[rank {H.rank}] generated {n} geometries ({data.size / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
+    eng = engine_for(H)
+    d_data, d_off = DevBuf.from_numpy(eng, data), DevBuf.from_numpy(eng, off)
     g = N.KdBlobs()
-    g.n, g.data, g.off, g.mem, g.size_hint = n, d_data.data_ptr(), d_off.data_ptr(), N.KD_MEM_DEVICE, 0
-    match = torch.empty(n, dtype=torch.uint8, device=D.dev)
-    enc = torch.empty(n * nb, dtype=torch.uint8, device=D.dev)
-    ok = torch.empty(n, dtype=torch.uint8, device=D.dev)
-    ovl = torch.empty(n, dtype=torch.uint8, device=D.dev)
+    g.n, g.data, g.off, g.mem, g.size_hint = n, d_data.ptr, d_off.ptr, N.KD_MEM_DEVICE, 0
+    match, enc, ok, ovl = DevBuf(eng, n), DevBuf(eng, n * nb), DevBuf(eng, n), DevBuf(eng, n)
     fe = (ctypes.c_double * 4)(*synth.C5_FILTER)
     q = (ctypes.c_double * 4)(synth.C5_FILTER[0], synth.C5_FILTER[2], synth.C5_FILTER[1], synth.C5_FILTER[3])
     L, ctx = eng.L, eng.ctx
 
     def step():
-        N.check(L.kd_envelopes(ctx, ctypes.byref(g), fe, bits, match.data_ptr(), enc.data_ptr(), ok.data_ptr(),
-                               N.KD_MEM_DEVICE, None), "kd_envelopes")
-        N.check(L.kd_env_overlap(ctx, enc.data_ptr(), n, bits, q, ovl.data_ptr(), N.KD_MEM_DEVICE), "kd_env_overlap")
+        N.check(L.kd_envelopes(ctx, ctypes.byref(g), fe, bits, match.ptr, enc.ptr, ok.ptr, N.KD_MEM_DEVICE, None),
+                "kd_envelopes")
+        N.check(L.kd_env_overlap(ctx, enc.ptr, n, bits, q, ovl.ptr, N.KD_MEM_DEVICE), "kd_env_overlap")
 
     for _ in range(max(1, args.warmup)):
         step()
-    torch.cuda.synchronize()
+    eng.sync()
+    h_match, h_ok = match.download(np.uint8, n), ok.download(np.uint8, n)
     if not args.no_check:  # size-independent: an encoded envelope only where the indexer stores one
-        assert not (ok.cpu().numpy().astype(bool) & (match.cpu().numpy() == 2)).any(), "enc_ok on a null geometry"
+        assert not (h_ok.astype(bool) & (h_match == 2)).any(), "enc_ok on a null geometry"
     eng.prof_reset()
     eng.prof_select(None if args.time_all else ["k_envelopes"])
     eng.prof_enable(not args.no_events)
-    cnt = torch.zeros(1, dtype=torch.int64, device=D.dev)
-    gathered = [torch.empty_like(cnt) for _ in range(D.world)]
-    elapsed = D.timed(step, args.steps, lambda: D.dist.all_gather(gathered, cnt))
+    elapsed = timed(H, eng, step, args.steps)
     eng.prof_enable(False)
-    (total,) = D.total(n)
+    total = sum(H.allgather(n))
     kern = kernel_times(eng, ("k_envelopes", "k_env_overlap"))
     npt = int(is_pt.sum())
     # algorithmic bytes per k_envelopes launch: offsets (8 B) + GPKG header (8 B) + stored envelope
     # (32 B, polygons) or point WKB (21 B) read; match + enc_ok flags (2 B) + encoded envelope written
     alg = n * (8 + 8 + 2 + nb) + npt * 21 + (n - npt) * 32
-    roof = roofline(kern, "k_envelopes", alg, args.traffic_json, "n_geoms", n)
+    roof = roofline(kern, "k_envelopes", alg, args.traffic_json, n)
     cpu = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from oracle import oracle as O
-
+    if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
+        O = oracle()
         m = min(n, 2_000_000)
+        h_enc = enc.download(np.uint8, m * nb).reshape(m, nb)
         t0 = time.perf_counter()
         reps = 0
         while True:
             om, oe, okk, _ = O.envelope_batch(data[: int(off[m])], off[: m + 1], synth.C5_FILTER, bits)
             if reps == 0 and not args.no_check:  # the baseline's sample doubles as a bit-exact check
-                assert np.array_equal(match[:m].cpu().numpy(), om), "k_envelopes match flags differ from the oracle"
-                assert np.array_equal(ok[:m].cpu().numpy(), okk), "k_envelopes enc_ok differs from the oracle"
-                assert np.array_equal(enc[: m * nb].cpu().numpy().reshape(m, nb), oe), "EnvelopeEncoder bytes differ"
+                assert np.array_equal(h_match[:m], om), "k_envelopes match flags differ from the oracle"
+                assert np.array_equal(h_ok[:m], okk), "k_envelopes enc_ok differs from the oracle"
+                assert np.array_equal(h_enc, oe), "EnvelopeEncoder bytes differ"
                 t0 = time.perf_counter()
             reps += 1
             if time.perf_counter() - t0 >= min(args.cpu_seconds, 5.0):
@@ -337,86 +486,69 @@ def run_c5(args, D):
                          f"envelope batch (bbox test + index envelope + EnvelopeEncoder), 1 thread"}
     eng.close()
     return {
-        "metric": METRIC,
-        "value": round(total * args.steps / elapsed / 1e6, 2),
-        "unit": "M geometries/s",
-        "n_gpus": D.world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64 (envelopes, EnvelopeEncoder) + u8",
+        "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M geometries/s",
+        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64 (envelopes, EnvelopeEncoder) + u8",
         "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
         "config": {"workload": f"C5 (scaled to {n} geometries per GPU): spatial-filter envelopes + "
                                "EnvelopeEncoder + encoded-envelope overlap",
                    "geoms_per_gpu": n, "points": npt, "bits": bits, "filter": list(synth.C5_FILTER),
-                   "parallelism": f"independent shards x{D.world}"},
+                   "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
-        "roofline": roof,
-        "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu,
     }
 
 
 # ---------------------------------------------------------------------------------------------
-def run_c6(args, D):
+def run_c6(args, H):
     """Writer formatting: hex WKB of every geometry of the C5 layer (kd_hex_encode,
     KD_HEX_GPKG_WKB), the formatting `kart diff -o json` applies per geometry value."""
     import ctypes
 
-    torch = D.torch
     from kart_amd import _native as N
     from kart_amd import synth
-    from kart_amd.device import to_dev
-    from kart_amd.engine import Engine
+    from kart_amd.device import DevBuf
 
     n = args.n
     t0 = time.time()
-    data, off, is_pt = synth.geometry_layer(n, seed=synth.SEED + D.rank)
+    data, off, is_pt = synth.geometry_layer(n, seed=synth.SEED + H.rank)
     nbytes = int(off[-1])
-    log(f"[rank {D.rank}] generated {n} geometries ({nbytes / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
-    eng = Engine(torch.cuda.current_device())
-    eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    d_data, d_off = to_dev(data, D.dev), to_dev(off, D.dev)
+    log(f"[rank {H.rank}] generated {n} geometries ({nbytes / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
+    eng = engine_for(H)
+    d_data, d_off = DevBuf.from_numpy(eng, data), DevBuf.from_numpy(eng, off)
     g = N.KdBlobs()
-    g.n, g.data, g.off, g.mem, g.size_hint = n, d_data.data_ptr(), d_off.data_ptr(), N.KD_MEM_DEVICE, 0
-    hexbuf = torch.empty(2 * nbytes, dtype=torch.uint8, device=D.dev)
-    start = torch.empty(n, dtype=torch.int32, device=D.dev)
-    status = torch.empty(n, dtype=torch.uint8, device=D.dev)
+    g.n, g.data, g.off, g.mem, g.size_hint = n, d_data.ptr, d_off.ptr, N.KD_MEM_DEVICE, 0
+    hexbuf, start, status = DevBuf(eng, 2 * nbytes), DevBuf(eng, 4 * n), DevBuf(eng, n)
     L, ctx = eng.L, eng.ctx
 
     def step():
-        N.check(L.kd_hex_encode(ctx, ctypes.byref(g), N.KD_HEX_GPKG_WKB, hexbuf.data_ptr(), start.data_ptr(),
-                                status.data_ptr(), N.KD_MEM_DEVICE), "kd_hex_encode")
+        N.check(L.kd_hex_encode(ctx, ctypes.byref(g), N.KD_HEX_GPKG_WKB, hexbuf.ptr, start.ptr, status.ptr,
+                                N.KD_MEM_DEVICE), "kd_hex_encode")
 
     for _ in range(max(1, args.warmup)):
         step()
-    torch.cuda.synchronize()
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle import oracle as O
-
+    eng.sync()
+    O = oracle()
     if not args.no_check:  # every geometry is valid LE GPKG; sampled strings equal the oracle's
-        assert int(status.max().item()) == 0, "kd_hex_encode flagged a valid geometry"
-        st = start.cpu().numpy()
+        assert int(status.download(np.uint8, n).max()) == 0, "kd_hex_encode flagged a valid geometry"
+        st = start.download(np.uint32, n)
         for i in list(range(0, n, max(1, n // 2000))) + [n - 1]:
             o, e = int(off[i]), int(off[i + 1])
-            got = hexbuf[2 * (o + int(st[i])): 2 * e].cpu().numpy().tobytes().decode()
+            a = 2 * (o + int(st[i]))
+            got = hexbuf.download(np.uint8, 2 * e - a, offset=a).tobytes().decode()
             assert got == O.hex_wkb(data[o:e].tobytes()), f"hex WKB of geometry {i} differs from the oracle"
     eng.prof_reset()
     eng.prof_select(None if args.time_all else ["k_hex"])
     eng.prof_enable(not args.no_events)
-    cnt = torch.zeros(1, dtype=torch.int64, device=D.dev)
-    gathered = [torch.empty_like(cnt) for _ in range(D.world)]
-    elapsed = D.timed(step, args.steps, lambda: D.dist.all_gather(gathered, cnt))
+    elapsed = timed(H, eng, step, args.steps)
     eng.prof_enable(False)
-    (total,) = D.total(n)
+    total = sum(H.allgather(n))
     kern = kernel_times(eng, ("k_hex", "k_wkb_start"))
     # algorithmic bytes per k_hex launch: the geometry arena read once, two hex chars written per byte
-    alg = 3 * nbytes
-    roof = roofline(kern, "k_hex", alg, args.traffic_json, "n_geoms", n)
+    roof = roofline(kern, "k_hex", 3 * nbytes, args.traffic_json, n)
     cpu = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+    if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         m = min(n, 200_000)
         blobs = [data[int(off[i]):int(off[i + 1])].tobytes() for i in range(m)]
         t0 = time.perf_counter()
@@ -433,60 +565,47 @@ def run_c6(args, D):
                          f"(the reference's gpkg_geom_to_hex_wkb restated: slice + hexlify + upper), 1 thread"}
     eng.close()
     return {
-        "metric": METRIC,
-        "value": round(total * args.steps / elapsed / 1e6, 2),
-        "unit": "M geometries/s",
-        "n_gpus": D.world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
+        "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M geometries/s",
+        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
         "config": {"workload": f"C6 (SURVEY 8f #2, {n} geometries per GPU): hex WKB of every geometry "
                                "(Geometry.to_hex_wkb for kart diff -o json)",
                    "geoms_per_gpu": n, "points": int(is_pt.sum()), "arena_bytes": nbytes,
-                   "parallelism": f"independent shards x{D.world}"},
+                   "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
-        "roofline": roof,
-        "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu,
     }
 
 
 # ---------------------------------------------------------------------------------------------
-def run_c4(args, D):
-    torch = D.torch
+def run_c4(args, H):
     from kart_amd import synth
     from kart_amd.device import MergePipeline
-    from kart_amd.engine import Engine
 
     n = args.n
     t0 = time.time()
-    M = synth.table3_layers(n, seed=synth.SEED + D.rank)
+    M = synth.table3_layers(n, seed=synth.SEED + H.rank)
     A, O_, T = M.ancestor, M.ours, M.theirs
-    log(f"[rank {D.rank}] generated ancestor/ours/theirs {A.n}/{O_.n}/{T.n} string-pk rows in {time.time() - t0:.1f}s "
+    log(f"[rank {H.rank}] generated ancestor/ours/theirs {A.n}/{O_.n}/{T.n} string-pk rows in {time.time() - t0:.1f}s "
         f"({M.n_conflict} conflicts planned)")
-    eng = Engine(torch.cuda.current_device())
-    eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    pipe = MergePipeline(eng, A, O_, T, D.dev)
+    eng = engine_for(H)
+    pipe = MergePipeline(eng, A, O_, T)
     for _ in range(max(1, args.warmup)):
         pipe.step()
-    torch.cuda.synchronize()
+    eng.sync()
     n_clean, conf, md = pipe.results()
     if not args.no_check:  # the generator's own plan (libgit2 rule over planned edits)
         assert conf.shape[0] == M.n_conflict, (conf.shape[0], M.n_conflict)
     eng.prof_reset()
     eng.prof_select(None if args.time_all else ["k_join2"])
     eng.prof_enable(not args.no_events)
-    cnt = torch.zeros(1, dtype=torch.int64, device=D.dev)
-    gathered = [torch.empty_like(cnt) for _ in range(D.world)]
-    elapsed = D.timed(pipe.step, args.steps, lambda: D.dist.all_gather(gathered, cnt))
+    elapsed = timed(H, eng, pipe.step, args.steps)
     eng.prof_enable(False)
-    (total,) = D.total(A.n + O_.n + T.n)
-    kern = kernel_times(eng, ("k_sorted3", "k_partition2", "k_join2", "k_place2", "k_resolve3"))
     nall = A.n + O_.n + T.n
+    total = sum(H.allgather(nall))
+    kern = kernel_times(eng, ("k_sorted3", "k_partition2", "k_join2", "k_place2", "k_resolve3"))
     # classify3 = classify2(ours, theirs) + k_resolve3 over the paths where they differ.
     # Dominant kernel k_join2, algorithmic bytes per launch: every ours/theirs key + OID once (28 B),
     # every ours/theirs filename once (hash keys are verified against the names) and one 8-B record
@@ -494,12 +613,10 @@ def run_c4(args, D):
     _, io, it = np.intersect1d(O_.key, T.key, assume_unique=True, return_indices=True)
     n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((O_.oid[io] != T.oid[it]).any(axis=1)))
     alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand
-    roof = roofline(kern, "k_join2", alg, args.traffic_json, "n_rows", n)
+    roof = roofline(kern, "k_join2", alg, args.traffic_json, n)
     cpu = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from oracle import oracle as Orc
-
+    if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
+        Orc = oracle()
         t0 = time.perf_counter()
         reps = 0
         while True:
@@ -518,37 +635,29 @@ def run_c4(args, D):
                          f"1 thread"}
     eng.close()
     return {
-        "metric": METRIC,
-        "value": round(total * args.steps / elapsed / 1e6, 2),
-        "unit": "M entries/s",
-        "n_gpus": D.world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8/u64 (integer)",
+        "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M entries/s",
+        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8/u64 (integer)",
         "data": "synthetic (seeded string-PK table: MsgpackHashPathEncoder paths, synthetic OIDs)",
         "config": {"workload": f"C4: {n}-row string-PK table per GPU, three-way merge classification "
                                "(ancestor/ours/theirs join + libgit2 conflict rule)",
                    "rows_per_gpu": n, "entries_per_step": total, "conflicts": int(conf.shape[0]),
                    "merge_deltas": int(md.shape[0]), "differing_paths": n_cand,
-                   "parallelism": f"independent shards x{D.world}"},
+                   "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
-        "roofline": roof,
-        "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu,
     }
 
 
 def main():
     args = parse()
-    D = Dist()
-    out = {"c2": run_c2, "c3": lambda a, d: run_c2(a, d, polygons=True), "c4": run_c4,
-           "c5": run_c5, "c6": run_c6}[args.workload](args, D)
-    if D.rank == 0:
+    H = Harness()
+    out = {"c2": lambda a, h: run_diff(a, h, polygons=False), "c3": lambda a, h: run_diff(a, h, polygons=True),
+           "c4": run_c4, "c5": run_c5, "c6": run_c6}[args.workload](args, H)
+    if H.rank == 0:
         print(json.dumps(out), flush=True)
-    D.close()
+    H.close()
 
 
 if __name__ == "__main__":

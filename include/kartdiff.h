@@ -18,6 +18,12 @@
  *                     (vendor/spatial-filter/spatial_filter.cpp:170-260).
  *   kd_hex_encode  <- Geometry.to_hex_wkb / gpkg_geom_to_hex_wkb (kart/geometry.py:346-375) and
  *                     bytes.hex(v), as feature_as_json formats them (kart/feature_output.py:34-56).
+ *   kd_diff2_sharded / kd_diff2_gather
+ *                  <- the same diff split by dataset3 path-bucket range over several GPUs (the
+ *                     reference's own sharding idea: kart/fast_import.py:289-337), counts and
+ *                     compacted delta records all-gathered over RCCL (xGMI).
+ *   kd_malloc / kd_memcpy / kd_host_alloc ...
+ *                  device HBM and pinned host staging for callers without a GPU framework.
  *   kd_pack_*      <- Dataset3.decode_path_to_1pk / PathEncoder (kart/dataset3.py:250-259,
  *                     kart/dataset3_paths.py:202-215,292-299): host-side key packing.
  *
@@ -190,9 +196,58 @@ int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const 
 int kd_hex_encode(kd_ctx* ctx, const kd_blobs* blobs, uint32_t mode, uint8_t* hex, uint32_t* start,
                   uint8_t* status, uint32_t out_mem);
 
+/* -------- packing on the GPU (the sort that follows the leaf-path decode) -------- */
+/* Sort one side's n entries by join key on the device: an LSD radix sort over the keys' varying
+ * bits (LDS-ranked tiles, stable).  d_key [n] is sorted in place; d_order [n] <- original index of
+ * sorted entry k; d_oid [n*20] (may be NULL) is permuted in place.  *h_dup (may be NULL) <- 1 when
+ * the sorted keys are not strictly ascending (two entries share a key: the caller's fallback).
+ * Replaces the host sort of the packer (Dataset3 leaves arrive in git path order, not key order). */
+int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32_t* d_order, uint64_t n, uint32_t* h_dup);
+
+/* -------- device memory and copies (no GPU framework needed by the caller) -------- */
+#define KD_COPY_H2D 1u
+#define KD_COPY_D2H 2u
+#define KD_COPY_D2D 3u
+int kd_malloc(kd_ctx* ctx, uint64_t bytes, void** dptr);   /* HBM of the context's device      */
+int kd_mfree(kd_ctx* ctx, void* dptr);
+int kd_host_alloc(uint64_t bytes, void** hptr);            /* pinned (page-locked) host memory */
+int kd_host_free(void* hptr);
+/* asynchronous on the context stream (host buffers should be pinned for a true async copy) */
+int kd_memcpy(kd_ctx* ctx, void* dst, const void* src, uint64_t bytes, uint32_t kind);
+int kd_memset(kd_ctx* ctx, void* dst, int value, uint64_t bytes);
+int kd_device_sync(kd_ctx* ctx);                           /* hipDeviceSynchronize + profiling */
+
+/* -------- multi-GPU: bucket-range shards, RCCL all-gather -------- */
+#define KD_COMM_ID_BYTES 128
+/* One process per GPU: rank 0 makes the id, the caller broadcasts it (any channel), every rank
+ * calls kd_comm_init with it.  The library owns the communicator (RCCL, loaded at first use). */
+int kd_comm_unique_id(uint8_t id[KD_COMM_ID_BYTES]);
+int kd_comm_init(kd_ctx* ctx, int nranks, int rank, const uint8_t id[KD_COMM_ID_BYTES]);
+int kd_comm_fini(kd_ctx* ctx);
+/* d_recv[nranks * n] <- every rank's d_send[n] (device buffers, context stream) */
+int kd_allgather_u64(kd_ctx* ctx, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);
+/* One rank's step of a sharded diff: kd_diff2_device on this rank's shard (device sides holding
+ * the global sorted entries [base_off, base_off + base.n) / [target_off, ...) of one bucket range),
+ * its delta records rebased to global indices, then all-gathered with the counts:
+ *   d_all_counts / h_all_counts [nranks * 8]: rank r's inserts, updates, deletes, deltas, error word;
+ *   d_all_delta [all_cap * 2]: rank r's records at 2 * r * stride, stride = max_r deltas(r).
+ * Ranks hold consecutive bucket ranges, so the gathered records in rank order are key-ordered.
+ * One host sync (the record stride).  d_upd may be NULL. */
+int kd_diff2_gather(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint64_t base_off,
+                    uint64_t target_off, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
+                    uint64_t* d_counts, uint32_t* d_err, uint32_t* d_all_delta, uint64_t all_cap,
+                    uint64_t* d_all_counts, uint64_t* h_all_counts);
+/* One process driving g GPUs (one context each): host sides are cut into g bucket ranges of about
+ * equal entry count (bucket = the key's top bucket_bits bits: 24 for KD_KEY_INT, 6 per tree level
+ * for base64 hash paths, 8 per level for hex), each shard diffed on its GPU, and the records
+ * all-gathered over a communicator the library keeps on ctxs[0].  Result as kd_diff2. */
+int kd_diff2_sharded(kd_ctx** ctxs, int g, const kd_side* base, const kd_side* target, int bucket_bits,
+                     uint32_t flags, kd_diff_result** out);
+
 /* -------- host-side key packing (CPU, multithreaded) -------- */
-/* KD_KEY_INT: filenames b64(msgpack([pk])) -> keys.  status[i] = 0 ok / 1 not an int pk /
- * 2 pk outside [-2^63, 2^63).  Returns number of bad entries. */
+/* KD_KEY_INT: filenames b64(msgpack([pk])) -> keys (entries may be whole relative paths
+ * "c/c/c/c/<filename>": the part after the last '/' is decoded).  status[i] = 0 ok / 1 not an int
+ * pk / 2 pk outside [-2^63, 2^63).  Returns number of bad entries. */
 int64_t kd_pack_int_keys(const uint8_t* names, const uint64_t* name_off, uint64_t n,
                          uint64_t* keys, uint8_t* status);
 /* KD_KEY_HASH: "c1/../cL/<filename>" relative paths -> keys (levels, hex=0 base64 / 1 hex). */

@@ -22,6 +22,10 @@ KD_KEY_HASH = 1
 KD_DIFF_UNORDERED = 0x1
 KD_HEX_BYTES = 0
 KD_HEX_GPKG_WKB = 1
+KD_COPY_H2D = 1
+KD_COPY_D2H = 2
+KD_COPY_D2D = 3
+KD_COMM_ID_BYTES = 128
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -153,6 +157,30 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.POINTER(KdBlobs), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_void_p, ctypes.c_uint32],
     ),
+    "kd_sort_side": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p]),
+    "kd_malloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    "kd_mfree": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "kd_host_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    "kd_host_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_memcpy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]),
+    "kd_memset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]),
+    "kd_device_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "kd_comm_fini": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_allgather_u64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "kd_diff2_gather": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.c_uint64, ctypes.c_uint64,
+         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "kd_diff2_sharded": (
+        ctypes.c_int,
+        [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.c_int,
+         ctypes.c_uint32, ctypes.POINTER(ctypes.POINTER(KdDiffResult))],
+    ),
     "kd_pack_int_keys": (
         ctypes.c_int64,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
@@ -176,17 +204,11 @@ _lib = None
 
 
 def lib():
-    """Load libkartdiff.so once; raise NativeUnavailable (never silently fall back)."""
+    """Load libkartdiff.so once; raise NativeUnavailable (never silently fall back).  The library
+    needs no GPU framework: it allocates, copies and communicates itself (kd_malloc, kd_memcpy,
+    kd_comm_*)."""
     global _lib
     if _lib is None:
-        # One HIP runtime per process: torch ships its own libamdhip64/libhsa-runtime64 with the
-        # same sonames as /opt/rocm's.  Whichever loads first serves both, so load torch's first
-        # when it is installed — the device pipeline hands torch-allocated HBM and torch's stream
-        # to this library.  (Without torch, /opt/rocm's runtime is used.)
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
         if not os.path.exists(LIB_PATH):
             raise NativeUnavailable(
                 f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"

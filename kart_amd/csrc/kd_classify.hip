@@ -266,7 +266,7 @@ using namespace kd;
 
 // --------------------------------------------------------------------------------------------
 // host-form helpers
-static int stage_side(kd_ctx* ctx, const kd_side* s, const char* tag, kd_side* dev) {
+int kd::stage_side(kd_ctx* ctx, const kd_side* s, const char* tag, kd_side* dev) {
     *dev = *s;
     dev->mem = KD_MEM_DEVICE;
     std::string p(tag);
@@ -285,7 +285,7 @@ static int stage_side(kd_ctx* ctx, const kd_side* s, const char* tag, kd_side* d
     return KD_OK;
 }
 
-static int check_side(const kd_side* s, const char* which) {
+int kd::check_side(const kd_side* s, const char* which) {
     KD_CHECK(s, "%s side is NULL", which);
     KD_CHECK(s->n == 0 || (s->key && s->oid), "%s side: key/oid NULL", which);
     KD_CHECK(s->mem == KD_MEM_HOST || s->mem == KD_MEM_DEVICE, "%s side: bad mem", which);

@@ -217,6 +217,7 @@ int kd_fini(kd_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     prof_flush(ctx);
+    comm_release(ctx);
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -286,6 +287,8 @@ int64_t kd_pack_int_keys(const uint8_t* names, const uint64_t* name_off, uint64_
     u64 bad = 0;
     par_for(n, [&](u64 i) {
         u64 a = name_off[i], b = name_off[i + 1];
+        for (u64 j = b; j > a; j--)  // a relative path "c/c/c/c/<filename>": its filename
+            if (names[j - 1] == '/') { a = j; break; }
         u64 k = 0;
         int st = (b - a > 24) ? 1 : decode_int_name(names + a, (int)(b - a), &k);
         keys[i] = k;

@@ -75,6 +75,11 @@ struct kd_ctx {
     // when the next call's tables are identical)
     std::vector<uint8_t> fd_tab;
     int n_cu = 256;  // compute units (grid sizing of grid-stride kernels)
+    // multi-GPU (kd_comm.hip): this rank's communicator, and kd_diff2_sharded's per-device set
+    void* comm = nullptr;
+    int nranks = 1, rank = 0;
+    std::vector<int> group_devs;
+    std::vector<void*> group_comms;
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
 };
 
@@ -114,6 +119,11 @@ inline int launch(kd_ctx* ctx, const char* name, F&& f) {
 
 // copy a host/device side array to device (returns device pointer; device input is passed through)
 int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem, const void** dev);
+// a side's arrays staged to device scratch slots "<tag>.*" (device sides pass through); checks
+int stage_side(kd_ctx* ctx, const kd_side* s, const char* tag, kd_side* dev);
+int check_side(const kd_side* s, const char* which);
+// destroy the context's communicators (kd_fini)
+void comm_release(kd_ctx* ctx);
 
 // ---- classify2 (device form), kd_classify.hip ----
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,

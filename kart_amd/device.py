@@ -1,59 +1,107 @@
-"""Device-resident pipeline: sides and blob arenas held in HBM (torch allocations as plumbing),
-classify2 -> fielddiff launched back to back on one stream with no host round trip.
+"""Device-resident pipelines on libkartdiff's own memory API (kd_malloc / kd_memcpy): sides and blob
+arenas held in HBM, classify2 -> fielddiff launched back to back on the context stream with no host
+round trip.  No GPU framework is involved.
 
 This is the path bench.py times: inputs already resident, outputs stay resident (the delta list,
-update list, per-update changed-field masks).  torch only allocates memory and provides the
-stream; every kernel is libkartdiff's.
+update list, per-update changed-field masks).
 """
 import ctypes
 
 import numpy as np
-import torch
 
 from . import _native as N
 
 
-def to_dev(a, device):
-    """numpy -> torch device tensor with the same bytes (uint64 stored as int64)"""
-    a = np.ascontiguousarray(a)
-    if a.dtype == np.uint64:
-        a = a.view(np.int64)
-    elif a.dtype == np.uint32:
-        a = a.view(np.int32)
-    t = torch.from_numpy(a)
-    return t.to(device, non_blocking=False)
+class DevBuf:
+    """One HBM allocation of the engine's device (freed with the object or by ``free()``)."""
+
+    def __init__(self, engine, nbytes):
+        self.eng = engine
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        N.check(engine.L.kd_malloc(engine.ctx, max(self.nbytes, 16), ctypes.byref(p)), "kd_malloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_numpy(cls, engine, a):
+        """device copy of a numpy array (synchronous; pinned staging is the caller's choice)"""
+        a = np.ascontiguousarray(a)
+        b = cls(engine, a.nbytes)
+        b.upload(a)
+        return b
+
+    def upload(self, a, offset=0, sync=True):
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        if a.nbytes:
+            N.check(self.eng.L.kd_memcpy(self.eng.ctx, self.ptr + offset, a.ctypes.data, a.nbytes, N.KD_COPY_H2D),
+                    "kd_memcpy H2D")
+            if sync:
+                self.eng.sync()
+
+    def download(self, dtype, count, offset=0):
+        """host numpy copy of `count` items of `dtype` at byte `offset` (synchronous)"""
+        dt = np.dtype(dtype)
+        out = np.empty(int(count), dt)
+        if out.nbytes:
+            assert offset + out.nbytes <= self.nbytes
+            N.check(self.eng.L.kd_memcpy(self.eng.ctx, out.ctypes.data, self.ptr + offset, out.nbytes, N.KD_COPY_D2H),
+                    "kd_memcpy D2H")
+            self.eng.sync()
+        return out
+
+    def zero(self):
+        N.check(self.eng.L.kd_memset(self.eng.ctx, self.ptr, 0, self.nbytes), "kd_memset")
+
+    def free(self):
+        if self.ptr and self.eng.ctx:
+            self.eng.L.kd_mfree(self.eng.ctx, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _nonempty(a, dtype, width=1):
+    return a if a is not None and a.size else np.zeros(width, dtype)
 
 
 class DevSide:
-    def __init__(self, side, device):
+    """A PackedSide's arrays in HBM."""
+
+    def __init__(self, engine, side):
         self.n = side.n
         self.key_mode = side.key_mode
-        self.key = to_dev(side.key if side.n else np.zeros(1, np.uint64), device)
-        self.oid = to_dev(side.oid.reshape(-1) if side.n else np.zeros(20, np.uint8), device)
+        self.key = DevBuf.from_numpy(engine, _nonempty(side.key, np.uint64))
+        self.oid = DevBuf.from_numpy(engine, _nonempty(side.oid.reshape(-1) if side.n else None, np.uint8, 20))
         self.name = self.name_off = None
         if side.name is not None:
-            self.name = to_dev(side.name if side.name.size else np.zeros(1, np.uint8), device)
-            self.name_off = to_dev(side.name_off, device)
+            self.name = DevBuf.from_numpy(engine, _nonempty(side.name, np.uint8))
+            self.name_off = DevBuf.from_numpy(engine, side.name_off)
 
     def kd_side(self):
         s = N.KdSide()
         s.n = self.n
-        s.key = self.key.data_ptr()
-        s.oid = self.oid.data_ptr()
-        s.name = self.name.data_ptr() if self.name is not None else None
-        s.name_off = self.name_off.data_ptr() if self.name_off is not None else None
+        s.key = self.key.ptr
+        s.oid = self.oid.ptr
+        s.name = self.name.ptr if self.name is not None else None
+        s.name_off = self.name_off.ptr if self.name_off is not None else None
         s.mem = N.KD_MEM_DEVICE
         s.key_mode = self.key_mode
         return s
 
 
 class DevBlobs:
-    def __init__(self, data, off, device):
+    """A blob arena (uint8 data, uint64 off[n+1]) in HBM."""
+
+    def __init__(self, engine, data, off):
         self.n = int(off.shape[0]) - 1
-        self.data = to_dev(data if data.size else np.zeros(1, np.uint8), device)
-        self.off = to_dev(off, device)
+        self.data = DevBuf.from_numpy(engine, _nonempty(data, np.uint8))
+        self.off = DevBuf.from_numpy(engine, off)
         self.nbytes = int(data.size)
-        self.max_len = int((off[1:] - off[:-1]).max()) if self.n else 0
         # typical blob = mean over the non-empty blobs (an arena may hold only the blobs a diff reads)
         nz = int(np.count_nonzero(off[1:] != off[:-1])) if self.n else 0
         self.mean_len = int((int(off[-1]) - int(off[0]) + nz - 1) // nz) if nz else 0
@@ -61,84 +109,122 @@ class DevBlobs:
     def kd_blobs(self):
         b = N.KdBlobs()
         b.n = self.n
-        b.data = self.data.data_ptr()
-        b.off = self.off.data_ptr()
+        b.data = self.data.ptr
+        b.off = self.off.ptr
         b.mem = N.KD_MEM_DEVICE
-        b.size_hint = min(self.mean_len, 0xFFFFFFFF)  # typical (mean) blob size: sizes the LDS pool
+        b.size_hint = min(self.mean_len, 0xFFFFFFFF)  # typical (mean) blob size: picks the window shape
         return b
 
 
 class DiffPipeline:
-    """classify2 + fused-by-stream fielddiff over device-resident sides (one GPU)."""
+    """classify2 + fielddiff over device-resident sides (one GPU), back to back on one stream.
 
-    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, device, ordered=True):
+    ``gather=(base_off, target_off)``: this GPU holds one bucket-range shard of a larger diff (its
+    entries start at those global sorted indices); each step then runs kd_diff2_gather — the shard's
+    join, its delta records rebased to global indices and all-gathered with every rank's counts over
+    the library's RCCL communicator (``engine.comm_init`` first) — and field-diffs the shard's own
+    updates."""
+
+    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, ordered=True, gather=None):
         self.eng = engine
         self.flags = 0 if ordered else N.KD_DIFF_UNORDERED
-        self.device = device
-        self.A = DevSide(base, device)
-        self.B = DevSide(target, device)
-        self.OB = DevBlobs(*base_blobs, device)
-        self.NB = DevBlobs(*target_blobs, device)
+        self.A = DevSide(engine, base)
+        self.B = DevSide(engine, target)
+        self.OB = DevBlobs(engine, *base_blobs)
+        self.NB = DevBlobs(engine, *target_blobs)
         self.maps = maps
         cap = base.n + target.n + 1
         self.cap_upd = min(base.n, target.n)  # updates <= matched keys
-        self.delta = torch.empty(2 * cap, dtype=torch.int32, device=device)
-        self.upd = torch.empty(2 * cap, dtype=torch.int32, device=device)
-        self.counts = torch.zeros(8, dtype=torch.int64, device=device)  # [0..3] counts, [4] err
-        self.masks = torch.empty(cap * maps.words, dtype=torch.int64, device=device)
-        self.status = torch.empty(cap, dtype=torch.uint8, device=device)
+        self.delta = DevBuf(engine, 8 * cap)
+        self.upd = DevBuf(engine, 8 * cap)
+        self.counts = DevBuf(engine, 64)  # [0..3] counts, [4] error word
+        self.counts.zero()
+        self.masks = DevBuf(engine, 8 * cap * maps.words)
+        self.status = DevBuf(engine, cap)
         self._sa, self._sb = self.A.kd_side(), self.B.kd_side()
         self._ob, self._nb = self.OB.kd_blobs(), self.NB.kd_blobs()
         self._km = maps.kd_maps()
+        self.gather = gather
+        if gather is not None:
+            self.world = engine.nranks
+            self.all_counts = DevBuf(engine, 64 * self.world)
+            self.h_counts = np.zeros(8 * self.world, np.uint64)
+            self.all_cap = cap * self.world  # until reserve_gather() knows the largest shard's deltas
+            self.all_delta = DevBuf(engine, 8 * self.all_cap)
         engine.reserve(max(base.n, target.n))
+        engine.sync()
+
+    def reserve_gather(self, max_deltas_per_rank):
+        """size the gathered-record buffer for at most this many deltas on any rank"""
+        self.all_delta.free()
+        self.all_cap = max(int(max_deltas_per_rank), 1) * self.world
+        self.all_delta = DevBuf(self.eng, 8 * self.all_cap)
 
     def step(self):
         L, ctx = self.eng.L, self.eng.ctx
-        err_ptr = self.counts.data_ptr() + 4 * 8
-        N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.data_ptr(),
-                                  self.upd.data_ptr(), self.counts.data_ptr(), err_ptr), "kd_diff2_device")
-        N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.data_ptr(), self.cap_upd,
-                               ctypes.cast(self.counts.data_ptr() + 8, N.c_u64p), N.KD_MEM_DEVICE,
-                               ctypes.byref(self._km), self.masks.data_ptr(), self.status.data_ptr(),
-                               N.KD_MEM_DEVICE), "kd_fielddiff")
+        if self.gather is None:
+            N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.ptr,
+                                      self.upd.ptr, self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
+        else:
+            N.check(L.kd_diff2_gather(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.gather[0], self.gather[1],
+                                      self.flags, self.delta.ptr, self.upd.ptr, self.counts.ptr, self.counts.ptr + 32,
+                                      self.all_delta.ptr, self.all_cap, self.all_counts.ptr, self.h_counts.ctypes.data),
+                    "kd_diff2_gather")
+        N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.ptr, self.cap_upd,
+                               ctypes.cast(self.counts.ptr + 8, N.c_u64p), N.KD_MEM_DEVICE,
+                               ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE), "kd_fielddiff")
 
     def results(self):
-        """host copies (after a sync): counts dict, delta [n,2], upd [m,2], masks, status"""
-        c = self.counts.cpu().numpy()
+        """host copies (synchronous): counts dict, delta [n,2], upd [m,2], masks, status"""
+        c = self.counts.download(np.uint64, 8)
         if c[4]:
             raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flag {int(c[4])}")
         nd, nu = int(c[3]), int(c[1])
-        delta = self.delta[: 2 * nd].cpu().numpy().view(np.uint32).reshape(nd, 2)
-        upd = self.upd[: 2 * nu].cpu().numpy().view(np.uint32).reshape(nu, 2)
-        masks = self.masks[: nu * self.maps.words].cpu().numpy().view(np.uint64).reshape(nu, self.maps.words)
-        status = self.status[:nu].cpu().numpy()
+        delta = self.delta.download(np.uint32, 2 * nd).reshape(nd, 2)
+        upd = self.upd.download(np.uint32, 2 * nu).reshape(nu, 2)
+        masks = self.masks.download(np.uint64, nu * self.maps.words).reshape(nu, self.maps.words)
+        status = self.status.download(np.uint8, nu)
         return {"inserts": int(c[0]), "updates": nu, "deletes": int(c[2]), "deltas": nd}, delta, upd, masks, status
+
+    def gathered(self):
+        """(gather mode, after a step + sync) the whole diff: global delta records in key order and
+        the summed counts of every rank"""
+        c = self.h_counts.reshape(self.world, 8)
+        if c[:, 4].any():
+            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flags {c[:, 4].tolist()}")
+        stride = int(c[:, 3].max())
+        rec = self.all_delta.download(np.uint32, 2 * stride * self.world).reshape(self.world, stride, 2)
+        delta = np.concatenate([rec[r, :int(c[r, 3])] for r in range(self.world)]) if stride else np.zeros((0, 2), np.uint32)
+        return {"inserts": int(c[:, 0].sum()), "updates": int(c[:, 1].sum()), "deletes": int(c[:, 2].sum()),
+                "deltas": int(c[:, 3].sum())}, delta
 
 
 class MergePipeline:
     """classify3 (three-way merge classification) over device-resident sides (one GPU)."""
 
-    def __init__(self, engine, ancestor, ours, theirs, device):
+    def __init__(self, engine, ancestor, ours, theirs):
         self.eng = engine
-        self.S = [DevSide(x, device) for x in (ancestor, ours, theirs)]
+        self.S = [DevSide(engine, x) for x in (ancestor, ours, theirs)]
         self._s = [x.kd_side() for x in self.S]
         na, no, nt = ancestor.n, ours.n, theirs.n
-        self.conf = torch.empty(3 * (na + no + nt + 1), dtype=torch.int32, device=device)
-        self.md = torch.empty(2 * (no + nt + 1), dtype=torch.int32, device=device)
-        self.counts = torch.zeros(8, dtype=torch.int64, device=device)  # [0..3] counts, [4] err
+        self.conf = DevBuf(engine, 12 * (na + no + nt + 1))
+        self.md = DevBuf(engine, 8 * (no + nt + 1))
+        self.counts = DevBuf(engine, 64)  # [0..3] counts, [4] error word
+        self.counts.zero()
+        engine.sync()
 
     def step(self):
         L, ctx = self.eng.L, self.eng.ctx
         N.check(L.kd_merge3_device(ctx, ctypes.byref(self._s[0]), ctypes.byref(self._s[1]), ctypes.byref(self._s[2]), 0,
-                                   self.conf.data_ptr(), self.md.data_ptr(), self.counts.data_ptr(),
-                                   self.counts.data_ptr() + 4 * 8), "kd_merge3_device")
+                                   self.conf.ptr, self.md.ptr, self.counts.ptr, self.counts.ptr + 32),
+                "kd_merge3_device")
 
     def results(self):
-        """host copies (after a sync): n_clean, conflicts [n,3], merge deltas [m,2]"""
-        c = self.counts.cpu().numpy()
+        """host copies (synchronous): n_clean, conflicts [n,3], merge deltas [m,2]"""
+        c = self.counts.download(np.uint64, 8)
         if c[4]:
             raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flag {int(c[4])}")
         nc, nm = int(c[1]), int(c[2])
-        conf = self.conf[: 3 * nc].cpu().numpy().view(np.uint32).reshape(nc, 3)
-        md = self.md[: 2 * nm].cpu().numpy().view(np.uint32).reshape(nm, 2)
+        conf = self.conf.download(np.uint32, 3 * nc).reshape(nc, 3)
+        md = self.md.download(np.uint32, 2 * nm).reshape(nm, 2)
         return int(c[0]), conf, md

@@ -1,8 +1,8 @@
 """Engine: one libkartdiff context per GPU, with numpy-in / numpy-out calls.
 
 Every method goes through the HIP library; there is no CPU implementation here.  Device-resident
-pipelines (bench.py) use ``libkartdiff`` through torch-allocated device buffers instead
-(see ``kart_amd.device``).
+pipelines (bench.py) keep their buffers in HBM through the library's own allocator
+(``kart_amd.device``).
 """
 import ctypes
 from dataclasses import dataclass
@@ -66,6 +66,25 @@ class Engine:
     def sync(self):
         N.check(self.L.kd_sync(self.ctx), "kd_sync")
 
+    def device_sync(self):
+        """hipDeviceSynchronize (every stream of the device) + profiling flush"""
+        N.check(self.L.kd_device_sync(self.ctx), "kd_device_sync")
+
+    # ---- multi-GPU (RCCL owned by the library) ---------------------------------------------
+    @staticmethod
+    def comm_unique_id():
+        buf = (ctypes.c_uint8 * N.KD_COMM_ID_BYTES)()
+        N.check(N.lib().kd_comm_unique_id(buf), "kd_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (ctypes.c_uint8 * N.KD_COMM_ID_BYTES).from_buffer_copy(uid)
+        N.check(self.L.kd_comm_init(self.ctx, int(nranks), int(rank), buf), "kd_comm_init")
+        self.nranks, self.rank = int(nranks), int(rank)
+
+    def comm_fini(self):
+        N.check(self.L.kd_comm_fini(self.ctx), "kd_comm_fini")
+
     def reserve(self, max_entries, max_updates=0):
         N.check(self.L.kd_reserve(self.ctx, int(max_entries), int(max_updates)), "kd_reserve")
 
@@ -100,6 +119,25 @@ class Engine:
             return Diff2Result(int(r.n_insert), nu, int(r.n_delete), delta, upd)
         finally:
             self.L.kd_free(res)
+
+    @staticmethod
+    def diff2_sharded(engines, base, target, bucket_bits, flags=0) -> Diff2Result:
+        """One process, len(engines) GPUs: kd_diff2_sharded cuts base/target (host PackedSides) into
+        bucket ranges, diffs each on its GPU and all-gathers the records over RCCL."""
+        ctxs = (ctypes.c_void_p * len(engines))(*[e.ctx.value for e in engines])
+        sa, sb = base.kd_side(), target.kd_side()
+        L = engines[0].L
+        res = ctypes.POINTER(N.KdDiffResult)()
+        N.check(L.kd_diff2_sharded(ctxs, len(engines), ctypes.byref(sa), ctypes.byref(sb), int(bucket_bits), flags,
+                                   ctypes.byref(res)), "kd_diff2_sharded")
+        try:
+            r = res.contents
+            nd, nu = int(r.n_delta), int(r.n_update)
+            delta = np.ctypeslib.as_array(r.delta, (nd * 2,)).reshape(nd, 2).copy() if nd else np.zeros((0, 2), np.uint32)
+            upd = np.ctypeslib.as_array(r.upd, (nu * 2,)).reshape(nu, 2).copy() if nu else np.zeros((0, 2), np.uint32)
+            return Diff2Result(int(r.n_insert), nu, int(r.n_delete), delta, upd)
+        finally:
+            L.kd_free(res)
 
     def fielddiff(self, old_data, old_off, new_data, new_off, pairs, maps):
         """Blob arenas (uint8 data, uint64 off[n+1]) per side; pairs uint32 [n, 2] (old blob,

@@ -59,17 +59,6 @@ def _arena(strings):
     return data, off
 
 
-def basenames(paths, path_off):
-    """Filename start offsets inside a relative-path arena ('c/c/c/c/<name>')."""
-    n = len(path_off) - 1
-    starts = np.empty(n, np.uint64)
-    for i in range(n):
-        a, b = int(path_off[i]), int(path_off[i + 1])
-        j = paths[a:b].tobytes().rfind(b"/")
-        starts[i] = a + j + 1
-    return starts
-
-
 @dataclass
 class PackedSide:
     """Key-sorted side arrays (host memory).  ``order[k]`` = index of sorted entry k in the
@@ -82,6 +71,7 @@ class PackedSide:
     name: Optional[np.ndarray] = None  # uint8 arena (KD_KEY_HASH: relative paths, sorted order)
     name_off: Optional[np.ndarray] = None  # uint64 [n+1]
     encoding: PathEncoding = field(default_factory=lambda: INT_PK_ENCODING)
+    dev: Optional[tuple] = None  # (key, oid) DevBufs when the side was packed on the GPU
 
     @property
     def n(self):
@@ -90,6 +80,10 @@ class PackedSide:
     def kd_side(self):
         s = N.KdSide()
         s.n = self.n
+        if self.dev is not None and self.key_mode == N.KD_KEY_INT:  # already in HBM (GPU pack)
+            s.key, s.oid, s.mem, s.key_mode = self.dev[0].ptr, self.dev[1].ptr, N.KD_MEM_DEVICE, self.key_mode
+            s.name = s.name_off = None
+            return s
         s.key = N.ptr(self.key)
         s.oid = N.ptr(self.oid)
         s.name = N.ptr(self.name) if self.name is not None and self.name.size else None
@@ -108,51 +102,85 @@ class PackError(ValueError):
     pass
 
 
-def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None):
+def parse_keys(paths, off, encoding: PathEncoding):
+    """join keys of a relative-path arena, in arena order (native, multithreaded); PackError on a
+    path the encoding cannot pack"""
+    n = len(off) - 1
+    keys = np.empty(n, np.uint64)
+    status = np.empty(n, np.uint8)
+    L = N.lib()
+    pp = N.ptr(paths) if paths.size else N.ptr(np.zeros(1, np.uint8))
+    if encoding.key_mode == N.KD_KEY_INT:  # the native packer decodes each path's filename
+        bad = L.kd_pack_int_keys(pp, N.ptr(off), n, N.ptr(keys), N.ptr(status))
+    else:
+        hex_ = 1 if encoding.encoding == "hex" else 0
+        if (hex_ and encoding.branches != 256) or (not hex_ and encoding.branches != 64):
+            raise PackError(f"unsupported path structure {encoding}")
+        bad = L.kd_pack_hash_keys(pp, N.ptr(off), n, encoding.levels, hex_, N.ptr(keys), N.ptr(status))
+    if bad < 0:
+        N.check(int(bad), "pack")
+    if bad:
+        i = int(np.nonzero(status)[0][0])
+        raise PackError(f"{bad} feature paths not packable, first: {paths[int(off[i]):int(off[i+1])].tobytes()!r}")
+    return keys
+
+
+def sort_on_device(engine, keys, oids):
+    """GPU pack: (arena-order keys, oids) -> device-resident sorted side (kd_sort_side, LDS-ranked
+    LSD radix sort) + host copies (sorted keys, sorted oids, order).  PackError on duplicate keys."""
+    import ctypes
+
+    from .device import DevBuf
+
+    n = keys.shape[0]
+    dk = DevBuf.from_numpy(engine, keys if n else np.zeros(1, np.uint64))
+    do = DevBuf.from_numpy(engine, oids.reshape(-1) if n else np.zeros(20, np.uint8))
+    dord = DevBuf(engine, 4 * max(n, 1))
+    dup = ctypes.c_uint32(0)
+    N.check(engine.L.kd_sort_side(engine.ctx, dk.ptr, do.ptr, dord.ptr, n, ctypes.byref(dup)), "kd_sort_side")
+    if dup.value:
+        raise PackError("duplicate join keys within one side")
+    return dk, do, dord
+
+
+def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None, engine=None):
     """Pack leaves: rel_paths = list[str] (relative to feature/) or a uint8 arena with
     ``rel_off``; oids = uint8 [n, 20].  Returns PackedSide.  Raises PackError on paths that are
-    not valid for the encoding (the caller falls back to the reference path)."""
+    not valid for the encoding (the caller falls back to the reference path).
+
+    With an ``engine`` the sort runs on the GPU (kd_sort_side) and the side keeps its device copy
+    (``side.dev``), which the engine's diffs then use without another upload."""
     if rel_off is None:
         paths, off = _arena(rel_paths)
     else:
         paths, off = np.ascontiguousarray(rel_paths, np.uint8), np.ascontiguousarray(rel_off, np.uint64)
     n = len(off) - 1
     oids = np.ascontiguousarray(oids, np.uint8).reshape(n, 20)
-    keys = np.empty(n, np.uint64)
-    status = np.empty(n, np.uint8)
-    L = N.lib()
-    if encoding.key_mode == N.KD_KEY_INT:
-        starts = basenames(paths, off)
-        # contiguous filename arena for the native packer
-        names = [paths[int(starts[i]):int(off[i + 1])].tobytes() for i in range(n)]
-        nd, noff = _arena(names)
-        bad = L.kd_pack_int_keys(N.ptr(nd) if nd.size else None, N.ptr(noff), n, N.ptr(keys), N.ptr(status))
+    keys = parse_keys(paths, off, encoding)
+    dev = None
+    if engine is not None:
+        dk, do, dord = sort_on_device(engine, keys, oids)
+        keys = dk.download(np.uint64, n)
+        order = dord.download(np.uint32, n).astype(np.int64)
+        sorted_oids = do.download(np.uint8, 20 * n).reshape(n, 20)
+        dev = (dk, do)
     else:
-        hex_ = 1 if encoding.encoding == "hex" else 0
-        glen = 2 if hex_ else 1
-        levels = encoding.levels if encoding.branches in (64, 256) else encoding.levels
-        if (hex_ and encoding.branches != 256) or (not hex_ and encoding.branches != 64):
-            raise PackError(f"unsupported path structure {encoding}")
-        del glen
-        bad = L.kd_pack_hash_keys(N.ptr(paths) if paths.size else None, N.ptr(off), n, levels, hex_,
-                                  N.ptr(keys), N.ptr(status))
-    if bad < 0:
-        N.check(int(bad), "pack")
-    if bad:
-        i = int(np.nonzero(status)[0][0])
-        raise PackError(f"{bad} feature paths not packable, first: {paths[int(off[i]):int(off[i+1])].tobytes()!r}")
-    order = np.argsort(keys, kind="stable")
-    keys = keys[order]
-    if n > 1 and not np.all(keys[1:] > keys[:-1]):
-        raise PackError("duplicate join keys within one side")
-    side = PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(oids[order]),
+        order = np.argsort(keys, kind="stable")
+        keys = keys[order]
+        if n > 1 and not np.all(keys[1:] > keys[:-1]):
+            raise PackError("duplicate join keys within one side")
+        sorted_oids = oids[order]
+    side = PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(sorted_oids),
                       key_mode=encoding.key_mode, order=order.astype(np.int64), encoding=encoding)
+    side.dev = dev
     if encoding.key_mode == N.KD_KEY_HASH:
         # sorted relative-path arena (needed for collision verification + pk decode)
         lens = (off[1:] - off[:-1])[order]
         noff = np.zeros(n + 1, np.uint64)
         noff[1:] = np.cumsum(lens)
-        idx = np.concatenate([np.arange(int(off[i]), int(off[i + 1])) for i in order]) if n else np.zeros(0, np.int64)
+        # byte j of sorted path k comes from off[order[k]] + j: one vectorised gather
+        lens_i = lens.astype(np.int64)
+        idx = np.arange(int(noff[-1]), dtype=np.int64) + np.repeat(off[:-1][order].astype(np.int64) - noff[:-1].astype(np.int64), lens_i)
         side.name = np.ascontiguousarray(paths[idx]) if n else np.zeros(0, np.uint8)
         side.name_off = noff
     return side

@@ -7,8 +7,8 @@ shards.  The join key's top bits *are* the bucket (packing.py), so a cut on buck
 
 The cuts balance ``n_base + n_target`` per shard (the same idea as the reference's parallel
 import, kart/fast_import.py:289-337, at bucket granularity).  After the per-shard diffs the only
-exchange is an all-gather of each shard's counts and compacted delta records (RCCL over xGMI on
-GPUs, gloo on CPU).
+exchange is an all-gather of each shard's counts and compacted delta records: on GPUs inside the
+library over RCCL (xGMI), ``ShardRank`` / ``Engine.diff2_sharded``; on CPU (tests) over gloo.
 """
 import numpy as np
 
@@ -75,12 +75,14 @@ def rank_pk_base(rank, n_per_rank):
     return base
 
 
-def diff2_sharded(base, target, shards, run_shard, rank=0, world=1, group=None):
+def diff2_sharded(base, target, shards, run_shard, rank=0, world=1, exchange=None):
     """Split (base, target) into ``shards`` bucket ranges, run ``run_shard(b, t) -> Diff2Result``
-    on the shards this rank owns (shard s -> rank s % world), and all-gather results.
+    on the shards this rank owns (shard s -> rank s % world), and gather the results.
 
     Returns the merged (delta [n,2] in global sorted indices, counts) on every rank.  With
-    world > 1 ``torch.distributed`` must be initialised (nccl on GPUs, gloo on CPU)."""
+    world > 1, ``exchange(local) -> list`` all-gathers the per-shard ``(shard id, records,
+    (inserts, updates, deletes))`` tuples of every rank (the GPU path does this inside the library
+    over RCCL: ``ShardRank``; CPU tests pass a gloo all-gather)."""
     bits = bucket_bits(base.key_mode, base.encoding)
     cuts = cut_points([base.key, target.key], shards, bits)
     ba, tb = slice_bounds(base.key, cuts, bits), slice_bounds(target.key, cuts, bits)
@@ -96,51 +98,74 @@ def diff2_sharded(base, target, shards, run_shard, rank=0, world=1, group=None):
         local.append((s, np.stack([da, db], 1).astype(np.uint32) if d.size else np.zeros((0, 2), np.uint32),
                       (r.n_insert, r.n_update, r.n_delete)))
     if world > 1:
-        local = _all_gather(local, group)
+        if exchange is None:
+            raise ValueError("world > 1 needs an exchange (all-gather) callable")
+        local = exchange(local)
     local.sort(key=lambda x: x[0])
     delta = np.concatenate([x[1] for x in local]) if local else np.zeros((0, 2), np.uint32)
     c = np.sum([x[2] for x in local], axis=0) if local else np.zeros(3, np.int64)
     return delta, {"inserts": int(c[0]), "updates": int(c[1]), "deletes": int(c[2])}
 
 
-def _all_gather(local, group):
-    """all-gather of per-shard (id, delta records, counts): counts first, then records padded to
-    the max count (RCCL has no all-gatherv)."""
-    import torch
-    import torch.distributed as dist
+class ShardRank:
+    """One rank (one GPU, one process) of a bucket-range sharded two-way diff.
 
-    world = dist.get_world_size(group)
-    backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    flat = [(s, d, c) for s, d, c in local]
-    hdr = torch.tensor([len(flat)] + [int(d.shape[0]) for _, d, _ in flat] + [0] * 0, dtype=torch.int64)
-    n_local = torch.tensor([len(flat), sum(int(d.shape[0]) for _, d, _ in flat)], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, n_local, group=group)
-    max_sh = max(int(x[0]) for x in sizes)
-    max_rec = max(int(x[1]) for x in sizes)
-    # per-shard headers: id, n_records, inserts, updates, deletes
-    h = torch.zeros((max(max_sh, 1), 5), dtype=torch.int64, device=dev)
-    recs = torch.zeros((max(max_rec, 1), 2), dtype=torch.int64, device=dev)
-    pos = 0
-    for i, (s, d, c) in enumerate(flat):
-        h[i] = torch.tensor([s, d.shape[0], c[0], c[1], c[2]], dtype=torch.int64)
-        if d.shape[0]:
-            recs[pos:pos + d.shape[0]] = torch.from_numpy(d.astype(np.int64)).to(dev)
-        pos += d.shape[0]
-    hs = [torch.empty_like(h) for _ in range(world)]
-    rs = [torch.empty_like(recs) for _ in range(world)]
-    dist.all_gather(hs, h, group=group)
-    dist.all_gather(rs, recs, group=group)
-    out = []
-    for r in range(world):
-        nsh = int(sizes[r][0])
-        hr = hs[r].cpu().numpy()
-        rr = rs[r].cpu().numpy()
-        p = 0
-        for i in range(nsh):
-            s, nrec, ci, cu, cd = (int(x) for x in hr[i])
-            out.append((s, rr[p:p + nrec].astype(np.uint32), (ci, cu, cd)))
-            p += nrec
-    del hdr
-    return out
+    The rank holds its slice of both sides in HBM (``base`` / ``target`` PackedSides of the rank's
+    bucket range, starting at global sorted indices ``base_off`` / ``target_off``); ``step()`` runs
+    kd_diff2_gather: the device join of the slice, its delta records rebased to global indices, and
+    the all-gather of every rank's counts and records over the library's RCCL communicator
+    (``engine.comm_init`` first).  The gathered records, in rank order, are the whole diff in key
+    order."""
+
+    def __init__(self, engine, base, target, base_off, target_off, flags=0):
+        from .device import DevBuf, DevSide
+
+        self.eng = engine
+        self.flags = flags
+        self.world = engine.nranks
+        self.A, self.B = DevSide(engine, base), DevSide(engine, target)
+        self._sa, self._sb = self.A.kd_side(), self.B.kd_side()
+        self.base_off, self.target_off = int(base_off), int(target_off)
+        cap = base.n + target.n + 1
+        self.cap = cap
+        self.delta = DevBuf(engine, 8 * cap)
+        self.upd = DevBuf(engine, 8 * cap)
+        self.counts = DevBuf(engine, 64)
+        self.counts.zero()
+        self.all_counts = DevBuf(engine, 64 * self.world)
+        self.h_counts = np.zeros(8 * self.world, np.uint64)
+        self.all_cap = 0
+        self.all_delta = None
+        engine.reserve(max(base.n, target.n))
+        engine.sync()
+
+    def reserve_gather(self, max_deltas_per_rank):
+        """size the gathered-record buffer for up to this many deltas on any rank"""
+        need = int(max_deltas_per_rank) * self.world
+        if need > self.all_cap:
+            from .device import DevBuf
+
+            self.all_delta = DevBuf(self.eng, 8 * max(need, 1))
+            self.all_cap = need
+
+    def step(self):
+        import ctypes
+
+        if self.all_delta is None:
+            self.reserve_gather(self.cap)
+        N.check(self.eng.L.kd_diff2_gather(
+            self.eng.ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.base_off, self.target_off, self.flags,
+            self.delta.ptr, self.upd.ptr, self.counts.ptr, self.counts.ptr + 32, self.all_delta.ptr, self.all_cap,
+            self.all_counts.ptr, self.h_counts.ctypes.data), "kd_diff2_gather")
+
+    def results(self):
+        """(delta [n, 2] global sorted indices in key order, counts) of the whole diff (sync)"""
+        self.eng.sync()
+        c = self.h_counts.reshape(self.world, 8)
+        if c[:, 4].any():
+            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flags {c[:, 4].tolist()}")
+        stride = int(c[:, 3].max()) if self.world else 0
+        allrec = self.all_delta.download(np.uint32, 2 * stride * self.world).reshape(self.world, stride, 2)
+        delta = np.concatenate([allrec[r, :int(c[r, 3])] for r in range(self.world)]) if stride else \
+            np.zeros((0, 2), np.uint32)
+        return delta, {"inserts": int(c[:, 0].sum()), "updates": int(c[:, 1].sum()), "deletes": int(c[:, 2].sum())}

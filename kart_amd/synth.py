@@ -202,7 +202,7 @@ def polygon_blobs(pk, gver, aver, legend_hex, rng_seed=SEED):
     np.cumsum(blen, out=off[1:])
     if n == 0:
         return np.zeros(0, np.uint8), off
-    W = int(blen.max())
+    W = int(blen.max()) + 16  # slack: a group's 16 reference chars are written before its length cut
     mat = np.zeros((n, W), np.uint8)
     lon = -180.0 + (hg & np.uint64(0xFFFFFF)).astype(np.float64) / float(1 << 24) * 359.0
     lat = -85.0 + ((hg >> np.uint64(24)) & np.uint64(0xFFFFFF)).astype(np.float64) / float(1 << 24) * 169.0
@@ -273,41 +273,49 @@ def _sparse_arena(n, sel, data, off_sel):
     return data, off
 
 
-def polygons_layer(n, frac_geom=0.04, frac_attr=0.04, frac_delete=0.01, frac_insert=0.01, seed=SEED, pk0=0,
-                   batch=1 << 20):
-    """C3: n int-PK MULTIPOLYGON features, 10 % edits = 4 % geometry updates + 4 % attribute updates
-    + 1 % deletes + 1 % inserts.  Feature blobs are materialised for the updated
-    features only (both versions): the diff reads no other blob — classification needs only keys and
-    OIDs — so every other entry has a zero-length blob in the arena."""
-    rng = np.random.default_rng(seed)
+C3_SEED = 0x43334C59  # edit selection of the C3 layer (a hash of the pk: any pk range is generable alone)
+
+
+def c3_plan(pk, n, seed=C3_SEED):
+    """Edit class of base pks (0 unchanged, 1 geometry update, 2 attribute update, 3 delete): a seeded
+    hash of the pk, 4 % / 4 % / 1 % in expectation (10 % edits with the 1 % inserts)."""
+    h = splitmix64(np.asarray(pk, np.int64).view(np.uint64) ^ np.uint64(seed)) % np.uint64(10000)
+    return np.where(h < 400, 1, np.where(h < 800, 2, np.where(h < 900, 3, 0))).astype(np.uint8)
+
+
+def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20):
+    """C3: n int-PK MULTIPOLYGON features (pks 0..n-1) and n // 100 inserts (pks n..), 10 % edits =
+    4 % geometry updates + 4 % attribute updates + 1 % deletes + 1 % inserts, edits
+    picked by a hash of the pk (c3_plan).
+
+    ``lo, hi``: generate only the pks in [lo, hi) — a contiguous range of whole 64-pk leaf buckets
+    is one bucket-range shard of the same layer (bench.py --gpus N splits it this way).
+    Feature blobs are materialised for the updated features only (both versions): the diff reads no
+    other blob — classification needs only keys and OIDs — so every other entry has a zero-length
+    blob in the arena."""
     schema = Schema.from_column_dicts(POLYGON_SCHEMA)
     legend = Legend(["p-fid"], [c["id"] for c in POLYGON_SCHEMA[1:]])
     lh = legend.hexhash()
-    pks = np.arange(pk0, pk0 + n, dtype=np.int64)
-    n_g, n_a = int(n * frac_geom), int(n * frac_attr)
-    n_del, n_ins = int(n * frac_delete), int(n * frac_insert)
-    perm = rng.permutation(n)
-    g_i, a_i = np.sort(perm[:n_g]), np.sort(perm[n_g:n_g + n_a])
-    del_i = np.sort(perm[n_g + n_a:n_g + n_a + n_del])
-    del perm
-    gver = np.zeros(n, np.uint8)
-    aver = np.zeros(n, np.uint8)
-    gver[g_i] = 1
-    aver[a_i] = 1
-    upd = np.zeros(n, bool)
-    upd[g_i] = upd[a_i] = True
-    keep = np.ones(n, bool)
-    keep[del_i] = False
-    ins_pk = np.arange(pk0 + n, pk0 + n + n_ins, dtype=np.int64)
+    n_ins = n // 100
+    hi = n + n_ins if hi is None else min(hi, n + n_ins)
+    lo = max(0, min(lo, hi))
+    pks = np.arange(lo, min(hi, n), dtype=np.int64)
+    plan = c3_plan(pks, n)
+    gver = (plan == 1).astype(np.uint8)
+    aver = (plan == 2).astype(np.uint8)
+    upd = plan == 1
+    upd |= plan == 2
+    keep = plan != 3
+    ins_pk = np.arange(max(lo, n), hi, dtype=np.int64)
     t_pk = np.concatenate([pks[keep], ins_pk])
-    ver_b = np.zeros(n, np.uint64)
+    ver_b = np.zeros(pks.shape[0], np.uint64)
     ver_t = np.concatenate([(gver.astype(np.uint64) | (aver.astype(np.uint64) << np.uint64(1)))[keep],
-                            np.full(n_ins, 4, np.uint64)])
+                            np.full(ins_pk.shape[0], 4, np.uint64)])
     base = packing.PackedSide(key=_int_keys(pks), oid=synth_oids(pks, ver_b), key_mode=0,
-                              order=np.arange(n, dtype=np.int64), encoding=packing.INT_PK_ENCODING)
+                              order=np.arange(pks.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
     target = packing.PackedSide(key=_int_keys(t_pk), oid=synth_oids(t_pk, ver_t), key_mode=0,
                                 order=np.arange(t_pk.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
-    ub = np.nonzero(upd)[0]  # updated entries: base index; target index = position among kept + 0
+    ub = np.nonzero(upd)[0]  # updated entries: base index; target index by search (target is pk-sorted)
     ut = np.searchsorted(t_pk, pks[ub])
 
     def blobs(idx_pk, gv, av):
@@ -320,9 +328,60 @@ def polygons_layer(n, frac_geom=0.04, frac_attr=0.04, frac_delete=0.01, frac_ins
 
     bd, bo = blobs(pks[ub], np.zeros(ub.size, np.uint64), np.zeros(ub.size, np.uint64))
     td, to = blobs(pks[ub], gver[ub].astype(np.uint64), aver[ub].astype(np.uint64))
-    bb = _sparse_arena(n, ub, bd, bo)
+    bb = _sparse_arena(pks.shape[0], ub, bd, bo)
     tb = _sparse_arena(t_pk.shape[0], ut, td, to)
-    return Layer(base, target, bb, tb, schema, {lh: legend}, n_ins, int(ub.size), n_del)
+    return Layer(base, target, bb, tb, schema, {lh: legend}, int(ins_pk.shape[0]), int(ub.size),
+                 int(np.count_nonzero(plan == 3)))
+
+
+def shard_pk_range(rank, world, n_pks):
+    """[lo, hi) of rank's bucket-range shard of a layer with int pks 0..n_pks-1: whole 64-pk leaf
+    buckets (bucket = pk // 64 below 2**30), about n_pks / world pks each."""
+    if n_pks >= (1 << 30):
+        raise ValueError("synthetic layer exceeds one bucket wrap (2**30 pks)")
+    nb = (n_pks + 63) // 64
+    return 64 * (nb * rank // world), min(n_pks, 64 * (nb * (rank + 1) // world))
+
+
+_B64 = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_", np.uint8)
+
+
+def int_pk_paths(pk):
+    """IntPathEncoder relative paths (kart/dataset3_paths.py:292-299) of non-negative int pks below
+    2**32, vectorised: 'c/c/c/c/' + urlsafe_b64(msgpack([pk])) -> (uint8 arena, uint64 off[n+1])."""
+    pk = np.asarray(pk, np.int64)
+    n = pk.shape[0]
+    if n and (pk.min() < 0 or pk.max() >= (1 << 32)):
+        raise ValueError("int_pk_paths: pks in [0, 2**32)")
+    # msgpack([pk]): 0x91 + positive fixint / uint8 / uint16 / uint32
+    w = np.where(pk < 128, 0, np.where(pk < 256, 1, np.where(pk < 65536, 2, 4)))
+    mlen = 2 + w
+    mp = np.zeros((n, 6), np.uint8)
+    mp[:, 0] = 0x91
+    mp[:, 1] = np.where(w == 0, pk, np.where(w == 1, 0xCC, np.where(w == 2, 0xCD, 0xCE))).astype(np.uint8)
+    for k in range(4):  # big-endian payload bytes at 2 .. 2+w
+        shift = 8 * (w - 1 - k)
+        byte = (pk >> np.maximum(shift, 0)) & 0xFF
+        mp[:, 2 + k] = np.where(k < w, byte, 0).astype(np.uint8)
+    # base64 of mlen bytes: 4 chars per 3-byte group, '=' padded
+    blen = 4 * ((mlen + 2) // 3)
+    g = mp.reshape(n, 2, 3).astype(np.uint32)
+    v = g[:, :, 0] << 16 | g[:, :, 1] << 8 | g[:, :, 2]
+    ch = _B64[np.stack([(v >> 18) & 63, (v >> 12) & 63, (v >> 6) & 63, v & 63], 2).reshape(n, 8)]
+    pad = blen - (4 * mlen + 2) // 3  # '=' count: (3 - mlen % 3) % 3
+    pos = np.arange(8)[None, :]
+    ch = np.where(pos >= (blen - pad)[:, None], ord("="), ch).astype(np.uint8)
+    bucket = (pk // 64) % (1 << 24)
+    tree = np.stack([_B64[(bucket >> (18 - 6 * k)) & 63] for k in range(4)], 1)
+    rows = np.zeros((n, 16), np.uint8)
+    rows[:, 0:8:2] = tree
+    rows[:, 1:8:2] = ord("/")
+    rows[:, 8:] = ch
+    plen = 8 + blen
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(plen, out=off[1:])
+    arena = rows[np.arange(16)[None, :] < plen[:, None]]
+    return arena, off
 
 
 def _int_keys(pk):

@@ -371,7 +371,7 @@ int kdo_fielddiff(uint64_t n_upd,
                   const uint64_t* cmp_mask,
                   uint64_t* masks, uint8_t* status) {
     enum { MAXV = 4096 };
-    static uint32_t voff_o[MAXV], voff_n[MAXV];
+    static __thread uint32_t voff_o[MAXV], voff_n[MAXV];  /* per thread: the bench runs shards in parallel */
     for (uint64_t u = 0; u < n_upd; u++) {
         uint64_t oi = old_idx ? old_idx[u] : u, ni = new_idx ? new_idx[u] : u;
         const uint8_t* ob = old_data + old_off[oi];

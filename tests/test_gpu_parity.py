@@ -241,17 +241,15 @@ def test_gpu_env_overlap_vs_oracle(engine):
                                      (2_000_000, "polygons")])
 def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered):
     """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes),
-    on the C2 points layer and the C3 polygon layer (~370-B blobs: the large LDS pool)"""
-    import torch
-
+    on the C2 points layer and the C3 polygon layer (~370-B blobs: head + tail windows and the
+    cooperative payload compares); buffers from the library's own allocator"""
     from kart_amd import synth
     from kart_amd.device import DiffPipeline
     from kart_amd.schema import FieldMaps
 
     L = synth.points_layer(n, seed=11) if layer == "points" else synth.polygons_layer(n, seed=12)
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
-    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, torch.device("cuda", 0),
-                        ordered=ordered)
+    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered)
     for _ in range(3):  # repeated steps reuse the workspaces and counters
         pipe.step()
     engine.sync()
@@ -285,13 +283,11 @@ def test_gpu_merge3_device_c4_layer_vs_oracle(engine, n):
     """the C4 bench layer (string PKs, MsgpackHashPathEncoder paths, mod/mod, mod/del, del/mod and
     add/add edits) through the device-resident kd_merge3_device pipeline bench.py times, and the host
     kd_merge3: conflicts and merge deltas bit-exact with the oracle, conflicts = the generator's plan"""
-    import torch
-
     from kart_amd import synth
     from kart_amd.device import MergePipeline
 
     M = synth.table3_layers(n, seed=n)
-    pipe = MergePipeline(engine, M.ancestor, M.ours, M.theirs, torch.device("cuda", 0))
+    pipe = MergePipeline(engine, M.ancestor, M.ours, M.theirs)
     for _ in range(2):  # repeated steps reuse the workspaces and counters
         pipe.step()
     engine.sync()
@@ -426,3 +422,72 @@ def test_gpu_hash_names_verified(engine, lens):
     b = bytearray(bad[only_at[0]]); b[-1] ^= 1; bad[only_at[0]] = bytes(b)
     with pytest.raises(N.Unsupported):
         engine.merge3(A, O_, side(selT, oT, bad))
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU packing: kd_sort_side (LDS-ranked LSD radix sort of the join keys + OID permute)
+def _sort_dev(engine, keys, oids):
+    from kart_amd import packing
+
+    n = keys.shape[0]
+    dk, do, dord = packing.sort_on_device(engine, keys, oids)
+    return dk.download(np.uint64, n), do.download(np.uint8, 20 * n).reshape(n, 20), dord.download(np.uint32, n)
+
+
+@pytest.mark.parametrize("n,kind", [(1, "rand"), (2, "rand"), (4095, "rand"), (4097, "rand"), (100_000, "rand"),
+                                    (3_000_000, "rand"), (1_000_000, "int30"), (300_000, "hi_bits"),
+                                    (50_000, "one_bit")])
+def test_gpu_sort_side_vs_argsort(engine, n, kind):
+    """the device sort equals a stable host argsort: keys, order and the OIDs that travel with them
+    (random 64-bit keys = 8 passes; int keys of pks < 2**30 = 4 passes; keys varying only in the top
+    byte or in one bit)"""
+    rng = np.random.default_rng(n)
+    if kind == "rand":
+        keys = np.unique(rng.integers(0, 2**64 - 1, size=n + n // 8, dtype=np.uint64))[:n]
+        rng.shuffle(keys)
+    elif kind == "int30":
+        from kart_amd import synth
+
+        keys = synth._int_keys(rng.permutation(n).astype(np.int64) * 3)
+    elif kind == "hi_bits":
+        keys = (np.arange(n, dtype=np.uint64) << np.uint64(40)) | np.uint64(0xABCDE)
+        rng.shuffle(keys)
+    else:
+        keys = np.array([5, 5 | (1 << 63)] * (n // 2), np.uint64)[:n]
+        keys = np.unique(keys)
+    n = keys.shape[0]
+    oids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    k, o, order = _sort_dev(engine, keys, oids)
+    ref = np.argsort(keys, kind="stable")
+    assert np.array_equal(order, ref.astype(np.uint32))
+    assert np.array_equal(k, keys[ref]) and np.array_equal(o, oids[ref])
+
+
+def test_gpu_sort_side_duplicates_rejected(engine):
+    from kart_amd import packing
+
+    keys = np.array([9, 3, 7, 3], np.uint64)
+    with pytest.raises(packing.PackError):
+        packing.sort_on_device(engine, keys, np.zeros((4, 20), np.uint8))
+
+
+@pytest.mark.parametrize("n", [1000, 2_000_000])
+def test_gpu_pack_side_equals_host_pack(engine, n):
+    """pack_side(engine=...) (native parse + GPU sort, device-resident result) == the host packer,
+    and a diff of two GPU-packed sides == the oracle's"""
+    from kart_amd import packing, synth
+
+    L = synth.polygons_layer(n, seed=3)
+    sides = []
+    for S in (L.base, L.target):
+        pks = (S.key >> np.uint64(40)).astype(np.int64) * 64 + (S.key & np.uint64(63)).astype(np.int64)
+        perm = np.random.default_rng(n).permutation(S.n)  # leaves in another (walk) order
+        arena, off = synth.int_pk_paths(pks[perm])
+        host = packing.pack_side(arena, S.oid[perm], packing.INT_PK_ENCODING, rel_off=off)
+        dev = packing.pack_side(arena, S.oid[perm], packing.INT_PK_ENCODING, rel_off=off, engine=engine)
+        assert np.array_equal(dev.key, host.key) and np.array_equal(dev.oid, host.oid)
+        assert np.array_equal(dev.order, host.order) and np.array_equal(dev.key, S.key)
+        sides.append(dev)
+    r = engine.diff2(*sides)
+    od, _ = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
+    assert np.array_equal(r.delta, od)

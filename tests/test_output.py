@@ -145,25 +145,26 @@ def test_gpu_hex_device_unaligned(engine):
     """device-resident arena off the 16-B grid takes the byte-wise kernel; same strings"""
     import ctypes
 
-    import torch
     from kart_amd import _native as N
+    from kart_amd.device import DevBuf
 
     rng = np.random.default_rng(9)
     vals = [rng.bytes(int(rng.integers(0, 50))) for _ in range(3000)]
     data = np.frombuffer(b"".join(vals), np.uint8)
     off = np.zeros(len(vals) + 1, np.uint64)
     np.cumsum([len(v) for v in vals], out=off[1:])
-    dev = torch.device("cuda", 0)
-    d_data = torch.zeros(data.size + 3, dtype=torch.uint8, device=dev)
-    d_data[3:] = torch.from_numpy(data.copy()).to(dev)
-    d_off = torch.from_numpy(off.view(np.int64).copy()).to(dev)
-    d_hex = torch.zeros(2 * data.size + 5, dtype=torch.uint8, device=dev)
+    d_data = DevBuf(engine, data.size + 3)
+    d_data.zero()
+    d_data.upload(data, offset=3)
+    d_off = DevBuf.from_numpy(engine, off)
+    d_hex = DevBuf(engine, 2 * data.size + 5)
+    d_hex.zero()
     g = N.KdBlobs()
-    g.n, g.data, g.off, g.mem, g.size_hint = len(vals), d_data.data_ptr() + 3, d_off.data_ptr(), N.KD_MEM_DEVICE, 0
-    N.check(engine.L.kd_hex_encode(engine.ctx, ctypes.byref(g), N.KD_HEX_BYTES, d_hex.data_ptr() + 1, None, None,
+    g.n, g.data, g.off, g.mem, g.size_hint = len(vals), d_data.ptr + 3, d_off.ptr, N.KD_MEM_DEVICE, 0
+    N.check(engine.L.kd_hex_encode(engine.ctx, ctypes.byref(g), N.KD_HEX_BYTES, d_hex.ptr + 1, None, None,
                                    N.KD_MEM_DEVICE), "kd_hex_encode")
-    torch.cuda.synchronize()
-    assert d_hex[1:1 + 2 * data.size].cpu().numpy().tobytes() == data.tobytes().hex().encode()
+    engine.sync()
+    assert d_hex.download(np.uint8, 2 * data.size, offset=1).tobytes() == data.tobytes().hex().encode()
 
 
 @pytest.mark.gpu

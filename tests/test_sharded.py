@@ -68,6 +68,16 @@ def test_sharded_equals_unsharded_cpu(n, shards):
     assert (counts["inserts"], counts["updates"], counts["deletes"]) == (ref.n_insert, ref.n_update, ref.n_delete)
 
 
+def _gloo_exchange(local):
+    """all-gather of the per-shard (id, records, counts) tuples over gloo (CPU stand-in for the
+    library's RCCL all-gather)"""
+    import torch.distributed as dist
+
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, local)
+    return [x for part in out for x in part]
+
+
 def _gloo_worker(rank, world, port, n, shards, out_dir):
     import torch.distributed as dist
 
@@ -76,7 +86,8 @@ def _gloo_worker(rank, world, port, n, shards, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         L = _layer(n, 23)
-        delta, counts = shard.diff2_sharded(L.base, L.target, shards, _oracle_run, rank=rank, world=world)
+        delta, counts = shard.diff2_sharded(L.base, L.target, shards, _oracle_run, rank=rank, world=world,
+                                            exchange=_gloo_exchange)
         np.save(os.path.join(out_dir, f"delta_{rank}.npy"), delta)
         np.save(os.path.join(out_dir, f"counts_{rank}.npy"),
                 np.array([counts["inserts"], counts["updates"], counts["deletes"]], np.int64))
@@ -108,3 +119,41 @@ def test_sharded_gpu(engine, n, shards):
     delta, counts = shard.diff2_sharded(L.base, L.target, shards, engine.diff2)
     assert np.array_equal(delta, whole.delta)
     assert (counts["inserts"], counts["updates"], counts["deletes"]) == (whole.n_insert, whole.n_update, whole.n_delete)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 5000, 600_000])
+def test_diff2_sharded_library_g1(engine, n):
+    """kd_diff2_sharded (the library cuts the sides, owns the RCCL communicator) with one GPU"""
+    from kart_amd.engine import Engine
+
+    L = _layer(n, 41)
+    ref = _oracle_run(L.base, L.target)
+    r = Engine.diff2_sharded([engine], L.base, L.target, shard.bucket_bits(L.base.key_mode, L.base.encoding))
+    assert np.array_equal(r.delta, ref.delta) and np.array_equal(r.upd, ref.upd)
+    assert (r.n_insert, r.n_update, r.n_delete) == (ref.n_insert, ref.n_update, ref.n_delete)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [3000, 400_000])
+def test_shard_rank_gather_world1(engine, n):
+    """ShardRank / kd_diff2_gather on a one-rank communicator: rebased records + counts through RCCL"""
+    from kart_amd.engine import Engine
+
+    L = _layer(n, 43)
+    ref = _oracle_run(L.base, L.target)
+    engine.comm_init(1, 0, Engine.comm_unique_id())
+    try:
+        bits = shard.bucket_bits(L.base.key_mode, L.base.encoding)
+        cuts = shard.cut_points([L.base.key, L.target.key], 3, bits)  # one rank owning the middle shard
+        ba, tb = shard.slice_bounds(L.base.key, cuts, bits), shard.slice_bounds(L.target.key, cuts, bits)
+        rk = shard.ShardRank(engine, shard.shard_side(L.base, ba[1], ba[2]), shard.shard_side(L.target, tb[1], tb[2]),
+                             ba[1], tb[1])
+        for _ in range(2):
+            rk.step()
+        delta, counts = rk.results()
+        sel = ((ref.delta[:, 0] >= ba[1]) & (ref.delta[:, 0] < ba[2])) | ((ref.delta[:, 1] >= tb[1]) & (ref.delta[:, 1] < tb[2]))
+        assert np.array_equal(delta, ref.delta[sel])
+        assert counts["inserts"] + counts["updates"] + counts["deletes"] == int(sel.sum())
+    finally:
+        engine.comm_fini()

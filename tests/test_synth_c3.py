@@ -12,10 +12,13 @@ def test_polygons_layer_plan_and_encoding():
     import msgpack
 
     L = synth.polygons_layer(20_000, seed=5)
-    assert (L.n_update, L.n_insert, L.n_delete) == (1600, 200, 200)
+    plan = synth.c3_plan(np.arange(20_000), 20_000)
+    assert (L.n_update, L.n_insert, L.n_delete) == (int(((plan == 1) | (plan == 2)).sum()), 200, int((plan == 3).sum()))
+    assert 1400 < L.n_update < 1800 and 150 < L.n_delete < 250  # 8 % / 1 % of 20k in expectation
     od, counts = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
     upd = od[(od[:, 0] != 0xFFFFFFFF) & (od[:, 1] != 0xFFFFFFFF)]
     assert upd.shape[0] == L.n_update
+    assert (counts["inserts"], counts["deletes"]) == (L.n_insert, L.n_delete)
     d, off = L.base_blobs
     lens = np.diff(off)
     assert np.count_nonzero(lens) == L.n_update  # blobs only where the diff reads them
@@ -31,3 +34,38 @@ def test_polygons_layer_plan_and_encoding():
     m = masks[:, 0]
     assert np.all((m == geom_bit) | ((m & geom_bit) == 0) & (m != 0))
     assert 0.4 < np.mean(m == geom_bit) < 0.6
+
+
+def test_polygons_layer_shards_concatenate():
+    """bucket-range slices (bench.py --gpus N) are exactly the whole layer's entries, in order"""
+    n = 30_000
+    whole = synth.polygons_layer(n, seed=9)
+    parts = [synth.polygons_layer(n, seed=9, lo=a, hi=b) for a, b in
+             (synth.shard_pk_range(r, 4, n + n // 100) for r in range(4))]
+    for side in ("base", "target"):
+        assert np.array_equal(np.concatenate([getattr(p, side).key for p in parts]), getattr(whole, side).key)
+        assert np.array_equal(np.concatenate([getattr(p, side).oid for p in parts]), getattr(whole, side).oid)
+    assert sum(p.n_update for p in parts) == whole.n_update
+    assert sum(p.n_insert for p in parts) == whole.n_insert and sum(p.n_delete for p in parts) == whole.n_delete
+    # shard edges fall on 64-pk leaf buckets
+    for r in range(4):
+        lo, hi = synth.shard_pk_range(r, 4, n + n // 100)
+        assert lo % 64 == 0 and (hi % 64 == 0 or hi == n + n // 100)
+
+
+def test_int_pk_paths_match_reference_encoder():
+    """vectorised IntPathEncoder paths == the reference encoding restated per pk
+    (tests/test_structure.py:851-925 KAT: 1181 -> A/A/A/S/kc0EnQ==)"""
+    import base64
+
+    import msgpack
+
+    pks = np.array([0, 1, 63, 64, 127, 128, 255, 256, 1181, 65535, 65536, 2**24, 2**30 - 1, 2**32 - 1], np.int64)
+    arena, off = synth.int_pk_paths(pks)
+    alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
+    for i, pk in enumerate(pks.tolist()):
+        b = (pk // 64) % (1 << 24)
+        tree = "/".join(alpha[(b >> (18 - 6 * k)) & 63] for k in range(4))
+        want = tree + "/" + base64.urlsafe_b64encode(msgpack.packb([pk])).decode()
+        assert arena[off[i]:off[i + 1]].tobytes().decode() == want
+    assert arena[off[8]:off[9]].tobytes() == b"A/A/A/S/kc0EnQ=="
