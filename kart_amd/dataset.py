@@ -23,7 +23,7 @@ import numpy as np
 
 from . import _native as N
 from . import packing
-from .deltas import DatasetDiff, Delta, DeltaDiff
+from .adaptor import structs
 from .schema import FieldMaps, Legend, Schema
 
 FEATURE_PATH = "feature/"
@@ -194,6 +194,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False):
     present = base if base is not None else target
     if present is None:
         return
+    S = structs()
     empty = packing.empty_side(present.encoding)
     A = base.packed if base is not None else empty
     B = target.packed if target is not None else empty
@@ -227,19 +228,28 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False):
         if has_b[i]:
             blob = new_v.get_blob(int(B.order[b_idx[i]]))
             new_half = (npk, functools.partial(new_v.get_feature_from_blob, blob))
-        yield Delta(old_half, new_half)
+        yield S.Delta(old_half, new_half)
 
 
 def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
-    """RichBaseDataset.diff: {"meta": dict diff, "feature": DeltaDiff}"""
-    out = DatasetDiff()
+    """RichBaseDataset.diff (kart/rich_base_dataset.py:170-181): {"meta": dict diff, "feature": DeltaDiff}"""
+    S = structs()
+    out = S.DatasetDiff()
     old, new = (target, base) if reverse else (base, target)
-    out["meta"] = DeltaDiff.diff_dicts(old.meta_items() if old else {}, new.meta_items() if new else {})
+    out["meta"] = S.DeltaDiff.diff_dicts(old.meta_items() if old else {}, new.meta_items() if new else {})
     ffilter = None
     if ds_filter is not None and not getattr(ds_filter, "match_all", False):
-        ffilter = ds_filter.get("feature")
-    out["feature"] = DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse))
+        # a filter without a "feature" entry matches no feature (the reference falls back to an empty
+        # child filter: ds_filter.get("feature", ds_filter.child_type()), :177)
+        ffilter = ds_filter.get("feature", _NoKeys())
+    out["feature"] = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse))
     return out
+
+
+class _NoKeys(frozenset):
+    """an empty, non-match-all key filter"""
+
+    match_all = False
 
 
 def get_dataset_diff(engine, base, target, ds_filter=None):
@@ -249,7 +259,7 @@ def get_dataset_diff(engine, base, target, ds_filter=None):
         base, target = target, base
         params["reverse"] = True
     if base is None:
-        return DatasetDiff()
+        return structs().DatasetDiff()
     ds = dataset_diff(engine, base, target, ds_filter, **params)
     ds.prune()
     return ds

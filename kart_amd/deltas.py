@@ -2,9 +2,9 @@
 
 Behavioural mirror of kart/diff_structs.py (KeyValue :12-40, Delta :47-188 incl. the
 concatenation algebra :142-180, DeltaDiff :375-458, DatasetDiff/RepoDiff :461-480), so the engine
-can hand back objects the diff writers already understand.  Inside Kart the adaptor is pointed at
-``kart.diff_structs`` itself (``kart_amd.adaptor.use_structs``); this module is what it uses when
-Kart is not importable (this repo's tests, the GPU box).
+can hand back objects the diff writers already understand.  Inside Kart the engine returns
+``kart.diff_structs`` itself (``kart_amd.adaptor.use_structs``, picked automatically when Kart is
+importable); this module is what it uses when Kart is not (this repo's tests, the GPU box).
 """
 from collections import UserDict
 from numbers import Number

@@ -19,6 +19,8 @@ from .dataset import DatasetVersion
 from .schema import Legend, Schema
 
 DATASET_DIRNAME = ".table-dataset"
+# libgit2 error subcodes Kart's pygit2 attaches to a KeyError (kart/promisor_utils.py:10-22)
+ENOSUCHPATH, EOBJECTMISSING, EOBJECTPROMISED = -3001, -3002, -3003
 
 
 class GitRepo:
@@ -28,12 +30,23 @@ class GitRepo:
         # Kart's index carries a "kart" extension stock git rejects; never touch it
         self.env["GIT_INDEX_FILE"] = index_file or os.path.join(gitdir, "kart_amd.index")
         self._cat = None
+        self._promisor = None
 
     def git(self, *args):
         return subprocess.run(["git", *args], env=self.env, check=True, capture_output=True).stdout
 
     def rev_tree(self, spec):
         return self.git("rev-parse", spec + "^{tree}").decode().strip()
+
+    def promisor_remote(self):
+        """the promisor remote of a partial clone, or None (promisor_utils.get_promisor_remote)"""
+        if self._promisor is None:
+            out = subprocess.run(["git", "config", "--get-regexp", r"^remote\..*\.promisor$"], env=self.env,
+                                 capture_output=True).stdout.decode().split("\n")
+            names = [ln.split()[0][len("remote."):-len(".promisor")] for ln in out
+                     if ln.strip() and ln.split()[-1].lower() in ("true", "1", "yes", "on")]
+            self._promisor = names[0] if names else ""
+        return self._promisor or None
 
     def cat(self, oid_hex):
         if self._cat is None:
@@ -43,7 +56,12 @@ class GitRepo:
         self._cat.stdin.flush()
         hdr = self._cat.stdout.readline().split()
         if len(hdr) < 3 or hdr[1] == b"missing":
-            raise KeyError(f"object {oid_hex} missing (promised?)")
+            # kart/base_dataset.py:256-265 + promisor_utils.py:10-29: a KeyError with the libgit2
+            # subcode — promised (partial clone: DeltaFetcher fetches it) or missing
+            promised = self.promisor_remote() is not None
+            e = KeyError(f"object {oid_hex} {'promised' if promised else 'missing'}")
+            e.subcode = EOBJECTPROMISED if promised else EOBJECTMISSING
+            raise e
         data = self._cat.stdout.read(int(hdr[2]))
         self._cat.stdout.read(1)
         return data
@@ -64,6 +82,43 @@ class GitRepo:
             names.append(path)
             oids.append(meta.split(b" ")[2])
         return names, oids
+
+    def ls_tree(self, treeish):
+        """one tree level: [(mode, type, oid hex, name)]"""
+        out = []
+        for rec in self.git("ls-tree", "-z", treeish).split(b"\0"):
+            if rec:
+                meta, name = rec.split(b"\t", 1)
+                mode, typ, oid = meta.split(b" ")
+                out.append((int(mode, 8), typ.decode(), oid.decode(), name.decode()))
+        return out
+
+    def non_feature_entries(self, spec):
+        """{path: (mode, oid hex)} of every blob of a commit outside the datasets' feature trees
+        (meta items, structure files): the walk never enters a .table-dataset/feature tree"""
+        out = {}
+        stack = [(self.rev_tree(spec), "")]
+        while stack:
+            tree, pre = stack.pop()
+            for mode, typ, oid, name in self.ls_tree(tree):
+                path = pre + name
+                if typ == "tree":
+                    if not path.endswith("/" + DATASET_DIRNAME + "/feature") and path != DATASET_DIRNAME + "/feature":
+                        stack.append((oid, path + "/"))
+                elif typ == "blob":
+                    out[path] = (mode, oid)
+        return out
+
+    def write_index_tree(self, index_info):
+        """a tree from '<mode> <oid>\\t<path>\\0' records (git update-index -z --index-info into a
+        scratch index, then write-tree): what libgit2's index.write_tree does"""
+        import tempfile
+
+        with tempfile.TemporaryDirectory() as td:
+            env = dict(self.env, GIT_INDEX_FILE=os.path.join(td, "index"))
+            subprocess.run(["git", "update-index", "-z", "--index-info"], input=index_info, env=env, check=True,
+                           capture_output=True)
+            return subprocess.run(["git", "write-tree"], env=env, check=True, capture_output=True).stdout.decode().strip()
 
     def dataset_paths(self, spec):
         """dataset paths of a commit (dirs containing .table-dataset)"""

@@ -4,12 +4,13 @@
 #   2. --pmc FETCH_SIZE        (own pass; gfx950: reads 1/2 of wide streaming bytes, doubled later)
 #   3. --pmc WRITE_SIZE        (own pass)
 # Each step is time-limited and chained with &&: a failure ends the script.
+# usage: WL=c3 KERN=k_fielddiff NUNITS=100000000 bash scripts/profile_gpu.sh TAG
 set -e
 R=$(pwd)
-TAG=${1:-r01}
-WL=${WL:-c2}
-KERN=${KERN:-k_join2}
-ARGS=${BENCH_ARGS:-"--workload $WL --steps 10 --warmup 2 --no-cpu-baseline"}
+TAG=${1:-r02}
+WL=${WL:-c3}
+KERN=${KERN:-k_fielddiff}
+ARGS=${BENCH_ARGS:-"--workload $WL --steps 5 --warmup 1 --no-cpu-baseline --no-host-timing"}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -20,7 +21,5 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format c
     python3 $R/bench.py $ARGS > $OUT/fetch_bench.json 2> $OUT/fetch_bench.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d $OUT/write -o run -- \
     python3 $R/bench.py $ARGS > $OUT/write_bench.json 2> $OUT/write_bench.err
-timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -T --output-format csv -d $OUT/sq -o run -- \
-    python3 $R/bench.py $ARGS > $OUT/sq_bench.json 2> $OUT/sq_bench.err
 echo "profile done"
-cd $R && python3 scripts/pmc_summary.py $OUT --n ${NPTS:-10000000} --kernel $KERN --write-traffic $OUT/traffic_$WL.json
+cd $R && python3 scripts/pmc_summary.py $OUT --n ${NUNITS:-100000000} --kernel $KERN --write-traffic $OUT/traffic_$WL.json

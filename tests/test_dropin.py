@@ -15,6 +15,7 @@ import pytest
 from checks import NONE
 from fixtures import DIFF_FIXTURES, load, pk_of
 from kart_amd import dataset as D
+from kart_amd.adaptor import structs
 from kart_amd.engine import Diff2Result
 
 
@@ -139,7 +140,7 @@ def test_key_filter(eng):
     class F(set):
         match_all = False
 
-    fd = D.DeltaDiff(D.diff_feature(eng, old, new, F({"1166", "1182", "999999"})))
+    fd = structs().DeltaDiff(D.diff_feature(eng, old, new, F({"1166", "1182", "999999"})))
     assert sorted(fd.keys()) == [1166, 1182]
 
 
