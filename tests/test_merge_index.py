@@ -186,36 +186,35 @@ def test_missing_and_promised_blob_subcodes(tmp_path):
 @pytest.mark.skipif(not os.path.isdir("/root/reference/kart"), reason="build container only (reads /root/reference)")
 def test_engine_returns_the_references_own_diff_structs():
     """Inside Kart the engine hands back kart.diff_structs objects: with the reference's own module
-    (imported through tests/golden/refshim.py), get_dataset_diff on the points fixture yields its
-    DatasetDiff / DeltaDiff / Delta, whose sorted_items, type_counts and lazy values match the golden"""
+    (imported through tests/golden/refshim.py, in a child interpreter so its stub modules stay out of
+    this one), get_dataset_diff on the points fixture yields its DatasetDiff / DeltaDiff / Delta,
+    whose sorted_items, type_counts and lazy values match the golden"""
     import sys
 
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
-    saved = {k: v for k, v in sys.modules.items() if k == "kart" or k.startswith("kart.")}
-    from fixtures import pk_of
-    from kart_amd import adaptor
-    from kart_amd import dataset as D
-
-    try:
-        import refshim
-
-        refshim.load_reference()
-        import importlib
-
-        ref = importlib.import_module("kart.diff_structs")
-        adaptor.use_structs(ref)
-        fx = load("repo_points")
-        (case,) = [c for c in fx.cases("diff2") if c["base"] == "head1" and c["target"] == "head"]
-        ds = D.get_dataset_diff(OracleEngine(), version(fx, "head1"), version(fx, "head"))
-        assert type(ds) is ref.DatasetDiff and type(ds["feature"]) is ref.DeltaDiff
-        fd = ds["feature"]
-        assert all(type(d) is ref.Delta for d in fd.values())
-        assert [k for k, _ in fd.sorted_items()] == [pk_of(d["old_pk"]) for d in case["deltas"]] == [1095, 1166, 1168, 1181, 1182]
-        assert fd.type_counts() == {"updates": 5}
-        k, d = fd.sorted_items()[0]
-        assert d.old_value["fid"] == k and callable(d.old.value) and d.old.value.args[0].id.hex
-    finally:
-        adaptor.reset()
-        for k in [k for k in sys.modules if k == "kart" or k.startswith("kart.")]:
-            del sys.modules[k]
-        sys.modules.update(saved)
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = f"""
+import importlib, sys
+sys.dont_write_bytecode = True
+sys.path[:0] = [{os.path.dirname(here)!r}, {here!r}, {os.path.join(here, "golden")!r}]
+import refshim
+refshim.load_reference()
+ref = importlib.import_module("kart.diff_structs")
+from kart_amd import adaptor, dataset as D
+from fixtures import load, pk_of
+from test_merge_index import OracleEngine
+from test_dropin import version
+adaptor.use_structs(ref)
+fx = load("repo_points")
+(case,) = [c for c in fx.cases("diff2") if c["base"] == "head1" and c["target"] == "head"]
+ds = D.get_dataset_diff(OracleEngine(), version(fx, "head1"), version(fx, "head"))
+assert type(ds) is ref.DatasetDiff and type(ds["feature"]) is ref.DeltaDiff
+fd = ds["feature"]
+assert all(type(d) is ref.Delta for d in fd.values())
+assert [k for k, _ in fd.sorted_items()] == [pk_of(d["old_pk"]) for d in case["deltas"]] == [1095, 1166, 1168, 1181, 1182]
+assert fd.type_counts() == {{"updates": 5}}
+k, d = fd.sorted_items()[0]
+assert d.old_value["fid"] == k and callable(d.old.value) and d.old.value.args[0].id.hex
+print("REF-STRUCTS-OK")
+"""
+    r = subprocess.run([sys.executable, "-B", "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "REF-STRUCTS-OK" in r.stdout, r.stdout + r.stderr
