@@ -26,6 +26,10 @@
  *                  device HBM and pinned host staging for callers without a GPU framework.
  *   kd_pack_*      <- Dataset3.decode_path_to_1pk / PathEncoder (kart/dataset3.py:250-259,
  *                     kart/dataset3_paths.py:202-215,292-299): host-side key packing.
+ *   kd_odb_* / kd_walk
+ *                  <- libgit2's ODB reads and tree iteration under Dataset3 (kart/dataset3.py:
+ *                     26-35,225-231; kart/base_dataset.py:230-265), with diff_to_tree's subtree
+ *                     pruning: the leaves the packer above consumes, read natively.
  *
  * Conventions: plain pointers and sizes only; return 0 on success, KD_EINVAL (-1) on bad
  * arguments, KD_EHIP (-2) on a HIP runtime error, KD_EUNSUPPORTED (-3) when the input needs
@@ -255,6 +259,40 @@ int64_t kd_pack_hash_keys(const uint8_t* paths, const uint64_t* path_off, uint64
                           int hex, uint64_t* keys, uint8_t* status);
 /* Inverse of the KD_KEY_INT key: pk = ((wrap - 2^33) * 2^24 + bucket) * 64 + r. */
 int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks);
+
+/* -------- git object database + leaf walk (host, no GPU) -------- */
+/* Replaces libgit2's ODB and tree iteration under Dataset3 (kart/dataset3.py:26-35,225-231,
+ * kart/base_dataset.py:230-265) and the subtree pruning of Tree.diff_to_tree
+ * (kart/rich_base_dataset.py:212-232).  Loose objects, pack v2 (idx v1/v2), zlib, OFS/REF delta
+ * chains, objects/info/alternates.  The pack set is read at open: reopen to see new packs. */
+#define KD_ENOTFOUND (-4) /* object not in the odb (missing, or promised by a partial clone) */
+typedef struct kd_odb kd_odb;
+int kd_odb_open(const char* gitdir, kd_odb** out);
+int kd_odb_close(kd_odb* odb);
+/* One object (*type 1 commit, 2 tree, 3 blob, 4 tag); *data malloc'd (kd_free). */
+int kd_odb_read(kd_odb* odb, const uint8_t oid[20], int* type, uint8_t** data, uint64_t* len);
+/* n blobs into one arena *data (kd_free): blob i = (*data)[off[i] .. off[i+1]) (off [n+1]);
+ * status[i] 0 ok, 1 missing (empty), 2 corrupt / not a blob (empty).  threads 0 = up to 16. */
+int kd_odb_read_batch(kd_odb* odb, const uint8_t* oids, uint64_t n, int threads, uint8_t** data,
+                      uint64_t* off, uint8_t* status);
+/* A walk's leaves for one root, one block (kd_free): leaf i = path[path_off[i] .. path_off[i+1])
+ * relative to the walked tree, '/'-separated, in git path order (what `git ls-tree -r` lists). */
+typedef struct kd_leaves {
+    uint64_t n;
+    uint64_t* path_off; /* [n+1] */
+    uint32_t* mode;     /* [n] git file modes (0100644, 0100755, 0120000, 0160000)  */
+    uint8_t* oid;       /* [n*20] */
+    uint8_t* path;
+    int32_t present;    /* 0: the walked tree does not exist in this root */
+} kd_leaves;
+#define KD_WALK_ALL (-1)
+/* Walk the tree at `subpath` ("" or NULL = the root) of k roots (commit, tag or tree OIDs, 20 raw
+ * bytes each, k <= 3) into out[0..k).  cmp0/cmp1 (root indices) prune: an entry (subtree or leaf)
+ * identical in roots cmp0 and cmp1 — same mode and OID, or absent from both — is skipped in every
+ * root and a pruned subtree is never read.  KD_WALK_ALL (both) lists everything.  The first levels
+ * are expanded breadth-first, then subtrees are walked depth-first by `threads` (0 = up to 16). */
+int kd_walk(kd_odb* odb, const uint8_t* roots, int k, const char* subpath, int cmp0, int cmp1,
+            int threads, kd_leaves** out);
 
 /* -------- profiling (hipEvents around every launch on the context stream) -------- */
 int kd_prof_enable(kd_ctx* ctx, int on);

@@ -14,6 +14,8 @@ KD_OK = 0
 KD_EINVAL = -1
 KD_EHIP = -2
 KD_EUNSUPPORTED = -3
+KD_ENOTFOUND = -4
+KD_WALK_ALL = -1
 KD_NONE = 0xFFFFFFFF
 KD_MEM_HOST = 0
 KD_MEM_DEVICE = 1
@@ -47,6 +49,21 @@ class KdError(RuntimeError):
 
 class Unsupported(KdError):
     """KD_EUNSUPPORTED: this input needs the reference CPU path."""
+
+
+class NotFound(KdError):
+    """KD_ENOTFOUND: a git object is not in the object database."""
+
+
+class KdLeaves(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("path_off", c_u64p),
+        ("mode", c_u32p),
+        ("oid", c_u8p),
+        ("path", c_u8p),
+        ("present", ctypes.c_int32),
+    ]
 
 
 class KdSide(ctypes.Structure):
@@ -191,6 +208,22 @@ SIGNATURES = {
          ctypes.c_void_p, ctypes.c_void_p],
     ),
     "kd_int_keys_to_pks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "kd_odb_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "kd_odb_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_odb_read": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_u8p), c_u64p],
+    ),
+    "kd_odb_read_batch": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(c_u8p), ctypes.c_void_p,
+         ctypes.c_void_p],
+    ),
+    "kd_walk": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.POINTER(ctypes.POINTER(KdLeaves))],
+    ),
     "kd_prof_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "kd_prof_select": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "kd_prof_get": (
@@ -231,6 +264,8 @@ def check(rc, what=""):
     msg = lib().kd_last_error().decode(errors="replace")
     if rc == KD_EUNSUPPORTED:
         raise Unsupported(rc, f"{what}: {msg}")
+    if rc == KD_ENOTFOUND:
+        raise NotFound(rc, f"{what}: {msg}")
     raise KdError(rc, f"{what}: {msg}")
 
 

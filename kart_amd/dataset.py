@@ -106,10 +106,15 @@ class DatasetVersion:
     """One commit's version of one dataset (the state Dataset3 wraps): leaves + meta.
 
     ``rel_paths``: uint8 arena + offsets of the leaf paths relative to ``feature/``;
-    ``oids`` [n, 20]; ``read_blob(i)`` -> bytes of leaf i (original order).
+    ``oids`` [n, 20]; ``read_blob(i)`` -> bytes of leaf i (original order); ``read_blobs(idx)``
+    (optional) -> (data, off, status) of many leaves in one batched read.  ``partial``: the leaves
+    are only those under the subtrees a pruned walk opened (gitsource.dataset_versions).
     """
 
-    def __init__(self, path, schema, legends, encoding, rel_paths, rel_off, oids, read_blob, meta=None):
+    partial = False
+
+    def __init__(self, path, schema, legends, encoding, rel_paths, rel_off, oids, read_blob, meta=None,
+                 read_blobs=None):
         self.path = path
         self.schema = schema
         self.legends = dict(legends)
@@ -118,6 +123,7 @@ class DatasetVersion:
         self.rel_off = np.ascontiguousarray(rel_off, np.uint64)
         self.oids = np.ascontiguousarray(oids, np.uint8).reshape(-1, 20)
         self.read_blob = read_blob
+        self._read_blobs = read_blobs
         self.meta = dict(meta or {})
         self._packed = None
 
@@ -166,15 +172,29 @@ class DatasetVersion:
         """BaseDataset.get_feature_from_blob (kart/base_dataset.py:506-507)"""
         return self.get_feature(path=blob.name, data=memoryview(blob.data))
 
+    def read_blobs(self, idx):
+        """(data, off, status) of leaves ``idx`` (original order) as one arena; status 1 = the blob
+        is not in the repository (its bytes are empty; reading it alone raises the KeyError)"""
+        if self._read_blobs is not None:
+            return self._read_blobs(idx)
+        bs, status = [], np.zeros(len(idx), np.uint8)
+        for k, i in enumerate(idx):
+            try:
+                bs.append(bytes(self.read_blob(int(i))))
+            except KeyError:
+                bs.append(b"")
+                status[k] = 1
+        data, off = packing._arena(bs)
+        return data, off, status
+
     def blob_arena(self, sorted_idx):
         """contiguous (data, off) of the blobs at the given sorted indices (host packing for
-        kd_fielddiff)"""
+        kd_fielddiff); KeyError when one is missing"""
         order = self.packed.order
-        bs = [self.read_blob(int(order[k])) for k in sorted_idx]
-        off = np.zeros(len(bs) + 1, np.uint64)
-        if bs:
-            off[1:] = np.cumsum([len(b) for b in bs])
-        data = np.frombuffer(b"".join(bs), np.uint8).copy() if bs else np.zeros(0, np.uint8)
+        idx = order[np.asarray(sorted_idx, np.int64)]
+        data, off, status = self.read_blobs(idx)
+        if status.any():
+            self.read_blob(int(idx[int(np.nonzero(status)[0][0])]))  # raises the reference's KeyError
         return data, off
 
 
@@ -311,11 +331,26 @@ def field_diff(engine, feature_diff, old_version, new_version):
     if not ups:
         return 0
     maps = FieldMaps(old_version.schema, old_version.legends, new_version.schema, new_version.legends)
-    ob = [d.old.value.args[0].data for d in ups]
-    nb = [d.new.value.args[0].data for d in ups]
-    od, oo = packing._arena(ob)
-    nd, no = packing._arena(nb)
+    od, oo = _blob_arena([d.old.value.args[0] for d in ups])
+    nd, no = _blob_arena([d.new.value.args[0] for d in ups])
     masks, status = engine.fielddiff(od, oo, nd, no, None, maps)
     for d, m, s in zip(ups, masks, status):
         d.changed_fields = maps.changed_names(m) if s == 0 else None
     return len(ups)
+
+
+def _blob_arena(blobs):
+    """(data, off) of LazyBlobs: those not yet read come from one batched read per dataset version
+    (kd_odb_read_batch under gitsource); a missing blob raises its KeyError as a single read does"""
+    groups = {}
+    for k, b in enumerate(blobs):
+        r = getattr(b, "_read", None)
+        if getattr(b, "_data", 1) is None and isinstance(r, functools.partial) and isinstance(
+                getattr(r.func, "__self__", None), DatasetVersion):
+            groups.setdefault(id(r.func.__self__), (r.func.__self__, []))[1].append(k)
+    for v, ks in groups.values():
+        data, off, status = v.read_blobs([blobs[k]._read.args[0] for k in ks])
+        for j, k in enumerate(ks):
+            if status[j] == 0:
+                blobs[k]._data = data[int(off[j]):int(off[j + 1])].tobytes()
+    return packing._arena([b.data for b in blobs])

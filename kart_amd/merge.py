@@ -161,10 +161,14 @@ def _side(version, encoding):
     return version.packed
 
 
-def merge_trees(engine, ancestor, ours, theirs, prefix=""):
+def merge_trees(engine, ancestor, ours, theirs, prefix="", ours_all=None):
     """Three-way classification of one dataset's feature tree (DatasetVersion or None for each of
     ancestor / ours / theirs) -> MergeIndex of its feature paths (``prefix`` + relative path, e.g.
-    "<ds>/.table-dataset/feature/").  Entries and conflicts follow libgit2's rule exactly."""
+    "<ds>/.table-dataset/feature/").  Entries and conflicts follow libgit2's rule exactly.
+
+    Versions from a pruned walk (``.partial``: only the subtrees where ours and theirs differ,
+    gitsource.merge_versions) classify the same; ``ours_all() -> [(rel path, oid hex)]`` then lists
+    every leaf of ours, for the merged entries outside those subtrees (ours == theirs there)."""
     present = next((v for v in (ours, theirs, ancestor) if v is not None), None)
     if present is None:
         return MergeIndex({}, {})
@@ -186,6 +190,12 @@ def merge_trees(engine, ancestor, ours, theirs, prefix=""):
     conf = [conf[j] for j in order]
 
     def build():
+        if ours_all is not None and ours is not None and ours.partial:
+            # outside the opened subtrees ours == theirs: the merge keeps ours
+            opened = {ours.rel_path(i) for i in range(ours.n)}
+            for rel, oid in ours_all():
+                if rel not in opened:
+                    yield Entry(prefix + rel, oid, FILEMODE_BLOB)
         # ours, then the merge deltas (take theirs) ...
         o = sides[1]
         skip = np.zeros(o.n, bool)
@@ -251,8 +261,14 @@ def merge_repo(engine, repo, ancestor, ours, theirs):
             entries[p] = Entry(p, res[1], res[0])
     parts = []
     for ds in ds_paths:
-        vers = [repo.dataset_version(s, ds) for s in specs]
-        parts.append(merge_trees(engine, *vers, prefix=f"{ds}/.table-dataset/feature/"))
+        pre = f"{ds}/.table-dataset/feature/"
+        vers = repo.merge_versions(*specs, ds)  # pruned to the subtrees where ours and theirs differ
+
+        def ours_all(pre=pre):
+            (lv,) = repo.walk([ours], pre.rstrip("/"))
+            return lv.items()
+
+        parts.append(merge_trees(engine, *vers, prefix=pre, ours_all=ours_all))
     for mi in parts:
         conf.extend(mi.conflicts.values())
     conf.sort(key=lambda c: next(e for e in c if e).path.encode())

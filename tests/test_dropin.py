@@ -198,6 +198,14 @@ def test_gitsource_walk(eng, tmp_path):
     assert sorted(fd.keys()) == [1095, 1166, 1168, 1181, 1182]
     D.field_diff(eng, fd, old, new)
     assert sum(len(d.changed_fields) for d in fd.values()) == 13
+    # the pruned walk (only subtrees whose OIDs differ are opened) gives the same diff
+    old_p, new_p = repo.diff_versions("refs/heads/c0", "refs/heads/c1", ds)
+    assert old_p.partial and new_p.partial and old_p.n == new_p.n == 5 < old.n
+    fdp = D.get_dataset_diff(eng, old_p, new_p)["feature"]
+    assert sorted(fdp.keys()) == [1095, 1166, 1168, 1181, 1182]
+    D.field_diff(eng, fdp, old_p, new_p)
+    assert {k: d.changed_fields for k, d in fdp.items()} == {k: d.changed_fields for k, d in fd.items()}
+    assert {k: d.new_value for k, d in fdp.items()} == {k: d.new_value for k, d in fd.items()}
     repo.close()
 
 

@@ -1,0 +1,223 @@
+"""The native object store + leaf walk (kd_odb_* / kd_walk, kart_amd/odb.py) against git itself:
+every listing equals `git ls-tree -r`, every object equals `git cat-file`, over packed (fast-import),
+repacked (deep OFS delta chains), loose and alternate object stores.  Pruned walks keep exactly
+the leaves a tree diff must see.  CPU only (host code)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from kart_amd import _native as N
+from kart_amd.odb import ObjectDB
+
+FEAT = "ds/.table-dataset/feature"
+
+
+def _git(gitdir, *args, input=None):
+    return subprocess.run(["git", "--git-dir", gitdir, *args], input=input, capture_output=True, check=True).stdout
+
+
+def _fast_import(gitdir, commits):
+    """commits: [(branch, {path: bytes | (mode, bytes)})], each on top of the previous"""
+    lines = []
+    for ci, (br, files) in enumerate(commits):
+        lines.append(b"commit refs/heads/%s\ncommitter t <t@t> %d +0000\ndata 1\nx\n" % (br.encode(), 1600000000 + ci))
+        if ci:
+            lines.append(b"from refs/heads/%s\n" % commits[ci - 1][0].encode())
+        lines.append(b"deleteall\n")
+        for p, d in files.items():
+            mode, d = d if isinstance(d, tuple) else (0o100644, d)
+            lines.append(b"M %o inline %s\ndata %d\n%s\n" % (mode, p.encode(), len(d), d))
+        lines.append(b"\n")
+    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
+                   check=True)
+
+
+def _ls(gitdir, spec, pre=""):
+    out = _git(gitdir, "ls-tree", "-r", "-z", spec, *(["--", pre] if pre else []))
+    res = []
+    for rec in out.split(b"\0"):
+        if rec:
+            meta, path = rec.split(b"\t", 1)
+            path = path.decode()
+            res.append((path[len(pre) + 1:] if pre else path, meta.split()[2].decode(), int(meta.split()[0], 8)))
+    return res
+
+
+def _rev(gitdir, spec):
+    return _git(gitdir, "rev-parse", spec).decode().strip()
+
+
+def _layer(seed, n=3000, drop=0.0, change=0.0):
+    rng = np.random.default_rng(seed)
+    files = {}
+    for i in range(n):
+        if drop and rng.random() < drop:
+            continue
+        v = int(rng.integers(1, 1000)) if change and rng.random() < change else 0
+        files[f"{FEAT}/{i % 7}/{(i // 7) % 13}/f{i}"] = b"feature %d v%d" % (i, v)
+    # names that sort around a tree named "0" (git orders a tree as "0/")
+    files[f"{FEAT}/0-x"] = b"before 0/"
+    files[f"{FEAT}/0.x"] = b"after 0/"
+    files[f"{FEAT}/00"] = b"after 0/ too"
+    files[f"{FEAT}/exec"] = (0o100755, b"#!/bin/sh\n")
+    files[f"{FEAT}/link"] = (0o120000, b"0/0/f0")
+    files["ds/.table-dataset/meta/schema.json"] = b"[]"
+    files["a b/\xc3\xa9 name"] = b"non-ascii path"
+    return files
+
+
+@pytest.fixture(scope="module")
+def repo(tmp_path_factory):
+    gitdir = str(tmp_path_factory.mktemp("odb") / "r.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    _fast_import(gitdir, [("c0", _layer(0)), ("c1", _layer(1, drop=0.03, change=0.05)),
+                          ("c2", _layer(2, drop=0.05, change=0.10))])
+    return gitdir
+
+
+def _items(lv):
+    return [(lv.path(i), lv.oids[i].tobytes().hex(), int(lv.modes[i])) for i in range(lv.n)]
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_walk_equals_ls_tree(repo, threads):
+    db = ObjectDB(repo)
+    for spec in ("c0", "c1", "c2"):
+        (lv,) = db.walk([_rev(repo, spec)], FEAT, threads=threads)
+        assert lv.present and _items(lv) == _ls(repo, spec, FEAT)
+        (lv,) = db.walk([_rev(repo, spec)], "", threads=threads)
+        assert _items(lv) == _ls(repo, spec)
+    # a tree OID works as a root as well as a commit; an absent subpath is "not present"
+    (lv,) = db.walk([_rev(repo, "c0^{tree}")], "ds")
+    assert lv.n == len(_ls(repo, "c0", "ds"))
+    (lv,) = db.walk([_rev(repo, "c0")], "no/such/dir")
+    assert not lv.present and lv.n == 0
+
+
+def _changed(repo, a, b):
+    A = {p: o for p, o, _ in _ls(repo, a, FEAT)}
+    B = {p: o for p, o, _ in _ls(repo, b, FEAT)}
+    return A, B, {p for p in set(A) | set(B) if A.get(p) != B.get(p)}
+
+
+def test_pruned_walk_keeps_every_changed_leaf(repo):
+    db = ObjectDB(repo)
+    A, B, changed = _changed(repo, "c0", "c2")
+    la, lb = db.walk([_rev(repo, "c0"), _rev(repo, "c2")], FEAT, compare=(0, 1))
+    pa, pb = {p: o for p, o, _ in _items(la)}, {p: o for p, o, _ in _items(lb)}
+    assert changed <= set(pa) | set(pb)
+    assert all(A[p] == o for p, o in pa.items()) and all(B[p] == o for p, o in pb.items())
+    # subtrees and leaves equal on both sides are skipped: what is left is exactly the changed paths
+    assert set(pa) | set(pb) == changed
+    assert la.n < len(A) and lb.n < len(B)
+    # identical roots: nothing opened
+    la, lb = db.walk([_rev(repo, "c1")] * 2, FEAT, compare=(0, 1))
+    assert la.n == lb.n == 0
+
+
+def test_pruned_three_way_walk(repo):
+    """merge pruning: compare ours (1) and theirs (2); the ancestor's leaves under the opened
+    subtrees come along"""
+    db = ObjectDB(repo)
+    roots = [_rev(repo, s) for s in ("c0", "c1", "c2")]
+    a, o, t = db.walk(roots, FEAT, compare=(1, 2))
+    O, T, changed = _changed(repo, "c1", "c2")
+    po, pt = {p for p, _, _ in _items(o)}, {p for p, _, _ in _items(t)}
+    assert po | pt == changed  # a leaf equal in ours and theirs is skipped even inside an opened tree
+    full_a = {p: x for p, x, _ in _ls(repo, "c0", FEAT)}
+    assert {p: x for p, x, _ in _items(a)} == {p: x for p, x in full_a.items() if O.get(p) != T.get(p)}
+
+
+def test_deep_delta_chains_and_batch_reads(tmp_path):
+    """40 commits editing a 600-entry tree, repacked with --depth=50: trees reach long OFS_DELTA
+    chains; every version's walk and every blob equal git's"""
+    gitdir = str(tmp_path / "d.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    base = {f"t/{i // 40}/{i:04d}": b"row %d " % i + b"x" * 200 for i in range(600)}
+    commits = []
+    for c in range(40):
+        files = dict(base)
+        for i in range(c * 15, c * 15 + 15):
+            files[f"t/{(i % 600) // 40}/{i % 600:04d}"] = b"row %d edit %d " % (i % 600, c) + b"y" * 200
+        base = files
+        commits.append((f"v{c}", files))
+    _fast_import(gitdir, commits)
+    _git(gitdir, "repack", "-adfq", "--depth=50", "--window=250")
+    packs = [f for f in os.listdir(os.path.join(gitdir, "objects", "pack")) if f.endswith(".idx")]
+    vp = _git(gitdir, "verify-pack", "-v", *[os.path.join(gitdir, "objects", "pack", f) for f in packs]).decode()
+    depths = [int(ln.split("=")[1].split(":")[0]) for ln in vp.splitlines() if ln.startswith("chain length")]
+    assert max(depths) >= 10, vp[-400:]
+    db = ObjectDB(gitdir)
+    for spec in ("v0", "v17", "v39"):
+        (lv,) = db.walk([_rev(gitdir, spec)], "t")
+        assert _items(lv) == _ls(gitdir, spec, "t")
+        data, off, st = db.read_batch(lv.oids, threads=4)
+        assert not st.any()
+        want = _git(gitdir, "cat-file", "--batch", input="".join(lv.oids[i].tobytes().hex() + "\n"
+                                                                for i in range(lv.n)).encode())
+        pos = 0
+        for i in range(lv.n):
+            nl = want.index(b"\n", pos)
+            size = int(want[pos:nl].split()[2])
+            assert data[int(off[i]):int(off[i + 1])].tobytes() == want[nl + 1:nl + 1 + size]
+            pos = nl + 1 + size + 1
+
+
+def test_loose_objects_missing_and_corrupt(tmp_path, repo):
+    gitdir = str(tmp_path / "l.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    big = bytes(range(256)) * 4000
+    oid = _git(gitdir, "hash-object", "-w", "--stdin", input=big).decode().strip()
+    empty = _git(gitdir, "hash-object", "-w", "--stdin", input=b"").decode().strip()
+    db = ObjectDB(gitdir)
+    assert db.read(oid) == (3, big)
+    assert db.read(empty) == (3, b"")
+    # a loose tree (update-index + write-tree) walks like a packed one
+    env = dict(os.environ, GIT_DIR=gitdir, GIT_INDEX_FILE=str(tmp_path / "idx"))
+    info = b"100644 %s\tx/y/big\x00100644 %s\tx/empty\x00" % (oid.encode(), empty.encode())
+    subprocess.run(["git", "update-index", "-z", "--index-info"], input=info, env=env, check=True)
+    tree = subprocess.run(["git", "write-tree"], env=env, capture_output=True, check=True).stdout.decode().strip()
+    (lv,) = db.walk([tree], "")
+    assert [(p, o) for p, o, _ in _items(lv)] == [("x/empty", empty), ("x/y/big", oid)]
+    with pytest.raises(N.NotFound):
+        db.read("1" * 40)
+    data, off, st = db.read_batch(np.frombuffer(bytes.fromhex(oid) + b"\x11" * 20 + bytes.fromhex(tree), np.uint8))
+    assert st.tolist() == [0, 1, 2] and int(off[1]) == len(big) and off[1] == off[3]
+    with pytest.raises(N.NotFound):
+        db.walk(["2" * 40], "")
+    # a truncated loose object is an error, never a crash
+    p = os.path.join(gitdir, "objects", oid[:2], oid[2:])
+    os.chmod(p, 0o644)
+    raw = open(p, "rb").read()
+    open(p, "wb").write(raw[: len(raw) // 2])
+    with pytest.raises(N.KdError):
+        ObjectDB(gitdir).read(oid)
+
+
+def test_alternates(tmp_path, repo):
+    gitdir = str(tmp_path / "alt.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    with open(os.path.join(gitdir, "objects", "info", "alternates"), "w") as f:
+        f.write(os.path.join(repo, "objects") + "\n")
+    db = ObjectDB(gitdir)
+    (lv,) = db.walk([_rev(repo, "c1")], FEAT)
+    assert _items(lv) == _ls(repo, "c1", FEAT)
+
+
+def test_gitrepo_refs_and_dataset_paths(repo):
+    from kart_amd.gitsource import GitRepo
+
+    r = GitRepo(repo)
+    try:
+        assert r.rev_parse("c1") == _rev(repo, "c1")
+        assert r.rev_parse("refs/heads/c2") == _rev(repo, "c2")
+        assert r.rev_parse("c2~1") == _rev(repo, "c1")  # expression: git rev-parse
+        assert r.rev_tree("c0") == _rev(repo, "c0^{tree}")
+        _git(repo, "pack-refs", "--all")
+        assert GitRepo(repo).rev_parse("c0") == _rev(repo, "c0")
+        assert r.dataset_paths("c0") == ["ds"]
+        assert [e[3] for e in r.ls_tree("c0")] == ["a b", "ds"]
+    finally:
+        r.close()
