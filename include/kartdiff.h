@@ -16,6 +16,9 @@
  *                     CRS (kart/spatial_filter/index.py:485-579,639-707).
  *   kd_env_overlap <- sf_filter_blob decode + cyclic_range_overlaps
  *                     (vendor/spatial-filter/spatial_filter.cpp:170-260).
+ *   kd_geom_filter <- BaseDiffWriter.filtered_ds_feature_deltas (kart/base_diff_writer.py:279-329):
+ *                     the geometry of each delta's old/new feature blob, envelope-tested, kept
+ *                     deltas compacted on the GPU.
  *   kd_hex_encode  <- Geometry.to_hex_wkb / gpkg_geom_to_hex_wkb (kart/geometry.py:346-375) and
  *                     bytes.hex(v), as feature_as_json formats them (kart/feature_output.py:34-56).
  *   kd_diff2_sharded / kd_diff2_gather
@@ -187,6 +190,33 @@ int kd_envelopes(kd_ctx* ctx, const kd_blobs* geoms, const double filt_env[4], i
  * out[i] = cyclic(w,e) && range(s,n) overlap (spatial_filter.cpp:187-260). */
 int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const double q[4],
                    uint8_t* out, uint32_t mem);
+
+/* -------- spatially filtered diff -------- */
+/* BaseDiffWriter.filtered_ds_feature_deltas (kart/base_diff_writer.py:279-329) with
+ * SpatialFilter.matches (kart/spatial_filter/__init__.py:534-605): for every delta, the geometry
+ * column is located in the old and new feature blobs (legend -> value position), its GPKG
+ * envelope (or point) tested against the filter envelope in FP64.  Per side (match[2d], match[2d+1]):
+ *   0 NON_MATCHING, 1 CANDIDATE (bbox passes: the exact Intersects is the caller's),
+ *   2 MATCHING (null geometry / no geometry column / inside a KD_GF_RECT filter),
+ *   3 FALLBACK (the caller decides on the CPU: unknown legend, nested value, envelope needs OGR),
+ *   4 NONEXISTENT (KD_NONE side).  Empty geometries are NON_MATCHING (Intersects(empty) is false).
+ * keep[0..*n_keep) <- the delta indices (in delta order) with either side 1, 2 or 3.
+ * enc/enc_ok (optional, NULL): the new side's spatial-index envelope (EnvelopeEncoder, bits/2
+ * bytes per delta), as kd_envelopes computes it.  pairs = (old blob | KD_NONE, new blob | KD_NONE)
+ * per delta — classify2's delta list with the arenas indexed by sorted entry.  With d_n the count
+ * is read on the device (pairs and outputs device memory, n = capacity).  match must be 2-B aligned. */
+#define KD_GF_RECT 0x1u /* the filter geometry is its own envelope (an axis-aligned rectangle) */
+typedef struct kd_geom_cols {
+    int32_t n_leg_old, n_leg_new;
+    const uint8_t* leg_old_hex; /* [n_leg_old*40] legend hexhashes (host memory) */
+    const int16_t* gidx_old;    /* [n_leg_old] value index of the geometry column, -1 none */
+    const uint8_t* leg_new_hex;
+    const int16_t* gidx_new;
+} kd_geom_cols;
+int kd_geom_filter(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_blobs* new_blobs, const uint32_t* pairs,
+                   uint64_t n, const uint64_t* d_n, uint32_t pairs_mem, const kd_geom_cols* cols,
+                   const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
+                   uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem);
 
 /* -------- writer formatting -------- */
 #define KD_HEX_BYTES 0u    /* bytes.hex(v): lowercase hex of every byte of every blob                */

@@ -28,6 +28,7 @@ KD_COPY_H2D = 1
 KD_COPY_D2H = 2
 KD_COPY_D2D = 3
 KD_COMM_ID_BYTES = 128
+KD_GF_RECT = 0x1
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -102,6 +103,17 @@ class KdLegendMaps(ctypes.Structure):
     ]
 
 
+class KdGeomCols(ctypes.Structure):
+    _fields_ = [
+        ("n_leg_old", ctypes.c_int32),
+        ("n_leg_new", ctypes.c_int32),
+        ("leg_old_hex", ctypes.c_void_p),
+        ("gidx_old", ctypes.c_void_p),
+        ("leg_new_hex", ctypes.c_void_p),
+        ("gidx_new", ctypes.c_void_p),
+    ]
+
+
 class KdDiffResult(ctypes.Structure):
     _fields_ = [
         ("n_insert", ctypes.c_uint64),
@@ -168,6 +180,12 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_dblp, ctypes.c_void_p,
          ctypes.c_uint32],
+    ),
+    "kd_geom_filter": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(KdBlobs), ctypes.POINTER(KdBlobs), ctypes.c_void_p, ctypes.c_uint64,
+         ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(KdGeomCols), c_dblp, ctypes.c_uint32, ctypes.c_int,
+         ctypes.c_void_p, ctypes.c_void_p, c_u64p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32],
     ),
     "kd_hex_encode": (
         ctypes.c_int,

@@ -1,0 +1,553 @@
+// kd_geomfilter.hip — the spatially filtered diff on the GPU: for every delta of a two-way diff,
+// the geometry column is located inside the old and new feature blobs (msgpack), its GPKG header
+// decoded (stored envelope, or the point WKB), tested against the filter envelope in FP64, and the
+// deltas whose old or new value may match are compacted in key order; the new side's
+// spatial-filter index envelope (EnvelopeEncoder) comes out of the same pass.
+//
+// Reference (file:line under /root/reference):
+//   BaseDiffWriter.filtered_ds_feature_deltas ... kart/base_diff_writer.py:279-329
+//       do_yield = old matches || new matches (a delta is kept when either side may match)
+//   SpatialFilter.matches / matches_delta_value . kart/spatial_filter/__init__.py:534-605
+//       None value -> NONEXISTENT; geometry None -> MATCHING; envelope (stored, else OGR's:
+//       point (x,x,y,y), empty (0,0,0,0)) fails bbox_intersects_fast -> NON_MATCHING; else the
+//       prepared filter's Intersects decides
+//   Dataset3.get_feature ........................ kart/dataset3.py:185-223 (blob = msgpack
+//       [legend hex, [non-pk values]]; the legend names the value positions, kart/schema.py:19-102)
+//   index envelope ............................... kart/spatial_filter/index.py:485-579 (kd_geom.h)
+//
+// Per side the code is 0 NON_MATCHING, 1 CANDIDATE (bbox passes; the exact Intersects is the
+// caller's), 2 MATCHING (null geometry, no geometry column, or — for a rectangular filter — the
+// envelope inside the rectangle, where Intersects is certain), 3 FALLBACK (the host decides:
+// unknown legend, nested values, envelope that needs OGR), 4 NONEXISTENT (no such side).  Empty
+// geometries never match (Intersects(empty) is false), whatever their (0,0,0,0) envelope does.
+//
+// Layout: one lane per delta, 4096 deltas per workgroup (16 rounds of 256).  The fast path loads
+// 112 bytes from each blob start (7 dwordx4, realigned with v_alignbyte) and decodes the common
+// shape — [legend str8(40), fixarray|array16 values, geometry first as ext8/16/32 'G'] — from
+// registers; anything else takes the byte-wise decoder on global memory.
+#include <type_traits>
+
+#include "kd_geom.h"
+
+namespace kd {
+
+constexpr int GF_NT = 256;
+constexpr int GF_ROUNDS = 16;
+constexpr int GF_TILE = GF_NT * GF_ROUNDS;
+constexpr int GF_MAXLEG = 64;  // legends per side held in LDS
+
+enum { GF_NON = 0, GF_CAND = 1, GF_MATCH = 2, GF_FALLBACK = 3, GF_NONE = 4 };
+
+struct GfArgs {
+    const u8* data[2];
+    const u64* off[2];
+    u64 nblob[2];
+    const u8* leg_hex[2];  // [n_leg * 40]
+    const i16* gidx[2];    // [n_leg]
+    int n_leg[2];
+    const u32* pairs;  // [2 * cap]
+    u64 cap;
+    const u64* d_n;  // device delta count (or null: cap)
+    double f0, f1, f2, f3;
+    int rect;
+    int bits;
+    u8* match;  // [2 * cap]
+    u8* enc;    // [cap * bits/2] new side index envelope (optional)
+    u8* enc_ok;
+    u32* tile_cnt;  // [tiles]
+};
+
+struct GHit {
+    int code;
+    int r, pc;  // gpkg_env / point_env results (index envelope input)
+    bool empty;
+    double e[4], pe[4];
+};
+
+// ---- byte-wise msgpack walk (global memory) ----
+__device__ __forceinline__ u32 be_n(const u8* p, int n) {
+    u32 v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+// skip one msgpack value at p (end e), nested arrays / maps included (a count of values still
+// to skip instead of recursion); false on truncation or an invalid byte
+__device__ bool mp_skip(const u8*& p, const u8* e) {
+    u64 pending = 1;
+    while (pending) {
+        if (p >= e || pending > (u64)(e - p)) return false;  // every value takes at least one byte
+        const u8 c = *p++;
+        pending--;
+        u64 n = 0;
+        if (c <= 0x7f || c >= 0xe0 || c == 0xc0 || c == 0xc2 || c == 0xc3) continue;
+        if ((c & 0xe0) == 0xa0) n = c & 31;
+        else if ((c & 0xf0) == 0x90) { pending += c & 15; continue; }
+        else if ((c & 0xf0) == 0x80) { pending += 2 * (c & 15); continue; }
+        else {
+            switch (c) {
+                case 0xcc: case 0xd0: n = 1; break;
+                case 0xcd: case 0xd1: n = 2; break;
+                case 0xce: case 0xd2: case 0xca: n = 4; break;
+                case 0xcf: case 0xd3: case 0xcb: n = 8; break;
+                case 0xd9: case 0xc4: if (p + 1 > e) return false; n = be_n(p, 1); p += 1; break;
+                case 0xda: case 0xc5: if (p + 2 > e) return false; n = be_n(p, 2); p += 2; break;
+                case 0xdb: case 0xc6: if (p + 4 > e) return false; n = be_n(p, 4); p += 4; break;
+                case 0xd4: n = 2; break;
+                case 0xd5: n = 3; break;
+                case 0xd6: n = 5; break;
+                case 0xd7: n = 9; break;
+                case 0xd8: n = 17; break;
+                case 0xc7: if (p + 1 > e) return false; n = be_n(p, 1) + 1; p += 1; break;
+                case 0xc8: if (p + 2 > e) return false; n = be_n(p, 2) + 1; p += 2; break;
+                case 0xc9: if (p + 4 > e) return false; n = (u64)be_n(p, 4) + 1; p += 4; break;
+                case 0xdc: if (p + 2 > e) return false; pending += be_n(p, 2); p += 2; continue;
+                case 0xdd: if (p + 4 > e) return false; pending += be_n(p, 4); p += 4; continue;
+                case 0xde: if (p + 2 > e) return false; pending += 2ull * be_n(p, 2); p += 2; continue;
+                case 0xdf: if (p + 4 > e) return false; pending += 2ull * be_n(p, 4); p += 4; continue;
+                default: return false;  // 0xc1 (never used)
+            }
+        }
+        if ((u64)(e - p) < n) return false;
+        p += n;
+    }
+    return true;
+}
+
+// legend index of a 40-byte hex at p (LDS table), -1 if unknown
+__device__ __forceinline__ int leg_lookup_bytes(const u8* p, const u32* s_leg, int n_leg) {
+    for (int l = 0; l < n_leg; l++) {
+        bool eq = true;
+        for (int j = 0; j < 40 && eq; j++) eq = p[j] == (u8)(s_leg[l * 10 + (j >> 2)] >> (8 * (j & 3)));
+        if (eq) return l;
+    }
+    return -1;
+}
+
+// geometry payload (GPKG bytes) of a feature blob, byte-wise: rc 1 found (offset, length in the
+// blob), 0 null geometry / no geometry column (MATCHING), -1 fallback.  The rare path: kept out of
+// line, its result returned in registers.
+struct GeomLoc {
+    int rc;
+    u32 off;
+    u64 len;
+};
+__device__ __noinline__ GeomLoc find_geom_slow(const u8* b, u64 len, const u32* s_leg, const i16* s_gidx, int n_leg) {
+    const u8 *p = b, *e = b + len;
+    if (len < 2 || *p++ != 0x92) return GeomLoc{-1, 0, 0};
+    // legend hex: a 40-byte str
+    u32 sl;
+    const u8 c = *p++;
+    if ((c & 0xe0) == 0xa0) sl = c & 31;
+    else if (c == 0xd9 && p < e) sl = *p++;
+    else if (c == 0xda && p + 2 <= e) { sl = be_n(p, 2); p += 2; }
+    else return GeomLoc{-1, 0, 0};
+    if (sl != 40 || p + 40 > e) return GeomLoc{-1, 0, 0};
+    const int l = leg_lookup_bytes(p, s_leg, n_leg);
+    if (l < 0) return GeomLoc{-1, 0, 0};
+    p += 40;
+    const int gi = s_gidx[l];
+    if (gi < 0) return GeomLoc{0, 0, 0};
+    if (p >= e) return GeomLoc{-1, 0, 0};
+    u32 cnt;
+    const u8 h = *p++;
+    if ((h & 0xf0) == 0x90) cnt = h & 15;
+    else if (h == 0xdc && p + 2 <= e) { cnt = be_n(p, 2); p += 2; }
+    else if (h == 0xdd && p + 4 <= e) { cnt = be_n(p, 4); p += 4; }
+    else return GeomLoc{-1, 0, 0};
+    if ((u32)gi >= cnt) return GeomLoc{-1, 0, 0};
+    for (int k = 0; k < gi; k++)
+        if (!mp_skip(p, e)) return GeomLoc{-1, 0, 0};
+    if (p >= e) return GeomLoc{-1, 0, 0};
+    const u8 v = *p++;
+    if (v == 0xc0) return GeomLoc{0, 0, 0};
+    u64 n;
+    switch (v) {
+        case 0xd4: n = 1; break;
+        case 0xd5: n = 2; break;
+        case 0xd6: n = 4; break;
+        case 0xd7: n = 8; break;
+        case 0xd8: n = 16; break;
+        case 0xc7: if (p + 1 > e) return GeomLoc{-1, 0, 0}; n = be_n(p, 1); p += 1; break;
+        case 0xc8: if (p + 2 > e) return GeomLoc{-1, 0, 0}; n = be_n(p, 2); p += 2; break;
+        case 0xc9: if (p + 4 > e) return GeomLoc{-1, 0, 0}; n = be_n(p, 4); p += 4; break;
+        default: return GeomLoc{-1, 0, 0};  // not an ext value
+    }
+    if (p >= e || *p++ != 'G') return GeomLoc{-1, 0, 0};
+    if ((u64)(e - p) < n) return GeomLoc{-1, 0, 0};
+    return GeomLoc{1, (u32)(p - b), n};
+}
+
+// compile-time loop: f(integral_constant<I>) for I in [I0, N) — register-window indices stay
+// constants from the first optimisation pass on, so the windows never spill to scratch
+template <int I, int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, N>(f);
+    }
+}
+
+// match code of one geometry given its decoded envelope state
+__device__ __forceinline__ int geom_code(const GfArgs& a, GHit& h, u8 hflags) {
+    h.empty = h.r >= 0 && (hflags & 0x10);
+    double env[4];
+    bool have = false;
+    if (h.r == 1) {
+        have = true;
+    } else if (h.r >= 0) {
+        if (h.empty || h.pc == 0) return GF_NON;  // empty geometry (or empty point): Intersects is false
+        have = h.pc == 1;  // the point's envelope (decode_side moved it into e)
+    }
+    env[0] = h.e[0]; env[1] = h.e[1]; env[2] = h.e[2]; env[3] = h.e[3];
+    if (!have) return GF_FALLBACK;
+    int x = range_ov(a.f0, a.f1, env[0], env[1]);
+    if (x > 0) x = range_ov(a.f2, a.f3, env[2], env[3]);
+    if (x < 0) return GF_FALLBACK;  // inverted envelope: the reference raises
+    if (x == 0) return GF_NON;
+    if (a.rect && a.f0 <= env[0] && env[1] <= a.f1 && a.f2 <= env[2] && env[3] <= a.f3) return GF_MATCH;
+    return GF_CAND;
+}
+
+// decode side s's blob `bi` for one lane
+__device__ __forceinline__ void decode_side(const GfArgs& a, int s, u32 bi, const u32* s_leg, const i16* s_gidx, GHit& h) {
+    typedef const __attribute__((address_space(1))) u32x4* gx4;
+    h.r = -1;
+    h.pc = -1;
+    h.empty = false;
+    if (bi == KD_NONE) { h.code = GF_NONE; return; }
+    if ((u64)bi >= a.nblob[s]) { h.code = GF_FALLBACK; return; }
+    const u64 o = a.off[s][bi], len = a.off[s][bi + 1] - o;
+    const u8* b = a.data[s] + o;
+    const u64 arena_end = (u64)a.data[s] + a.off[s][a.nblob[s]];
+    const int n_leg = a.n_leg[s];
+    const u8* gp = nullptr;
+    u64 glen = 0;
+    u8 hflags = 0;
+    bool fast = false, located = false;
+    const u64 a0 = (u64)b, a4 = a0 & ~(u64)3;
+    if (len >= 52 && a4 + 112 <= arena_end) {
+        u32 w[28];
+        sfor<0, 7>([&](auto k) {
+            const u32x4 v = *(gx4)(a4 + 16 * k);
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        });
+        const u32 sh = (u32)(a0 - a4);
+        u32 rr[27];
+        sfor<0, 27>([&](auto j) { rr[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh); });
+        // [0x92, 0xd9, 40, hex x40, values header]
+        if ((rr[0] & 0xFFFFFFu) == 0x28d992u) {
+            u32 hx[10];
+            sfor<0, 10>([&](auto j) { hx[j] = __builtin_amdgcn_alignbyte(rr[j + 1], rr[j], 3); });
+            int l = -1;
+            for (int q = 0; q < n_leg && l < 0; q++) {
+                bool eq = true;
+                sfor<0, 10>([&](auto j) { eq &= hx[j] == s_leg[q * 10 + j]; });
+                if (eq) l = q;
+            }
+            const u32 ah = rr[10] >> 24;  // byte 43
+            const int p = (ah & 0xf0) == 0x90 ? 44 : ah == 0xdc ? 46 : -1;
+            if (l < 0) { h.code = GF_FALLBACK; return; }  // unknown legend: the reference raises KeyError
+            const int gi = s_gidx[l];
+            if (gi < 0) { h.code = GF_MATCH; return; }  // this legend has no geometry column: value None
+            if (gi == 0 && p > 0) {
+                const u32 w11 = rr[11];
+                const u32 v = p == 44 ? (w11 & 0xff) : ((w11 >> 16) & 0xff);
+                if (v == 0xc0) { h.code = GF_MATCH; return; }  // null geometry
+                // ext header bytes p+1 .. p+5 (p = 44: bytes 45..49, p = 46: 47..51)
+                const u32 x0 = p == 44 ? __builtin_amdgcn_alignbyte(rr[12], rr[11], 1)
+                                       : __builtin_amdgcn_alignbyte(rr[12], rr[11], 3);
+                const u32 x1 = p == 44 ? __builtin_amdgcn_alignbyte(rr[13], rr[12], 1)
+                                       : __builtin_amdgcn_alignbyte(rr[13], rr[12], 3);
+                int q = -1;
+                u32 gl = 0, typ = 0;
+                if (v == 0xc7) { gl = x0 & 0xff; typ = (x0 >> 8) & 0xff; q = p + 3; }
+                else if (v == 0xc8) { gl = ((x0 & 0xff) << 8) | ((x0 >> 8) & 0xff); typ = (x0 >> 16) & 0xff; q = p + 4; }
+                else if (v == 0xc9) { gl = __builtin_bswap32(x0); typ = x1 & 0xff; q = p + 6; }
+                if (q > 0) {
+                    if (typ != 'G' || (u64)q + gl > len) { h.code = GF_FALLBACK; return; }
+                    located = true;
+                    gp = b + q;
+                    glen = gl;
+                    // GPKG window: 11 dwords from byte q (q in 47..52: dwords 11..13 + j)
+                    const int qd = q >> 2, qs = q & 3;  // qd in 11..13
+                    u32 rq[11];
+                    sfor<0, 11>([&](auto j) {
+                        const u32 a11 = rr[11 + j], a12 = rr[12 + j], a13 = rr[13 + j], a14 = rr[14 + j];
+                        const u32 lo = qd == 11 ? a11 : qd == 12 ? a12 : a13;
+                        const u32 hi = qd == 11 ? a12 : qd == 12 ? a13 : a14;
+                        rq[j] = __builtin_amdgcn_alignbyte(hi, lo, qs);
+                    });
+                    if (glen >= 8) {
+                        fast = env_fast(rq, glen, h.r, h.e, h.pc, h.pe);
+                        hflags = rq[0] >> 24;
+                    }
+                }
+            }
+        }
+    }
+    if (!located) {
+        const GeomLoc f = find_geom_slow(b, len, s_leg, s_gidx, n_leg);
+        if (f.rc < 0) { h.code = GF_FALLBACK; return; }
+        if (f.rc == 0) { h.code = GF_MATCH; return; }
+        gp = b + f.off;
+        glen = f.len;
+    }
+    if (!fast) {  // byte-wise GPKG decode (short or unusual geometry headers)
+        h.r = gpkg_env(gp, glen, h.e);
+        h.pc = -1;
+        if (h.r == 0 || h.r == 2) h.pc = point_env(gp, glen, h.pe);
+        if (h.r >= 0) hflags = gp[3];
+    }
+    if (h.r != 1 && h.pc >= 0) {  // one envelope from here on: the point's (x, x, y, y)
+        h.e[0] = h.pe[0]; h.e[1] = h.pe[1]; h.e[2] = h.pe[2]; h.e[3] = h.pe[3];
+    }
+    h.code = geom_code(a, h, hflags);
+}
+
+__global__ __launch_bounds__(GF_NT) void k_gf_match(GfArgs a) {
+    __shared__ u32 s_leg[2][GF_MAXLEG * 10];
+    __shared__ i16 s_gidx[2][GF_MAXLEG];
+    __shared__ u8 s_enc[GF_NT * 16];
+    __shared__ u8 s_ok[GF_NT];
+    __shared__ u32 s_wc[GF_NT / 64];
+    const int tid = threadIdx.x;
+    // legend tables: hex as little-endian dwords (compared with the realigned blob words)
+    for (int s = 0; s < 2; s++) {
+        for (int i = tid; i < a.n_leg[s]; i += GF_NT) s_gidx[s][i] = a.gidx[s][i];
+        for (int i = tid; i < a.n_leg[s] * 10; i += GF_NT) {
+            const u8* p = a.leg_hex[s] + 4 * i;
+            s_leg[s][i] = (u32)p[0] | (u32)p[1] << 8 | (u32)p[2] << 16 | (u32)p[3] << 24;
+        }
+    }
+    __syncthreads();
+    const u64 n = a.d_n ? *a.d_n : a.cap;
+    const int nb = a.bits / 2;
+    const double vmax = (double)((1ull << a.bits) - 1);
+    const u64 t0 = (u64)blockIdx.x * GF_TILE;
+    u32 kept = 0;
+    for (int r = 0; r < GF_ROUNDS; r++) {
+        const u64 d0 = t0 + (u64)r * GF_NT;
+        if (d0 >= n) break;  // block-uniform
+        const u64 d = d0 + tid;
+        bool keep = false;
+        u8 ok = 0;
+        if (a.enc)
+            for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
+        if (d < n) {
+            const u32 po = a.pairs[2 * d], pn = a.pairs[2 * d + 1];
+            GHit h;
+            decode_side(a, 0, po, s_leg[0], s_gidx[0], h);
+            const int co = h.code;
+            decode_side(a, 1, pn, s_leg[1], s_gidx[1], h);
+            const int cn = h.code;
+            keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
+            *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
+            if (a.enc && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
+                ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { s_enc[tid * nb + k] = v; });
+        }
+        const u64 bal = __ballot(keep);
+        kept += (u32)__popcll(bal);
+        if (a.enc) {  // index envelopes through LDS: contiguous dword stores
+            s_ok[tid] = ok;
+            __syncthreads();
+            const u32 cnt = (u32)(n - d0 < GF_NT ? n - d0 : GF_NT);
+            u8* dst = a.enc + d0 * nb;
+            const u32 bytes = cnt * nb;
+            if ((((u64)dst) & 3) == 0) {
+                const u32 nw = bytes >> 2;
+                for (u32 k = tid; k < nw; k += GF_NT) ((u32*)dst)[k] = ((const u32*)s_enc)[k];
+                for (u32 k = 4 * nw + tid; k < bytes; k += GF_NT) dst[k] = s_enc[k];
+            } else {
+                for (u32 k = tid; k < bytes; k += GF_NT) dst[k] = s_enc[k];
+            }
+            for (u32 k = tid; k < cnt; k += GF_NT) a.enc_ok[d0 + k] = s_ok[k];
+            __syncthreads();
+        }
+    }
+    if ((tid & 63) == 0) s_wc[tid >> 6] = kept;
+    __syncthreads();
+    if (tid == 0) {
+        u32 t = 0;
+        for (int w = 0; w < GF_NT / 64; w++) t += s_wc[w];
+        a.tile_cnt[blockIdx.x] = t;
+    }
+}
+
+// one block: exclusive scan of the tile counts in place, the total to *n_keep
+__global__ __launch_bounds__(1024) void k_gf_scan(u32* __restrict__ cnt, u32 ntiles, u64* __restrict__ n_keep) {
+    __shared__ u32 s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    u32 carry = 0;
+    for (u32 base = 0; base < ntiles; base += 1024) {
+        const u32 i = base + tid;
+        const u32 x = i < ntiles ? cnt[i] : 0;
+        u32 s = x;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane == 63) s_w[wid] = s;
+        __syncthreads();
+        u32 wp = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            if (w < wid) wp += s_w[w];
+            all += s_w[w];
+        }
+        if (i < ntiles) cnt[i] = carry + wp + s - x;
+        carry += all;
+        __syncthreads();
+    }
+    if (tid == 0) *n_keep = carry;
+}
+
+// kept delta indices in key order: tile base (scanned) + rank inside the tile
+__global__ __launch_bounds__(GF_NT) void k_gf_place(const u8* __restrict__ match, u64 cap, const u64* __restrict__ d_n,
+                                                    const u32* __restrict__ tile_base, u32* __restrict__ keep) {
+    __shared__ u32 s_w[GF_NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 n = d_n ? *d_n : cap;
+    const u64 t0 = (u64)blockIdx.x * GF_TILE;
+    u32 run = tile_base[blockIdx.x];
+    for (int r = 0; r < GF_ROUNDS; r++) {
+        const u64 d0 = t0 + (u64)r * GF_NT;
+        if (d0 >= n) break;
+        const u64 d = d0 + tid;
+        bool k = false;
+        if (d < n) {
+            const u16 m = *(const u16*)(match + 2 * d);
+            const u32 co = m & 0xff, cn = m >> 8;
+            k = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
+        }
+        const u64 bal = __ballot(k);
+        if (lane == 0) s_w[wid] = (u32)__popcll(bal);
+        __syncthreads();
+        u32 wp = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < GF_NT / 64; w++) {
+            if (w < wid) wp += s_w[w];
+            all += s_w[w];
+        }
+        if (k) keep[run + wp + __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0))] = (u32)d;
+        run += all;
+        __syncthreads();
+    }
+}
+
+}  // namespace kd
+
+using namespace kd;
+
+extern "C" int kd_geom_filter(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_blobs* new_blobs, const uint32_t* pairs,
+                              uint64_t n, const uint64_t* d_n, uint32_t pairs_mem, const kd_geom_cols* cols,
+                              const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
+                              uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem) {
+    KD_CHECK(ctx && old_blobs && new_blobs && cols && filt_env && match && keep && n_keep, "kd_geom_filter: NULL argument");
+    KD_CHECK(n == 0 || pairs, "kd_geom_filter: pairs NULL");
+    KD_CHECK(d_n == nullptr || (out_mem == KD_MEM_DEVICE && pairs_mem == KD_MEM_DEVICE),
+             "kd_geom_filter: a device count needs device pairs and outputs");
+    KD_CHECK(filt_env[0] <= filt_env[1] && filt_env[2] <= filt_env[3], "kd_geom_filter: inverted filter envelope");
+    KD_CHECK(!enc || (enc_ok && bits >= 2 && bits <= 32 && bits % 2 == 0), "kd_geom_filter: bits must be even and <= 32");
+    KD_CHECK(cols->n_leg_old >= 0 && cols->n_leg_new >= 0, "kd_geom_filter: legend counts");
+    if (cols->n_leg_old > GF_MAXLEG || cols->n_leg_new > GF_MAXLEG) {
+        set_error("kd_geom_filter: more than %d legends on a side", GF_MAXLEG);
+        return KD_EUNSUPPORTED;
+    }
+    KD_CHECK(old_blobs->mem == new_blobs->mem, "kd_geom_filter: both arenas in the same memory");
+    KD_HIP(hipSetDevice(ctx->device));
+    int rc;
+    GfArgs a{};
+    const kd_blobs* bl[2] = {old_blobs, new_blobs};
+    const char* tag[2][2] = {{"gf.od", "gf.oo"}, {"gf.nd", "gf.no"}};
+    for (int s = 0; s < 2; s++) {
+        const kd_blobs* B = bl[s];
+        const void *dd, *doff;
+        const u64 bytes = B->mem == KD_MEM_HOST ? (B->n ? B->off[B->n] : 0) : 0;
+        if ((rc = stage_in(ctx, tag[s][1], B->off, (B->n + 1) * 8, B->mem, &doff))) return rc;
+        if ((rc = stage_in(ctx, tag[s][0], B->data, bytes ? bytes : 1, B->mem, &dd))) return rc;
+        a.data[s] = (const u8*)dd;
+        a.off[s] = (const u64*)doff;
+        a.nblob[s] = B->n;
+    }
+    // legend tables (host memory, small)
+    const int nl[2] = {cols->n_leg_old, cols->n_leg_new};
+    const uint8_t* lh[2] = {cols->leg_old_hex, cols->leg_new_hex};
+    const int16_t* gx[2] = {cols->gidx_old, cols->gidx_new};
+    const char* ltag[2][2] = {{"gf.lo", "gf.go"}, {"gf.ln", "gf.gn"}};
+    for (int s = 0; s < 2; s++) {
+        KD_CHECK(nl[s] == 0 || (lh[s] && gx[s]), "kd_geom_filter: legend table NULL");
+        const void *dl, *dg;
+        static const u8 zero16[16] = {0};
+        if ((rc = stage_in(ctx, ltag[s][0], nl[s] ? (const void*)lh[s] : zero16, nl[s] ? (size_t)nl[s] * 40 : 16,
+                           KD_MEM_HOST, &dl)))
+            return rc;
+        if ((rc = stage_in(ctx, ltag[s][1], nl[s] ? (const void*)gx[s] : zero16, nl[s] ? (size_t)nl[s] * 2 : 16,
+                           KD_MEM_HOST, &dg)))
+            return rc;
+        a.leg_hex[s] = (const u8*)dl;
+        a.gidx[s] = (const i16*)dg;
+        a.n_leg[s] = nl[s];
+    }
+    const void* dp;
+    if ((rc = stage_in(ctx, "gf.pairs", n ? (const void*)pairs : nullptr, n ? n * 8 : 0, pairs_mem, &dp))) return rc;
+    const u64 tiles = (n + GF_TILE - 1) / GF_TILE;
+    KD_CHECK(tiles < (1ull << 31), "kd_geom_filter: too many deltas");
+    u8* dm = match;
+    u32* dk = keep;
+    u8 *de = enc, *dok = enc_ok;
+    const int nb = bits / 2;
+    void *t_cnt, *t_nk;
+    if ((rc = ensure(ctx, "gf.tiles", (tiles + 1) * 4, &t_cnt)) || (rc = ensure(ctx, "gf.nk", 8, &t_nk))) return rc;
+    if (out_mem == KD_MEM_HOST) {
+        void *x, *y, *z = nullptr, *w = nullptr;
+        if ((rc = ensure(ctx, "gf.match", 2 * n + 2, &x)) || (rc = ensure(ctx, "gf.keep", 4 * n + 4, &y))) return rc;
+        if (enc && ((rc = ensure(ctx, "gf.enc", n * nb + 4, &z)) || (rc = ensure(ctx, "gf.encok", n + 4, &w)))) return rc;
+        dm = (u8*)x; dk = (u32*)y; de = (u8*)z; dok = (u8*)w;
+    }
+    a.pairs = (const u32*)dp;
+    a.cap = n;
+    a.d_n = d_n;
+    a.f0 = filt_env[0]; a.f1 = filt_env[1]; a.f2 = filt_env[2]; a.f3 = filt_env[3];
+    a.rect = (flags & KD_GF_RECT) ? 1 : 0;
+    a.bits = enc ? bits : 2;
+    a.match = dm;
+    a.enc = enc ? de : nullptr;
+    a.enc_ok = enc ? dok : nullptr;
+    a.tile_cnt = (u32*)t_cnt;
+    KD_HIP(hipMemsetAsync(t_nk, 0, 8, ctx->stream));
+    if (tiles) {
+        if ((rc = launch(ctx, "k_gf_match", [&] {
+                 hipLaunchKernelGGL(k_gf_match, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a);
+             })))
+            return rc;
+        if ((rc = launch(ctx, "k_gf_scan", [&] {
+                 hipLaunchKernelGGL(k_gf_scan, dim3(1), dim3(1024), 0, ctx->stream, (u32*)t_cnt, (u32)tiles, (u64*)t_nk);
+             })))
+            return rc;
+        if ((rc = launch(ctx, "k_gf_place", [&] {
+                 hipLaunchKernelGGL(k_gf_place, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, (const u8*)dm, n, d_n,
+                                    (const u32*)t_cnt, dk);
+             })))
+            return rc;
+    }
+    if (out_mem == KD_MEM_DEVICE) {
+        KD_HIP(hipMemcpyAsync(n_keep, t_nk, 8, hipMemcpyDeviceToDevice, ctx->stream));
+        return KD_OK;
+    }
+    u64 nk = 0;
+    KD_HIP(hipMemcpyAsync(&nk, t_nk, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KD_HIP(hipStreamSynchronize(ctx->stream));
+    if (n) {
+        KD_HIP(hipMemcpyAsync(match, dm, 2 * n, hipMemcpyDeviceToHost, ctx->stream));
+        if (nk) KD_HIP(hipMemcpyAsync(keep, dk, 4 * nk, hipMemcpyDeviceToHost, ctx->stream));
+        if (enc) {
+            KD_HIP(hipMemcpyAsync(enc, de, n * nb, hipMemcpyDeviceToHost, ctx->stream));
+            KD_HIP(hipMemcpyAsync(enc_ok, dok, n, hipMemcpyDeviceToHost, ctx->stream));
+        }
+    }
+    KD_HIP(hipStreamSynchronize(ctx->stream));
+    *n_keep = nk;
+    return prof_flush(ctx);
+}

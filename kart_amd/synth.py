@@ -283,7 +283,7 @@ def c3_plan(pk, n, seed=C3_SEED):
     return np.where(h < 400, 1, np.where(h < 800, 2, np.where(h < 900, 3, 0))).astype(np.uint8)
 
 
-def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20):
+def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False):
     """C3: n int-PK MULTIPOLYGON features (pks 0..n-1) and n // 100 inserts (pks n..), 10 % edits =
     4 % geometry updates + 4 % attribute updates + 1 % deletes + 1 % inserts, edits
     picked by a hash of the pk (c3_plan).
@@ -292,7 +292,8 @@ def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20):
     is one bucket-range shard of the same layer (bench.py --gpus N splits it this way).
     Feature blobs are materialised for the updated features only (both versions): the diff reads no
     other blob — classification needs only keys and OIDs — so every other entry has a zero-length
-    blob in the arena."""
+    blob in the arena.  ``delta_blobs``: also the deleted features' base blobs and the inserted
+    features' target blobs (what a spatially filtered diff reads: C5)."""
     schema = Schema.from_column_dicts(POLYGON_SCHEMA)
     legend = Legend(["p-fid"], [c["id"] for c in POLYGON_SCHEMA[1:]])
     lh = legend.hexhash()
@@ -326,9 +327,19 @@ def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20):
             offs.append(o[1:] + offs[-1][-1])
         return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), np.concatenate(offs)
 
-    bd, bo = blobs(pks[ub], np.zeros(ub.size, np.uint64), np.zeros(ub.size, np.uint64))
-    td, to = blobs(pks[ub], gver[ub].astype(np.uint64), aver[ub].astype(np.uint64))
-    bb = _sparse_arena(pks.shape[0], ub, bd, bo)
+    bsel, tpk, tgv, tav = ub, pks[ub], gver[ub].astype(np.uint64), aver[ub].astype(np.uint64)
+    if delta_blobs:
+        bsel = np.nonzero(upd | (plan == 3))[0]
+        ti = np.concatenate([ut, np.arange(t_pk.shape[0] - ins_pk.shape[0], t_pk.shape[0])])
+        o = np.argsort(ti, kind="stable")
+        ut = ti[o]
+        z = np.zeros(ins_pk.shape[0], np.uint64)
+        tpk = np.concatenate([tpk, ins_pk])[o]
+        tgv = np.concatenate([tgv, z])[o]
+        tav = np.concatenate([tav, z])[o]
+    bd, bo = blobs(pks[bsel], np.zeros(bsel.size, np.uint64), np.zeros(bsel.size, np.uint64))
+    td, to = blobs(tpk, tgv, tav)
+    bb = _sparse_arena(pks.shape[0], bsel, bd, bo)
     tb = _sparse_arena(t_pk.shape[0], ut, td, to)
     return Layer(base, target, bb, tb, schema, {lh: legend}, int(ins_pk.shape[0]), int(ub.size),
                  int(np.count_nonzero(plan == 3)))

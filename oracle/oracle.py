@@ -60,6 +60,8 @@ def C():
         L.kdo_index_envelope.argtypes = [_vp, _vp]
         L.kdo_gpkg_envelope.restype = ctypes.c_int
         L.kdo_gpkg_envelope.argtypes = [_vp, ctypes.c_uint64, _vp]
+        L.kdo_point_envelope.restype = ctypes.c_int
+        L.kdo_point_envelope.argtypes = [_vp, ctypes.c_uint64, _vp]
         L.kdo_int_pk_key.restype = ctypes.c_int
         L.kdo_int_pk_key.argtypes = [ctypes.c_int64, ctypes.c_uint64, _vp]
         L.kdo_decode_int_filename.restype = ctypes.c_int
@@ -145,6 +147,98 @@ def envelope_overlap(enc, bits, q):
         r = C().kdo_envelope_overlap(_p(np.ascontiguousarray(enc[i])), bits, _p(qa))
         out[i] = 2 if r < 0 else r
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# spatially filtered diff restated (kart/base_diff_writer.py:279-329 + SpatialFilter.matches,
+# kart/spatial_filter/__init__.py:534-605), envelope part only: per side 0 NON_MATCHING,
+# 1 CANDIDATE (exact Intersects outstanding), 2 MATCHING, 3 FALLBACK (OGR / malformed), 4 NONEXISTENT
+GF_NON, GF_CAND, GF_MATCH, GF_FALLBACK, GF_NONE = range(5)
+
+
+class _GeomExt(bytes):
+    pass
+
+
+def _gf_hook(code, data):
+    return _GeomExt(data) if code == ord("G") else msgpack.ExtType(code, data)
+
+
+def sf_envelope_code(g, filt_env, rect):
+    """SpatialFilter.matches for a GPKG geometry (bytes or None), without the exact test"""
+    if g is None:
+        return GF_MATCH  # geometry None: MATCHING (:549-551)
+    gb = np.frombuffer(bytes(g), np.uint8) if len(g) else np.zeros(1, np.uint8)
+    env = np.zeros(4)
+    r = C().kdo_gpkg_envelope(_p(gb), len(g), _p(env))
+    if r < 0:
+        return GF_FALLBACK  # the reference raises (ValueError / NotImplementedError)
+    if r == 0 and g[3] & 0x10:
+        return GF_NON  # empty: envelope (0,0,0,0) from OGR, then Intersects(empty) is False
+    if r != 1:  # no stored envelope (or NaN): OGR's envelope — a point's is (x, x, y, y)
+        pc = C().kdo_point_envelope(_p(gb), len(g), _p(env))
+        if pc == 0:
+            return GF_NON  # empty point
+        if pc < 0:
+            return GF_FALLBACK  # needs OGR
+    fe = np.asarray(filt_env, np.float64)
+    x = C().kdo_bbox_intersects(_p(fe), _p(env))
+    if x < 0:
+        return GF_FALLBACK
+    if x == 0:
+        return GF_NON
+    if rect and fe[0] <= env[0] and env[1] <= fe[1] and fe[2] <= env[2] and env[3] <= fe[3]:
+        return GF_MATCH  # inside a rectangular filter: Intersects is certain
+    return GF_CAND
+
+
+def feature_geometry(blob, gidx_by_legend):
+    """(status, GPKG bytes | None) of a feature blob: status 0 ok, 3 fallback (unknown legend,
+    malformed, geometry value not an ext 'G')"""
+    try:
+        legend, values = msgpack.unpackb(bytes(blob), raw=False, ext_hook=_gf_hook)
+    except Exception:
+        return GF_FALLBACK, None
+    if legend not in gidx_by_legend:
+        return GF_FALLBACK, None
+    gi = gidx_by_legend[legend]
+    if gi < 0:
+        return 0, None
+    if gi >= len(values):
+        return GF_FALLBACK, None
+    v = values[gi]
+    if v is None:
+        return 0, None
+    if not isinstance(v, _GeomExt):
+        return GF_FALLBACK, None
+    return 0, bytes(v)
+
+
+def geom_filter(old_data, old_off, new_data, new_off, pairs, old_cols, new_cols, filt_env, rect, bits=20):
+    """codes [n, 2], kept delta indices, new-side index envelopes (enc [n, bits/2], enc_ok [n]).
+    old_cols/new_cols: {legend hex: geometry value index | -1}."""
+    n = pairs.shape[0]
+    codes = np.zeros((n, 2), np.uint8)
+    geoms_new = []
+    for d in range(n):
+        for s, (data, off, cols) in enumerate(((old_data, old_off, old_cols), (new_data, new_off, new_cols))):
+            bi = int(pairs[d, s])
+            g = None
+            if bi == NONE:
+                codes[d, s] = GF_NONE
+            else:
+                st, g = feature_geometry(data[int(off[bi]):int(off[bi + 1])].tobytes(), cols)
+                codes[d, s] = st if st else sf_envelope_code(g, filt_env, rect)
+            if s == 1:
+                geoms_new.append(g if codes[d, 1] not in (GF_NONE, GF_FALLBACK) else None)
+    keep = np.nonzero(((codes >= 1) & (codes <= 3)).any(axis=1))[0].astype(np.uint32)
+    gb = [g or b"" for g in geoms_new]
+    goff = np.zeros(n + 1, np.uint64)
+    if n:
+        goff[1:] = np.cumsum([len(g) for g in gb])
+    gdata = np.frombuffer(b"".join(gb), np.uint8) if n else np.zeros(0, np.uint8)
+    _, enc, ok, _ = envelope_batch(gdata, goff, filt_env, bits)
+    return codes, keep, enc, ok
 
 
 # ------------------------------------------------------------------------------------------
