@@ -18,10 +18,12 @@ CPU; no device memory, stream or collective of the measured path goes through to
 torch is not imported at all.
 
 --workload c2 (configs[1]): a 10M-point layer per GPU, 1 % upd/del/ins (weak scaling at N>1);
-c4 (configs[3]): 50M-row string-PK three-way merge classification; c5 (configs[4], scaled):
-spatial-filter envelopes + EnvelopeEncoder + overlap; c6: hex WKB of every geometry.
+c4 (configs[3]): 50M-row string-PK three-way merge classification; c5 (configs[4]): the spatially
+filtered diff of the 100M-feature polygon layer (classify2 + per-delta geometry envelope filter +
+EnvelopeEncoder); c5env: the envelope kernels alone over a raw geometry arena; c6:
+hex WKB of every geometry.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c6] [--n UNITS]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c5env|c6] [--n UNITS]
                        [--no-cpu-baseline] [--no-host-timing]
 """
 import argparse
@@ -49,10 +51,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "c6"])
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "c5env", "c6"])
     ap.add_argument("--n", type=int, default=0,
                     help="units (c3: polygons of the whole layer, 100M; c2: points per GPU, 10M; c4: rows, 50M; "
-                         "c5/c6: geometries, 20M)")
+                         "c5: features of the filtered layer, 100M; c5env/c6: geometries, 20M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-timing", action="store_true", help="skip the host pack / H2D timings")
     ap.add_argument("--unordered", action="store_true",
@@ -66,7 +68,8 @@ def parse():
                          "so the events do not inflate the step time)")
     a = ap.parse_args()
     if not a.n:
-        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c4": 50_000_000, "c5": 20_000_000, "c6": 20_000_000}[a.workload]
+        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c4": 50_000_000, "c5": 100_000_000, "c5env": 20_000_000,
+               "c6": 20_000_000}[a.workload]
     if a.traffic_json is None:
         a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
     return a
@@ -420,6 +423,114 @@ def host_timing(eng, L, h2d_s, h2d_bytes):
 
 # ---------------------------------------------------------------------------------------------
 def run_c5(args, H):
+    """C5 (configs[4]): the spatially filtered diff of a 100M-feature layer — the C3 polygon layer,
+    one step = classify2 (k_partition2 / k_join2 / k_place2) + kd_geom_filter over its key-ordered
+    delta list (each delta's old and new geometry located in its feature blob, GPKG envelope bbox-
+    tested against the filter in FP64, matching deltas compacted, the new side's EnvelopeEncoder
+    index envelope written), all on the device (BaseDiffWriter.filtered_ds_feature_deltas)."""
+    import types
+
+    from kart_amd import synth
+    from kart_amd.device import FilterPipeline
+    from kart_amd.spatial import GeomCols
+
+    n, bits = args.n, 20
+    if H.world > 1:
+        n_pks = n + n // 100
+        lo, hi = synth.shard_pk_range(H.rank, H.world, n_pks)
+    else:
+        lo, hi = 0, None
+    t0 = time.time()
+    L = synth.polygons_layer(n, lo=lo, hi=hi, delta_blobs=True)
+    log(f"[rank {H.rank}] generated {L.base.n}+{L.target.n} entries in {time.time() - t0:.1f}s")
+    ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
+    cols = GeomCols(ver, ver, "geom", "geom")
+    eng = engine_for(H)
+    pipe = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits)
+    for _ in range(max(1, args.warmup)):
+        pipe.step()
+    eng.sync()
+    counts, delta, codes, keep, enc, enc_ok = pipe.results()
+    plan = (L.n_insert, L.n_update, L.n_delete)
+    if not args.no_check:
+        assert (counts["inserts"], counts["updates"], counts["deletes"]) == plan, (counts, plan)
+        # size-independent: kept = deltas with a side that may match, in delta order; codes in range
+        may = ((codes >= 1) & (codes <= 3)).any(axis=1)
+        assert np.array_equal(keep, np.nonzero(may)[0]), "kept deltas differ from the per-delta codes"
+        assert codes.max() <= 4 and not (codes == 3).any(), "fallback codes on synthetic polygons"
+        assert ((delta[:, 0] == 0xFFFFFFFF) == (codes[:, 0] == 4)).all() and \
+            ((delta[:, 1] == 0xFFFFFFFF) == (codes[:, 1] == 4)).all()
+    eng.prof_reset()
+    eng.prof_select(None if args.time_all else ["k_gf_match"])
+    eng.prof_enable(not args.no_events)
+    elapsed = timed(H, eng, pipe.step, args.steps)
+    eng.prof_enable(False)
+    kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_gf_match", "k_gf_scan", "k_gf_place"))
+    n_pairs = L.base.n + L.n_insert
+    total_pairs = sum(H.allgather(n_pairs))
+    # algorithmic bytes per k_gf_match launch: the delta pairs (8 B); per present side its offsets
+    # (16 B) and the blob head up to the end of the GPKG envelope (<= 96 B); codes (2 B) + index
+    # envelope (bits/2 + 1 B) written per delta
+    ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
+    head = 0
+    for col, off in ((delta[:, 0], ob_off), (delta[:, 1], nb_off)):
+        pres = col[col != 0xFFFFFFFF].astype(np.int64)
+        head += int(np.minimum(off[pres + 1] - off[pres], 96).sum()) + 16 * pres.size
+    nd = counts["deltas"]
+    alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
+    roof = roofline(kern, "k_gf_match", alg, args.traffic_json, n)
+    cpu = None
+    if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_filter(L, delta, codes, keep, enc, enc_ok, args, bits)
+    eng.close()
+    return {
+        "metric": METRIC, "value": round(total_pairs * args.steps / elapsed / 1e6, 2), "unit": "M feature-pairs/s",
+        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong" if H.world > 1 else "weak", "vs_baseline": None,
+        "dtype": "u8/u64 (integer join) + f64 (envelopes, EnvelopeEncoder)",
+        "data": "synthetic (the C3 MULTIPOLYGON layer; blobs materialised for every delta's old/new version)",
+        "config": {"workload": f"C5: spatially filtered diff of ONE {n}-feature polygon layer"
+                               f"{f' split into {H.world} bucket-range shards' if H.world > 1 else ''}: classify2 + "
+                               "per-delta geometry envelope filter + EnvelopeEncoder of the new side",
+                   "features": n, "pairs_per_step": total_pairs, "deltas_per_step": sum(H.allgather(nd)),
+                   "kept_per_step": sum(H.allgather(counts["kept"])), "bits": bits, "filter": list(synth.C5_FILTER),
+                   "parallelism": f"bucket-range shards x{H.world} (counts per rank, no exchange)"},
+        "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
+        "roofline": roof, "cpu_baseline": cpu,
+    }
+
+
+def cpu_baseline_filter(L, delta, codes, keep, enc, enc_ok, args, bits):
+    """the oracle's classify2 + geom_filter restatement on a bounded sample (1 thread, Python +
+    C): the first deltas of the layer; it doubles as a bit-exact check of the device results"""
+    O = oracle()
+    m = min(delta.shape[0], 20000)
+    cols = {h: 0 for h in L.legends}
+    (od, oo), (nd, no) = L.base_blobs, L.target_blobs
+    t0 = time.perf_counter()
+    oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta[:m], cols, cols, synth_filter(), False, bits)
+    dt = time.perf_counter() - t0
+    if not args.no_check:
+        assert np.array_equal(codes[:m], oc), "kd_geom_filter codes differ from the oracle"
+        assert np.array_equal(keep[keep < m], okeep), "kept deltas differ from the oracle"
+        assert np.array_equal(enc_ok[:m], ook) and np.array_equal(enc[:m][ook == 1], oenc[ook == 1])
+    rate = m / dt / 1e6
+    return {"value": round(rate, 4), "unit": "M deltas/s", "cores": 1, "kind": "port",
+            "sample": f"first {m} deltas of the layer: oracle geom_filter (msgpack decode + kd_oracle.c envelope, "
+                      f"bbox, EnvelopeEncoder), 1 thread, {dt:.1f}s; the classify2 leg is C2/C3's baseline"}
+
+
+def synth_filter():
+    from kart_amd import synth
+
+    return synth.C5_FILTER
+
+
+# ---------------------------------------------------------------------------------------------
+def run_c5env(args, H):
+    """k_envelopes + k_env_overlap over a raw GPKG geometry arena (the spatial-index envelope
+    kernels alone, no diff)"""
     import ctypes
 
     from kart_amd import _native as N
@@ -491,8 +602,8 @@ def run_c5(args, H):
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64 (envelopes, EnvelopeEncoder) + u8",
         "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
-        "config": {"workload": f"C5 (scaled to {n} geometries per GPU): spatial-filter envelopes + "
-                               "EnvelopeEncoder + encoded-envelope overlap",
+        "config": {"workload": f"C5-envelopes: {n} raw GPKG geometries per GPU: spatial-filter envelopes + "
+                               "EnvelopeEncoder + encoded-envelope overlap (no diff)",
                    "geoms_per_gpu": n, "points": npt, "bits": bits, "filter": list(synth.C5_FILTER),
                    "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
@@ -654,7 +765,7 @@ def main():
     args = parse()
     H = Harness()
     out = {"c2": lambda a, h: run_diff(a, h, polygons=False), "c3": lambda a, h: run_diff(a, h, polygons=True),
-           "c4": run_c4, "c5": run_c5, "c6": run_c6}[args.workload](args, H)
+           "c4": run_c4, "c5": run_c5, "c5env": run_c5env, "c6": run_c6}[args.workload](args, H)
     if H.rank == 0:
         print(json.dumps(out), flush=True)
     H.close()

@@ -210,16 +210,17 @@ __device__ __forceinline__ int geom_code(const GfArgs& a, GHit& h, u8 hflags) {
 }
 
 // decode side s's blob `bi` for one lane
-__device__ __forceinline__ void decode_side(const GfArgs& a, int s, u32 bi, const u32* s_leg, const i16* s_gidx, GHit& h) {
+// (o, len): the blob's arena offset and length, loaded by the caller for both sides up front (the
+// second side's offset loads are not serialised behind the first side's decode)
+__device__ __forceinline__ void decode_side(const GfArgs& a, int s, u32 bi, u64 o, u64 len, u64 arena_end,
+                                            const u32* s_leg, const i16* s_gidx, GHit& h) {
     typedef const __attribute__((address_space(1))) u32x4* gx4;
     h.r = -1;
     h.pc = -1;
     h.empty = false;
     if (bi == KD_NONE) { h.code = GF_NONE; return; }
     if ((u64)bi >= a.nblob[s]) { h.code = GF_FALLBACK; return; }
-    const u64 o = a.off[s][bi], len = a.off[s][bi + 1] - o;
     const u8* b = a.data[s] + o;
-    const u64 arena_end = (u64)a.data[s] + a.off[s][a.nblob[s]];
     const int n_leg = a.n_leg[s];
     const u8* gp = nullptr;
     u64 glen = 0;
@@ -325,6 +326,7 @@ __global__ __launch_bounds__(GF_NT) void k_gf_match(GfArgs a) {
     const int nb = a.bits / 2;
     const double vmax = (double)((1ull << a.bits) - 1);
     const u64 t0 = (u64)blockIdx.x * GF_TILE;
+    const u64 end0 = (u64)a.data[0] + a.off[0][a.nblob[0]], end1 = (u64)a.data[1] + a.off[1][a.nblob[1]];
     u32 kept = 0;
     for (int r = 0; r < GF_ROUNDS; r++) {
         const u64 d0 = t0 + (u64)r * GF_NT;
@@ -336,10 +338,13 @@ __global__ __launch_bounds__(GF_NT) void k_gf_match(GfArgs a) {
             for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
         if (d < n) {
             const u32 po = a.pairs[2 * d], pn = a.pairs[2 * d + 1];
+            const bool vo = (u64)po < a.nblob[0], vn = (u64)pn < a.nblob[1];
+            const u64 oo = vo ? a.off[0][po] : 0, oe = vo ? a.off[0][po + 1] : 0;
+            const u64 no = vn ? a.off[1][pn] : 0, ne = vn ? a.off[1][pn + 1] : 0;
             GHit h;
-            decode_side(a, 0, po, s_leg[0], s_gidx[0], h);
+            decode_side(a, 0, po, oo, oe - oo, end0, s_leg[0], s_gidx[0], h);
             const int co = h.code;
-            decode_side(a, 1, pn, s_leg[1], s_gidx[1], h);
+            decode_side(a, 1, pn, no, ne - no, end1, s_leg[1], s_gidx[1], h);
             const int cn = h.code;
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);

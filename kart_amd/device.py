@@ -199,6 +199,65 @@ class DiffPipeline:
                 "deltas": int(c[:, 3].sum())}, delta
 
 
+class FilterPipeline:
+    """The spatially filtered diff over device-resident sides (one GPU): classify2's key-ordered
+    delta list feeds kd_geom_filter directly (the delta count stays on the device), which tests
+    every delta's old and new geometry against the filter, compacts the deltas that may match and
+    encodes the new side's index envelopes — BaseDiffWriter.filtered_ds_feature_deltas's work for a
+    whole layer in one stream."""
+
+    def __init__(self, engine, base, target, base_blobs, target_blobs, geom_cols, filt_env, rectangle=False, bits=20):
+        import ctypes as _c
+
+        self.eng = engine
+        self.A, self.B = DevSide(engine, base), DevSide(engine, target)
+        self.OB, self.NB = DevBlobs(engine, *base_blobs), DevBlobs(engine, *target_blobs)
+        cap = base.n + target.n + 1
+        self.cap = cap
+        self.bits = bits
+        self.delta = DevBuf(engine, 8 * cap)
+        self.upd = DevBuf(engine, 8 * cap)
+        self.counts = DevBuf(engine, 64)
+        self.counts.zero()
+        self.match = DevBuf(engine, 2 * cap)
+        self.keep = DevBuf(engine, 4 * cap)
+        self.n_keep = DevBuf(engine, 8)
+        self.enc = DevBuf(engine, cap * max(bits // 2, 1)) if bits else None
+        self.enc_ok = DevBuf(engine, cap) if bits else None
+        self._sa, self._sb = self.A.kd_side(), self.B.kd_side()
+        self._ob, self._nb = self.OB.kd_blobs(), self.NB.kd_blobs()
+        self.cols = geom_cols
+        self._kc = geom_cols.kd_cols()
+        self._fe = (_c.c_double * 4)(*[float(x) for x in filt_env])
+        self.flags = N.KD_GF_RECT if rectangle else 0
+        engine.reserve(max(base.n, target.n))
+        engine.sync()
+
+    def step(self):
+        L, ctx = self.eng.L, self.eng.ctx
+        N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), 0, self.delta.ptr, self.upd.ptr,
+                                  self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
+        N.check(L.kd_geom_filter(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.delta.ptr, self.cap,
+                                 ctypes.cast(self.counts.ptr + 24, N.c_u64p), N.KD_MEM_DEVICE, ctypes.byref(self._kc),
+                                 self._fe, self.flags, self.bits, self.match.ptr, self.keep.ptr,
+                                 ctypes.cast(self.n_keep.ptr, N.c_u64p), self.enc.ptr if self.enc else None,
+                                 self.enc_ok.ptr if self.enc_ok else None, N.KD_MEM_DEVICE), "kd_geom_filter")
+
+    def results(self):
+        """host copies: counts, delta [n, 2], codes [n, 2], keep [k], enc [n, bits/2], enc_ok [n]"""
+        c = self.counts.download(np.uint64, 8)
+        if c[4]:
+            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flag {int(c[4])}")
+        nd = int(c[3])
+        k = int(self.n_keep.download(np.uint64, 1)[0])
+        nb = self.bits // 2
+        return ({"inserts": int(c[0]), "updates": int(c[1]), "deletes": int(c[2]), "deltas": nd, "kept": k},
+                self.delta.download(np.uint32, 2 * nd).reshape(nd, 2), self.match.download(np.uint8, 2 * nd).reshape(nd, 2),
+                self.keep.download(np.uint32, k),
+                self.enc.download(np.uint8, nd * nb).reshape(nd, nb) if self.enc else None,
+                self.enc_ok.download(np.uint8, nd) if self.enc_ok else None)
+
+
 class MergePipeline:
     """classify3 (three-way merge classification) over device-resident sides (one GPU)."""
 

@@ -203,3 +203,27 @@ def test_gpu_filtered_diff_points_edit_golden(engine):
     assert len(list(S.filtered_ds_feature_deltas(engine, ds, head1, head, S.SpatialFilter.MATCH_ALL))) == 5
     far = S.SpatialFilter.from_rectangle(0, 1, 0, 1)
     assert list(S.filtered_ds_feature_deltas(engine, ds, head1, head, far)) == []
+
+
+@pytest.mark.gpu
+def test_gpu_filter_pipeline_device_resident(engine):
+    """FilterPipeline: classify2's device delta list straight into kd_geom_filter (device count),
+    equal to the oracle over the same deltas"""
+    import types
+
+    from kart_amd import synth
+    from kart_amd.device import FilterPipeline
+
+    L = synth.polygons_layer(200_000, seed=9, delta_blobs=True)
+    ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
+    pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, S.GeomCols(ver, ver, "geom", "geom"),
+                          synth.C5_FILTER, False, 20)
+    pipe.step()
+    pipe.step()  # a second step over the same buffers gives the same answer
+    counts, delta, codes, keep, enc, ok = pipe.results()
+    assert (counts["inserts"], counts["updates"], counts["deletes"]) == (L.n_insert, L.n_update, L.n_delete)
+    cols = {h: 0 for h in L.legends}
+    (od, oo), (nd, no) = L.base_blobs, L.target_blobs
+    oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta, cols, cols, synth.C5_FILTER, False, 20)
+    assert np.array_equal(codes, oc) and np.array_equal(keep, okeep) and counts["kept"] == len(okeep)
+    assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1])
