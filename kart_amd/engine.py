@@ -11,6 +11,9 @@ import numpy as np
 
 from . import _native as N
 
+# placeholder a native call gets for an empty host array: a module-level array, alive for every call
+_PAD = np.zeros(16, np.uint8)
+
 
 @dataclass
 class Diff2Result:
@@ -153,7 +156,7 @@ class Engine:
         ob, nb = N.KdBlobs(), N.KdBlobs()
         for b, d, o in ((ob, old_data, old_off), (nb, new_data, new_off)):
             b.n = int(o.shape[0]) - 1
-            b.data = N.ptr(d) if d.size else N.ptr(np.zeros(1, np.uint8))
+            b.data = N.ptr(d) if d.size else N.ptr(_PAD)
             b.off = N.ptr(o)
             b.mem = N.KD_MEM_HOST
         masks = np.zeros((max(n, 1), maps.words), np.uint64)
@@ -187,7 +190,7 @@ class Engine:
         n = int(off.shape[0]) - 1
         g = N.KdBlobs()
         g.n = n
-        g.data = N.ptr(data) if data.size else N.ptr(np.zeros(1, np.uint8))
+        g.data = N.ptr(data) if data.size else N.ptr(_PAD)
         g.off = N.ptr(off)
         g.mem = N.KD_MEM_HOST
         nb = bits // 2
@@ -208,7 +211,7 @@ class Engine:
         n = int(off.shape[0]) - 1
         g = N.KdBlobs()
         g.n = n
-        g.data = N.ptr(data) if data.size else N.ptr(np.zeros(1, np.uint8))
+        g.data = N.ptr(data) if data.size else N.ptr(_PAD)
         g.off = N.ptr(off)
         g.mem = N.KD_MEM_HOST
         nbytes = int(off[-1]) if n >= 0 and off.size else 0
@@ -224,6 +227,6 @@ class Engine:
         n = enc.shape[0]
         out = np.zeros(max(n, 1), np.uint8)
         qq = (ctypes.c_double * 4)(*[float(x) for x in q])
-        N.check(self.L.kd_env_overlap(self.ctx, N.ptr(enc) if enc.size else N.ptr(np.zeros(1, np.uint8)), n, int(bits),
+        N.check(self.L.kd_env_overlap(self.ctx, N.ptr(enc) if enc.size else N.ptr(_PAD), n, int(bits),
                                       qq, N.ptr(out), N.KD_MEM_HOST), "kd_env_overlap")
         return out[:n]

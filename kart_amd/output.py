@@ -25,6 +25,13 @@ def _arena(values):
     return data, off
 
 
+def _slices(hexbuf, lo, hi):
+    """the hex strings [lo[i], hi[i]) of one output buffer: decoded to one str once, then sliced
+    with bounds computed in numpy (no per-value int() / bytes slice / decode)"""
+    text = hexbuf.tobytes().decode("ascii")
+    return [text[a:b] for a, b in zip(lo.tolist(), hi.tolist())]
+
+
 def hex_wkb_batch(engine, geoms):
     """geoms: sequence of GPKG geometry bytes or None.  Returns (hex_list, fallback_indices):
     hex_list[i] is the uppercase hex WKB (str), None for a None/empty-bytes geometry, or None with
@@ -32,17 +39,16 @@ def hex_wkb_batch(engine, geoms):
     vals = [b"" if g is None else bytes(g) for g in geoms]
     data, off = _arena(vals)
     hexbuf, start, status = engine.hex_encode(data, off, N.KD_HEX_GPKG_WKB)
-    raw = hexbuf.tobytes()
-    out, fallback = [], []
-    for i in range(len(vals)):
-        st = int(status[i])
-        if st == 0:
-            out.append(raw[2 * (int(off[i]) + int(start[i])): 2 * int(off[i + 1])].decode("ascii"))
-        else:
-            out.append(None)
-            if st == 3:
-                fallback.append(i)
-    return out, fallback
+    n = len(vals)
+    lo = 2 * (off[:n].astype(np.int64) + start.astype(np.int64))
+    hi = 2 * off[1:].astype(np.int64)
+    ok = status == 0
+    hi = np.where(ok, hi, lo)
+    out = _slices(hexbuf, lo, hi)
+    bad = np.nonzero(~ok)[0]
+    for i in bad.tolist():
+        out[i] = None
+    return out, np.nonzero(status == 3)[0].tolist()
 
 
 def bytes_hex_batch(engine, values):
@@ -50,20 +56,24 @@ def bytes_hex_batch(engine, values):
     vals = [bytes(v) for v in values]
     data, off = _arena(vals)
     hexbuf, _, _ = engine.hex_encode(data, off, N.KD_HEX_BYTES)
-    raw = hexbuf.tobytes()
-    return [raw[2 * int(off[i]): 2 * int(off[i + 1])].decode("ascii") for i in range(len(vals))]
+    o = 2 * off.astype(np.int64)
+    return _slices(hexbuf, o[:-1], o[1:])
 
 
-def features_as_json(engine, rows, geometry_type=bytes):
-    """feature_as_json for many rows (dicts): geometries (instances of ``geometry_type``, Kart's
-    ``Geometry`` bytes subclass) -> hex WKB, other bytes -> bytes.hex, everything else unchanged.
+def features_as_json(engine, rows, geometry_type=None):
+    """feature_as_json for many rows (dicts): geometries (instances of ``geometry_type``, by default
+    kart_amd.dataset.Geometry — what this package's get_feature returns; Kart passes its own
+    ``Geometry``) -> hex WKB, other ``bytes`` values -> bytes.hex, everything else (bytearray
+    included, as kart/feature_output.py:54 tests isinstance(v, bytes)) unchanged.
     Raises NotImplementedError naming the first geometry that needs the CPU (OGR) path."""
+    if geometry_type is None:
+        from .dataset import Geometry as geometry_type
     geo_at, geoms, byt_at, byts = [], [], [], []
     for r, row in enumerate(rows):
         for k, v in row.items():
-            if isinstance(v, geometry_type) and geometry_type is not bytes:
+            if isinstance(v, geometry_type):
                 geo_at.append((r, k)); geoms.append(v)
-            elif isinstance(v, (bytes, bytearray)):
+            elif isinstance(v, bytes):
                 byt_at.append((r, k)); byts.append(v)
     out = [dict(row) for row in rows]
     if geoms:

@@ -20,6 +20,9 @@ import numpy as np
 
 from . import _native as N
 
+# placeholder a native call gets for an empty host array: a module-level array, alive for every call
+_PAD = np.zeros(16, np.uint8)
+
 
 @dataclass
 class PathEncoding:
@@ -109,7 +112,7 @@ def parse_keys(paths, off, encoding: PathEncoding):
     keys = np.empty(n, np.uint64)
     status = np.empty(n, np.uint8)
     L = N.lib()
-    pp = N.ptr(paths) if paths.size else N.ptr(np.zeros(1, np.uint8))
+    pp = N.ptr(paths) if paths.size else N.ptr(_PAD)
     if encoding.key_mode == N.KD_KEY_INT:  # the native packer decodes each path's filename
         bad = L.kd_pack_int_keys(pp, N.ptr(off), n, N.ptr(keys), N.ptr(status))
     else:

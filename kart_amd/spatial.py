@@ -20,6 +20,9 @@ from enum import Enum, auto
 import numpy as np
 
 from . import _native as N
+
+# placeholder a native call gets for an empty host array: a module-level array, alive for every call
+_PAD = np.zeros(16, np.uint8)
 from . import packing
 from .deltas import WORKING_COPY_EDIT
 
@@ -253,7 +256,7 @@ def geom_filter(engine, old_arena, new_arena, pairs, cols, filt_env, rectangle=F
     for d, o in ((od, oo), (nd, no)):
         b = N.KdBlobs()
         b.n = int(o.shape[0]) - 1
-        b.data = N.ptr(d) if d.size else N.ptr(np.zeros(1, np.uint8))
+        b.data = N.ptr(d) if d.size else N.ptr(_PAD)
         b.off = N.ptr(o)
         b.mem = N.KD_MEM_HOST
         blobs.append(b)

@@ -222,3 +222,23 @@ def test_output_host_slicing():
     be = G(b"GP\x00\x00" + struct.pack(">i", 4326) + struct.pack(">bIdd", 0, 1, 1.5, -2.5))
     with pytest.raises(NotImplementedError):
         features_as_json(eng, [{"g": be}], geometry_type=G)
+
+
+def test_features_as_json_defaults_to_package_geometry():
+    """no geometry_type: the Geometry values this package's own get_feature returns are hex WKB
+    (uppercase, header stripped); bytearray values stay as they are (feature_output.py:54 tests
+    isinstance(v, bytes))"""
+    from fixtures import load
+    from kart_amd.output import features_as_json
+    from test_dropin import version
+
+    fx = load("repo_points")
+    v = version(fx, "head")
+    i = int(v.packed.order[2])
+    row = v.get_feature(path=v.rel_path(i), data=v.read_blob(i))
+    row["ba"] = bytearray(b"\x01\x02")
+    row["raw"] = b"\x00\xff"
+    (out,) = features_as_json(_ArenaEngine(), [row])
+    g = row[fx.schema("head").geometry_columns[0].name]
+    assert out[fx.schema("head").geometry_columns[0].name] == O.hex_wkb(bytes(g))
+    assert out["ba"] == bytearray(b"\x01\x02") and out["raw"] == "00ff"
