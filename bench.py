@@ -678,13 +678,16 @@ def run_c6(args, H):
         # D2H, one decode + numpy-bounded slicing), against a per-value binascii.hexlify loop
         import binascii
 
-        from kart_amd.output import hex_wkb_batch
+        from kart_amd.output import hex_wkb_arena, hex_wkb_batch
 
         e2e = eng
         hx, fb = hex_wkb_batch(e2e, blobs[:1000])  # warm the staging slots
         t0 = time.perf_counter()
         hx, fb = hex_wkb_batch(e2e, blobs)
         t_batch = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        hb, lo, hi, st = hex_wkb_arena(e2e, blobs)
+        t_arena = time.perf_counter() - t0
         t0 = time.perf_counter()
         ref = [binascii.hexlify(b[8 + (32 if (b[3] >> 1) & 7 else 0):]).decode().upper() for b in blobs]
         t_loop = time.perf_counter() - t0
@@ -694,6 +697,8 @@ def run_c6(args, H):
             "hex_wkb_batch": {"value": round(m / t_batch / 1e6, 3), "unit": "M geometries/s",
                               "sample": f"{m} host geometries -> list of str via kart_amd.output.hex_wkb_batch "
                                         "(arena join + H2D + kd_hex_encode + D2H + slicing), 1 GPU"},
+            "hex_wkb_arena": {"value": round(m / t_arena / 1e6, 3), "unit": "M geometries/s",
+                              "sample": f"the same {m} geometries -> one hex buffer + bounds (no str per value)"},
             "per_value_hexlify": {"value": round(m / t_loop / 1e6, 3), "unit": "M geometries/s",
                                   "sample": f"the same {m} geometries, binascii.hexlify(wkb).upper() per value, 1 thread"}}
     eng.close()

@@ -2,7 +2,8 @@
 
 Mirrors the reference's per-value formatting, batched:
   * ``hex_wkb_batch``     <- ``gpkg_geom_to_hex_wkb`` / ``Geometry.to_hex_wkb``
-                             (kart/geometry.py:346-375, :142-143)
+                             (kart/geometry.py:346-375, :142-143); ``hex_wkb_arena`` gives the same
+                             hex as one buffer + bounds for writers that stream bytes
   * ``bytes_hex_batch``   <- ``bytes.hex(v)`` as ``feature_as_json`` applies it (kart/feature_output.py:54-55)
   * ``features_as_json``  <- ``feature_as_json(row, pk_value)`` with no geometry transform
                              (kart/feature_output.py:34-56), for a list of rows at once.
@@ -32,18 +33,26 @@ def _slices(hexbuf, lo, hi):
     return [text[a:b] for a, b in zip(lo.tolist(), hi.tolist())]
 
 
-def hex_wkb_batch(engine, geoms):
-    """geoms: sequence of GPKG geometry bytes or None.  Returns (hex_list, fallback_indices):
-    hex_list[i] is the uppercase hex WKB (str), None for a None/empty-bytes geometry, or None with
-    i in fallback_indices when the reference would go through OGR or raise."""
-    vals = [b"" if g is None else bytes(g) for g in geoms]
+def hex_wkb_arena(engine, geoms):
+    """The hex WKB of many geometries without building a str per value — for a writer that
+    streams bytes: (hex uint8 buffer, lo int64[n], hi int64[n], status uint8[n]); geometry i's
+    uppercase hex WKB is buffer[lo[i]:hi[i]] (empty unless status[i] == 0: 1 None / empty bytes,
+    3 the reference's OGR path or error)."""
+    vals = [b"" if g is None else g for g in geoms]
     data, off = _arena(vals)
     hexbuf, start, status = engine.hex_encode(data, off, N.KD_HEX_GPKG_WKB)
     n = len(vals)
     lo = 2 * (off[:n].astype(np.int64) + start.astype(np.int64))
-    hi = 2 * off[1:].astype(np.int64)
+    hi = np.where(status == 0, 2 * off[1:].astype(np.int64), lo)
+    return hexbuf, lo, hi, status
+
+
+def hex_wkb_batch(engine, geoms):
+    """geoms: sequence of GPKG geometry bytes or None.  Returns (hex_list, fallback_indices):
+    hex_list[i] is the uppercase hex WKB (str), None for a None/empty-bytes geometry, or None with
+    i in fallback_indices when the reference would go through OGR or raise."""
+    hexbuf, lo, hi, status = hex_wkb_arena(engine, geoms)
     ok = status == 0
-    hi = np.where(ok, hi, lo)
     out = _slices(hexbuf, lo, hi)
     bad = np.nonzero(~ok)[0]
     for i in bad.tolist():
