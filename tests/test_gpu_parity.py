@@ -236,9 +236,12 @@ def test_gpu_env_overlap_vs_oracle(engine):
         assert np.array_equal(g, o)
 
 
-@pytest.mark.parametrize("ordered", [True, False])
-@pytest.mark.parametrize("n,layer", [(1000, "points"), (3_000_000, "points"), (1000, "polygons"),
-                                     (2_000_000, "polygons")])
+@pytest.mark.parametrize("ordered,n,layer", [
+    (o, n, layer) for o in (True, False)
+    for n, layer in [(1000, "points"), (3_000_000, "points"), (1000, "polygons"), (2_000_000, "polygons")]] + [
+    (True, 10_000_000, "points"),       # C2 at its stated size (configs[1])
+    (True, 100_000_000, "polygons"),    # C3 at its stated size (configs[2], the bench's default workload)
+])
 def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered):
     """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes),
     on the C2 points layer and the C3 polygon layer (~370-B blobs: head + tail windows and the

@@ -206,7 +206,8 @@ def test_gpu_filtered_diff_points_edit_golden(engine):
 
 
 @pytest.mark.gpu
-def test_gpu_filter_pipeline_device_resident(engine):
+@pytest.mark.parametrize("n", [200_000, 5_000_000])
+def test_gpu_filter_pipeline_device_resident(engine, n):
     """FilterPipeline: classify2's device delta list straight into kd_geom_filter (device count),
     equal to the oracle over the same deltas"""
     import types
@@ -214,7 +215,7 @@ def test_gpu_filter_pipeline_device_resident(engine):
     from kart_amd import synth
     from kart_amd.device import FilterPipeline
 
-    L = synth.polygons_layer(200_000, seed=9, delta_blobs=True)
+    L = synth.polygons_layer(n, seed=9, delta_blobs=True)
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, S.GeomCols(ver, ver, "geom", "geom"),
                           synth.C5_FILTER, False, 20)
