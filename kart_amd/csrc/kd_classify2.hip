@@ -10,8 +10,9 @@
 //   k_join2    one tile per 256-thread workgroup: keys by LDS-DMA into LDS, branch-free 4-ary split
 //              search + register walk, OIDs of matched pairs compared straight from HBM, ballot
 //              compaction into the tile's staging slot + tile counts + 64-tile group sums;
-//   k_place2   one wave per tile: earlier groups' sums + earlier tiles of its group -> offset, staged
-//              records -> final key-ordered positions; the last tile writes the totals.
+//   k_gscan2   one block: exclusive prefix of the 64-tile group sums, and the totals
+//   k_place2   one wave per tile: its group's prefix + earlier tiles of its group -> offset, staged
+//              records -> final key-ordered positions.
 // KD_DIFF_UNORDERED: k_join2 appends each tile's records at an atomically reserved offset (tiles in
 // completion order, key order inside each tile); no k_place2.
 // (Earlier variants — a persistent register-prefetched join, a decoupled look-back and a per-wave
@@ -501,62 +502,74 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     }
 }
 
-// Staged path: tile-local staging -> final key-ordered positions; one tile per block.  The tile's
-// output offset = the group sums of all earlier C2_GROUP-tile groups + the counts of the earlier
-// tiles of its own group; the last block also writes the totals.  tile_cnt = inserts, updates,
-// deletes, deltas per tile.
+// Staged path, step 1: one block scans the C2_GROUP-tile group sums (exclusive prefix of deltas and
+// updates per group) and writes the totals — so each k_place2 tile reads one prefix instead of
+// summing every earlier group (which made k_place2 O(tiles x groups): 0.30 ms at C3's 195k tiles).
+__global__ __launch_bounds__(1024) void k_gscan2(const u64* __restrict__ gsum, u64 ngroups, u64* __restrict__ gpre,
+                                                 u64* __restrict__ counts) {
+    __shared__ u64 s_w[4][16];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    u64 cd = 0, cu = 0, ci = 0, cx = 0;
+    for (u64 base = 0; base < ngroups; base += 1024) {
+        const u64 k = base + tid;
+        const u64 a = k < ngroups ? gsum[2 * k] : 0, b = k < ngroups ? gsum[2 * k + 1] : 0;
+        const u64 d = a & 0xFFFFFFFFu, u = a >> 32;
+        u64 sd = d, su = u, si = b & 0xFFFFFFFFu, sx = b >> 32;  // inclusive wave scans (d, u), sums (i, x)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u64 yd = __shfl_up(sd, o, 64), yu = __shfl_up(su, o, 64);
+            if (lane >= o) { sd += yd; su += yu; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { si += __shfl_xor(si, o, 64); sx += __shfl_xor(sx, o, 64); }
+        if (lane == 63) { s_w[0][wid] = sd; s_w[1][wid] = su; }
+        if (lane == 0) { s_w[2][wid] = si; s_w[3][wid] = sx; }
+        __syncthreads();
+        u64 wd = 0, wu = 0, td = 0, tu = 0, ti = 0, tx = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            if (w < wid) { wd += s_w[0][w]; wu += s_w[1][w]; }
+            td += s_w[0][w]; tu += s_w[1][w]; ti += s_w[2][w]; tx += s_w[3][w];
+        }
+        if (k < ngroups) {
+            gpre[2 * k] = cd + wd + sd - d;
+            gpre[2 * k + 1] = cu + wu + su - u;
+        }
+        cd += td; cu += tu; ci += ti; cx += tx;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        counts[0] = ci;
+        counts[1] = cu;
+        counts[2] = cx;
+        counts[3] = cd;
+    }
+}
+
+// Staged path, step 2: tile-local staging -> final key-ordered positions; one tile per block.  The
+// tile's output offset = its group's prefix (k_gscan2) + the counts of the earlier tiles of its own
+// group.  tile_cnt = inserts, updates, deletes, deltas per tile.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
-                                               const u32* __restrict__ tile_cnt, const u64* __restrict__ gsum,
-                                               u64 ntiles, int tile_items, uint2* __restrict__ out_delta,
-                                               uint2* __restrict__ out_upd, u64* __restrict__ counts) {
-    __shared__ u64 s_red[4][NT / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+                                               const u32* __restrict__ tile_cnt, const u64* __restrict__ gpre,
+                                               int tile_items, uint2* __restrict__ out_delta, uint2* __restrict__ out_upd) {
+    static_assert(NT == 64, "k_place2: one wave per tile");
+    const int tid = threadIdx.x;
     const u64 t = blockIdx.x;
-    const u64 grp = t / C2_GROUP, ngroups = (ntiles + C2_GROUP - 1) / C2_GROUP;
-    const bool last = t == ntiles - 1;
-    const u64 g_end = last ? ngroups : grp;  // the last block sums every group for the totals
-    u64 pd = 0, pu = 0, si = 0, sx = 0;
-    for (u64 k = tid; k < g_end; k += NT) {
-        const u64 a = gsum[2 * k];
-        if (k < grp) { pd += a & 0xFFFFFFFFu; pu += a >> 32; }
-        if (last) {
-            const u64 b = gsum[2 * k + 1];
-            si += b & 0xFFFFFFFFu; sx += b >> 32;
-            if (k >= grp) { pd += a & 0xFFFFFFFFu; pu += a >> 32; }  // totals: all groups
-        }
-    }
+    const u64 grp = t / C2_GROUP;
     const u64 t_lo = grp * C2_GROUP;
-    if (!last && tid < (int)(t - t_lo)) {
+    u64 pd = 0, pu = 0;
+    if (tid < (int)(t - t_lo)) {
         const uint4 c = *(const uint4*)(tile_cnt + 4 * (t_lo + tid));
-        pd += c.w;
-        pu += c.y;
+        pd = c.w;
+        pu = c.y;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { pd += __shfl_xor(pd, o, 64); pu += __shfl_xor(pu, o, 64); }
+    pd += gpre[2 * grp];
+    pu += gpre[2 * grp + 1];
     const uint4 ownc = *(const uint4*)(tile_cnt + 4 * t);
     const uint2 own = make_uint2(ownc.w, ownc.y);  // (deltas, updates) of this tile
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        pd += __shfl_xor(pd, o, 64); pu += __shfl_xor(pu, o, 64);
-        si += __shfl_xor(si, o, 64); sx += __shfl_xor(sx, o, 64);
-    }
-    if (lane == 0) { s_red[0][wid] = pd; s_red[1][wid] = pu; s_red[2][wid] = si; s_red[3][wid] = sx; }
-    __syncthreads();
-    pd = pu = 0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; w++) { pd += s_red[0][w]; pu += s_red[1][w]; }
-    if (last) {
-        if (tid == 0) {
-            u64 ti = 0, tx = 0;
-#pragma unroll
-            for (int w = 0; w < NT / 64; w++) { ti += s_red[2][w]; tx += s_red[3][w]; }
-            counts[0] = ti;
-            counts[1] = pu;
-            counts[2] = tx;
-            counts[3] = pd;
-        }
-        pd -= own.x;
-        pu -= own.y;
-    }
     const uint2* sdp = stage_delta + t * (u64)tile_items;
     const uint2* sup = stage_upd + t * (u64)tile_items;
     constexpr int UC = C2_TILE / NT;
@@ -600,7 +613,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         KD_HIP(hipMemsetAsync(d_counts, 0, 4 * sizeof(u64), ctx->stream));
         return KD_OK;
     }
-    void *part, *tcnt = nullptr, *sdel = nullptr, *supd = nullptr, *gsum = nullptr;
+    void *part, *tcnt = nullptr, *sdel = nullptr, *supd = nullptr, *gsum = nullptr, *gpre = nullptr;
     int rc;
     if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
     u64* zero = nullptr;
@@ -609,6 +622,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         n_zero = 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
         if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
         if ((rc = ensure(ctx, "c2.gsum", n_zero * sizeof(u64), &gsum))) return rc;
+        if ((rc = ensure(ctx, "c2.gpre", n_zero * sizeof(u64), &gpre))) return rc;
         if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_STAGE * sizeof(uint2), &sdel))) return rc;
         if ((rc = ensure(ctx, "c2.supd", ntiles * C2_STAGE * sizeof(uint2), &supd))) return rc;
         zero = (u64*)gsum;
@@ -653,10 +667,15 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         }
     });
     if (rc || unord) return rc;
+    rc = launch(ctx, "k_gscan2", [&] {
+        hipLaunchKernelGGL(k_gscan2, dim3(1), dim3(1024), 0, ctx->stream, (const u64*)gsum, (u64)(n_zero / 2),
+                           (u64*)gpre, d_counts);
+    });
+    if (rc) return rc;
     return launch(ctx, "k_place2", [&] {
         hipLaunchKernelGGL((k_place2<KD_PLACE_NT>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
-                           (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gsum, ntiles,
-                           (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, d_counts);
+                           (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gpre,
+                           (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd);
     });
 }
 
