@@ -764,7 +764,16 @@ __device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n, const u8* dumm
     return ((bal >> (16 * grp)) & 0xFFFF) != 0;
 }
 
-constexpr u32 FD_TAB_LDS_MAX = 16384;  // tables up to this size are copied into each block's LDS
+constexpr u32 FD_TAB_LDS_MAX = 16384;
+// window shapes (updates per round, head chunks, tail chunks): small features / larger ones
+#ifndef KD_FD_SHAPE_L
+#define KD_FD_SHAPE_L 48, 5, 5  // C3 (20M): 32 / 40 / 48 / 56 / 64 updates per round = 0.42 / 0.41 / 0.39 / 0.66 / 0.42 ms
+#endif
+#ifndef KD_FD_SHAPE_S
+#define KD_FD_SHAPE_S 32, 8, 3
+#endif
+template <int UPR, int NH, int NTL>
+constexpr int fd_upr(const void*) { return UPR; }  // tables up to this size are copied into each block's LDS
 typedef __attribute__((address_space(3))) void* fd_lds_vp;
 typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 
@@ -1070,12 +1079,12 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
     // calculator for this launch's LDS), capped at the measured optimum.
     const void* kern = !lds_tab ? (const void*)k_fielddiff_g
-                       : small ? (const void*)k_fielddiff<32, 8, 3> : (const void*)k_fielddiff<32, 5, 5>;
+                       : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
     int per_cu = 0;
     KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FD_NT, lds_tab ? o_end : 0));
     // measured on C3 (polygons, 1.6M updates): 9 / 10 / 11 blocks per CU = 0.45 / 0.42 / 0.53 ms
     per_cu = std::max(1, std::min(per_cu, 10));
-    const u64 upr = lds_tab ? 32 : FD_NT;
+    const u64 upr = !lds_tab ? FD_NT : small ? fd_upr<KD_FD_SHAPE_S>(nullptr) : fd_upr<KD_FD_SHAPE_L>(nullptr);
     unsigned blocks = (unsigned)std::min<u64>((work + upr - 1) / upr, (u64)ctx->n_cu * (u64)per_cu);
     if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
@@ -1088,8 +1097,8 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
             hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks,
                                d_status);
-        else if (small) args(k_fielddiff<32, 8, 3>);
-        else args(k_fielddiff<32, 5, 5>);
+        else if (small) args(k_fielddiff<KD_FD_SHAPE_S>);
+        else args(k_fielddiff<KD_FD_SHAPE_L>);
     });
     if (rc) return rc;
     if (out_mem == KD_MEM_HOST) {
