@@ -1,0 +1,132 @@
+"""End-to-end `kart diff HEAD^ HEAD` of a Kart-shaped git repository through the drop-in path:
+object store + walk (gitsource) -> key packing -> kd_diff2 -> Delta objects -> batched blob read +
+kd_fielddiff, timed stage by stage, next to `git diff-tree -r` (the tree diff libgit2 does for the
+reference) and the reference's own Python path rate (0.54 M feature-pairs/s).
+
+The repository: N points features (IntPathEncoder paths, the reference's feature blob encoding,
+EPSG:4326), a second commit with 1 % updates / deletes / inserts.  Prints one JSON object.
+usage: python scripts/e2e_repo_bench.py [--n 1000000] [--out FILE]   (GPU needed for the diff)
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from kart_amd import synth  # noqa: E402
+from kart_amd.schema import Legend  # noqa: E402
+
+DS = "nz_points"
+REFERENCE_RATE = 0.54e6  # the reference diff hot path, feature pairs / s, 1 core
+
+
+def build(gitdir, n, seed=3):
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    legend = Legend(["c-fid"], [c["id"] for c in synth.POINT_SCHEMA[1:]])
+    lh = legend.hexhash()
+    rng = np.random.default_rng(seed)
+    pks = np.arange(1, n + 1, dtype=np.int64)
+    perm = rng.permutation(n)
+    k = n // 100
+    upd, dele = np.sort(perm[:k]), np.sort(perm[k:2 * k])
+    ins = np.arange(n + 1, n + 1 + k, dtype=np.int64)
+    inner = f"{DS}/.table-dataset"
+    meta = {f"{inner}/meta/schema.json": json.dumps(synth.POINT_SCHEMA).encode(),
+            f"{inner}/meta/path-structure.json": json.dumps(
+                {"scheme": "int", "branches": 64, "levels": 4, "encoding": "base64"}).encode(),
+            f"{inner}/meta/legend/{lh}": legend.dumps(),
+            f"{inner}/meta/crs/EPSG:4326.wkt": b'GEOGCS["WGS 84",AUTHORITY["EPSG","4326"]]',
+            ".kart.repostructure.version": b"3\n"}
+
+    def feature_lines(p, ver):
+        arena, off = synth.int_pk_paths(p)
+        data, boff = synth.point_blobs(p, ver, lh)
+        out = []
+        for i in range(p.shape[0]):
+            path = arena[int(off[i]):int(off[i + 1])].tobytes()
+            blob = data[int(boff[i]):int(boff[i + 1])].tobytes()
+            out.append(b"M 100644 inline %s/feature/%s\ndata %d\n%s\n" % (inner.encode(), path, len(blob), blob))
+        return out
+
+    lines = [b"commit refs/heads/main\ncommitter t <t@t> 1600000000 +0000\ndata 1\nx\n"]
+    for p, d in meta.items():
+        lines.append(b"M 100644 inline %s\ndata %d\n%s\n" % (p.encode(), len(d), d))
+    lines += feature_lines(pks, np.zeros(n, np.uint64))
+    lines.append(b"\ncommit refs/heads/main\ncommitter t <t@t> 1600000001 +0000\ndata 1\ny\n")
+    lines += feature_lines(pks[upd], np.ones(k, np.uint64))
+    lines += feature_lines(ins, np.full(k, 2, np.uint64))
+    arena, off = synth.int_pk_paths(pks[dele])
+    for i in range(k):
+        lines.append(b"D %s/feature/%s\n" % (inner.encode(), arena[int(off[i]):int(off[i + 1])].tobytes()))
+    lines.append(b"\n")
+    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
+                   check=True)
+    return k
+
+
+def timed(fn):
+    t0 = time.perf_counter()
+    r = fn()
+    return time.perf_counter() - t0, r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--repo", default=None)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    gitdir = a.repo or f"/tmp/kart_e2e_{a.n}.git"
+    if not os.path.isdir(gitdir):
+        t, k = timed(lambda: build(gitdir, a.n))
+        print(f"built {gitdir} in {t:.1f} s", file=sys.stderr)
+    from kart_amd import dataset as D
+    from kart_amd.engine import Engine
+    from kart_amd.gitsource import GitRepo
+
+    feat = f"{DS}/.table-dataset/feature"
+    t_git, out = timed(lambda: subprocess.run(["git", "--git-dir", gitdir, "diff-tree", "-r", "--name-only",
+                                               "main^", "main", "--", feat], capture_output=True, check=True).stdout)
+    n_git = out.count(b"\n")
+    res = {"n": a.n, "changed_paths": n_git, "git_diff_tree_s": round(t_git, 4),
+           "reference_path_s_estimate": round((a.n + a.n // 100) / REFERENCE_RATE, 2)}
+    with Engine(0) as eng:
+        for label, pruned in (("pruned walk", True), ("full walk", False)):
+            stages = {}
+            t0 = time.perf_counter()
+            repo = GitRepo(gitdir)
+            if pruned:
+                t, (old, new) = timed(lambda: repo.diff_versions("main^", "main", DS))
+            else:
+                t, (old, new) = timed(lambda: (repo.dataset_version("main^", DS), repo.dataset_version("main", DS)))
+            stages["walk_s"] = t
+            t, _ = timed(lambda: (old.packed, new.packed))
+            stages["pack_s"] = t
+            t, ds = timed(lambda: D.get_dataset_diff(eng, old, new))
+            stages["diff_s"] = t
+            fd = ds["feature"]
+            t, nu = timed(lambda: D.field_diff(eng, fd, old, new))
+            stages["field_diff_s"] = t
+            total = time.perf_counter() - t0
+            counts = fd.type_counts()
+            assert sum(counts.values()) == n_git, (counts, n_git)
+            assert all(d.changed_fields for d in fd.values() if d.type == "update")
+            repo.close()
+            res[label] = {**{k: round(v, 4) for k, v in stages.items()}, "total_s": round(total, 4),
+                          "counts": counts, "leaves": [int(old.n), int(new.n)],
+                          "speedup_vs_reference_path": round(res["reference_path_s_estimate"] / total, 1)}
+    s = json.dumps(res, indent=1)
+    print(s)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
