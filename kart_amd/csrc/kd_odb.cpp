@@ -132,9 +132,17 @@ struct Pack {
 
 }  // namespace
 
+namespace {
+struct Reader;
+}
+
 struct kd_odb {
     std::vector<std::string> objdirs;  // objects/ and its alternates
     std::vector<std::unique_ptr<Pack>> packs;
+    // idle readers (zlib stream + base cache) reused by single-object reads: building one costs
+    // more than reading a small object (ctypes drops the GIL, so calls may be concurrent)
+    std::mutex pool_mu;
+    std::vector<Reader*> pool;
 };
 
 namespace {
@@ -744,17 +752,42 @@ extern "C" int kd_odb_open(const char* gitdir, kd_odb** out) {
 }
 
 extern "C" int kd_odb_close(kd_odb* odb) {
+    if (odb)
+        for (Reader* r : odb->pool) delete r;
     delete odb;
     return KD_OK;
 }
+
+namespace {
+// a pooled reader for the duration of one call
+struct PooledReader {
+    kd_odb* db;
+    Reader* r;
+    explicit PooledReader(kd_odb* d) : db(d), r(nullptr) {
+        {
+            std::lock_guard<std::mutex> g(db->pool_mu);
+            if (!db->pool.empty()) {
+                r = db->pool.back();
+                db->pool.pop_back();
+            }
+        }
+        if (!r) r = new Reader(db);
+    }
+    ~PooledReader() {
+        std::lock_guard<std::mutex> g(db->pool_mu);
+        if (db->pool.size() < 64) db->pool.push_back(r);
+        else delete r;
+    }
+};
+}  // namespace
 
 extern "C" int kd_odb_read(kd_odb* odb, const uint8_t* oid, int* type, uint8_t** data, uint64_t* len) {
     if (!odb || !oid || !type || !data || !len) { kd::set_error("kd_odb_read: NULL"); return KD_EINVAL; }
     *data = nullptr;
     *len = 0;
-    Reader rd(odb);
+    PooledReader pr(odb);
     std::vector<u8> buf;
-    const int rc = rd.read(oid, type, buf);
+    const int rc = pr.r->read(oid, type, buf);
     char hx[41];
     hex40(oid, hx);
     if (rc == RD_MISSING) { kd::set_error("object %s missing", hx); return KD_ENOTFOUND; }

@@ -154,10 +154,38 @@ class DatasetVersion:
             raise ValueError(f"Expected a single pk_value, got {pks}")
         return pks[0]
 
+    def _read_one(self, i):
+        return self.read_blob(i)
+
     def get_blob(self, i):
-        """leaf i (original order) as a lazy blob (BaseDataset.get_blob_at)"""
-        return LazyBlob(functools.partial(self.read_blob, i), os.path.basename(self.rel_path(i)),
-                        self.oids[i].tobytes().hex())
+        """leaf i (original order) as a lazy blob (BaseDataset.get_blob_at); its read is a bound
+        method of this version, so a batch of them is read in one call (field_diff)"""
+        return LazyBlob(functools.partial(self._read_one, i), self.blob_name(i), self.oids[i].tobytes().hex())
+
+    def blob_name(self, i):
+        """the leaf's filename (the last path component)"""
+        a, b = int(self.rel_off[i]), int(self.rel_off[i + 1])
+        seg = self.rel_paths[a:b].tobytes()
+        return seg[seg.rfind(b"/") + 1:].decode()
+
+    def get_blobs(self, idx):
+        """LazyBlobs of many leaves (original order): names and OIDs sliced from one bytes object
+        each instead of per-leaf numpy indexing"""
+        idx = np.asarray(idx, np.int64)
+        if idx.size == 0:
+            return []
+        if getattr(self, "_arena_bytes", None) is None:
+            self._arena_bytes = self.rel_paths.tobytes()
+        arena = self._arena_bytes
+        starts = self.rel_off[idx].tolist()
+        ends = self.rel_off[idx + 1].tolist()
+        hexes = self.oids[idx].tobytes().hex()
+        out = []
+        for k, (i, a, b) in enumerate(zip(idx.tolist(), starts, ends)):
+            cut = arena.rfind(b"/", a, b) + 1
+            out.append(LazyBlob(functools.partial(self._read_one, i), arena[max(cut, a):b].decode(),
+                                hexes[40 * k:40 * k + 40]))
+        return out
 
     def get_feature(self, pk_values=None, *, path=None, data=None):
         """Dataset3.get_feature (kart/dataset3.py:185-223)"""
@@ -237,17 +265,22 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False):
         for i, pk in zip(ib.tolist(), _pks(new_v, b_idx[ib])):
             new_pks[i] = pk
     match_all = feature_filter is None or getattr(feature_filter, "match_all", False)
+    # the lazy blobs of every delta side, built in two batches
+    old_blobs = [None] * d.shape[0]
+    new_blobs = [None] * d.shape[0]
+    if has_a.any():
+        for i, b in zip(ia.tolist(), old_v.get_blobs(A.order[a_idx[ia]])):
+            old_blobs[i] = b
+    if has_b.any():
+        for i, b in zip(ib.tolist(), new_v.get_blobs(B.order[b_idx[ib]])):
+            new_blobs[i] = b
     for i in range(d.shape[0]):
         opk, npk = old_pks[i], new_pks[i]
         if not match_all and str(opk) not in feature_filter and str(npk) not in feature_filter:
             continue
-        old_half = new_half = None
-        if has_a[i]:
-            blob = old_v.get_blob(int(A.order[a_idx[i]]))
-            old_half = (opk, functools.partial(old_v.get_feature_from_blob, blob))
-        if has_b[i]:
-            blob = new_v.get_blob(int(B.order[b_idx[i]]))
-            new_half = (npk, functools.partial(new_v.get_feature_from_blob, blob))
+        ob, nb = old_blobs[i], new_blobs[i]
+        old_half = (opk, functools.partial(old_v.get_feature_from_blob, ob)) if ob is not None else None
+        new_half = (npk, functools.partial(new_v.get_feature_from_blob, nb)) if nb is not None else None
         yield S.Delta(old_half, new_half)
 
 
