@@ -15,7 +15,9 @@ calls ``get_feature`` zero times; each value access calls it once (tests/test_di
 ``value.args[0]`` is the blob (base_diff_writer.py:505-507, DeltaFetcher).
 """
 import base64
+import contextlib
 import functools
+import gc
 import os
 
 import msgpack
@@ -72,27 +74,33 @@ class Oid(str):
 
 
 class LazyBlob:
-    """What get_blob_at returns (a pygit2.Blob in Kart): .name / .id now, content on first use —
-    so classification never reads a blob, and a missing (promised) blob raises KeyError only when
-    its value is accessed, as in the reference (DeltaFetcher relies on that)."""
+    """What get_blob_at returns (a pygit2.Blob in Kart): .name / .id / content, each computed on
+    first use from (dataset version, leaf index) — so classification reads no blob and builds no
+    name or OID string, and a missing (promised) blob raises KeyError only when its value is
+    accessed, as in the reference (DeltaFetcher relies on that)."""
 
-    __slots__ = ("name", "id", "_read", "_data")
+    __slots__ = ("_src", "_i", "_data")
     type_str = "blob"
 
-    def __init__(self, read, name, oid_hex):
-        self._read = read
-        self.name = name
-        self.id = Oid(oid_hex)
+    def __init__(self, src, i):
+        self._src = src
+        self._i = i
         self._data = None
 
     @property
-    def oid(self):
-        return self.id
+    def name(self):
+        return self._src.blob_name(self._i)
+
+    @property
+    def id(self):
+        return Oid(self._src.oids[self._i].tobytes().hex())
+
+    oid = id
 
     @property
     def data(self):
         if self._data is None:
-            self._data = self._read()
+            self._data = self._src.read_blob(self._i)
         return self._data
 
     def __bytes__(self):
@@ -154,13 +162,10 @@ class DatasetVersion:
             raise ValueError(f"Expected a single pk_value, got {pks}")
         return pks[0]
 
-    def _read_one(self, i):
-        return self.read_blob(i)
-
     def get_blob(self, i):
-        """leaf i (original order) as a lazy blob (BaseDataset.get_blob_at); its read is a bound
-        method of this version, so a batch of them is read in one call (field_diff)"""
-        return LazyBlob(functools.partial(self._read_one, i), self.blob_name(i), self.oids[i].tobytes().hex())
+        """leaf i (original order) as a lazy blob (BaseDataset.get_blob_at); a batch of them is read
+        in one call (prefetch_blobs)"""
+        return LazyBlob(self, int(i))
 
     def blob_name(self, i):
         """the leaf's filename (the last path component)"""
@@ -169,23 +174,8 @@ class DatasetVersion:
         return seg[seg.rfind(b"/") + 1:].decode()
 
     def get_blobs(self, idx):
-        """LazyBlobs of many leaves (original order): names and OIDs sliced from one bytes object
-        each instead of per-leaf numpy indexing"""
-        idx = np.asarray(idx, np.int64)
-        if idx.size == 0:
-            return []
-        if getattr(self, "_arena_bytes", None) is None:
-            self._arena_bytes = self.rel_paths.tobytes()
-        arena = self._arena_bytes
-        starts = self.rel_off[idx].tolist()
-        ends = self.rel_off[idx + 1].tolist()
-        hexes = self.oids[idx].tobytes().hex()
-        out = []
-        for k, (i, a, b) in enumerate(zip(idx.tolist(), starts, ends)):
-            cut = arena.rfind(b"/", a, b) + 1
-            out.append(LazyBlob(functools.partial(self._read_one, i), arena[max(cut, a):b].decode(),
-                                hexes[40 * k:40 * k + 40]))
-        return out
+        """LazyBlobs of many leaves (original order)"""
+        return [LazyBlob(self, i) for i in np.asarray(idx, np.int64).tolist()]
 
     def get_feature(self, pk_values=None, *, path=None, data=None):
         """Dataset3.get_feature (kart/dataset3.py:185-223)"""
@@ -295,8 +285,23 @@ def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
         # a filter without a "feature" entry matches no feature (the reference falls back to an empty
         # child filter: ds_filter.get("feature", ds_filter.child_type()), :177)
         ffilter = ds_filter.get("feature", _NoKeys())
-    out["feature"] = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse))
+    with _gc_paused():
+        out["feature"] = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse))
     return out
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    """Bulk construction of deltas (about ten small objects each, none of them cyclic garbage):
+    with the cyclic collector running, its generation-2 passes rescan the whole heap several times
+    per 100K deltas, which doubled the host cost of a diff"""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class _NoKeys(frozenset):
@@ -367,23 +372,35 @@ def field_diff(engine, feature_diff, old_version, new_version):
     od, oo = _blob_arena([d.old.value.args[0] for d in ups])
     nd, no = _blob_arena([d.new.value.args[0] for d in ups])
     masks, status = engine.fielddiff(od, oo, nd, no, None, maps)
-    for d, m, s in zip(ups, masks, status):
-        d.changed_fields = maps.changed_names(m) if s == 0 else None
+    for d, names, s in zip(ups, maps.changed_names_rows(masks[:len(ups)]), status.tolist()):
+        d.changed_fields = names if s == 0 else None
     return len(ups)
 
 
-def _blob_arena(blobs):
-    """(data, off) of LazyBlobs: those not yet read come from one batched read per dataset version
-    (kd_odb_read_batch under gitsource); a missing blob raises its KeyError as a single read does"""
+def prefetch_blobs(blobs):
+    """Read the not-yet-read LazyBlobs of ``blobs`` with one batched read per dataset version
+    (kd_odb_read_batch under gitsource).  Returns ok[] — False where the blob is not in the
+    repository (reading it alone raises the reference's KeyError)."""
     groups = {}
     for k, b in enumerate(blobs):
-        r = getattr(b, "_read", None)
-        if getattr(b, "_data", 1) is None and isinstance(r, functools.partial) and isinstance(
-                getattr(r.func, "__self__", None), DatasetVersion):
-            groups.setdefault(id(r.func.__self__), (r.func.__self__, []))[1].append(k)
+        if type(b) is LazyBlob and b._data is None:
+            groups.setdefault(id(b._src), (b._src, []))[1].append(k)
+    ok = np.ones(len(blobs), bool)
     for v, ks in groups.values():
-        data, off, status = v.read_blobs([blobs[k]._read.args[0] for k in ks])
+        data, off, status = v.read_blobs([blobs[k]._i for k in ks])
+        raw, offs, st = data.tobytes(), off.tolist(), status.tolist()
         for j, k in enumerate(ks):
-            if status[j] == 0:
-                blobs[k]._data = data[int(off[j]):int(off[j + 1])].tobytes()
+            if st[j] == 0:
+                blobs[k]._data = raw[offs[j]:offs[j + 1]]
+            else:
+                ok[k] = False
+    return ok
+
+
+def _blob_arena(blobs):
+    """(data, off) of LazyBlobs, read in batches; a missing blob raises its KeyError as a single
+    read does"""
+    ok = prefetch_blobs(blobs)
+    if not ok.all():
+        blobs[int(np.nonzero(~ok)[0][0])].data  # raises the reference's KeyError
     return packing._arena([b.data for b in blobs])

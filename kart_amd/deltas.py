@@ -27,6 +27,8 @@ class KeyValue:
 
     @classmethod
     def of(cls, obj):
+        if type(obj) is tuple and len(obj) == 2:
+            return cls(obj[0], obj[1])
         if obj is None or isinstance(obj, KeyValue):
             return obj
         if isinstance(obj, tuple):
@@ -53,11 +55,14 @@ class Delta:
     """old -> new change of one object; either side may be None (insert / delete)."""
 
     def __init__(self, old, new):
-        self.old = KeyValue.of(old)
-        self.new = KeyValue.of(new)
-        if self.old is None and self.new is None:
-            raise ValueError("Empty Delta")
-        self.type = "insert" if self.old is None else "delete" if self.new is None else "update"
+        self.old = old = KeyValue.of(old)
+        self.new = new = KeyValue.of(new)
+        if old is None:
+            if new is None:
+                raise ValueError("Empty Delta")
+            self.type = "insert"
+        else:
+            self.type = "delete" if new is None else "update"
         self.flags = 0
 
     insert = staticmethod(lambda new: Delta(None, new))
@@ -211,8 +216,12 @@ class DeltaDiff(_TypedDict):
             for k, v in initial.items():
                 self[k] = v
         else:
-            for delta in initial:
-                self.add_delta(delta)
+            data = self.data
+            for delta in initial:  # add_delta, inlined for bulk construction
+                if type(delta) is not Delta:
+                    self.add_delta(delta)  # raises the type error
+                old = delta.old
+                data[old.key if old is not None else delta.new.key] = delta
 
     def __setitem__(self, key, delta):
         if key != delta.key:

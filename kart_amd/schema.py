@@ -156,3 +156,17 @@ class FieldMaps:
             if (int(mask_row[k >> 6]) >> (k & 63)) & 1:
                 out.append(name)
         return out
+
+    def changed_names_rows(self, masks):
+        """changed_names of every row of ``masks`` [n, words], one fresh list per row; each
+        distinct mask (a layer's updates share a handful) is decoded once"""
+        masks = np.ascontiguousarray(masks, np.uint64)
+        raw, w = masks.tobytes(), 8 * masks.shape[1]
+        memo, out = {}, []
+        for r in range(masks.shape[0]):
+            key = raw[r * w:(r + 1) * w]
+            names = memo.get(key)
+            if names is None:
+                names = memo[key] = tuple(self.changed_names(masks[r]))
+            out.append(list(names))
+        return out

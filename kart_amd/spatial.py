@@ -362,24 +362,9 @@ def _resolve(sf, code, kv):
 def _safe_arena(blobs):
     """(data, off, ok[]) of LazyBlobs; a blob missing from the repository gets ok False (its
     KeyError is raised — or turned into PROMISED — when that side is resolved on the host)"""
-    from .dataset import DatasetVersion
+    from .dataset import prefetch_blobs
 
-    import functools
-
-    groups = {}
-    for k, b in enumerate(blobs):
-        r = getattr(b, "_read", None)
-        if getattr(b, "_data", 1) is None and isinstance(r, functools.partial) and isinstance(
-                getattr(r.func, "__self__", None), DatasetVersion):
-            groups.setdefault(id(r.func.__self__), (r.func.__self__, []))[1].append(k)
-    ok = np.ones(len(blobs), bool)
-    for v, ks in groups.values():
-        data, off, status = v.read_blobs([blobs[k]._read.args[0] for k in ks])
-        for j, k in enumerate(ks):
-            if status[j] == 0:
-                blobs[k]._data = data[int(off[j]):int(off[j + 1])].tobytes()
-            else:
-                ok[k] = False
+    ok = prefetch_blobs(blobs)
     raw = []
     for k, b in enumerate(blobs):
         if ok[k]:
