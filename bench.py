@@ -166,7 +166,7 @@ def roofline(kern, dom, alg_bytes, traffic_json, n_units):
             tj = json.load(f)
         if tj.get("kernel") == dom and int(tj.get("n_units", tj.get("n_points", -1))) == n_units:
             traffic = tj.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+    except (OSError, ValueError, TypeError):
         pass
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_bytes_per_launch": int(alg_bytes),
