@@ -13,7 +13,7 @@
 //
 // k_fielddiff (one wave per workgroup, UPR updates per round, one lane per update):
 //   1. LDS windows.  Per blob only a head window (NH 16-B chunks from the blob's aligned start) and a
-//      tail window (the NTL-1 aligned chunks ending with the blob's last byte + one pad chunk) are
+//      tail window (the NTL aligned chunks ending with the blob's last byte) are
 //      copied to LDS by LDS-DMA — the msgpack headers, the legend, and the short values that follow
 //      a long one.  Long payloads (geometries) never enter LDS, so ~10 KiB per 32 updates keeps
 //      ~10 waves per CU resident.
@@ -374,20 +374,29 @@ struct MpTab {
         }
     }
 };
-__shared__ u32 s_mp[256];
+__shared__ u32 s_mp[32];  // entries of 0xc0..0xdf; the fix ranges are computed (128 B of LDS, not 1 KiB)
 
 __device__ __forceinline__ void mp_tab_to_lds() {
     constexpr MpTab T{};
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_mp[i] = T.e[i];
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) s_mp[i] = T.e[0xc0 + i];
+}
+
+__device__ __forceinline__ u32 mp_entry(u32 t) {
+    const u32 fix = t < 0x80 ? MpTab::mk(V_INT, 1, 0, 0, 0, 0, 0, 0) | t << 24          // positive fixint
+                  : t >= 0xe0 ? MpTab::mk(V_INT, 1, 0, 0, 0, 1, 0, 0) | t << 24       // negative fixint
+                  : t >= 0xa0 ? MpTab::mk(V_STR, 1, 0, 0, 0, 0, 0, 0) | (t & 31) << 6  // fixstr
+                  : MpTab::mk(7, 1, 0, 0, 0, 0, 0, 0);                                  // fixmap / fixarray
+    const u32 tab = s_mp[t & 31];
+    return (t >> 5) == 6 ? tab : fix;
 }
 
 // One blob of one lane: its bytes in HBM, and the LDS image of its head and tail windows.
 //   head: chunks [hb, hb + 16 NH)                      (hb = start rounded down to 16)
-//   tail: chunks [tb, tb + 16 NTL), tb = last chunk - 16 (NTL - 2): NTL-1 chunks ending with the
-//         chunk holding the last byte, then one pad chunk, so a window read at any valid position
-//         fits.
-// Chunks holding no byte of the blob are loaded from device zeros instead (never a possibly
-// unmapped address), so window bytes past the blob are zero; every decode bounds-checks anyway.
+//   tail: chunks [tb, tb + 16 NTL), tb = last chunk - 16 (NTL - 1): the NTL chunks ending with the
+//         chunk holding the last byte.  A read that starts inside it runs on into the next image
+//         (or past the array); the bytes it needs lie inside, as no blob byte follows the window.
+// Chunks holding no byte of the blob are not loaded: their LDS bytes are stale, and every decode
+// is bounded by the blob length.
 template <int NH, int NTL>
 struct WBlob {
     u64 start;  // device address of byte 0
@@ -399,7 +408,10 @@ struct WBlob {
     __device__ __forceinline__ u32 win(u32 x, u32 n) const {
         if (x + n <= 16 * NH) return x;
         const int y = (int)x - t0;
-        if (y >= 0 && (u32)y + n <= 16 * NTL) return 16 * NH + (u32)y;
+        // the tail window ends with the blob's last byte: a read starting inside it needs no byte
+        // past it (what it reads beyond lands in the next image or past the array, and every
+        // decoded byte is bounded by the blob length)
+        if (y >= 0 && y < 16 * NTL) return 16 * NH + (u32)y;
         return ~0u;
     }
 };
@@ -464,7 +476,7 @@ struct WVal {
 __device__ __forceinline__ u32 decode_w(u32 x0, u32 x1, u32 x2, u32 avail, WVal& v) {
     const u64 lo = (u64)x0 | (u64)x1 << 32;
     const u32 t = x0 & 0xff;
-    const u32 e = s_mp[t];
+    const u32 e = mp_entry(t);
     u32 cls = e & 7;
     const u32 hdr = (e >> 3) & 7, plen = (e >> 6) & 31, lenw = (e >> 11) & 7, numw = (e >> 14) & 15;
     const u64 be = __builtin_bswap64((lo >> 8) | (u64)x2 << 56);  // bytes 1..8, big-endian
@@ -563,6 +575,27 @@ struct FdQueue {
     u32 cap;
 };
 
+// bytes [pa, pa + n) of blob A against [pb, pb + n) of blob B: 0 equal, 1 changed, 3 queued for
+// the cooperative compare (from the LDS windows when both ranges lie in one, else queued while the
+// round's queue has room, else compared by this lane from HBM)
+template <class BL>
+__device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb, u32 n, int key, const FdQueue& q) {
+    const u32 ya = pa + A.s0, yb = pb + B.s0;  // offsets from the head bases
+    const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
+    if (oa != ~0u && ob != ~0u) return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
+    const u64 xa = A.start + pa, xb = B.start + pb;
+    if (key < 64) {
+        const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t < q.cap) {
+            q.task[3 * t] = xa;
+            q.task[3 * t + 1] = xb;
+            q.task[3 * t + 2] = (u64)n | (u64)threadIdx.x << 32 | (u64)key << 48;
+            return 3;
+        }
+    }
+    return glb_bytes_eq(xa, xb, n) ? 0u : 1u;
+}
+
 // byte payloads of a and b (same class, ext, length >= 1) at blob positions pa / pb:
 // 0 equal, 1 changed, 3 queued
 template <class BL>
@@ -574,20 +607,7 @@ __device__ __forceinline__ u32 payload_eq(const WVal& a, const BL& A, u32 pa, co
         const u32 m1 = n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1;
         return (((a.bits ^ b.bits) & m0) | ((a.hi ^ b.hi) & m1)) ? 1u : 0u;
     }
-    const u32 ya = pa + a.hdr() + A.s0, yb = pb + b.hdr() + B.s0;  // payload offsets from hb
-    const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
-    if (oa != ~0u && ob != ~0u) return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
-    const u64 xa = A.start + pa + a.hdr(), xb = B.start + pb + b.hdr();
-    if (key < 64) {
-        const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (t < q.cap) {
-            q.task[3 * t] = xa;
-            q.task[3 * t + 1] = xb;
-            q.task[3 * t + 2] = (u64)n | (u64)threadIdx.x << 32 | (u64)key << 48;
-            return 3;
-        }
-    }
-    return glb_bytes_eq(xa, xb, n) ? 0u : 1u;
+    return range_eq(A, pa + a.hdr(), B, pb + b.hdr(), n, key, q);
 }
 
 template <class BL>
@@ -712,7 +732,7 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
 // c = 16 s + j of the payload's aligned range and the matching 16 new bytes (two aligned chunks,
 // funnel-shifted by the two sides' relative skew).  Returns "differs" on every lane of the group.
 // A chunk is loaded only if it holds a byte of its payload (else the device zeros).
-__device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n, const u8* dummy) {
+__device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n) {
     const u32 j = threadIdx.x & 15, grp = (threadIdx.x >> 4) & 3;
     const u32 sa = (u32)(a & 15);
     const u64 abase = a - sa;
@@ -767,10 +787,10 @@ __device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n, const u8* dumm
 constexpr u32 FD_TAB_LDS_MAX = 16384;
 // window shapes (updates per round, head chunks, tail chunks): small features / larger ones
 #ifndef KD_FD_SHAPE_L
-#define KD_FD_SHAPE_L 48, 5, 5  // C3 (20M): 32 / 40 / 48 / 56 / 64 updates per round = 0.42 / 0.41 / 0.39 / 0.66 / 0.42 ms
+#define KD_FD_SHAPE_L 52, 5, 4  // C3 (100M): 48 / 52 / 56 updates per round = 1.73 (8 blocks per CU) / 1.69 (9) / 1.82 ms (8)
 #endif
 #ifndef KD_FD_SHAPE_S
-#define KD_FD_SHAPE_S 32, 8, 3
+#define KD_FD_SHAPE_S 32, 8, 3  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
 #endif
 template <int UPR, int NH, int NTL>
 constexpr int fd_upr(const void*) { return UPR; }  // tables up to this size are copied into each block's LDS
@@ -782,15 +802,14 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
                                                      const u64* __restrict__ n_upd_dev, FdTab tg, FdTabOff to,
-                                                     const u8* __restrict__ tab_base, const u8* __restrict__ dummy,
+                                                     const u8* __restrict__ tab_base,
                                                      u64* __restrict__ masks, u8* __restrict__ status) {
     constexpr int NC = NH + NTL;       // chunks per blob image
     constexpr int LS = 2 * NC;         // a lane's two images
     constexpr int NCH = (UPR * LS + 63) / 64 * 64;  // image chunks per round (whole instructions)
     constexpr u32 TCAP = UPR;          // queued payload compares per round (then a lane compares alone)
-    static_assert(NTL >= 2, "window shape");
+    static_assert(NTL >= 1, "window shape");
     __shared__ u32x4 s_img[NCH];
-    __shared__ u64 s_desc[4 * UPR];    // per blob (lane l, side s at 2l + s): head base, last chunk
     __shared__ u64 s_task[3 * TCAP];
     __shared__ u64 s_res[UPR];         // mask bits (keys < 64) found by the cooperative compares
     __shared__ u32 s_ntask;
@@ -801,6 +820,9 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     const bool spec = n_upd_dev && n_upd_host;
     const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
     const u64 lim = spec ? n_upd_host : n_upd;
+    const u64 end = min(lim, n_upd);
+    // Rounds are assigned grid-stride.  (Handing them out by an atomic counter instead, so that a
+    // block made resident late takes fewer rounds, measured ~20 % slower at C3.)
     const u64 step = (u64)gridDim.x * UPR;
     auto load_pair = [&](u64 uu) {
         uint2 p = make_uint2((u32)uu, (u32)uu);
@@ -818,7 +840,8 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         }
     };
     u64 u0 = (u64)blockIdx.x * UPR;
-    if (u0 >= lim || u0 >= n_upd) return;  // wave-uniform: no round for this block
+    if (u0 >= end) return;  // wave-uniform: no round for this block
+    u64 u1 = u0 + step;
     u64 os, ns;
     u32 on, nn;
     // the first round's pair and offsets are in flight while the tables are copied to LDS
@@ -840,14 +863,19 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
     const FdQueue queue{(lds_u64p)s_task, (lds_u32p)&s_ntask, TCAP};
     const u32 img0 = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img;
-    // window descriptors of one round: head base and last chunk of both blobs (no chunk: last < head)
-    auto put_desc = [&](u64 a0, u32 an, u64 b0, u32 bn, bool a) {
-        if (owner) {
-            s_desc[4 * lane] = a0 & ~(u64)15;
-            s_desc[4 * lane + 1] = a && an ? (a0 + an - 1) & ~(u64)15 : 0;
-            s_desc[4 * lane + 2] = b0 & ~(u64)15;
-            s_desc[4 * lane + 3] = a && bn ? (b0 + bn - 1) & ~(u64)15 : 0;
-        }
+    // window descriptors of one round, in the owner lanes' registers: head chunk and last chunk of
+    // both blobs as 16-B chunk indices from the arenas' aligned bases (no chunk: last < head);
+    // the staging lanes read them with lane shuffles (no LDS)
+    const u64 obase = (u64)od & ~(u64)15, nbase = (u64)nd & ~(u64)15;
+    u32 dha = 0, dla = 0, dhb = 0, dlb = 0;
+    auto put_desc = [&](u64 os_, u32 an, u64 ns_, u32 bn, bool a) {
+        const u64 xa = os_ + ((u64)od & 15), xb = ns_ + ((u64)nd & 15);  // offsets from the bases
+        dha = (u32)(xa >> 4);
+        dla = a && an ? (u32)((xa + an - 1) >> 4) : 0;
+        dhb = (u32)(xb >> 4);
+        dlb = a && bn ? (u32)((xb + bn - 1) >> 4) : 0;
+        if (!(a && an)) dha = 1;  // no chunk: last < head
+        if (!(a && bn)) dhb = 1;
     };
     // LDS-DMA of one round's windows: instruction k fills image chunks [64k, 64k + 64), lane l chunk
     // 64k + l (its blob and window position from the descriptors)
@@ -857,10 +885,14 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             const u32 c = 64 * k + lane;
             const u32 ow = c / LS, r = c - ow * LS;  // (LS even: an odd stride measured 50 % slower)
             const u32 bl = 2 * ow + (r >= (u32)NC), i = r >= (u32)NC ? r - NC : r;
-            const bool real = ow < (u32)UPR && r < 2u * NC;
-            const u64 hb = s_desc[2 * (real ? bl : 0)], lc = s_desc[2 * (real ? bl : 0) + 1];
-            const u64 addr = i < (u32)NH ? hb + 16ull * i : lc - 16ull * (NTL - 2) + 16ull * (i - NH);
-            const bool valid = real && addr >= hb && addr <= lc;
+            const bool real = ow < (u32)UPR && r < (u32)LS;
+            const int src = real ? (int)ow : 0;
+            const u32 ha = __shfl(dha, src), la = __shfl(dla, src), hb_ = __shfl(dhb, src), lb = __shfl(dlb, src);
+            const bool sb = bl & 1;
+            const u32 h = sb ? hb_ : ha, l = sb ? lb : la;  // chunk indices
+            const u32 ci = i < (u32)NH ? h + i : l - (NTL - 1) + (i - NH);
+            const bool valid = real && (int)(ci - h) >= 0 && (int)(l - ci) >= 0 && l >= h;
+            const u64 addr = (sb ? nbase : obase) + 16ull * ci;
             // chunks holding no blob byte are not loaded (their LDS bytes are never decoded: every
             // read is bounded by the blob length)
             if (valid) __builtin_amdgcn_global_load_lds((fd_glb_vp)addr, (fd_lds_vp)(s_img + 64 * k), 16, 0, 0);
@@ -869,19 +901,20 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
     // Software pipeline, one HBM round trip per round: round r's windows are parsed while nothing
     // is in flight but the next offsets; then round r+1's windows (LDS-DMA into the freed image)
     // and round r's queued payloads are loaded together.
-    put_desc((u64)od + os, on, (u64)nd + ns, nn, owner && u0 + lane < n_upd);
-    __syncthreads();
+    put_desc(os, on, ns, nn, owner && u0 + lane < n_upd);
     stage();
-    uint2 pr_n = load_pair(u0 + step + lane);
+    uint2 pr_n = load_pair(u1 + lane);
     __syncthreads();  // vmcnt(0) + barrier: round 0's windows have landed
     for (;;) {
         const u64 u = u0 + lane;
         const bool act = owner && u < n_upd;
-        const u64 u1 = u0 + step;
-        const bool more = u1 < lim && u1 < n_upd;  // wave-uniform
-        u64 os_n = 0, ns_n = 0;
+        const bool more = u1 < end;  // wave-uniform
+        u64 os_n = 0, ns_n = 0, u2 = end;
         u32 on_n = 0, nn_n = 0;
-        if (more) load_off(pr_n, owner && u1 + lane < n_upd, os_n, ns_n, on_n, nn_n);
+        if (more) {
+            load_off(pr_n, owner && u1 + lane < n_upd, os_n, ns_n, on_n, nn_n);
+            u2 = u1 + step;
+        }
         // ---- parse ----
         u64 mk[4] = {0, 0, 0, 0};  // mask words kept in registers for <= 256 keys
         u8 st = 0;
@@ -891,25 +924,24 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
             BL A, B;
             A.start = a0; A.len = on; A.s0 = (u32)(a0 & 15);
-            A.t0 = (int)(((a0 + (on ? on - 1 : 0)) & ~(u64)15) - (a0 & ~(u64)15)) - 16 * (NTL - 2);
+            A.t0 = (int)(((a0 + (on ? on - 1 : 0)) & ~(u64)15) - (a0 & ~(u64)15)) - 16 * (NTL - 1);
             A.img = img0 + 16u * (u32)(lane * LS);
             B.start = b0; B.len = nn; B.s0 = (u32)(b0 & 15);
-            B.t0 = (int)(((b0 + (nn ? nn - 1 : 0)) & ~(u64)15) - (b0 & ~(u64)15)) - 16 * (NTL - 2);
+            B.t0 = (int)(((b0 + (nn ? nn - 1 : 0)) & ~(u64)15) - (b0 & ~(u64)15)) - 16 * (NTL - 1);
             B.img = img0 + 16u * (u32)(lane * LS + NC);
             st = diff_one_w(A, B, tb, mk, m, queue);
         }
         __syncthreads();  // parse done: the image is free, the queue complete
         if (more) {
-            put_desc((u64)od + os_n, on_n, (u64)nd + ns_n, nn_n, owner && u1 + lane < n_upd);
-            __syncthreads();
+            put_desc(os_n, on_n, ns_n, nn_n, owner && u1 + lane < n_upd);
             stage();
-            pr_n = load_pair(u1 + step + lane);
+            pr_n = load_pair(u2 + lane);
         }
         // ---- the queued payloads, 16 lanes per payload ----
         const u32 nt = min(s_ntask, TCAP);
         for (u32 t = (u32)lane >> 4; t < nt; t += 4) {
             const u64 x = s_task[3 * t + 2];
-            const bool d = coop_differs(s_task[3 * t], s_task[3 * t + 1], (u32)x, dummy);
+            const bool d = coop_differs(s_task[3 * t], s_task[3 * t + 1], (u32)x);
             if (d && (lane & 15) == 0) {
                 const u32 ow = (u32)(x >> 32) & 0xFFFF, key = (u32)(x >> 48);
                 atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
@@ -927,6 +959,7 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         if (!more) break;
         __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations stay in program order)
         u0 = u1;
+        u1 = u2;
         os = os_n; ns = ns_n; on = on_n; nn = nn_n;
     }
 }
@@ -1059,8 +1092,6 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
         d_status = (u8*)b;
     }
     if (n_upd == 0 && d_n_upd == nullptr) return KD_OK;
-    void* dz;
-    if ((rc = device_zeros(ctx, &dz))) return rc;
     u64 work = d_n_upd ? (n_upd ? n_upd : (u64)1 << 22) : n_upd;
     // typical blob size: kd_blobs.size_hint, or the mean of host arenas
     auto typical = [](const kd_blobs* b) -> u64 {
@@ -1083,7 +1114,10 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     int per_cu = 0;
     KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FD_NT, lds_tab ? o_end : 0));
     // measured on C3 (polygons, 1.6M updates): 9 / 10 / 11 blocks per CU = 0.45 / 0.42 / 0.53 ms
-    per_cu = std::max(1, std::min(per_cu, 10));
+#ifndef KD_FD_CAP
+#define KD_FD_CAP 10
+#endif
+    per_cu = std::max(1, std::min(per_cu, KD_FD_CAP));
     const u64 upr = !lds_tab ? FD_NT : small ? fd_upr<KD_FD_SHAPE_S>(nullptr) : fd_upr<KD_FD_SHAPE_L>(nullptr);
     unsigned blocks = (unsigned)std::min<u64>((work + upr - 1) / upr, (u64)ctx->n_cu * (u64)per_cu);
     if (blocks == 0) blocks = 1;
@@ -1091,7 +1125,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
         auto args = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
-                               tb, to, (const u8*)dt, (const u8*)dz, d_masks, d_status);
+                               tb, to, (const u8*)dt, d_masks, d_status);
         };
         if (!lds_tab)
             hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
