@@ -271,6 +271,16 @@ int kd_diff2_gather(kd_ctx* ctx, const kd_side* base, const kd_side* target, uin
                     uint64_t target_off, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
                     uint64_t* d_counts, uint32_t* d_err, uint32_t* d_all_delta, uint64_t all_cap,
                     uint64_t* d_all_counts, uint64_t* h_all_counts);
+/* kd_diff2_gather in two halves, so the caller can queue work between them (the shard's
+ * kd_fielddiff): _begin queues the join, the rebase and the counts' all-gather (no host wait);
+ * _end waits for the counts, queues the records' all-gather on the context's communication
+ * stream (overlapping the work queued in between) and makes the context stream wait for it.
+ * kd_diff2_gather = _begin + _end. */
+int kd_diff2_gather_begin(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint64_t base_off,
+                          uint64_t target_off, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
+                          uint64_t* d_counts, uint32_t* d_err, uint64_t* d_all_counts);
+int kd_diff2_gather_end(kd_ctx* ctx, const uint32_t* d_delta, uint32_t* d_all_delta, uint64_t all_cap,
+                        uint64_t* h_all_counts);
 /* One process driving g GPUs (one context each): host sides are cut into g bucket ranges of about
  * equal entry count (bucket = the key's top bucket_bits bits: 24 for KD_KEY_INT, 6 per tree level
  * for base64 hash paths, 8 per level for hex), each shard diffed on its GPU, and the records

@@ -211,6 +211,14 @@ SIGNATURES = {
          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
     ),
+    "kd_diff2_gather_begin": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.c_uint64, ctypes.c_uint64,
+         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "kd_diff2_gather_end": (
+        ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p],
+    ),
     "kd_diff2_sharded": (
         ctypes.c_int,
         [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.c_int,

@@ -106,6 +106,17 @@ void comm_release(kd_ctx* ctx) {
     ctx->group_devs.clear();
 }
 
+void gather_release(kd_ctx* ctx) {
+    if (ctx->ev_counts) (void)hipEventDestroy(ctx->ev_counts);
+    if (ctx->ev_gathered) (void)hipEventDestroy(ctx->ev_gathered);
+    if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
+    if (ctx->h_counts_pin) (void)hipHostFree(ctx->h_counts_pin);
+    ctx->ev_counts = ctx->ev_gathered = nullptr;
+    ctx->comm_stream = nullptr;
+    ctx->h_counts_pin = nullptr;
+    ctx->h_counts_ranks = 0;
+}
+
 }  // namespace kd
 
 using namespace kd;
@@ -221,39 +232,81 @@ int kd_allgather_u64(kd_ctx* ctx, const uint64_t* d_send, uint64_t* d_recv, uint
     return KD_OK;
 }
 
-int kd_diff2_gather(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint64_t base_off, uint64_t target_off,
-                    uint32_t flags, uint32_t* d_delta, uint32_t* d_upd, uint64_t* d_counts, uint32_t* d_err,
-                    uint32_t* d_all_delta, uint64_t all_cap, uint64_t* d_all_counts, uint64_t* h_all_counts) {
+int kd_diff2_gather_begin(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint64_t base_off,
+                          uint64_t target_off, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd, uint64_t* d_counts,
+                          uint32_t* d_err, uint64_t* d_all_counts) {
     KD_CHECK(ctx && ctx->comm, "kd_diff2_gather: no communicator (kd_comm_init)");
     KD_CHECK(base && target && base->mem == KD_MEM_DEVICE && target->mem == KD_MEM_DEVICE,
              "kd_diff2_gather: sides must be device-resident");
-    KD_CHECK(d_delta && d_counts && d_err && d_all_delta && d_all_counts && h_all_counts, "kd_diff2_gather: NULL");
+    KD_CHECK(d_delta && d_counts && d_err && d_all_counts, "kd_diff2_gather: NULL");
     KD_CHECK(base_off + base->n < 0xFFFFFFFFull && target_off + target->n < 0xFFFFFFFFull,
              "kd_diff2_gather: global indices exceed uint32");
     Rccl* R;
     int rc;
     if ((rc = rccl(&R))) return rc;
     KD_HIP(hipSetDevice(ctx->device));
+    if (!ctx->ev_counts) {
+        KD_HIP(hipEventCreateWithFlags(&ctx->ev_counts, hipEventDisableTiming));
+        KD_HIP(hipEventCreateWithFlags(&ctx->ev_gathered, hipEventDisableTiming));
+        KD_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+    }
+    if (ctx->h_counts_ranks < ctx->nranks) {
+        if (ctx->h_counts_pin) KD_HIP(hipHostFree(ctx->h_counts_pin));
+        ctx->h_counts_pin = nullptr;
+        KD_HIP(hipHostMalloc((void**)&ctx->h_counts_pin, (size_t)ctx->nranks * 64, hipHostMallocDefault));
+        ctx->h_counts_ranks = ctx->nranks;
+    }
     // 1. this rank's shard (the device form; counts stay on the device)
     if ((rc = diff2_device(ctx, base, target, flags, d_delta, d_upd, d_counts, d_err))) return rc;
     // 2. records -> global sorted indices
     if ((rc = rebase(ctx, d_delta, d_counts + 3, base->n + target->n, base_off, target_off))) return rc;
-    // 3. all-gather the counts (+ the error word): [nranks][8] u64
+    // 3. all-gather the counts (+ the error word): [nranks][8] u64, then to pinned host memory
+    //    (asynchronous: the caller's next work is queued before anything waits for them)
     void* pack;
     if ((rc = ensure(ctx, "gather.pack", 64, &pack))) return rc;
     KD_HIP(hipMemcpyAsync(pack, d_counts, 32, hipMemcpyDeviceToDevice, ctx->stream));
     KD_HIP(hipMemsetAsync((u8*)pack + 32, 0, 32, ctx->stream));
     KD_HIP(hipMemcpyAsync((u8*)pack + 32, d_err, 4, hipMemcpyDeviceToDevice, ctx->stream));
     KD_NCCL(R, R->allGather(pack, d_all_counts, 8, ncclUint64, (ncclComm_t)ctx->comm, ctx->stream));
-    KD_HIP(hipMemcpyAsync(h_all_counts, d_all_counts, (size_t)ctx->nranks * 64, hipMemcpyDeviceToHost, ctx->stream));
-    KD_HIP(hipStreamSynchronize(ctx->stream));
-    // 4. all-gather the delta records, each rank's padded to the largest count (no all-gatherv)
+    KD_HIP(hipMemcpyAsync(ctx->h_counts_pin, d_all_counts, (size_t)ctx->nranks * 64, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    KD_HIP(hipEventRecord(ctx->ev_counts, ctx->stream));
+    return KD_OK;
+}
+
+int kd_diff2_gather_end(kd_ctx* ctx, const uint32_t* d_delta, uint32_t* d_all_delta, uint64_t all_cap,
+                        uint64_t* h_all_counts) {
+    KD_CHECK(ctx && ctx->comm && ctx->ev_counts, "kd_diff2_gather_end: no kd_diff2_gather_begin");
+    KD_CHECK(d_delta && d_all_delta && h_all_counts, "kd_diff2_gather_end: NULL");
+    Rccl* R;
+    int rc;
+    if ((rc = rccl(&R))) return rc;
+    KD_HIP(hipSetDevice(ctx->device));
+    // 4. the counts (the one host wait: the record stride), then the delta records, each rank's
+    //    padded to the largest count (no all-gatherv), on the communication stream
+    KD_HIP(hipEventSynchronize(ctx->ev_counts));
+    std::memcpy(h_all_counts, ctx->h_counts_pin, (size_t)ctx->nranks * 64);
     u64 mx = 0;
     for (int r = 0; r < ctx->nranks; r++) mx = std::max<u64>(mx, h_all_counts[8 * r + 3]);
     KD_CHECK(mx * (u64)ctx->nranks <= all_cap, "kd_diff2_gather: d_all_delta holds %llu records, %llu needed",
              (unsigned long long)all_cap, (unsigned long long)(mx * ctx->nranks));
-    if (mx) KD_NCCL(R, R->allGather(d_delta, d_all_delta, 2 * mx, ncclUint32, (ncclComm_t)ctx->comm, ctx->stream));
+    if (mx) {
+        KD_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->ev_counts, 0));
+        KD_NCCL(R, R->allGather(d_delta, d_all_delta, 2 * mx, ncclUint32, (ncclComm_t)ctx->comm, ctx->comm_stream));
+        KD_HIP(hipEventRecord(ctx->ev_gathered, ctx->comm_stream));
+        KD_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_gathered, 0));  // later work on the stream sees the records
+    }
     return KD_OK;
+}
+
+int kd_diff2_gather(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint64_t base_off, uint64_t target_off,
+                    uint32_t flags, uint32_t* d_delta, uint32_t* d_upd, uint64_t* d_counts, uint32_t* d_err,
+                    uint32_t* d_all_delta, uint64_t all_cap, uint64_t* d_all_counts, uint64_t* h_all_counts) {
+    int rc;
+    if ((rc = kd_diff2_gather_begin(ctx, base, target, base_off, target_off, flags, d_delta, d_upd, d_counts, d_err,
+                                    d_all_counts)))
+        return rc;
+    return kd_diff2_gather_end(ctx, d_delta, d_all_delta, all_cap, h_all_counts);
 }
 
 // ------------------------------------------------------------------------------------------

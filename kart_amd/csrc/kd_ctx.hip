@@ -218,6 +218,7 @@ int kd_fini(kd_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     prof_flush(ctx);
     comm_release(ctx);
+    gather_release(ctx);
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);

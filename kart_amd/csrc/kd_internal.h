@@ -80,6 +80,12 @@ struct kd_ctx {
     int nranks = 1, rank = 0;
     std::vector<int> group_devs;
     std::vector<void*> group_comms;
+    // kd_diff2_gather_begin / _end: the counts' pinned landing area, the event after it, and the
+    // stream the record all-gather runs on (overlapping whatever the caller queued in between)
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_counts = nullptr, ev_gathered = nullptr;
+    uint64_t* h_counts_pin = nullptr;
+    int h_counts_ranks = 0;
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
 };
 
@@ -87,6 +93,7 @@ namespace kd {
 
 // device scratch slot, grown as needed (never shrinks).  Not called inside timed regions once
 // kd_reserve() has sized it.
+void gather_release(kd_ctx* ctx);  // kd_comm.hip: kd_diff2_gather_begin/_end resources
 int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out);
 
 // 256 zero bytes of device memory: what empty inputs point at, and the target of loads issued by

@@ -166,13 +166,17 @@ class DiffPipeline:
             N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.ptr,
                                       self.upd.ptr, self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
         else:
-            N.check(L.kd_diff2_gather(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.gather[0], self.gather[1],
-                                      self.flags, self.delta.ptr, self.upd.ptr, self.counts.ptr, self.counts.ptr + 32,
-                                      self.all_delta.ptr, self.all_cap, self.all_counts.ptr, self.h_counts.ctypes.data),
-                    "kd_diff2_gather")
+            # the join, rebase and counts' all-gather; the field diff is queued before anything waits
+            # for the counts, and the records' all-gather (communication stream) overlaps it
+            N.check(L.kd_diff2_gather_begin(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.gather[0],
+                                            self.gather[1], self.flags, self.delta.ptr, self.upd.ptr, self.counts.ptr,
+                                            self.counts.ptr + 32, self.all_counts.ptr), "kd_diff2_gather_begin")
         N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.ptr, self.cap_upd,
                                ctypes.cast(self.counts.ptr + 8, N.c_u64p), N.KD_MEM_DEVICE,
                                ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE), "kd_fielddiff")
+        if self.gather is not None:
+            N.check(L.kd_diff2_gather_end(ctx, self.delta.ptr, self.all_delta.ptr, self.all_cap,
+                                          self.h_counts.ctypes.data), "kd_diff2_gather_end")
 
     def results(self):
         """host copies (synchronous): counts dict, delta [n,2], upd [m,2], masks, status"""

@@ -157,3 +157,34 @@ def test_shard_rank_gather_world1(engine, n):
         assert counts["inserts"] + counts["updates"] + counts["deletes"] == int(sel.sum())
     finally:
         engine.comm_fini()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [5000, 300_000])
+def test_diff_pipeline_gather_world1(engine, n):
+    """bench.py's N>1 step on a one-rank communicator: kd_diff2_gather_begin, the shard's field diff
+    queued before the counts are waited for, kd_diff2_gather_end (records all-gathered on the
+    communication stream) — gathered records, counts, masks and statuses against the oracle"""
+    from kart_amd import synth
+    from kart_amd.device import DiffPipeline
+    from kart_amd.engine import Engine
+    from kart_amd.schema import FieldMaps
+    from oracle import oracle as O
+
+    L = synth.polygons_layer(n, seed=17)
+    maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    engine.comm_init(1, 0, Engine.comm_unique_id())
+    try:
+        pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, gather=(0, 0))
+        for _ in range(3):  # repeated steps: the next join waits for the previous records' gather
+            pipe.step()
+        engine.sync()
+        g_counts, g_delta = pipe.gathered()
+        counts, delta, upd, masks, status = pipe.results()
+    finally:
+        engine.comm_fini()
+    od, oc = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
+    assert np.array_equal(g_delta, od) and np.array_equal(delta, od)
+    assert (g_counts["inserts"], g_counts["updates"], g_counts["deletes"]) == (oc["inserts"], oc["updates"], oc["deletes"])
+    om, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
+    assert np.array_equal(masks, om) and np.array_equal(status, ost)
