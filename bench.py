@@ -262,7 +262,8 @@ def run_diff(args, H, polygons):
         "k_fielddiff": upd_bytes + counts["updates"] * (8 + 8 * maps.words + 1),
     }
     dom = max((k for k in kern if k in alg), key=lambda k: kern[k][1]) if kern else None
-    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, n) if dom else None
+    # (the committed traffic files are 1-GPU profiles of the whole layer: not a shard's bytes)
+    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, n if world == 1 else -1) if dom else None
     cpu = host = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_diff(L, maps, args.cpu_seconds, "C3" if polygons else "C2")
