@@ -15,8 +15,7 @@
 //   1. LDS windows.  Per blob only a head window (NH 16-B chunks from the blob's aligned start) and a
 //      tail window (the NTL aligned chunks ending with the blob's last byte) are
 //      copied to LDS by LDS-DMA — the msgpack headers, the legend, and the short values that follow
-//      a long one.  Long payloads (geometries) never enter LDS, so ~10 KiB per 32 updates keeps
-//      ~10 waves per CU resident.
+//      a long one.  Long payloads (geometries) never enter LDS: 17.3 KiB per 52-update round.
 //   2. Parse: each lane walks its two blobs value by value from the windows (table-driven header
 //      decode from a 12-byte window; bytes outside both windows come from global memory), compares
 //      scalars and short payloads in registers or LDS, and queues every byte payload it cannot see
