@@ -877,18 +877,28 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         if (!(a && bn)) dhb = 1;
     };
     // LDS-DMA of one round's windows: instruction k fills image chunks [64k, 64k + 64), lane l chunk
-    // 64k + l (its blob and window position from the descriptors)
+    // 64k + l (its blob and window position from the descriptors).  The old blobs' images come
+    // first (owner o's at chunk NC o), then the new blobs' (at NC (UPR + o)): every instruction but
+    // the one straddling the two halves stages one side only, so it shuffles two descriptor words,
+    // not four (the fully unrolled stage keeps every shuffle result live until its one wait).
+    constexpr u32 HALF = (u32)UPR * NC;
     auto stage = [&]() {
-#pragma unroll 2
+#pragma unroll
         for (int k = 0; k < NCH / 64; k++) {
-            const u32 c = 64 * k + lane;
-            const u32 ow = c / LS, r = c - ow * LS;  // (LS even: an odd stride measured 50 % slower)
-            const u32 bl = 2 * ow + (r >= (u32)NC), i = r >= (u32)NC ? r - NC : r;
-            const bool real = ow < (u32)UPR && r < (u32)LS;
+            const u32 c = 64 * k + (lane & 63);
+            const bool sb = c >= HALF;
+            const u32 cs = sb ? c - HALF : c;
+            const u32 ow = cs / NC, i = cs - ow * NC;
+            const bool real = ow < (u32)UPR;
             const int src = real ? (int)ow : 0;
-            const u32 ha = __shfl(dha, src), la = __shfl(dla, src), hb_ = __shfl(dhb, src), lb = __shfl(dlb, src);
-            const bool sb = bl & 1;
-            const u32 h = sb ? hb_ : ha, l = sb ? lb : la;  // chunk indices
+            u32 h, l;  // chunk indices
+            if (64u * k + 63 < HALF) { h = __shfl(dha, src); l = __shfl(dla, src); }
+            else if (64u * k >= HALF) { h = __shfl(dhb, src); l = __shfl(dlb, src); }
+            else {
+                const u32 ha = __shfl(dha, src), la = __shfl(dla, src), hb_ = __shfl(dhb, src), lb = __shfl(dlb, src);
+                h = sb ? hb_ : ha;
+                l = sb ? lb : la;
+            }
             const u32 ci = i < (u32)NH ? h + i : l - (NTL - 1) + (i - NH);
             const bool valid = real && (int)(ci - h) >= 0 && (int)(l - ci) >= 0 && l >= h;
             const u64 addr = (sb ? nbase : obase) + 16ull * ci;
@@ -924,10 +934,10 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             BL A, B;
             A.start = a0; A.len = on; A.s0 = (u32)(a0 & 15);
             A.t0 = (int)(((a0 + (on ? on - 1 : 0)) & ~(u64)15) - (a0 & ~(u64)15)) - 16 * (NTL - 1);
-            A.img = img0 + 16u * (u32)(lane * LS);
+            A.img = img0 + 16u * (u32)(lane * NC);
             B.start = b0; B.len = nn; B.s0 = (u32)(b0 & 15);
             B.t0 = (int)(((b0 + (nn ? nn - 1 : 0)) & ~(u64)15) - (b0 & ~(u64)15)) - 16 * (NTL - 1);
-            B.img = img0 + 16u * (u32)(lane * LS + NC);
+            B.img = img0 + 16u * (u32)(UPR * NC + lane * NC);
             st = diff_one_w(A, B, tb, mk, m, queue);
         }
         __syncthreads();  // parse done: the image is free, the queue complete
