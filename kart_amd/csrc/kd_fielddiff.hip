@@ -786,7 +786,7 @@ __device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n) {
 constexpr u32 FD_TAB_LDS_MAX = 16384;
 // window shapes (updates per round, head chunks, tail chunks): small features / larger ones
 #ifndef KD_FD_SHAPE_L
-#define KD_FD_SHAPE_L 52, 5, 4  // C3 (100M): 48 / 52 / 56 updates per round = 1.73 (8 blocks per CU) / 1.69 (9) / 1.82 ms (8)
+#define KD_FD_SHAPE_L 60, 5, 4  // C3: 44 / 48 (9 blocks) / 52 / 56 / 60 updates per round = 1.691 / 1.753 / 1.705 / 1.659 / 1.633 ms
 #endif
 #ifndef KD_FD_SHAPE_S
 #define KD_FD_SHAPE_S 32, 8, 3  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
