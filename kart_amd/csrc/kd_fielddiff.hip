@@ -1122,7 +1122,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
                        : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
     int per_cu = 0;
     KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FD_NT, lds_tab ? o_end : 0));
-    // measured on C3 (polygons, 1.6M updates): 9 / 10 / 11 blocks per CU = 0.45 / 0.42 / 0.53 ms
+    // (the calculator can count one block per CU more than becomes resident: DESIGN.md §3.2)
 #ifndef KD_FD_CAP
 #define KD_FD_CAP 12  // C2 points: 10 / 12 blocks per CU = 36.8 / 35.1 us (C3 is LDS-bound at 8)
 #endif
