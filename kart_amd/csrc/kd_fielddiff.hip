@@ -727,76 +727,95 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
     return 0;
 }
 
-// Cooperative compare of one queued payload by a 16-lane group: lane j of step s takes old chunk
-// c = 16 s + j of the payload's aligned range and the matching 16 new bytes (two aligned chunks,
-// funnel-shifted by the two sides' relative skew).  Returns "differs" on every lane of the group.
-// A chunk is loaded only if it holds a byte of its payload (else the device zeros).
-__device__ __forceinline__ bool coop_differs(u64 a, u64 b, u32 n) {
+// Cooperative compare of M queued payloads by one 16-lane group: lane j of step s takes old chunk
+// c = 16 s + j of each payload's aligned range and the matching 16 new bytes (two aligned chunks,
+// funnel-shifted by the two sides' relative skew), every payload's loads issued before any compare.
+// d[m] = "payload m differs", on every lane of the group.  A chunk is loaded only if it holds a
+// byte of its payload (else zeros); an absent payload has n = 0.
+template <int M>
+__device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M], const u32 (&n)[M], bool (&d)[M]) {
     const u32 j = threadIdx.x & 15, grp = (threadIdx.x >> 4) & 3;
-    const u32 sa = (u32)(a & 15);
-    const u64 abase = a - sa;
-    const u64 e = b - sa, ebase = e & ~(u64)15;
-    const u32 sd = (u32)(e & 15), q = sd >> 2, sb = sd & 3;
-    const u64 bend = b + n;
-    const u32 nch = (n + sa + 15) >> 4;
-    bool diff = false;
-    for (u32 c0 = 0; c0 < nch; c0 += 32) {
-        u32x4 O[2], N0[2], N1[2];
+    u32 sa[M], sd[M], nch[M];
+    u64 abase[M], ebase[M];
+    u32 nmax = 0;
+    bool diff[M];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {  // both steps' loads issued before any compare
-            const u32 c = c0 + 16 * s + j;
-            const bool act = c < nch;
-            const u64 oa = abase + 16ull * c, na = ebase + 16ull * c;
-            const bool ok0 = act && na < bend && na + 16 > b;
-            const bool ok1 = act && sd != 0 && na + 16 < bend;
-            const u32x4 z = {0, 0, 0, 0};
-            O[s] = act ? *(gp128)oa : z;
-            N0[s] = ok0 ? *(gp128)na : z;
-            N1[s] = ok1 ? *(gp128)(na + 16) : z;
-        }
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const u32 c = c0 + 16 * s + j;
-            // dwords q .. q+4 of the 8 new dwords (two select stages on named values: an array
-            // here was turned into a dynamically indexed scratch copy)
-            const bool s1 = q & 1, s2 = q & 2;
-            const u32 b0 = s1 ? N0[s].y : N0[s].x, b1 = s1 ? N0[s].z : N0[s].y, b2 = s1 ? N0[s].w : N0[s].z;
-            const u32 b3 = s1 ? N1[s].x : N0[s].w, b4 = s1 ? N1[s].y : N1[s].x, b5 = s1 ? N1[s].z : N1[s].y;
-            const u32 b6 = s1 ? N1[s].w : N1[s].z;
-            const u32 t2[5] = {s2 ? b2 : b0, s2 ? b3 : b1, s2 ? b4 : b2, s2 ? b5 : b3, s2 ? b6 : b4};
-            const u32 o[4] = {O[s].x, O[s].y, O[s].z, O[s].w};
-            // payload bytes of this chunk: t in [lo, hi)
-            const int lo = c == 0 ? (int)sa : 0;
-            const int hi = (int)n + (int)sa - 16 * (int)c;
-            u32 d = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const u32 nw = __builtin_amdgcn_alignbyte(t2[k + 1], t2[k], sb);
-                const u32 lm = lo >= 4 * k + 4 ? 0u : lo <= 4 * k ? ~0u : ~0u << (8 * (lo - 4 * k));
-                const u32 hm = hi <= 4 * k ? 0u : hi >= 4 * k + 4 ? ~0u : (1u << (8 * (hi - 4 * k))) - 1;
-                d |= (o[k] ^ nw) & lm & hm;
-            }
-            diff |= c < nch && d != 0;
-        }
+    for (int m = 0; m < M; m++) {
+        sa[m] = (u32)(a[m] & 15);
+        abase[m] = a[m] - sa[m];
+        const u64 e = b[m] - sa[m];
+        ebase[m] = e & ~(u64)15;
+        sd[m] = (u32)(e & 15);
+        nch[m] = n[m] ? (n[m] + sa[m] + 15) >> 4 : 0;
+        nmax = nch[m] > nmax ? nch[m] : nmax;
+        diff[m] = false;
     }
-    const u64 bal = __ballot(diff);
-    return ((bal >> (16 * grp)) & 0xFFFF) != 0;
+    for (u32 c0 = 0; c0 < nmax; c0 += 32) {
+        u32x4 O[M][2], N0[M][2], N1[M][2];
+#pragma unroll
+        for (int m = 0; m < M; m++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const u32 c = c0 + 16 * s + j;
+                const bool act = c < nch[m];
+                const u64 oa = abase[m] + 16ull * c, na = ebase[m] + 16ull * c, bend = b[m] + n[m];
+                const bool ok0 = act && na < bend && na + 16 > b[m];
+                const bool ok1 = act && sd[m] != 0 && na + 16 < bend;
+                const u32x4 z = {0, 0, 0, 0};
+                O[m][s] = act ? *(gp128)oa : z;
+                N0[m][s] = ok0 ? *(gp128)na : z;
+                N1[m][s] = ok1 ? *(gp128)(na + 16) : z;
+            }
+#pragma unroll
+        for (int m = 0; m < M; m++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const u32 c = c0 + 16 * s + j;
+                const u32 q = sd[m] >> 2, sb = sd[m] & 3;
+                // dwords q .. q+4 of the 8 new dwords (two select stages on named values: an array
+                // here was turned into a dynamically indexed scratch copy)
+                const u32x4 P0 = N0[m][s], P1 = N1[m][s];
+                const bool s1 = q & 1, s2 = q & 2;
+                const u32 b0 = s1 ? P0.y : P0.x, b1 = s1 ? P0.z : P0.y, b2 = s1 ? P0.w : P0.z;
+                const u32 b3 = s1 ? P1.x : P0.w, b4 = s1 ? P1.y : P1.x, b5 = s1 ? P1.z : P1.y;
+                const u32 b6 = s1 ? P1.w : P1.z;
+                const u32 t2[5] = {s2 ? b2 : b0, s2 ? b3 : b1, s2 ? b4 : b2, s2 ? b5 : b3, s2 ? b6 : b4};
+                const u32 o[4] = {O[m][s].x, O[m][s].y, O[m][s].z, O[m][s].w};
+                // payload bytes of this chunk: t in [lo, hi)
+                const int lo = c == 0 ? (int)sa[m] : 0;
+                const int hi = (int)n[m] + (int)sa[m] - 16 * (int)c;
+                u32 dd = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const u32 nw = __builtin_amdgcn_alignbyte(t2[k + 1], t2[k], sb);
+                    const u32 lm = lo >= 4 * k + 4 ? 0u : lo <= 4 * k ? ~0u : ~0u << (8 * (lo - 4 * k));
+                    const u32 hm = hi <= 4 * k ? 0u : hi >= 4 * k + 4 ? ~0u : (1u << (8 * (hi - 4 * k))) - 1;
+                    dd |= (o[k] ^ nw) & lm & hm;
+                }
+                diff[m] |= c < nch[m] && dd != 0;
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (16 * grp)) & 0xFFFF) != 0;
 }
 
 constexpr u32 FD_TAB_LDS_MAX = 16384;
 // window shapes (updates per round, head chunks, tail chunks): small features / larger ones
 #ifndef KD_FD_SHAPE_L
-#define KD_FD_SHAPE_L 60, 5, 4  // C3: 44 / 48 (9 blocks) / 52 / 56 / 60 updates per round = 1.691 / 1.753 / 1.705 / 1.659 / 1.633 ms
+#ifndef KD_FD_TM_L
+#define KD_FD_TM_L 3  // payloads per 16-lane group per pass (C3: 1 / 2 / 3 / 4 = 1.60 / 1.60 / 1.53-1.56 / 2.32 ms)
+#endif
+#define KD_FD_SHAPE_L 60, 5, 4, KD_FD_TM_L  // C3: 44 / 48 (9 blocks) / 52 / 56 / 60 updates per round = 1.691 / 1.753 / 1.705 / 1.659 / 1.633 ms
 #endif
 #ifndef KD_FD_SHAPE_S
-#define KD_FD_SHAPE_S 32, 8, 3  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
+#define KD_FD_SHAPE_S 32, 8, 3, 1  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
 #endif
-template <int UPR, int NH, int NTL>
+template <int UPR, int NH, int NTL, int TM>
 constexpr int fd_upr(const void*) { return UPR; }  // tables up to this size are copied into each block's LDS
 typedef __attribute__((address_space(3))) void* fd_lds_vp;
 typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 
-template <int UPR, int NH, int NTL>
+template <int UPR, int NH, int NTL, int TM>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
@@ -948,13 +967,28 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         }
         // ---- the queued payloads, 16 lanes per payload ----
         const u32 nt = min(s_ntask, TCAP);
-        for (u32 t = (u32)lane >> 4; t < nt; t += 4) {
-            const u64 x = s_task[3 * t + 2];
-            const bool d = coop_differs(s_task[3 * t], s_task[3 * t + 1], (u32)x);
-            if (d && (lane & 15) == 0) {
-                const u32 ow = (u32)(x >> 32) & 0xFFFF, key = (u32)(x >> 48);
-                atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
+        // (M payloads per 16-lane group per pass: their loads share one memory round trip)
+        constexpr int M = TM;
+        for (u32 t = (u32)lane >> 4; t < nt; t += 4 * M) {
+            u64 ta[M], tbb[M], tx[M];
+            u32 tn[M];
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                const u32 tm = t + 4 * m;
+                const bool h = tm < nt;
+                ta[m] = h ? s_task[3 * tm] : 0;
+                tbb[m] = h ? s_task[3 * tm + 1] : 0;
+                tx[m] = h ? s_task[3 * tm + 2] : 0;
+                tn[m] = (u32)tx[m];
             }
+            bool d[M];
+            coop_differs<M>(ta, tbb, tn, d);
+#pragma unroll
+            for (int m = 0; m < M; m++)
+                if (d[m] && (lane & 15) == 0) {
+                    const u32 ow = (u32)(tx[m] >> 32) & 0xFFFF, key = (u32)(tx[m] >> 48);
+                    atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
+                }
         }
         __syncthreads();  // the compares are in s_res; vmcnt(0): the next windows have landed
         if (act) {
