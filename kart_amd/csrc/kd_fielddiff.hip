@@ -732,9 +732,9 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
 // funnel-shifted by the two sides' relative skew), every payload's loads issued before any compare.
 // d[m] = "payload m differs", on every lane of the group.  A chunk is loaded only if it holds a
 // byte of its payload (else zeros); an absent payload has n = 0.
-template <int M>
+template <int M, int G, int S>
 __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M], const u32 (&n)[M], bool (&d)[M]) {
-    const u32 j = threadIdx.x & 15, grp = (threadIdx.x >> 4) & 3;
+    const u32 j = threadIdx.x & (G - 1), grp = (threadIdx.x & 63) / G;
     u32 sa[M], sd[M], nch[M];
     u64 abase[M], ebase[M];
     u32 nmax = 0;
@@ -750,13 +750,13 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
         nmax = nch[m] > nmax ? nch[m] : nmax;
         diff[m] = false;
     }
-    for (u32 c0 = 0; c0 < nmax; c0 += 32) {
-        u32x4 O[M][2], N0[M][2], N1[M][2];
+    for (u32 c0 = 0; c0 < nmax; c0 += G * S) {
+        u32x4 O[M][S], N0[M][S], N1[M][S];
 #pragma unroll
         for (int m = 0; m < M; m++)
 #pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const u32 c = c0 + 16 * s + j;
+            for (int s = 0; s < S; s++) {
+                const u32 c = c0 + G * s + j;
                 const bool act = c < nch[m];
                 const u64 oa = abase[m] + 16ull * c, na = ebase[m] + 16ull * c, bend = b[m] + n[m];
                 const bool ok0 = act && na < bend && na + 16 > b[m];
@@ -769,8 +769,8 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
 #pragma unroll
         for (int m = 0; m < M; m++)
 #pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const u32 c = c0 + 16 * s + j;
+            for (int s = 0; s < S; s++) {
+                const u32 c = c0 + G * s + j;
                 const u32 q = sd[m] >> 2, sb = sd[m] & 3;
                 // dwords q .. q+4 of the 8 new dwords (two select stages on named values: an array
                 // here was turned into a dynamically indexed scratch copy)
@@ -796,7 +796,7 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
             }
     }
 #pragma unroll
-    for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (16 * grp)) & 0xFFFF) != 0;
+    for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
 }
 
 constexpr u32 FD_TAB_LDS_MAX = 16384;
@@ -805,17 +805,20 @@ constexpr u32 FD_TAB_LDS_MAX = 16384;
 #ifndef KD_FD_TM_L
 #define KD_FD_TM_L 3  // payloads per 16-lane group per pass (C3: 1 / 2 / 3 / 4 = 1.60 / 1.60 / 1.53-1.56 / 2.32 ms)
 #endif
-#define KD_FD_SHAPE_L 60, 5, 4, KD_FD_TM_L  // C3: 44 / 48 (9 blocks) / 52 / 56 / 60 updates per round = 1.691 / 1.753 / 1.705 / 1.659 / 1.633 ms
+#ifndef KD_FD_TGS_L
+#define KD_FD_TGS_L 16, 2  // lanes per payload, 16-B steps per lane per pass
+#endif
+#define KD_FD_SHAPE_L 60, 5, 4, KD_FD_TM_L, KD_FD_TGS_L  // C3: 44 / 48 (9 blocks) / 52 / 56 / 60 updates per round = 1.691 / 1.753 / 1.705 / 1.659 / 1.633 ms
 #endif
 #ifndef KD_FD_SHAPE_S
-#define KD_FD_SHAPE_S 32, 8, 3, 1  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
+#define KD_FD_SHAPE_S 32, 8, 3, 1, 16, 2  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
 #endif
-template <int UPR, int NH, int NTL, int TM>
+template <int UPR, int NH, int NTL, int TM, int TG, int TS>
 constexpr int fd_upr(const void*) { return UPR; }  // tables up to this size are copied into each block's LDS
 typedef __attribute__((address_space(3))) void* fd_lds_vp;
 typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 
-template <int UPR, int NH, int NTL, int TM>
+template <int UPR, int NH, int NTL, int TM, int TG, int TS>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
@@ -968,13 +971,13 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
         // ---- the queued payloads, 16 lanes per payload ----
         const u32 nt = min(s_ntask, TCAP);
         // (M payloads per 16-lane group per pass: their loads share one memory round trip)
-        constexpr int M = TM;
-        for (u32 t = (u32)lane >> 4; t < nt; t += 4 * M) {
+        constexpr int M = TM, G = TG, NG = 64 / TG;
+        for (u32 t = (u32)lane / G; t < nt; t += NG * M) {
             u64 ta[M], tbb[M], tx[M];
             u32 tn[M];
 #pragma unroll
             for (int m = 0; m < M; m++) {
-                const u32 tm = t + 4 * m;
+                const u32 tm = t + NG * m;
                 const bool h = tm < nt;
                 ta[m] = h ? s_task[3 * tm] : 0;
                 tbb[m] = h ? s_task[3 * tm + 1] : 0;
@@ -982,10 +985,10 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
                 tn[m] = (u32)tx[m];
             }
             bool d[M];
-            coop_differs<M>(ta, tbb, tn, d);
+            coop_differs<M, G, TS>(ta, tbb, tn, d);
 #pragma unroll
             for (int m = 0; m < M; m++)
-                if (d[m] && (lane & 15) == 0) {
+                if (d[m] && (lane & (G - 1)) == 0) {
                     const u32 ow = (u32)(tx[m] >> 32) & 0xFFFF, key = (u32)(tx[m] >> 48);
                     atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
                 }
