@@ -59,6 +59,11 @@ def parse():
     ap.add_argument("--no-host-timing", action="store_true", help="skip the host pack / H2D timings")
     ap.add_argument("--unordered", action="store_true",
                     help="c2/c3: tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
+    ap.add_argument("--sort-gather", action="store_true",
+                    help="with-sort steps: permute the OIDs in the sort (k_gather_oid) instead of reading them "
+                         "through the order in the join")
+    ap.add_argument("--no-sort", action="store_true",
+                    help="c2/c3: skip the with-sort steps (sides from git walk order, both GPU sorts in the step)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
@@ -209,6 +214,11 @@ def run_diff(args, H, polygons):
     log(f"[rank {rank}] generated {L.base.n}+{L.target.n} entries in {gen_s:.1f}s "
         f"(+{L.n_insert} ins, {L.n_update} upd, -{L.n_delete} del)")
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    walk = None
+    if not args.no_sort:  # the sides as the tree walk hands them to the packer: git path order
+        t0 = time.time()
+        walk = (synth.walk_perm(L.base.key), synth.walk_perm(L.target.key))
+        log(f"[rank {rank}] walk (git tree) order of both sides in {time.time() - t0:.1f}s")
     eng = engine_for(H)
     gather = None
     if split:  # global sorted index of this shard's first entry on each side
@@ -216,7 +226,7 @@ def run_diff(args, H, polygons):
         gather = (sum(s[0] for s in sizes[:rank]), sum(s[1] for s in sizes[:rank]))
     t0 = time.perf_counter()
     pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=not args.unordered,
-                        gather=gather)
+                        gather=gather, walk=walk, late=not args.sort_gather)
     h2d_s = time.perf_counter() - t0
     h2d_bytes = 28 * (L.base.n + L.target.n) + int(L.base_blobs[0].size + L.target_blobs[0].size) + \
         8 * int(L.base_blobs[1].size + L.target_blobs[1].size)
@@ -230,6 +240,12 @@ def run_diff(args, H, polygons):
     if not args.no_check:
         assert (counts["inserts"], counts["updates"], counts["deletes"]) == plan, (counts, plan)
         assert not status.any(), "fielddiff status flags set"
+        if walk is not None:  # the GPU sorts rebuilt the key-ordered sides exactly
+            for S, side, perm, order in zip((pipe.A, pipe.B), (L.base, L.target), walk, pipe.orders()):
+                assert np.array_equal(S.key.download(np.uint64, side.n), side.key), "sorted keys differ"
+                assert np.array_equal(S.oid.download(np.uint8, 20 * side.n).reshape(side.n, 20), side.oid), \
+                    "sorted OIDs differ"
+                assert np.array_equal(perm[order], np.arange(side.n)), "sort order differs"
     if split:
         mx = max(x for x in H.allgather(counts["deltas"]))
         pipe.reserve_gather(mx)
@@ -245,11 +261,34 @@ def run_diff(args, H, polygons):
     eng.prof_reset()
     eng.prof_select(None if args.time_all else ["k_fielddiff" if polygons else "k_join2"])
     eng.prof_enable(not args.no_events)
-    elapsed = timed(H, eng, pipe.step, args.steps)
+    elapsed = timed(H, eng, pipe.diff_step, args.steps)  # presorted device-resident sides
     eng.prof_enable(False)
     total_pairs = sum(H.allgather(n_pairs))
     total_deltas = sum(H.allgather(counts["deltas"]))
     kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_fielddiff", "k_rebase"))
+    sort = None
+    if walk is not None:  # the same steps from walk-order sides: both GPU side sorts inside each step
+        elapsed_ws = timed(H, eng, pipe.step, args.steps)
+        eng.prof_reset()
+        eng.prof_select(None)
+        eng.prof_enable(True)
+        for _ in range(3):  # per-kernel times of the sorts (untimed steps, events around every launch)
+            pipe.sort_step()
+        eng.sync()
+        eng.prof_enable(False)
+        sk = kernel_times(eng, SORT_KERNELS)
+        sort = sort_summary(L, sk, elapsed_ws, elapsed, args.steps, total_pairs, H, pipe.late)
+        if pipe.late:  # the join of the with-sort step reads OIDs through the orders: its own time
+            eng.prof_reset()
+            eng.prof_select(["k_join2"])
+            eng.prof_enable(True)
+            for _ in range(3):
+                pipe.step()
+            eng.sync()
+            eng.prof_enable(False)
+            jp = kernel_times(eng, ("k_join2",))
+            if "k_join2" in jp:
+                sort["k_join2_perm_avg_ms"] = round(jp["k_join2"][1], 5)
 
     # ---- roofline of the dominant kernel (algorithmic bytes per launch) ----
     nA, nB = L.base.n, L.target.n
@@ -297,9 +336,63 @@ def run_diff(args, H, polygons):
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if sort:
+        out["value_with_sort"] = sort.pop("value_with_sort")
+        out["ms_per_step_with_sort"] = sort.pop("ms_per_step_with_sort")
+        out["sort"] = sort
     if host:
         out["host"] = host
     return out
+
+
+SORT_KERNELS = ("k_rs_bits", "k_sort_hist", "k_sort_scan", "k_sort_pass", "k_gather_oid")
+
+
+def sort_bytes(keys, gather_oids):
+    """algorithmic HBM bytes of kd_sort_side_into over one side: the varying-bit
+    pass (8 B read per key), the all-pass histogram (8 B), the digit passes (first: 8-B key read,
+    4-B compact key + 4-B index written; middle: 8 B read + 8 B written; last: 8 B read, 8-B key +
+    4-B order written; 64-bit compact keys move 4 B more per key each way), and the OID gather
+    (4-B order + 20-B row read, 20 B written) unless the join reads the OIDs through the order
+    (late materialisation: kd_diff2_device_perm).  Returns (bytes, passes)."""
+    n = int(keys.shape[0])
+    if n < 2:
+        return 0, 0
+    vary = int(np.bitwise_or.reduce(keys ^ keys[0]))
+    bits = bin(vary).count("1")  # compact width (gaps absorbed only beyond 4 runs: not for int keys)
+    npass = -(-bits // 8)
+    ck = 4 if bits <= 32 else 8
+    b = 8 * n + 8 * n  # bits + histogram
+    for p in range(npass):
+        rd = 8 if p == 0 else ck + 4
+        wr = 12 if p == npass - 1 else ck + 4
+        b += (rd + wr) * n
+    if gather_oids:
+        b += 44 * n
+    return b, npass
+
+
+def sort_summary(L, sk, elapsed_ws, elapsed, steps, total_pairs, H, late):
+    bb, pb = sort_bytes(L.base.key, not late)
+    bt, pt = sort_bytes(L.target.key, not late)
+    ms_sorts = sum(v[0] * v[1] for v in sk.values()) / 3  # both sides, per step (3 profiled steps)
+    alg = bb + bt
+    return {
+        "value_with_sort": round(total_pairs * steps / elapsed_ws / 1e6, 2),
+        "ms_per_step_with_sort": round(elapsed_ws / steps * 1e3, 4),
+        "what": "each step sorts both sides from git tree (walk) order on the GPU (kd_sort_side_into: onesweep LSD "
+                "radix sort of the compacted varying key bits) then classify2 + field diff; " +
+                ("the join reads the walk-order OIDs through the sort order (kd_diff2_device_perm)" if late else
+                 "the OIDs are gathered into key order by the sort"),
+        "passes": [pb, pt],
+        "kernels_avg_ms": {k: round(v[1], 5) for k, v in sk.items()},
+        "kernel_launches_per_step": {k: v[0] // 3 for k, v in sk.items()},
+        "sort_ms_per_step_events": round(ms_sorts, 4),
+        "sort_ms_per_step_wall": round((elapsed_ws - elapsed) / steps * 1e3, 4),
+        "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": int(alg),
+                     "achieved": round(alg / (ms_sorts * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(alg / (ms_sorts * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+    }
 
 
 def _shard_bounds(L, parts):

@@ -151,6 +151,15 @@ int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t f
 int kd_diff2_device(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags,
                     uint32_t* d_delta, uint32_t* d_upd, uint64_t* d_counts, uint32_t* d_err);
 
+/* Late-materialised form, what follows kd_sort_side_into(..., d_oid_out = NULL, ...): each side's
+ * keys are sorted but its OIDs (and KD_KEY_HASH filename offsets) are still in the order the tree
+ * walk produced them; row order[i] belongs to sorted entry i.  The join reads OIDs through the order
+ * (one extra coalesced 4-B load per matched entry), so no side's OIDs are ever permuted.  Results are
+ * identical to kd_diff2_device on the permuted sides (indices are sorted-entry indices). */
+int kd_diff2_device_perm(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* base_order,
+                         const uint32_t* target_order, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
+                         uint64_t* d_counts, uint32_t* d_err);
+
 /* -------- field diff -------- */
 /* For each update u: old blob = old->data[old->off[pu[2u]] ..], new blob = neu->...[pu[2u+1]]
  * (pu = the (base, target) update pairs, or NULL: blob u on both sides).  masks[u*words + w]
@@ -231,12 +240,20 @@ int kd_hex_encode(kd_ctx* ctx, const kd_blobs* blobs, uint32_t mode, uint8_t* he
                   uint8_t* status, uint32_t out_mem);
 
 /* -------- packing on the GPU (the sort that follows the leaf-path decode) -------- */
-/* Sort one side's n entries by join key on the device: an LSD radix sort over the keys' varying
- * bits (LDS-ranked tiles, stable).  d_key [n] is sorted in place; d_order [n] <- original index of
+/* Sort one side's n entries by join key on the device: an onesweep LSD radix sort over the keys'
+ * varying bits (LDS-ranked, LDS-reordered tiles, decoupled look-back; stable).  d_key [n] is sorted in place; d_order [n] <- original index of
  * sorted entry k; d_oid [n*20] (may be NULL) is permuted in place.  *h_dup (may be NULL) <- 1 when
  * the sorted keys are not strictly ascending (two entries share a key: the caller's fallback).
  * Replaces the host sort of the packer (Dataset3 leaves arrive in git path order, not key order). */
 int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32_t* d_order, uint64_t n, uint32_t* h_dup);
+/* Out-of-place form (what a device pipeline runs): d_key_in / d_oid_in hold the side in walk order
+ * and are left unchanged; d_key_out [n] <- the keys ascending, d_oid_out [n*20] <- the OIDs in that
+ * order (both oid pointers NULL to skip), d_order [n] <- input index of sorted entry k.  d_dup
+ * (device, may be NULL: a following kd_diff2_device checks strict order anyway) <- 1 when two
+ * entries share a key.  Outputs must not alias inputs.  Asynchronous on the context stream except
+ * for one 16-byte read-back (which key bits vary: it sizes the passes). */
+int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oid_in, uint64_t* d_key_out,
+                      uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup);
 
 /* -------- device memory and copies (no GPU framework needed by the caller) -------- */
 #define KD_COPY_H2D 1u

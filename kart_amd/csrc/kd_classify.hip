@@ -374,6 +374,20 @@ int kd_diff2_device(kd_ctx* ctx, const kd_side* base, const kd_side* target, uin
     return diff2_device(ctx, base, target, flags, d_delta, d_upd, d_counts, d_err);
 }
 
+int kd_diff2_device_perm(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* base_order,
+                         const uint32_t* target_order, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
+                         uint64_t* d_counts, uint32_t* d_err) {
+    KD_CHECK(ctx, "kd_diff2_device_perm: ctx NULL");
+    int rc;
+    if ((rc = check_side(base, "base")) || (rc = check_side(target, "target"))) return rc;
+    KD_CHECK(base->mem == KD_MEM_DEVICE && target->mem == KD_MEM_DEVICE, "kd_diff2_device_perm: sides must be device memory");
+    KD_CHECK(d_delta && d_counts && d_err, "kd_diff2_device_perm: NULL output");
+    KD_CHECK((base->n == 0 || base_order) && (target->n == 0 || target_order), "kd_diff2_device_perm: NULL order");
+    KD_HIP(hipSetDevice(ctx->device));
+    return diff2_device(ctx, base, target, flags, d_delta, d_upd, d_counts, d_err,
+                        base_order ? base_order : (const u32*)nullptr, target_order);
+}
+
 int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags, kd_diff_result** out) {
     KD_CHECK(ctx && out, "kd_diff2: NULL");
     int rc;

@@ -145,6 +145,8 @@ struct Join2Args {
     const u64* nameOffB;
     int hash_mode;
     const u8* dummy;     // >= 16 readable device bytes: source of masked-off chunk loads
+    const u32* ordA;     // PERM: row of sorted entry i in the OID (and filename-offset) arrays
+    const u32* ordB;
     uint2* stage_delta;  // staged path: tile-local slots of TILE records
     uint2* stage_upd;
     u32* tile_cnt;       // staged path: [ntiles*4] inserts, updates, deletes, deltas
@@ -316,16 +318,34 @@ __device__ __forceinline__ void tile_walk(const u64* sA, const u64* sB, const Ti
 
 // OID compare straight from HBM (keys-only LDS image): each thread loads the two 20-B OIDs of its own
 // matched pairs (consecutive items -> neighbouring entries across lanes), all loads issued before any
-// compare
-template <int IPT>
-__device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGeo& q, u32 rec[IPT]) {
+// compare.  PERM (late materialisation after kd_sort_side_into without OIDs): the OIDs stay in the
+// order the walk produced them and sorted entry i's row is ord[i] — one more (coalesced) load round
+// trip instead of a 44-B-per-entry OID gather per side.  ra / rb <- the rows of the matched pairs.
+template <int IPT, bool PERM>
+__device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGeo& q, u32 rec[IPT], u32 ra[IPT],
+                                                u32 rb[IPT]) {
     typedef const __attribute__((address_space(1))) u32* gp32;
     u32 x[IPT][5], y[IPT][5];
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
+        ra[k] = (u32)q.i0 + (rec[k] & 0xFFF);
+        rb[k] = (u32)q.j0 + ((rec[k] >> 12) & 0xFFF);
+    }
+    if (PERM) {
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const bool m = (rec[k] >> 25) == R_MATCH;
+            const gp32 oa = m ? (gp32)(g.ordA + ra[k]) : (gp32)g.dummy;
+            const gp32 ob = m ? (gp32)(g.ordB + rb[k]) : (gp32)g.dummy;
+            ra[k] = *oa;
+            rb[k] = *ob;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
         const bool m = (rec[k] >> 25) == R_MATCH;
-        const gp32 pa = m ? (gp32)(g.oidA + 20 * (q.i0 + (rec[k] & 0xFFF))) : (gp32)g.dummy;
-        const gp32 pb = m ? (gp32)(g.oidB + 20 * (q.j0 + ((rec[k] >> 12) & 0xFFF))) : (gp32)g.dummy;
+        const gp32 pa = m ? (gp32)(g.oidA + 20ull * ra[k]) : (gp32)g.dummy;
+        const gp32 pb = m ? (gp32)(g.oidB + 20ull * rb[k]) : (gp32)g.dummy;
 #pragma unroll
         for (int w = 0; w < 5; w++) { x[k][w] = pa[w]; y[k][w] = pb[w]; }
     }
@@ -341,14 +361,10 @@ __device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGe
 // KD_KEY_HASH: a matched key must also match the full filename (a 64-bit key collision between two
 // different names would otherwise be read as an update)
 template <int IPT>
-__device__ __forceinline__ void tile_names(const Join2Args& g, const TileGeo& q, const u32 rec[IPT]) {
-    u32 ia[IPT], jb[IPT], act = 0;
+__device__ __forceinline__ void tile_names(const Join2Args& g, const u32 rec[IPT], const u32 ia[IPT], const u32 jb[IPT]) {
+    u32 act = 0;
 #pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        ia[k] = (u32)q.i0 + (rec[k] & 0xFFF);
-        jb[k] = (u32)q.j0 + ((rec[k] >> 12) & 0xFFF);
-        act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
-    }
+    for (int k = 0; k < IPT; k++) act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
     if (names_ne_batch<IPT, 8>(g.nameA, g.nameOffA, ia, g.nameB, g.nameOffB, jb, act)) atomicOr(g.err, 2u);
 }
 
@@ -424,7 +440,7 @@ __device__ __forceinline__ void tile_write(const u32 rec[IPT], const TileCounts&
 // The tile is staged in ONE HBM round trip: keys and OIDs of both sides go global -> LDS by LDS-DMA
 // (global_load_lds_dwordx4: 16 B per lane, the wave's 64 chunks land contiguously), all issued
 // before any use.
-template <int NT, int IPT, bool UNORD, bool HASH>
+template <int NT, int IPT, bool UNORD, bool HASH, bool PERM>
 __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // (HASH: filename checks compiled in; the int-key instantiation carries none of their registers)
     using LD = Join2Lds<NT, IPT>;
@@ -467,8 +483,9 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // (the first against the lookbehind key) is checked here as well
     for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
     for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
-    tile_oid_global<IPT>(g, q, rec);
-    if (HASH) tile_names<IPT>(g, q, rec);
+    u32 ra[IPT], rb[IPT];
+    tile_oid_global<IPT, PERM>(g, q, rec, ra, rb);
+    if (HASH) tile_names<IPT>(g, rec, ra, rb);
     if (bad) atomicOr(g.err, 1u);
     const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
     uint2 *sd, *su;
@@ -611,7 +628,7 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
 }
 
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
-                 u64* d_counts, u32* d_err) {
+                 u64* d_counts, u32* d_err, const u32* ordA, const u32* ordB) {
     const bool unord = (flags & KD_DIFF_UNORDERED) != 0;
     const u64 nA = A->n, nB = B->n, total = nA + nB;
     KD_CHECK(nA < 0xFFFFFFFFull && nB < 0xFFFFFFFFull, "diff2: side too large for uint32 indices");
@@ -662,21 +679,23 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.nameOffB = nB && B->name_off ? B->name_off : (const u64*)dz;
     g.hash_mode = hash ? 1 : 0;
     g.dummy = (const u8*)dz;
+    const bool perm = ordA != nullptr || ordB != nullptr;
+    g.ordA = nA && ordA ? ordA : (const u32*)dz;
+    g.ordB = nB && ordB ? ordB : (const u32*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
     g.tile_cnt = (u32*)tcnt; g.gsum = (u64*)gsum; g.err = d_err;
     g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd; g.counts = d_counts;
     g.ntiles = ntiles;
     rc = launch(ctx, "k_join2", [&] {
-        if (unord) {
-            if (hash)
-                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
-            else
-                hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, true, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
-        } else if (hash) {
-            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+#define KD_J2(U, H, P) hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, U, H, P>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g)
+        if (perm) {
+            if (unord) { if (hash) KD_J2(true, true, true); else KD_J2(true, false, true); }
+            else { if (hash) KD_J2(false, true, true); else KD_J2(false, false, true); }
         } else {
-            hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, false, false>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g);
+            if (unord) { if (hash) KD_J2(true, true, false); else KD_J2(true, false, false); }
+            else { if (hash) KD_J2(false, true, false); else KD_J2(false, false, false); }
         }
+#undef KD_J2
     });
     if (rc || unord) return rc;
     rc = launch(ctx, "k_gscan2", [&] {

@@ -258,6 +258,7 @@ int kd_diff2_gather_begin(kd_ctx* ctx, const kd_side* base, const kd_side* targe
     }
     // 1. this rank's shard (the device form; counts stay on the device)
     if ((rc = diff2_device(ctx, base, target, flags, d_delta, d_upd, d_counts, d_err))) return rc;
+    ctx->gather_send_cap = base->n + target->n + 1;  // records d_delta holds (the documented capacity)
     // 2. records -> global sorted indices
     if ((rc = rebase(ctx, d_delta, d_counts + 3, base->n + target->n, base_off, target_off))) return rc;
     // 3. all-gather the counts (+ the error word): [nranks][8] u64, then to pinned host memory
@@ -286,16 +287,32 @@ int kd_diff2_gather_end(kd_ctx* ctx, const uint32_t* d_delta, uint32_t* d_all_de
     //    padded to the largest count (no all-gatherv), on the communication stream
     KD_HIP(hipEventSynchronize(ctx->ev_counts));
     std::memcpy(h_all_counts, ctx->h_counts_pin, (size_t)ctx->nranks * 64);
+    // Every decision before the collective uses only the gathered counts, which every rank holds
+    // identically: no rank may return early while the others enter the all-gather.
     u64 mx = 0;
     for (int r = 0; r < ctx->nranks; r++) mx = std::max<u64>(mx, h_all_counts[8 * r + 3]);
-    KD_CHECK(mx * (u64)ctx->nranks <= all_cap, "kd_diff2_gather: d_all_delta holds %llu records, %llu needed",
-             (unsigned long long)all_cap, (unsigned long long)(mx * ctx->nranks));
+    const bool fits = mx * (u64)ctx->nranks <= all_cap;
     if (mx) {
-        KD_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->ev_counts, 0));
-        KD_NCCL(R, R->allGather(d_delta, d_all_delta, 2 * mx, ncclUint32, (ncclComm_t)ctx->comm, ctx->comm_stream));
+        const u64 mine = h_all_counts[8 * ctx->rank + 3];
+        const void* send = d_delta;
+        void* recv = d_all_delta;
+        KD_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->ev_counts, 0));  // the records are final by then
+        if (mx > ctx->gather_send_cap) {  // this shard's d_delta is shorter than the padded stride
+            void* sb;
+            if ((rc = ensure(ctx, "gather.send", mx * 8, &sb))) return rc;
+            if (mine) KD_HIP(hipMemcpyAsync(sb, d_delta, mine * 8, hipMemcpyDeviceToDevice, ctx->comm_stream));
+            send = sb;
+        }
+        if (!fits) {  // still take part (into scratch), then report the short buffer
+            if ((rc = ensure(ctx, "gather.recv", mx * (u64)ctx->nranks * 8, &recv))) return rc;
+        }
+        KD_NCCL(R, R->allGather(send, recv, 2 * mx, ncclUint32, (ncclComm_t)ctx->comm, ctx->comm_stream));
         KD_HIP(hipEventRecord(ctx->ev_gathered, ctx->comm_stream));
         KD_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_gathered, 0));  // later work on the stream sees the records
     }
+    KD_CHECK(fits, "kd_diff2_gather: d_all_delta holds %llu records, %llu needed (this rank took part in the "
+                   "all-gather; records not delivered)",
+             (unsigned long long)all_cap, (unsigned long long)(mx * ctx->nranks));
     return KD_OK;
 }
 
@@ -402,14 +419,25 @@ int kd_diff2_sharded(kd_ctx** ctxs, int g, const kd_side* base, const kd_side* t
         return KD_EUNSUPPORTED;
     }
     if (mx) {
+        std::vector<const u32*> send(g);
         for (int i = 0; i < g; i++) {
             void* a;
+            KD_HIP(hipSetDevice(ctxs[i]->device));
             if ((rc = ensure(ctxs[i], "sh.all", (size_t)g * mx * 8, &a))) return rc;
             dall[i] = (u32*)a;
+            send[i] = dd[i];
+            const u64 cap = a_lo[i + 1] - a_lo[i] + b_lo[i + 1] - b_lo[i] + 1;  // records sh.delta holds
+            if (mx > cap) {  // a shard shorter than the padded stride sends from a copy of stride size
+                void* sb;
+                if ((rc = ensure(ctxs[i], "sh.send", mx * 8, &sb))) return rc;
+                if (hc[8 * i + 3])
+                    KD_HIP(hipMemcpyAsync(sb, dd[i], hc[8 * i + 3] * 8, hipMemcpyDeviceToDevice, ctxs[i]->stream));
+                send[i] = (const u32*)sb;
+            }
         }
         KD_NCCL(R, R->groupStart());
         for (int i = 0; i < g; i++)
-            KD_NCCL(R, R->allGather(dd[i], dall[i], 2 * mx, ncclUint32, (ncclComm_t)ctxs[0]->group_comms[i], ctxs[i]->stream));
+            KD_NCCL(R, R->allGather(send[i], dall[i], 2 * mx, ncclUint32, (ncclComm_t)ctxs[0]->group_comms[i], ctxs[i]->stream));
         KD_NCCL(R, R->groupEnd());
     }
     // ---- result from GPU 0: the shards in bucket order = key order ----

@@ -86,7 +86,9 @@ struct kd_ctx {
     hipEvent_t ev_counts = nullptr, ev_gathered = nullptr;
     uint64_t* h_counts_pin = nullptr;
     int h_counts_ranks = 0;
+    uint64_t gather_send_cap = 0;  // records the last _begin's d_delta holds (base.n + target.n + 1)
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
+    uint32_t rs_epoch = 0;  // kd_sort: epoch of the last pass's look-back words (kd_sort.hip)
 };
 
 namespace kd {
@@ -133,8 +135,10 @@ int check_side(const kd_side* s, const char* which);
 void comm_release(kd_ctx* ctx);
 
 // ---- classify2 (device form), kd_classify.hip ----
+// ordA / ordB (both or neither): the sides' OIDs and filename offsets are in another order, row
+// ord[i] belongs to sorted entry i (kd_diff2_device_perm)
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
-                 u32* d_upd, u64* d_counts, u32* d_err);
+                 u32* d_upd, u64* d_counts, u32* d_err, const u32* ordA = nullptr, const u32* ordB = nullptr);
 #ifndef KD_C2_NT
 #define KD_C2_NT 256
 #endif

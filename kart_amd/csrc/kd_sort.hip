@@ -1,30 +1,84 @@
-// kd_sort.hip — packing a side on the GPU: join keys sorted with an LDS-ranked LSD radix sort,
-// OIDs permuted by the sort order, duplicate keys detected.
+// kd_sort.hip — packing a side on the GPU: join keys sorted by an LDS-staged onesweep LSD radix
+// sort, OIDs permuted by the sort order, duplicate keys detected.
 //
 // Replaces the sort the host packer did after decoding the leaf paths (Dataset3's leaves arrive in
 // git path order — kart/dataset3.py:225-231 walks the trees — which is not join-key order: base64
 // tree names sort by ASCII, not by bucket value, and b64(msgpack(pk)) filenames do not sort by pk).
 //
-// Only the bits that differ between keys are sorted: int keys of pks below 2^30 vary in 30 of 64
-// bits (bucket24 | pk % 64), so four 8-bit passes instead of eight.  Per pass:
-//   k_rs_hist    one wave per 4096-key tile: digit counts of the tile (ballot ranking, LDS counters)
-//   k_rs_scan    one block per digit: exclusive scan of that digit's tile counts (digit-major)
-//   k_rs_scatter one wave per tile: the same ranking again (stable: rounds in item order, lanes in
-//                lane order), digit base + earlier tiles' count + rank -> destination of (key, index)
-// A digit's rank inside a 64-item round comes from 8 ballots (lanes whose digit bits all agree),
-// its running count from one LDS counter per digit updated by the lowest lane of each digit group.
+// 1. k_rs_bits     OR of key ^ key[0]: the bits that vary.  One 8-B read-back sizes the sort.
+//    Only those bits are sorted: they are gathered ("compacted", an order-preserving bit gather of at
+//    most 4 runs of bits) into a 32-bit key when they fit (int keys of pks below 2^30 vary in
+//    6 + 24 bits) and expanded back to the full 64-bit key on the last pass's store.
+// 2. k_sort_hist   one read of the keys: the digit histograms of EVERY pass (digits of up to 9 bits), run-
+//                  length counted per thread over 16 consecutive keys, LDS atomics, one global add
+//                  per (block, pass, digit).  k_sort_scan turns them into each digit's global base.
+// 3. k_sort_pass   one launch per digit pass, one tile of NT*IPT keys per workgroup, tiles taken in
+//                  order from an atomic counter (every earlier tile is resident or done):
+//      a. load the tile (wave-striped, so (wave, item, lane) order is input order: stable);
+//      b. early counts: the tile's digit histogram (LDS atomics) is published at once, so the
+//         tiles after it rarely wait for it in their look-back;
+//      c. rank: per wave and item, the lanes holding the same digit (one ballot per digit bit), a
+//         per-(digit, wave) LDS counter bumped by the group's lowest lane; one block scan over the
+//         [digit][wave] counters gives every (digit, wave) its start inside the tile;
+//      d. reorder the tile in LDS by digit, look back over earlier tiles' published counts for
+//         this tile's global offset per digit (decoupled look-back, a window of earlier tiles per
+//         round trip, epoch-tagged 8-B agent-scope words: no per-pass clearing);
+//      e. scatter from LDS in digit order: a digit's run of the tile is written to consecutive
+//         addresses (coalesced), the last pass stores full keys + the original index.
+// 4. k_gather_oid  OIDs permuted by the order (sorted k reads row order[k]; git-order leaves of one
+//                  64-entry leaf tree stay within ~1.3 KB, so the reads are near-coalesced).
 #include "kd_internal.h"
 
 namespace kd {
 
-constexpr int RS_TILE = 4096;          // keys per tile (one wave, 64 rounds of 64)
-constexpr int RS_ROUNDS = RS_TILE / 64;
+#ifndef KD_RS_RB
+#define KD_RS_RB 9
+#endif
+constexpr int RS_RB = KD_RS_RB;      // digit bits per pass (at most)
+constexpr int RS_RD = 1 << RS_RB;    // digits
+constexpr int RS_MAXRUNS = 4;        // compaction runs (more are merged, taking the constant gap bits)
+constexpr int RS_HIST_NT = 256, RS_HIST_IPT = 16;
+#ifndef KD_RS_NT
+#define KD_RS_NT 512
+#endif
+#ifndef KD_RS_IPT32
+#define KD_RS_IPT32 16
+#endif
+#ifndef KD_RS_IPT64
+#define KD_RS_IPT64 8
+#endif
+constexpr int RS_NT = KD_RS_NT;
 
-// lanes of the wave holding the same 8-bit digit as this lane
+// which bits vary, and how they are gathered into the compact key
+struct SortPlan {
+    u64 kconst;                 // key bits outside the runs (equal in every key)
+    u64 mask[RS_MAXRUNS];       // run r: (key >> lo[r]) & mask[r] -> compact bits at pos[r]
+    u32 lo[RS_MAXRUNS], pos[RS_MAXRUNS];
+    u32 nruns, bits;            // runs, compact key width
+};
+
+template <typename CK>
+__device__ __forceinline__ CK rs_compact(u64 k, const SortPlan& p) {
+    u64 c = 0;
+#pragma unroll
+    for (int r = 0; r < RS_MAXRUNS; r++)
+        if (r < (int)p.nruns) c |= ((k >> p.lo[r]) & p.mask[r]) << p.pos[r];
+    return (CK)c;
+}
+
+__device__ __forceinline__ u64 rs_expand(u64 c, const SortPlan& p) {
+    u64 k = p.kconst;
+#pragma unroll
+    for (int r = 0; r < RS_MAXRUNS; r++)
+        if (r < (int)p.nruns) k |= ((c >> p.pos[r]) & p.mask[r]) << p.lo[r];
+    return k;
+}
+
+// lanes of the wave holding the same digit as this lane
 __device__ __forceinline__ u64 digit_peers(u32 d, bool valid) {
     u64 m = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
+    for (int b = 0; b < RS_RB; b++) {
         const u64 v = __ballot(valid && ((d >> b) & 1));
         m &= ((d >> b) & 1) ? v : ~v;
     }
@@ -35,120 +89,293 @@ __device__ __forceinline__ u32 lanes_below(u64 m) {
     return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0));
 }
 
-// varying bits of the keys: OR of (key ^ key[0]) over all keys
+// varying bits of the keys: OR of (key ^ key[0]) over all keys (16-B loads, four in flight per lane)
 __global__ __launch_bounds__(256) void k_rs_bits(const u64* __restrict__ key, u64 n, u64* __restrict__ out) {
     const u64 k0 = key[0];
     u64 x = 0;
-    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) x |= key[i] ^ k0;
+    const u64 tid = (u64)blockIdx.x * 256 + threadIdx.x, nt = (u64)gridDim.x * 256;
+    u64 done = 0;
+    if (((uintptr_t)key & 15) == 0) {
+        const u64x2* p = (const u64x2*)key;
+        const u64 n2 = n / 2;
+        u64 i = tid;
+        for (; i + 3 * nt < n2; i += 4 * nt) {
+            const u64x2 a = p[i], b = p[i + nt], c = p[i + 2 * nt], d = p[i + 3 * nt];
+            x |= (a.x ^ k0) | (a.y ^ k0) | (b.x ^ k0) | (b.y ^ k0) | (c.x ^ k0) | (c.y ^ k0) | (d.x ^ k0) | (d.y ^ k0);
+        }
+        for (; i < n2; i += nt) x |= (p[i].x ^ k0) | (p[i].y ^ k0);
+        done = 2 * n2;
+    }
+    for (u64 i = done + tid; i < n; i += nt) x |= key[i] ^ k0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
     if ((threadIdx.x & 63) == 0 && x) atomicOr((unsigned long long*)out, (unsigned long long)x);
 }
 
-__global__ __launch_bounds__(64) void k_rs_hist(const u64* __restrict__ key, u64 n, int shift, u32 ntiles,
-                                               u32* __restrict__ hist) {
-    __shared__ u32 s_cnt[256];
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 256; i += 64) s_cnt[i] = 0;
-    __builtin_amdgcn_wave_barrier();
-    const u64 t0 = (u64)blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ROUNDS; r++) {
-        const u64 i = t0 + (u64)r * 64 + lane;
-        const bool v = i < n;
-        const u32 d = v ? (u32)(key[i] >> shift) & 0xFF : 0;
-        const u64 m = digit_peers(d, v);
-        if (v && lanes_below(m) == 0) s_cnt[d] += (u32)__popcll(m);  // one lane per digit group
-        __builtin_amdgcn_wave_barrier();
+// ---- all passes' digit histograms in one read of the keys ----
+template <typename CK>
+__global__ __launch_bounds__(RS_HIST_NT) void k_sort_hist(const u64* __restrict__ key, u64 n, int npass, int width,
+                                                           SortPlan plan, u32* __restrict__ hist) {
+    __shared__ u32 s_h[8 * RS_RD];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT) s_h[i] = 0;
+    __syncthreads();
+    const u32 dmask = (1u << width) - 1;
+    const bool al16 = ((uintptr_t)key & 15) == 0;
+    constexpr u64 CH = (u64)RS_HIST_NT * RS_HIST_IPT;
+    for (u64 base = (u64)blockIdx.x * CH; base < n; base += (u64)gridDim.x * CH) {
+        const u64 i0 = base + (u64)tid * RS_HIST_IPT;  // 16 consecutive keys per thread: runs of equal digits
+        const int cnt = i0 < n ? (int)min<u64>(RS_HIST_IPT, n - i0) : 0;
+        CK c[RS_HIST_IPT];
+        if (cnt == RS_HIST_IPT && al16) {
+            const u64x2* p = (const u64x2*)(key + i0);
+#pragma unroll
+            for (int j = 0; j < RS_HIST_IPT / 2; j++) {
+                const u64x2 v = p[j];
+                c[2 * j] = rs_compact<CK>(v.x, plan);
+                c[2 * j + 1] = rs_compact<CK>(v.y, plan);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < RS_HIST_IPT; j++) c[j] = j < cnt ? rs_compact<CK>(key[i0 + j], plan) : 0;
+        }
+        for (int p = 0; p < npass; p++) {
+            const int sh = p * width;
+            u32 cur = (u32)(c[0] >> sh) & dmask, run = 0;
+#pragma unroll
+            for (int j = 0; j < RS_HIST_IPT; j++) {
+                if (j < cnt) {
+                    const u32 d = (u32)(c[j] >> sh) & dmask;
+                    if (d != cur) {
+                        atomicAdd(&s_h[p * RS_RD + cur], run);
+                        cur = d;
+                        run = 0;
+                    }
+                    run++;
+                }
+            }
+            if (run) atomicAdd(&s_h[p * RS_RD + cur], run);
+        }
     }
-    for (int i = lane; i < 256; i += 64) hist[(u64)i * ntiles + blockIdx.x] = s_cnt[i];  // digit-major
+    __syncthreads();
+    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
-// one block per digit: exclusive scan of hist[d][0..ntiles) in place, the digit's total to tot[d]
-__global__ __launch_bounds__(256) void k_rs_scan(u32* __restrict__ hist, u32 ntiles, u32* __restrict__ tot) {
-    __shared__ u32 s_w[4];
-    u32* h = hist + (u64)blockIdx.x * ntiles;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    u32 carry = 0;
-    for (u32 base = 0; base < ntiles; base += 256) {
-        const u32 i = base + tid;
-        const u32 x = i < ntiles ? h[i] : 0;
-        u32 s = x;  // inclusive wave scan
+// one block: hist[p][d] -> exclusive scan over d (each digit's first output position in pass p)
+__global__ __launch_bounds__(RS_RD) void k_sort_scan(const u32* __restrict__ hist, int npass, u32* __restrict__ gbase) {
+    __shared__ u32 s_w[RS_RD / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int p = 0; p < npass; p++) {
+        const u32 x = hist[p * RS_RD + tid];
+        u32 s = x;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const u32 y = __shfl_up(s, o, 64);
             if (lane >= o) s += y;
         }
-        if (lane == 63) s_w[wid] = s;
+        if (lane == 63) s_w[wv] = s;
         __syncthreads();
-        u32 wp = 0, all = 0;
+        u32 pre = 0;
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            if (w < wid) wp += s_w[w];
-            all += s_w[w];
-        }
-        if (i < ntiles) h[i] = carry + wp + s - x;
-        carry += all;
+        for (int w = 0; w < RS_RD / 64; w++)
+            if (w < wv) pre += s_w[w];
+        gbase[p * RS_RD + tid] = pre + s - x;
         __syncthreads();
     }
-    if (tid == 0) tot[blockIdx.x] = carry;
 }
 
-// stable scatter of one pass; pass 0 takes the item index as its value
-__global__ __launch_bounds__(64) void k_rs_scatter(const u64* __restrict__ key, const u32* __restrict__ val, u64 n,
-                                                  int shift, u32 ntiles, const u32* __restrict__ hist,
-                                                  const u32* __restrict__ tot, u64* __restrict__ okey,
-                                                  u32* __restrict__ oval) {
-    __shared__ u32 s_off[256];
-    const int lane = threadIdx.x;
-    // digit bases: exclusive scan of the 256 totals (4 per lane) + this tile's earlier-tile counts
-    {
-        u32 t[4], s = 0;
+// look-back words: flag << 62 | epoch << 40 | count; a word of another epoch is "not yet"
+constexpr u64 RS_AGG = 1ull << 62, RS_INC = 2ull << 62, RS_CNT = (1ull << 40) - 1;
+constexpr u32 RS_EPOCHS = 1u << 22;
+#ifndef KD_RS_LBW
+#define KD_RS_LBW 4
+#endif
+constexpr int RS_LBW = KD_RS_LBW;  // look-back words per round trip
+__device__ __forceinline__ void rs_store(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ u64 rs_load(const u64* p) {
+    return __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One digit pass.  FIRST: input = the caller's 64-bit keys (compacted on load), value = the input
+// index.  LAST: output = full 64-bit keys (expanded) + the values (original indices).
+template <typename CK, int NT, int IPT, bool FIRST, bool LAST>
+__global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, const u32* __restrict__ vin,
+                                                  void* __restrict__ kout, u32* __restrict__ vout, u64 n, int shift,
+                                                  u32 dmask, const u32* __restrict__ gbase, u64* __restrict__ status, u32 epoch,
+                                                  u32* __restrict__ tile_ctr, SortPlan plan) {
+    constexpr int NW = NT / 64, TILE = NT * IPT, CPT = RS_RD * NW / NT;
+    static_assert(NT >= RS_RD && (RS_RD * NW) % NT == 0, "tile shape");
+    __shared__ u16 s_cnt[RS_RD * NW];  // [digit][wave]: item counts, then (after the scan) starts (<= TILE)
+    __shared__ u32 s_hist[RS_RD];      // the tile's digit counts (early: published before the ranking)
+    __shared__ CK s_key[TILE];
+    __shared__ u32 s_val[TILE];
+    __shared__ u32 s_goff[RS_RD];      // global position of the digit's tile-local position 0
+    __shared__ u32 s_wsum[NW];
+    __shared__ u32 s_tile;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    for (int i = tid; i < RS_RD * NW; i += NT) s_cnt[i] = 0;
+    for (int i = tid; i < RS_RD; i += NT) s_hist[i] = 0;
+    __syncthreads();
+    const u32 tile = s_tile;
+    const u64 t0 = (u64)tile * TILE;
+    const u32 valid = (u32)min<u64>((u64)TILE, n - t0);
+    const u64 wbase = t0 + (u64)wv * 64 * IPT + lane;
+    // ---- a. load ----
+    CK c[IPT];
+    u32 v[IPT], rk[IPT];
 #pragma unroll
-        for (int j = 0; j < 4; j++) { t[j] = tot[4 * lane + j]; s += t[j]; }
+    for (int i = 0; i < IPT; i++) {
+        const u64 idx = wbase + (u64)i * 64;
+        const bool ok = idx < n;
+        if (FIRST) {
+            c[i] = ok ? rs_compact<CK>(((const u64*)kin)[idx], plan) : (CK)0;
+            v[i] = (u32)idx;
+        } else {
+            c[i] = ok ? ((const CK*)kin)[idx] : (CK)0;
+            v[i] = ok ? vin[idx] : 0;
+        }
+    }
+    // ---- b. early counts: the tile's digit histogram, published before the ranking so that later
+    //         tiles' look-backs find this tile's aggregate as early as possible ----
+#pragma unroll
+    for (int i = 0; i < IPT; i++)
+        if (wbase + (u64)i * 64 < n) atomicAdd(&s_hist[(u32)(c[i] >> shift) & dmask], 1u);
+    __syncthreads();
+    u32 dcnt = 0;
+    u64* st = status + (u64)tile * RS_RD + tid;
+    if (tid < RS_RD) {
+        dcnt = s_hist[tid];
+        rs_store(st, (tile == 0 ? RS_INC : RS_AGG) | ((u64)epoch << 40) | dcnt);
+    }
+    // ---- c. rank within the wave, then a block scan of the [digit][wave] counters ----
+#pragma unroll
+    for (int i = 0; i < IPT; i++) {
+        const bool ok = wbase + (u64)i * 64 < n;
+        const u32 d = (u32)(c[i] >> shift) & dmask;
+        const u64 m = digit_peers(d, ok);
+        const u32 below = lanes_below(m);
+        u16* ctr = &s_cnt[d * NW + wv];
+        const u32 pre = *ctr;  // read by every lane of the group before its lowest lane moves it
+        __builtin_amdgcn_wave_barrier();
+        if (ok && below == 0) *ctr = (u16)(pre + (u32)__popcll(m));
+        __builtin_amdgcn_wave_barrier();
+        rk[i] = pre + below;
+    }
+    __syncthreads();
+    {
+        u32 x[CPT], s = 0;
+#pragma unroll
+        for (int j = 0; j < CPT; j++) {
+            x[j] = s_cnt[tid * CPT + j];
+            s += x[j];
+        }
         u32 inc = s;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const u32 y = __shfl_up(inc, o, 64);
             if (lane >= o) inc += y;
         }
+        if (lane == 63) s_wsum[wv] = inc;
+        __syncthreads();
         u32 ex = inc - s;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const u32 d = 4 * lane + j;
-            s_off[d] = ex + hist[(u64)d * ntiles + blockIdx.x];
-            ex += t[j];
+        for (int w = 0; w < NW; w++)
+            if (w < wv) ex += s_wsum[w];
+#pragma unroll
+        for (int j = 0; j < CPT; j++) {
+            s_cnt[tid * CPT + j] = (u16)ex;
+            ex += x[j];
         }
     }
-    __builtin_amdgcn_wave_barrier();
-    const u64 t0 = (u64)blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ROUNDS; r++) {
-        const u64 i = t0 + (u64)r * 64 + lane;
-        const bool v = i < n;
-        const u64 k = v ? key[i] : 0;
-        const u32 x = v ? (val ? val[i] : (u32)i) : 0;
-        const u32 d = (u32)(k >> shift) & 0xFF;
-        const u64 m = digit_peers(d, v);
-        const u32 below = lanes_below(m);
-        const u32 base = s_off[d];  // read by every lane before the leader moves it
-        __builtin_amdgcn_wave_barrier();
-        if (v && below == 0) s_off[d] = base + (u32)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
-        if (v) {
-            okey[base + below] = k;
-            oval[base + below] = x;
+    __syncthreads();
+    // ---- d. reorder in LDS, look back ----
+    const u32 dstart = tid < RS_RD ? (u32)s_cnt[tid * NW] : 0;
+#pragma unroll
+    for (int i = 0; i < IPT; i++) {
+        if (wbase + (u64)i * 64 < n) {
+            const u32 d = (u32)(c[i] >> shift) & dmask;
+            const u32 p = s_cnt[d * NW + wv] + rk[i];
+            s_key[p] = c[i];
+            s_val[p] = v[i];
         }
+    }
+    if (tid < RS_RD) {
+        u64 ex = 0;
+#ifdef KD_RS_PROBE_NOLB
+        if (false) {  // probe: no look-back wait (wrong offsets, in bounds: times the rest)
+#else
+        if (tile > 0) {
+#endif
+            // RS_LBW earlier tiles' words per round trip (t-1, t-2, ...): their counts add up to the
+            // first inclusive prefix; a word not yet published stops the round, and the next round
+            // starts at it.  Tile 0 always publishes an inclusive prefix, so the walk ends there.
+            i64 t = (i64)tile - 1;
+            while (true) {
+                u64 w[RS_LBW];
+#pragma unroll
+                for (int k = 0; k < RS_LBW; k++) w[k] = t - k >= 0 ? rs_load(status + (u64)(t - k) * RS_RD + tid) : RS_INC;
+                int used = 0;
+                bool done = false;
+#pragma unroll
+                for (int k = 0; k < RS_LBW; k++) {
+                    if (done || used < k) continue;  // stopped earlier in this round
+                    const u64 x = w[k];
+                    const bool ready = (x >> 62) != 0 && ((u32)((x >> 40) & (RS_EPOCHS - 1)) == epoch || t - k < 0);
+                    if (!ready) continue;
+                    ex += x & RS_CNT;
+                    used = k + 1;
+                    done = (x >> 62) == 2;
+                }
+                if (done) break;
+                t -= used;
+                if (used < RS_LBW) __builtin_amdgcn_s_sleep(1);  // a predecessor has not published yet
+            }
+            rs_store(st, RS_INC | ((u64)epoch << 40) | (ex + dcnt));
+        }
+        s_goff[tid] = gbase[tid] + (u32)ex - dstart;
+    }
+    __syncthreads();
+    // ---- e. scatter in digit order ----
+    for (u32 j = tid; j < valid; j += NT) {
+        const CK k = s_key[j];
+        const u32 x = s_val[j];
+        const u32 dst = s_goff[(u32)(k >> shift) & dmask] + j;
+        if (LAST) ((u64*)kout)[dst] = rs_expand((u64)k, plan);
+        else ((CK*)kout)[dst] = k;
+        vout[dst] = x;
     }
 }
 
-// rows of 20 bytes gathered by the sort order: out[k] = in[order[k]]
+// rows of 20 bytes gathered by the sort order: out[k] = in[order[k]].  One wave per 64 rows: each
+// lane loads its row (5 dwords; rows of one git leaf tree lie within ~1.3 KB), the wave's 1280 B
+// go through LDS and leave as 80 coalesced 16-B stores.
 __global__ __launch_bounds__(256) void k_gather_oid(const u8* __restrict__ in, const u32* __restrict__ order, u64 n,
                                                     u8* __restrict__ out) {
     typedef const __attribute__((address_space(1))) u32* gp32;
-    for (u64 k = (u64)blockIdx.x * 256 + threadIdx.x; k < n; k += (u64)gridDim.x * 256) {
-        const gp32 s = (gp32)(in + 20ull * order[k]);  // 20-B rows: 4-B aligned
-        u32* d = (u32*)(out + 20ull * k);
-        const u32 a = s[0], b = s[1], c = s[2], e = s[3], f = s[4];
-        d[0] = a; d[1] = b; d[2] = c; d[3] = e; d[4] = f;
+    __shared__ __attribute__((aligned(16))) u32 s_rows[4][64 * 5];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32* R = s_rows[wv];
+    const bool al16 = ((uintptr_t)out & 15) == 0;
+    for (u64 r0 = ((u64)blockIdx.x * 4 + wv) * 64; r0 < n; r0 += (u64)gridDim.x * 256) {
+        const u64 k = r0 + lane;
+        const u32 m = (u32)min<u64>(64, n - r0);
+        if (k < n) {
+            const gp32 s = (gp32)(in + 20ull * order[k]);  // 20-B rows: 4-B aligned
+            const u32 a = s[0], b = s[1], c = s[2], e = s[3], f = s[4];
+            R[5 * lane] = a; R[5 * lane + 1] = b; R[5 * lane + 2] = c; R[5 * lane + 3] = e; R[5 * lane + 4] = f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        u32* d = (u32*)(out + 20ull * r0);
+        if (m == 64 && al16) {
+            const u32x4* S = (const u32x4*)R;
+            ((u32x4*)d)[lane] = S[lane];
+            if (lane < 16) ((u32x4*)d)[64 + lane] = S[64 + lane];
+        } else {
+            for (u32 j = lane; j < 5 * m; j += 64) d[j] = R[j];
+        }
+        __builtin_amdgcn_wave_barrier();  // the next chunk's LDS writes after this chunk's reads
     }
 }
 
@@ -163,9 +390,220 @@ __global__ __launch_bounds__(256) void k_check_sorted(const u64* __restrict__ ke
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(dup, 1u);
 }
 
+// ---------------------------------------------------------------------------------------------
+// host side
+// the varying-bit mask -> compaction runs (at most RS_MAXRUNS: the narrowest gaps are absorbed)
+static SortPlan make_plan(u64 vary, u64 k0) {
+    SortPlan p{};
+    u32 lo[32], hi[32], nr = 0;  // runs [lo, hi)
+    for (u32 b = 0; b < 64;) {
+        if (!((vary >> b) & 1)) { b++; continue; }
+        u32 e = b;
+        while (e < 64 && ((vary >> e) & 1)) e++;
+        lo[nr] = b;
+        hi[nr] = e;
+        nr++;
+        b = e;
+    }
+    while (nr > (u32)RS_MAXRUNS) {  // merge the pair of neighbouring runs with the narrowest gap
+        u32 best = 0;
+        for (u32 r = 1; r + 1 < nr; r++)
+            if (lo[r + 1] - hi[r] < lo[best + 1] - hi[best]) best = r;
+        hi[best] = hi[best + 1];
+        for (u32 r = best + 1; r + 1 < nr; r++) { lo[r] = lo[r + 1]; hi[r] = hi[r + 1]; }
+        nr--;
+    }
+    u64 used = 0;
+    u32 pos = 0;
+    for (u32 r = 0; r < nr; r++) {
+        const u32 len = hi[r] - lo[r];
+        const u64 m = len >= 64 ? ~0ull : ((1ull << len) - 1);
+        p.mask[r] = m;
+        p.lo[r] = lo[r];
+        p.pos[r] = pos;
+        used |= m << lo[r];
+        pos += len;
+    }
+    p.nruns = nr;
+    p.bits = pos;
+    p.kconst = k0 & ~used;
+    return p;
+}
+
+struct SortState {
+    u64* status = nullptr;
+    u32* tctr = nullptr;
+    u32* hist = nullptr;
+    u32* gbase = nullptr;
+};
+
+static int rs_epoch(kd_ctx* ctx, u64 status_bytes, SortState& S, u32* ep) {
+    const size_t before = ctx->bufs["rs.status"].bytes;
+    void* p;
+    int rc = ensure(ctx, "rs.status", status_bytes, &p);
+    if (rc) return rc;
+    S.status = (u64*)p;
+    const size_t after = ctx->bufs["rs.status"].bytes;
+    if (after != before || ctx->rs_epoch + 1 >= RS_EPOCHS) {  // fresh memory, or the epochs wrapped
+        KD_HIP(hipMemsetAsync(p, 0, after, ctx->stream));
+        ctx->rs_epoch = 0;
+    }
+    *ep = ++ctx->rs_epoch;
+    return KD_OK;
+}
+
+template <typename CK, bool FIRST, bool LAST>
+static int rs_launch_pass(kd_ctx* ctx, SortState& S, const void* kin, const u32* vin, void* kout, u32* vout, u64 n,
+                          int pass, int shift, int width, const SortPlan& plan) {
+    constexpr int IPT = sizeof(CK) == 4 ? KD_RS_IPT32 : KD_RS_IPT64;
+    constexpr u64 TILE = (u64)RS_NT * IPT;
+    const u64 ntiles = (n + TILE - 1) / TILE;
+    u32 ep;
+    int rc = rs_epoch(ctx, ntiles * RS_RD * 8, S, &ep);
+    if (rc) return rc;
+    const u32* gb = S.gbase + pass * RS_RD;
+    u32* tc = S.tctr + pass;
+    u64* status = S.status;
+    return launch(ctx, "k_sort_pass", [&] {
+        hipLaunchKernelGGL((k_sort_pass<CK, RS_NT, IPT, FIRST, LAST>), dim3((unsigned)ntiles), dim3(RS_NT), 0,
+                           ctx->stream, kin, vin, kout, vout, n, shift,
+                           (u32)((1u << width) - 1), gb, status, ep, tc, plan);
+    });
+}
+
+template <typename CK>
+static int rs_passes(kd_ctx* ctx, SortState& S, const u64* key_in, u64* key_out, u32* order, u64 n, int npass,
+                     int width, const SortPlan& plan) {
+    int rc;
+    void *kb[2], *vb[2];
+    if (npass > 1) {
+        if ((rc = ensure(ctx, "rs.k0", n * sizeof(CK), &kb[0]))) return rc;
+        if ((rc = ensure(ctx, "rs.v0", n * 4, &vb[0]))) return rc;
+    }
+    if (npass > 2) {
+        if ((rc = ensure(ctx, "rs.k1", n * sizeof(CK), &kb[1]))) return rc;
+        if ((rc = ensure(ctx, "rs.v1", n * 4, &vb[1]))) return rc;
+    }
+    for (int p = 0; p < npass; p++) {
+        const bool first = p == 0, last = p == npass - 1;
+        const void* kin = first ? (const void*)key_in : kb[(p - 1) & 1];
+        const u32* vin = first ? nullptr : (const u32*)vb[(p - 1) & 1];
+        void* kout = last ? (void*)key_out : kb[p & 1];
+        u32* vout = last ? order : (u32*)vb[p & 1];
+        const int sh = p * width;
+        if (first && last) rc = rs_launch_pass<CK, true, true>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
+        else if (first) rc = rs_launch_pass<CK, true, false>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
+        else if (last) rc = rs_launch_pass<CK, false, true>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
+        else rc = rs_launch_pass<CK, false, false>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
+        if (rc) return rc;
+    }
+    return KD_OK;
+}
+
+// keys: key_in -> key_out (sorted), order[k] = input index of sorted entry k.  key_out may alias
+// key_in only when the sort takes two passes or more (the caller checks *passes_out first).
+static int sort_keys(kd_ctx* ctx, const u64* key_in, u64* key_out, u32* order, u64 n, bool inplace) {
+    int rc;
+    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 8));
+    void* bits;
+    if ((rc = ensure(ctx, "rs.bits", 16, &bits))) return rc;
+    // ---- which bits vary (one 8-byte read-back decides the passes) ----
+    KD_HIP(hipMemsetAsync(bits, 0, 16, ctx->stream));
+    rc = launch(ctx, "k_rs_bits", [&] {
+        hipLaunchKernelGGL(k_rs_bits, dim3(gs), dim3(256), 0, ctx->stream, key_in, n, (u64*)bits);
+    });
+    if (rc) return rc;
+    u64 hv[2] = {0, 0};
+    KD_HIP(hipMemcpyAsync(hv, bits, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KD_HIP(hipMemcpyAsync(hv + 1, key_in, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KD_HIP(hipStreamSynchronize(ctx->stream));
+    const u64 vary = hv[0];
+    if (vary == 0) {  // every key equal (n == 1, or duplicates): identity order
+        if (key_out != key_in) KD_HIP(hipMemcpyAsync(key_out, key_in, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        return launch(ctx, "k_iota", [&] {
+            hipLaunchKernelGGL(k_iota_u32, dim3(gs), dim3(256), 0, ctx->stream, order, n);
+        });
+    }
+    const SortPlan plan = make_plan(vary, hv[1]);
+    const int npass = (int)((plan.bits + RS_RB - 1) / RS_RB);
+    const int width = (int)((plan.bits + npass - 1) / npass);  // spread the bits evenly over the passes
+    if (inplace && npass == 1) {  // the single pass would read and write the caller's array
+        void* tmp;
+        if ((rc = ensure(ctx, "rs.kin", n * 8, &tmp))) return rc;
+        KD_HIP(hipMemcpyAsync(tmp, key_in, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        key_in = (const u64*)tmp;
+    }
+    SortState S;
+    void *tc, *hist, *gb;
+    if ((rc = ensure(ctx, "rs.tctr", 64, &tc))) return rc;
+    if ((rc = ensure(ctx, "rs.hist", 8 * RS_RD * 4, &hist))) return rc;
+    if ((rc = ensure(ctx, "rs.gbase", 8 * RS_RD * 4, &gb))) return rc;
+    S.tctr = (u32*)tc;
+    S.hist = (u32*)hist;
+    S.gbase = (u32*)gb;
+    KD_HIP(hipMemsetAsync(tc, 0, 64, ctx->stream));
+    KD_HIP(hipMemsetAsync(hist, 0, (size_t)npass * RS_RD * 4, ctx->stream));
+    const bool narrow = plan.bits <= 32;
+    constexpr u64 HCH = (u64)RS_HIST_NT * RS_HIST_IPT;
+    const unsigned hg = (unsigned)std::max<u64>(1, std::min<u64>((n + HCH - 1) / HCH, (u64)ctx->n_cu * 2));
+    rc = launch(ctx, "k_sort_hist", [&] {
+        if (narrow)
+            hipLaunchKernelGGL(k_sort_hist<u32>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, key_in, n, npass, width, plan,
+                               (u32*)hist);
+        else
+            hipLaunchKernelGGL(k_sort_hist<u64>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, key_in, n, npass, width, plan,
+                               (u32*)hist);
+    });
+    if (rc) return rc;
+    rc = launch(ctx, "k_sort_scan", [&] {
+        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(RS_RD), 0, ctx->stream, (const u32*)hist, npass, (u32*)gb);
+    });
+    if (rc) return rc;
+    return narrow ? rs_passes<u32>(ctx, S, key_in, key_out, order, n, npass, width, plan)
+                  : rs_passes<u64>(ctx, S, key_in, key_out, order, n, npass, width, plan);
+}
+
+static int gather_and_check(kd_ctx* ctx, const u8* oid_in, u8* oid_out, const u32* order, const u64* key_sorted, u64 n,
+                            u32* d_dup) {
+    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 8));
+    int rc;
+    if (oid_in) {
+        if ((rc = launch(ctx, "k_gather_oid", [&] {
+                 hipLaunchKernelGGL(k_gather_oid, dim3(gs), dim3(256), 0, ctx->stream, oid_in, order, n, oid_out);
+             })))
+            return rc;
+    }
+    if (d_dup) {
+        KD_HIP(hipMemsetAsync(d_dup, 0, 4, ctx->stream));
+        if ((rc = launch(ctx, "k_check_sorted", [&] {
+                 hipLaunchKernelGGL(k_check_sorted, dim3(gs), dim3(256), 0, ctx->stream, key_sorted, n, d_dup);
+             })))
+            return rc;
+    }
+    return KD_OK;
+}
+
 }  // namespace kd
 
 using namespace kd;
+
+extern "C" int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oid_in, uint64_t* d_key_out,
+                                 uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup) {
+    KD_CHECK(ctx && (n == 0 || (d_key_in && d_key_out && d_order)), "kd_sort_side_into: NULL");
+    KD_CHECK(!d_oid_in == !d_oid_out, "kd_sort_side_into: OID input and output go together");
+    KD_CHECK(n < 0xFFFFFFFFull, "kd_sort_side_into: side too large for uint32 indices");
+    KD_CHECK(n == 0 || ((const void*)d_key_in != (const void*)d_key_out &&
+                        (!d_oid_in || (const void*)d_oid_in != (const void*)d_oid_out)),
+             "kd_sort_side_into: outputs must not alias the inputs (kd_sort_side sorts in place)");
+    KD_HIP(hipSetDevice(ctx->device));
+    if (n == 0) {
+        if (d_dup) KD_HIP(hipMemsetAsync(d_dup, 0, 4, ctx->stream));
+        return KD_OK;
+    }
+    int rc = sort_keys(ctx, d_key_in, d_key_out, d_order, n, false);
+    if (rc) return rc;
+    return gather_and_check(ctx, d_oid_in, d_oid_out, d_order, d_key_out, n, d_dup);
+}
 
 extern "C" int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32_t* d_order, uint64_t n,
                             uint32_t* h_dup) {
@@ -174,79 +612,13 @@ extern "C" int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32
     KD_HIP(hipSetDevice(ctx->device));
     if (h_dup) *h_dup = 0;
     if (n == 0) return KD_OK;
-    int rc;
-    const u32 ntiles = (u32)((n + RS_TILE - 1) / RS_TILE);
-    void *bits, *hist, *tot, *k2, *v2, *dup;
-    if ((rc = ensure(ctx, "rs.bits", 16, &bits))) return rc;
-    if ((rc = ensure(ctx, "rs.hist", (u64)ntiles * 256 * 4, &hist))) return rc;
-    if ((rc = ensure(ctx, "rs.tot", 256 * 4, &tot))) return rc;
-    if ((rc = ensure(ctx, "rs.k2", n * 8, &k2))) return rc;
-    if ((rc = ensure(ctx, "rs.v2", n * 4, &v2))) return rc;
-    if ((rc = ensure(ctx, "rs.dup", 16, &dup))) return rc;
-    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 8));
-    // ---- which bits vary (one 8-byte read-back decides the pass count) ----
-    KD_HIP(hipMemsetAsync(bits, 0, 16, ctx->stream));
-    rc = launch(ctx, "k_rs_bits", [&] {
-        hipLaunchKernelGGL(k_rs_bits, dim3(gs), dim3(256), 0, ctx->stream, (const u64*)d_key, n, (u64*)bits);
-    });
+    int rc = sort_keys(ctx, d_key, d_key, d_order, n, true);
     if (rc) return rc;
-    u64 vary = 0;
-    KD_HIP(hipMemcpyAsync(&vary, bits, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KD_HIP(hipStreamSynchronize(ctx->stream));
-    int lo = 0, hi = -1;
-    if (vary) { lo = __builtin_ctzll(vary); hi = 63 - __builtin_clzll(vary); }
-    const int passes = vary ? (hi - lo + 8) / 8 : 0;
-    // ---- LSD passes, ping-ponging between the caller's arrays and scratch ----
-    u64* ka = d_key;
-    u32* va = nullptr;  // pass 0: values are the item indices
-    u64* kb = (u64*)k2;
-    u32* vb = (u32*)v2;
-    for (int p = 0; p < passes; p++) {
-        const int shift = lo + 8 * p;
-        if ((rc = launch(ctx, "k_rs_hist", [&] {
-                 hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(64), 0, ctx->stream, (const u64*)ka, n, shift, ntiles,
-                                    (u32*)hist);
-             })))
-            return rc;
-        if ((rc = launch(ctx, "k_rs_scan", [&] {
-                 hipLaunchKernelGGL(k_rs_scan, dim3(256), dim3(256), 0, ctx->stream, (u32*)hist, ntiles, (u32*)tot);
-             })))
-            return rc;
-        if ((rc = launch(ctx, "k_rs_scatter", [&] {
-                 hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(64), 0, ctx->stream, (const u64*)ka, (const u32*)va,
-                                    n, shift, ntiles, (const u32*)hist, (const u32*)tot, kb, vb);
-             })))
-            return rc;
-        // next pass reads what this one wrote; the value array alternates between d_order and scratch
-        std::swap(ka, kb);
-        if (p == 0) { va = vb; vb = d_order; }
-        else std::swap(va, vb);
-    }
-    // ---- results into the caller's arrays ----
-    if (passes == 0) {  // all keys equal (n == 1, or duplicates): identity order
-        rc = launch(ctx, "k_iota", [&] {
-            hipLaunchKernelGGL(k_iota_u32, dim3(gs), dim3(256), 0, ctx->stream, d_order, n);
-        });
-        if (rc) return rc;
-    } else {
-        if (ka != d_key) KD_HIP(hipMemcpyAsync(d_key, ka, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        if (va != d_order) KD_HIP(hipMemcpyAsync(d_order, va, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
-    }
-    if (d_oid) {  // OIDs permuted by the order (through scratch, then back in place)
-        void* o2;
-        if ((rc = ensure(ctx, "rs.oid", n * 20, &o2))) return rc;
-        if ((rc = launch(ctx, "k_gather_oid", [&] {
-                 hipLaunchKernelGGL(k_gather_oid, dim3(gs), dim3(256), 0, ctx->stream, (const u8*)d_oid, (const u32*)d_order, n,
-                                    (u8*)o2);
-             })))
-            return rc;
-        KD_HIP(hipMemcpyAsync(d_oid, o2, n * 20, hipMemcpyDeviceToDevice, ctx->stream));
-    }
-    KD_HIP(hipMemsetAsync(dup, 0, 4, ctx->stream));
-    if ((rc = launch(ctx, "k_check_sorted", [&] {
-             hipLaunchKernelGGL(k_check_sorted, dim3(gs), dim3(256), 0, ctx->stream, (const u64*)d_key, n, (u32*)dup);
-         })))
-        return rc;
+    void *o2 = nullptr, *dup = nullptr;
+    if (d_oid && (rc = ensure(ctx, "rs.oid", n * 20, &o2))) return rc;
+    if (h_dup && (rc = ensure(ctx, "rs.dup", 16, &dup))) return rc;
+    if ((rc = gather_and_check(ctx, d_oid, (u8*)o2, d_order, d_key, n, (u32*)dup))) return rc;
+    if (d_oid) KD_HIP(hipMemcpyAsync(d_oid, o2, n * 20, hipMemcpyDeviceToDevice, ctx->stream));  // in place
     if (h_dup) {
         KD_HIP(hipMemcpyAsync(h_dup, dup, 4, hipMemcpyDeviceToHost, ctx->stream));
         KD_HIP(hipStreamSynchronize(ctx->stream));

@@ -94,6 +94,16 @@ class DevSide:
         return s
 
 
+class _WalkSide:
+    """a side's arrays in walk order (what DevSide uploads)"""
+
+    def __init__(self, key, oid):
+        self.key, self.oid = np.ascontiguousarray(key), np.ascontiguousarray(oid)
+        self.n = int(key.shape[0])
+        self.key_mode = N.KD_KEY_INT
+        self.name = None
+
+
 class DevBlobs:
     """A blob arena (uint8 data, uint64 off[n+1]) in HBM."""
 
@@ -125,11 +135,25 @@ class DiffPipeline:
     the library's RCCL communicator (``engine.comm_init`` first) — and field-diffs the shard's own
     updates."""
 
-    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, ordered=True, gather=None):
+    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, ordered=True, gather=None, walk=None,
+                 late=True):
         self.eng = engine
         self.flags = 0 if ordered else N.KD_DIFF_UNORDERED
         self.A = DevSide(engine, base)
         self.B = DevSide(engine, target)
+        # walk = (base_perm, target_perm): the sides are also held in walk (git tree) order —
+        # side.key[perm] — and every step first sorts them into the sorted side buffers above
+        # (kd_sort_side_into), as the drop-in does after packing the leaves it walked
+        # late (walk mode, single GPU): sort the keys only and let the join read the walk-order OIDs
+        # through the sort order (kd_diff2_device_perm) instead of permuting them (kd_sort_side_into's
+        # OID gather)
+        self.walk = None
+        self.late = bool(late) and gather is None
+        if walk is not None:
+            self.walk = []
+            for side, perm in zip((base, target), walk):
+                w = _WalkSide(side.key[perm], side.oid[perm])
+                self.walk.append((DevSide(engine, w), DevBuf(engine, 4 * max(side.n, 1)), side.n))
         self.OB = DevBlobs(engine, *base_blobs)
         self.NB = DevBlobs(engine, *target_blobs)
         self.maps = maps
@@ -144,6 +168,7 @@ class DiffPipeline:
         self._sa, self._sb = self.A.kd_side(), self.B.kd_side()
         self._ob, self._nb = self.OB.kd_blobs(), self.NB.kd_blobs()
         self._km = maps.kd_maps()
+        self._perm_sides = None
         self.gather = gather
         if gather is not None:
             self.world = engine.nranks
@@ -160,9 +185,44 @@ class DiffPipeline:
         self.all_cap = max(int(max_deltas_per_rank), 1) * self.world
         self.all_delta = DevBuf(self.eng, 8 * self.all_cap)
 
-    def step(self):
+    def sort_step(self):
+        """the two GPU side sorts (walk order -> the sorted side buffers), walk mode only"""
         L, ctx = self.eng.L, self.eng.ctx
-        if self.gather is None:
+        for (w, order, n), S in zip(self.walk, (self.A, self.B)):
+            if self.late:
+                N.check(L.kd_sort_side_into(ctx, w.key.ptr, None, S.key.ptr, None, order.ptr, n, None),
+                        "kd_sort_side_into")
+            else:
+                N.check(L.kd_sort_side_into(ctx, w.key.ptr, w.oid.ptr, S.key.ptr, S.oid.ptr, order.ptr, n, None),
+                        "kd_sort_side_into")
+
+    def orders(self):
+        """(walk mode) host copies of the two sort orders: walk index of sorted entry k"""
+        return [order.download(np.uint32, n) for _, order, n in self.walk]
+
+    def step(self):
+        """one pass of the hot path: (walk mode) both side sorts, then the diff + field diff"""
+        if self.walk is not None:
+            self.sort_step()
+        self._diff(self.walk is not None and self.late)
+
+    def diff_step(self):
+        """classify2 + fielddiff over the presorted side buffers (keys and OIDs in key order)"""
+        self._diff(False)
+
+    def _diff(self, perm):
+        L, ctx = self.eng.L, self.eng.ctx
+        if perm:  # sorted keys, walk-order OIDs read through the sort orders
+            if self._perm_sides is None:
+                self._perm_sides = []
+                for S, (w, _, _) in zip((self.A, self.B), self.walk):
+                    k = S.kd_side()
+                    k.oid = w.oid.ptr
+                    self._perm_sides.append(k)
+            N.check(L.kd_diff2_device_perm(ctx, ctypes.byref(self._perm_sides[0]), ctypes.byref(self._perm_sides[1]),
+                                           self.walk[0][1].ptr, self.walk[1][1].ptr, self.flags, self.delta.ptr,
+                                           self.upd.ptr, self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device_perm")
+        elif self.gather is None:
             N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.ptr,
                                       self.upd.ptr, self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
         else:

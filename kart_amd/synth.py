@@ -395,6 +395,61 @@ def int_pk_paths(pk):
     return arena, off
 
 
+def walk_sort_keys(pk):
+    """u64 sort keys whose ascending order is git tree order (what kd_walk / `git ls-tree -r` lists,
+    kart/dataset3.py:225-231) of the IntPathEncoder paths of int pks in [0, 2**30): the four tree
+    characters (ASCII, big-endian) above the last base64 group of the filename.  Within one 64-pk
+    leaf tree every filename has the same length and differs only in that last group (the msgpack
+    width changes at 128 / 256 / 65536, multiples of 64), so the two fields order the paths exactly."""
+    pk = np.asarray(pk, np.int64)
+    n = pk.shape[0]
+    if n and (pk.min() < 0 or pk.max() >= (1 << 30)):
+        raise ValueError("walk_sort_keys: pks in [0, 2**30)")
+    t12 = _b64_pairs()
+    out = np.empty(n, np.uint64)
+    for s in range(0, n, 1 << 23):
+        p = pk[s:s + (1 << 23)]
+        bucket = p >> 6
+        tree = (t12[bucket >> 12] << np.uint64(16)) | t12[bucket & 4095]
+        # pk >= 65536: msgpack 91 ce b3 b2 b1 b0, the last group is (b2, b1, b0) = pk & 0xFFFFFF
+        v = p & 0xFFFFFF
+        last = (t12[v >> 12] << np.uint64(16)) | t12[v & 4095]
+        small = np.nonzero(p < 65536)[0]
+        if small.size:  # narrower msgpack ints: the general form (last group padded with '=')
+            q = p[small]
+            w = np.where(q < 128, 0, np.where(q < 256, 1, 2))
+            mlen = 2 + w
+            mp = np.zeros((q.shape[0], 6), np.int64)
+            mp[:, 0] = 0x91
+            mp[:, 1] = np.where(w == 0, q, np.where(w == 1, 0xCC, 0xCD))
+            for k in range(2):
+                mp[:, 2 + k] = np.where(k < w, (q >> np.maximum(8 * (w - 1 - k), 0)) & 0xFF, 0)
+            g = (mlen + 2) // 3 - 1  # index of the last 3-byte group
+            rows = np.arange(q.shape[0])
+            vv = mp[rows, 3 * g] << 16 | mp[rows, 3 * g + 1] << 8 | mp[rows, 3 * g + 2]
+            pad = (3 - mlen % 3) % 3  # '=' chars ending the name
+            ch = [_B64[(vv >> (18 - 6 * j)) & 63].astype(np.uint64) for j in range(4)]
+            ch[3] = np.where(pad >= 1, ord("="), ch[3]).astype(np.uint64)
+            ch[2] = np.where(pad >= 2, ord("="), ch[2]).astype(np.uint64)
+            last[small] = (ch[0] << np.uint64(24)) | (ch[1] << np.uint64(16)) | (ch[2] << np.uint64(8)) | ch[3]
+        out[s:s + p.shape[0]] = (tree << np.uint64(32)) | last
+    return out
+
+
+def _b64_pairs():
+    """[4096] u64: the two base64 chars (ASCII, big-endian) of a 12-bit value"""
+    v = np.arange(4096)
+    return (_B64[v >> 6].astype(np.uint64) << np.uint64(8)) | _B64[v & 63].astype(np.uint64)
+
+
+def walk_perm(keys):
+    """perm such that keys[perm] is the side in git tree (walk) order, for KD_KEY_INT keys of pks in
+    [0, 2**30) — the order the native walker hands the packer its leaves"""
+    keys = np.asarray(keys, np.uint64)
+    pk = (keys >> np.uint64(40)).astype(np.int64) * 64 + (keys & np.uint64(63)).astype(np.int64)
+    return np.argsort(walk_sort_keys(pk), kind="stable")
+
+
 def _int_keys(pk):
     """vectorised KD_KEY_INT (same formula as kd_pack_int_keys / packing.pk_to_int_key)"""
     pk = np.asarray(pk, np.int64)

@@ -3,6 +3,7 @@
 Every comparison is bit-exact: delta sets, update lists, changed-field masks, conflict sets,
 encoded envelopes and match flags are integer / byte results.
 """
+import ctypes
 import json
 import os
 
@@ -12,6 +13,8 @@ import pytest
 from checks import check_diff_case, check_merge_case
 from fixtures import DIFF_FIXTURES, GOLDEN, MERGE_FIXTURES, load
 from oracle import oracle as O
+
+from kart_amd import _native as N
 
 pytestmark = pytest.mark.gpu
 
@@ -236,26 +239,44 @@ def test_gpu_env_overlap_vs_oracle(engine):
         assert np.array_equal(g, o)
 
 
-@pytest.mark.parametrize("ordered,n,layer", [
-    (o, n, layer) for o in (True, False)
+@pytest.mark.parametrize("ordered,n,layer,walk", [
+    (o, n, layer, False) for o in (True, False)
     for n, layer in [(1000, "points"), (3_000_000, "points"), (1000, "polygons"), (2_000_000, "polygons")]] + [
-    (True, 10_000_000, "points"),       # C2 at its stated size (configs[1])
-    (True, 100_000_000, "polygons"),    # C3 at its stated size (configs[2], the bench's default workload)
+    (True, 1000, "points", "late"), (True, 3_000_000, "points", "late"), (False, 2_000_000, "polygons", "late"),
+    (True, 1000, "points", "gather"), (True, 2_000_000, "polygons", "gather"),
+    (True, 10_000_000, "points", False),    # C2 at its stated size (configs[1])
+    (True, 100_000_000, "polygons", "late"),  # C3 at its stated size (configs[2], the bench's default
+                                              # workload), from walk-order sides: both 100M sorts included
 ])
-def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered):
+def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
     """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes),
     on the C2 points layer and the C3 polygon layer (~370-B blobs: head + tail windows and the
-    cooperative payload compares); buffers from the library's own allocator"""
+    cooperative payload compares); buffers from the library's own allocator.  walk: the sides start
+    in git tree order and every step sorts them on the GPU first (kd_sort_side_into): the sorted
+    keys and OIDs must equal the generator's key-ordered sides and the order must invert the walk
+    permutation (= a stable argsort of the walk-order keys), bit for bit"""
     from kart_amd import synth
     from kart_amd.device import DiffPipeline
     from kart_amd.schema import FieldMaps
 
     L = synth.points_layer(n, seed=11) if layer == "points" else synth.polygons_layer(n, seed=12)
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
-    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered)
+    perms = (synth.walk_perm(L.base.key), synth.walk_perm(L.target.key)) if walk else None
+    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered, walk=perms,
+                        late=walk == "late")
+    if walk:  # scramble the sorted buffers first: the sort (and, gathering, its OID permute) must rewrite them
+        for S in (pipe.A, pipe.B):
+            N.check(engine.L.kd_memset(engine.ctx, S.key.ptr, 0xA5, S.key.nbytes), "kd_memset")
+            N.check(engine.L.kd_memset(engine.ctx, S.oid.ptr, 0x5A, S.oid.nbytes), "kd_memset")
     for _ in range(3):  # repeated steps reuse the workspaces and counters
         pipe.step()
     engine.sync()
+    if walk:
+        for S, side, perm, order in zip((pipe.A, pipe.B), (L.base, L.target), perms, pipe.orders()):
+            assert np.array_equal(S.key.download(np.uint64, side.n), side.key)
+            if walk == "gather":
+                assert np.array_equal(S.oid.download(np.uint8, 20 * side.n).reshape(side.n, 20), side.oid)
+            assert np.array_equal(perm[order], np.arange(side.n))  # walk_keys[order] ascending
     counts, delta, upd, masks, status = pipe.results()
     od, oc = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
     if ordered:
@@ -466,6 +487,65 @@ def test_gpu_sort_side_vs_argsort(engine, n, kind):
     assert np.array_equal(k, keys[ref]) and np.array_equal(o, oids[ref])
 
 
+@pytest.mark.parametrize("n,kind", [(1, "rand"), (2, "rand"), (3, "one_bit"), (8191, "rand"), (8192, "int30"),
+                                    (8193, "int30"), (4095, "rand"), (4097, "rand"), (1_000_003, "rand"),
+                                    (2_000_000, "walk"), (500_000, "runs5"), (300_000, "hi_bits"), (77, "equal")])
+def test_gpu_sort_side_into_vs_argsort(engine, n, kind):
+    """the out-of-place device sort (the pipeline's form) equals a stable host argsort: keys, order
+    and OIDs; the inputs stay untouched.  Tile edges (8192 keys per 32-bit tile, 4096 per 64-bit
+    tile), random 64-bit keys (8 passes over the 64-bit compact key), int keys (compact 32-bit key),
+    walk-order C3 keys, a varying-bit mask of 5 runs (merged into 4), and all-equal keys (no pass;
+    flagged as duplicates)"""
+    from kart_amd import synth
+    from kart_amd.device import DevBuf
+
+    rng = np.random.default_rng(n)
+    if kind == "rand":
+        keys = np.unique(rng.integers(0, 2**64 - 1, size=n + n // 8 + 8, dtype=np.uint64))[:n]
+        rng.shuffle(keys)
+    elif kind == "int30":
+        keys = synth._int_keys(rng.permutation(n).astype(np.int64) * 5)
+    elif kind == "walk":
+        keys = synth._int_keys(np.arange(n, dtype=np.int64))
+        keys = keys[synth.walk_perm(keys)]
+    elif kind == "runs5":
+        spread = np.uint64(0)
+        for b in (0, 1, 9, 10, 20, 33, 34, 35, 50, 63):
+            spread |= np.uint64(1) << np.uint64(b)
+        vals = rng.permutation(1 << 10)[: min(n, 1 << 10)].astype(np.uint64)
+        keys = np.zeros(vals.shape[0], np.uint64)
+        bits = [b for b in range(64) if (int(spread) >> b) & 1]
+        for j, b in enumerate(bits):
+            keys |= ((vals >> np.uint64(j)) & np.uint64(1)) << np.uint64(b)
+        keys |= np.uint64(0x0000_0100_0004_0000)  # constant bits between the runs
+    elif kind == "hi_bits":
+        keys = (np.arange(n, dtype=np.uint64) << np.uint64(40)) | np.uint64(0xABCDE)
+        rng.shuffle(keys)
+    elif kind == "one_bit":
+        keys = np.array([5 | (1 << 63), 5, 7][:n], np.uint64)
+    else:
+        keys = np.full(n, 12345, np.uint64)
+    n = keys.shape[0]
+    oids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
+    dk, do = DevBuf.from_numpy(engine, keys), DevBuf.from_numpy(engine, oids.reshape(-1))
+    ko, oo, order, dup = DevBuf(engine, 8 * n), DevBuf(engine, 20 * n), DevBuf(engine, 4 * n), DevBuf(engine, 4)
+    N.check(engine.L.kd_sort_side_into(engine.ctx, dk.ptr, do.ptr, ko.ptr, oo.ptr, order.ptr, n, dup.ptr),
+            "kd_sort_side_into")
+    ref = np.argsort(keys, kind="stable")
+    assert np.array_equal(order.download(np.uint32, n), ref.astype(np.uint32))
+    assert np.array_equal(ko.download(np.uint64, n), keys[ref])
+    assert np.array_equal(oo.download(np.uint8, 20 * n).reshape(n, 20), oids[ref])
+    assert np.array_equal(dk.download(np.uint64, n), keys) and np.array_equal(do.download(np.uint8, 20 * n), oids.reshape(-1))
+    assert int(dup.download(np.uint32, 1)[0]) == (1 if kind == "equal" and n > 1 else 0)
+
+
+def test_gpu_sort_side_into_rejects_aliasing(engine):
+    from kart_amd.device import DevBuf
+
+    dk, do, order = DevBuf(engine, 80), DevBuf(engine, 200), DevBuf(engine, 40)
+    assert engine.L.kd_sort_side_into(engine.ctx, dk.ptr, do.ptr, dk.ptr, do.ptr, order.ptr, 10, None) == N.KD_EINVAL
+
+
 def test_gpu_sort_side_duplicates_rejected(engine):
     from kart_amd import packing
 
@@ -494,3 +574,63 @@ def test_gpu_pack_side_equals_host_pack(engine, n):
     r = engine.diff2(*sides)
     od, _ = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
     assert np.array_equal(r.delta, od)
+
+
+@pytest.mark.parametrize("kind,n", [("int", 1), ("int", 5000), ("int", 2_000_000), ("hash", 300_000), ("hash", 3)])
+def test_gpu_diff2_perm_equals_sorted(engine, kind, n):
+    """kd_diff2_device_perm (sorted keys, OIDs + filename offsets left in a scrambled row order, read
+    through the sort order) gives exactly kd_diff2_device's result on the key-ordered sides — and
+    the oracle's; KD_KEY_HASH filenames are verified through the same rows"""
+    from kart_amd import synth
+    from kart_amd.device import DevBuf, DevSide
+
+    if kind == "int":
+        L = synth.points_layer(n, seed=21)
+        A, B = L.base, L.target
+    else:
+        M = synth.table3_layers(n, seed=22)
+        A, B = M.ours, M.theirs
+    rng = np.random.default_rng(n)
+    sides, orders, keep = [], [], []
+    for S in (A, B):
+        P = rng.permutation(S.n)  # walk row r holds sorted entry P[r]
+        inv = np.argsort(P).astype(np.uint32)  # sorted entry i lives at row inv[i]
+        dk = DevBuf.from_numpy(engine, S.key if S.n else np.zeros(1, np.uint64))
+        do = DevBuf.from_numpy(engine, S.oid[P].reshape(-1) if S.n else np.zeros(20, np.uint8))
+        orders.append(DevBuf.from_numpy(engine, inv if S.n else np.zeros(1, np.uint32)))
+        s = N.KdSide()
+        s.n, s.key, s.oid, s.mem, s.key_mode = S.n, dk.ptr, do.ptr, N.KD_MEM_DEVICE, S.key_mode
+        s.name = s.name_off = None
+        if S.key_mode == N.KD_KEY_HASH:
+            lens = (S.name_off[1:] - S.name_off[:-1]).astype(np.int64)[P]
+            off = np.zeros(S.n + 1, np.uint64)
+            off[1:] = np.cumsum(lens)
+            names = np.concatenate([S.name[int(S.name_off[p]):int(S.name_off[p + 1])] for p in P]) if S.n else \
+                np.zeros(1, np.uint8)
+            dn, dno = DevBuf.from_numpy(engine, names), DevBuf.from_numpy(engine, off)
+            s.name, s.name_off = dn.ptr, dno.ptr
+            keep += [dn, dno]
+        sides.append(s)
+        keep += [dk, do]
+    DA, DB = DevSide(engine, A), DevSide(engine, B)
+    sa, sb = DA.kd_side(), DB.kd_side()
+    cap = A.n + B.n + 1
+    outs = []
+    for perm in (True, False):
+        delta, upd, counts = DevBuf(engine, 8 * cap), DevBuf(engine, 8 * cap), DevBuf(engine, 64)
+        counts.zero()
+        if perm:
+            rc = engine.L.kd_diff2_device_perm(engine.ctx, ctypes.byref(sides[0]), ctypes.byref(sides[1]),
+                                               orders[0].ptr, orders[1].ptr, 0, delta.ptr, upd.ptr, counts.ptr,
+                                               counts.ptr + 32)
+        else:
+            rc = engine.L.kd_diff2_device(engine.ctx, ctypes.byref(sa), ctypes.byref(sb), 0, delta.ptr, upd.ptr,
+                                          counts.ptr, counts.ptr + 32)
+        N.check(rc, "diff2")
+        c = counts.download(np.uint64, 8)
+        assert c[4] == 0
+        outs.append((c[:4].tolist(), delta.download(np.uint32, 2 * int(c[3])), upd.download(np.uint32, 2 * int(c[1]))))
+    assert outs[0][0] == outs[1][0]
+    assert np.array_equal(outs[0][1], outs[1][1]) and np.array_equal(outs[0][2], outs[1][2])
+    od, _ = O.classify2(A.key, A.oid, B.key, B.oid)
+    assert np.array_equal(outs[0][1].reshape(-1, 2), od)

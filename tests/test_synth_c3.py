@@ -69,3 +69,22 @@ def test_int_pk_paths_match_reference_encoder():
         want = tree + "/" + base64.urlsafe_b64encode(msgpack.packb([pk])).decode()
         assert arena[off[i]:off[i + 1]].tobytes().decode() == want
     assert arena[off[8]:off[9]].tobytes() == b"A/A/A/S/kc0EnQ=="
+
+
+def test_walk_order_is_git_path_order():
+    """synth.walk_perm puts a side in git tree order: the order `git ls-tree -r` / kd_walk lists the
+    IntPathEncoder paths (byte-wise path order), which the GPU sort starts from (bench.py's
+    value_with_sort, the walk-mode pipeline tests)"""
+    rng = np.random.default_rng(3)
+    pks = np.unique(np.concatenate([np.arange(0, 400), np.arange(65_000, 66_000), np.arange(2**24 - 70, 2**24 + 70),
+                                    rng.integers(0, 2**30, 30_000)]))
+    rng.shuffle(pks)
+    arena, off = synth.int_pk_paths(pks)
+    paths = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(pks.shape[0])]
+    want = sorted(range(pks.shape[0]), key=lambda i: paths[i])
+    keys = synth._int_keys(pks)
+    perm = synth.walk_perm(keys)
+    assert np.array_equal(perm, np.array(want))
+    # and the walk order is far from key order (what makes the GPU sort necessary)
+    w = keys[perm]
+    assert np.count_nonzero(w[1:] < w[:-1]) > pks.shape[0] // 20
