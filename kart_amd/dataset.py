@@ -18,6 +18,7 @@ import base64
 import contextlib
 import functools
 import gc
+import operator
 import os
 
 import msgpack
@@ -29,6 +30,7 @@ from .adaptor import structs
 from .schema import FieldMaps, Legend, Schema
 
 FEATURE_PATH = "feature/"
+GPU_SORT_MIN = 1 << 20  # sides at least this long are sorted on the GPU when an engine is at hand
 
 
 class Geometry(bytes):
@@ -100,7 +102,8 @@ class LazyBlob:
     @property
     def data(self):
         if self._data is None:
-            self._data = self._src.read_blob(self._i)
+            d = self._src.cached_blob(self._i) if self._src._arenas else None
+            self._data = d if d is not None else self._src.read_blob(self._i)
         return self._data
 
     def __bytes__(self):
@@ -134,6 +137,7 @@ class DatasetVersion:
         self._read_blobs = read_blobs
         self.meta = dict(meta or {})
         self._packed = None
+        self._arenas = []
 
     @property
     def n(self):
@@ -141,11 +145,18 @@ class DatasetVersion:
 
     @property
     def packed(self):
+        return self.pack()
+
+    def pack(self, engine=None):
+        """the side packed for the join (cached).  With a GPU engine and a large side the sort runs
+        on the GPU (kd_sort_side); the host parses the keys either way."""
         if self._packed is None:
             if self.n == 0:
                 self._packed = packing.empty_side(self.encoding)
             else:
-                self._packed = packing.pack_side(self.rel_paths, self.oids, self.encoding, rel_off=self.rel_off)
+                gpu = engine if self.n >= GPU_SORT_MIN and hasattr(engine, "ctx") else None
+                self._packed = packing.pack_side(self.rel_paths, self.oids, self.encoding, rel_off=self.rel_off,
+                                                 engine=gpu)
         return self._packed
 
     # ---- Dataset3 API used by the diff path ----------------------------------------------------
@@ -205,6 +216,27 @@ class DatasetVersion:
         data, off = packing._arena(bs)
         return data, off, status
 
+    def blob_arena_leaves(self, leaf_idx):
+        """contiguous (data, off) of the blobs of leaves ``leaf_idx`` (original order), one batched
+        read; KeyError when one is missing.  The arena is remembered, so a later value access of
+        one of these leaves slices it instead of reading the object again."""
+        idx = np.asarray(leaf_idx, np.int64)
+        data, off, status = self.read_blobs(idx)
+        if status.any():
+            self.read_blob(int(idx[int(np.nonzero(status)[0][0])]))  # raises the reference's KeyError
+        order = np.argsort(idx, kind="stable")
+        self._arenas.append((idx[order], order, data, off))
+        return data, off
+
+    def cached_blob(self, i):
+        """leaf i's bytes from an arena blob_arena_leaves read, or None"""
+        for idx, order, data, off in self._arenas:
+            p = int(np.searchsorted(idx, i))
+            if p < idx.shape[0] and idx[p] == i:
+                r = int(order[p])
+                return data[int(off[r]):int(off[r + 1])].tobytes()
+        return None
+
     def blob_arena(self, sorted_idx):
         """contiguous (data, off) of the blobs at the given sorted indices (host packing for
         kd_fielddiff); KeyError when one is missing"""
@@ -225,17 +257,32 @@ def _pks(version, sorted_idx):
     return [version.decode_path_to_1pk(version.rel_path(int(order[k]))) for k in sorted_idx]
 
 
-def diff_feature(engine, base, target, feature_filter=None, reverse=False):
+class UpdateBatch:
+    """The update deltas one diff_feature run yielded, with both sides' leaf indices (original
+    order): what field_diff needs to read the blobs straight into one arena per side, without
+    walking the DeltaDiff or touching a blob object"""
+
+    __slots__ = ("old_v", "new_v", "old_leaf", "new_leaf", "deltas", "keys", "n_total")
+
+    def __init__(self):
+        self.old_v = self.new_v = None
+        self.old_leaf = self.new_leaf = None
+        self.deltas, self.keys, self.n_total = [], [], -1
+
+
+def diff_feature(engine, base, target, feature_filter=None, reverse=False, updates=None):
     """Generator of Delta with lazy values (RichBaseDataset.diff_feature semantics).
 
-    base / target: DatasetVersion or None (a missing dataset diffs against the empty tree)."""
+    base / target: DatasetVersion or None (a missing dataset diffs against the empty tree).
+    updates: an UpdateBatch that receives the yielded update deltas (set once the generator is
+    exhausted)."""
     present = base if base is not None else target
     if present is None:
         return
     S = structs()
     empty = packing.empty_side(present.encoding)
-    A = base.packed if base is not None else empty
-    B = target.packed if target is not None else empty
+    A = base.pack(engine) if base is not None else empty
+    B = target.pack(engine) if target is not None else empty
     res = engine.diff2(A, B)
     old_v, new_v = (target, base) if reverse else (base, target)
     d = res.delta
@@ -264,6 +311,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False):
     if has_b.any():
         for i, b in zip(ib.tolist(), new_v.get_blobs(B.order[b_idx[ib]])):
             new_blobs[i] = b
+    upd_rows, upd_deltas, upd_keys, n_total = [], [], [], 0
     for i in range(d.shape[0]):
         opk, npk = old_pks[i], new_pks[i]
         if not match_all and str(opk) not in feature_filter and str(npk) not in feature_filter:
@@ -271,7 +319,19 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False):
         ob, nb = old_blobs[i], new_blobs[i]
         old_half = (opk, functools.partial(old_v.get_feature_from_blob, ob)) if ob is not None else None
         new_half = (npk, functools.partial(new_v.get_feature_from_blob, nb)) if nb is not None else None
-        yield S.Delta(old_half, new_half)
+        delta = S.Delta(old_half, new_half)
+        if ob is not None and nb is not None:
+            upd_rows.append(i)
+            upd_deltas.append(delta)
+            upd_keys.append(opk)
+        n_total += 1
+        yield delta
+    if updates is not None:
+        rows = np.asarray(upd_rows, np.int64)
+        updates.old_v, updates.new_v = old_v, new_v
+        updates.old_leaf = A.order[a_idx[rows]] if rows.size else np.zeros(0, np.int64)
+        updates.new_leaf = B.order[b_idx[rows]] if rows.size else np.zeros(0, np.int64)
+        updates.deltas, updates.keys, updates.n_total = upd_deltas, upd_keys, n_total
 
 
 def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
@@ -285,8 +345,11 @@ def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
         # a filter without a "feature" entry matches no feature (the reference falls back to an empty
         # child filter: ds_filter.get("feature", ds_filter.child_type()), :177)
         ffilter = ds_filter.get("feature", _NoKeys())
+    batch = UpdateBatch()
     with _gc_paused():
-        out["feature"] = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse))
+        fd = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch))
+    fd._kd_updates = batch
+    out["feature"] = fd
     return out
 
 
@@ -339,8 +402,8 @@ def get_exact_diff_blob_count(engine, base, target):
     if present is None:
         return 0
     empty = packing.empty_side(present.encoding)
-    A = base.packed if base is not None else empty
-    B = target.packed if target is not None else empty
+    A = base.pack(engine) if base is not None else empty
+    B = target.pack(engine) if target is not None else empty
     r = engine.diff2(A, B)
     return int(r.n_insert + r.n_update + r.n_delete)
 
@@ -364,17 +427,46 @@ def estimate_diff_feature_counts(engine, base_datasets, target_datasets, *, accu
 def field_diff(engine, feature_diff, old_version, new_version):
     """Attach ``changed_fields`` (names, in _all_feature_keys order) to every update delta of
     ``feature_diff``, computed by kd_fielddiff in one batch.  Updates the GPU cannot handle
-    (status != 0) get None and the caller uses the reference loop for them."""
-    ups = [d for d in feature_diff.values() if d.type == "update"]
-    if not ups:
-        return 0
-    maps = FieldMaps(old_version.schema, old_version.legends, new_version.schema, new_version.legends)
-    od, oo = _blob_arena([d.old.value.args[0] for d in ups])
-    nd, no = _blob_arena([d.new.value.args[0] for d in ups])
-    masks, status = engine.fielddiff(od, oo, nd, no, None, maps)
-    for d, names, s in zip(ups, maps.changed_names_rows(masks[:len(ups)]), status.tolist()):
-        d.changed_fields = names if s == 0 else None
-    return len(ups)
+    (status != 0) get None and the caller uses the reference loop for them.
+
+    A DeltaDiff that dataset_diff built carries its updates' leaf indices: each side's blobs are
+    read by one kd_odb_read_batch straight into the arena kd_fielddiff takes (no per-blob Python
+    object), and the arena is kept for later value reads.  Any other DeltaDiff (built by hand,
+    combined with ``+``) goes through its lazy blobs."""
+    with _gc_paused():
+        batch = _live_batch(feature_diff, old_version, new_version)
+        if batch is not None:
+            ups = batch.deltas
+            if not ups:
+                return 0
+            od, oo = old_version.blob_arena_leaves(batch.old_leaf)
+            nd, no = new_version.blob_arena_leaves(batch.new_leaf)
+        else:
+            ups = [d for d in feature_diff.values() if d.type == "update"]
+            if not ups:
+                return 0
+            od, oo = _blob_arena([d.old.value.args[0] for d in ups])
+            nd, no = _blob_arena([d.new.value.args[0] for d in ups])
+        maps = FieldMaps(old_version.schema, old_version.legends, new_version.schema, new_version.legends)
+        masks, status = engine.fielddiff(od, oo, nd, no, None, maps)
+        names = maps.changed_names_rows(masks[:len(ups)])
+        for d, nm, s in zip(ups, names, status.tolist()):
+            d.changed_fields = nm if s == 0 else None
+        return len(ups)
+
+
+def _live_batch(feature_diff, old_version, new_version):
+    """the UpdateBatch of a DeltaDiff that still holds exactly the deltas dataset_diff put there:
+    same size, and every recorded update still stored under its key (C-level loops, no walk of the
+    whole diff)"""
+    batch = getattr(feature_diff, "_kd_updates", None)
+    if batch is None or batch.old_v is not old_version or batch.new_v is not new_version:
+        return None
+    if len(feature_diff) != batch.n_total:
+        return None
+    if not all(map(operator.is_, map(feature_diff.get, batch.keys), batch.deltas)):
+        return None
+    return batch
 
 
 def prefetch_blobs(blobs):

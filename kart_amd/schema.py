@@ -160,13 +160,9 @@ class FieldMaps:
     def changed_names_rows(self, masks):
         """changed_names of every row of ``masks`` [n, words], one fresh list per row; each
         distinct mask (a layer's updates share a handful) is decoded once"""
-        masks = np.ascontiguousarray(masks, np.uint64)
-        raw, w = masks.tobytes(), 8 * masks.shape[1]
-        memo, out = {}, []
-        for r in range(masks.shape[0]):
-            key = raw[r * w:(r + 1) * w]
-            names = memo.get(key)
-            if names is None:
-                names = memo[key] = tuple(self.changed_names(masks[r]))
-            out.append(list(names))
-        return out
+        masks = np.ascontiguousarray(masks, np.uint64).reshape(-1, self.words)
+        if masks.shape[0] == 0:
+            return []
+        uniq, inv = np.unique(masks, axis=0, return_inverse=True)
+        names = [tuple(self.changed_names(row)) for row in uniq]
+        return [list(names[j]) for j in inv.reshape(-1).tolist()]

@@ -225,3 +225,46 @@ def test_exact_feature_counts(eng, name):
         if base is not None:  # dataset deleted in the target: every feature is a changed path
             assert D.get_exact_diff_blob_count(eng, base, None) == base.n
     assert D.get_exact_diff_blob_count(eng, None, None) == 0
+
+
+def test_field_diff_batch_path(eng):
+    """field_diff on a DeltaDiff from dataset_diff reads each side's update blobs in one batched
+    read by leaf index (no per-delta blob object) and keeps the arena: the values the writer reads
+    afterwards come from it, with no further object read.  A diff changed after dataset_diff (a
+    delta removed) goes through the lazy blobs and gives the same fields."""
+    fx = load("repo_points")
+    old, new = version(fx, "head1"), version(fx, "head")
+    batches = {"n": 0}
+    reads = {"n": 0}
+    for v in (old, new):
+        rb = v.read_blob
+
+        def counted_read(i, _rb=rb):
+            reads["n"] += 1
+            return _rb(i)
+
+        def batch_read(idx, _rb=rb):
+            batches["n"] += 1
+            bs = [bytes(_rb(int(i))) for i in idx]
+            off = np.zeros(len(bs) + 1, np.uint64)
+            off[1:] = np.cumsum([len(b) for b in bs])
+            return np.frombuffer(b"".join(bs), np.uint8).copy(), off, np.zeros(len(bs), np.uint8)
+
+        v.read_blob = counted_read
+        v._read_blobs = batch_read
+    fd = D.dataset_diff(eng, old, new)["feature"]
+    assert fd._kd_updates.n_total == len(fd) == 5
+    assert D.field_diff(eng, fd, old, new) == 5
+    assert batches["n"] == 2 and reads["n"] == 0
+    fields = {k: d.changed_fields for k, d in fd.items()}
+    assert sum(len(v) for v in fields.values()) == 13
+    vals = {k: (d.old_value, d.new_value) for k, d in fd.items()}
+    assert reads["n"] == 0  # every value came from the field diff's arenas
+    # a mutated diff: the recorded batch no longer describes it -> the lazy-blob path
+    fd2 = D.dataset_diff(eng, version(fx, "head1"), version(fx, "head"))["feature"]
+    gone = sorted(fd2.keys())[0]
+    del fd2[gone]
+    assert D._live_batch(fd2, fd2._kd_updates.old_v, fd2._kd_updates.new_v) is None
+    assert D.field_diff(eng, fd2, fd2._kd_updates.old_v, fd2._kd_updates.new_v) == 4
+    assert {k: d.changed_fields for k, d in fd2.items()} == {k: v for k, v in fields.items() if k != gone}
+    assert {k: (d.old_value, d.new_value) for k, d in fd2.items()} == {k: v for k, v in vals.items() if k != gone}
