@@ -16,6 +16,9 @@
  *                     CRS (kart/spatial_filter/index.py:485-579,639-707).
  *   kd_env_overlap <- sf_filter_blob decode + cyclic_range_overlaps
  *                     (vendor/spatial-filter/spatial_filter.cpp:170-260).
+ *   kd_sf_index_build / kd_sf_filter
+ *                  <- sf_filter_blob (vendor/spatial-filter/spatial_filter.cpp:212-260): the clone-time
+ *                     spatial filter over a batch of object ids against feature_envelopes.
  *   kd_geom_filter <- BaseDiffWriter.filtered_ds_feature_deltas (kart/base_diff_writer.py:279-329):
  *                     the geometry of each delta's old/new feature blob, envelope-tested, kept
  *                     deltas compacted on the GPU.
@@ -199,6 +202,22 @@ int kd_envelopes(kd_ctx* ctx, const kd_blobs* geoms, const double filt_env[4], i
  * out[i] = cyclic(w,e) && range(s,n) overlap (spatial_filter.cpp:187-260). */
 int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const double q[4],
                    uint8_t* out, uint32_t mem);
+
+/* -------- clone-time spatial filter -------- */
+/* sf_filter_blob (vendor/spatial-filter/spatial_filter.cpp:212-260) for a batch of objects.  The
+ * feature_envelopes table (blob id -> EnvelopeEncoder bytes, bits/2 each: bits = 8 * bytes / 4 as
+ * the reference derives it) is loaded once into HBM: oid [n*20] and env [n*bits/2] in any row order
+ * (mem: where they live).  kd_sf_filter answers m objects: oid [m*20] (4-byte aligned), is_feature
+ * [m] (may be NULL = all are feature blobs: 1 when the object's path contains
+ * "/.table-dataset/feature/" or "/.sno-dataset/feature/"), q = (w, s, e, n) of the filter;
+ * result[i] = 0 MATCH (not a feature, not in the index, or the envelope overlaps), 1 NOT_MATCHED,
+ * 2 ERROR (an inverted range: the reference aborts).  An inverted query latitude range is KD_EINVAL. */
+typedef struct kd_sf_index kd_sf_index;
+int kd_sf_index_build(kd_ctx* ctx, const uint8_t* oid, const uint8_t* env, uint64_t n, int bits, uint32_t mem,
+                      kd_sf_index** out);
+int kd_sf_filter(kd_ctx* ctx, const kd_sf_index* index, const uint8_t* oid, const uint8_t* is_feature, uint64_t m,
+                 const double q[4], uint8_t* result, uint32_t mem);
+int kd_sf_index_free(kd_sf_index* index);
 
 /* -------- spatially filtered diff -------- */
 /* BaseDiffWriter.filtered_ds_feature_deltas (kart/base_diff_writer.py:279-329) with

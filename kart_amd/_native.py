@@ -181,6 +181,11 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_dblp, ctypes.c_void_p,
          ctypes.c_uint32],
     ),
+    "kd_sf_index_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "kd_sf_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     c_dblp, ctypes.c_void_p, ctypes.c_uint32]),
+    "kd_sf_index_free": (ctypes.c_int, [ctypes.c_void_p]),
     "kd_geom_filter": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.POINTER(KdBlobs), ctypes.POINTER(KdBlobs), ctypes.c_void_p, ctypes.c_uint64,

@@ -67,6 +67,34 @@ __device__ __forceinline__ int range_ov(double a1, double a2, double b1, double 
     return (b2 != b1) && (a2 != a1);
 }
 
+// EnvelopeEncoder::decode of one big-endian record of 4 x bits (spatial_filter.cpp:106-128), then
+// cyclic_range_overlaps(w, e, qw, qe) && range_overlaps(s, n, qs, qn) (:170-208, :249):
+// 1 overlaps, 0 not, -1 an inverted range (the reference aborts)
+__device__ __forceinline__ int enc_overlap(const u8* p, int bits, double qw, double qs, double qe, double qn) {
+    const int nb = bits / 2;
+    const double vmax = (double)((1ull << bits) - 1);
+    const u64 mask = (1ull << bits) - 1;
+    unsigned __int128 acc = 0;
+    for (int k = 0; k < nb; k++) acc = (acc << 8) | p[k];
+    double v[4];
+    const double mins[4] = {-180, -90, -180, -90}, maxs[4] = {180, 90, 180, 90};
+    for (int k = 3; k >= 0; k--) {
+        const u64 q = (u64)(acc & mask);
+        acc >>= bits;
+        v[k] = ((double)q / vmax) * (maxs[k] - mins[k]) + mins[k];
+    }
+    double a1 = v[0], a2 = v[2], b1 = qw, b2 = qe;
+    if (a1 > a2) a2 += 360;
+    if (b1 > b2) b2 += 360;
+    int r = range_ov(a1, a2, b1, b2);
+    if (r == 0) {
+        if (a1 < b1) { a1 += 360; a2 += 360; } else { b1 += 360; b2 += 360; }
+        r = range_ov(a1, a2, b1, b2);
+    }
+    if (r > 0) r = range_ov(v[1], v[3], qs, qn);
+    return r;
+}
+
 __device__ __attribute__((noinline)) double py_mod360_slow(double a) {
     double m = fmod(a, 360.0);
     if (m != 0.0) {

@@ -373,6 +373,49 @@ struct Reader {
         s.data = data;
     }
 
+    // one loose object file: zlib("<type> <size>\0" + content)
+    int parse_loose(const std::vector<u8>& raw, int* type, std::vector<u8>& out) {
+        if (!zok || inflateReset(&z) != Z_OK) return RD_CORRUPT;
+        u8 hdr[64];
+        z.next_in = const_cast<u8*>(raw.data());
+        z.avail_in = (uInt)raw.size();
+        z.next_out = hdr;
+        z.avail_out = sizeof hdr;
+        int zr = inflate(&z, Z_NO_FLUSH);
+        if (zr != Z_OK && zr != Z_STREAM_END) return RD_CORRUPT;
+        const size_t got = sizeof hdr - z.avail_out;
+        const u8* nul = (const u8*)memchr(hdr, 0, got);
+        if (!nul) return RD_CORRUPT;
+        const u8* sp = (const u8*)memchr(hdr, ' ', nul - hdr);
+        if (!sp) return RD_CORRUPT;
+        const size_t tl = sp - hdr;
+        int t = tl == 4 && !memcmp(hdr, "blob", 4) ? OBJ_BLOB
+                : tl == 4 && !memcmp(hdr, "tree", 4) ? OBJ_TREE
+                : tl == 6 && !memcmp(hdr, "commit", 6) ? OBJ_COMMIT
+                : tl == 3 && !memcmp(hdr, "tag", 3) ? OBJ_TAG : 0;
+        if (!t) return RD_CORRUPT;
+        u64 size = 0;
+        for (const u8* q = sp + 1; q < nul; q++) {
+            if (*q < '0' || *q > '9' || size > (1ull << 50)) return RD_CORRUPT;
+            size = size * 10 + (*q - '0');
+        }
+        const size_t have = got - (nul + 1 - hdr);
+        if (have > size) return RD_CORRUPT;
+        out.resize(size);
+        memcpy(out.data(), nul + 1, have);
+        if (zr != Z_STREAM_END) {
+            z.next_out = out.data() + have;
+            z.avail_out = (uInt)(size - have);
+            zr = inflate(&z, Z_FINISH);
+            if (zr != Z_STREAM_END) return RD_CORRUPT;
+        }
+        if (z.total_out != size + (nul + 1 - hdr)) return RD_CORRUPT;
+        *type = t;
+        return RD_OK;
+    }
+
+    // the object's loose file in the first object directory (own, then alternates) that holds a
+    // readable copy: a corrupt copy in one directory does not hide a good one in the next
     int read_loose(const u8* oid, int* type, std::vector<u8>& out) {
         static const char hx[] = "0123456789abcdef";
         char name[42];
@@ -380,6 +423,7 @@ struct Reader {
             name[2 * i] = hx[oid[i] >> 4];
             name[2 * i + 1] = hx[oid[i] & 15];
         }
+        int result = RD_MISSING;
         for (const std::string& dir : db->objdirs) {
             std::string path = dir + "/" + std::string(name, 2) + "/" + std::string(name + 2, 38);
             int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
@@ -389,46 +433,11 @@ struct Reader {
             ssize_t r;
             while ((r = ::read(fd, buf, sizeof buf)) > 0) raw.insert(raw.end(), buf, buf + r);
             ::close(fd);
-            if (r < 0 || !zok || inflateReset(&z) != Z_OK) return RD_CORRUPT;
-            // header "<type> <size>\0", then the content
-            u8 hdr[64];
-            z.next_in = raw.data();
-            z.avail_in = (uInt)raw.size();
-            z.next_out = hdr;
-            z.avail_out = sizeof hdr;
-            int zr = inflate(&z, Z_NO_FLUSH);
-            if (zr != Z_OK && zr != Z_STREAM_END) return RD_CORRUPT;
-            const size_t got = sizeof hdr - z.avail_out;
-            const u8* nul = (const u8*)memchr(hdr, 0, got);
-            if (!nul) return RD_CORRUPT;
-            const u8* sp = (const u8*)memchr(hdr, ' ', nul - hdr);
-            if (!sp) return RD_CORRUPT;
-            const size_t tl = sp - hdr;
-            int t = tl == 4 && !memcmp(hdr, "blob", 4) ? OBJ_BLOB
-                    : tl == 4 && !memcmp(hdr, "tree", 4) ? OBJ_TREE
-                    : tl == 6 && !memcmp(hdr, "commit", 6) ? OBJ_COMMIT
-                    : tl == 3 && !memcmp(hdr, "tag", 3) ? OBJ_TAG : 0;
-            if (!t) return RD_CORRUPT;
-            u64 size = 0;
-            for (const u8* q = sp + 1; q < nul; q++) {
-                if (*q < '0' || *q > '9' || size > (1ull << 50)) return RD_CORRUPT;
-                size = size * 10 + (*q - '0');
-            }
-            const size_t have = got - (nul + 1 - hdr);
-            if (have > size) return RD_CORRUPT;
-            out.resize(size);
-            memcpy(out.data(), nul + 1, have);
-            if (zr != Z_STREAM_END) {
-                z.next_out = out.data() + have;
-                z.avail_out = (uInt)(size - have);
-                zr = inflate(&z, Z_FINISH);
-                if (zr != Z_STREAM_END) return RD_CORRUPT;
-            }
-            if (z.total_out != size + (nul + 1 - hdr)) return RD_CORRUPT;
-            *type = t;
-            return RD_OK;
+            const int rc = r < 0 ? RD_CORRUPT : parse_loose(raw, type, out);
+            if (rc == RD_OK) return RD_OK;
+            result = rc;
         }
-        return RD_MISSING;
+        return result;
     }
 
     int read(const u8* oid, int* type, std::vector<u8>& out, int depth = 0) {
@@ -802,7 +811,7 @@ extern "C" int kd_odb_read(kd_odb* odb, const uint8_t* oid, int* type, uint8_t**
 
 extern "C" int kd_odb_read_batch(kd_odb* odb, const uint8_t* oids, uint64_t n, int threads, uint8_t** data,
                                  uint64_t* off, uint8_t* status) {
-    if (!odb || (n && (!oids || !off || !status)) || !data) { kd::set_error("kd_odb_read_batch: NULL"); return KD_EINVAL; }
+    if (!odb || !off || (n && (!oids || !status)) || !data) { kd::set_error("kd_odb_read_batch: NULL"); return KD_EINVAL; }
     *data = nullptr;
     const int nt = default_threads(threads);
     // blobs in chunks of 256 per task: each task fills its own buffer, the arena is stitched after

@@ -111,7 +111,10 @@ class GitRepo:
         try:
             return self.odb.read(oid)
         except N.NotFound:
-            self.odb.reopen()  # packs written since the store was opened
+            # packs written since the store was opened (a miss with an unchanged pack set does
+            # not reopen: promised blobs of a partial clone miss on every read)
+            if not self.odb.refresh():
+                raise self._missing(oid_bytes(oid).hex()) from None
             try:
                 return self.odb.read(oid)
             except N.NotFound:
@@ -127,8 +130,7 @@ class GitRepo:
     def read_blobs(self, oids):
         """(data, off, status) of blobs [n, 20] in one batched native read"""
         data, off, status = self.odb.read_batch(oids)
-        if status.any():
-            self.odb.reopen()
+        if status.any() and self.odb.refresh():
             data, off, status = self.odb.read_batch(oids)
         return data, off, status
 
@@ -147,7 +149,8 @@ class GitRepo:
         try:
             return self.odb.walk(roots, subpath, compare)
         except N.NotFound:
-            self.odb.reopen()
+            if not self.odb.refresh():
+                raise
             return self.odb.walk(roots, subpath, compare)
 
     def ls_tree_r(self, treeish, prefix):

@@ -6,6 +6,8 @@ kart/rich_base_dataset.py:212-232), read natively: loose objects, packs with del
 a multithreaded leaf walk that never opens a subtree whose OID two roots share.
 """
 import ctypes
+import os
+import threading
 
 import numpy as np
 
@@ -73,24 +75,55 @@ def _take_leaves(L, p):
 
 class ObjectDB:
     """A repository's object store (``gitdir`` = the .git directory or a bare repo).  The pack
-    set is read at open; ``reopen()`` picks up packs written since."""
+    set is read at open; ``refresh()`` reopens when packs were written since (``reopen()``
+    unconditionally).  Native calls and reopening share one lock, so a thread never closes the
+    handle under another thread's GIL-released native call."""
 
     def __init__(self, gitdir):
         self.gitdir = gitdir
         self.L = N.lib()
         self._h = None
+        self._lock = threading.RLock()
+        self._sig = None
+        self.n_opens = 0
         self.reopen()
 
+    def _pack_signature(self):
+        """what a reopen would see differently: the pack directory's files and the alternates"""
+        sig = []
+        for rel in ("objects/pack", "objects/info/alternates"):
+            path = os.path.join(self.gitdir, rel)
+            try:
+                st = os.stat(path)
+            except OSError:
+                sig.append(None)
+                continue
+            sig.append((st.st_mtime_ns, st.st_size, tuple(sorted(os.listdir(path))) if os.path.isdir(path) else ()))
+        return tuple(sig)
+
     def reopen(self):
-        self.close()
-        h = ctypes.c_void_p()
-        N.check(self.L.kd_odb_open(self.gitdir.encode(), ctypes.byref(h)), "kd_odb_open")
-        self._h = h
+        with self._lock:
+            self.close()
+            sig = self._pack_signature()
+            h = ctypes.c_void_p()
+            N.check(self.L.kd_odb_open(self.gitdir.encode(), ctypes.byref(h)), "kd_odb_open")
+            self._h = h
+            self._sig = sig
+            self.n_opens += 1
+
+    def refresh(self):
+        """reopen if packs or alternates changed since the last open; True when it reopened"""
+        with self._lock:
+            if self._h is not None and self._pack_signature() == self._sig:
+                return False
+            self.reopen()
+            return True
 
     def close(self):
-        if self._h is not None and self._h.value:
-            self.L.kd_odb_close(self._h)
-        self._h = None
+        with self._lock:
+            if self._h is not None and self._h.value:
+                self.L.kd_odb_close(self._h)
+            self._h = None
 
     def __del__(self):
         try:
@@ -104,7 +137,9 @@ class ObjectDB:
         t = ctypes.c_int()
         data = N.c_u8p()
         n = ctypes.c_uint64()
-        N.check(self.L.kd_odb_read(self._h, raw, ctypes.byref(t), ctypes.byref(data), ctypes.byref(n)), "kd_odb_read")
+        with self._lock:
+            N.check(self.L.kd_odb_read(self._h, raw, ctypes.byref(t), ctypes.byref(data), ctypes.byref(n)),
+                    "kd_odb_read")
         try:
             return t.value, ctypes.string_at(data, n.value)
         finally:
@@ -118,8 +153,9 @@ class ObjectDB:
         off = np.zeros(n + 1, np.uint64)
         status = np.zeros(max(n, 1), np.uint8)
         data = N.c_u8p()
-        N.check(self.L.kd_odb_read_batch(self._h, oids.ctypes.data if n else None, n, threads, ctypes.byref(data),
-                                         off.ctypes.data, status.ctypes.data), "kd_odb_read_batch")
+        with self._lock:
+            N.check(self.L.kd_odb_read_batch(self._h, oids.ctypes.data if n else None, n, threads, ctypes.byref(data),
+                                             off.ctypes.data, status.ctypes.data), "kd_odb_read_batch")
         try:
             total = int(off[-1])
             arena = np.ctypeslib.as_array(data, (total,)).copy() if total else np.zeros(0, np.uint8)
@@ -134,7 +170,8 @@ class ObjectDB:
         k = len(roots)
         c0, c1 = compare if compare is not None else (N.KD_WALK_ALL, N.KD_WALK_ALL)
         outs = (ctypes.POINTER(N.KdLeaves) * k)()
-        N.check(self.L.kd_walk(self._h, b"".join(roots), k, subpath.encode(), c0, c1, threads, outs), "kd_walk")
+        with self._lock:
+            N.check(self.L.kd_walk(self._h, b"".join(roots), k, subpath.encode(), c0, c1, threads, outs), "kd_walk")
         return [_take_leaves(self.L, outs[i]) for i in range(k)]
 
     def tree_entries(self, oid):

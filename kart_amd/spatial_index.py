@@ -5,7 +5,7 @@ Mirrors ``update_spatial_filter_index`` (kart/spatial_filter/index.py:273-371):
 
 * which blobs — ``iter_feature_oids`` runs ``git rev-list --objects`` over the commits to index
   ``--not`` the already-indexed ones (:193-206); here the commit graph is read from the object
-  store and each commit's feature trees are walked against its first parent with ``kd_walk``'s
+  store and each commit's feature trees are walked against each of its parents with ``kd_walk``'s
   tree-OID pruning, so unchanged subtrees are never opened;
 * the geometry of each blob — ``get_geometry`` (:463-483): the legend's geometry value;
 * its envelope — ``get_envelope_for_indexing`` + ``EnvelopeEncoder.encode`` (:485-579) for an
@@ -16,7 +16,12 @@ Mirrors ``update_spatial_filter_index`` (kart/spatial_filter/index.py:273-371):
   everything indexed, and a later run stops at those commits.
 
 Datasets whose CRS is not EPSG:4326 need PROJ (out of scope): they are skipped and reported.
+
+``CloneFilter`` is the other end: the clone-time decision git's spatial-filter extension makes per
+object from this index (sf_filter_blob, vendor/spatial-filter/spatial_filter.cpp:212-260), for a
+whole batch of objects per GPU call.
 """
+import ctypes
 import json
 import os
 import re
@@ -102,22 +107,39 @@ def minimal_description(repo, commits, cache=None):
 
 def iter_feature_oids(repo, start, stop, cache=None):
     """{(dataset path, blob oid hex)} of every feature blob reachable from ``start`` and not from
-    ``stop`` (iter_feature_oids, :193-206), from pruned walks of each commit against its first
-    parent"""
+    ``stop`` (iter_feature_oids, :193-206): per commit, the feature blobs at paths where it differs
+    from every one of its parents (a blob a merge takes from one parent is that parent's, not
+    new), from pruned walks of the commit against each parent"""
     cache = {} if cache is None else cache
     out = set()
+
+    def tree_of(c):
+        if c not in cache:
+            cache[c] = commit_info(repo, c)
+        return cache[c][0]
+
+    def feature_leaves(lv):
+        got = set()
+        for i in range(lv.n):
+            m = DS_FEATURE.match(lv.path(i))
+            if m:
+                got.add((lv.path(i), m.group(1), lv.oids[i].tobytes().hex()))
+        return got
+
     for c in commits_to_index(repo, start, stop, cache):
         tree, parents = cache[c]
-        if parents:
-            _, lv = repo.odb.walk([cache[parents[0]][0] if parents[0] in cache else commit_info(repo, parents[0])[0],
-                                   tree], "", compare=(0, 1))
-        else:
+        if not parents:
             (lv,) = repo.odb.walk([tree], "")
-        for i in range(lv.n):
-            p = lv.path(i)
-            m = DS_FEATURE.match(p)
-            if m:
-                out.add((m.group(1), lv.oids[i].tobytes().hex()))
+            new = feature_leaves(lv)
+        else:
+            new = None
+            for p in parents:
+                _, lv = repo.odb.walk([tree_of(p), tree], "", compare=(0, 1))
+                changed = feature_leaves(lv)
+                new = changed if new is None else new & changed
+                if not new:
+                    break
+        out.update((d, o) for _, d, o in new)
     return out
 
 
@@ -253,3 +275,91 @@ def read_index(db_path):
     finally:
         db.close()
     return env, commits
+
+
+# ---- clone-time filtering: sf_filter_blob over batches -----------------------------------------
+FEATURE_PATH_MARKERS = ("/.sno-dataset/feature/", "/.table-dataset/feature/")
+SF_MATCH, SF_NOT_MATCHED, SF_ERROR = 0, 1, 2  # spatial_filter.cpp:154-158 (enum match_result)
+
+
+def parse_filter_arg(filter_arg):
+    """sf_init's bounds argument (spatial_filter.cpp:268-285): '<w>,<s>,<e>,<n>' -> 4 floats"""
+    parts = [p for p in str(filter_arg).replace(",", " ").split()]
+    try:
+        rect = [float(p) for p in parts]
+    except ValueError:
+        rect = []
+    if len(rect) != 4:
+        raise ValueError("spatial-filter: Error: invalid bounds, expected '<lng_w>,<lat_s>,<lng_e>,<lat_n>'")
+    return tuple(rect)
+
+
+class CloneFilter:
+    """The git filter extension's per-object decision (sf_filter_blob,
+    vendor/spatial-filter/spatial_filter.cpp:212-260) for batches of objects: feature_envelopes is
+    loaded into HBM once (kd_sf_index_build), then every batch is one kd_sf_filter call.
+
+    ``available`` is False when the repository has no index database: the reference then omits
+    nothing (sf_init, :287-292), and so every object matches."""
+
+    def __init__(self, engine, db_path, filter_arg):
+        self.engine = engine
+        self.q = parse_filter_arg(filter_arg)
+        self._ix = ctypes.c_void_p()
+        self.available = os.path.isfile(db_path)
+        self.n_index = 0
+        if not self.available:
+            return
+        db = sqlite3.connect(f"file:{db_path}?mode=ro", uri=True)
+        try:
+            rows = db.execute("SELECT blob_id, envelope FROM feature_envelopes;").fetchall()
+        finally:
+            db.close()
+        self.n_index = len(rows)
+        nbytes = len(rows[0][1]) if rows else 10
+        if any(len(e) != nbytes for _, e in rows) or any(len(b) != 20 for b, _ in rows):
+            raise ValueError("feature_envelopes: rows of different widths")
+        self.bits = nbytes * 8 // 4  # sf_filter_blob: bits_per_value = num_bytes * 8 / 4
+        oid = np.frombuffer(b"".join(bytes(b) for b, _ in rows), np.uint8) if rows else np.zeros(20, np.uint8)
+        env = np.frombuffer(b"".join(bytes(e) for _, e in rows), np.uint8) if rows else np.zeros(nbytes, np.uint8)
+        N.check(engine.L.kd_sf_index_build(engine.ctx, N.ptr(oid), N.ptr(env), len(rows), self.bits, N.KD_MEM_HOST,
+                                            ctypes.byref(self._ix)), "kd_sf_index_build")
+
+    def close(self):
+        if self._ix:
+            N.check(self.engine.L.kd_sf_index_free(self._ix), "kd_sf_index_free")
+            self._ix = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def feature_paths(paths):
+        """1 where the path is a feature blob's (the only objects the filter may omit)"""
+        return np.fromiter((any(m in p for m in FEATURE_PATH_MARKERS) for p in paths), np.uint8, len(paths))
+
+    def filter(self, oids, paths=None, is_feature=None):
+        """MR codes (SF_MATCH / SF_NOT_MATCHED / SF_ERROR) of objects ``oids`` [m, 20]; ``paths``
+        (their paths in the traversal) or ``is_feature`` flags decide which are feature blobs
+        (neither: all are)"""
+        oids = np.ascontiguousarray(oids, np.uint8).reshape(-1, 20)
+        m = oids.shape[0]
+        if is_feature is None and paths is not None:
+            is_feature = self.feature_paths(paths)
+        if not self.available or m == 0:
+            return np.zeros(m, np.uint8)
+        feat = None if is_feature is None else np.ascontiguousarray(is_feature, np.uint8)
+        out = np.zeros(m, np.uint8)
+        q = (ctypes.c_double * 4)(*self.q)
+        N.check(self.engine.L.kd_sf_filter(self.engine.ctx, self._ix, N.ptr(oids), N.ptr(feat) if feat is not None else None,
+                                           m, q, N.ptr(out), N.KD_MEM_HOST), "kd_sf_filter")
+        return out

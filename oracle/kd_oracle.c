@@ -640,3 +640,25 @@ int64_t kdo_envelope_batch(uint64_t n, const uint8_t* data, const uint64_t* off,
     }
     return npass;
 }
+
+/* sf_filter_blob (vendor/spatial-filter/spatial_filter.cpp:212-260) over a batch of m objects.
+ * The index (feature_envelopes) is given sorted by blob id (memcmp order, as sqlite's primary key
+ * orders BLOBs): idx_oid [n_idx*20], idx_env [n_idx*bits/2].  is_feature [m] may be NULL (all
+ * feature blobs).  out[i]: 0 MR_MATCH (not a feature path :219-223, not in the index :236-238, or
+ * overlapping :249-255), 1 MR_NOT_MATCHED, 2 MR_ERROR (inverted range: the reference aborts). */
+void kdo_sf_filter_batch(uint64_t n_idx, const uint8_t* idx_oid, const uint8_t* idx_env, int bits, uint64_t m,
+                         const uint8_t* oid, const uint8_t* is_feature, const double q[4], uint8_t* out) {
+    int nb = bits / 2;
+    for (uint64_t i = 0; i < m; i++) {
+        out[i] = 0;
+        if (is_feature && !is_feature[i]) continue;
+        uint64_t lo = 0, hi = n_idx;
+        while (lo < hi) {
+            uint64_t mid = lo + (hi - lo) / 2;
+            if (memcmp(idx_oid + 20 * mid, oid + 20 * i, 20) < 0) lo = mid + 1; else hi = mid;
+        }
+        if (lo == n_idx || memcmp(idx_oid + 20 * lo, oid + 20 * i, 20) != 0) continue;
+        int r = kdo_envelope_overlap(idx_env + (uint64_t)nb * lo, bits, q);
+        out[i] = r < 0 ? 2 : (r ? 0 : 1);
+    }
+}

@@ -52,6 +52,8 @@ def C():
         L.kdo_envelope_decode.argtypes = [_vp, ctypes.c_int, _vp]
         L.kdo_envelope_overlap.restype = ctypes.c_int
         L.kdo_envelope_overlap.argtypes = [_vp, ctypes.c_int, _vp]
+        L.kdo_sf_filter_batch.restype = None
+        L.kdo_sf_filter_batch.argtypes = [ctypes.c_uint64, _vp, _vp, ctypes.c_int, ctypes.c_uint64, _vp, _vp, _vp, _vp]
         L.kdo_bbox_intersects.restype = ctypes.c_int
         L.kdo_bbox_intersects.argtypes = [_vp, _vp]
         L.kdo_wrap_lon.restype = ctypes.c_double
@@ -138,6 +140,32 @@ def envelope_batch(data, off, filt_env, bits=20):
     d = data if data.size else np.zeros(1, np.uint8)
     npass = C().kdo_envelope_batch(n, _p(d), _p(off), _p(fe), bits, _p(match), _p(enc), _p(ok))
     return match[:n], enc[:n], ok[:n], int(npass)
+
+
+def envelope_decode(enc, bits=20):
+    """EnvelopeEncoder.decode (kart/spatial_filter/index.py:532-548): encoded bytes -> (w, s, e, n)"""
+    e = np.ascontiguousarray(np.frombuffer(bytes(enc), np.uint8))
+    out = np.zeros(4)
+    C().kdo_envelope_decode(_p(e), bits, _p(out))
+    return tuple(float(x) for x in out)
+
+
+def sf_filter_batch(idx_oid, idx_env, bits, oid, is_feature, q):
+    """sf_filter_blob over a batch (vendor/spatial-filter/spatial_filter.cpp:212-260); the index
+    rows in any order (sorted here by blob id)"""
+    idx_oid = np.ascontiguousarray(idx_oid, np.uint8).reshape(-1, 20)
+    idx_env = np.ascontiguousarray(idx_env, np.uint8).reshape(idx_oid.shape[0], -1)
+    srt = np.argsort(idx_oid.view("S20").reshape(-1), kind="stable")
+    io, ie = np.ascontiguousarray(idx_oid[srt]), np.ascontiguousarray(idx_env[srt])
+    oid = np.ascontiguousarray(oid, np.uint8).reshape(-1, 20)
+    m = oid.shape[0]
+    out = np.zeros(max(m, 1), np.uint8)
+    feat = None if is_feature is None else np.ascontiguousarray(is_feature, np.uint8)
+    pad = np.zeros(20, np.uint8)
+    C().kdo_sf_filter_batch(io.shape[0], _p(io if io.size else pad), _p(ie if ie.size else pad), bits, m,
+                            _p(oid if m else pad), _p(feat) if feat is not None else None,
+                            _p(np.asarray(q, np.float64)), _p(out))
+    return out[:m]
 
 
 def envelope_overlap(enc, bits, q):

@@ -221,3 +221,87 @@ def test_gitrepo_refs_and_dataset_paths(repo):
         assert [e[3] for e in r.ls_tree("c0")] == ["a b", "ds"]
     finally:
         r.close()
+
+
+def test_ref_delta_pack(tmp_path):
+    """a pack written with REF_DELTA bases (repack.useDeltaBaseOffset=false, what older git and
+    some servers send) reads like the OFS_DELTA one"""
+    gitdir = str(tmp_path / "r.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    base = {f"t/{i // 40}/{i:04d}": b"row %d " % i + b"x" * 200 for i in range(400)}
+    commits = []
+    for c in range(12):
+        files = dict(base)
+        for i in range(c * 20, c * 20 + 20):
+            files[f"t/{(i % 400) // 40}/{i % 400:04d}"] = b"row %d edit %d " % (i % 400, c) + b"y" * 200
+        base = files
+        commits.append((f"v{c}", files))
+    _fast_import(gitdir, commits)
+    subprocess.run(["git", "--git-dir", gitdir, "-c", "repack.useDeltaBaseOffset=false", "repack", "-adfq",
+                    "--depth=20", "--window=50"], check=True)
+    packs = [f for f in os.listdir(os.path.join(gitdir, "objects", "pack")) if f.endswith(".pack")]
+    raw = open(os.path.join(gitdir, "objects", "pack", packs[0]), "rb").read()
+    # object type 7 (REF_DELTA) occurs in the pack's entry headers; 6 (OFS_DELTA) does not
+    vp = _git(gitdir, "verify-pack", "-v", os.path.join(gitdir, "objects", "pack", packs[0])).decode()
+    assert "chain length" in vp
+    types = set()
+    for ln in vp.splitlines():
+        parts = ln.split()
+        if len(parts) >= 5 and len(parts[0]) == 40:
+            off = int(parts[4])
+            types.add((raw[off] >> 4) & 7)
+    assert 7 in types and 6 not in types, types
+    db = ObjectDB(gitdir)
+    for spec in ("v0", "v11"):
+        (lv,) = db.walk([_rev(gitdir, spec)], "t")
+        assert _items(lv) == _ls(gitdir, spec, "t")
+        data, off, st = db.read_batch(lv.oids)
+        assert not st.any()
+        for i in (0, lv.n // 2, lv.n - 1):
+            want = _git(gitdir, "cat-file", "blob", lv.oids[i].tobytes().hex())
+            assert data[int(off[i]):int(off[i + 1])].tobytes() == want
+
+
+def test_corrupt_loose_copy_falls_through_to_alternate(tmp_path, repo):
+    """a truncated loose copy in the repository's own object directory does not hide the good copy
+    in an alternate"""
+    alt = str(tmp_path / "alt_src.git")
+    subprocess.run(["git", "init", "-q", "--bare", alt], check=True)
+    blob = b"the good copy " * 100
+    oid = _git(alt, "hash-object", "-w", "--stdin", input=blob).decode().strip()
+    gitdir = str(tmp_path / "main.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    with open(os.path.join(gitdir, "objects", "info", "alternates"), "w") as f:
+        f.write(os.path.join(alt, "objects") + "\n")
+    good = open(os.path.join(alt, "objects", oid[:2], oid[2:]), "rb").read()
+    os.makedirs(os.path.join(gitdir, "objects", oid[:2]), exist_ok=True)
+    with open(os.path.join(gitdir, "objects", oid[:2], oid[2:]), "wb") as f:
+        f.write(good[: len(good) // 2])
+    db = ObjectDB(gitdir)
+    assert db.read(oid) == (3, blob)
+    data, off, st = db.read_batch(np.frombuffer(bytes.fromhex(oid), np.uint8))
+    assert st.tolist() == [0] and data.tobytes() == blob
+
+
+def test_refresh_only_when_packs_change(tmp_path):
+    """a miss with an unchanged pack set does not reopen the store (promised blobs miss on every
+    read); a pack written after the open is picked up by the next miss"""
+    from kart_amd.gitsource import EOBJECTMISSING, GitRepo
+
+    gitdir = str(tmp_path / "p.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    _fast_import(gitdir, [("a", {"x/one": b"one"})])
+    r = GitRepo(gitdir)
+    try:
+        h = r.odb.n_opens
+        with pytest.raises(KeyError) as ei:
+            r.cat("3" * 40)
+        assert ei.value.subcode == EOBJECTMISSING
+        assert r.odb.n_opens == h  # not reopened
+        _fast_import(gitdir, [("b", {"x/two": b"two, in a new pack"})])
+        _git(gitdir, "repack", "-adq")  # small imports land loose: put everything in a new pack
+        oid = _git(gitdir, "rev-parse", "b:x/two").decode().strip()
+        assert r.cat(oid) == b"two, in a new pack"
+        assert r.odb.n_opens == h + 1
+    finally:
+        r.close()

@@ -1,0 +1,202 @@
+"""Clone-time spatial filter over batches: sf_filter_blob (vendor/spatial-filter/spatial_filter.cpp:
+212-260) as kd_sf_index_build + kd_sf_filter (kart_amd.spatial_index.CloneFilter).
+
+CPU: the C oracle's batch equals a direct Python restatement of the reference function (dict lookup
+standing in for the sqlite primary-key query, EnvelopeEncoder.decode, range_overlaps /
+cyclic_range_overlaps) on crafted envelopes — antimeridian-wrapped, zero-width, shared edges — and
+the bounds parser follows sf_init.  GPU: the kernel equals the oracle bit for bit on the points
+history index (pinned to the reference's own index summary in test_spatial_index) and on 2M-row
+synthetic indexes with 64-bit-prefix collisions, absent ids and non-feature paths."""
+import numpy as np
+import pytest
+
+from kart_amd import spatial_index as SI
+from oracle import oracle as O
+
+
+def _range_overlaps(a1, a2, b1, b2):  # spatial_filter.cpp:170-185
+    if a1 > a2 or b1 > b2:
+        raise ValueError("Ranges don't make sense")  # the reference aborts
+    if b1 < a1:
+        return b2 > a1
+    if a1 < b1:
+        return a2 > b1
+    return b2 != b1 and a2 != a1
+
+
+def _cyclic_range_overlaps(a1, a2, b1, b2):  # :187-208
+    if a1 > a2:
+        a2 += 360
+    if b1 > b2:
+        b2 += 360
+    if _range_overlaps(a1, a2, b1, b2):
+        return True
+    if a1 < b1:
+        a1 += 360
+        a2 += 360
+    else:
+        b1 += 360
+        b2 += 360
+    return _range_overlaps(a1, a2, b1, b2)
+
+
+def _decode(enc, bits):  # EnvelopeEncoder::decode / kart/spatial_filter/index.py:532-548
+    vmax = 2 ** bits - 1
+    x = int.from_bytes(bytes(enc), "big")
+    n = (x & vmax) / vmax * 180 - 90
+    x >>= bits
+    e = (x & vmax) / vmax * 360 - 180
+    x >>= bits
+    s = (x & vmax) / vmax * 180 - 90
+    x >>= bits
+    w = (x & vmax) / vmax * 360 - 180
+    return w, s, e, n
+
+
+def py_sf_filter_blob(index, oid, is_feature, q, bits):
+    """sf_filter_blob restated: 0 MR_MATCH, 1 MR_NOT_MATCHED, 2 MR_ERROR"""
+    if not is_feature:
+        return 0
+    enc = index.get(bytes(oid))
+    if enc is None:
+        return 0
+    w, s, e, n = _decode(enc, bits)
+    try:
+        ok = _cyclic_range_overlaps(w, e, q[0], q[2]) and _range_overlaps(s, n, q[1], q[3])
+    except ValueError:
+        return 2
+    return 0 if ok else 1
+
+
+def _encode(wsen, bits=20):
+    out = np.zeros(bits // 2, np.uint8)
+    assert O.C().kdo_envelope_encode(O._p(np.asarray(wsen, np.float64)), bits, O._p(out)) == 0
+    return out
+
+
+CRAFTED = [(170.0, -10.0, -170.0, 10.0),  # wraps the antimeridian
+           (-180.0, -90.0, 180.0, 90.0), (10.0, 10.0, 10.0, 10.0),  # everything; a point
+           (175.0, -40.0, 178.0, -35.0), (-178.0, -42.0, -176.0, -40.0), (0.0, 0.0, 5.0, 5.0),
+           (5.0, 5.0, 9.0, 9.0), (-5.0, -5.0, 0.0, 0.0), (179.999, 0.0, -179.999, 1.0)]
+QUERIES = [(170.0, -45.0, 180.0, -30.0), (175.0, -50.0, -175.0, 0.0),  # NZ; across the antimeridian
+           (0.0, 0.0, 5.0, 5.0), (5.0, 5.0, 5.0, 5.0), (-180.0, -90.0, 180.0, 90.0), (10.0, 10.0, 10.0, 10.0)]
+
+
+def _synthetic(rng, n_idx, m, crafted=True, collide=64):
+    idx = rng.integers(0, 256, size=(n_idx, 20), dtype=np.uint8)
+    if collide:  # index rows sharing their first 8 bytes with another row (equal 64-bit prefixes)
+        src = rng.choice(n_idx, size=collide, replace=False)
+        dst = rng.choice(n_idx, size=collide, replace=False)
+        idx[dst, :8] = idx[src, :8]
+    idx = np.unique(idx.view("S20").reshape(-1)).view(np.uint8).reshape(-1, 20)
+    idx = idx[rng.permutation(idx.shape[0])]
+    n_idx = idx.shape[0]
+    w = rng.uniform(-180, 180, n_idx)
+    s = rng.uniform(-90, 80, n_idx)
+    wd = np.exp(rng.uniform(np.log(1e-6), np.log(30), n_idx))
+    e = ((w + wd + 180) % 360) - 180  # some wrap past 180
+    nn = np.minimum(s + rng.uniform(0, 10, n_idx), 90)
+    env = np.stack([_encode((float(a), float(b), float(c), float(d))) for a, b, c, d in zip(w, s, e, nn)]) \
+        if n_idx <= 4000 else None
+    if env is None:  # vectorised encode (the same floor / ceil formula as the oracle's encoder)
+        vmax = float(2 ** 20 - 1)
+        q = [np.floor((w + 180) / 360 * vmax), np.floor((s + 90) / 180 * vmax),
+             np.ceil((e + 180) / 360 * vmax), np.ceil((nn + 90) / 180 * vmax)]
+        big = [int(a) << 60 | int(b) << 40 | int(c) << 20 | int(d) for a, b, c, d in zip(*q)]
+        env = np.frombuffer(b"".join(v.to_bytes(10, "big") for v in big), np.uint8).reshape(n_idx, 10).copy()
+    if crafted:
+        k = min(len(CRAFTED), n_idx)
+        env[:k] = np.stack([_encode(c) for c in CRAFTED[:k]])
+    # queries: index members (some with a flipped last byte: absent, same prefix), random absents
+    take = rng.integers(0, n_idx, size=m)
+    qo = idx[take].copy()
+    flip = rng.random(m) < 0.2
+    qo[flip, 19] ^= 0x5A
+    fresh = rng.random(m) < 0.1
+    qo[fresh] = rng.integers(0, 256, size=(int(fresh.sum()), 20), dtype=np.uint8)
+    feat = (rng.random(m) > 0.05).astype(np.uint8)
+    return idx, env, qo, feat
+
+
+def test_oracle_sf_filter_equals_reference_restatement():
+    rng = np.random.default_rng(5)
+    idx, env, qo, feat = _synthetic(rng, 3000, 5000)
+    index = {bytes(o): bytes(e) for o, e in zip(idx, env)}
+    for q in QUERIES:
+        got = O.sf_filter_batch(idx, env, 20, qo, feat, q)
+        want = [py_sf_filter_blob(index, o, f, q, 20) for o, f in zip(qo, feat)]
+        assert got.tolist() == want
+        assert O.sf_filter_batch(idx, env, 20, qo, None, q).tolist() == \
+            [py_sf_filter_blob(index, o, 1, q, 20) for o in qo]
+    # crafted rows against the crafted queries: both outcomes occur
+    got = O.sf_filter_batch(idx, env, 20, idx[:len(CRAFTED)], None, QUERIES[1])
+    assert set(got.tolist()) == {0, 1}
+
+
+def test_parse_filter_arg():
+    assert SI.parse_filter_arg("174.5,-41.5,175,-41") == (174.5, -41.5, 175.0, -41.0)
+    assert SI.parse_filter_arg("1 2 3 4") == (1.0, 2.0, 3.0, 4.0)
+    for bad in ("1,2,3", "1,2,3,4,5", "a,b,c,d", ""):
+        with pytest.raises(ValueError):
+            SI.parse_filter_arg(bad)
+    assert SI.CloneFilter.feature_paths(["nz/.table-dataset/feature/A/A/A/A/kQ==", "nz/.table-dataset/meta/schema.json",
+                                         "x/.sno-dataset/feature/a/b", ".kart.repostructure.version"]).tolist() == [1, 0, 1, 0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_idx,m", [(1, 10), (3000, 5000), (2_000_000, 3_000_000)])
+def test_gpu_sf_filter_vs_oracle(engine, tmp_path, n_idx, m):
+    import sqlite3
+
+    rng = np.random.default_rng(n_idx)
+    idx, env, qo, feat = _synthetic(rng, n_idx, m, collide=64 if n_idx > 100 else 0)
+    db = str(tmp_path / "fe.db")
+    con = sqlite3.connect(db)
+    con.execute("CREATE TABLE feature_envelopes (blob_id BLOB NOT NULL PRIMARY KEY, envelope BLOB NOT NULL) WITHOUT ROWID;")
+    con.executemany("INSERT INTO feature_envelopes VALUES (?, ?);", ((o.tobytes(), e.tobytes()) for o, e in zip(idx, env)))
+    con.commit()
+    con.close()
+    for q in QUERIES[:3]:
+        with SI.CloneFilter(engine, db, ",".join(map(str, q))) as cf:
+            assert cf.n_index == idx.shape[0] and cf.bits == 20
+            got = cf.filter(qo, is_feature=feat)
+            want = O.sf_filter_batch(idx, env, 20, qo, feat, q)
+            assert np.array_equal(got, want)
+            assert 0 < np.count_nonzero(got == 1) < m or n_idx == 1
+            assert np.array_equal(cf.filter(qo), O.sf_filter_batch(idx, env, 20, qo, None, q))
+    # no index database: nothing is omitted (sf_init's warning path)
+    cf = SI.CloneFilter(engine, str(tmp_path / "absent.db"), "0,0,1,1")
+    assert not cf.available and not cf.filter(qo).any()
+
+
+@pytest.mark.gpu
+def test_gpu_sf_filter_points_history(engine, tmp_path):
+    """the points history index (update_spatial_filter_index on the GPU, pinned to the reference's
+    index summary in test_spatial_index) queried with every object of the history plus non-feature
+    paths: equal to the oracle; a Wellington-region filter omits most features"""
+    from fixtures import load
+    from kart_amd.gitsource import GitRepo
+    from test_spatial_index import _git, _history_repo, _revlist_blobs
+
+    fx = load("repo_points")
+    gitdir = _history_repo(tmp_path, fx, ["head1", "head"])
+    repo = GitRepo(gitdir)
+    db = str(tmp_path / "env.db")
+    try:
+        SI.update_spatial_filter_index(engine, repo, ["main"], db)
+        env, _ = SI.read_index(db)
+        c1 = _git(gitdir, "rev-parse", "main").strip()
+        objs = sorted({o for _, o in _revlist_blobs(gitdir, [c1], [])})
+        oids = np.frombuffer(b"".join(bytes.fromhex(o) for o in objs), np.uint8).reshape(-1, 20)
+        paths = [f"{fx.meta['ds_path']}/.table-dataset/feature/x"] * len(objs)
+        paths[:3] = [f"{fx.meta['ds_path']}/.table-dataset/meta/schema.json"] * 3
+        io = np.frombuffer(b"".join(bytes.fromhex(o) for o in env), np.uint8).reshape(-1, 20)
+        ie = np.frombuffer(b"".join(env.values()), np.uint8).reshape(-1, 10)
+        q = (174.6, -41.5, 175.2, -40.8)
+        with SI.CloneFilter(engine, db, ",".join(map(str, q))) as cf:
+            got = cf.filter(oids, paths=paths)
+        want = O.sf_filter_batch(io, ie, 20, oids, SI.CloneFilter.feature_paths(paths), q)
+        assert np.array_equal(got, want)
+        assert (got[:3] == 0).all() and np.count_nonzero(got == 1) > len(objs) // 2
+    finally:
+        repo.close()

@@ -47,6 +47,51 @@ def _history_repo(tmp_path, fx, keys, crs_name="EPSG:4326.wkt", crs=WGS84):
     return gitdir
 
 
+# tests/test_spatial_filter_index.py:39-66 (EXPECTED_POINTS_INDEX): the reference's index of the
+# points repository (HEAD^ then HEAD) -- blob ids and decoded envelopes of its extreme entries
+EXPECTED_POINTS_INDEX = {
+    "features": 2148,
+    "first_blob_id": ("0075ca2608a7ea5a8883123d4767eb0056dc9fbe", (174.37455885, -35.81883419, 174.37455885, -35.81883419)),
+    "last_blob_id": ("ffefdaa2170c33397e147d9c521dbd0e83362cfc", (174.51729394, -38.89953452, 174.51729394, -38.89953452)),
+    "westernmost": ("ea098c7b7bbbb57d5069bbfefe332300bc5af316", (170.61676942, -45.73477461, 170.61676942, -45.73477461)),
+    "southernmost": ("ea098c7b7bbbb57d5069bbfefe332300bc5af316", (170.61676942, -45.73477461, 170.61676942, -45.73477461)),
+    "easternmost": ("6523dde7f3b2172c6090563d9e99b32918703017", (178.43023198, -37.64119695, 178.43023198, -37.64119695)),
+    "northernmost": ("81e591a2e7c4985e2b82b6ef3e74a3a1b298e472", (172.99773191, -34.40609417, 172.99773191, -34.40609417)),
+}
+
+
+def index_summary(env, unwrap_lon=-180.0):
+    """_get_index_summary (tests/test_spatial_filter_index.py:332-387): the first strictly-better
+    entry per score over the index rows, envelopes decoded by EnvelopeEncoder.decode"""
+    scores = {
+        "first_blob_id": lambda b, e: -int(b, 16),
+        "last_blob_id": lambda b, e: int(b, 16),
+        "westernmost": lambda b, e: -(e[0] + 360 if e[0] < unwrap_lon else e[0]),
+        "southernmost": lambda b, e: -e[1],
+        "easternmost": lambda b, e: e[2] + 360 if e[2] < unwrap_lon else e[2],
+        "northernmost": lambda b, e: e[3],
+    }
+    best = {k: (-float("inf"), None) for k in scores}
+    for blob_id, enc in env.items():
+        e = O.envelope_decode(enc, 20)
+        for k, f in scores.items():
+            sc = f(blob_id, e)
+            if sc > best[k][0]:
+                best[k] = (sc, (blob_id, e))
+    return {"features": len(env), **{k: v[1] for k, v in best.items()}}
+
+
+def check_index(actual, expected, abs_=1e-3):
+    """_check_index / _check_envelope (:166-189): same blob ids, envelopes within abs_ and never
+    smaller than the original"""
+    assert actual["features"] == expected["features"]
+    for k, (blob_id, want) in ((k, v) for k, v in expected.items() if k != "features"):
+        got_id, got = actual[k]
+        assert got_id == blob_id, k
+        assert got == pytest.approx(want, abs=abs_), k
+        assert got[0] <= want[0] and got[1] <= want[1] and got[2] >= want[2] and got[3] >= want[3], k
+
+
 def _git(gitdir, *a):
     return subprocess.run(["git", "--git-dir", gitdir, *a], capture_output=True, check=True).stdout.decode()
 
@@ -94,6 +139,7 @@ def test_gpu_index_history_and_incremental(engine, tmp_path):
         r0 = SI.update_spatial_filter_index(engine, repo, [c0], db)
         env0, commits0 = SI.read_index(db)
         assert commits0 == {c0} and r0["commits"] == 1 and r0["features"] == len(env0)
+        assert len(env0) == 2143  # test_index_points_commit_by_commit (:236-242): HEAD^ alone
         r1 = SI.update_spatial_filter_index(engine, repo, ["main"], db)
         env, commits = SI.read_index(db)
         assert commits == {c1} and r1["commits"] == 1  # the second run walks only the new commit
@@ -113,10 +159,46 @@ def test_gpu_index_history_and_incremental(engine, tmp_path):
         data, off = _arena(geoms)
         _, oenc, ok, _ = O.envelope_batch(data, off, SI.WORLD, 20)
         want = {o: oenc[i].tobytes() for i, o in enumerate(blobs) if ok[i]}
-        assert env == want and len(env) > 2000
+        assert env == want
+        # pinned to the reference's own index of this history (:225-248)
+        check_index(index_summary(env), EXPECTED_POINTS_INDEX)
         # a dataset in another CRS is skipped, not mis-indexed
         gd2 = _history_repo(tmp_path / "b", fx, ["head1"], "EPSG:2193.wkt", b'PROJCS["NZTM",AUTHORITY["EPSG","2193"]]')
         r = SI.update_spatial_filter_index(engine, GitRepo(gd2), ["main"], str(tmp_path / "b.db"))
         assert r["features"] == 0 and "non-identity" in r["skipped"][fx.meta["ds_path"]]
+    finally:
+        repo.close()
+
+
+def _oracle_index(repo, fx, blobs):
+    """{blob id: EnvelopeEncoder bytes} of the given feature blobs by the CPU oracle"""
+    import msgpack
+
+    from test_oracle_golden import _arena
+
+    geoms = []
+    gcol = fx.schema("head").geometry_columns[0].id
+    for o in blobs:
+        lh, vals = msgpack.unpackb(repo.cat(o), raw=False, ext_hook=lambda c, d: d)
+        geoms.append(vals[fx.legends[lh].non_pk_columns.index(gcol)] or b"")
+    data, off = _arena(geoms)
+    _, oenc, ok, _ = O.envelope_batch(data, off, SI.WORLD, 20)
+    return {o: oenc[i].tobytes() for i, o in enumerate(blobs) if ok[i]}
+
+
+def test_oracle_index_pinned_to_reference(tmp_path):
+    """the oracle's index envelopes of the points history equal the reference's own index
+    summary (tests/test_spatial_filter_index.py:39-66,225-248): 2143 features after HEAD^, 2148
+    after HEAD, the same extreme blob ids and envelopes"""
+    fx = load("repo_points")
+    gitdir = _history_repo(tmp_path, fx, ["head1", "head"])
+    repo = GitRepo(gitdir)
+    try:
+        c1 = _git(gitdir, "rev-parse", "main").strip()
+        c0 = _git(gitdir, "rev-parse", "main~1").strip()
+        env0 = _oracle_index(repo, fx, sorted({o for _, o in _revlist_blobs(gitdir, [c0], [])}))
+        assert len(env0) == 2143
+        env = _oracle_index(repo, fx, sorted({o for _, o in _revlist_blobs(gitdir, [c1], [])}))
+        check_index(index_summary(env), EXPECTED_POINTS_INDEX)
     finally:
         repo.close()
