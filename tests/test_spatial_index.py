@@ -202,3 +202,52 @@ def test_oracle_index_pinned_to_reference(tmp_path):
         check_index(index_summary(env), EXPECTED_POINTS_INDEX)
     finally:
         repo.close()
+
+
+def test_feature_oids_merge_commit_equal_rev_list(tmp_path):
+    """a merge commit: the blobs it takes from either parent are not new (iter_feature_oids prunes
+    against every parent), so with either branch already indexed the blob set still equals
+    `git rev-list --objects START --not STOP`"""
+    from test_odb import _fast_import
+
+    gitdir = str(tmp_path / "m.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    feat = "nz/.table-dataset/feature"
+    base = {f"{feat}/A/A/{i:03d}": b"feature %d" % i for i in range(60)}
+    base["nz/.table-dataset/meta/schema.json"] = b"[]"
+    a = dict(base, **{f"{feat}/A/A/001": b"edited on a", f"{feat}/A/A/002": b"edited on a too"})
+    b = dict(base, **{f"{feat}/A/A/050": b"edited on b"})
+    _fast_import(gitdir, [("c0", base)])
+    merged = dict(a, **{f"{feat}/A/A/050": b"edited on b"})
+    env = dict(os.environ, GIT_DIR=gitdir)
+    # a and b on top of c0, the merge on top of both
+    c0 = _git(gitdir, "rev-parse", "c0").strip()
+
+    def commit(tree_files, parents, msg):
+        idx = str(tmp_path / f"idx_{msg}")
+        e = dict(env, GIT_INDEX_FILE=idx)
+        info = b""
+        for p, d in tree_files.items():
+            oid = subprocess.run(["git", "hash-object", "-w", "--stdin"], input=d, env=e, capture_output=True,
+                                 check=True).stdout.decode().strip()
+            info += b"100644 %s\t%s\0" % (oid.encode(), p.encode())
+        subprocess.run(["git", "update-index", "-z", "--index-info"], input=info, env=e, check=True)
+        tree = subprocess.run(["git", "write-tree"], env=e, capture_output=True, check=True).stdout.decode().strip()
+        args = ["git", "commit-tree", tree, "-m", msg]
+        for p in parents:
+            args += ["-p", p]
+        return subprocess.run(args, env=dict(e, GIT_AUTHOR_NAME="t", GIT_AUTHOR_EMAIL="t@t", GIT_COMMITTER_NAME="t",
+                                             GIT_COMMITTER_EMAIL="t@t"), capture_output=True,
+                              check=True).stdout.decode().strip()
+
+    ca = commit(a, [c0], "a")
+    cb = commit(b, [c0], "b")
+    cm = commit(merged, [ca, cb], "merge")
+    repo = GitRepo(gitdir)
+    try:
+        for stop in ([], [ca], [cb], [c0]):
+            got = SI.iter_feature_oids(repo, {cm}, set(stop))
+            assert got == _revlist_blobs(gitdir, [cm], stop), stop
+        assert len(SI.iter_feature_oids(repo, {cm}, {cb})) == 2  # a's two edits, not b's
+    finally:
+        repo.close()
