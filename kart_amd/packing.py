@@ -13,6 +13,7 @@ become SoA arrays in join-key order (DESIGN.md "join key"):
 
 Packing runs on the CPU in the native library (kd_pack_*), multithreaded.
 """
+import time
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -75,6 +76,7 @@ class PackedSide:
     name_off: Optional[np.ndarray] = None  # uint64 [n+1]
     encoding: PathEncoding = field(default_factory=lambda: INT_PK_ENCODING)
     dev: Optional[tuple] = None  # (key, oid) DevBufs when the side was packed on the GPU
+    timing: Optional[dict] = None  # pack_side's stage times (parse_s, sort_s, sort_on)
 
     @property
     def n(self):
@@ -159,7 +161,9 @@ def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None, engine=None
         paths, off = np.ascontiguousarray(rel_paths, np.uint8), np.ascontiguousarray(rel_off, np.uint64)
     n = len(off) - 1
     oids = np.ascontiguousarray(oids, np.uint8).reshape(n, 20)
+    t0 = time.perf_counter()
     keys = parse_keys(paths, off, encoding)
+    t1 = time.perf_counter()
     dev = None
     if engine is not None:
         dk, do, dord = sort_on_device(engine, keys, oids)
@@ -176,6 +180,7 @@ def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None, engine=None
     side = PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(sorted_oids),
                       key_mode=encoding.key_mode, order=order.astype(np.int64), encoding=encoding)
     side.dev = dev
+    side.timing = {"parse_s": t1 - t0, "sort_s": time.perf_counter() - t1, "sort_on": "gpu" if dev else "host"}
     if encoding.key_mode == N.KD_KEY_HASH:
         # sorted relative-path arena (needed for collision verification + pk decode)
         lens = (off[1:] - off[:-1])[order]

@@ -8,6 +8,7 @@ EPSG:4326), a second commit with 1 % updates / deletes / inserts.  Prints one JS
 usage: python scripts/e2e_repo_bench.py [--n 1000000] [--out FILE]   (GPU needed for the diff)
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -26,6 +27,93 @@ DS = "nz_points"
 REFERENCE_RATE = 0.54e6  # the reference diff hot path, feature pairs / s, 1 core
 
 
+def _import_blobs(args):
+    """one worker: write a chunk of blobs with its own `git fast-import` (one pack) and return their
+    object ids (sha1 of the loose-object header + content, as git names them)"""
+    gitdir, data, off = args
+    n = off.shape[0] - 1
+    raw = data.tobytes()
+    ids = bytearray(20 * n)
+    parts = []
+    for i in range(n):
+        b = raw[int(off[i]):int(off[i + 1])]
+        ids[20 * i:20 * i + 20] = hashlib.sha1(b"blob %d\0" % len(b) + b).digest()
+        parts.append(b"blob\ndata %d\n%s\n" % (len(b), b))
+    subprocess.run(["git", "-c", "fastimport.unpackLimit=0", "fast-import", "--quiet"], input=b"".join(parts),
+                   env=dict(os.environ, GIT_DIR=gitdir), check=True)
+    return bytes(ids)
+
+
+def _blob_ids(gitdir, data, off, procs):
+    """all blobs of the arena into the repository, `procs` fast-imports in parallel"""
+    from multiprocessing import Pool
+
+    n = off.shape[0] - 1
+    cuts = np.linspace(0, n, procs + 1).astype(np.int64)
+    jobs = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        lo, hi = int(off[a]), int(off[b])
+        jobs.append((gitdir, data[lo:hi], (off[a:b + 1] - np.uint64(lo)).astype(np.uint64)))
+    with Pool(procs) as pool:
+        ids = pool.map(_import_blobs, jobs)
+    return np.frombuffer(b"".join(ids), np.uint8).reshape(n, 20)
+
+
+def build_parallel(gitdir, n, seed=3, procs=16):
+    """the same repository as build(), with the blobs written by parallel fast-imports (packs of
+    blobs) and the two commits by one fast-import referencing them by id: for 10M features"""
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    legend = Legend(["c-fid"], [c["id"] for c in synth.POINT_SCHEMA[1:]])
+    lh = legend.hexhash()
+    rng = np.random.default_rng(seed)
+    pks = np.arange(1, n + 1, dtype=np.int64)
+    perm = rng.permutation(n)
+    k = n // 100
+    upd, dele = np.sort(perm[:k]), np.sort(perm[k:2 * k])
+    ins = np.arange(n + 1, n + 1 + k, dtype=np.int64)
+    inner = f"{DS}/.table-dataset"
+    meta = _meta(inner, lh, legend)
+    t0 = time.perf_counter()
+    feats = []
+    for p, ver in ((pks, 0), (pks[upd], 1), (ins, 2)):
+        data, boff = synth.point_blobs(p, np.full(p.shape[0], ver, np.uint64), lh)
+        feats.append((p, _blob_ids(gitdir, data, boff, procs)))
+        print(f"  blobs of version {ver}: {p.shape[0]} in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+
+    def m_lines(p, ids):
+        arena, off = synth.int_pk_paths(p)
+        hexes = ids.tobytes().hex()
+        pre = f"M 100644 ".encode()
+        return [pre + hexes[40 * i:40 * i + 40].encode() + b" %s/feature/%s\n" % (
+            inner.encode(), arena[int(off[i]):int(off[i + 1])].tobytes()) for i in range(p.shape[0])]
+
+    lines = [b"commit refs/heads/main\ncommitter t <t@t> 1600000000 +0000\ndata 1\nx\n"]
+    for path, d in meta.items():
+        lines.append(b"M 100644 inline %s\ndata %d\n%s\n" % (path.encode(), len(d), d))
+    lines += m_lines(*feats[0])
+    lines.append(b"\ncommit refs/heads/main\ncommitter t <t@t> 1600000001 +0000\ndata 1\ny\n")
+    lines += m_lines(*feats[1])
+    lines += m_lines(*feats[2])
+    arena, off = synth.int_pk_paths(pks[dele])
+    for i in range(k):
+        lines.append(b"D %s/feature/%s\n" % (inner.encode(), arena[int(off[i]):int(off[i + 1])].tobytes()))
+    lines.append(b"\n")
+    print(f"  tree stream built in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
+                   check=True)
+    print(f"  commits written in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    return k
+
+
+def _meta(inner, lh, legend):
+    return {f"{inner}/meta/schema.json": json.dumps(synth.POINT_SCHEMA).encode(),
+            f"{inner}/meta/path-structure.json": json.dumps(
+                {"scheme": "int", "branches": 64, "levels": 4, "encoding": "base64"}).encode(),
+            f"{inner}/meta/legend/{lh}": legend.dumps(),
+            f"{inner}/meta/crs/EPSG:4326.wkt": b'GEOGCS["WGS 84",AUTHORITY["EPSG","4326"]]',
+            ".kart.repostructure.version": b"3\n"}
+
+
 def build(gitdir, n, seed=3):
     subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
     legend = Legend(["c-fid"], [c["id"] for c in synth.POINT_SCHEMA[1:]])
@@ -37,12 +125,7 @@ def build(gitdir, n, seed=3):
     upd, dele = np.sort(perm[:k]), np.sort(perm[k:2 * k])
     ins = np.arange(n + 1, n + 1 + k, dtype=np.int64)
     inner = f"{DS}/.table-dataset"
-    meta = {f"{inner}/meta/schema.json": json.dumps(synth.POINT_SCHEMA).encode(),
-            f"{inner}/meta/path-structure.json": json.dumps(
-                {"scheme": "int", "branches": 64, "levels": 4, "encoding": "base64"}).encode(),
-            f"{inner}/meta/legend/{lh}": legend.dumps(),
-            f"{inner}/meta/crs/EPSG:4326.wkt": b'GEOGCS["WGS 84",AUTHORITY["EPSG","4326"]]',
-            ".kart.repostructure.version": b"3\n"}
+    meta = _meta(inner, lh, legend)
 
     def feature_lines(p, ver):
         arena, off = synth.int_pk_paths(p)
@@ -81,11 +164,12 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--repo", default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--procs", type=int, default=16, help="parallel blob writers when building the repository")
     a = ap.parse_args()
     gitdir = a.repo or f"/tmp/kart_e2e_{a.n}.git"
     if not os.path.isdir(gitdir):
-        t, k = timed(lambda: build(gitdir, a.n))
-        print(f"built {gitdir} in {t:.1f} s", file=sys.stderr)
+        t, k = timed(lambda: build_parallel(gitdir, a.n, procs=a.procs))
+        print(f"built {gitdir} in {t:.1f} s", file=sys.stderr, flush=True)
     from kart_amd import dataset as D
     from kart_amd.engine import Engine
     from kart_amd.gitsource import GitRepo
@@ -108,8 +192,11 @@ def main():
             else:
                 t, (old, new) = timed(lambda: (repo.dataset_version("main^", DS), repo.dataset_version("main", DS)))
             stages["walk_s"] = t
-            t, _ = timed(lambda: (old.packed, new.packed))
+            t, (pa, pb) = timed(lambda: (old.pack(eng), new.pack(eng)))
             stages["pack_s"] = t
+            stages["pack_parse_s"] = pa.timing["parse_s"] + pb.timing["parse_s"]
+            stages["pack_sort_s"] = pa.timing["sort_s"] + pb.timing["sort_s"]
+            stages["sort_on"] = pa.timing["sort_on"]
             t, ds = timed(lambda: D.get_dataset_diff(eng, old, new))
             stages["diff_s"] = t
             fd = ds["feature"]
@@ -120,7 +207,8 @@ def main():
             assert sum(counts.values()) == n_git, (counts, n_git)
             assert all(d.changed_fields for d in fd.values() if d.type == "update")
             repo.close()
-            res[label] = {**{k: round(v, 4) for k, v in stages.items()}, "total_s": round(total, 4),
+            res[label] = {**{k: round(v, 4) if isinstance(v, float) else v for k, v in stages.items()},
+                          "total_s": round(total, 4),
                           "counts": counts, "leaves": [int(old.n), int(new.n)],
                           "speedup_vs_reference_path": round(res["reference_path_s_estimate"] / total, 1)}
     s = json.dumps(res, indent=1)
