@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "c5env", "c6"])
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3v", "c4", "c5", "c5env", "c6"])
+    ap.add_argument("--same-len", type=float, default=0.6,
+                    help="c3v: fraction of features whose geometry edits keep the blob length (vertex moves)")
     ap.add_argument("--n", type=int, default=0,
                     help="units (c3: polygons of the whole layer, 100M; c2: points per GPU, 10M; c4: rows, 50M; "
                          "c5: features of the filtered layer, 100M; c5env/c6: geometries, 20M)")
@@ -73,7 +75,7 @@ def parse():
                          "so the events do not inflate the step time)")
     a = ap.parse_args()
     if not a.n:
-        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c4": 50_000_000, "c5": 100_000_000, "c5env": 20_000_000,
+        a.n = {"c2": 10_000_000, "c3": 100_000_000, "c3v": 100_000_000, "c4": 50_000_000, "c5": 100_000_000, "c5env": 20_000_000,
                "c6": 20_000_000}[a.workload]
     if a.traffic_json is None:
         a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
@@ -207,7 +209,7 @@ def run_diff(args, H, polygons):
     if polygons:
         n_pks = n + n // 100
         lo, hi = synth.shard_pk_range(rank, world, n_pks) if split else (0, n_pks)
-        L = synth.polygons_layer(n, lo=lo, hi=hi)
+        L = synth.polygons_layer(n, lo=lo, hi=hi, same_len=args.same_len if args.workload == "c3v" else 0.0)
     else:
         L = synth.points_layer(n, seed=synth.SEED + rank, pk0=shard.rank_pk_base(rank, n))
     gen_s = time.time() - t0
@@ -310,7 +312,9 @@ def run_diff(args, H, polygons):
         host = host_timing(eng, L, h2d_s, h2d_bytes)
     eng.close()
     wl = (f"C3: ONE {n}-polygon int-PK layer{f' split into {world} bucket-range shards' if split else ''}, 10% edits "
-          "(4% geometry + 4% attribute updates, 1% del, 1% ins), two-commit diff + field diff") if polygons else \
+          "(4% geometry + 4% attribute updates, 1% del, 1% ins), two-commit diff + field diff" +
+          (f"; geometry edits keep the blob length for {args.same_len:.0%} of features (vertex moves)"
+           if args.workload == "c3v" else "")) if polygons else \
         f"C2: {n}-point int-PK layer per GPU, 1% upd/del/ins, two-commit diff + field diff"
     out = {
         "metric": METRIC,
@@ -886,6 +890,7 @@ def main():
     args = parse()
     H = Harness()
     out = {"c2": lambda a, h: run_diff(a, h, polygons=False), "c3": lambda a, h: run_diff(a, h, polygons=True),
+           "c3v": lambda a, h: run_diff(a, h, polygons=True),
            "c4": run_c4, "c5": run_c5, "c5env": run_c5env, "c6": run_c6}[args.workload](args, H)
     if H.rank == 0:
         print(json.dumps(out), flush=True)

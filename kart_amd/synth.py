@@ -178,20 +178,26 @@ def points_layer(n, frac_update=0.01, frac_delete=0.01, frac_insert=0.01, seed=S
     return Layer(base, target, bb, tb, schema, {lh: legend}, n_ins, n_upd, n_del)
 
 
-def polygon_blobs(pk, gver, aver, legend_hex, rng_seed=SEED):
+def polygon_blobs(pk, gver, aver, legend_hex, rng_seed=SEED, same_len=0.0):
     """Polygons-layer feature blobs (the shape of tests/data/polygons: 245-582 B).
 
     values = [geom MULTIPOLYGON (ext 'G': 8-B GPKG header, XY envelope, one ring of 5-24 points),
               date_adjusted str (20-char timestamp), survey_reference str|None, adjusted_nodes int32].
     The geometry is a function of (pk, gver), the attributes of (pk, aver), so a geometry edit and an
-    attribute edit change different fields.  Canonical (smallest-width) msgpack headers throughout."""
+    attribute edit change different fields.  Canonical (smallest-width) msgpack headers throughout.
+    ``same_len``: the fraction of features (by a hash of the pk) whose ring size depends on the pk
+    only, so a geometry edit moves vertices and keeps the blob's length (0: every edit redraws it)."""
     pk = np.asarray(pk, np.int64)
     n = pk.shape[0]
     u = pk.view(np.uint64)
     hg = splitmix64(u ^ (np.asarray(gver, np.uint64) << np.uint64(48)) ^ np.uint64(rng_seed ^ 0x6706))
     ha = splitmix64(u ^ (np.asarray(aver, np.uint64) << np.uint64(48)) ^ np.uint64(rng_seed ^ 0xA77A))
     ha2 = splitmix64(ha)
-    npts = (5 + (hg >> np.uint64(58)) % np.uint64(20)).astype(np.int64)  # 5..24 ring points
+    hsize = hg
+    if same_len > 0:
+        hp = splitmix64(u ^ np.uint64(rng_seed ^ 0x5E1E))
+        hsize = np.where(hp % np.uint64(1000) < np.uint64(int(round(same_len * 1000))), hp, hg)
+    npts = (5 + (hsize >> np.uint64(58)) % np.uint64(20)).astype(np.int64)  # 5..24 ring points
     glen = 8 + 32 + 22 + 16 * npts  # GPKG header + envelope + MULTIPOLYGON/POLYGON/ring headers + xy
     ehdr = np.where(glen <= 255, 3, 4)  # c7 len 47 | c8 len16 47
     has_ref = ((ha2 >> np.uint64(7)) & np.uint64(3)) != 0
@@ -283,7 +289,7 @@ def c3_plan(pk, n, seed=C3_SEED):
     return np.where(h < 400, 1, np.where(h < 800, 2, np.where(h < 900, 3, 0))).astype(np.uint8)
 
 
-def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False):
+def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False, same_len=0.0):
     """C3: n int-PK MULTIPOLYGON features (pks 0..n-1) and n // 100 inserts (pks n..), 10 % edits =
     4 % geometry updates + 4 % attribute updates + 1 % deletes + 1 % inserts, edits
     picked by a hash of the pk (c3_plan).
@@ -293,7 +299,8 @@ def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False
     Feature blobs are materialised for the updated features only (both versions): the diff reads no
     other blob — classification needs only keys and OIDs — so every other entry has a zero-length
     blob in the arena.  ``delta_blobs``: also the deleted features' base blobs and the inserted
-    features' target blobs (what a spatially filtered diff reads: C5)."""
+    features' target blobs (what a spatially filtered diff reads: C5).  ``same_len``: the fraction of
+    features whose geometry edits keep the blob length (vertex moves; polygon_blobs)."""
     schema = Schema.from_column_dicts(POLYGON_SCHEMA)
     legend = Legend(["p-fid"], [c["id"] for c in POLYGON_SCHEMA[1:]])
     lh = legend.hexhash()
@@ -322,7 +329,7 @@ def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False
     def blobs(idx_pk, gv, av):
         parts, offs = [], [np.zeros(1, np.uint64)]
         for s in range(0, idx_pk.shape[0], batch):
-            d, o = polygon_blobs(idx_pk[s:s + batch], gv[s:s + batch], av[s:s + batch], lh, seed)
+            d, o = polygon_blobs(idx_pk[s:s + batch], gv[s:s + batch], av[s:s + batch], lh, seed, same_len)
             parts.append(d)
             offs.append(o[1:] + offs[-1][-1])
         return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), np.concatenate(offs)

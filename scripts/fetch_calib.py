@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""FETCH_SIZE calibration summary (scripts/fetch_calib.hip under rocprofv3 --pmc FETCH_SIZE).
+
+usage: fetch_calib.py PATTERNS.jsonl COUNTER_CSV [--out calib.json]
+For each pattern: FETCH_SIZE (rocprofv3 reports KB) in bytes, and its ratio to the requested bytes
+and to the distinct 32 / 64 / 128-B blocks the pattern touched."""
+import argparse
+import collections
+import csv
+import json
+import re
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("patterns")
+    ap.add_argument("counters")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    pats = [json.loads(ln) for ln in open(a.patterns) if ln.startswith("{")]
+    fetch = collections.defaultdict(float)
+    with open(a.counters) as f:
+        for r in csv.DictReader(f):
+            m = re.search(r"k_pat<(\d+)>", r["Kernel_Name"])
+            if m and r["Counter_Name"] == "FETCH_SIZE":
+                fetch[int(m.group(1))] += float(r["Counter_Value"]) * 1024
+    out = []
+    for i, p in enumerate(pats):
+        fb = fetch.get(i)
+        row = dict(p, fetch_size_bytes=fb)
+        if fb:
+            for k in ("bytes", "b32", "b64", "b128"):
+                row[f"fetch_over_{k}"] = round(fb / p[k], 4)
+        out.append(row)
+        print(json.dumps(row))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
