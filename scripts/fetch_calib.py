@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """FETCH_SIZE calibration summary (scripts/fetch_calib.hip under rocprofv3 --pmc FETCH_SIZE).
 
-usage: fetch_calib.py PATTERNS.jsonl COUNTER_CSV [--out calib.json]
+usage: fetch_calib.py PATTERNS.jsonl PMC_DIR [--out calib.json]   (PMC_DIR: the rocprofv3 -d directory)
 For each pattern: FETCH_SIZE (rocprofv3 reports KB) in bytes, and its ratio to the requested bytes
 and to the distinct 32 / 64 / 128-B blocks the pattern touched."""
 import argparse
 import collections
 import csv
+import glob
 import json
+import os
 import re
 
 
@@ -19,11 +21,12 @@ def main():
     a = ap.parse_args()
     pats = [json.loads(ln) for ln in open(a.patterns) if ln.startswith("{")]
     fetch = collections.defaultdict(float)
-    with open(a.counters) as f:
-        for r in csv.DictReader(f):
-            m = re.search(r"k_pat<(\d+)>", r["Kernel_Name"])
-            if m and r["Counter_Name"] == "FETCH_SIZE":
-                fetch[int(m.group(1))] += float(r["Counter_Value"]) * 1024
+    for path in glob.glob(os.path.join(a.counters, "**", "run_counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                m = re.search(r"k_pat<(\d+)>", r["Kernel_Name"])
+                if m and r["Counter_Name"] == "FETCH_SIZE":
+                    fetch[int(m.group(1))] += float(r["Counter_Value"]) * 1024
     out = []
     for i, p in enumerate(pats):
         fb = fetch.get(i)

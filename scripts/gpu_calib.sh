@@ -13,5 +13,5 @@ cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d $OUT/pmc -o run -- \
     $OUT/fetch_calib > $OUT/pmc_stdout.txt 2> $OUT/pmc_stderr.txt
 cd $R
-python3 scripts/fetch_calib.py $OUT/patterns.jsonl $(ls $OUT/pmc/*/run_counter_collection.csv $OUT/pmc/run_counter_collection.csv 2>/dev/null | head -1) --out gpurun_out/${TAG}_calib.json
+python3 scripts/fetch_calib.py $OUT/patterns.jsonl $OUT/pmc --out gpurun_out/${TAG}_calib.json
 rm -f $OUT/fetch_calib
