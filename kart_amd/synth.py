@@ -11,6 +11,8 @@ Generation is vectorised numpy, fast enough for the 10M-point C2 layer in second
 """
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 
 from . import packing
@@ -540,6 +542,13 @@ class Merge3Layer:
     n_conflict: int  # libgit2 rule over the generator's plan (o == t -> o; a == o -> t; a == t -> o)
 
 
+def _sha256_prefixes(rows):
+    """the first 3 bytes of sha256 of each 12-byte record"""
+    import hashlib
+
+    return b"".join(hashlib.sha256(rows[i:i + 12]).digest()[:3] for i in range(0, len(rows), 12))
+
+
 def _hash_paths(ids):
     """MsgpackHashPathEncoder paths (dataset3_paths.py:202-215, 4 levels x 64 branches, base64) of the
     string pks 'R%09d' % id: 'c/c/c/c/' + urlsafe_b64(msgpack([pk])) — 24 bytes each, [n, 24] uint8."""
@@ -561,8 +570,16 @@ def _hash_paths(ids):
     out[:, 8:] = alpha[fn]
     # tree: first 24 bits of sha256(packed) as 4 base64 chars (b64hash, serialise_util.py:82-85)
     rows = packed.tobytes()
-    h = np.frombuffer(b"".join(hashlib.sha256(rows[12 * i:12 * i + 12]).digest()[:3] for i in range(n)),
-                      np.uint8).reshape(n, 3).astype(np.uint32)
+    if n >= 1 << 21:  # large layers: the digests on a process pool
+        from multiprocessing import Pool
+
+        nproc = max(1, min(16, os.cpu_count() or 1))
+        cuts = np.linspace(0, n, 4 * nproc + 1).astype(np.int64)
+        with Pool(nproc) as pool:
+            parts = pool.map(_sha256_prefixes, [rows[12 * a:12 * b] for a, b in zip(cuts[:-1], cuts[1:])])
+        h = np.frombuffer(b"".join(parts), np.uint8).reshape(n, 3).astype(np.uint32)
+    else:
+        h = np.frombuffer(_sha256_prefixes(rows), np.uint8).reshape(n, 3).astype(np.uint32)
     hv = h[:, 0] << 16 | h[:, 1] << 8 | h[:, 2]
     for k in range(4):
         out[:, 2 * k] = alpha[(hv >> (18 - 6 * k)) & 63]
@@ -582,7 +599,7 @@ def _pack_fixed(paths, oids):
     bad = N.lib().kd_pack_hash_keys(N.ptr(flat), N.ptr(off), n, 4, 0, N.ptr(keys), N.ptr(status))
     if bad:
         raise packing.PackError(f"{bad} synthetic paths not packable")
-    order = np.argsort(keys, kind="stable")
+    order = np.argsort(keys)  # (keys are distinct, checked below: any sort is stable)
     keys = keys[order]
     if n > 1 and not np.all(keys[1:] > keys[:-1]):
         raise packing.PackError("synthetic key collision")

@@ -662,3 +662,168 @@ void kdo_sf_filter_batch(uint64_t n_idx, const uint8_t* idx_oid, const uint8_t* 
         out[i] = r < 0 ? 2 : (r ? 0 : 1);
     }
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* spatially filtered diff (kart/base_diff_writer.py:279-329 + SpatialFilter.matches,          */
+/* kart/spatial_filter/__init__.py:534-605), envelope part: the C form of oracle.geom_filter     */
+/* ------------------------------------------------------------------------------------------ */
+enum { GF_NON = 0, GF_CAND = 1, GF_MATCH = 2, GF_FALLBACK = 3, GF_NONE = 4 };
+
+/* one msgpack object of any kind (containers nested), as msgpack.unpackb walks it: bytes consumed,
+ * 0 when malformed.  *top_ext_g / *is_nil describe a scalar (an ext 'G' payload, nil) */
+static uint32_t skip_any(const uint8_t* p, const uint8_t* end, int depth) {
+    if (p >= end || depth > 512) return 0;
+    const uint8_t t = p[0];
+    uint64_t avail = (uint64_t)(end - p), cnt = 0;
+    uint32_t hdr = 0;
+    int map = 0;
+    if (t >= 0x90 && t <= 0x9f) { cnt = t & 15; hdr = 1; }
+    else if (t >= 0x80 && t <= 0x8f) { cnt = t & 15; hdr = 1; map = 1; }
+    else if (t == 0xdc || t == 0xde) { if (avail < 3) return 0; cnt = be(p + 1, 2); hdr = 3; map = t == 0xde; }
+    else if (t == 0xdd || t == 0xdf) { if (avail < 5) return 0; cnt = be(p + 1, 4); hdr = 5; map = t == 0xdf; }
+    else {
+        kval v;
+        uint32_t c = decode_value(p, end, &v);
+        if (c) return c;
+        /* decode_value refuses an ext 'G' payload not starting "GP"; unpackb with the oracle's hook
+         * (oracle.py _gf_hook) accepts any payload: skip it by its length */
+        if ((t >= 0xd4 && t <= 0xd8) || (t >= 0xc7 && t <= 0xc9)) {
+            uint32_t n, h;
+            if (t <= 0xd8 && t >= 0xd4) { n = 1u << (t - 0xd4); h = 2; }
+            else { int w = 1 << (t - 0xc7); if (avail < (uint64_t)(2 + w)) return 0; n = (uint32_t)be(p + 1, w); h = 2 + w; }
+            if ((uint64_t)h + n > avail) return 0;
+            return h + n;
+        }
+        return 0;
+    }
+    uint64_t o = hdr;
+    for (uint64_t i = 0; i < cnt * (map ? 2 : 1); i++) {
+        uint32_t c = skip_any(p + o, end, depth + 1);
+        if (!c) return 0;
+        o += c;
+    }
+    return (uint32_t)o;
+}
+
+/* feature_geometry (oracle.py): status 0 with *g / *gn = the geometry payload (g NULL: None),
+ * or GF_FALLBACK (malformed, unknown legend, value index out of range, not an ext 'G') */
+static int feature_geometry_c(const uint8_t* b, uint32_t n, int n_leg, const uint8_t* leg_hex, const int16_t* gidx,
+                              const uint8_t** g, uint32_t* gn) {
+    *g = NULL;
+    *gn = 0;
+    const uint8_t* end = b + n;
+    if (skip_any(b, end, 0) != n) return GF_FALLBACK;  /* unpackb raises (incl. ExtraData) */
+    if (n < 1 || !((b[0] >= 0x90 && b[0] <= 0x9f) || b[0] == 0xdc || b[0] == 0xdd)) return GF_FALLBACK;
+    uint32_t o = b[0] <= 0x9f ? 1 : b[0] == 0xdc ? 3 : 5;
+    uint64_t cnt = b[0] <= 0x9f ? (uint64_t)(b[0] & 15) : be(b + 1, b[0] == 0xdc ? 2 : 4);
+    if (cnt != 2) return GF_FALLBACK;                   /* legend, values = ... */
+    kval lv;
+    uint32_t c = decode_value(b + o, end, &lv);
+    if (!c || lv.cls != V_STR || lv.len != 40) return GF_FALLBACK;
+    int li = -1;
+    for (int l = 0; l < n_leg; l++) if (!memcmp(leg_hex + 40 * l, lv.p, 40)) { li = l; break; }
+    if (li < 0) return GF_FALLBACK;
+    const int gi = gidx[li];
+    if (gi < 0) return 0;
+    o += c;
+    const uint8_t t = b[o];
+    uint64_t nv;
+    uint32_t h;
+    if (t >= 0x90 && t <= 0x9f) { nv = t & 15; h = 1; }
+    else if (t == 0xdc) { nv = be(b + o + 1, 2); h = 3; }
+    else if (t == 0xdd) { nv = be(b + o + 1, 4); h = 5; }
+    else return GF_FALLBACK;  /* values not an array */
+    if ((uint64_t)gi >= nv) return GF_FALLBACK;
+    o += h;
+    for (int i = 0; i < gi; i++) o += skip_any(b + o, end, 1);
+    const uint8_t vt = b[o];
+    if (vt == 0xc0) return 0;                          /* None */
+    uint32_t pl, ph;
+    if (vt >= 0xd4 && vt <= 0xd8) { pl = 1u << (vt - 0xd4); ph = 2; }
+    else if (vt >= 0xc7 && vt <= 0xc9) { int w = 1 << (vt - 0xc7); pl = (uint32_t)be(b + o + 1, w); ph = 2 + w; }
+    else return GF_FALLBACK;
+    if ((int8_t)b[o + ph - 1] != 'G') return GF_FALLBACK;
+    *g = b + o + ph;
+    *gn = pl;
+    return 0;
+}
+
+/* sf_envelope_code (oracle.py): SpatialFilter.matches without the exact Intersects */
+static int sf_envelope_code_c(const uint8_t* g, uint32_t gn, const double filt[4], int rect) {
+    static const uint8_t zero[1] = {0};
+    if (!g) return GF_MATCH;                           /* geometry None: MATCHING (:549-551) */
+    const uint8_t* gb = gn ? g : zero;
+    double env[4];
+    int r = kdo_gpkg_envelope(gb, gn, env);
+    if (r < 0) return GF_FALLBACK;
+    if (r == 0 && (gb[3] & 0x10)) return GF_NON;     /* empty: Intersects(empty) is False */
+    if (r != 1) {
+        int pc = kdo_point_envelope(gb, gn, env);
+        if (pc == 0) return GF_NON;
+        if (pc < 0) return GF_FALLBACK;
+    }
+    int x = kdo_bbox_intersects(filt, env);
+    if (x < 0) return GF_FALLBACK;
+    if (x == 0) return GF_NON;
+    if (rect && filt[0] <= env[0] && env[1] <= filt[1] && filt[2] <= env[2] && env[3] <= filt[3]) return GF_MATCH;
+    return GF_CAND;
+}
+
+/* the per-geometry body of kdo_envelope_batch */
+static void envelope_one(const uint8_t* g, uint64_t len, const double filt[4], int bits, uint8_t* match, uint8_t* enc,
+                         uint8_t* enc_ok) {
+    int nb = bits / 2;
+    double env[4], src[4], wsen[4];
+    memset(enc, 0, nb);
+    *enc_ok = 0;
+    if (len == 0) { *match = 2; return; }
+    if (matches_envelope(g, len, env) < 0) *match = 3;
+    else {
+        int hit = kdo_bbox_intersects(filt, env);
+        *match = hit < 0 ? 3 : (uint8_t)hit;
+    }
+    if (len >= 4 && (g[3] & 0x10)) return;
+    if (index_source_envelope(g, len, src) != 1) return;
+    if (kdo_index_envelope(src, wsen) != 1) return;
+    if (kdo_envelope_encode(wsen, bits, enc) != 0) { memset(enc, 0, nb); return; }
+    *enc_ok = 1;
+}
+
+/* geom_filter (oracle.py): per delta d and side s, codes[2d+s] (GF_*), and the new side's index
+ * envelope (enc [n*bits/2], enc_ok [n]) of the geometry when that side is neither NONE nor
+ * FALLBACK.  pairs [2n] = (old blob | KD_NONE, new blob | KD_NONE).  Returns the kept count
+ * (deltas with a side in CANDIDATE..FALLBACK). */
+int64_t kdo_geom_filter(uint64_t n, const uint8_t* od, const uint64_t* ooff, const uint8_t* nd, const uint64_t* noff,
+                        const uint32_t* pairs, int n_leg_o, const uint8_t* leg_o, const int16_t* gidx_o, int n_leg_n,
+                        const uint8_t* leg_n, const int16_t* gidx_n, const double filt[4], int rect, int bits,
+                        uint8_t* codes, uint8_t* enc, uint8_t* enc_ok) {
+    int64_t kept = 0;
+    const int nb = bits / 2;
+    for (uint64_t d = 0; d < n; d++) {
+        const uint8_t* gnew = NULL;
+        uint32_t gnew_n = 0;
+        int use_new = 0;
+        for (int s = 0; s < 2; s++) {
+            const uint32_t bi = pairs[2 * d + s];
+            uint8_t code;
+            const uint8_t* g = NULL;
+            uint32_t gn = 0;
+            if (bi == 0xFFFFFFFFu) code = GF_NONE;
+            else {
+                const uint8_t* data = s ? nd : od;
+                const uint64_t* off = s ? noff : ooff;
+                const int st = feature_geometry_c(data + off[bi], (uint32_t)(off[bi + 1] - off[bi]), s ? n_leg_n : n_leg_o,
+                                                  s ? leg_n : leg_o, s ? gidx_n : gidx_o, &g, &gn);
+                code = st ? (uint8_t)st : (uint8_t)sf_envelope_code_c(g, gn, filt, rect);
+            }
+            codes[2 * d + s] = code;
+            if (s == 1 && code != GF_NONE && code != GF_FALLBACK) { gnew = g; gnew_n = gn; use_new = 1; }
+        }
+        uint8_t m;
+        if (use_new && gnew) envelope_one(gnew, gnew_n, filt, bits, &m, enc + d * nb, enc_ok + d);
+        else { memset(enc + d * nb, 0, nb); enc_ok[d] = 0; }
+        const uint8_t a = codes[2 * d], b = codes[2 * d + 1];
+        kept += (a >= 1 && a <= 3) || (b >= 1 && b <= 3);
+    }
+    return kept;
+}

@@ -54,6 +54,9 @@ def C():
         L.kdo_envelope_overlap.argtypes = [_vp, ctypes.c_int, _vp]
         L.kdo_sf_filter_batch.restype = None
         L.kdo_sf_filter_batch.argtypes = [ctypes.c_uint64, _vp, _vp, ctypes.c_int, ctypes.c_uint64, _vp, _vp, _vp, _vp]
+        L.kdo_geom_filter.restype = ctypes.c_int64
+        L.kdo_geom_filter.argtypes = [ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp, _vp, ctypes.c_int,
+                                      _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]
         L.kdo_bbox_intersects.restype = ctypes.c_int
         L.kdo_bbox_intersects.argtypes = [_vp, _vp]
         L.kdo_wrap_lon.restype = ctypes.c_double
@@ -242,9 +245,39 @@ def feature_geometry(blob, gidx_by_legend):
     return 0, bytes(v)
 
 
+def _cols_arrays(cols):
+    hexes = sorted(cols)
+    hx = np.frombuffer(b"".join(h.encode() for h in hexes), np.uint8).copy() if hexes else np.zeros(40, np.uint8)
+    gi = np.array([cols[h] for h in hexes] or [-1], np.int16)
+    return len(hexes), hx, gi
+
+
 def geom_filter(old_data, old_off, new_data, new_off, pairs, old_cols, new_cols, filt_env, rect, bits=20):
     """codes [n, 2], kept delta indices, new-side index envelopes (enc [n, bits/2], enc_ok [n]).
-    old_cols/new_cols: {legend hex: geometry value index | -1}."""
+    old_cols/new_cols: {legend hex: geometry value index | -1}.  The C restatement
+    (kdo_geom_filter) of geom_filter_py below, fast enough for C5's 10M deltas."""
+    pairs = np.ascontiguousarray(pairs, np.uint32).reshape(-1, 2)
+    n = pairs.shape[0]
+    nlo, hxo, gio = _cols_arrays(old_cols)
+    nln, hxn, gin = _cols_arrays(new_cols)
+    codes = np.zeros((max(n, 1), 2), np.uint8)
+    enc = np.zeros((max(n, 1), bits // 2), np.uint8)
+    ok = np.zeros(max(n, 1), np.uint8)
+    pad = np.zeros(16, np.uint8)
+    od = old_data if old_data.size else pad
+    nd = new_data if new_data.size else pad
+    C().kdo_geom_filter(n, _p(od), _p(np.ascontiguousarray(old_off, np.uint64)), _p(nd),
+                        _p(np.ascontiguousarray(new_off, np.uint64)), _p(pairs if n else np.zeros(2, np.uint32)),
+                        nlo, _p(hxo), _p(gio), nln, _p(hxn), _p(gin), _p(np.asarray(filt_env, np.float64)),
+                        1 if rect else 0, bits, _p(codes), _p(enc), _p(ok))
+    codes, enc, ok = codes[:n], enc[:n], ok[:n]
+    keep = np.nonzero(((codes >= 1) & (codes <= 3)).any(axis=1))[0].astype(np.uint32)
+    return codes, keep, enc, ok
+
+
+def geom_filter_py(old_data, old_off, new_data, new_off, pairs, old_cols, new_cols, filt_env, rect, bits=20):
+    """the Python restatement (msgpack.unpackb with the ext hook, per delta): the reference for
+    kdo_geom_filter on small inputs"""
     n = pairs.shape[0]
     codes = np.zeros((n, 2), np.uint8)
     geoms_new = []

@@ -302,11 +302,12 @@ def test_gpu_envelopes_c5_layer_vs_oracle(engine, n, seed):
     assert 0 < gc < n
 
 
-@pytest.mark.parametrize("n", [1000, 400_000])
+@pytest.mark.parametrize("n", [1000, 400_000, pytest.param(50_000_000, marks=pytest.mark.timeout(900))])
 def test_gpu_merge3_device_c4_layer_vs_oracle(engine, n):
     """the C4 bench layer (string PKs, MsgpackHashPathEncoder paths, mod/mod, mod/del, del/mod and
     add/add edits) through the device-resident kd_merge3_device pipeline bench.py times, and the host
-    kd_merge3: conflicts and merge deltas bit-exact with the oracle, conflicts = the generator's plan"""
+    kd_merge3: conflicts and merge deltas bit-exact with the oracle, conflicts = the generator's plan.
+    50M rows = C4 at its stated size (BASELINE configs[3])"""
     from kart_amd import synth
     from kart_amd.device import MergePipeline
 

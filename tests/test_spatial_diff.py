@@ -206,10 +206,12 @@ def test_gpu_filtered_diff_points_edit_golden(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [200_000, 5_000_000])
+@pytest.mark.parametrize("n", [200_000, 5_000_000, pytest.param(100_000_000, marks=pytest.mark.timeout(900))])
 def test_gpu_filter_pipeline_device_resident(engine, n):
     """FilterPipeline: classify2's device delta list straight into kd_geom_filter (device count),
-    equal to the oracle over the same deltas"""
+    equal to the oracle over the same deltas (the C restatement, kdo_geom_filter).  100M features =
+    C5 at its stated size (BASELINE configs[4]): ~10M deltas, both sides' codes, the kept list and
+    the new side's index envelopes bit-exact"""
     import types
 
     from kart_amd import synth
@@ -228,3 +230,39 @@ def test_gpu_filter_pipeline_device_resident(engine, n):
     oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta, cols, cols, synth.C5_FILTER, False, 20)
     assert np.array_equal(codes, oc) and np.array_equal(keep, okeep) and counts["kept"] == len(okeep)
     assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1])
+
+
+@pytest.mark.parametrize("bits", [20, 16])
+def test_oracle_geom_filter_c_equals_python(bits):
+    """the C restatement of the filtered diff's per-side decision (kdo_geom_filter, what the
+    full-size C5 check uses) equals the Python one (msgpack.unpackb + the envelope functions) on
+    crafted blobs: nested values, ext8/16/32 geometries, unknown legends, null and empty geometries,
+    truncated and trailing-byte blobs"""
+    rng = np.random.default_rng(bits)
+    ob, cols = _crafted(rng, 3000)
+    nb, _ = _crafted(np.random.default_rng(bits + 1), 3000)
+    h = sorted(cols)[0]
+    extra = [msgpack.packb([h, [msgpack.ExtType(ord("G"), b""), 1, 2]], use_bin_type=True),  # empty ext 'G'
+             msgpack.packb([h, [msgpack.ExtType(ord("G"), b"XX123456"), 1, 2]], use_bin_type=True),  # not GPKG
+             msgpack.packb([h, [msgpack.ExtType(5, b"abc"), 1, 2]], use_bin_type=True),  # another ext
+             msgpack.packb([h, [1.5, 1, 2]], use_bin_type=True), msgpack.packb([h, []], use_bin_type=True),
+             msgpack.packb([h], use_bin_type=True), msgpack.packb([h, [None], 3], use_bin_type=True),
+             msgpack.packb({"a": 1, "b": 2}, use_bin_type=True), b"\x92", b"",
+             msgpack.packb([h, [{"k": [1, {"x": None}]}, 1, 2]], use_bin_type=True) + b"\x00"]
+    ob = ob + extra
+    nb = nb + extra
+    od, oo = _arena(ob)
+    nd, no = _arena(nb)
+    n = 6000
+    pairs = np.stack([rng.integers(0, len(ob), n), rng.integers(0, len(nb), n)], axis=1).astype(np.uint32)
+    pairs[-2 * len(extra):-len(extra), 0] = np.arange(len(ob) - len(extra), len(ob))
+    pairs[-len(extra):, 1] = np.arange(len(nb) - len(extra), len(nb))
+    pairs[rng.random(n) < 0.2, 0] = NONE
+    pairs[rng.random(n) < 0.2, 1] = NONE
+    for filt, rect in [((170.0, 178.0, -45.0, -30.0), True), ((-10.0, 10.0, -5.0, 5.0), False),
+                       ((-180.0, 180.0, -90.0, 90.0), True)]:
+        c = O.geom_filter(od, oo, nd, no, pairs, cols, cols, filt, rect, bits)
+        p = O.geom_filter_py(od, oo, nd, no, pairs, cols, cols, filt, rect, bits)
+        for x, y in zip(c, p):
+            assert np.array_equal(x, y)
+    assert {0, 1, 2, 3, 4} <= set(np.unique(c[0]).tolist())
