@@ -323,6 +323,11 @@ int kd_diff2_gather_end(kd_ctx* ctx, const uint32_t* d_delta, uint32_t* d_all_de
  * all-gathered over a communicator the library keeps on ctxs[0].  Result as kd_diff2. */
 int kd_diff2_sharded(kd_ctx** ctxs, int g, const kd_side* base, const kd_side* target, int bucket_bits,
                      uint32_t flags, kd_diff_result** out);
+/* The cut kd_diff2_sharded uses (host only, no GPU): cut [g+1] bucket edges, shard s = buckets
+ * [cut[s], cut[s+1]), each cut the smallest bucket with at least total*s/g entries of both sorted
+ * key arrays before it; a_lo / b_lo [g+1] the matching entry ranges of each side. */
+int kd_shard_cuts(const uint64_t* key_a, uint64_t n_a, const uint64_t* key_b, uint64_t n_b, int g, int bucket_bits,
+                  uint64_t* cut, uint64_t* a_lo, uint64_t* b_lo);
 
 /* -------- host-side key packing (CPU, multithreaded) -------- */
 /* KD_KEY_INT: filenames b64(msgpack([pk])) -> keys (entries may be whole relative paths

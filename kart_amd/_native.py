@@ -181,6 +181,8 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_dblp, ctypes.c_void_p,
          ctypes.c_uint32],
     ),
+    "kd_shard_cuts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kd_sf_index_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     "kd_sf_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

@@ -327,6 +327,34 @@ int kd_diff2_gather(kd_ctx* ctx, const kd_side* base, const kd_side* target, uin
 }
 
 // ------------------------------------------------------------------------------------------
+// bucket-range cuts (host only): shard s holds buckets [cut[s], cut[s+1]) — cut[s] the smallest
+// bucket at or after cut[s-1] with at least total*s/g entries of both sides before it — and the
+// sorted entries [a_lo[s], a_lo[s+1]) / [b_lo[s], b_lo[s+1]) of each side
+int kd_shard_cuts(const uint64_t* key_a, uint64_t n_a, const uint64_t* key_b, uint64_t n_b, int g, int bucket_bits,
+                  uint64_t* cut, uint64_t* a_lo, uint64_t* b_lo) {
+    KD_CHECK(g >= 1 && cut && a_lo && b_lo && (n_a == 0 || key_a) && (n_b == 0 || key_b), "kd_shard_cuts: bad args");
+    KD_CHECK(bucket_bits >= 1 && bucket_bits <= 32, "kd_shard_cuts: bucket_bits %d", bucket_bits);
+    const u64 total = n_a + n_b;
+    cut[0] = 0;
+    cut[g] = 1ull << bucket_bits;
+    for (int s = 1; s < g; s++) {
+        const u64 want = total * (u64)s / (u64)g;
+        u64 lo = cut[s - 1], hi = cut[g];
+        while (lo < hi) {  // smallest bucket whose lower edge has >= want entries before it
+            const u64 mid = lo + (hi - lo) / 2;
+            const u64 c = bucket_lower(key_a, n_a, mid, bucket_bits) + bucket_lower(key_b, n_b, mid, bucket_bits);
+            if (c >= want) hi = mid; else lo = mid + 1;
+        }
+        cut[s] = lo;
+    }
+    for (int s = 0; s <= g; s++) {
+        a_lo[s] = bucket_lower(key_a, n_a, cut[s], bucket_bits);
+        b_lo[s] = bucket_lower(key_b, n_b, cut[s], bucket_bits);
+    }
+    return KD_OK;
+}
+
+// ------------------------------------------------------------------------------------------
 // single process, g GPUs: the library cuts the sides, runs every shard and owns the communicator
 int kd_diff2_sharded(kd_ctx** ctxs, int g, const kd_side* base, const kd_side* target, int bucket_bits,
                      uint32_t flags, kd_diff_result** out) {
@@ -340,23 +368,10 @@ int kd_diff2_sharded(kd_ctx** ctxs, int g, const kd_side* base, const kd_side* t
     Rccl* R;
     if ((rc = rccl(&R))) return rc;
     // ---- bucket cuts: shard s holds buckets [cut[s], cut[s+1]), about total/g entries ----
-    const u64 nA = base->n, nB = target->n, total = nA + nB;
     std::vector<u64> cut(g + 1, 0), a_lo(g + 1), b_lo(g + 1);
-    cut[g] = 1ull << bucket_bits;
-    for (int s = 1; s < g; s++) {
-        const u64 want = total * (u64)s / (u64)g;
-        u64 lo = cut[s - 1], hi = cut[g];
-        while (lo < hi) {  // smallest bucket whose lower edge has >= want entries before it
-            const u64 mid = lo + (hi - lo) / 2;
-            const u64 c = bucket_lower(base->key, nA, mid, bucket_bits) + bucket_lower(target->key, nB, mid, bucket_bits);
-            if (c >= want) hi = mid; else lo = mid + 1;
-        }
-        cut[s] = lo;
-    }
-    for (int s = 0; s <= g; s++) {
-        a_lo[s] = bucket_lower(base->key, nA, cut[s], bucket_bits);
-        b_lo[s] = bucket_lower(target->key, nB, cut[s], bucket_bits);
-    }
+    if ((rc = kd_shard_cuts(base->key, base->n, target->key, target->n, g, bucket_bits, cut.data(), a_lo.data(),
+                            b_lo.data())))
+        return rc;
     // ---- communicator over these devices (kept on ctxs[0] for the same device set) ----
     std::vector<int> devs(g);
     for (int i = 0; i < g; i++) devs[i] = ctxs[i]->device;

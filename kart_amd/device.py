@@ -253,14 +253,25 @@ class DiffPipeline:
     def gathered(self):
         """(gather mode, after a step + sync) the whole diff: global delta records in key order and
         the summed counts of every rank"""
-        c = self.h_counts.reshape(self.world, 8)
-        if c[:, 4].any():
-            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flags {c[:, 4].tolist()}")
-        stride = int(c[:, 3].max())
-        rec = self.all_delta.download(np.uint32, 2 * stride * self.world).reshape(self.world, stride, 2)
-        delta = np.concatenate([rec[r, :int(c[r, 3])] for r in range(self.world)]) if stride else np.zeros((0, 2), np.uint32)
-        return {"inserts": int(c[:, 0].sum()), "updates": int(c[:, 1].sum()), "deletes": int(c[:, 2].sum()),
-                "deltas": int(c[:, 3].sum())}, delta
+        stride = int(self.h_counts.reshape(self.world, 8)[:, 3].max())
+        rec = self.all_delta.download(np.uint32, 2 * stride * self.world)
+        return assemble_gathered(self.h_counts, rec, self.world)
+
+
+def assemble_gathered(h_counts, records, world):
+    """The whole diff from kd_diff2_gather's outputs: h_counts [world * 8] (rank r's inserts,
+    updates, deletes, deltas, error word, ...) and the all-gathered records [world * stride * 2]
+    (rank r's rebased records at 2 * r * stride, stride = the largest rank's delta count, the tail
+    of each slot padding).  Ranks hold consecutive bucket ranges, so their records in rank order are
+    the key-ordered delta list.  Returns (summed counts, delta [n, 2])."""
+    c = np.asarray(h_counts, np.uint64).reshape(world, 8)
+    if c[:, 4].any():
+        raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flags {c[:, 4].tolist()}")
+    stride = int(c[:, 3].max())
+    rec = np.asarray(records, np.uint32)[:2 * stride * world].reshape(world, stride, 2)
+    delta = np.concatenate([rec[r, :int(c[r, 3])] for r in range(world)]) if stride else np.zeros((0, 2), np.uint32)
+    return {"inserts": int(c[:, 0].sum()), "updates": int(c[:, 1].sum()), "deletes": int(c[:, 2].sum()),
+            "deltas": int(c[:, 3].sum())}, delta
 
 
 class FilterPipeline:
