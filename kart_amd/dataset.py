@@ -424,7 +424,7 @@ def estimate_diff_feature_counts(engine, base_datasets, target_datasets, *, accu
     return counts
 
 
-def field_diff(engine, feature_diff, old_version, new_version):
+def field_diff(engine, feature_diff, old_version, new_version, stats=None):
     """Attach ``changed_fields`` (names, in _all_feature_keys order) to every update delta of
     ``feature_diff``, computed by kd_fielddiff in one batch.  Updates the GPU cannot handle
     (status != 0) get None and the caller uses the reference loop for them.
@@ -432,7 +432,11 @@ def field_diff(engine, feature_diff, old_version, new_version):
     A DeltaDiff that dataset_diff built carries its updates' leaf indices: each side's blobs are
     read by one kd_odb_read_batch straight into the arena kd_fielddiff takes (no per-blob Python
     object), and the arena is kept for later value reads.  Any other DeltaDiff (built by hand,
-    combined with ``+``) goes through its lazy blobs."""
+    combined with ``+``) goes through its lazy blobs.  ``stats`` (a dict) receives the seconds of
+    the blob reads, the kernel call and the name attachment."""
+    import time
+
+    t0 = time.perf_counter()
     with _gc_paused():
         batch = _live_batch(feature_diff, old_version, new_version)
         if batch is not None:
@@ -447,11 +451,15 @@ def field_diff(engine, feature_diff, old_version, new_version):
                 return 0
             od, oo = _blob_arena([d.old.value.args[0] for d in ups])
             nd, no = _blob_arena([d.new.value.args[0] for d in ups])
+        t1 = time.perf_counter()
         maps = FieldMaps(old_version.schema, old_version.legends, new_version.schema, new_version.legends)
         masks, status = engine.fielddiff(od, oo, nd, no, None, maps)
+        t2 = time.perf_counter()
         names = maps.changed_names_rows(masks[:len(ups)])
         for d, nm, s in zip(ups, names, status.tolist()):
             d.changed_fields = nm if s == 0 else None
+        if stats is not None:
+            stats.update(read_s=t1 - t0, kernel_s=t2 - t1, attach_s=time.perf_counter() - t2)
         return len(ups)
 
 

@@ -99,8 +99,21 @@ def build_parallel(gitdir, n, seed=3, procs=16):
         lines.append(b"D %s/feature/%s\n" % (inner.encode(), arena[int(off[i]):int(off[i + 1])].tobytes()))
     lines.append(b"\n")
     print(f"  tree stream built in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
-    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
-                   check=True)
+    import threading
+
+    done = threading.Event()
+
+    def heartbeat():  # fast-import builds 10M-entry trees silently for minutes
+        while not done.wait(30):
+            print(f"  fast-import running, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
+                       check=True)
+    finally:
+        done.set()
     print(f"  commits written in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     return k
 
@@ -200,8 +213,10 @@ def main():
             t, ds = timed(lambda: D.get_dataset_diff(eng, old, new))
             stages["diff_s"] = t
             fd = ds["feature"]
-            t, nu = timed(lambda: D.field_diff(eng, fd, old, new))
+            fds = {}
+            t, nu = timed(lambda: D.field_diff(eng, fd, old, new, stats=fds))
             stages["field_diff_s"] = t
+            stages["field_diff_parts_s"] = {k: round(v, 4) for k, v in fds.items()}
             total = time.perf_counter() - t0
             counts = fd.type_counts()
             assert sum(counts.values()) == n_git, (counts, n_git)

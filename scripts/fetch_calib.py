@@ -20,13 +20,15 @@ def main():
     ap.add_argument("--out")
     a = ap.parse_args()
     pats = [json.loads(ln) for ln in open(a.patterns) if ln.startswith("{")]
-    fetch = collections.defaultdict(float)
+    # rocprofv3 names the template instances all "k_pat": they run in pattern order, so the k-th
+    # k_pat dispatch is pattern k
+    per = collections.defaultdict(float)
     for path in glob.glob(os.path.join(a.counters, "**", "run_counter_collection.csv"), recursive=True):
         with open(path) as f:
             for r in csv.DictReader(f):
-                m = re.search(r"k_pat<(\d+)>", r["Kernel_Name"])
-                if m and r["Counter_Name"] == "FETCH_SIZE":
-                    fetch[int(m.group(1))] += float(r["Counter_Value"]) * 1024
+                if re.match(r"k_pat\b", r["Kernel_Name"]) and r["Counter_Name"] == "FETCH_SIZE":
+                    per[int(r["Dispatch_Id"])] += float(r["Counter_Value"]) * 1024
+    fetch = {i: per[d] for i, d in enumerate(sorted(per))}
     out = []
     for i, p in enumerate(pats):
         fb = fetch.get(i)
