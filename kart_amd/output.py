@@ -148,15 +148,19 @@ def _slices(hexbuf, lo, hi):
     return [text[a:b] for a, b in zip(lo.tolist(), hi.tolist())]
 
 
-def hex_wkb_arena(engine, geoms):
+def hex_wkb_arena(engine, geoms=None, arena=None):
     """The hex WKB of many geometries without building a str per value — for a writer that
     streams bytes: (hex uint8 buffer, lo int64[n], hi int64[n], status uint8[n]); geometry i's
     uppercase hex WKB is buffer[lo[i]:hi[i]] (empty unless status[i] == 0: 1 None / empty bytes,
-    3 the reference's OGR path or error)."""
-    vals = [b"" if g is None else g for g in geoms]
-    data, off = _arena(vals)
+    3 the reference's OGR path or error).  ``arena=(data, off)``: geometries already in one buffer
+    (e.g. a blob read's arena sliced to the geometry values) — nothing is joined on the host."""
+    if arena is None:
+        data, off = _arena([b"" if g is None else g for g in geoms])
+    else:
+        data, off = arena
     hexbuf, start, status = engine.hex_encode(data, off, N.KD_HEX_GPKG_WKB)
-    n = len(vals)
+    n = int(np.asarray(off).shape[0]) - 1
+    off = np.asarray(off, np.uint64)
     lo = 2 * (off[:n].astype(np.int64) + start.astype(np.int64))
     hi = np.where(status == 0, 2 * off[1:].astype(np.int64), lo)
     return hexbuf, lo, hi, status

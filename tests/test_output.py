@@ -112,6 +112,12 @@ def test_gpu_hexwkb_vs_oracle(engine, n, seed):
     want = [O.hex_wkb(g) for g in geoms]
     assert fb == [i for i, w in enumerate(want) if w == "fallback"]
     assert hexes == [None if w == "fallback" else w for w in want]
+    # the same from an arena the caller already holds (no per-value join): buffer + bounds
+    from kart_amd.output import _arena, hex_wkb_arena
+
+    hb, lo, hi, st = hex_wkb_arena(engine, arena=_arena([b"" if g is None else g for g in geoms]))
+    text = hb.tobytes().decode()
+    assert [text[a:b] if s == 0 else None for a, b, s in zip(lo.tolist(), hi.tolist(), st.tolist())] == hexes
 
 
 @pytest.mark.gpu
@@ -242,3 +248,106 @@ def test_features_as_json_defaults_to_package_geometry():
     g = row[fx.schema("head").geometry_columns[0].name]
     assert out[fx.schema("head").geometry_columns[0].name] == O.hex_wkb(bytes(g))
     assert out["ba"] == bytearray(b"\x01\x02") and out["raw"] == "00ff"
+
+
+# ---------------------------------------------------------------------------------------------
+# text writer lines (kart/feature_output.py:9-31): golden lines from the reference's own text diff
+# tests, produced here from the fixture repos' feature blobs
+POINTS_TEXT_3 = [  # tests/test_diff.py:75-81 (points HEAD feature 3, deleted in the working copy)
+    "-                                      fid = 3",
+    "-                                     geom = POINT(...)",
+    "-                                  t50_fid = 2426273",
+    "-                               name_ascii = Tauwhare Pa",
+    "-                               macronated = N",
+    "-                                     name = Tauwhare Pa",
+]
+POINTS_TEXT_2_NAME = "-                                     name = ␀"  # tests/test_diff.py:69-73 (feature 2)
+POLYGONS_TEXT_1452332 = [  # tests/test_diff.py:392-397 (polygons HEAD feature 1452332)
+    "-                                       id = 1452332",
+    "-                                     geom = MULTIPOLYGON(...)",
+    "-                            date_adjusted = 2011-06-07T15:22:58",
+    "-                         survey_reference = ␀",
+    "-                           adjusted_nodes = 558",
+]
+
+
+def _row(fixture, side, pk):
+    from test_dropin import version
+
+    fx = load(fixture)
+    v = version(fx, side)
+    for i in range(v.n):
+        name = v.blob_name(i)
+        if v.decode_path_to_1pk(name) == pk:
+            return v.get_feature(path=name, data=v.read_blob(i))
+    raise KeyError(pk)
+
+
+def test_feature_as_text_golden():
+    from kart_amd import output as OUT
+
+    # TextDiffWriter.write_feature_delta's prefixes are "- " / "+ " (kart/text_diff_writer.py:115-145)
+    assert OUT.feature_as_text(_row("repo_points", "head", 3), "- ").split("\n") == POINTS_TEXT_3
+    assert POINTS_TEXT_2_NAME in OUT.feature_as_text(_row("repo_points", "head", 2), "- ").split("\n")
+    assert OUT.feature_as_text(_row("repo_polygons", "head", 1452332), "- ").split("\n") == POLYGONS_TEXT_1452332
+    row = {"__hidden": 1, "b": b"\x00\x01", "n": None, "f": 1.5, "i": -3, "s": "x"}
+    assert OUT.feature_as_text(row, "+").split("\n") == [
+        "+" + " " * 39 + "b = BLOB(...)", "+" + " " * 39 + "n = ␀", "+" + " " * 39 + "f = 1.5",
+        "+" + " " * 39 + "i = -3", "+" + " " * 39 + "s = x"]
+
+
+def _gpkg(typ, le=True, flags_extra=0, env=0):
+    flags = (1 if le else 0) | (env << 1) | flags_extra
+    head = b"GP\x00" + bytes([flags]) + struct.pack("<i", 4326) + b"\x00" * {1: 32, 2: 48, 3: 48, 4: 64}.get(env, 0)
+    return head + (b"\x01" + struct.pack("<I", typ) if le else b"\x00" + struct.pack(">I", typ)) + b"\x00" * 16
+
+
+@pytest.mark.parametrize("typ,le,extra,env,want", [
+    (1, True, 0, 0, "POINT"), (1001, True, 0, 0, "POINT Z"),  # tests/test_diff.py:1234 (points-3d)
+    (2001, True, 0, 0, "POINT M"), (3001, False, 0, 0, "POINT ZM"), (0x80000003, True, 0, 1, "POLYGON Z"),
+    (6, False, 0, 1, "MULTIPOLYGON"), (1007, True, 0, 2, "GEOMETRYCOLLECTION Z"), (2005, True, 0, 4, "MULTILINESTRING M"),
+    (1, True, 0x10, 0, "POINT EMPTY"), (4, True, 0x10, 0, "MULTIPOINT EMPTY"),  # tests/test_geometry.py:43-49
+    (15, True, 0, 0, None), (8, True, 0, 0, None), (1, True, 0, 5, None)])
+def test_geometry_type_labels(typ, le, extra, env, want):
+    """Geometry.geometry_type_name with OGR's GT_Flatten / GT_HasZ / GT_HasM rules (ISO 1000 / 2000 /
+    3000 offsets, the 2.5D bit), EMPTY from the GPKG flags; types outside GeometryType and invalid
+    envelope indicators raise (ValueError) as the reference does — the batch form flags them"""
+    from kart_amd import dataset as D
+    from kart_amd import output as OUT
+
+    g = D.Geometry(_gpkg(typ, le, extra, env))
+    data, off = np.frombuffer(bytes(g), np.uint8), np.array([0, len(g)], np.uint64)
+    labels, bad = OUT.geometry_type_names(data, off)
+    if want is None:
+        with pytest.raises(ValueError):
+            OUT.feature_field_as_text({"g": g}, "g", "")
+        assert bad.tolist() == [0]
+        return
+    line = OUT.feature_field_as_text({"g": g}, "g", "")
+    label = want if want.endswith("EMPTY") else f"{want}(...)"
+    assert line == " " * 39 + "g = " + label
+    assert labels[0] == label and bad.size == 0
+
+
+def test_geometry_type_names_batch_equals_per_value():
+    from kart_amd import dataset as D
+    from kart_amd import output as OUT
+
+    rng = np.random.default_rng(4)
+    geoms = _mixed_geoms(rng, 3000) + [_gpkg(t, bool(rng.integers(2)), int(rng.integers(2)) * 0x10, int(rng.integers(5)))
+                                      for t in rng.choice([1, 3, 6, 1001, 2003, 3006, 0x80000002, 9, 17], 500)]
+    vals = [b"" if g is None else bytes(g) for g in geoms]
+    off = np.zeros(len(vals) + 1, np.uint64)
+    off[1:] = np.cumsum([len(v) for v in vals])
+    labels, bad = OUT.geometry_type_names(np.frombuffer(b"".join(vals), np.uint8), off)
+    badset = set(bad.tolist())
+    for i, v in enumerate(vals):
+        if not v:
+            assert labels[i] is None and i not in badset
+            continue
+        try:
+            want = OUT.feature_field_as_text({"g": D.Geometry(v)}, "g", "").split(" = ", 1)[1]
+        except (ValueError, struct.error, IndexError):
+            assert i in badset
+            continue
+        assert i not in badset and labels[i] == want
