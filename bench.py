@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--no-sort", action="store_true",
                     help="c2/c3: skip the with-sort steps (sides from git walk order, both GPU sorts in the step)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--arena", action="store_true",
+                    help="c5: filter from the blob arenas (kd_geom_filter) instead of the geometry heads")
+    ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
@@ -544,7 +547,9 @@ def run_c5(args, H):
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     cols = GeomCols(ver, ver, "geom", "geom")
     eng = engine_for(H)
-    pipe = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits)
+    heads = not args.arena
+    pipe = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits,
+                          heads=heads)
     for _ in range(max(1, args.warmup)):
         pipe.step()
     eng.sync()
@@ -558,30 +563,51 @@ def run_c5(args, H):
         assert codes.max() <= 4 and not (codes == 3).any(), "fallback codes on synthetic polygons"
         assert ((delta[:, 0] == 0xFFFFFFFF) == (codes[:, 0] == 4)).all() and \
             ((delta[:, 1] == 0xFFFFFFFF) == (codes[:, 1] == 4)).all()
+    kname = "k_gf_heads" if heads else "k_gf_match"
     eng.prof_reset()
-    eng.prof_select(None if args.time_all else ["k_gf_match"])
+    eng.prof_select(None if args.time_all else [kname])
     eng.prof_enable(not args.no_events)
     elapsed = timed(H, eng, pipe.step, args.steps)
     eng.prof_enable(False)
-    kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_gf_match", "k_gf_scan", "k_gf_place"))
+    kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", kname, "k_gf_scan", "k_gf_place"))
     n_pairs = L.base.n + L.n_insert
     total_pairs = sum(H.allgather(n_pairs))
-    # algorithmic bytes per k_gf_match launch: the delta pairs (8 B); per present side its offsets
-    # (16 B) and the blob head up to the end of the GPKG envelope (<= 96 B); codes (2 B) + index
-    # envelope (bits/2 + 1 B) written per delta
-    ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
-    head = 0
-    for col, off in ((delta[:, 0], ob_off), (delta[:, 1], nb_off)):
-        pres = col[col != 0xFFFFFFFF].astype(np.int64)
-        head += int(np.minimum(off[pres + 1] - off[pres], 96).sum()) + 16 * pres.size
     nd = counts["deltas"]
-    alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
-    roof = roofline(kern, "k_gf_match", alg, args.traffic_json, n)
+    ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
+    if heads:
+        # algorithmic bytes per k_gf_heads launch: the delta pairs (8 B), one 48-B head per present
+        # side, codes (2 B) + index envelope (bits/2 + 1 B) written per delta
+        pres = int((delta[:, 0] != 0xFFFFFFFF).sum() + (delta[:, 1] != 0xFFFFFFFF).sum())
+        alg = 8 * nd + 48 * pres + nd * (2 + bits // 2 + 1)
+    else:
+        # per k_gf_match launch: the delta pairs (8 B); per present side its offsets (16 B) and the
+        # blob head up to the end of the GPKG envelope (<= 96 B); codes + index envelope written
+        head = 0
+        for col, off in ((delta[:, 0], ob_off), (delta[:, 1], nb_off)):
+            prs = col[col != 0xFFFFFFFF].astype(np.int64)
+            head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
+        alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
+    roof = roofline(kern, kname, alg, args.traffic_json, n)
+    arena_path = None
+    if heads and not args.no_arena_timing:  # the same step through kd_geom_filter (blob arenas, msgpack walk)
+        pa = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits)
+        pa.step()
+        eng.sync()
+        eng.prof_reset()
+        eng.prof_select(["k_gf_match"])
+        eng.prof_enable(not args.no_events)
+        el_a = timed(H, eng, pa.step, args.steps)
+        eng.prof_enable(False)
+        ka = kernel_times(eng, ("k_gf_match",))
+        arena_path = {"value": round(total_pairs * args.steps / el_a / 1e6, 2),
+                      "ms_per_step": round(el_a / args.steps * 1e3, 4),
+                      "kernels_avg_ms": {k: round(v[1], 5) for k, v in ka.items()}}
+        del pa
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_filter(L, delta, codes, keep, enc, enc_ok, args, bits)
     eng.close()
-    return {
+    out = {
         "metric": METRIC, "value": round(total_pairs * args.steps / elapsed / 1e6, 2), "unit": "M feature-pairs/s",
         "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -590,33 +616,78 @@ def run_c5(args, H):
         "data": "synthetic (the C3 MULTIPOLYGON layer; blobs materialised for every delta's old/new version)",
         "config": {"workload": f"C5: spatially filtered diff of ONE {n}-feature polygon layer"
                                f"{f' split into {H.world} bucket-range shards' if H.world > 1 else ''}: classify2 + "
-                               "per-delta geometry envelope filter + EnvelopeEncoder of the new side",
+                               "per-delta geometry envelope filter + EnvelopeEncoder of the new side" +
+                               (" (from the 48-B geometry heads the blob reader extracts on the host: kd_geom_heads)"
+                                if heads else " (msgpack walk of the blob arenas on the GPU)"),
                    "features": n, "pairs_per_step": total_pairs, "deltas_per_step": sum(H.allgather(nd)),
                    "kept_per_step": sum(H.allgather(counts["kept"])), "bits": bits, "filter": list(synth.C5_FILTER),
                    "parallelism": f"bucket-range shards x{H.world} (counts per rank, no exchange)"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
         "roofline": roof, "cpu_baseline": cpu,
     }
+    if heads:
+        blobs = (L.base_blobs[1].shape[0] - 1) + (L.target_blobs[1].shape[0] - 1)
+        out["host"] = {"geom_heads_s": round(pipe.heads_s, 4), "blobs": int(blobs),
+                       "geom_heads_M_blobs_per_s": round(blobs / pipe.heads_s / 1e6, 2),
+                       "note": "kd_geom_heads: the blob reader's host pass (msgpack walk of every materialised blob, "
+                               f"{host_cores()} threads) that leaves 48 B per blob for the GPU; outside the timed step"}
+        out["arena_path"] = arena_path
+    return out
 
 
 def cpu_baseline_filter(L, delta, codes, keep, enc, enc_ok, args, bits):
-    """the oracle's classify2 + geom_filter restatement on a bounded sample (1 thread, Python +
-    C): the first deltas of the layer; it doubles as a bit-exact check of the device results"""
+    """The C oracle's classify2 + filtered-diff decision (kdo_classify2 + kdo_geom_filter: msgpack walk,
+    envelope, bbox, EnvelopeEncoder) on the host cores over bucket-range shards of the whole layer,
+    and one thread over one shard.  The first shard doubles as a bit-exact check of the device codes."""
+    from concurrent.futures import ThreadPoolExecutor
+
     O = oracle()
-    m = min(delta.shape[0], 20000)
     cols = {h: 0 for h in L.legends}
     (od, oo), (nd, no) = L.base_blobs, L.target_blobs
-    t0 = time.perf_counter()
-    oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta[:m], cols, cols, synth_filter(), False, bits)
-    dt = time.perf_counter() - t0
-    if not args.no_check:
+    cores = host_cores()
+    parts = 4 * cores
+    ba, bb = _shard_bounds(L, parts)
+    filt = synth_filter()
+
+    def shard(s):
+        A, B = L.base, L.target
+        a0, a1, b0, b1 = int(ba[s]), int(ba[s + 1]), int(bb[s]), int(bb[s + 1])
+        d, c = O.classify2(A.key[a0:a1], A.oid[a0:a1], B.key[b0:b1], B.oid[b0:b1])
+        g = d.astype(np.int64)
+        g[:, 0] = np.where(d[:, 0] == O.NONE, O.NONE, g[:, 0] + a0)
+        g[:, 1] = np.where(d[:, 1] == O.NONE, O.NONE, g[:, 1] + b0)
+        res = O.geom_filter(od, oo, nd, no, g.astype(np.uint32), cols, cols, filt, False, bits)
+        return (a1 - a0) + c["inserts"], g.astype(np.uint32), res
+
+    if not args.no_check:  # shard 0 against the device's first deltas
+        _, g0, (oc, okeep, oenc, ook) = shard(0)
+        m = g0.shape[0]
+        assert np.array_equal(delta[:m], g0), "classify2 differs from the oracle"
         assert np.array_equal(codes[:m], oc), "kd_geom_filter codes differ from the oracle"
         assert np.array_equal(keep[keep < m], okeep), "kept deltas differ from the oracle"
         assert np.array_equal(enc_ok[:m], ook) and np.array_equal(enc[:m][ook == 1], oenc[ook == 1])
-    rate = m / dt / 1e6
-    return {"value": round(rate, 4), "unit": "M deltas/s", "cores": 1, "kind": "port",
-            "sample": f"first {m} deltas of the layer: oracle geom_filter (msgpack decode + kd_oracle.c envelope, "
-                      f"bbox, EnvelopeEncoder), 1 thread, {dt:.1f}s; the classify2 leg is C2/C3's baseline"}
+    with ThreadPoolExecutor(cores) as ex:
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            pairs = sum(r[0] for r in ex.map(shard, range(parts)))
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    reps1 = 0
+    while True:
+        p1 = shard(0)[0]
+        reps1 += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds / 2:
+            break
+    dt1 = time.perf_counter() - t0
+    return {"value": round(pairs * reps / dt / 1e6, 2), "unit": "M feature-pairs/s", "cores": cores, "kind": "port",
+            "sample": f"the full C5 layer ({pairs} pairs) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c classify2 + "
+                      f"geom_filter on {cores} threads over {parts} bucket-range shards",
+            "one_thread": {"value": round(p1 * reps1 / dt1 / 1e6, 3), "unit": "M feature-pairs/s", "cores": 1,
+                           "sample": f"one shard ({p1} pairs, 1/{parts} of the layer) x {reps1} reps in {dt1:.1f}s"}}
 
 
 def synth_filter():

@@ -21,7 +21,8 @@
  *                     spatial filter over a batch of object ids against feature_envelopes.
  *   kd_geom_filter <- BaseDiffWriter.filtered_ds_feature_deltas (kart/base_diff_writer.py:279-329):
  *                     the geometry of each delta's old/new feature blob, envelope-tested, kept
- *                     deltas compacted on the GPU.
+ *                     deltas compacted on the GPU.  kd_geom_heads + kd_geom_filter_heads: the same
+ *                     from 48-byte geometry heads the blob reader extracts on the host.
  *   kd_hex_encode  <- Geometry.to_hex_wkb / gpkg_geom_to_hex_wkb (kart/geometry.py:346-375) and
  *                     bytes.hex(v), as feature_as_json formats them (kart/feature_output.py:34-56).
  *   kd_diff2_sharded / kd_diff2_gather
@@ -245,6 +246,32 @@ int kd_geom_filter(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_blobs* new_b
                    uint64_t n, const uint64_t* d_n, uint32_t pairs_mem, const kd_geom_cols* cols,
                    const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
                    uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem);
+
+/* Geometry heads (host, multithreaded): the filtered diff from 48 contiguous bytes per blob.  For
+ * each feature blob (msgpack [legend_hex, [values]]) the geometry column's value is located as
+ * msgpack.unpackb + Dataset3.get_feature would (kart/dataset3.py:185-223; the whole blob validated:
+ * nested values skipped, trailing bytes refused) and its GPKG bytes summarised: */
+#define KD_GH_GEOM 0u     /* a geometry: gpkg[] = its first min(glen, 40) bytes (header + XY envelope) */
+#define KD_GH_NULL 2u     /* null geometry, or no geometry column in the blob's legend (MATCHING)    */
+#define KD_GH_FALLBACK 3u /* malformed blob, unknown legend, value not an ext 'G': the caller decides */
+typedef struct kd_geom_head {
+    uint8_t gpkg[40];
+    uint32_t glen;        /* GPKG value length                                                        */
+    uint32_t goff_status; /* (status << 24) | offset of the GPKG value in its blob (< 2^24)           */
+} kd_geom_head;
+/* n_leg legends (40-byte hex each) with gidx[l] = the geometry value's index (-1: none); threads
+ * 0 = up to 16.  Blob i = data[off[i] .. off[i+1]) (host memory). */
+int kd_geom_heads(const uint8_t* data, const uint64_t* off, uint64_t n, int n_leg, const uint8_t* leg_hex,
+                  const int16_t* gidx, int threads, kd_geom_head* out);
+/* kd_geom_filter from the heads: same codes, keep list and index envelopes.  heads_old [n_old] /
+ * heads_new [n_new] in heads_mem; pairs index them.  A geometry whose decode needs bytes past its
+ * head (an XYZ/XYM/XYZM envelope, a NaN envelope) is read from old_blobs / new_blobs (the arenas
+ * the heads came from, device or host); with NULL arenas such a side is 3 FALLBACK. */
+int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_old, const kd_geom_head* heads_new,
+                         uint64_t n_new, uint32_t heads_mem, const kd_blobs* old_blobs, const kd_blobs* new_blobs,
+                         const uint32_t* pairs, uint64_t n, const uint64_t* d_n, uint32_t pairs_mem,
+                         const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
+                         uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem);
 
 /* -------- writer formatting -------- */
 #define KD_HEX_BYTES 0u    /* bytes.hex(v): lowercase hex of every byte of every blob                */

@@ -28,6 +28,7 @@ KD_COPY_H2D = 1
 KD_COPY_D2H = 2
 KD_COPY_D2D = 3
 KD_COMM_ID_BYTES = 128
+KD_GH_GEOM, KD_GH_NULL, KD_GH_FALLBACK = 0, 2, 3
 KD_GF_RECT = 0x1
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -179,6 +180,15 @@ SIGNATURES = {
     "kd_env_overlap": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, c_dblp, ctypes.c_void_p,
+         ctypes.c_uint32],
+    ),
+    "kd_geom_heads": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "kd_geom_filter_heads": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, c_dblp,
+         ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c_u64p, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_uint32],
     ),
     "kd_shard_cuts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,

@@ -379,6 +379,103 @@ __global__ __launch_bounds__(GF_NT) void k_gf_match(GfArgs a) {
     }
 }
 
+// ---- the heads form: one 48-B geometry head per blob side (kd_geom_heads), no msgpack walk ----
+struct GfHeadArgs {
+    const kd_geom_head* head[2];
+    u64 nhead[2];
+    const u8* data[2];  // the arenas the heads came from (null: no slow path, such sides FALLBACK)
+    const u64* off[2];
+};
+
+__device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g, int s, u32 bi, GHit& h) {
+    typedef const __attribute__((address_space(1))) u32x4* gx4;
+    h.r = -1;
+    h.pc = -1;
+    h.empty = false;
+    if (bi == KD_NONE) { h.code = GF_NONE; return; }
+    if ((u64)bi >= g.nhead[s]) { h.code = GF_FALLBACK; return; }
+    const u64 base = (u64)(g.head[s] + bi);
+    const u32x4 v0 = *(gx4)base, v1 = *(gx4)(base + 16), v2 = *(gx4)(base + 32);
+    const u32 st = v2.w >> 24;
+    if (st == KD_GH_NULL) { h.code = GF_MATCH; return; }
+    if (st != KD_GH_GEOM) { h.code = GF_FALLBACK; return; }
+    const u32 glen = v2.z;
+    const u32 r[11] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, 0u};
+    u8 hflags = (u8)(v0.x >> 24);
+    const bool fast = env_fast(r, glen, h.r, h.e, h.pc, h.pe);
+    if (!fast) {  // XYZ/XYM/XYZM envelope or a NaN one: the byte-wise decode on the blob
+        if (!g.data[s]) { h.code = GF_FALLBACK; h.r = -1; return; }
+        const u8* gp = g.data[s] + g.off[s][bi] + (v2.w & 0xFFFFFFu);
+        h.r = gpkg_env(gp, glen, h.e);
+        h.pc = -1;
+        if (h.r == 0 || h.r == 2) h.pc = point_env(gp, glen, h.pe);
+        if (h.r >= 0) hflags = gp[3];
+    }
+    if (h.r != 1 && h.pc >= 0) {
+        h.e[0] = h.pe[0]; h.e[1] = h.pe[1]; h.e[2] = h.pe[2]; h.e[3] = h.pe[3];
+    }
+    h.code = geom_code(a, h, hflags);
+}
+
+// k_gf_match over heads: the same tiles, codes, kept counts and index envelopes
+__global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
+    __shared__ u8 s_enc[GF_NT * 16];
+    __shared__ u8 s_ok[GF_NT];
+    __shared__ u32 s_wc[GF_NT / 64];
+    const int tid = threadIdx.x;
+    const u64 n = a.d_n ? *a.d_n : a.cap;
+    const int nb = a.bits / 2;
+    const double vmax = (double)((1ull << a.bits) - 1);
+    const u64 t0 = (u64)blockIdx.x * GF_TILE;
+    u32 kept = 0;
+    for (int rd = 0; rd < GF_ROUNDS; rd++) {
+        const u64 d0 = t0 + (u64)rd * GF_NT;
+        if (d0 >= n) break;  // block-uniform
+        const u64 d = d0 + tid;
+        bool keep = false;
+        u8 ok = 0;
+        if (a.enc)
+            for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
+        if (d < n) {
+            const uint2 pr = *(const uint2*)(a.pairs + 2 * d);
+            GHit h;
+            decode_head(a, g, 0, pr.x, h);
+            const int co = h.code;
+            decode_head(a, g, 1, pr.y, h);
+            const int cn = h.code;
+            keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
+            *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
+            if (a.enc && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
+                ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { s_enc[tid * nb + k] = v; });
+        }
+        const u64 bal = __ballot(keep);
+        kept += (u32)__popcll(bal);
+        if (a.enc) {
+            s_ok[tid] = ok;
+            __syncthreads();
+            const u32 cnt = (u32)(n - d0 < GF_NT ? n - d0 : GF_NT);
+            u8* dst = a.enc + d0 * nb;
+            const u32 bytes = cnt * nb;
+            if ((((u64)dst) & 3) == 0) {
+                const u32 nw = bytes >> 2;
+                for (u32 k = tid; k < nw; k += GF_NT) ((u32*)dst)[k] = ((const u32*)s_enc)[k];
+                for (u32 k = 4 * nw + tid; k < bytes; k += GF_NT) dst[k] = s_enc[k];
+            } else {
+                for (u32 k = tid; k < bytes; k += GF_NT) dst[k] = s_enc[k];
+            }
+            for (u32 k = tid; k < cnt; k += GF_NT) a.enc_ok[d0 + k] = s_ok[k];
+            __syncthreads();
+        }
+    }
+    if ((tid & 63) == 0) s_wc[tid >> 6] = kept;
+    __syncthreads();
+    if (tid == 0) {
+        u32 t = 0;
+        for (int w = 0; w < GF_NT / 64; w++) t += s_wc[w];
+        a.tile_cnt[blockIdx.x] = t;
+    }
+}
+
 // one block: exclusive scan of the tile counts in place, the total to *n_keep
 __global__ __launch_bounds__(1024) void k_gf_scan(u32* __restrict__ cnt, u32 ntiles, u64* __restrict__ n_keep) {
     __shared__ u32 s_w[16];
@@ -441,6 +538,79 @@ __global__ __launch_bounds__(GF_NT) void k_gf_place(const u8* __restrict__ match
     }
 }
 
+
+// the launches and result copies shared by kd_geom_filter (arenas) and kd_geom_filter_heads (heads)
+static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* pairs, uint64_t n, const uint64_t* d_n,
+                  uint32_t pairs_mem, const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
+                  uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem) {
+    int rc;
+    const void* dp;
+    if ((rc = stage_in(ctx, "gf.pairs", n ? (const void*)pairs : nullptr, n ? n * 8 : 0, pairs_mem, &dp))) return rc;
+    const u64 tiles = (n + GF_TILE - 1) / GF_TILE;
+    KD_CHECK(tiles < (1ull << 31), "kd_geom_filter: too many deltas");
+    u8* dm = match;
+    u32* dk = keep;
+    u8 *de = enc, *dok = enc_ok;
+    const int nb = bits / 2;
+    void *t_cnt, *t_nk;
+    if ((rc = ensure(ctx, "gf.tiles", (tiles + 1) * 4, &t_cnt)) || (rc = ensure(ctx, "gf.nk", 8, &t_nk))) return rc;
+    if (out_mem == KD_MEM_HOST) {
+        void *x, *y, *z = nullptr, *w = nullptr;
+        if ((rc = ensure(ctx, "gf.match", 2 * n + 2, &x)) || (rc = ensure(ctx, "gf.keep", 4 * n + 4, &y))) return rc;
+        if (enc && ((rc = ensure(ctx, "gf.enc", n * nb + 4, &z)) || (rc = ensure(ctx, "gf.encok", n + 4, &w)))) return rc;
+        dm = (u8*)x; dk = (u32*)y; de = (u8*)z; dok = (u8*)w;
+    }
+    a.pairs = (const u32*)dp;
+    a.cap = n;
+    a.d_n = d_n;
+    a.f0 = filt_env[0]; a.f1 = filt_env[1]; a.f2 = filt_env[2]; a.f3 = filt_env[3];
+    a.rect = (flags & KD_GF_RECT) ? 1 : 0;
+    a.bits = enc ? bits : 2;
+    a.match = dm;
+    a.enc = enc ? de : nullptr;
+    a.enc_ok = enc ? dok : nullptr;
+    a.tile_cnt = (u32*)t_cnt;
+    KD_HIP(hipMemsetAsync(t_nk, 0, 8, ctx->stream));
+    if (tiles) {
+        if (g) {
+            if ((rc = launch(ctx, "k_gf_heads", [&] {
+                     hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a, *g);
+                 })))
+                return rc;
+        } else if ((rc = launch(ctx, "k_gf_match", [&] {
+                        hipLaunchKernelGGL(k_gf_match, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a);
+                    })))
+            return rc;
+        if ((rc = launch(ctx, "k_gf_scan", [&] {
+                 hipLaunchKernelGGL(k_gf_scan, dim3(1), dim3(1024), 0, ctx->stream, (u32*)t_cnt, (u32)tiles, (u64*)t_nk);
+             })))
+            return rc;
+        if ((rc = launch(ctx, "k_gf_place", [&] {
+                 hipLaunchKernelGGL(k_gf_place, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, (const u8*)dm, n, d_n,
+                                    (const u32*)t_cnt, dk);
+             })))
+            return rc;
+    }
+    if (out_mem == KD_MEM_DEVICE) {
+        KD_HIP(hipMemcpyAsync(n_keep, t_nk, 8, hipMemcpyDeviceToDevice, ctx->stream));
+        return KD_OK;
+    }
+    u64 nk = 0;
+    KD_HIP(hipMemcpyAsync(&nk, t_nk, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KD_HIP(hipStreamSynchronize(ctx->stream));
+    if (n) {
+        KD_HIP(hipMemcpyAsync(match, dm, 2 * n, hipMemcpyDeviceToHost, ctx->stream));
+        if (nk) KD_HIP(hipMemcpyAsync(keep, dk, 4 * nk, hipMemcpyDeviceToHost, ctx->stream));
+        if (enc) {
+            KD_HIP(hipMemcpyAsync(enc, de, n * nb, hipMemcpyDeviceToHost, ctx->stream));
+            KD_HIP(hipMemcpyAsync(enc_ok, dok, n, hipMemcpyDeviceToHost, ctx->stream));
+        }
+    }
+    KD_HIP(hipStreamSynchronize(ctx->stream));
+    *n_keep = nk;
+    return prof_flush(ctx);
+}
+
 }  // namespace kd
 
 using namespace kd;
@@ -495,64 +665,57 @@ extern "C" int kd_geom_filter(kd_ctx* ctx, const kd_blobs* old_blobs, const kd_b
         a.gidx[s] = (const i16*)dg;
         a.n_leg[s] = nl[s];
     }
-    const void* dp;
-    if ((rc = stage_in(ctx, "gf.pairs", n ? (const void*)pairs : nullptr, n ? n * 8 : 0, pairs_mem, &dp))) return rc;
-    const u64 tiles = (n + GF_TILE - 1) / GF_TILE;
-    KD_CHECK(tiles < (1ull << 31), "kd_geom_filter: too many deltas");
-    u8* dm = match;
-    u32* dk = keep;
-    u8 *de = enc, *dok = enc_ok;
-    const int nb = bits / 2;
-    void *t_cnt, *t_nk;
-    if ((rc = ensure(ctx, "gf.tiles", (tiles + 1) * 4, &t_cnt)) || (rc = ensure(ctx, "gf.nk", 8, &t_nk))) return rc;
-    if (out_mem == KD_MEM_HOST) {
-        void *x, *y, *z = nullptr, *w = nullptr;
-        if ((rc = ensure(ctx, "gf.match", 2 * n + 2, &x)) || (rc = ensure(ctx, "gf.keep", 4 * n + 4, &y))) return rc;
-        if (enc && ((rc = ensure(ctx, "gf.enc", n * nb + 4, &z)) || (rc = ensure(ctx, "gf.encok", n + 4, &w)))) return rc;
-        dm = (u8*)x; dk = (u32*)y; de = (u8*)z; dok = (u8*)w;
-    }
-    a.pairs = (const u32*)dp;
-    a.cap = n;
-    a.d_n = d_n;
-    a.f0 = filt_env[0]; a.f1 = filt_env[1]; a.f2 = filt_env[2]; a.f3 = filt_env[3];
-    a.rect = (flags & KD_GF_RECT) ? 1 : 0;
-    a.bits = enc ? bits : 2;
-    a.match = dm;
-    a.enc = enc ? de : nullptr;
-    a.enc_ok = enc ? dok : nullptr;
-    a.tile_cnt = (u32*)t_cnt;
-    KD_HIP(hipMemsetAsync(t_nk, 0, 8, ctx->stream));
-    if (tiles) {
-        if ((rc = launch(ctx, "k_gf_match", [&] {
-                 hipLaunchKernelGGL(k_gf_match, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a);
-             })))
+    return gf_run(ctx, a, nullptr, pairs, n, d_n, pairs_mem, filt_env, flags, bits, match, keep, n_keep, enc, enc_ok,
+                  out_mem);
+}
+
+extern "C" int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_old,
+                                    const kd_geom_head* heads_new, uint64_t n_new, uint32_t heads_mem,
+                                    const kd_blobs* old_blobs, const kd_blobs* new_blobs, const uint32_t* pairs,
+                                    uint64_t n, const uint64_t* d_n, uint32_t pairs_mem, const double filt_env[4],
+                                    uint32_t flags, int bits, uint8_t* match, uint32_t* keep, uint64_t* n_keep,
+                                    uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem) {
+    KD_CHECK(ctx && filt_env && match && keep && n_keep, "kd_geom_filter_heads: NULL argument");
+    KD_CHECK((n_old == 0 || heads_old) && (n_new == 0 || heads_new), "kd_geom_filter_heads: heads NULL");
+    KD_CHECK(n == 0 || pairs, "kd_geom_filter_heads: pairs NULL");
+    KD_CHECK(d_n == nullptr || (out_mem == KD_MEM_DEVICE && pairs_mem == KD_MEM_DEVICE),
+             "kd_geom_filter_heads: a device count needs device pairs and outputs");
+    KD_CHECK(filt_env[0] <= filt_env[1] && filt_env[2] <= filt_env[3], "kd_geom_filter_heads: inverted filter envelope");
+    KD_CHECK(!enc || (enc_ok && bits >= 2 && bits <= 32 && bits % 2 == 0),
+             "kd_geom_filter_heads: bits must be even and <= 32");
+    KD_CHECK(!old_blobs == !new_blobs, "kd_geom_filter_heads: both arenas or neither");
+    KD_HIP(hipSetDevice(ctx->device));
+    static_assert(sizeof(kd_geom_head) == 48, "kd_geom_head is 48 bytes");
+    int rc;
+    GfArgs a{};
+    GfHeadArgs g{};
+    const kd_geom_head* hs[2] = {heads_old, heads_new};
+    const u64 nh[2] = {n_old, n_new};
+    const char* htag[2] = {"gh.o", "gh.n"};
+    for (int s = 0; s < 2; s++) {
+        const void* dh;
+        if ((rc = stage_in(ctx, htag[s], nh[s] ? (const void*)hs[s] : nullptr, nh[s] * sizeof(kd_geom_head), heads_mem, &dh)))
             return rc;
-        if ((rc = launch(ctx, "k_gf_scan", [&] {
-                 hipLaunchKernelGGL(k_gf_scan, dim3(1), dim3(1024), 0, ctx->stream, (u32*)t_cnt, (u32)tiles, (u64*)t_nk);
-             })))
-            return rc;
-        if ((rc = launch(ctx, "k_gf_place", [&] {
-                 hipLaunchKernelGGL(k_gf_place, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, (const u8*)dm, n, d_n,
-                                    (const u32*)t_cnt, dk);
-             })))
-            return rc;
+        KD_CHECK(((u64)dh & 15) == 0, "kd_geom_filter_heads: heads must be 16-byte aligned");
+        g.head[s] = (const kd_geom_head*)dh;
+        g.nhead[s] = nh[s];
     }
-    if (out_mem == KD_MEM_DEVICE) {
-        KD_HIP(hipMemcpyAsync(n_keep, t_nk, 8, hipMemcpyDeviceToDevice, ctx->stream));
-        return KD_OK;
-    }
-    u64 nk = 0;
-    KD_HIP(hipMemcpyAsync(&nk, t_nk, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KD_HIP(hipStreamSynchronize(ctx->stream));
-    if (n) {
-        KD_HIP(hipMemcpyAsync(match, dm, 2 * n, hipMemcpyDeviceToHost, ctx->stream));
-        if (nk) KD_HIP(hipMemcpyAsync(keep, dk, 4 * nk, hipMemcpyDeviceToHost, ctx->stream));
-        if (enc) {
-            KD_HIP(hipMemcpyAsync(enc, de, n * nb, hipMemcpyDeviceToHost, ctx->stream));
-            KD_HIP(hipMemcpyAsync(enc_ok, dok, n, hipMemcpyDeviceToHost, ctx->stream));
+    if (old_blobs) {
+        const kd_blobs* bl[2] = {old_blobs, new_blobs};
+        const char* tag[2][2] = {{"gf.od", "gf.oo"}, {"gf.nd", "gf.no"}};
+        for (int s = 0; s < 2; s++) {
+            const kd_blobs* B = bl[s];
+            KD_CHECK(B->n == nh[s], "kd_geom_filter_heads: arena %d holds %llu blobs, %llu heads", s,
+                     (unsigned long long)B->n, (unsigned long long)nh[s]);
+            const void *dd, *doff;
+            const u64 bytes = B->mem == KD_MEM_HOST ? (B->n ? B->off[B->n] : 0) : 0;
+            if ((rc = stage_in(ctx, tag[s][1], B->off, (B->n + 1) * 8, B->mem, &doff))) return rc;
+            if ((rc = stage_in(ctx, tag[s][0], B->data, bytes ? bytes : 1, B->mem, &dd))) return rc;
+            g.data[s] = (const u8*)dd;
+            g.off[s] = (const u64*)doff;
         }
     }
-    KD_HIP(hipStreamSynchronize(ctx->stream));
-    *n_keep = nk;
-    return prof_flush(ctx);
+    a.nblob[0] = n_old;
+    a.nblob[1] = n_new;
+    return gf_run(ctx, a, &g, pairs, n, d_n, pairs_mem, filt_env, flags, bits, match, keep, n_keep, enc, enc_ok, out_mem);
 }

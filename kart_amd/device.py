@@ -281,7 +281,8 @@ class FilterPipeline:
     encodes the new side's index envelopes — BaseDiffWriter.filtered_ds_feature_deltas's work for a
     whole layer in one stream."""
 
-    def __init__(self, engine, base, target, base_blobs, target_blobs, geom_cols, filt_env, rectangle=False, bits=20):
+    def __init__(self, engine, base, target, base_blobs, target_blobs, geom_cols, filt_env, rectangle=False, bits=20,
+                 heads=False):
         import ctypes as _c
 
         self.eng = engine
@@ -305,6 +306,19 @@ class FilterPipeline:
         self._kc = geom_cols.kd_cols()
         self._fe = (_c.c_double * 4)(*[float(x) for x in filt_env])
         self.flags = N.KD_GF_RECT if rectangle else 0
+        self.heads = None
+        self.heads_s = None
+        if heads:  # the blob reader's host pass, then 48 bytes per blob in HBM (kd_geom_filter_heads)
+            import time
+
+            from .spatial import geom_heads
+
+            t0 = time.perf_counter()
+            hs = [geom_heads(*base_blobs, geom_cols.old_hex, geom_cols.old_gidx, len(geom_cols.old_map)),
+                  geom_heads(*target_blobs, geom_cols.new_hex, geom_cols.new_gidx, len(geom_cols.new_map))]
+            self.heads_s = time.perf_counter() - t0
+            self.heads = [(DevBuf.from_numpy(engine, h.view(np.uint8).reshape(-1)) if h.size else DevBuf(engine, 48), h.size)
+                          for h in hs]
         engine.reserve(max(base.n, target.n))
         engine.sync()
 
@@ -312,6 +326,16 @@ class FilterPipeline:
         L, ctx = self.eng.L, self.eng.ctx
         N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), 0, self.delta.ptr, self.upd.ptr,
                                   self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
+        if self.heads is not None:
+            (ho, no), (hn, nn) = self.heads
+            N.check(L.kd_geom_filter_heads(ctx, ho.ptr, no, hn.ptr, nn, N.KD_MEM_DEVICE, ctypes.byref(self._ob),
+                                           ctypes.byref(self._nb), self.delta.ptr, self.cap,
+                                           ctypes.cast(self.counts.ptr + 24, N.c_u64p), N.KD_MEM_DEVICE, self._fe,
+                                           self.flags, self.bits, self.match.ptr, self.keep.ptr,
+                                           ctypes.cast(self.n_keep.ptr, N.c_u64p), self.enc.ptr if self.enc else None,
+                                           self.enc_ok.ptr if self.enc_ok else None, N.KD_MEM_DEVICE),
+                    "kd_geom_filter_heads")
+            return
         N.check(L.kd_geom_filter(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.delta.ptr, self.cap,
                                  ctypes.cast(self.counts.ptr + 24, N.c_u64p), N.KD_MEM_DEVICE, ctypes.byref(self._kc),
                                  self._fe, self.flags, self.bits, self.match.ptr, self.keep.ptr,

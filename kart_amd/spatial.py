@@ -276,6 +276,55 @@ def geom_filter(engine, old_arena, new_arena, pairs, cols, filt_env, rectangle=F
     return match[:n], keep[:k], (enc[:n] if bits else None), (ok[:n] if bits else None)
 
 
+# kd_geom_head: the first 40 bytes of a blob's geometry value, its length, (status << 24) | offset
+GEOM_HEAD = np.dtype([("gpkg", np.uint8, 40), ("glen", "<u4"), ("goff_status", "<u4")])
+
+
+def geom_heads(data, off, hexarr, gidx, n_leg, threads=0):
+    """kd_geom_heads over a host arena of feature blobs: one 48-byte head per blob (status
+    KD_GH_GEOM / KD_GH_NULL / KD_GH_FALLBACK in the top byte of goff_status)"""
+    data = np.ascontiguousarray(data, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    n = int(off.shape[0]) - 1
+    out = np.zeros(max(n, 1), GEOM_HEAD)
+    N.check(N.lib().kd_geom_heads(N.ptr(data) if data.size else N.ptr(_PAD), N.ptr(off), n, int(n_leg), N.ptr(hexarr),
+                                  N.ptr(gidx), int(threads), out.ctypes.data), "kd_geom_heads")
+    return out[:n]
+
+
+def geom_filter_heads(engine, old_heads, new_heads, pairs, filt_env, rectangle=False, bits=0, arenas=None):
+    """kd_geom_filter_heads over host heads: (codes uint8 [n, 2], keep uint32 [k], enc, enc_ok).
+    ``arenas`` ((od, oo), (nd, no)) for the geometries whose decode needs more than their head;
+    without them such sides come back 3 (FALLBACK: the host decides)."""
+    pairs = np.ascontiguousarray(pairs, np.uint32).reshape(-1, 2)
+    n = pairs.shape[0]
+    hs = [np.ascontiguousarray(h, GEOM_HEAD) for h in (old_heads, new_heads)]
+    blobs = [None, None]
+    if arenas is not None:
+        for s, (d, o) in enumerate(arenas):
+            b = N.KdBlobs()
+            b.n = int(o.shape[0]) - 1
+            b.data = N.ptr(d) if d.size else N.ptr(_PAD)
+            b.off = N.ptr(o)
+            b.mem = N.KD_MEM_HOST
+            blobs[s] = b
+    match = np.zeros((max(n, 1), 2), np.uint8)
+    keep = np.zeros(max(n, 1), np.uint32)
+    nk = ctypes.c_uint64()
+    nb = bits // 2
+    enc = np.zeros((max(n, 1), max(nb, 1)), np.uint8) if bits else None
+    ok = np.zeros(max(n, 1), np.uint8) if bits else None
+    fe = (ctypes.c_double * 4)(*[float(x) for x in filt_env])
+    N.check(engine.L.kd_geom_filter_heads(
+        engine.ctx, hs[0].ctypes.data if hs[0].size else None, hs[0].shape[0], hs[1].ctypes.data if hs[1].size else None,
+        hs[1].shape[0], N.KD_MEM_HOST, ctypes.byref(blobs[0]) if blobs[0] else None,
+        ctypes.byref(blobs[1]) if blobs[1] else None, N.ptr(pairs), n, None, N.KD_MEM_HOST, fe,
+        N.KD_GF_RECT if rectangle else 0, int(bits), N.ptr(match), N.ptr(keep), ctypes.byref(nk), N.ptr(enc), N.ptr(ok),
+        N.KD_MEM_HOST), "kd_geom_filter_heads")
+    k = int(nk.value)
+    return match[:n], keep[:k], (enc[:n] if bits else None), (ok[:n] if bits else None)
+
+
 def _blob_of(kv):
     """the LazyBlob behind a delta half's lazy value (Delta.old / .new), or None"""
     if kv is None:
@@ -326,7 +375,11 @@ def filtered_ds_feature_deltas(engine, ds_diff, old_version, new_version, spatia
     cols = GeomCols(old_version, new_version, old_sf.geom_column_name, new_sf.geom_column_name)
     env = (old_sf if not old_sf.match_all else new_sf).filter_env
     rect = (old_sf if not old_sf.match_all else new_sf).rectangle
-    codes, keep, _, _ = geom_filter(engine, sides[0], sides[1], pairs, cols, env, rect)
+    # the blob reader's host pass: 48-byte geometry heads, the only bytes that go to the GPU (a
+    # geometry whose decode needs more comes back FALLBACK and is decided below on the host)
+    heads = [geom_heads(sides[0][0], sides[0][1], cols.old_hex, cols.old_gidx, len(cols.old_map)),
+             geom_heads(sides[1][0], sides[1][1], cols.new_hex, cols.new_gidx, len(cols.new_map))]
+    codes, keep, _, _ = geom_filter_heads(engine, heads[0], heads[1], pairs, env, rect)
     kept = np.zeros(n, bool)
     kept[keep] = True
     for i, (key, d) in enumerate(items):

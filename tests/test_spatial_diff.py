@@ -158,6 +158,17 @@ def test_gpu_geom_filter_vs_oracle_crafted(engine, bits):
         if bits:
             assert np.array_equal(ok, ook)
             assert np.array_equal(enc[ok == 1], oenc[ook == 1])
+        # the heads form: kd_geom_heads on the host, 48 bytes per blob to the GPU
+        hs = [S.geom_heads(d, o, gc.old_hex, gc.old_gidx, len(cols)) for d, o in ((od, oo), (nd, no))]
+        hc, hk, he, hok = S.geom_filter_heads(engine, hs[0], hs[1], pairs, filt, rect, bits, arenas=((od, oo), (nd, no)))
+        assert np.array_equal(hc, oc) and np.array_equal(hk, okeep)
+        if bits:
+            assert np.array_equal(hok, ook) and np.array_equal(he[hok == 1], oenc[ook == 1])
+        # without the arenas a geometry that needs more than its head (XYZ envelope, NaN envelope)
+        # comes back FALLBACK, every other side as before
+        hc2, _, _, _ = S.geom_filter_heads(engine, hs[0], hs[1], pairs, filt, rect, bits)
+        diff = hc2 != oc
+        assert diff.any() and (hc2[diff] == 3).all()
     assert {0, 1, 2, 3, 4} <= set(np.unique(oc).tolist())
 
 
@@ -182,6 +193,10 @@ def test_gpu_geom_filter_polygon_layer(engine, n):
     assert np.array_equal(codes, oc)
     assert np.array_equal(keep, okeep) and 0 < len(keep) < len(r.delta)
     assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1])
+    hs = [S.geom_heads(d, o, gc.old_hex, gc.old_gidx, len(hexes)) for d, o in ((od, oo), (nd, no))]
+    hc, hk, he, hok = S.geom_filter_heads(engine, hs[0], hs[1], r.delta, filt, False, 20)  # XY envelopes: no arena
+    assert np.array_equal(hc, oc) and np.array_equal(hk, okeep)
+    assert np.array_equal(hok, ook) and np.array_equal(he[hok == 1], oenc[ook == 1])
 
 
 @pytest.mark.gpu
@@ -206,8 +221,9 @@ def test_gpu_filtered_diff_points_edit_golden(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [200_000, 5_000_000, pytest.param(100_000_000, marks=pytest.mark.timeout(900))])
-def test_gpu_filter_pipeline_device_resident(engine, n):
+@pytest.mark.parametrize("n,heads", [(200_000, False), (200_000, True), (5_000_000, False), (5_000_000, True),
+                                     pytest.param(100_000_000, True, marks=pytest.mark.timeout(900))])
+def test_gpu_filter_pipeline_device_resident(engine, n, heads):
     """FilterPipeline: classify2's device delta list straight into kd_geom_filter (device count),
     equal to the oracle over the same deltas (the C restatement, kdo_geom_filter).  100M features =
     C5 at its stated size (BASELINE configs[4]): ~10M deltas, both sides' codes, the kept list and
@@ -220,7 +236,7 @@ def test_gpu_filter_pipeline_device_resident(engine, n):
     L = synth.polygons_layer(n, seed=9, delta_blobs=True)
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, S.GeomCols(ver, ver, "geom", "geom"),
-                          synth.C5_FILTER, False, 20)
+                          synth.C5_FILTER, False, 20, heads=heads)
     pipe.step()
     pipe.step()  # a second step over the same buffers gives the same answer
     counts, delta, codes, keep, enc, ok = pipe.results()
@@ -266,3 +282,42 @@ def test_oracle_geom_filter_c_equals_python(bits):
         for x, y in zip(c, p):
             assert np.array_equal(x, y)
     assert {0, 1, 2, 3, 4} <= set(np.unique(c[0]).tolist())
+
+
+def test_geom_heads_equal_oracle_feature_geometry():
+    """kd_geom_heads (host, the blob reader's pass) against the oracle's feature_geometry
+    (msgpack.unpackb + the legend's geometry position): status, GPKG length and its first 40 bytes,
+    on the crafted blobs (nested values, ext8/16/32, unknown legends, null geometries) and malformed
+    ones (trailing bytes, empty, wrong top-level shape, non-'G' ext, empty ext 'G')"""
+    from kart_amd import _native as N
+
+    rng = np.random.default_rng(3)
+    blobs, cols = _crafted(rng, 4000)
+    h = sorted(cols)[0]
+    blobs += [msgpack.packb([h, [msgpack.ExtType(ord("G"), b""), 1, 2]], use_bin_type=True),
+              msgpack.packb([h, [msgpack.ExtType(ord("G"), b"XX123456"), 1, 2]], use_bin_type=True),
+              msgpack.packb([h, [msgpack.ExtType(5, b"abc"), 1, 2]], use_bin_type=True),
+              msgpack.packb([h, [1.5, 1, 2]], use_bin_type=True), msgpack.packb([h, []], use_bin_type=True),
+              msgpack.packb([h], use_bin_type=True), msgpack.packb([h, [None], 3], use_bin_type=True),
+              msgpack.packb({"a": 1, "b": 2}, use_bin_type=True), b"\x92", b"",
+              msgpack.packb([h, [{"k": [1, {"x": None}]}, 1, 2]], use_bin_type=True) + b"\x00"]
+    data, off = _arena(blobs)
+    hexes = sorted(cols)
+    hx = np.frombuffer(b"".join(x.encode() for x in hexes), np.uint8).copy()
+    gi = np.array([cols[x] for x in hexes], np.int16)
+    heads = S.geom_heads(data, off, hx, gi, len(hexes), threads=3)
+    seen = set()
+    for i, b in enumerate(blobs):
+        st, g = O.feature_geometry(b, cols)
+        hs = int(heads["goff_status"][i]) >> 24
+        if st:
+            assert hs == N.KD_GH_FALLBACK, i
+        elif g is None:
+            assert hs == N.KD_GH_NULL, i
+        else:
+            assert hs == N.KD_GH_GEOM and int(heads["glen"][i]) == len(g), i
+            assert heads["gpkg"][i].tobytes()[:min(40, len(g))] == g[:40]
+            goff = int(heads["goff_status"][i]) & 0xFFFFFF
+            assert bytes(blobs[i][goff:goff + len(g)]) == g
+        seen.add(hs)
+    assert seen == {N.KD_GH_GEOM, N.KD_GH_NULL, N.KD_GH_FALLBACK}
