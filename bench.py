@@ -588,6 +588,50 @@ def run_c5(args, H):
             head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
         alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
     roof = roofline(kern, kname, alg, args.traffic_json, n)
+    delta_order = None
+    if heads and H.world == 1:
+        # the drop-in's layout: the blob reader reads the deltas' blobs after classification, so the
+        # heads lie in delta order (spatial.filtered_ds_feature_deltas); kd_geom_filter_heads alone on
+        # that layout, over the same deltas
+        import ctypes
+
+        from kart_amd import _native as N
+        from kart_amd.device import DevBuf
+        hs, pc = [], np.full(delta.shape, 0xFFFFFFFF, np.uint32)
+        for s_ in range(2):  # a head depends on its blob only: the per-entry heads, gathered into delta order
+            col = delta[:, s_]
+            pres = np.nonzero(col != 0xFFFFFFFF)[0]
+            hs.append(np.ascontiguousarray(pipe.heads_host[s_][col[pres].astype(np.int64)]))
+            pc[pres, s_] = np.arange(pres.size, dtype=np.uint32)
+        dh = [DevBuf.from_numpy(eng, h.view(np.uint8).reshape(-1)) for h in hs]
+        dp = DevBuf.from_numpy(eng, pc.reshape(-1))
+        m2, kp, nk = DevBuf(eng, 2 * nd + 2), DevBuf(eng, 4 * nd + 4), DevBuf(eng, 8)
+        e2, ok2 = DevBuf(eng, nd * (bits // 2) + 4), DevBuf(eng, nd + 4)
+        fe = (ctypes.c_double * 4)(*[float(x) for x in synth.C5_FILTER])
+
+        def filt():
+            N.check(eng.L.kd_geom_filter_heads(eng.ctx, dh[0].ptr, hs[0].size, dh[1].ptr, hs[1].size, N.KD_MEM_DEVICE,
+                                               None, None, dp.ptr, nd, None, N.KD_MEM_DEVICE, fe, 0, bits, m2.ptr,
+                                               kp.ptr, ctypes.cast(nk.ptr, N.c_u64p), e2.ptr, ok2.ptr, N.KD_MEM_DEVICE),
+                    "kd_geom_filter_heads")
+
+        filt()
+        eng.sync()
+        if not args.no_check:
+            assert np.array_equal(m2.download(np.uint8, 2 * nd).reshape(nd, 2), codes), "delta-order heads differ"
+        eng.prof_reset()
+        eng.prof_select(["k_gf_heads"])
+        eng.prof_enable(True)
+        el_d = timed(H, eng, filt, args.steps)
+        eng.prof_enable(False)
+        kd = kernel_times(eng, ("k_gf_heads",))
+        alg_d = 8 * nd + 48 * (hs[0].size + hs[1].size) + nd * (2 + bits // 2 + 1)
+        delta_order = {"what": "kd_geom_filter_heads alone over the same deltas with the heads in delta order (the "
+                               "drop-in's layout: the blob reader reads the deltas' blobs after classification)",
+                       "ms_per_call": round(el_d / args.steps * 1e3, 4),
+                       "roofline": roofline(kd, "k_gf_heads", alg_d, "", -1)}
+        for b in dh + [dp, m2, kp, nk, e2, ok2]:
+            b.free()
     arena_path = None
     if heads and not args.no_arena_timing:  # the same step through kd_geom_filter (blob arenas, msgpack walk)
         pa = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits)
@@ -626,12 +670,13 @@ def run_c5(args, H):
         "roofline": roof, "cpu_baseline": cpu,
     }
     if heads:
-        blobs = (L.base_blobs[1].shape[0] - 1) + (L.target_blobs[1].shape[0] - 1)
-        out["host"] = {"geom_heads_s": round(pipe.heads_s, 4), "blobs": int(blobs),
+        blobs = int(np.count_nonzero(np.diff(L.base_blobs[1])) + np.count_nonzero(np.diff(L.target_blobs[1])))
+        out["host"] = {"geom_heads_s": round(pipe.heads_s, 4), "blobs": blobs,
                        "geom_heads_M_blobs_per_s": round(blobs / pipe.heads_s / 1e6, 2),
                        "note": "kd_geom_heads: the blob reader's host pass (msgpack walk of every materialised blob, "
                                f"{host_cores()} threads) that leaves 48 B per blob for the GPU; outside the timed step"}
         out["arena_path"] = arena_path
+        out["heads_delta_order"] = delta_order
     return out
 
 

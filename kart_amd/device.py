@@ -308,6 +308,7 @@ class FilterPipeline:
         self.flags = N.KD_GF_RECT if rectangle else 0
         self.heads = None
         self.heads_s = None
+        self.heads_host = None
         if heads:  # the blob reader's host pass, then 48 bytes per blob in HBM (kd_geom_filter_heads)
             import time
 
@@ -317,6 +318,7 @@ class FilterPipeline:
             hs = [geom_heads(*base_blobs, geom_cols.old_hex, geom_cols.old_gidx, len(geom_cols.old_map)),
                   geom_heads(*target_blobs, geom_cols.new_hex, geom_cols.new_gidx, len(geom_cols.new_map))]
             self.heads_s = time.perf_counter() - t0
+            self.heads_host = hs
             self.heads = [(DevBuf.from_numpy(engine, h.view(np.uint8).reshape(-1)) if h.size else DevBuf(engine, 48), h.size)
                           for h in hs]
         engine.reserve(max(base.n, target.n))
