@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--arena", action="store_true",
                     help="c5: filter from the blob arenas (kd_geom_filter) instead of the geometry heads")
     ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
+    ap.add_argument("--no-delta-order", action="store_true",
+                    help="c5: skip timing the heads kernel on the drop-in's delta-order layout")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
@@ -165,8 +167,30 @@ def timed(H, eng, step, steps):
     return H.max(time.perf_counter() - t0)
 
 
-def roofline(kern, dom, alg_bytes, traffic_json, n_units):
-    """roofline object of the dominant kernel: algorithmic bytes per launch / its average launch time"""
+ROCPROF_STATS = {"c3": "profiles/r03/c3_kernel_stats.csv", "c3v": "profiles/r03/c3v_kernel_stats.csv",
+                 "c5": "profiles/r03/c5_kernel_stats.csv"}
+
+
+def rocprof_avg_ms(workload, kernel):
+    """the kernel's average duration in the committed `rocprofv3 --kernel-trace --stats` summary of
+    this workload (profiles/r03), or None"""
+    path = os.path.join(ROOT, ROCPROF_STATS.get(workload, "-"))
+    try:
+        import csv
+
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if r["Name"].split("(")[0].split("<")[0] == kernel:
+                    return float(r["AverageNs"]) / 1e6, os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
+        pass
+    return None
+
+
+def roofline(kern, dom, alg_bytes, traffic_json, n_units, workload=None):
+    """roofline object of the dominant kernel: algorithmic bytes per launch / its average launch time
+    (HIP events on the launch stream); next to it the same from the committed rocprofv3 summary of
+    the workload (the rocprof duration is the conservative one: quote both)"""
     if dom not in kern:
         return None
     achieved = alg_bytes / (kern[dom][1] * 1e-3) / 1e9
@@ -178,9 +202,15 @@ def roofline(kern, dom, alg_bytes, traffic_json, n_units):
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError, TypeError):
         pass
-    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_bytes_per_launch": int(alg_bytes),
-            "avg_launch_ms": round(kern[dom][1], 5)}
+    out = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_bytes_per_launch": int(alg_bytes),
+           "avg_launch_ms": round(kern[dom][1], 5)}
+    rp = rocprof_avg_ms(workload, dom) if workload else None
+    if rp:
+        ms, path = rp
+        out["rocprof"] = {"avg_launch_ms": round(ms, 5), "frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "stats": path}
+    return out
 
 
 def kernel_times(eng, names):
@@ -307,7 +337,8 @@ def run_diff(args, H, polygons):
     }
     dom = max((k for k in kern if k in alg), key=lambda k: kern[k][1]) if kern else None
     # (the committed traffic files are 1-GPU profiles of the whole layer: not a shard's bytes)
-    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, n if world == 1 else -1) if dom else None
+    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, n if world == 1 else -1,
+                    args.workload if world == 1 else None) if dom else None
     cpu = host = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_diff(L, maps, args.cpu_seconds, "C3" if polygons else "C2")
@@ -587,9 +618,9 @@ def run_c5(args, H):
             prs = col[col != 0xFFFFFFFF].astype(np.int64)
             head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
         alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
-    roof = roofline(kern, kname, alg, args.traffic_json, n)
+    roof = roofline(kern, kname, alg, args.traffic_json, n, "c5" if heads and H.world == 1 else None)
     delta_order = None
-    if heads and H.world == 1:
+    if heads and H.world == 1 and not args.no_delta_order:
         # the drop-in's layout: the blob reader reads the deltas' blobs after classification, so the
         # heads lie in delta order (spatial.filtered_ds_feature_deltas); kd_geom_filter_heads alone on
         # that layout, over the same deltas

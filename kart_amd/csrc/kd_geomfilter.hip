@@ -387,15 +387,31 @@ struct GfHeadArgs {
     const u64* off[2];
 };
 
-__device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g, int s, u32 bi, GHit& h) {
+struct HeadLd {
+    u32x4 v0, v1, v2;
+};
+
+// one side's head record (three 16-B loads; zeros for an absent side)
+__device__ __forceinline__ HeadLd load_head(const GfHeadArgs& g, int s, u32 bi) {
     typedef const __attribute__((address_space(1))) u32x4* gx4;
+    HeadLd L;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    const bool ok = bi != KD_NONE && (u64)bi < g.nhead[s];
+    const u64 base = ok ? (u64)(g.head[s] + bi) : 0;
+    L.v0 = ok ? *(gx4)base : z;
+    L.v1 = ok ? *(gx4)(base + 16) : z;
+    L.v2 = ok ? *(gx4)(base + 32) : z;
+    return L;
+}
+
+__device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g, int s, u32 bi, const HeadLd& L,
+                                            GHit& h) {
     h.r = -1;
     h.pc = -1;
     h.empty = false;
     if (bi == KD_NONE) { h.code = GF_NONE; return; }
     if ((u64)bi >= g.nhead[s]) { h.code = GF_FALLBACK; return; }
-    const u64 base = (u64)(g.head[s] + bi);
-    const u32x4 v0 = *(gx4)base, v1 = *(gx4)(base + 16), v2 = *(gx4)(base + 32);
+    const u32x4 v0 = L.v0, v1 = L.v1, v2 = L.v2;
     const u32 st = v2.w >> 24;
     if (st == KD_GH_NULL) { h.code = GF_MATCH; return; }
     if (st != KD_GH_GEOM) { h.code = GF_FALLBACK; return; }
@@ -428,20 +444,25 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
     const double vmax = (double)((1ull << a.bits) - 1);
     const u64 t0 = (u64)blockIdx.x * GF_TILE;
     u32 kept = 0;
+    // software pipeline: round r+1's delta pair is in flight while round r's heads (both sides,
+    // issued together) are loaded and decoded: one dependent round trip per round
+    auto ld_pair = [&](u64 d) { return d < n ? *(const uint2*)(a.pairs + 2 * d) : make_uint2(KD_NONE, KD_NONE); };
+    uint2 pr = ld_pair(t0 + tid);
     for (int rd = 0; rd < GF_ROUNDS; rd++) {
         const u64 d0 = t0 + (u64)rd * GF_NT;
         if (d0 >= n) break;  // block-uniform
         const u64 d = d0 + tid;
         bool keep = false;
         u8 ok = 0;
+        const HeadLd L0 = load_head(g, 0, pr.x), L1 = load_head(g, 1, pr.y);
+        const uint2 pr_next = rd + 1 < GF_ROUNDS ? ld_pair(d + GF_NT) : make_uint2(KD_NONE, KD_NONE);
         if (a.enc)
             for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
         if (d < n) {
-            const uint2 pr = *(const uint2*)(a.pairs + 2 * d);
             GHit h;
-            decode_head(a, g, 0, pr.x, h);
+            decode_head(a, g, 0, pr.x, L0, h);
             const int co = h.code;
-            decode_head(a, g, 1, pr.y, h);
+            decode_head(a, g, 1, pr.y, L1, h);
             const int cn = h.code;
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
@@ -466,6 +487,7 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
             for (u32 k = tid; k < cnt; k += GF_NT) a.enc_ok[d0 + k] = s_ok[k];
             __syncthreads();
         }
+        pr = pr_next;
     }
     if ((tid & 63) == 0) s_wc[tid >> 6] = kept;
     __syncthreads();
