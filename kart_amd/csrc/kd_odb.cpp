@@ -358,7 +358,9 @@ struct Reader {
             if (rc) return rc;
             if (apply_delta(out.data(), out.size(), dbuf.data(), dbuf.size(), tmp)) return RD_CORRUPT;
             out.swap(tmp);
-            if (j) remember(&pk, L.off, btype, out);  // intermediate bases: siblings share them
+            // every resolved link, the object itself included: in a batch read in pack order the
+            // next object is usually a delta against this one (fast-import and repack chains)
+            remember(&pk, L.off, btype, out);
         }
         *type = btype;
         return RD_OK;
@@ -814,21 +816,41 @@ extern "C" int kd_odb_read_batch(kd_odb* odb, const uint8_t* oids, uint64_t n, i
     if (!odb || !off || (n && (!oids || !status)) || !data) { kd::set_error("kd_odb_read_batch: NULL"); return KD_EINVAL; }
     *data = nullptr;
     const int nt = default_threads(threads);
-    // blobs in chunks of 256 per task: each task fills its own buffer, the arena is stitched after
     constexpr u64 CH = 256;
     const u64 nch = (n + CH - 1) / CH;
+    // the objects are read in pack order (pack, then offset; loose objects last), as git's
+    // unordered batch reads do: a delta chain's objects lie together (fast-import deltas each blob
+    // against the one before), so the next object's base is usually in the reader's cache and a
+    // chain of d deltas costs one inflate per object instead of up to d
+    std::vector<std::pair<u64, u64>> ord(n);  // (pack position, input index)
+    par_items(nch, nt, [&](size_t c, int) {
+        for (u64 i = c * CH; i < std::min(n, (c + 1) * CH); i++) {
+            u64 key = ~0ull, o;
+            for (size_t k = 0; k < odb->packs.size() && k < 0xFFFF; k++)
+                if (odb->packs[k]->find(oids + 20 * i, &o)) { key = (u64)k << 48 | std::min<u64>(o, (1ull << 48) - 1); break; }
+            ord[i] = {key, i};
+        }
+    });
+    std::sort(ord.begin(), ord.end());
+    // chunks of 256 objects in that order per task, each into its own buffer; stitched in input
+    // order after
     std::vector<std::vector<u8>> part(nch);
+    std::vector<u64> at(n);  // object i's bytes: part[chunk of its sorted position] at at[i]
+    std::vector<u32> chunk_of(n);
     std::vector<std::unique_ptr<Reader>> rds(nt);
     off[0] = 0;
     par_items(nch, nt, [&](size_t c, int tid) {
         if (!rds[tid]) rds[tid] = std::make_unique<Reader>(odb);
         Reader& rd = *rds[tid];
         std::vector<u8> buf;
-        for (u64 i = c * CH; i < std::min(n, (c + 1) * CH); i++) {
+        for (u64 s = c * CH; s < std::min(n, (c + 1) * CH); s++) {
+            const u64 i = ord[s].second;
             int type = 0;
             const int rc = rd.read(oids + 20 * i, &type, buf);
             status[i] = rc == RD_OK && type != OBJ_BLOB ? 2 : (u8)rc;
             if (status[i]) buf.clear();
+            at[i] = part[c].size();
+            chunk_of[i] = (u32)c;
             part[c].insert(part[c].end(), buf.begin(), buf.end());
             off[i + 1] = buf.size();  // lengths first, prefix-summed below
         }
@@ -837,7 +859,8 @@ extern "C" int kd_odb_read_batch(kd_odb* odb, const uint8_t* oids, uint64_t n, i
     u8* p = (u8*)std::malloc(std::max<u64>(n ? off[n] : 0, 1));
     if (!p) { kd::set_error("kd_odb_read_batch: out of memory"); return KD_EINVAL; }
     par_items(nch, nt, [&](size_t c, int) {
-        if (!part[c].empty()) memcpy(p + off[c * CH], part[c].data(), part[c].size());
+        for (u64 i = c * CH; i < std::min(n, (c + 1) * CH); i++)
+            if (off[i + 1] > off[i]) memcpy(p + off[i], part[chunk_of[i]].data() + at[i], off[i + 1] - off[i]);
     });
     *data = p;
     return KD_OK;

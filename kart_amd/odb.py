@@ -8,6 +8,7 @@ a multithreaded leaf walk that never opens a subtree whose OID two roots share.
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -156,12 +157,15 @@ class ObjectDB:
         with self._lock:
             N.check(self.L.kd_odb_read_batch(self._h, oids.ctypes.data if n else None, n, threads, ctypes.byref(data),
                                              off.ctypes.data, status.ctypes.data), "kd_odb_read_batch")
-        try:
-            total = int(off[-1])
-            arena = np.ctypeslib.as_array(data, (total,)).copy() if total else np.zeros(0, np.uint8)
-        finally:
-            self.L.kd_free(ctypes.cast(data, ctypes.c_void_p))
-        return arena, off, status[:n]
+        total = int(off[-1])
+        addr = ctypes.cast(data, ctypes.c_void_p).value
+        if not total:
+            self.L.kd_free(ctypes.c_void_p(addr))
+            return np.zeros(0, np.uint8), off, status[:n]
+        # the library's buffer itself, freed when the last array over it goes (no copy)
+        buf = (ctypes.c_uint8 * total).from_address(addr)
+        weakref.finalize(buf, self.L.kd_free, ctypes.c_void_p(addr))
+        return np.frombuffer(buf, np.uint8), off, status[:n]
 
     def walk(self, roots, subpath="", compare=None, threads=0):
         """Leaves under ``subpath`` of each root (commit/tag/tree ids), one Leaves per root.

@@ -268,3 +268,23 @@ def test_field_diff_batch_path(eng):
     assert D.field_diff(eng, fd2, fd2._kd_updates.old_v, fd2._kd_updates.new_v) == 4
     assert {k: d.changed_fields for k, d in fd2.items()} == {k: v for k, v in fields.items() if k != gone}
     assert {k: (d.old_value, d.new_value) for k, d in fd2.items()} == {k: v for k, v in vals.items() if k != gone}
+
+
+def test_changed_names_rows_matches_per_row():
+    """the batch decode (one np.unique over the rows' words) equals changed_names row by row, for
+    one- and multi-word masks, with a fresh list per row"""
+    from kart_amd.schema import FieldMaps
+
+    rng = np.random.default_rng(3)
+    for n_keys in (5, 64, 65, 130):
+        fm = object.__new__(FieldMaps)
+        fm.keys = [f"k{i}" for i in range(n_keys)]
+        fm.n_keys, fm.words = n_keys, max(1, (n_keys + 63) // 64)
+        distinct = rng.integers(0, 2**63, (7, fm.words), dtype=np.uint64) | np.uint64(1 << 63)
+        if n_keys % 64:
+            distinct[:, -1] &= np.uint64((1 << (n_keys % 64)) - 1)
+        masks = distinct[rng.integers(0, 7, 500)]
+        rows = fm.changed_names_rows(masks)
+        assert rows == [fm.changed_names(r) for r in masks]
+        assert len({id(r) for r in rows}) == len(rows)
+    assert fm.changed_names_rows(np.zeros((0, fm.words), np.uint64)) == []

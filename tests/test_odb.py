@@ -163,6 +163,12 @@ def test_deep_delta_chains_and_batch_reads(tmp_path):
             size = int(want[pos:nl].split()[2])
             assert data[int(off[i]):int(off[i + 1])].tobytes() == want[nl + 1:nl + 1 + size]
             pos = nl + 1 + size + 1
+        # shuffled and repeated: read in pack order, the arena stitched back in input order
+        pick = np.random.default_rng(5).integers(0, lv.n, 3 * lv.n)
+        d2, o2, s2 = db.read_batch(lv.oids[pick], threads=3)
+        assert not s2.any() and int(o2[-1]) == int(sum(off[i + 1] - off[i] for i in pick))
+        for k, i in enumerate(pick):
+            assert d2[int(o2[k]):int(o2[k + 1])].tobytes() == data[int(off[i]):int(off[i + 1])].tobytes()
 
 
 def test_loose_objects_missing_and_corrupt(tmp_path, repo):
