@@ -13,6 +13,7 @@
 // off32[n] (MSB -> index into off64[]); pack entries = type/size varint header, zlib stream;
 // OFS_DELTA base = this offset - (offset varint); delta = src/dst size varints + copy/insert ops.
 #include <dirent.h>
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -232,6 +233,33 @@ int apply_delta(const u8* base, size_t blen, const u8* d, size_t dlen, std::vect
     return w == dst ? 0 : -1;
 }
 
+// libdeflate (the image's libdeflate.so.0, when present) inflates a whole zlib stream of known
+// size in one call, without zlib's per-stream state machine: a pack read is mostly tiny delta
+// streams, so this is most of its CPU time.  Its documented C API, declared here (no header in the
+// image); zlib when the library is absent.
+struct Deflate {
+    typedef void* (*alloc_fn)();
+    typedef void (*free_fn)(void*);
+    typedef int (*zlib_ex_fn)(void*, const void*, size_t, void*, size_t, size_t*, size_t*);
+    alloc_fn alloc = nullptr;
+    free_fn release = nullptr;
+    zlib_ex_fn zlib_ex = nullptr;
+    Deflate() {
+        if (getenv("KD_ODB_ZLIB")) return;  // A/B switch: zlib only
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = (alloc_fn)dlsym(h, "libdeflate_alloc_decompressor");
+        release = (free_fn)dlsym(h, "libdeflate_free_decompressor");
+        zlib_ex = (zlib_ex_fn)dlsym(h, "libdeflate_zlib_decompress_ex");
+        if (!alloc || !release || !zlib_ex) alloc = nullptr;
+    }
+    bool ok() const { return alloc != nullptr; }
+};
+const Deflate& deflate_lib() {
+    static const Deflate d;
+    return d;
+}
+
 // One thread's reader: a zlib stream, a delta-base cache, scratch buffers.
 struct Reader {
     const kd_odb* db;
@@ -246,17 +274,27 @@ struct Reader {
     std::vector<Slot> cache;
     std::vector<u8> dbuf, tmp;
 
+    void* dec = nullptr;  // libdeflate decompressor
+
     explicit Reader(const kd_odb* d) : db(d), cache(CACHE_SLOTS) {
         memset(&z, 0, sizeof z);
         zok = inflateInit(&z) == Z_OK;
+        if (deflate_lib().ok()) dec = deflate_lib().alloc();
     }
     ~Reader() {
         if (zok) inflateEnd(&z);
+        if (dec) deflate_lib().release(dec);
     }
     Reader(const Reader&) = delete;
 
     // inflate one zlib stream starting at src into exactly `size` bytes
     int inflate_exact(const u8* src, size_t avail, u8* dst, size_t size) {
+        if (dec) {
+            u8 dummy;
+            size_t in_used = 0, out_used = 0;
+            const int r = deflate_lib().zlib_ex(dec, src, avail, size ? dst : &dummy, size, &in_used, &out_used);
+            return r == 0 && out_used == size ? RD_OK : RD_CORRUPT;  // 0: LIBDEFLATE_SUCCESS
+        }
         if (!zok || inflateReset(&z) != Z_OK) return RD_CORRUPT;
         z.next_in = (Bytef*)src;
         z.avail_in = (uInt)std::min<size_t>(avail, 0xFFFFFFFFu);

@@ -169,6 +169,17 @@ def test_deep_delta_chains_and_batch_reads(tmp_path):
         assert not s2.any() and int(o2[-1]) == int(sum(off[i + 1] - off[i] for i in pick))
         for k, i in enumerate(pick):
             assert d2[int(o2[k]):int(o2[k + 1])].tobytes() == data[int(off[i]):int(off[i + 1])].tobytes()
+    # the zlib inflate path (taken when libdeflate.so.0 is absent) reads the same bytes
+    import hashlib
+    import sys
+
+    prog = ("import hashlib, sys; sys.path.insert(0, %r); from kart_amd.odb import ObjectDB; "
+            "db = ObjectDB(%r); (lv,) = db.walk([%r], 't'); d, o, st = db.read_batch(lv.oids); "
+            "print(hashlib.sha256(d.tobytes() + o.tobytes()).hexdigest(), int(st.sum()))"
+            % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), gitdir, _rev(gitdir, "v39")))
+    out = subprocess.run([sys.executable, "-c", prog], env=dict(os.environ, KD_ODB_ZLIB="1"), capture_output=True,
+                         check=True, text=True).stdout.split()
+    assert out == [hashlib.sha256(data.tobytes() + off.tobytes()).hexdigest(), "0"]
 
 
 def test_loose_objects_missing_and_corrupt(tmp_path, repo):
