@@ -25,6 +25,7 @@ import msgpack
 import numpy as np
 
 from . import _native as N
+from . import deltas as _deltas
 from . import packing
 from .adaptor import structs
 from .schema import FieldMaps, Legend, Schema
@@ -312,14 +313,27 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
         for i, b in zip(ib.tolist(), new_v.get_blobs(B.order[b_idx[ib]])):
             new_blobs[i] = b
     upd_rows, upd_deltas, upd_keys, n_total = [], [], [], 0
+    # this module's own Delta / KeyValue: built field by field (the constructor's argument
+    # normalisation is most of a delta's host cost); Kart's classes through their constructor
+    own = S.Delta is _deltas.Delta
+    Delta, KeyValue, new_obj, partial = _deltas.Delta, _deltas.KeyValue, object.__new__, functools.partial
+    old_get, new_get = (old_v.get_feature_from_blob if old_v is not None else None,
+                        new_v.get_feature_from_blob if new_v is not None else None)
     for i in range(d.shape[0]):
         opk, npk = old_pks[i], new_pks[i]
         if not match_all and str(opk) not in feature_filter and str(npk) not in feature_filter:
             continue
         ob, nb = old_blobs[i], new_blobs[i]
-        old_half = (opk, functools.partial(old_v.get_feature_from_blob, ob)) if ob is not None else None
-        new_half = (npk, functools.partial(new_v.get_feature_from_blob, nb)) if nb is not None else None
-        delta = S.Delta(old_half, new_half)
+        if own:
+            delta = new_obj(Delta)
+            delta.old = KeyValue(opk, partial(old_get, ob)) if ob is not None else None
+            delta.new = KeyValue(npk, partial(new_get, nb)) if nb is not None else None
+            delta.type = "insert" if ob is None else ("delete" if nb is None else "update")
+            delta.flags = 0
+        else:
+            old_half = (opk, partial(old_get, ob)) if ob is not None else None
+            new_half = (npk, partial(new_get, nb)) if nb is not None else None
+            delta = S.Delta(old_half, new_half)
         if ob is not None and nb is not None:
             upd_rows.append(i)
             upd_deltas.append(delta)
