@@ -480,11 +480,25 @@ struct Reader {
         return result;
     }
 
-    int read(const u8* oid, int* type, std::vector<u8>& out, int depth = 0) {
-        for (const auto& pk : db->packs) {
-            u64 off;
-            if (pk->find(oid, &off)) return read_packed(*pk, off, type, out, depth);
+    // the pack holding oid (the one that held the previous object first: a batch's objects tend
+    // to share packs, and every miss is a binary search of another index), or -1
+    size_t last_pack = 0;
+    long locate(const u8* oid, u64* off) {
+        const size_t np = db->packs.size();
+        for (size_t k = 0; k < np; k++) {
+            const size_t p = k == 0 ? (last_pack < np ? last_pack : 0) : (k <= last_pack ? k - 1 : k);
+            if (db->packs[p]->find(oid, off)) {
+                last_pack = p;
+                return (long)p;
+            }
         }
+        return -1;
+    }
+
+    int read(const u8* oid, int* type, std::vector<u8>& out, int depth = 0) {
+        u64 off;
+        const long p = locate(oid, &off);
+        if (p >= 0) return read_packed(*db->packs[p], off, type, out, depth);
         return read_loose(oid, type, out);
     }
 };
@@ -860,13 +874,15 @@ extern "C" int kd_odb_read_batch(kd_odb* odb, const uint8_t* oids, uint64_t n, i
     // unordered batch reads do: a delta chain's objects lie together (fast-import deltas each blob
     // against the one before), so the next object's base is usually in the reader's cache and a
     // chain of d deltas costs one inflate per object instead of up to d
-    std::vector<std::pair<u64, u64>> ord(n);  // (pack position, input index)
-    par_items(nch, nt, [&](size_t c, int) {
+    std::vector<std::pair<u64, u64>> ord(n);  // (pack << 48 | offset, or ~0: read by id; input index)
+    std::vector<std::unique_ptr<Reader>> rds(nt);
+    par_items(nch, nt, [&](size_t c, int tid) {
+        if (!rds[tid]) rds[tid] = std::make_unique<Reader>(odb);
+        Reader& rd = *rds[tid];
         for (u64 i = c * CH; i < std::min(n, (c + 1) * CH); i++) {
-            u64 key = ~0ull, o;
-            for (size_t k = 0; k < odb->packs.size() && k < 0xFFFF; k++)
-                if (odb->packs[k]->find(oids + 20 * i, &o)) { key = (u64)k << 48 | std::min<u64>(o, (1ull << 48) - 1); break; }
-            ord[i] = {key, i};
+            u64 o;
+            const long p = rd.locate(oids + 20 * i, &o);
+            ord[i] = {p >= 0 && p < 0xFFFF && o < (1ull << 48) ? (u64)p << 48 | o : ~0ull, i};
         }
     });
     std::sort(ord.begin(), ord.end());
@@ -875,16 +891,16 @@ extern "C" int kd_odb_read_batch(kd_odb* odb, const uint8_t* oids, uint64_t n, i
     std::vector<std::vector<u8>> part(nch);
     std::vector<u64> at(n);  // object i's bytes: part[chunk of its sorted position] at at[i]
     std::vector<u32> chunk_of(n);
-    std::vector<std::unique_ptr<Reader>> rds(nt);
     off[0] = 0;
     par_items(nch, nt, [&](size_t c, int tid) {
         if (!rds[tid]) rds[tid] = std::make_unique<Reader>(odb);
         Reader& rd = *rds[tid];
         std::vector<u8> buf;
         for (u64 s = c * CH; s < std::min(n, (c + 1) * CH); s++) {
-            const u64 i = ord[s].second;
+            const u64 key = ord[s].first, i = ord[s].second;
             int type = 0;
-            const int rc = rd.read(oids + 20 * i, &type, buf);
+            const int rc = key != ~0ull ? rd.read_packed(*odb->packs[key >> 48], key & ((1ull << 48) - 1), &type, buf)
+                                        : rd.read(oids + 20 * i, &type, buf);
             status[i] = rc == RD_OK && type != OBJ_BLOB ? 2 : (u8)rc;
             if (status[i]) buf.clear();
             at[i] = part[c].size();

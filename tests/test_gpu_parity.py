@@ -247,6 +247,9 @@ def test_gpu_env_overlap_vs_oracle(engine):
     (True, 10_000_000, "points", False),    # C2 at its stated size (configs[1])
     (True, 100_000_000, "polygons", "late"),  # C3 at its stated size (configs[2], the bench's default
                                               # workload), from walk-order sides: both 100M sorts included
+    # C3v: 60 % of the geometry edits keep their length, so their payloads are compared byte by byte
+    (True, 2_000_000, "polygons_same", False), (False, 2_000_000, "polygons_same", False),
+    (True, 100_000_000, "polygons_same", False),
 ])
 def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
     """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes),
@@ -259,7 +262,8 @@ def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
     from kart_amd.device import DiffPipeline
     from kart_amd.schema import FieldMaps
 
-    L = synth.points_layer(n, seed=11) if layer == "points" else synth.polygons_layer(n, seed=12)
+    L = (synth.points_layer(n, seed=11) if layer == "points" else
+         synth.polygons_layer(n, seed=12, same_len=0.6 if layer == "polygons_same" else 0.0))
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     perms = (synth.walk_perm(L.base.key), synth.walk_perm(L.target.key)) if walk else None
     pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered, walk=perms,

@@ -322,3 +322,27 @@ def test_refresh_only_when_packs_change(tmp_path):
         assert r.odb.n_opens == h + 1
     finally:
         r.close()
+
+
+def test_batch_reads_across_several_packs(tmp_path):
+    """three fast-imports = three packs (each with its own delta chains): a shuffled batch over all
+    of them, read in (pack, offset) order and stitched back, equals git cat-file object by object"""
+    gitdir = str(tmp_path / "m.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    for b in range(3):
+        files = {f"p{b}/{i:04d}": b"pack %d row %d " % (b, i) + b"z" * (100 + i % 50) for i in range(400)}
+        _fast_import(gitdir, [(f"b{b}", files)])
+    packs = [f for f in os.listdir(os.path.join(gitdir, "objects", "pack")) if f.endswith(".idx")]
+    assert len(packs) == 3
+    db = ObjectDB(gitdir)
+    oids = np.concatenate([db.walk([_rev(gitdir, f"b{b}")], f"p{b}")[0].oids for b in range(3)])
+    pick = np.random.default_rng(7).permutation(np.concatenate([np.arange(oids.shape[0])] * 2))
+    data, off, st = db.read_batch(oids[pick], threads=4)
+    assert not st.any()
+    want = _git(gitdir, "cat-file", "--batch", input="".join(oids[i].tobytes().hex() + "\n" for i in pick).encode())
+    pos = 0
+    for k in range(pick.size):
+        nl = want.index(b"\n", pos)
+        size = int(want[pos:nl].split()[2])
+        assert data[int(off[k]):int(off[k + 1])].tobytes() == want[nl + 1:nl + 1 + size]
+        pos = nl + 1 + size + 1
