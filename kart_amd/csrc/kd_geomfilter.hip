@@ -385,22 +385,23 @@ struct GfHeadArgs {
     u64 nhead[2];
     const u8* data[2];  // the arenas the heads came from (null: no slow path, such sides FALLBACK)
     const u64* off[2];
+    const u8* zeros;    // >= 48 readable zero bytes: the source of an absent side's head loads
 };
 
 struct HeadLd {
     u32x4 v0, v1, v2;
 };
 
-// one side's head record (three 16-B loads; zeros for an absent side)
+// one side's head record (three 16-B loads; an absent side reads the zero block): unconditional,
+// so no branch hides them from the wait counting of a pipelined caller
 __device__ __forceinline__ HeadLd load_head(const GfHeadArgs& g, int s, u32 bi) {
     typedef const __attribute__((address_space(1))) u32x4* gx4;
     HeadLd L;
-    const u32x4 z = {0u, 0u, 0u, 0u};
     const bool ok = bi != KD_NONE && (u64)bi < g.nhead[s];
-    const u64 base = ok ? (u64)(g.head[s] + bi) : 0;
-    L.v0 = ok ? *(gx4)base : z;
-    L.v1 = ok ? *(gx4)(base + 16) : z;
-    L.v2 = ok ? *(gx4)(base + 32) : z;
+    const u64 base = ok ? (u64)(g.head[s] + bi) : (u64)g.zeros;
+    L.v0 = *(gx4)base;
+    L.v1 = *(gx4)(base + 16);
+    L.v2 = *(gx4)(base + 32);
     return L;
 }
 
@@ -433,31 +434,40 @@ __device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g
     h.code = geom_code(a, h, hflags);
 }
 
-// k_gf_match over heads: the same tiles, codes, kept counts and index envelopes
+// k_gf_match over heads: the same tiles, codes, kept counts and index envelopes.
+// Each wave works alone until the tile's kept count: its 64 deltas' index envelopes are staged in
+// its own LDS slice and written out as contiguous dwords by the wave (no block barrier per round —
+// a barrier's fence waits for every load in flight, prefetches included), and the loads run two
+// rounds deep: round r+1's heads and round r+2's delta pair are in flight while round r decodes.
 __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
-    __shared__ u8 s_enc[GF_NT * 16];
-    __shared__ u8 s_ok[GF_NT];
+    __shared__ u32 s_encw[GF_NT * 4];  // 16 B per lane: nb <= 16 index-envelope bytes
     __shared__ u32 s_wc[GF_NT / 64];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const u64 n = a.d_n ? *a.d_n : a.cap;
     const int nb = a.bits / 2;
     const double vmax = (double)((1ull << a.bits) - 1);
     const u64 t0 = (u64)blockIdx.x * GF_TILE;
+    u8* const wenc = (u8*)(s_encw + 64 * 4 * wid);  // this wave's slice
     u32 kept = 0;
-    // software pipeline: round r+1's delta pair is in flight while round r's heads (both sides,
-    // issued together) are loaded and decoded: one dependent round trip per round
-    auto ld_pair = [&](u64 d) { return d < n ? *(const uint2*)(a.pairs + 2 * d) : make_uint2(KD_NONE, KD_NONE); };
+    auto ld_pair = [&](u64 d) {  // (unconditional load, clamped index)
+        const uint2 v = *(n ? (const uint2*)a.pairs + (d < n ? d : n - 1) : (const uint2*)g.zeros);
+        return d < n ? v : make_uint2(KD_NONE, KD_NONE);
+    };
     uint2 pr = ld_pair(t0 + tid);
+    uint2 pr1 = GF_ROUNDS > 1 ? ld_pair(t0 + GF_NT + tid) : make_uint2(KD_NONE, KD_NONE);
+    HeadLd L0 = load_head(g, 0, pr.x), L1 = load_head(g, 1, pr.y);
     for (int rd = 0; rd < GF_ROUNDS; rd++) {
         const u64 d0 = t0 + (u64)rd * GF_NT;
         if (d0 >= n) break;  // block-uniform
         const u64 d = d0 + tid;
+        // issue order = wait order: the pair two rounds ahead, then the next round's heads (its
+        // pair arrived a round ago), then this round's decode waits only for this round's heads
+        const uint2 pr2 = rd + 2 < GF_ROUNDS ? ld_pair(d + 2 * GF_NT) : make_uint2(KD_NONE, KD_NONE);
+        const HeadLd M0 = load_head(g, 0, pr1.x), M1 = load_head(g, 1, pr1.y);
         bool keep = false;
         u8 ok = 0;
-        const HeadLd L0 = load_head(g, 0, pr.x), L1 = load_head(g, 1, pr.y);
-        const uint2 pr_next = rd + 1 < GF_ROUNDS ? ld_pair(d + GF_NT) : make_uint2(KD_NONE, KD_NONE);
         if (a.enc)
-            for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
+            for (int k = 0; k < nb; k++) wenc[lane * nb + k] = 0;
         if (d < n) {
             GHit h;
             decode_head(a, g, 0, pr.x, L0, h);
@@ -467,29 +477,31 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
             if (a.enc && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
-                ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { s_enc[tid * nb + k] = v; });
+                ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { wenc[lane * nb + k] = v; });
+            if (a.enc) a.enc_ok[d] = ok;
         }
-        const u64 bal = __ballot(keep);
-        kept += (u32)__popcll(bal);
+        kept += (u32)__popcll(__ballot(keep));
         if (a.enc) {
-            s_ok[tid] = ok;
-            __syncthreads();
-            const u32 cnt = (u32)(n - d0 < GF_NT ? n - d0 : GF_NT);
-            u8* dst = a.enc + d0 * nb;
+            __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations stay in program order)
+            const u64 w0 = d0 + 64ull * wid;
+            const u32 cnt = w0 < n ? (u32)(n - w0 < 64 ? n - w0 : 64) : 0u;
+            u8* dst = a.enc + w0 * nb;
             const u32 bytes = cnt * nb;
             if ((((u64)dst) & 3) == 0) {
                 const u32 nw = bytes >> 2;
-                for (u32 k = tid; k < nw; k += GF_NT) ((u32*)dst)[k] = ((const u32*)s_enc)[k];
-                for (u32 k = 4 * nw + tid; k < bytes; k += GF_NT) dst[k] = s_enc[k];
+                for (u32 k = lane; k < nw; k += 64) ((u32*)dst)[k] = ((const u32*)wenc)[k];
+                for (u32 k = 4 * nw + lane; k < bytes; k += 64) dst[k] = wenc[k];
             } else {
-                for (u32 k = tid; k < bytes; k += GF_NT) dst[k] = s_enc[k];
+                for (u32 k = lane; k < bytes; k += 64) dst[k] = wenc[k];
             }
-            for (u32 k = tid; k < cnt; k += GF_NT) a.enc_ok[d0 + k] = s_ok[k];
-            __syncthreads();
+            __builtin_amdgcn_wave_barrier();  // read out before the next round's zeroing
         }
-        pr = pr_next;
+        L0 = M0;
+        L1 = M1;
+        pr = pr1;
+        pr1 = pr2;
     }
-    if ((tid & 63) == 0) s_wc[tid >> 6] = kept;
+    if (lane == 0) s_wc[wid] = kept;
     __syncthreads();
     if (tid == 0) {
         u32 t = 0;
@@ -721,6 +733,11 @@ extern "C" int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, 
         KD_CHECK(((u64)dh & 15) == 0, "kd_geom_filter_heads: heads must be 16-byte aligned");
         g.head[s] = (const kd_geom_head*)dh;
         g.nhead[s] = nh[s];
+    }
+    {
+        void* dz;
+        if ((rc = device_zeros(ctx, &dz))) return rc;  // 256 zero bytes
+        g.zeros = (const u8*)dz;
     }
     if (old_blobs) {
         const kd_blobs* bl[2] = {old_blobs, new_blobs};
