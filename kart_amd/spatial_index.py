@@ -207,6 +207,31 @@ def _open_db(path, clear_existing):
     return db
 
 
+def _index_envelopes(engine, data, off, pairs, cols, bits):
+    """(codes, enc, enc_ok) of the blobs pairs[:, 1] of a host arena: the blob reader's 48-byte
+    geometry heads (kd_geom_heads, host threads) are all that goes to the GPU
+    (kd_geom_filter_heads); the few blobs whose head cannot decide (XYZ/XYM envelopes, NaN
+    envelopes, unusual layouts) are sent whole through kd_geom_filter, so the result is the
+    blob-arena kernel's on every row"""
+    from .spatial import GEOM_HEAD, geom_filter, geom_filter_heads, geom_heads
+
+    empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    heads = geom_heads(data, off, cols.new_hex, cols.new_gidx, len(cols.new_map))
+    codes, _, enc, ok = geom_filter_heads(engine, np.zeros(0, GEOM_HEAD), heads, pairs, WORLD, False, bits)
+    redo = np.nonzero(codes[:, 1] == 3)[0]
+    if redo.size:
+        rows = pairs[redo, 1].astype(np.int64)
+        lens = (off[rows + 1] - off[rows]).astype(np.int64)
+        sub_off = np.zeros(rows.size + 1, np.uint64)
+        np.cumsum(lens, out=sub_off[1:])
+        sub = np.concatenate([data[int(off[r]):int(off[r + 1])] for r in rows.tolist()]) if rows.size else empty[0]
+        sp = np.full((rows.size, 2), N.KD_NONE, np.uint32)
+        sp[:, 1] = np.arange(rows.size, dtype=np.uint32)
+        c2, _, e2, o2 = geom_filter(engine, empty, (sub, sub_off), sp, cols, WORLD, False, bits)
+        codes[redo], enc[redo], ok[redo] = c2, e2, o2
+    return codes, enc, ok
+
+
 def update_spatial_filter_index(engine, repo, commits, db_path=None, clear_existing=False, bits=None):
     """Index the feature envelopes of ``commits`` (revisions; their ancestors implicitly) into
     ``db_path`` (default <gitdir>/feature_envelopes.db), building on what is already indexed.
@@ -250,10 +275,7 @@ def update_spatial_filter_index(engine, repo, commits, db_path=None, clear_exist
         present = np.nonzero(status == 0)[0]  # promised blobs: not indexable here (the reference skips them too)
         pairs = np.full((present.size, 2), N.KD_NONE, np.uint32)
         pairs[:, 1] = present.astype(np.uint32)
-        from .spatial import geom_filter
-
-        codes, _, enc, ok = geom_filter(engine, (np.zeros(0, np.uint8), np.zeros(1, np.uint64)), (data, off), pairs,
-                                        _geom_cols(info), WORLD, False, bits)
+        codes, enc, ok = _index_envelopes(engine, data, off, pairs, _geom_cols(info), bits)
         out["fallback"] += int(np.count_nonzero(codes[:, 1] == 3))
         for j in np.nonzero(ok)[0].tolist():
             rows.append((raw[present[j]].tobytes(), enc[j].tobytes()))

@@ -173,6 +173,29 @@ def test_gpu_geom_filter_vs_oracle_crafted(engine, bits):
 
 
 @pytest.mark.gpu
+def test_gpu_index_envelopes_heads_equal_arena_path(engine):
+    """the spatial indexer's batch (spatial_index._index_envelopes: heads to the GPU, the rows a
+    head cannot decide re-run whole through kd_geom_filter) equals the blob-arena kernel row for
+    row on the crafted blobs (XYZ / NaN envelopes, ext16/32, unknown legends, nested values)"""
+    from kart_amd.spatial_index import WORLD, _index_envelopes
+
+    blobs, cols = _crafted(np.random.default_rng(21), 8000)
+    d, o = _arena(blobs)
+    gc = S.GeomCols.__new__(S.GeomCols)
+    gc.old_hex = gc.new_hex = np.frombuffer(b"".join(h.encode() for h in sorted(cols)), np.uint8).copy()
+    gc.old_gidx = gc.new_gidx = np.array([cols[h] for h in sorted(cols)], np.int16)
+    gc.old_map = gc.new_map = cols
+    rows = np.random.default_rng(22).permutation(len(blobs))[:7000]
+    pairs = np.full((rows.size, 2), NONE, np.uint32)
+    pairs[:, 1] = rows
+    codes, enc, ok = _index_envelopes(engine, d, o, pairs, gc, 20)
+    ac, _, ae, aok = S.geom_filter(engine, (np.zeros(0, np.uint8), np.zeros(1, np.uint64)), (d, o), pairs, gc, WORLD,
+                                   False, 20)
+    assert np.array_equal(codes, ac) and np.array_equal(ok, aok) and np.array_equal(enc[ok == 1], ae[aok == 1])
+    assert ok.sum() > 5000 and (codes[:, 1] == 3).any()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [2000, 300_000])
 def test_gpu_geom_filter_polygon_layer(engine, n):
     """the synthetic polygon layer (C3/C5 shape): classify2 deltas, then the filter over them"""
