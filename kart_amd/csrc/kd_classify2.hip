@@ -182,6 +182,12 @@ struct Join2Lds {
     // keys of both sides (8 B per item, +1 lookahead key on B, +1 lookbehind key per side) and at
     // most two extra (partial) chunks per range
     static constexpr int CHK = (8 * (TILE + 1) + 16 + 15) / 16 + 4;
+    // KD_KEY_HASH: the tile's filename bytes of both sides (a tile whose names need more takes the
+    // global compare); sized so four 256-thread blocks still fit a CU's LDS with the keys
+#ifndef KD_J2_NAME_CH
+#define KD_J2_NAME_CH 1900
+#endif
+    static constexpr int NMCH = KD_J2_NAME_CH;
     // 4-ary search rounds until a width of TILE shrinks to 0 (w -> ceil(w/4) - 1)
     static constexpr int rounds(int w) { return w <= 0 ? 0 : 1 + rounds((w + 3) / 4 - 1); }
     static constexpr int SEARCH_ROUNDS = rounds(TILE);
@@ -445,7 +451,10 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // (HASH: filename checks compiled in; the int-key instantiation carries none of their registers)
     using LD = Join2Lds<NT, IPT>;
     static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
+    // filenames of matched pairs compared from LDS (KD_KEY_HASH, sorted-order name arenas)
+    constexpr bool LNAMES = HASH && !PERM;
     __shared__ u32x4 s_ch[LD::CHK];  // the two key ranges; lanes past the tile's chunks are masked off
+    __shared__ u32x4 s_nm[LNAMES ? LD::NMCH : 1];
     __shared__ u32 s_wave[3 * NT / 64];
     __shared__ u64 s_base[2];
     const int tid = threadIdx.x;
@@ -453,26 +462,44 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     const TileGeo q = tile_geo(g, tile, LD::TILE);
     if (!q.ok && tid == 0) atomicOr(g.err, 1u);
     const TileRanges r = tile_ranges(g, q);
+    // the tile's filename byte ranges: A [off[i0], off[i1]), B [off[j0], off[j1e]) (the lookahead
+    // entry's name too: a match may pair with it) — loaded with the key DMA
+    u64 nmA0 = 0, nmA1 = 0, nmB0 = 0, nmB1 = 0;
+    if (LNAMES) {
+        nmA0 = g.nameOffA[q.i0]; nmA1 = g.nameOffA[q.i1];
+        nmB0 = g.nameOffB[q.j0]; nmB1 = g.nameOffB[q.j1e];
+    }
     // 64-chunk pieces (one wave-instruction each: wave-uniform source base and LDS base, lane l takes
     // chunk 64p + l), dealt round-robin to the waves across the two ranges: scalar address math
-    {
+    auto dma2 = [&](const Range& R0, const Range& R1, u32 c1, u32x4* dst) {
         constexpr int NW = NT / 64;
         const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
         u32 q0 = 0;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const Range& R = k == 0 ? r.ka : r.kb;
-            const u32 off = k == 0 ? 0 : r.c1;
+            const Range& R = k == 0 ? R0 : R1;
+            const u32 off = k == 0 ? 0 : c1;
             const u32 np = (R.nch + 63) >> 6;
             for (u32 p = (u32)(wid + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
                 const u32 c = 64 * p + lane;
                 if (c < R.nch)
-                    __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(s_ch + off + 64 * p), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(dst + off + 64 * p), 16, 0, 0);
             }
             q0 += np;
         }
-    }
+    };
+    dma2(r.ka, r.kb, r.c1, s_ch);
     __syncthreads();  // vmcnt(0) + barrier: the DMA has landed
+    // the names DMA runs under the walk and the OID loads
+    Range rnA{}, rnB{};
+    bool lnames = false;
+    if (LNAMES) {
+        nmA0 = uni64(nmA0); nmA1 = uni64(nmA1); nmB0 = uni64(nmB0); nmB1 = uni64(nmB1);
+        rnA = mk_range(g.nameA, nmA0, nmA1);
+        rnB = mk_range(g.nameB, nmB0, nmB1);
+        lnames = nmA1 >= nmA0 && nmB1 >= nmB0 && (u64)rnA.nch + rnB.nch <= (u64)LD::NMCH;
+        if (lnames) dma2(rnA, rnB, rnA.nch, s_nm);
+    }
     const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
     const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
     u32 rec[IPT];
@@ -484,8 +511,36 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
     for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
     u32 ra[IPT], rb[IPT];
+    // the matched pairs' name offsets, issued with the OID loads: low words only (differences of
+    // offsets inside one tile's names fit 32 bits, and modular arithmetic gives them exactly)
+    u32 oa0[IPT], oa1[IPT], ob0[IPT], ob1[IPT];
+    if (LNAMES && lnames) {
+        const u32* offA = (const u32*)g.nameOffA;
+        const u32* offB = (const u32*)g.nameOffB;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const bool m = (rec[k] >> 25) == R_MATCH;
+            const u64 i = q.i0 + (m ? (rec[k] & 0xFFF) : 0), j = q.j0 + (m ? ((rec[k] >> 12) & 0xFFF) : 0);
+            oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
+            ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
+        }
+    }
     tile_oid_global<IPT, PERM>(g, q, rec, ra, rb);
-    if (HASH) tile_names<IPT>(g, rec, ra, rb);
+    if (LNAMES && lnames) {
+        __syncthreads();  // vmcnt(0) + barrier: every wave's share of the names DMA has landed
+        const u32 nm = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_nm;
+        const u32 baseA = nm + rnA.skew, baseB = nm + 16 * rnA.nch + rnB.skew;
+        bool ne = false;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            if ((rec[k] >> 25) != R_MATCH) continue;
+            const u32 la = oa1[k] - oa0[k], lb = ob1[k] - ob0[k];
+            ne |= la != lb || !lds_eq_bytes(baseA + (oa0[k] - (u32)nmA0), baseB + (ob0[k] - (u32)nmB0), la);
+        }
+        if (ne) atomicOr(g.err, 2u);
+    } else if (HASH) {
+        tile_names<IPT>(g, rec, ra, rb);
+    }
     if (bad) atomicOr(g.err, 1u);
     const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
     uint2 *sd, *su;

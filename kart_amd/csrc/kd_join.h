@@ -42,6 +42,29 @@ __device__ bool names_eq(const u8* __restrict__ na, const u64* __restrict__ oa, 
     return diff == 0;
 }
 
+// bytes [a, a + n) and [b, b + n) of LDS (byte addresses) equal: 16-byte blocks, the 5 aligned
+// words of each side read together and realigned with v_alignbyte (reads may run 4 bytes past a
+// range: still LDS, masked)
+__device__ __forceinline__ bool lds_eq_bytes(u32 a, u32 b, u32 n) {
+    typedef const __attribute__((address_space(3))) u32* l32;
+    const u32 sa = a & 3, sb = b & 3;
+    u32 wa = a - sa, wb = b - sb, diff = 0;
+    for (u32 rem = n; rem > 0 && diff == 0; rem = rem > 16 ? rem - 16 : 0) {
+        u32 xa[5], xb[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) { xa[j] = *(l32)(size_t)(wa + 4 * j); xb[j] = *(l32)(size_t)(wb + 4 * j); }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32 d = __builtin_amdgcn_alignbyte(xa[j + 1], xa[j], sa) ^ __builtin_amdgcn_alignbyte(xb[j + 1], xb[j], sb);
+            const u32 valid = rem >= 4u * j + 4 ? 0xFFFFFFFFu : rem > 4u * j ? (1u << (8 * (rem - 4 * j))) - 1 : 0u;
+            diff |= d & valid;
+        }
+        wa += 16;
+        wb += 16;
+    }
+    return diff == 0;
+}
+
 // K filename comparisons at once, all loads issued before any compare: each name's offsets, then a
 // W-dword window of each name (the dwords holding its bytes; past its last dword the window
 // re-reads dword 0, so every load stays inside the name).  Bit k of the result = pair k is active

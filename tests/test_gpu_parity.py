@@ -407,10 +407,11 @@ def _hash_sides(rng, n, lens):
     return keys, names, oids, side
 
 
-@pytest.mark.parametrize("lens", [[24], [1, 2, 3, 5, 7, 13, 29, 30, 31, 33, 64, 100]])
+@pytest.mark.parametrize("lens", [[24], [1, 2, 3, 5, 7, 13, 29, 30, 31, 33, 64, 100], [200]])
 def test_gpu_hash_names_verified(engine, lens):
-    """KD_KEY_HASH: matched keys with equal filenames classify normally (the batched 32-B window and
-    the long-name loop both); one differing byte in one matched filename (first, middle or last
+    """KD_KEY_HASH: matched keys with equal filenames classify normally (the join's LDS-staged tile
+    names; with 200-byte names a tile's names overflow that buffer and take the global compare: the
+    batched 32-B window and the long-name loop); one differing byte in one matched filename (first, middle or last
     byte, or a length change) is a key collision -> Unsupported, for diff2 and for merge3 (ancestor
     vs ours and ancestor vs theirs-without-ours)"""
     from kart_amd import _native as N
