@@ -48,7 +48,6 @@ struct Resolve3Args {
     uint2* out_md;          // (o, t) per merge delta
     u64* counts;            // clean, conflicts, mdeltas, 0
     u32* err;
-    const u64* bracket;     // [2][chunk] ancestor bracket of each chunk (k_c3_brackets)
 };
 
 // ancestor strictly ascending (-> aux[1]), and the resolve's counters zeroed
@@ -94,24 +93,6 @@ __device__ __forceinline__ u64 half_lower_bound(const u64* __restrict__ X, u64 n
     return lo;
 }
 
-// every chunk's ancestor bracket [lower_bound(first key), lower_bound(last key) + 1), all chunks at
-// once ahead of k_resolve3 (one wave per chunk, grid-stride: a 32-ary search per key by each
-// half-wave), so a chunk's bracket is one load on k_resolve3's critical path, not ~6 dependent ones
-__global__ __launch_bounds__(256) void k_c3_brackets(Resolve3Args g, u64* __restrict__ br) {
-    const u64 n = g.c2[3];
-    const int lane = threadIdx.x & 63;
-    const u64 w0 = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((u64)gridDim.x * blockDim.x) >> 6;
-    for (u64 w = w0; w * C3_CH < n; w += nw) {
-        const u64 base = w * C3_CH;
-        const u32 cnt = (u32)(n - base < (u64)C3_CH ? n - base : (u64)C3_CH);
-        const uint2 r = g.cand[base + (lane < 32 ? 0 : cnt - 1)];
-        const u64 k = *(r.x != KD_NONE ? g.O + r.x : g.T + r.y);
-        const u64 p = half_lower_bound(g.A, g.nA, k);
-        if (lane == 0) br[2 * w] = p;
-        if (lane == 32) br[2 * w + 1] = p < g.nA ? p + 1 : g.nA;
-    }
-}
-
 template <int NT>
 __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
     constexpr int PT = C3_CH / NT;
@@ -134,10 +115,12 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
         if (base >= n) break;
         const u32 cnt = (u32)(n - base < (u64)C3_CH ? n - base : (u64)C3_CH);
         auto key_of = [&](uint2 r) { return *(r.x != KD_NONE ? g.O + r.x : g.T + r.y); };  // one load
-        // the chunk's ancestor bracket (k_c3_brackets)
-        if (tid == 0) {
-            s_b[1] = g.bracket[2 * t];
-            s_b[2] = g.bracket[2 * t + 1];
+        // the chunk's ancestor bracket: [lower_bound(first key), lower_bound(last key) + 1)
+        if (wid == 0) {
+            const u64 k = key_of(g.cand[base + (lane < 32 ? 0 : cnt - 1)]);
+            const u64 p = half_lower_bound(g.A, g.nA, k);
+            if (lane == 0) s_b[1] = p;
+            if (lane == 32) s_b[2] = p < g.nA ? p + 1 : g.nA;
         }
         uint2 rec[PT];
         u64 key[PT];
@@ -318,9 +301,8 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     int rc;
     const u64 nA = A.n, nO = O.n, nT = T.n;
     const u64 nchunk = (nO + nT) / C3_CH + 2;
-    void *cand, *c2, *desc, *aux, *dz, *br;
+    void *cand, *c2, *desc, *aux, *dz;
     if ((rc = ensure(ctx, "c3.cand", (nO + nT + 1) * 8, &cand))) return rc;
-    if ((rc = ensure(ctx, "c3.br", 2 * nchunk * 8, &br))) return rc;
     if ((rc = ensure(ctx, "c3.c2", 64, &c2))) return rc;
     if ((rc = ensure(ctx, "c3.desc", 2 * nchunk * 8, &desc))) return rc;
     const bool fresh_aux = ctx->bufs["c3.aux"].p == nullptr;
@@ -355,13 +337,6 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     g.cand = (const uint2*)cand; g.c2 = (const u64*)c2;
     g.desc = (u64*)desc; g.nchunk = nchunk; g.aux = (u32*)aux;
     g.out_conf = d_conf; g.out_md = d_md; g.counts = counts; g.err = derr;
-    g.bracket = (const u64*)br;
-    rc = launch(ctx, "k_c3_brackets", [&] {
-        const u64 waves = std::min<u64>(nchunk, (u64)ctx->n_cu * 16);
-        hipLaunchKernelGGL(k_c3_brackets, dim3((unsigned)std::max<u64>((waves + 3) / 4, 1)), dim3(256), 0, ctx->stream, g,
-                           (u64*)br);
-    });
-    if (rc) return rc;
     // persistent: at most every resident workgroup, at most one per chunk (+1 so someone adds the
     // clean count when there are no differing paths)
     const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)ctx->occ_resolve3);
