@@ -225,9 +225,12 @@ class DatasetVersion:
         data, off, status = self.read_blobs(idx)
         if status.any():
             self.read_blob(int(idx[int(np.nonzero(status)[0][0])]))  # raises the reference's KeyError
+        self._remember_arena(idx, data, off)
+        return data, off
+
+    def _remember_arena(self, idx, data, off):
         order = np.argsort(idx, kind="stable")
         self._arenas.append((idx[order], order, data, off))
-        return data, off
 
     def cached_blob(self, i):
         """leaf i's bytes from an arena blob_arena_leaves read, or None"""
@@ -457,8 +460,7 @@ def field_diff(engine, feature_diff, old_version, new_version, stats=None):
             ups = batch.deltas
             if not ups:
                 return 0
-            od, oo = old_version.blob_arena_leaves(batch.old_leaf)
-            nd, no = new_version.blob_arena_leaves(batch.new_leaf)
+            (od, oo), (nd, no) = _arena_pair(old_version, new_version, batch.old_leaf, batch.new_leaf)
         else:
             ups = [d for d in feature_diff.values() if d.type == "update"]
             if not ups:
@@ -475,6 +477,25 @@ def field_diff(engine, feature_diff, old_version, new_version, stats=None):
         if stats is not None:
             stats.update(read_s=t1 - t0, kernel_s=t2 - t1, attach_s=time.perf_counter() - t2)
         return len(ups)
+
+
+def _arena_pair(old_v, new_v, old_leaf, new_leaf):
+    """blob_arena_leaves of both sides; versions read from one repository take ONE batched read (one
+    thread pool over both sides' delta chains: the old side's deep chains and the new side's short
+    ones balance), split into two arenas over the same buffer"""
+    src = getattr(old_v._read_blobs, "source", None)
+    if src is None or src is not getattr(new_v._read_blobs, "source", None):
+        return old_v.blob_arena_leaves(old_leaf), new_v.blob_arena_leaves(new_leaf)
+    oi, ni = np.asarray(old_leaf, np.int64), np.asarray(new_leaf, np.int64)
+    data, off, status = src.read_blobs(np.concatenate([old_v.oids[oi], new_v.oids[ni]]))
+    if status.any():  # the per-side reads raise the reference's KeyError for the first missing blob
+        return old_v.blob_arena_leaves(old_leaf), new_v.blob_arena_leaves(new_leaf)
+    k = oi.size
+    cut = int(off[k])
+    arenas = ((data[:cut], off[:k + 1]), (data[cut:], off[k:] - off[k]))
+    old_v._remember_arena(oi, *arenas[0])
+    new_v._remember_arena(ni, *arenas[1])
+    return arenas
 
 
 def _live_batch(feature_diff, old_version, new_version):

@@ -235,6 +235,8 @@ class GitRepo:
         def read_blobs(idx):
             return repo.read_blobs(oid_arr[np.asarray(idx, np.int64)])
 
+        read_blobs.source = repo  # versions of one repository can share a batched read
+
         v = DatasetVersion(ds_path, schema, legends, PathEncoding.from_dict(path_structure), leaves.paths,
                            leaves.off, oid_arr, read_blob, meta, read_blobs=read_blobs)
         v.partial = partial

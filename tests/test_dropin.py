@@ -288,3 +288,35 @@ def test_changed_names_rows_matches_per_row():
         assert rows == [fm.changed_names(r) for r in masks]
         assert len({id(r) for r in rows}) == len(rows)
     assert fm.changed_names_rows(np.zeros((0, fm.words), np.uint64)) == []
+
+
+def test_field_diff_one_read_for_both_sides(tmp_path, eng):
+    """versions of one git repository: field_diff reads both sides' update blobs in ONE batched
+    read, split into two arenas over the same buffer; the changed fields are those whose values
+    differ, and every value the writer reads afterwards comes from the arenas"""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import e2e_repo_bench as E
+    from kart_amd.gitsource import GitRepo
+
+    gitdir = str(tmp_path / "r.git")
+    k = E.build(gitdir, 3000)
+    repo = GitRepo(gitdir)
+    try:
+        old, new = repo.diff_versions("main^", "main", E.DS)
+        calls, orig = [], repo.read_blobs
+        repo.read_blobs = lambda oids, *a, **kw: (calls.append(len(oids)), orig(oids, *a, **kw))[1]
+        fd = D.get_dataset_diff(eng, old, new)["feature"]
+        assert D.field_diff(eng, fd, old, new) == k
+        assert calls == [2 * k]
+        cats = []
+        old.read_blob = new.read_blob = lambda i: cats.append(i)  # no single-object read may happen
+        for d in fd.values():
+            if d.type != "update":
+                continue
+            a, b = d.old_value, d.new_value
+            assert sorted(d.changed_fields) == sorted(f for f in a if a[f] != b.get(f))
+        assert not cats and calls == [2 * k]
+    finally:
+        repo.close()
