@@ -188,6 +188,8 @@ struct Join2Lds {
 #define KD_J2_NAME_CH 1900
 #endif
     static constexpr int NMCH = KD_J2_NAME_CH;
+    // the tile's OIDs of both sides (20 B per entry, the lookahead entry too) when staged in LDS
+    static constexpr int OCH = (20 * (TILE + 1) + 32 + 15) / 16 + 4;
     // 4-ary search rounds until a width of TILE shrinks to 0 (w -> ceil(w/4) - 1)
     static constexpr int rounds(int w) { return w <= 0 ? 0 : 1 + rounds((w + 3) / 4 - 1); }
     static constexpr int SEARCH_ROUNDS = rounds(TILE);
@@ -446,15 +448,20 @@ __device__ __forceinline__ void tile_write(const u32 rec[IPT], const TileCounts&
 // The tile is staged in ONE HBM round trip: keys and OIDs of both sides go global -> LDS by LDS-DMA
 // (global_load_lds_dwordx4: 16 B per lane, the wave's 64 chunks land contiguously), all issued
 // before any use.
-template <int NT, int IPT, bool UNORD, bool HASH, bool PERM>
+template <int NT, int IPT, bool UNORD, bool HASH, bool PERM, bool OL = false>
 __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // (HASH: filename checks compiled in; the int-key instantiation carries none of their registers)
     using LD = Join2Lds<NT, IPT>;
     static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
     // filenames of matched pairs compared from LDS (KD_KEY_HASH, sorted-order name arenas)
     constexpr bool LNAMES = HASH && !PERM;
+    // OL (large int-key joins): the tile's OIDs by LDS-DMA with the keys, so the matched pairs
+    // compare from LDS with no global round trip after the walk (20.6 KB more LDS: 5 blocks per CU
+    // instead of 8, which costs more than it saves on small joins)
+    constexpr bool LOIDS = OL && !HASH && !PERM;
     __shared__ u32x4 s_ch[LD::CHK];  // the two key ranges; lanes past the tile's chunks are masked off
     __shared__ u32x4 s_nm[LNAMES ? LD::NMCH : 1];
+    __shared__ u32x4 s_oid[LOIDS ? LD::OCH : 1];
     __shared__ u32 s_wave[3 * NT / 64];
     __shared__ u64 s_base[2];
     const int tid = threadIdx.x;
@@ -489,6 +496,12 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         }
     };
     dma2(r.ka, r.kb, r.c1, s_ch);
+    Range roA{}, roB{};
+    if (LOIDS) {
+        roA = mk_range(g.oidA, 20 * q.i0, 20 * q.i1);
+        roB = mk_range(g.oidB, 20 * q.j0, 20 * q.j1e);
+        dma2(roA, roB, roA.nch, s_oid);
+    }
     __syncthreads();  // vmcnt(0) + barrier: the DMA has landed
     // the names DMA runs under the walk and the OID loads
     Range rnA{}, rnB{};
@@ -525,7 +538,22 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
             ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
         }
     }
-    tile_oid_global<IPT, PERM>(g, q, rec, ra, rb);
+    if (LOIDS) {  // matched pairs' OIDs from LDS (both tile ranges landed with the keys)
+        typedef const __attribute__((address_space(3))) u32* l32;
+        const u32 ob = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_oid;
+        const u32 baseA = ob + roA.skew, baseB = ob + 16 * roA.nch + roB.skew;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const bool m = (rec[k] >> 25) == R_MATCH;
+            const u32 pa = baseA + 20 * (m ? (rec[k] & 0xFFF) : 0), pb = baseB + 20 * (m ? ((rec[k] >> 12) & 0xFFF) : 0);
+            u32 d = 0;
+#pragma unroll
+            for (int w = 0; w < 5; w++) d |= *(l32)(size_t)(pa + 4 * w) ^ *(l32)(size_t)(pb + 4 * w);
+            if (m && d) rec[k] |= 1u << 24;
+        }
+    } else {
+        tile_oid_global<IPT, PERM>(g, q, rec, ra, rb);
+    }
     if (LNAMES && lnames) {
         __syncthreads();  // vmcnt(0) + barrier: every wave's share of the names DMA has landed
         const u32 nm = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_nm;
@@ -735,6 +763,13 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.hash_mode = hash ? 1 : 0;
     g.dummy = (const u8*)dz;
     const bool perm = ordA != nullptr || ordB != nullptr;
+    // OIDs staged in LDS from this many entries on (C3's 200M: k_join2 1.28 -> 1.20 ms; C2's 20M:
+    // 0.131 -> 0.136, profiles/r03/join2_oid_lds_ab.jsonl); KD_J2_OIDLDS_MIN overrides (tests)
+    static const u64 oid_lds_min = [] {
+        const char* e = getenv("KD_J2_OIDLDS_MIN");
+        return e ? strtoull(e, nullptr, 10) : (u64)1 << 26;
+    }();
+    const bool oid_lds = nA + nB >= oid_lds_min;
     g.ordA = nA && ordA ? ordA : (const u32*)dz;
     g.ordB = nB && ordB ? ordB : (const u32*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
@@ -743,14 +778,18 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.ntiles = ntiles;
     rc = launch(ctx, "k_join2", [&] {
 #define KD_J2(U, H, P) hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, U, H, P>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g)
+#define KD_J2OL(U) hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, U, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g)
         if (perm) {
             if (unord) { if (hash) KD_J2(true, true, true); else KD_J2(true, false, true); }
             else { if (hash) KD_J2(false, true, true); else KD_J2(false, false, true); }
+        } else if (!hash && oid_lds) {
+            if (unord) KD_J2OL(true); else KD_J2OL(false);
         } else {
             if (unord) { if (hash) KD_J2(true, true, false); else KD_J2(true, false, false); }
             else { if (hash) KD_J2(false, true, false); else KD_J2(false, false, false); }
         }
 #undef KD_J2
+#undef KD_J2OL
     });
     if (rc || unord) return rc;
     rc = launch(ctx, "k_gscan2", [&] {
