@@ -799,6 +799,12 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
     for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
 }
 
+#ifndef KD_FD_PROBE_NOPARSE
+#define KD_FD_PROBE_NOPARSE 0
+#endif
+#ifndef KD_FD_PROBE_NOCMP
+#define KD_FD_PROBE_NOCMP 0
+#endif
 constexpr u32 FD_TAB_LDS_MAX = 16384;
 // window shapes (updates per round, head chunks, tail chunks): small features / larger ones
 #ifndef KD_FD_SHAPE_L
@@ -960,7 +966,11 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             B.start = b0; B.len = nn; B.s0 = (u32)(b0 & 15);
             B.t0 = (int)(((b0 + (nn ? nn - 1 : 0)) & ~(u64)15) - (b0 & ~(u64)15)) - 16 * (NTL - 1);
             B.img = img0 + 16u * (u32)(UPR * NC + lane * NC);
+#if KD_FD_PROBE_NOPARSE  // timing probe only (results invalid): no parse, no queued payloads
+            (void)queue;
+#else
             st = diff_one_w(A, B, tb, mk, m, queue);
+#endif
         }
         __syncthreads();  // parse done: the image is free, the queue complete
         if (more) {
@@ -969,7 +979,11 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, 
             pr_n = load_pair(u2 + lane);
         }
         // ---- the queued payloads, 16 lanes per payload ----
+#if KD_FD_PROBE_NOCMP  // timing probe only (results invalid): queued payloads dropped
+        const u32 nt = 0;
+#else
         const u32 nt = min(s_ntask, TCAP);
+#endif
         // (M payloads per 16-lane group per pass: their loads share one memory round trip)
         constexpr int M = TM, G = TG, NG = 64 / TG;
         for (u32 t = (u32)lane / G; t < nt; t += NG * M) {
