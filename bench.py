@@ -73,6 +73,7 @@ def parse():
     ap.add_argument("--no-delta-order", action="store_true",
                     help="c5: skip timing the heads kernel on the drop-in's delta-order layout")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
+    ap.add_argument("--no-heads-path", action="store_true", help="c5env: skip the indexer's heads-path timing")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--time-all", action="store_true",
@@ -819,6 +820,9 @@ def run_c5env(args, H):
     # (32 B, polygons) or point WKB (21 B) read; match + enc_ok flags (2 B) + encoded envelope written
     alg = n * (8 + 8 + 2 + nb) + npt * 21 + (n - npt) * 32
     roof = roofline(kern, "k_envelopes", alg, args.traffic_json, n)
+    heads_path = None
+    if not args.no_heads_path:
+        heads_path = c5env_heads_path(args, H, eng, data, off, d_data, d_off, n, bits, nb, enc, ok)
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         O = oracle()
@@ -852,8 +856,72 @@ def run_c5env(args, H):
                    "geoms_per_gpu": n, "points": npt, "bits": bits, "filter": list(synth.C5_FILTER),
                    "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
-        "roofline": roof, "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu, "heads_path": heads_path,
     }
+
+
+def c5env_heads_path(args, H, eng, data, off, d_data, d_off, n, bits, nb, enc, ok):
+    """the spatial indexer's path over the same geometries (spatial_index._index_envelopes): one
+    48-B head per geometry (what kd_geom_heads leaves for a blob whose geometry value this is; built
+    here straight from the geometry arena, outside the timing) through kd_geom_filter_heads with the
+    arena for the heads that cannot decide; its index envelopes must equal k_envelopes'"""
+    import ctypes
+
+    from kart_amd import _native as N
+    from kart_amd.device import DevBuf
+    from kart_amd.spatial import GEOM_HEAD
+
+    heads = np.zeros(n, GEOM_HEAD)
+    lens = np.diff(off).astype(np.int64)
+    heads["glen"] = lens
+    heads["goff_status"] = np.where(lens > 0, N.KD_GH_GEOM << 24, N.KD_GH_NULL << 24).astype(np.uint32)
+    col = np.arange(40, dtype=np.int64)
+    for a in range(0, n, 1 << 19):  # first 40 bytes of each geometry (zeros past its end)
+        b = min(n, a + (1 << 19))
+        idx = off[a:b, None].astype(np.int64) + col
+        inside = col < lens[a:b, None]
+        heads["gpkg"][a:b] = np.where(inside, data[np.minimum(idx, data.size - 1)], 0)
+    dh = DevBuf.from_numpy(eng, heads.view(np.uint8).reshape(-1))
+    pairs = np.full((n, 2), N.KD_NONE, np.uint32)
+    pairs[:, 1] = np.arange(n, dtype=np.uint32)
+    dp = DevBuf.from_numpy(eng, pairs.reshape(-1))
+    m2, kp, nk = DevBuf(eng, 2 * n + 2), DevBuf(eng, 4 * n + 4), DevBuf(eng, 8)
+    e2, ok2 = DevBuf(eng, n * nb + 4), DevBuf(eng, n + 4)
+    empty_off = DevBuf.from_numpy(eng, np.zeros(1, np.uint64))
+    blobs = []
+    for d_, o_, cnt in ((d_data, empty_off, 0), (d_data, d_off, n)):
+        b_ = N.KdBlobs()
+        b_.n, b_.data, b_.off, b_.mem, b_.size_hint = cnt, d_.ptr, o_.ptr, N.KD_MEM_DEVICE, 0
+        blobs.append(b_)
+    fe = (ctypes.c_double * 4)(-180.0, 180.0, -90.0, 90.0)  # the indexer's world envelope
+
+    def filt():
+        N.check(eng.L.kd_geom_filter_heads(eng.ctx, dh.ptr, 0, dh.ptr, n, N.KD_MEM_DEVICE, ctypes.byref(blobs[0]),
+                                           ctypes.byref(blobs[1]), dp.ptr, n, None, N.KD_MEM_DEVICE, fe, 0, bits,
+                                           m2.ptr, kp.ptr, ctypes.cast(nk.ptr, N.c_u64p), e2.ptr, ok2.ptr,
+                                           N.KD_MEM_DEVICE), "kd_geom_filter_heads")
+
+    filt()
+    eng.sync()
+    if not args.no_check:
+        g_ok, h_ok = ok2.download(np.uint8, n), ok.download(np.uint8, n)
+        assert np.array_equal(g_ok, h_ok), "heads path enc_ok differs from k_envelopes"
+        g_enc, h_enc = e2.download(np.uint8, n * nb).reshape(n, nb), enc.download(np.uint8, n * nb).reshape(n, nb)
+        sel = h_ok == 1
+        assert np.array_equal(g_enc[sel], h_enc[sel]), "heads path envelopes differ from k_envelopes"
+    eng.prof_reset()
+    eng.prof_select(["k_gf_heads"])
+    eng.prof_enable(True)
+    el = timed(H, eng, filt, args.steps)
+    eng.prof_enable(False)
+    kd = kernel_times(eng, ("k_gf_heads",))
+    alg = 8 * n + 48 * n + n * (2 + nb + 1)
+    for b_ in (dh, dp, m2, kp, nk, e2, ok2, empty_off):
+        b_.free()
+    return {"what": "the spatial indexer's path: 48-B geometry heads (built from the arena outside the timing) "
+                    "through kd_geom_filter_heads, envelopes equal to k_envelopes'",
+            "ms_per_call": round(el / args.steps * 1e3, 4),
+            "roofline": roofline(kd, "k_gf_heads", alg, "", -1)}
 
 
 # ---------------------------------------------------------------------------------------------
