@@ -824,8 +824,13 @@ constexpr int fd_upr(const void*) { return UPR; }  // tables up to this size are
 typedef __attribute__((address_space(3))) void* fd_lds_vp;
 typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 
+#ifdef KD_FD_WPE  // probe builds: a waves-per-SIMD floor (the register budget follows from it)
+#define KD_FD_ATTR __attribute__((amdgpu_waves_per_eu(KD_FD_WPE)))
+#else
+#define KD_FD_ATTR
+#endif
 template <int UPR, int NH, int NTL, int TM, int TG, int TS>
-__global__ __launch_bounds__(FD_NT) void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
+__global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
                                                      const u64* __restrict__ n_upd_dev, FdTab tg, FdTabOff to,
