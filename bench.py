@@ -168,7 +168,7 @@ def timed(H, eng, step, steps):
     return H.max(time.perf_counter() - t0)
 
 
-ROCPROF_STATS = {"c3": "profiles/r03/c3_kernel_stats.csv", "c3v": "profiles/r03/c3v_kernel_stats.csv",
+ROCPROF_STATS = {"c3": "profiles/r03/c3_kernel_stats.csv", "c3v": "profiles/r03/c3v_kernel_stats.csv", "c4": "profiles/r03/c4_kernel_stats.csv",
                  "c5": "profiles/r03/c5_kernel_stats.csv"}
 
 
@@ -1064,7 +1064,7 @@ def run_c4(args, H):
     _, io, it = np.intersect1d(O_.key, T.key, assume_unique=True, return_indices=True)
     n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((O_.oid[io] != T.oid[it]).any(axis=1)))
     alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand
-    roof = roofline(kern, "k_join2", alg, args.traffic_json, n)
+    roof = roofline(kern, "k_join2", alg, args.traffic_json, n, "c4" if H.world == 1 else None)
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         Orc = oracle()
