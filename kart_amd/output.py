@@ -133,6 +133,12 @@ def geometry_type_names(data, off):
     return out, np.nonzero(bad)[0]
 
 
+try:
+    from . import _kd_pystr as _pystr  # built with libkartdiff (kart_amd/csrc/Makefile)
+except ImportError:  # pragma: no cover - the helper is optional host code
+    _pystr = None
+
+
 def _arena(values):
     lens = np.fromiter((len(v) for v in values), np.uint64, len(values))
     off = np.zeros(len(values) + 1, np.uint64)
@@ -142,10 +148,16 @@ def _arena(values):
 
 
 def _slices(hexbuf, lo, hi):
-    """the hex strings [lo[i], hi[i]) of one output buffer: decoded to one str once, then sliced
-    with bounds computed in numpy (no per-value int() / bytes slice / decode)"""
-    text = hexbuf.tobytes().decode("ascii")
-    return [text[a:b] for a, b in zip(lo.tolist(), hi.tolist())]
+    """the hex strings [lo[i], hi[i]) of one output buffer, one str per value: built in C straight
+    from the buffer (kart_amd/_kd_pystr: PyUnicode_New + memcpy per value); without that helper,
+    one decode of the buffer and a slice per value"""
+    buf = np.ascontiguousarray(hexbuf, np.uint8)
+    lo = np.ascontiguousarray(lo, np.int64)
+    hi = np.ascontiguousarray(hi, np.int64)
+    if _pystr is not None:
+        return _pystr.ascii_slices(buf, lo, hi)
+    text = str(memoryview(buf), "ascii")
+    return list(map(text.__getitem__, map(slice, lo.tolist(), hi.tolist())))
 
 
 def hex_wkb_arena(engine, geoms=None, arena=None):

@@ -351,3 +351,28 @@ def test_geometry_type_names_batch_equals_per_value():
             assert i in badset
             continue
         assert i not in badset and labels[i] == want
+
+
+def test_ascii_slices_helper_equals_python_slices():
+    """the writer's per-value str construction (kart_amd/_kd_pystr, built with libkartdiff) equals
+    slicing one decoded str, empty ranges and the buffer's ends included; bad ranges raise"""
+    import numpy as np
+
+    from kart_amd import output as OUT
+
+    assert OUT._pystr is not None, "kart_amd/_kd_pystr was not built (make -C kart_amd/csrc)"
+    rng = np.random.default_rng(4)
+    buf = np.frombuffer(rng.choice(np.frombuffer(b"0123456789ABCDEFabcdef", np.uint8), 5000).tobytes(), np.uint8)
+    lo = np.sort(rng.integers(0, 5000, 300)).astype(np.int64)
+    hi = np.minimum(lo + rng.integers(0, 60, 300), 5000).astype(np.int64)
+    lo[:3], hi[:3] = (0, 4990, 7), (10, 5000, 7)
+    text = buf.tobytes().decode("ascii")
+    want = [text[a:b] for a, b in zip(lo.tolist(), hi.tolist())]
+    assert OUT._slices(buf, lo, hi) == want
+    saved, OUT._pystr = OUT._pystr, None
+    try:
+        assert OUT._slices(buf, lo, hi) == want
+    finally:
+        OUT._pystr = saved
+    with pytest.raises(ValueError):
+        OUT._pystr.ascii_slices(buf, np.array([0], np.int64), np.array([5001], np.int64))
