@@ -320,3 +320,31 @@ def test_field_diff_one_read_for_both_sides(tmp_path, eng):
         assert not cats and calls == [2 * k]
     finally:
         repo.close()
+
+
+def test_gc_pause_leaves_collector_state():
+    """the bulk-construction pause re-enables the collector, promotes what it built without a
+    young-generation pass, and leaves objects the host froze itself frozen"""
+    import gc
+
+    assert gc.isenabled()
+    with D._gc_paused():
+        assert not gc.isenabled()
+        built = [[i] for i in range(1000)]
+    assert gc.isenabled() and gc.get_freeze_count() == 0
+    gc.freeze()
+    try:
+        n = gc.get_freeze_count()
+        with D._gc_paused():
+            more = [[i] for i in range(1000)]
+        assert gc.isenabled() and gc.get_freeze_count() == n  # the host's frozen set untouched
+    finally:
+        gc.unfreeze()
+    gc.disable()
+    try:
+        with D._gc_paused():
+            pass
+        assert not gc.isenabled()  # a collector the host had disabled stays disabled
+    finally:
+        gc.enable()
+    assert len(built) == len(more) == 1000
