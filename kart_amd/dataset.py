@@ -274,12 +274,13 @@ class UpdateBatch:
         self.deltas, self.keys, self.n_total = [], [], -1
 
 
-def diff_feature(engine, base, target, feature_filter=None, reverse=False, updates=None):
+def diff_feature(engine, base, target, feature_filter=None, reverse=False, updates=None, _collect=None):
     """Generator of Delta with lazy values (RichBaseDataset.diff_feature semantics).
 
     base / target: DatasetVersion or None (a missing dataset diffs against the empty tree).
     updates: an UpdateBatch that receives the yielded update deltas (set once the generator is
-    exhausted)."""
+    exhausted).  _collect=(keys, deltas): the deltas are appended there with their keys instead of
+    yielded (dataset_diff's bulk path)."""
     present = base if base is not None else target
     if present is None:
         return
@@ -319,6 +320,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
     # this module's own Delta / KeyValue: built field by field (the constructor's argument
     # normalisation is most of a delta's host cost); Kart's classes through their constructor
     own = S.Delta is _deltas.Delta
+    keys_append, deltas_append = (_collect[0].append, _collect[1].append) if _collect is not None else (None, None)
     Delta, KeyValue, new_obj, partial = _deltas.Delta, _deltas.KeyValue, object.__new__, functools.partial
     old_get, new_get = (old_v.get_feature_from_blob if old_v is not None else None,
                         new_v.get_feature_from_blob if new_v is not None else None)
@@ -342,7 +344,11 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
             upd_deltas.append(delta)
             upd_keys.append(opk)
         n_total += 1
-        yield delta
+        if _collect is None:
+            yield delta
+        else:
+            keys_append(opk if ob is not None else npk)
+            deltas_append(delta)
     if updates is not None:
         rows = np.asarray(upd_rows, np.int64)
         updates.old_v, updates.new_v = old_v, new_v
@@ -364,7 +370,15 @@ def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
         ffilter = ds_filter.get("feature", _NoKeys())
     batch = UpdateBatch()
     with _gc_paused():
-        fd = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch))
+        if S.DeltaDiff is _deltas.DeltaDiff:  # this module's own DeltaDiff: one dict update from the lists
+            keys, deltas = [], []
+            for _ in diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch,
+                                  _collect=(keys, deltas)):
+                pass
+            fd = S.DeltaDiff()
+            fd.data.update(zip(keys, deltas))
+        else:
+            fd = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch))
     fd._kd_updates = batch
     out["feature"] = fd
     return out
