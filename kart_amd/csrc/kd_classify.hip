@@ -27,9 +27,21 @@ namespace kd {
 // merge deltas in key order with a decoupled look-back.  The ancestor's keys are read only along
 // the lookups' paths and its OIDs only where a path differs; k_sorted3 checks it is strictly
 // ascending (one streaming pass over its keys).
+#ifndef KD_RS3_PROBE_NOSEARCH
+#define KD_RS3_PROBE_NOSEARCH 0
+#endif
+#ifndef KD_RS3_PROBE_NOOID
+#define KD_RS3_PROBE_NOOID 0
+#endif
+#ifndef KD_RS3_PROBE_NONAMES
+#define KD_RS3_PROBE_NONAMES 0
+#endif
 constexpr int C3_NT = 256;
 constexpr int C3_CH = 1024;  // differing paths per resolve chunk (4 per thread, contiguous)
-constexpr int C3_SAMPLE_BITS = 10;
+#ifndef KD_C3_SAMPLE_BITS
+#define KD_C3_SAMPLE_BITS 10
+#endif
+constexpr int C3_SAMPLE_BITS = KD_C3_SAMPLE_BITS;
 constexpr int C3_SAMPLES = 1 << C3_SAMPLE_BITS;  // ancestor keys sampled per chunk bracket (LDS)
 
 struct Resolve3Args {
@@ -138,7 +150,11 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
         // sub-bracket from an LDS search, then the global search inside it (~log2(span/NS) rounds)
         for (int x = tid; x < NS; x += NT) {
             const u32 pos = blo + (u32)(((u64)x * span) / NS);
+#if KD_RS3_PROBE_NOSEARCH  // timing probe only (results invalid)
+            s_smp[x] = (u64)pos;
+#else
             s_smp[x] = pos < bhi ? g.A[pos] : ~0ull;
+#endif
         }
         __syncthreads();
         u32 lo[PT], hi[PT];
@@ -163,7 +179,11 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
         u32 sub = 0;
 #pragma unroll
         for (int j = 0; j < PT; j++) sub = max(sub, hi[j] - lo[j]);
+#if KD_RS3_PROBE_NOSEARCH
+        const int rounds = 0;
+#else
         const int rounds = sub ? 32 - __clz(sub) : 0;
+#endif
         for (int it = 0; it < rounds; it++) {
             u64 v[PT];
             u32 m[PT];
@@ -192,10 +212,15 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
             const u32* qa = g.oA + (u64)(ia[j] != KD_NONE ? ia[j] : 0) * 5;
             const u32* qo = g.oO + (u64)(io[j] != KD_NONE ? io[j] : 0) * 5;
             const u32* qt = g.oT + (u64)(itt[j] != KD_NONE ? itt[j] : 0) * 5;
+#if KD_RS3_PROBE_NOOID  // timing probe only (results invalid)
+#pragma unroll
+            for (int w = 0; w < 5; w++) { xa[j][w] = (u32)(size_t)qa; xo[j][w] = (u32)(size_t)qo; xt[j][w] = (u32)(size_t)qt; }
+#else
 #pragma unroll
             for (int w = 0; w < 5; w++) { xa[j][w] = qa[w]; xo[j][w] = qo[w]; xt[j][w] = qt[w]; }
+#endif
         }
-        if (g.hash_mode) {  // a matched ancestor path must carry the same filename
+        if (g.hash_mode && !KD_RS3_PROBE_NONAMES) {  // a matched ancestor path must carry the same filename
             u32 act_o = 0, act_t = 0;
 #pragma unroll
             for (int j = 0; j < PT; j++) {
