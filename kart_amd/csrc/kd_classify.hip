@@ -39,7 +39,7 @@ namespace kd {
 constexpr int C3_NT = 256;
 constexpr int C3_CH = 1024;  // differing paths per resolve chunk (4 per thread, contiguous)
 #ifndef KD_C3_SAMPLE_BITS
-#define KD_C3_SAMPLE_BITS 10
+#define KD_C3_SAMPLE_BITS 11  // 2048 samples: C4 k_resolve3 0.745 -> 0.721 ms (8 / 9 bits: no better)
 #endif
 constexpr int C3_SAMPLE_BITS = KD_C3_SAMPLE_BITS;
 constexpr int C3_SAMPLES = 1 << C3_SAMPLE_BITS;  // ancestor keys sampled per chunk bracket (LDS)
