@@ -4,13 +4,15 @@
 Default workload (BASELINE.json configs[2], "C3", the north-star config): ONE synthetic
 100M-MULTIPOLYGON int-PK layer, 10 % edits (4 % geometry + 4 % attribute updates, 1 % deletes, 1 %
 inserts; kart_amd.synth.polygons_layer: the reference's feature blob and path encodings, synthetic
-OIDs).  One *step* = one full pass of the hot path over that layer: merge-path join + OID compare +
-key-ordered compaction of the delta set (k_partition2, k_join2, k_place2), then the msgpack field
-decode + Python-== column compare of every update (k_fielddiff) — all on the device, inputs
-resident in HBM before the timed region.
+OIDs), both sides as the tree walk lists them (git tree order, which is KD_KEY_INT key order: no side
+sort).  One *step* = one full pass of the hot path over that layer: merge-path join + OID compare +
+walk-ordered compaction of the delta set (k_partition2, k_join2, k_place2), the msgpack field decode +
+Python-== column compare of every update (k_fielddiff), then the delta and update records radix-sorted
+into pk order (kd_delta_pk_order: DeltaDiff.sorted_items) — all on the device, inputs resident in HBM
+before the timed region.
 
 --gpus N (one process per GPU, launched by torch.distributed.run): the SAME layer split into N
-bucket ranges (whole 64-pk leaf buckets: synth.shard_pk_range); each rank generates and diffs its
+bucket ranges (whole leaf trees, contiguous runs of the walk: synth.shard_rank_range); each rank generates and diffs its
 range, and every step all-gathers the per-rank counts and the compacted delta records (rebased to
 global indices) over RCCL inside libkartdiff (kd_diff2_gather) — strong scaling.  The harness
 (barrier, max-over-ranks time, the RCCL id broadcast) uses torch.distributed's gloo backend on the
@@ -62,10 +64,13 @@ def parse():
     ap.add_argument("--unordered", action="store_true",
                     help="c2/c3: tile-grouped delta list (per-tile atomic appends, no k_place2); default: key order")
     ap.add_argument("--sort-gather", action="store_true",
-                    help="with-sort steps: permute the OIDs in the sort (k_gather_oid) instead of reading them "
+                    help="fallback steps: permute the OIDs in the sort (k_gather_oid) instead of reading them "
                          "through the order in the join")
     ap.add_argument("--no-sort", action="store_true",
-                    help="c2/c3: skip the with-sort steps (sides from git walk order, both GPU sorts in the step)")
+                    help="c2/c3: skip timing the fallback steps (sides in a non-key order: both GPU side sorts in "
+                         "the step); c4: skip the presorted comparison")
+    ap.add_argument("--no-pk-order", action="store_true",
+                    help="c2/c3: leave the deltas in walk (key) order (no kd_delta_pk_order in the step)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--arena", action="store_true",
                     help="c5: filter from the blob arenas (kd_geom_filter) instead of the geometry heads")
@@ -241,28 +246,22 @@ def run_diff(args, H, polygons):
     split = polygons and world > 1  # C3: one layer split by bucket range (strong scaling)
     t0 = time.time()
     if polygons:
-        n_pks = n + n // 100
-        lo, hi = synth.shard_pk_range(rank, world, n_pks) if split else (0, n_pks)
-        L = synth.polygons_layer(n, lo=lo, hi=hi, same_len=args.same_len if args.workload == "c3v" else 0.0)
+        L = synth.polygons_layer(n, shard=(rank, world) if split else None,
+                                 same_len=args.same_len if args.workload == "c3v" else 0.0)
     else:
         L = synth.points_layer(n, seed=synth.SEED + rank, pk0=shard.rank_pk_base(rank, n))
     gen_s = time.time() - t0
     log(f"[rank {rank}] generated {L.base.n}+{L.target.n} entries in {gen_s:.1f}s "
         f"(+{L.n_insert} ins, {L.n_update} upd, -{L.n_delete} del)")
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
-    walk = None
-    if not args.no_sort:  # the sides as the tree walk hands them to the packer: git path order
-        t0 = time.time()
-        walk = (synth.walk_perm(L.base.key), synth.walk_perm(L.target.key))
-        log(f"[rank {rank}] walk (git tree) order of both sides in {time.time() - t0:.1f}s")
     eng = engine_for(H)
     gather = None
-    if split:  # global sorted index of this shard's first entry on each side
+    if split:  # global walk index of this shard's first entry on each side
         sizes = H.allgather((L.base.n, L.target.n))
         gather = (sum(s[0] for s in sizes[:rank]), sum(s[1] for s in sizes[:rank]))
     t0 = time.perf_counter()
     pipe = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=not args.unordered,
-                        gather=gather, walk=walk, late=not args.sort_gather)
+                        gather=gather, pk_order=not args.no_pk_order)
     h2d_s = time.perf_counter() - t0
     h2d_bytes = 28 * (L.base.n + L.target.n) + int(L.base_blobs[0].size + L.target_blobs[0].size) + \
         8 * int(L.base_blobs[1].size + L.target_blobs[1].size)
@@ -276,12 +275,8 @@ def run_diff(args, H, polygons):
     if not args.no_check:
         assert (counts["inserts"], counts["updates"], counts["deletes"]) == plan, (counts, plan)
         assert not status.any(), "fielddiff status flags set"
-        if walk is not None:  # the GPU sorts rebuilt the key-ordered sides exactly
-            for S, side, perm, order in zip((pipe.A, pipe.B), (L.base, L.target), walk, pipe.orders()):
-                assert np.array_equal(S.key.download(np.uint64, side.n), side.key), "sorted keys differ"
-                assert np.array_equal(S.oid.download(np.uint8, 20 * side.n).reshape(side.n, 20), side.oid), \
-                    "sorted OIDs differ"
-                assert np.array_equal(perm[order], np.arange(side.n)), "sort order differs"
+        if pipe.pk_order:  # the pk-ordered records: a stable argsort of the records' pks
+            check_pk_order(pipe, L, delta, upd)
     if split:
         mx = max(x for x in H.allgather(counts["deltas"]))
         pipe.reserve_gather(mx)
@@ -297,35 +292,25 @@ def run_diff(args, H, polygons):
     eng.prof_reset()
     eng.prof_select(None if args.time_all else ["k_fielddiff" if polygons else "k_join2"])
     eng.prof_enable(not args.no_events)
-    elapsed = timed(H, eng, pipe.diff_step, args.steps)  # presorted device-resident sides
+    elapsed = timed(H, eng, pipe.step, args.steps)  # walk-order device-resident sides: the whole step
     eng.prof_enable(False)
     total_pairs = sum(H.allgather(n_pairs))
     total_deltas = sum(H.allgather(counts["deltas"]))
     kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", "k_fielddiff", "k_rebase"))
+    # every kernel of the step once more with events around each launch (untimed steps): the parts
+    eng.prof_reset()
+    eng.prof_select(None)
+    eng.prof_enable(True)
+    for _ in range(3):
+        pipe.step()
+    eng.sync()
+    eng.prof_enable(False)
+    parts = kernel_times(eng, STEP_KERNELS)
+    pk_sort = pk_sort_summary(pipe, parts, counts) if pipe.pk_order else None
     sort = None
-    if walk is not None:  # the same steps from walk-order sides: both GPU side sorts inside each step
-        elapsed_ws = timed(H, eng, pipe.step, args.steps)
-        eng.prof_reset()
-        eng.prof_select(None)
-        eng.prof_enable(True)
-        for _ in range(3):  # per-kernel times of the sorts (untimed steps, events around every launch)
-            pipe.sort_step()
-        eng.sync()
-        eng.prof_enable(False)
-        sk = kernel_times(eng, SORT_KERNELS)
-        sort = sort_summary(L, sk, elapsed_ws, elapsed, args.steps, total_pairs, H, pipe.late)
-        if pipe.late:  # the join of the with-sort step reads OIDs through the orders: its own time
-            eng.prof_reset()
-            eng.prof_select(["k_join2"])
-            eng.prof_enable(True)
-            for _ in range(3):
-                pipe.step()
-            eng.sync()
-            eng.prof_enable(False)
-            jp = kernel_times(eng, ("k_join2",))
-            if "k_join2" in jp:
-                sort["k_join2_perm_avg_ms"] = round(jp["k_join2"][1], 5)
-
+    if not args.no_sort and not split:  # the fallback: sides in a non-key order, both GPU side sorts in the step
+        del pipe
+        sort = fallback_sort(args, H, eng, L, maps, elapsed, total_pairs)
     # ---- roofline of the dominant kernel (algorithmic bytes per launch) ----
     nA, nB = L.base.n, L.target.n
     ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
@@ -368,40 +353,85 @@ def run_diff(args, H, polygons):
                 "synthetic (seeded points layer: reference blob/path encodings, synthetic OIDs)",
         "config": {"workload": wl, "features": n if polygons else n * world, "pairs_per_step": total_pairs,
                    "deltas_per_step": total_deltas, "updates_per_step": sum(H.allgather(counts["updates"])),
-                   "delta_order": "tile-grouped (same delta set)" if args.unordered else "key",
+                   "delta_order": "tile-grouped (same delta set)" if args.unordered else
+                   ("walk (= key) order, then pk order (kd_delta_pk_order)" if pk_sort else "walk (= key) order"),
+                   "side_order": "git tree (walk) order as listed, no side sort",
                    "parallelism": f"bucket-range shards x{world}" + (", RCCL all-gather of counts + delta records"
                                                                       if split else "")},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
+        "step_kernels_avg_ms": {k: round(v[1], 5) for k, v in parts.items()},
+        "step_kernel_launches": {k: v[0] // 3 for k, v in parts.items()},
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if pk_sort:
+        out["pk_order"] = pk_sort
     if sort:
-        out["value_with_sort"] = sort.pop("value_with_sort")
-        out["ms_per_step_with_sort"] = sort.pop("ms_per_step_with_sort")
-        out["sort"] = sort
+        out["fallback_sort"] = sort
     if host:
         out["host"] = host
     return out
 
 
 SORT_KERNELS = ("k_rs_bits", "k_sort_hist", "k_sort_scan", "k_sort_pass", "k_gather_oid")
+STEP_KERNELS = ("k_partition2", "k_join2", "k_gscan2", "k_place2", "k_fielddiff", "k_dpk_keys", "k_sort_scan",
+                "k_sort_pass")
+RS_RB = 9  # digit bits per radix pass (kd_sort.hip RS_RB): passes = ceil(varying bits / 9)
 
 
-def sort_bytes(keys, gather_oids):
-    """algorithmic HBM bytes of kd_sort_side_into over one side: the varying-bit
-    pass (8 B read per key), the all-pass histogram (8 B), the digit passes (first: 8-B key read,
-    4-B compact key + 4-B index written; middle: 8 B read + 8 B written; last: 8 B read, 8-B key +
-    4-B order written; 64-bit compact keys move 4 B more per key each way), and the OID gather
-    (4-B order + 20-B row read, 20 B written) unless the join reads the OIDs through the order
-    (late materialisation: kd_diff2_device_perm).  Returns (bytes, passes)."""
-    n = int(keys.shape[0])
+def radix_passes(bits):
+    return -(-int(bits) // RS_RB) if bits else 0
+
+
+def check_pk_order(pipe, L, delta, upd):
+    from kart_amd import walkkey
+
+    d_pk, d_perm, u_pk, u_perm = pipe.pk_results()
+    for rec, pk_out, perm_out in ((delta, d_pk, d_perm), (upd, u_pk, u_perm)):
+        keys = np.where(rec[:, 0] != 0xFFFFFFFF, L.base.key[np.minimum(rec[:, 0], L.base.n - 1)],
+                        L.target.key[np.minimum(rec[:, 1], L.target.n - 1)])
+        pks = walkkey.int_keys_to_pks(keys)
+        want = np.argsort(pks, kind="stable")
+        assert np.array_equal(perm_out, want.astype(np.uint32)), "pk order differs from a stable argsort"
+        assert np.array_equal(pk_out, pks[want]), "pk-ordered pks differ"
+
+
+def pk_sort_summary(pipe, parts, counts):
+    """the deltas' and updates' pk sorts (kd_delta_pk_order, two calls per step): algorithmic bytes
+    from the library's own pass count (the pk range's varying bits, 9-bit digits).  Per record: the
+    record read (8 B) + its key gathered (8 B) + the compact key written (4 B); per pass the compact
+    key + index read and written (16 B; the last pass writes the 8-B pk: 20 B)"""
+    lo, hi = pipe.pk_range
+    d = (lo ^ (1 << 63)) ^ (hi ^ (1 << 63)) if hi != lo else 0
+    bits = d.bit_length()
+    npass = max(1, radix_passes(bits))
+    ck = 4 if bits <= 32 else 8
+    per_rec = 8 + 8 + ck + sum((ck if p == 0 else ck + 4) + (12 if p == npass - 1 else ck + 4) for p in range(npass))
+    recs = counts["deltas"] + counts["updates"]
+    ms = sum(parts[k][0] * parts[k][1] for k in ("k_dpk_keys", "k_sort_scan", "k_sort_pass") if k in parts) / 3
+    alg = per_rec * recs
+    return {"what": "deltas and updates radix-sorted by pk on the device (kd_delta_pk_order x2: k_dpk_keys + "
+                    "k_sort_scan + onesweep k_sort_pass per digit), the order DeltaDiff.sorted_items yields",
+            "records_per_step": recs, "varying_bits": bits, "passes_per_sort": npass,
+            "ms_per_step_events": round(ms, 4),
+            "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": int(alg),
+                         "achieved": round(alg / (ms * 1e-3) / 1e9, 1) if ms else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if ms else None}}
+
+
+def sort_bytes(info, n, gather_oids):
+    """algorithmic HBM bytes of kd_sort_side_into over one side, with the pass count the
+    library derives from the same kd_keys_scan (9-bit digits): the all-pass histogram (8 B read per
+    key), the digit passes (first: 8-B key read, compact key + 4-B index written; middle: compact key
+    + index read and written; last: compact key + index read, 8-B key + 4-B order written), and the OID
+    gather (4-B order + 20-B row read, 20 B written) unless the join reads the OIDs through the order
+    (late materialisation).  No varying-bit pass: the host scan sized the sort.  Returns (bytes, passes)."""
     if n < 2:
         return 0, 0
-    vary = int(np.bitwise_or.reduce(keys ^ keys[0]))
-    bits = bin(vary).count("1")  # compact width (gaps absorbed only beyond 4 runs: not for int keys)
-    npass = -(-bits // 8)
+    bits = bin(int(info.vary)).count("1")  # compact width (gaps absorbed only beyond 4 runs: not for int keys)
+    npass = radix_passes(bits)
     ck = 4 if bits <= 32 else 8
-    b = 8 * n + 8 * n  # bits + histogram
+    b = 8 * n  # histogram
     for p in range(npass):
         rd = 8 if p == 0 else ck + 4
         wr = 12 if p == npass - 1 else ck + 4
@@ -411,27 +441,61 @@ def sort_bytes(keys, gather_oids):
     return b, npass
 
 
-def sort_summary(L, sk, elapsed_ws, elapsed, steps, total_pairs, H, late):
-    bb, pb = sort_bytes(L.base.key, not late)
-    bt, pt = sort_bytes(L.target.key, not late)
-    ms_sorts = sum(v[0] * v[1] for v in sk.values()) / 3  # both sides, per step (3 profiled steps)
-    alg = bb + bt
-    return {
-        "value_with_sort": round(total_pairs * steps / elapsed_ws / 1e6, 2),
-        "ms_per_step_with_sort": round(elapsed_ws / steps * 1e3, 4),
-        "what": "each step sorts both sides from git tree (walk) order on the GPU (kd_sort_side_into: onesweep LSD "
-                "radix sort of the compacted varying key bits) then classify2 + field diff; " +
-                ("the join reads the walk-order OIDs through the sort order (kd_diff2_device_perm)" if late else
-                 "the OIDs are gathered into key order by the sort"),
-        "passes": [pb, pt],
-        "kernels_avg_ms": {k: round(v[1], 5) for k, v in sk.items()},
-        "kernel_launches_per_step": {k: v[0] // 3 for k, v in sk.items()},
-        "sort_ms_per_step_events": round(ms_sorts, 4),
-        "sort_ms_per_step_wall": round((elapsed_ws - elapsed) / steps * 1e3, 4),
-        "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": int(alg),
-                     "achieved": round(alg / (ms_sorts * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(alg / (ms_sorts * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-    }
+def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
+    """The fallback the drop-in takes for a side whose walk order is not key order (a leaf tree
+    mixing 2**30 pk wraps): the same step from scrambled sides, both GPU side sorts inside it (passes
+    sized by kd_keys_scan: no read-back), the join reading OIDs through the sort orders."""
+    from kart_amd.device import DiffPipeline
+
+    rng = np.random.default_rng(1)
+    perms = (rng.permutation(L.base.n), rng.permutation(L.target.n))
+    fp = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, unsorted=perms,
+                      late=not args.sort_gather, pk_order=not args.no_pk_order)
+    for _ in range(max(1, args.warmup)):
+        fp.step()
+    eng.sync()
+    if not args.no_check:
+        for S, side, perm, order in zip((fp.A, fp.B), (L.base, L.target), perms, fp.orders()):
+            assert np.array_equal(S.key.download(np.uint64, side.n), side.key), "sorted keys differ"
+            assert np.array_equal(perm[order], np.arange(side.n)), "sort order differs"
+    eng.prof_reset()
+    eng.prof_select(None)
+    eng.prof_enable(False)
+    el = timed(H, eng, fp.step, args.steps)
+    eng.prof_reset()
+    eng.prof_enable(True)
+    for _ in range(3):
+        fp.sort_step()
+    eng.sync()
+    eng.prof_enable(False)
+    sk = kernel_times(eng, SORT_KERNELS)
+    ms_sorts = sum(v[0] * v[1] for v in sk.values()) / 3
+    (bb, pb), (bt, pt) = [sort_bytes(w[3], w[2], not fp.late) for w in fp.walk]
+    eng.prof_reset()
+    eng.prof_select(["k_join2"])
+    eng.prof_enable(True)
+    for _ in range(3):
+        fp.step()
+    eng.sync()
+    eng.prof_enable(False)
+    jp = kernel_times(eng, ("k_join2",))
+    out = {"what": "the drop-in's fallback for sides whose walk order is not key order: each step sorts both "
+                   "(scrambled) sides on the GPU (kd_sort_side_into, onesweep LSD radix sort of the compacted varying "
+                   "key bits, passes sized by the host kd_keys_scan) then classify2 + field diff + pk order; " +
+                   ("the join reads the OIDs through the sort orders (kd_diff2_device_perm)" if fp.late else
+                    "the OIDs are gathered into key order by the sort"),
+           "value": round(total_pairs * args.steps / el / 1e6, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
+           "sort_ms_per_step_wall": round((el - elapsed) / args.steps * 1e3, 4),
+           "passes": [pb, pt], "kernels_avg_ms": {k: round(v[1], 5) for k, v in sk.items()},
+           "kernel_launches_per_step": {k: v[0] // 3 for k, v in sk.items()},
+           "sort_ms_per_step_events": round(ms_sorts, 4),
+           "k_join2_perm_avg_ms": round(jp["k_join2"][1], 5) if "k_join2" in jp else None,
+           "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": int(bb + bt),
+                        "achieved": round((bb + bt) / (ms_sorts * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round((bb + bt) / (ms_sorts * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+    assert out["kernel_launches_per_step"].get("k_sort_pass", 0) == pb + pt, "pass accounting differs from launches"
+    del fp
+    return out
 
 
 def _shard_bounds(L, parts):
@@ -491,9 +555,9 @@ def cpu_baseline_diff(L, maps, seconds, tag):
 
 def host_timing(eng, L, h2d_s, h2d_bytes):
     """What the drop-in path spends outside the timed device step, for the same layer:
-    * pack: the base side's relative leaf paths ('c/c/c/c/<b64(msgpack([pk]))>', as the tree walk
-      yields them) -> join keys (native, multithreaded) -> H2D of keys + OIDs from pinned staging ->
-      GPU radix sort (kd_sort_side) into a device-resident side;
+    * pack: the base side's relative leaf paths ('c/c/c/c/<b64(msgpack([pk]))>', in the order the tree
+      walk yields them) -> join keys (native, multithreaded) -> kd_keys_scan (already ascending: no
+      sort; the pk range for the pk-order passes) -> H2D of keys + OIDs from pinned staging;
     * h2d: uploading both sides + the update blob arenas from pageable numpy arrays (the pipeline
       setup above)."""
     import ctypes
@@ -504,7 +568,7 @@ def host_timing(eng, L, h2d_s, h2d_bytes):
     from kart_amd.device import DevBuf
 
     n = L.base.n
-    pks = (L.base.key >> np.uint64(40)).astype(np.int64) * 64 + (L.base.key & np.uint64(63)).astype(np.int64)
+    pks = packing.int_keys_to_pks(L.base.key)
     chunks = [(a, min(n, a + 4_000_000)) for a in range(0, n, 4_000_000)]
     t0 = time.perf_counter()
     with ThreadPoolExecutor(host_cores()) as ex:
@@ -521,6 +585,10 @@ def host_timing(eng, L, h2d_s, h2d_bytes):
     parse_s = time.perf_counter() - t0
     del arena, off
     assert np.array_equal(keys, L.base.key)
+    t0 = time.perf_counter()
+    info = packing.keys_scan(keys, N.KD_KEY_INT)
+    scan_s = time.perf_counter() - t0
+    assert info.ascending == 1, "the walk-order side is not key-ordered"
     # pinned staging -> HBM
     nbytes = 28 * n
     hp = ctypes.c_void_p()
@@ -529,7 +597,7 @@ def host_timing(eng, L, h2d_s, h2d_bytes):
         pinned = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_uint8)), (nbytes,))
         pinned[:8 * n] = keys.view(np.uint8)
         pinned[8 * n:] = L.base.oid.reshape(-1)
-        dk, do, dord = DevBuf(eng, 8 * n), DevBuf(eng, 20 * n), DevBuf(eng, 4 * n)
+        dk, do = DevBuf(eng, 8 * n), DevBuf(eng, 20 * n)
         eng.sync()
         t0 = time.perf_counter()
         N.check(eng.L.kd_memcpy(eng.ctx, dk.ptr, hp.value, 8 * n, N.KD_COPY_H2D), "kd_memcpy")
@@ -538,20 +606,14 @@ def host_timing(eng, L, h2d_s, h2d_bytes):
         pinned_s = time.perf_counter() - t0
     finally:
         N.lib().kd_host_free(hp)
-    dup = ctypes.c_uint32(0)
-    t0 = time.perf_counter()
-    N.check(eng.L.kd_sort_side(eng.ctx, dk.ptr, do.ptr, dord.ptr, n, ctypes.byref(dup)), "kd_sort_side")
-    eng.sync()
-    sort_s = time.perf_counter() - t0
-    assert not dup.value and np.array_equal(dk.download(np.uint64, n), L.base.key)
-    return {"pack_entries": n, "host_pack_s": round(parse_s, 3), "gpu_sort_s": round(sort_s, 4),
+    return {"pack_entries": n, "host_pack_s": round(parse_s, 3), "keys_scan_s": round(scan_s, 4), "gpu_sort_s": 0.0,
             "pack_h2d_pinned_s": round(pinned_s, 4), "pack_h2d_pinned_GBps": round(nbytes / pinned_s / 1e9, 1),
             "h2d_s": round(h2d_s, 3), "h2d_bytes": h2d_bytes, "h2d_GBps": round(h2d_bytes / h2d_s / 1e9, 1),
-            "note": f"host_pack_s = native parse of {n} relative leaf paths ('c/c/c/c/<b64 msgpack pk>', "
-                    f"generated in {gen_paths_s:.1f}s, not counted) into join keys on {host_cores()} threads; then "
-                    "H2D of keys + OIDs from pinned memory and kd_sort_side (LDS-ranked LSD radix sort + OID "
-                    "permute) leave a device-resident sorted side. h2d_s = the pipeline setup's uploads of both "
-                    "sides + update blobs from pageable memory."}
+            "note": f"host_pack_s = native parse of {n} relative leaf paths ('c/c/c/c/<b64 msgpack pk>', in walk "
+                    f"order, generated in {gen_paths_s:.1f}s, not counted) into join keys on {host_cores()} threads; "
+                    "keys_scan_s = kd_keys_scan (strictly ascending as walked: no sort; vary bits + pk range); then H2D "
+                    "of keys + OIDs from pinned memory leaves a device-resident side. h2d_s = the pipeline setup's "
+                    "uploads of both sides + update blobs from pageable memory."}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -568,13 +630,8 @@ def run_c5(args, H):
     from kart_amd.spatial import GeomCols
 
     n, bits = args.n, 20
-    if H.world > 1:
-        n_pks = n + n // 100
-        lo, hi = synth.shard_pk_range(H.rank, H.world, n_pks)
-    else:
-        lo, hi = 0, None
     t0 = time.time()
-    L = synth.polygons_layer(n, lo=lo, hi=hi, delta_blobs=True)
+    L = synth.polygons_layer(n, shard=(H.rank, H.world) if H.world > 1 else None, delta_blobs=True)
     log(f"[rank {H.rank}] generated {L.base.n}+{L.target.n} entries in {time.time() - t0:.1f}s")
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     cols = GeomCols(ver, ver, "geom", "geom")
@@ -1032,21 +1089,32 @@ def run_c6(args, H):
 
 # ---------------------------------------------------------------------------------------------
 def run_c4(args, H):
+    """C4 (configs[3]): three-way merge classification of a 50M-row string-PK table.  The sides come as
+    the tree walk lists them (git tree order: buckets ascending, each leaf tree's few entries in
+    filename order, not FNV-key order); one step = the three per-bucket sorts
+    (kd_sort_segmented_into) + classify2(ours, theirs) + k_resolve3, OIDs and filenames read through the
+    orders (kd_merge3_device_perm).  Beside it (``presorted``) the same merge over key-sorted sides."""
     from kart_amd import synth
     from kart_amd.device import MergePipeline
 
     n = args.n
     t0 = time.time()
-    M = synth.table3_layers(n, seed=synth.SEED + H.rank)
+    M = synth.table3_layers(n, seed=synth.SEED + H.rank, walk=True)
     A, O_, T = M.ancestor, M.ours, M.theirs
-    log(f"[rank {H.rank}] generated ancestor/ours/theirs {A.n}/{O_.n}/{T.n} string-pk rows in {time.time() - t0:.1f}s "
-        f"({M.n_conflict} conflicts planned)")
+    log(f"[rank {H.rank}] generated ancestor/ours/theirs {A.n}/{O_.n}/{T.n} string-pk rows (walk order) in "
+        f"{time.time() - t0:.1f}s ({M.n_conflict} conflicts planned)")
     eng = engine_for(H)
-    pipe = MergePipeline(eng, A, O_, T)
+    pipe = MergePipeline(eng, A, O_, T, segmented=True)
     for _ in range(max(1, args.warmup)):
         pipe.step()
     eng.sync()
     n_clean, conf, md = pipe.results()
+    srt = []
+    for S, order in zip((A, O_, T), pipe.orders()):
+        if not args.no_check:  # the per-bucket sorts == a full sort of the keys
+            ko = S.key[order]
+            assert np.all(ko[1:] > ko[:-1]), "segmented sort: keys not ascending"
+        srt.append((S.key[order], S.oid[order], order))
     if not args.no_check:  # the generator's own plan (libgit2 rule over planned edits)
         assert conf.shape[0] == M.n_conflict, (conf.shape[0], M.n_conflict)
     eng.prof_reset()
@@ -1056,47 +1124,90 @@ def run_c4(args, H):
     eng.prof_enable(False)
     nall = A.n + O_.n + T.n
     total = sum(H.allgather(nall))
-    kern = kernel_times(eng, ("k_sorted3", "k_partition2", "k_join2", "k_place2", "k_resolve3"))
+    kern = kernel_times(eng, ("k_seg_sort", "k_sorted3", "k_partition2", "k_join2", "k_place2", "k_resolve3"))
+    eng.prof_reset()
+    eng.prof_select(None)
+    eng.prof_enable(True)
+    for _ in range(3):
+        pipe.step()
+    eng.sync()
+    eng.prof_enable(False)
+    parts = kernel_times(eng, ("k_seg_sort", "k_sorted3", "k_partition2", "k_join2", "k_gscan2", "k_place2", "k_resolve3"))
     # classify3 = classify2(ours, theirs) + k_resolve3 over the paths where they differ.
     # Dominant kernel k_join2, algorithmic bytes per launch: every ours/theirs key + OID once (28 B),
     # every ours/theirs filename once (hash keys are verified against the names) and one 8-B record
-    # per differing path
-    _, io, it = np.intersect1d(O_.key, T.key, assume_unique=True, return_indices=True)
-    n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((O_.oid[io] != T.oid[it]).any(axis=1)))
-    alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand
+    # per differing path; with the OIDs in walk order, one 4-B order entry per matched pair
+    (kO, oO, _), (kT, oT, _) = srt[1], srt[2]
+    _, io, it = np.intersect1d(kO, kT, assume_unique=True, return_indices=True)
+    n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((oO[io] != oT[it]).any(axis=1)))
+    alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand + 8 * io.size
     roof = roofline(kern, "k_join2", alg, args.traffic_json, n, "c4" if H.world == 1 else None)
+    seg_alg = 20 * nall  # per entry: the key read, key + 4-B order written (neighbours hit the cache)
+    seg = {"what": "kd_sort_segmented_into x3: each bucket's entries (git filename order) ordered by key",
+           "ms_per_step_events": round(parts["k_seg_sort"][0] * parts["k_seg_sort"][1] / 3, 4) if "k_seg_sort" in parts else None,
+           "algorithmic_bytes_per_step": seg_alg}
+    if seg["ms_per_step_events"]:
+        seg["frac"] = round(seg_alg / (seg["ms_per_step_events"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    presorted = None
+    if not args.no_sort:  # the same merge over key-sorted sides (what the walk would give if it were key order)
+        from kart_amd import packing
+
+        ks = []
+        for S, (k, o, order) in zip((A, O_, T), srt):
+            P = packing.PackedSide(np.ascontiguousarray(k), np.ascontiguousarray(o), S.key_mode, np.arange(S.n),
+                                   encoding=S.encoding)
+            lens = (S.name_off[1:] - S.name_off[:-1])[order]
+            off = np.zeros(S.n + 1, np.uint64)
+            np.cumsum(lens, out=off[1:])
+            w = int(lens[0]) if S.n else 0
+            assert np.all(lens == w)
+            P.name = np.ascontiguousarray(S.name.reshape(S.n, w)[order]).reshape(-1)
+            P.name_off = off
+            ks.append(P)
+        del pipe
+        pp = MergePipeline(eng, *ks)
+        pp.step()
+        eng.sync()
+        c2, conf2, md2 = pp.results()
+        if not args.no_check:
+            assert np.array_equal(conf2, conf) and np.array_equal(md2, md) and c2 == n_clean, "presorted merge differs"
+        el2 = timed(H, eng, pp.step, args.steps)
+        presorted = {"value": round(total * args.steps / el2 / 1e6, 2), "ms_per_step": round(el2 / args.steps * 1e3, 4)}
+        del pp
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         Orc = oracle()
+        (kA, oA, _), (kO, oO, _), (kT, oT, _) = srt
         t0 = time.perf_counter()
         reps = 0
         while True:
-            oc, om, ocl = Orc.classify3(A.key, A.oid, O_.key, O_.oid, T.key, T.oid)
+            oc, om, ocl = Orc.classify3(kA, oA, kO, oO, kT, oT)
             if reps == 0 and not args.no_check:  # the baseline's run doubles as a bit-exact check
-                key = lambda r: sorted(map(tuple, np.asarray(r).tolist()))
-                assert key(conf) == key(oc), "classify3 conflicts differ from the oracle"
-                assert key(md) == key(om), "classify3 merge deltas differ from the oracle"
+                assert np.array_equal(conf, oc.reshape(-1, 3)), "classify3 conflicts differ from the oracle"
+                assert np.array_equal(md, om.reshape(-1, 2)), "classify3 merge deltas differ from the oracle"
                 t0 = time.perf_counter()
             reps += 1
             if time.perf_counter() - t0 >= min(args.cpu_seconds, 10.0):
                 break
         dt = time.perf_counter() - t0
         cpu = {"value": round(nall * reps / dt / 1e6, 3), "unit": "M entries/s", "cores": 1, "kind": "port",
-               "sample": f"the full C4 layer ({nall} entries) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c classify3, "
-                         f"1 thread"}
+               "sample": f"the full C4 layer ({nall} entries, key-sorted) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
+                         f"classify3, 1 thread"}
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M entries/s",
         "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8/u64 (integer)",
-        "data": "synthetic (seeded string-PK table: MsgpackHashPathEncoder paths, synthetic OIDs)",
+        "data": "synthetic (seeded string-PK table: MsgpackHashPathEncoder paths in git tree order, synthetic OIDs)",
         "config": {"workload": f"C4: {n}-row string-PK table per GPU, three-way merge classification "
-                               "(ancestor/ours/theirs join + libgit2 conflict rule)",
+                               "(ancestor/ours/theirs join + libgit2 conflict rule) from walk-order sides",
                    "rows_per_gpu": n, "entries_per_step": total, "conflicts": int(conf.shape[0]),
                    "merge_deltas": int(md.shape[0]), "differing_paths": n_cand,
                    "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
+        "step_kernels_avg_ms": {k: round(v[1], 5) for k, v in parts.items()},
+        "segmented_sort": seg, "presorted": presorted,
         "roofline": roof, "cpu_baseline": cpu,
     }
 

@@ -68,13 +68,16 @@ extern "C" {
 #define KD_MEM_DEVICE 1u
 
 /* key modes (see DESIGN.md "join key") */
-#define KD_KEY_INT 0u  /* IntPathEncoder: key = bucket24 | wrap34 | pk%64, bijective with pk  */
-#define KD_KEY_HASH 1u /* MsgpackHashPathEncoder: key = bucket bits | FNV-1a(filename) bits;
-                          matched keys are verified against the filename bytes            */
+#define KD_KEY_INT 0u  /* IntPathEncoder: key = rank24(bucket) | wrap34 | frank(pk), bijective with
+                          pk and ascending in git's tree order (DESIGN.md "join key")            */
+#define KD_KEY_HASH 1u /* MsgpackHashPathEncoder: key = rank-mapped bucket bits | FNV-1a(filename)
+                          bits; matched keys are verified against the filename bytes           */
 
 typedef struct kd_ctx kd_ctx;
 
-/* One commit's dataset feature tree, flattened: n leaf entries sorted by strictly ascending key. */
+/* One commit's dataset feature tree, flattened: n leaf entries sorted by strictly ascending key.
+ * KD_KEY_INT keys of a tree walk's leaves are ascending as listed (git tree order), unless a leaf
+ * tree mixes pks of different 2^30 wraps; KD_KEY_HASH leaves need kd_sort_segmented_into. */
 typedef struct kd_side {
     uint64_t n;
     const uint64_t* key;      /* [n] join keys, strictly ascending                                 */
@@ -189,6 +192,14 @@ int kd_merge3_device(kd_ctx* ctx, const kd_side* ancestor, const kd_side* ours, 
                      uint32_t flags, uint32_t* d_conflict, uint32_t* d_mdelta, uint64_t* d_counts,
                      uint32_t* d_err);
 
+/* Late-materialised form (after kd_sort_segmented_into / kd_sort_side_into without OIDs): keys
+ * sorted, each side's OIDs and KD_KEY_HASH filename offsets still in walk order, row order[i]
+ * belonging to sorted entry i.  Results identical to kd_merge3_device on the permuted sides. */
+int kd_merge3_device_perm(kd_ctx* ctx, const kd_side* ancestor, const kd_side* ours, const kd_side* theirs,
+                          const uint32_t* ancestor_order, const uint32_t* ours_order, const uint32_t* theirs_order,
+                          uint32_t flags, uint32_t* d_conflict, uint32_t* d_mdelta, uint64_t* d_counts,
+                          uint32_t* d_err);
+
 /* -------- spatial -------- */
 /* Per geometry blob (GPKG; length 0 = null geometry):
  *   match[i]: 0 NON_MATCHING, 1 CANDIDATE (bbox passed; exact GEOS test is the caller's),
@@ -292,14 +303,43 @@ int kd_hex_encode(kd_ctx* ctx, const kd_blobs* blobs, uint32_t mode, uint8_t* he
  * the sorted keys are not strictly ascending (two entries share a key: the caller's fallback).
  * Replaces the host sort of the packer (Dataset3 leaves arrive in git path order, not key order). */
 int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32_t* d_order, uint64_t n, uint32_t* h_dup);
+/* What a sort needs to know about a side's keys (host scan, kd_keys_scan): the bits that vary
+ * (OR of key[i] ^ key[0]) and key[0]; whether the keys are strictly ascending already (a walk-order
+ * KD_KEY_INT side usually is: no sort); for KD_KEY_INT the smallest and largest pk. */
+typedef struct kd_keys_info {
+    uint64_t vary;
+    uint64_t key0;
+    int64_t pk_min, pk_max; /* KD_KEY_INT only */
+    int32_t ascending;
+    int32_t reserved;
+} kd_keys_info;
+int kd_keys_scan(const uint64_t* keys, uint64_t n, uint32_t key_mode, kd_keys_info* out);
 /* Out-of-place form (what a device pipeline runs): d_key_in / d_oid_in hold the side in walk order
  * and are left unchanged; d_key_out [n] <- the keys ascending, d_oid_out [n*20] <- the OIDs in that
- * order (both oid pointers NULL to skip), d_order [n] <- input index of sorted entry k.  d_dup
- * (device, may be NULL: a following kd_diff2_device checks strict order anyway) <- 1 when two
- * entries share a key.  Outputs must not alias inputs.  Asynchronous on the context stream except
- * for one 16-byte read-back (which key bits vary: it sizes the passes). */
+ * order (both oid pointers NULL to skip: kd_diff2_device_perm then reads them through the order),
+ * d_order [n] <- input index of sorted entry k.  d_dup (device, may be NULL: a following
+ * kd_diff2_device checks strict order anyway) <- 1 when two entries share a key.  Outputs must not
+ * alias inputs.  info (host, from kd_keys_scan) sizes the passes; with NULL one 16-byte read-back
+ * finds the varying bits.  Otherwise asynchronous on the context stream.  This is the fallback of a
+ * side whose walk order is not key order (a leaf tree mixing pk wraps). */
 int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oid_in, uint64_t* d_key_out,
-                      uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup);
+                      uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup, const kd_keys_info* info);
+/* A KD_KEY_HASH side in walk order (its keys ascend in the top seg_bits bucket bits; inside a leaf
+ * tree the leaves are in filename order, not FNV order): each bucket's entries ordered by key.
+ * d_key_out [n] <- keys ascending, d_order [n] <- walk index of sorted entry k (the OIDs and
+ * filenames stay in walk order: kd_diff2_device_perm / kd_merge3_device_perm read through it).
+ * *d_err |= 1 on a duplicate key or descending bucket bits, 4 on a bucket of more than 512 entries
+ * (then sort with kd_sort_side_into).  One kernel, no host sync. */
+int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uint64_t* d_key_out, uint32_t* d_order,
+                           uint64_t n, int seg_bits, uint32_t* d_err);
+/* The deltas in pk order (DeltaDiff.sorted_items, kart/diff_structs.py:442-458; classify2 emits them in
+ * git walk order): for KD_KEY_INT device sides and a device delta list d_delta [cap] of (base | KD_NONE,
+ * target | KD_NONE) records (classify2's deltas or updates) with *d_n of them, d_pk [cap] <- their pks
+ * ascending, d_perm [cap] <- the record index of pk rank k.  pk_lo / pk_hi bound every pk of both sides
+ * (kd_keys_scan's pk_min / pk_max): they size the radix passes, no read-back.  Stable, asynchronous. */
+int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* d_delta,
+                      uint64_t cap, const uint64_t* d_n, int64_t pk_lo, int64_t pk_hi, int64_t* d_pk,
+                      uint32_t* d_perm);
 
 /* -------- device memory and copies (no GPU framework needed by the caller) -------- */
 #define KD_COPY_H2D 1u
@@ -365,7 +405,8 @@ int64_t kd_pack_int_keys(const uint8_t* names, const uint64_t* name_off, uint64_
 /* KD_KEY_HASH: "c1/../cL/<filename>" relative paths -> keys (levels, hex=0 base64 / 1 hex). */
 int64_t kd_pack_hash_keys(const uint8_t* paths, const uint64_t* path_off, uint64_t n, int levels,
                           int hex, uint64_t* keys, uint8_t* status);
-/* Inverse of the KD_KEY_INT key: pk = ((wrap - 2^33) * 2^24 + bucket) * 64 + r. */
+/* Inverse of the KD_KEY_INT key: pk = ((wrap - 2^33) * 2^24 + bucket) * 64 + low6, bucket and low6
+ * through the inverse rank maps. */
 int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks);
 
 /* -------- git object database + leaf walk (host, no GPU) -------- */

@@ -115,6 +115,17 @@ class KdGeomCols(ctypes.Structure):
     ]
 
 
+class KdKeysInfo(ctypes.Structure):
+    _fields_ = [
+        ("vary", ctypes.c_uint64),
+        ("key0", ctypes.c_uint64),
+        ("pk_min", ctypes.c_int64),
+        ("pk_max", ctypes.c_int64),
+        ("ascending", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
 class KdDiffResult(ctypes.Structure):
     _fields_ = [
         ("n_insert", ctypes.c_uint64),
@@ -172,6 +183,12 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
     ),
+    "kd_merge3_device_perm": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.POINTER(KdSide), ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p],
+    ),
     "kd_envelopes": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.POINTER(KdBlobs), c_dblp, ctypes.c_int, ctypes.c_void_p,
@@ -215,7 +232,14 @@ SIGNATURES = {
                                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p]),
     "kd_sort_side_into": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.POINTER(KdKeysInfo)]),
+    "kd_keys_scan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(KdKeysInfo)]),
+    "kd_sort_segmented_into": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
+    "kd_delta_pk_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
+                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "kd_malloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "kd_mfree": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "kd_host_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),

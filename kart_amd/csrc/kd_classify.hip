@@ -53,6 +53,7 @@ struct Resolve3Args {
     int hash_mode;
     const uint2* cand;      // classify2(ours, theirs) delta list: (ours | NONE, theirs | NONE)
     const u64* c2;          // its counts: inserts, updates, deletes, deltas
+    const u32 *pA, *pO, *pT;  // PERM: row of sorted entry i in the side's OID / filename arrays
     u64* desc;              // look-back descriptors [2][nchunk]
     u64 nchunk;
     u32* aux;               // [0] chunk ticket, [1] ancestor-order error (k_sorted3)
@@ -105,7 +106,7 @@ __device__ __forceinline__ u64 half_lower_bound(const u64* __restrict__ X, u64 n
     return lo;
 }
 
-template <int NT>
+template <int NT, bool PERM>
 __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
     constexpr int PT = C3_CH / NT;
     constexpr int NS = C3_SAMPLES;
@@ -203,15 +204,28 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
         }
         // every OID of the chunk's paths loaded before any compare
         u32 ia[PT], io[PT], itt[PT];
+        u32 ra[PT], ro[PT], rt[PT];  // their rows in the OID / filename arrays
         u32 xa[PT][5], xo[PT][5], xt[PT][5];
 #pragma unroll
         for (int j = 0; j < PT; j++) {
             ia[j] = found[j] ? lo[j] : KD_NONE;
             io[j] = rec[j].x;
             itt[j] = rec[j].y;
-            const u32* qa = g.oA + (u64)(ia[j] != KD_NONE ? ia[j] : 0) * 5;
-            const u32* qo = g.oO + (u64)(io[j] != KD_NONE ? io[j] : 0) * 5;
-            const u32* qt = g.oT + (u64)(itt[j] != KD_NONE ? itt[j] : 0) * 5;
+            ra[j] = ia[j]; ro[j] = io[j]; rt[j] = itt[j];
+        }
+        if (PERM) {  // late materialisation: the sides' OIDs and names stay in walk order
+#pragma unroll
+            for (int j = 0; j < PT; j++) {
+                ra[j] = ia[j] != KD_NONE ? g.pA[ia[j]] : KD_NONE;
+                ro[j] = io[j] != KD_NONE ? g.pO[io[j]] : KD_NONE;
+                rt[j] = itt[j] != KD_NONE ? g.pT[itt[j]] : KD_NONE;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const u32* qa = g.oA + (u64)(ra[j] != KD_NONE ? ra[j] : 0) * 5;
+            const u32* qo = g.oO + (u64)(ro[j] != KD_NONE ? ro[j] : 0) * 5;
+            const u32* qt = g.oT + (u64)(rt[j] != KD_NONE ? rt[j] : 0) * 5;
 #if KD_RS3_PROBE_NOOID  // timing probe only (results invalid)
 #pragma unroll
             for (int w = 0; w < 5; w++) { xa[j][w] = (u32)(size_t)qa; xo[j][w] = (u32)(size_t)qo; xt[j][w] = (u32)(size_t)qt; }
@@ -229,8 +243,8 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
                 // ancestor's (checked here): only ancestor-and-theirs-without-ours needs its own check
                 act_t |= (u32)(ia[j] != KD_NONE && itt[j] != KD_NONE && io[j] == KD_NONE) << j;
             }
-            if (names_ne_batch<PT, 8>(g.nmA, g.noA, ia, g.nmO, g.noO, io, act_o) |
-                names_ne_batch<PT, 8>(g.nmA, g.noA, ia, g.nmT, g.noT, itt, act_t))
+            if (names_ne_batch<PT, 8>(g.nmA, g.noA, ra, g.nmO, g.noO, ro, act_o) |
+                names_ne_batch<PT, 8>(g.nmA, g.noA, ra, g.nmT, g.noT, rt, act_t))
                 atomicOr(g.err, 2u);
         }
         u32 fc = 0, fm = 0, clean = 0;
@@ -322,7 +336,9 @@ int kd::check_side(const kd_side* s, const char* which) {
 // merge deltas -> d_md, counts[4] <- clean, conflicts, mdeltas, 0; *derr <- error bits.  Nothing
 // needs zeroing by the caller.
 static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
-                         u64* counts, u32* derr) {
+                         u64* counts, u32* derr, const u32* pA = nullptr, const u32* pO = nullptr,
+                         const u32* pT = nullptr) {
+    const bool perm = pA || pO || pT;
     int rc;
     const u64 nA = A.n, nO = O.n, nT = T.n;
     const u64 nchunk = (nO + nT) / C3_CH + 2;
@@ -343,12 +359,17 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     });
     if (rc) return rc;
     // ours vs theirs: key-ordered differing paths (+ filename checks, order check, error bits)
-    if ((rc = diff2_device(ctx, &O, &T, 0, (u32*)cand, nullptr, (u64*)c2, derr))) return rc;
-    if (ctx->occ_resolve3 <= 0) {
+    if ((rc = diff2_device(ctx, &O, &T, 0, (u32*)cand, nullptr, (u64*)c2, derr, perm ? pO : nullptr,
+                           perm ? pT : nullptr)))
+        return rc;
+    static int occ_r3[2] = {0, 0};  // resident k_resolve3 workgroups per CU, per instantiation
+    if (occ_r3[perm] <= 0) {
         int nb = 0;
-        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_resolve3<C3_NT>, C3_NT, 0));
-        ctx->occ_resolve3 = nb > 0 ? nb : 1;
+        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, perm ? (const void*)k_resolve3<C3_NT, true> : (const void*)k_resolve3<C3_NT, false>, C3_NT, 0));
+        occ_r3[perm] = nb > 0 ? nb : 1;
     }
+    ctx->occ_resolve3 = occ_r3[perm];
     // an empty side (or an absent filename arena) points at device zeros: lanes without an entry
     // load from index 0 of every array instead of branching, so each array must be readable
     auto ptr = [&](const void* p, u64 n) { return n && p ? p : (const void*)dz; };
@@ -360,13 +381,15 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     g.noA = (const u64*)ptr(A.name_off, nA); g.noO = (const u64*)ptr(O.name_off, nO); g.noT = (const u64*)ptr(T.name_off, nT);
     g.hash_mode = A.key_mode == KD_KEY_HASH;
     g.cand = (const uint2*)cand; g.c2 = (const u64*)c2;
+    g.pA = (const u32*)ptr(pA, nA); g.pO = (const u32*)ptr(pO, nO); g.pT = (const u32*)ptr(pT, nT);
     g.desc = (u64*)desc; g.nchunk = nchunk; g.aux = (u32*)aux;
     g.out_conf = d_conf; g.out_md = d_md; g.counts = counts; g.err = derr;
     // persistent: at most every resident workgroup, at most one per chunk (+1 so someone adds the
     // clean count when there are no differing paths)
     const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)ctx->occ_resolve3);
     return launch(ctx, "k_resolve3", [&] {
-        hipLaunchKernelGGL((k_resolve3<C3_NT>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
+        if (perm) hipLaunchKernelGGL((k_resolve3<C3_NT, true>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
+        else hipLaunchKernelGGL((k_resolve3<C3_NT, false>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
     });
 }
 
@@ -513,6 +536,28 @@ int kd_merge3_device(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const
              "kd_merge3_device: side too large");
     KD_HIP(hipSetDevice(ctx->device));
     return merge3_device(ctx, *anc, *ours, *theirs, d_conflict, (uint2*)d_mdelta, d_counts, d_err);
+}
+
+int kd_merge3_device_perm(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_side* theirs,
+                          const uint32_t* anc_order, const uint32_t* ours_order, const uint32_t* theirs_order,
+                          uint32_t flags, uint32_t* d_conflict, uint32_t* d_mdelta, uint64_t* d_counts, uint32_t* d_err) {
+    (void)flags;
+    KD_CHECK(ctx && d_conflict && d_mdelta && d_counts && d_err, "kd_merge3_device_perm: NULL");
+    int rc;
+    if ((rc = check_side(anc, "ancestor")) || (rc = check_side(ours, "ours")) || (rc = check_side(theirs, "theirs"))) return rc;
+    KD_CHECK(anc->mem == KD_MEM_DEVICE && ours->mem == KD_MEM_DEVICE && theirs->mem == KD_MEM_DEVICE,
+             "kd_merge3_device_perm: sides must be device memory");
+    KD_CHECK(anc->key_mode == ours->key_mode && ours->key_mode == theirs->key_mode, "kd_merge3_device_perm: key modes differ");
+    KD_CHECK(anc->n < 0xFFFFFFFFull && ours->n < 0xFFFFFFFFull && theirs->n < 0xFFFFFFFFull,
+             "kd_merge3_device_perm: side too large");
+    KD_CHECK((anc->n == 0 || anc_order) && (ours->n == 0 || ours_order) && (theirs->n == 0 || theirs_order),
+             "kd_merge3_device_perm: NULL order");
+    KD_HIP(hipSetDevice(ctx->device));
+    void* dz;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    auto ord = [&](const uint32_t* p) { return p ? p : (const u32*)dz; };
+    return merge3_device(ctx, *anc, *ours, *theirs, d_conflict, (uint2*)d_mdelta, d_counts, d_err, ord(anc_order),
+                         ord(ours_order), ord(theirs_order));
 }
 
 }  // extern "C"

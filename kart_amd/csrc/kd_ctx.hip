@@ -5,6 +5,7 @@
 #include <thread>
 
 #include "kd_internal.h"
+#include "kd_walkkey.h"
 
 namespace kd {
 
@@ -108,16 +109,10 @@ static inline int b64v(u8 c) {
     return -1;
 }
 
-// pk (sign, magnitude) -> int key; 0 ok, 2 out of range
+// pk (sign, magnitude) -> KD_KEY_INT walk key (kd_walkkey.h); 0 ok, 2 outside [-2^63, 2^63)
 static inline int int_key(bool neg, u64 mag, u64* key) {
-    __int128 pk = neg ? -(__int128)mag : (__int128)mag;
-    // floor division by powers of two == arithmetic shift on two's complement
-    __int128 q = pk >> 6;                       // pk // 64
-    u64 r = (u64)(pk - q * 64);                 // pk % 64 in [0, 64)
-    u64 bucket = (u64)(q & ((1 << 24) - 1));    // (pk // 64) % 2^24
-    __int128 k = (pk >> 30) + ((__int128)1 << 33);
-    if (k < 0 || k >= ((__int128)1 << 34)) return 2;
-    *key = (bucket << 40) | ((u64)k << 6) | r;
+    if (neg ? mag > (1ull << 63) : mag >= (1ull << 63)) return 2;
+    *key = wk::int_key(neg ? (i64)(0 - mag) : (i64)mag);
     return 0;
 }
 
@@ -322,7 +317,8 @@ int64_t kd_pack_hash_keys(const uint8_t* paths, const uint64_t* path_off, uint64
                 } else {
                     v = b64v(ch);
                     if (v < 0) { st = 1; break; }
-                    bucket = (bucket << 6) | (u64)v; bits += 6;
+                    // the digit's ASCII rank: bucket order = git's tree order (kd_walkkey.h)
+                    bucket = (bucket << 6) | (u64)wk::T.rank[v]; bits += 6;
                 }
             }
             if (!st && (pos >= len || s[pos] != '/')) st = 1;
@@ -341,17 +337,55 @@ int64_t kd_pack_hash_keys(const uint8_t* paths, const uint64_t* path_off, uint64
     return (int64_t)bad;
 }
 
+int kd_keys_scan(const uint64_t* keys, uint64_t n, uint32_t key_mode, kd_keys_info* out) {
+    KD_CHECK(out && (n == 0 || keys), "kd_keys_scan: NULL");
+    KD_CHECK(key_mode == KD_KEY_INT || key_mode == KD_KEY_HASH, "kd_keys_scan: bad key_mode");
+    *out = kd_keys_info{};
+    out->ascending = 1;
+    if (n == 0) return KD_OK;
+    const u64 k0 = keys[0];
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt == 0 ? 1 : nt > 32 ? 32 : nt;
+    if (n < 65536) nt = 1;
+    struct Part { u64 vary = 0; i64 lo = INT64_MAX, hi = INT64_MIN; bool asc = true; };
+    std::vector<Part> part(nt);
+    std::vector<std::thread> th;
+    const u64 chunk = (n + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; t++) {
+        const u64 a = t * chunk, b = std::min<u64>(n, a + chunk);
+        if (a >= b) break;
+        th.emplace_back([&, t, a, b] {
+            Part p;
+            for (u64 i = a; i < b; i++) {
+                const u64 k = keys[i];
+                p.vary |= k ^ k0;
+                if (i > 0) p.asc &= keys[i - 1] < k;
+                if (key_mode == KD_KEY_INT) {
+                    const i64 pk = wk::int_key_pk(k);
+                    p.lo = pk < p.lo ? pk : p.lo;
+                    p.hi = pk > p.hi ? pk : p.hi;
+                }
+            }
+            part[t] = p;
+        });
+    }
+    for (auto& t : th) t.join();
+    i64 lo = INT64_MAX, hi = INT64_MIN;
+    for (auto& p : part) {
+        out->vary |= p.vary;
+        out->ascending &= p.asc ? 1 : 0;
+        lo = p.lo < lo ? p.lo : lo;
+        hi = p.hi > hi ? p.hi : hi;
+    }
+    out->key0 = k0;
+    out->pk_min = key_mode == KD_KEY_INT ? lo : 0;
+    out->pk_max = key_mode == KD_KEY_INT ? hi : 0;
+    return KD_OK;
+}
+
 int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks) {
     KD_CHECK(keys && pks, "kd_int_keys_to_pks: NULL");
-    par_for(n, [&](u64 i) {
-        u64 key = keys[i];
-        i64 bucket = (i64)(key >> 40);
-        i64 k = (i64)((key >> 6) & ((1ull << 34) - 1)) - ((i64)1 << 33);
-        i64 r = (i64)(key & 63);
-        // ((k * 2^24 + bucket) * 64 + r), computed in unsigned arithmetic (wraps exactly to int64)
-        u64 v = (((u64)k << 24) + (u64)bucket) * 64u + (u64)r;
-        pks[i] = (i64)v;
-    });
+    par_for(n, [&](u64 i) { pks[i] = wk::int_key_pk(keys[i]); });
     return KD_OK;
 }
 

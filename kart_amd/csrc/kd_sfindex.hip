@@ -166,7 +166,7 @@ int kd_sf_index_build(kd_ctx* ctx, const uint8_t* oid, const uint8_t* env, uint6
         });
         if (rc) return fail(rc);
         // equal 64-bit prefixes of different OIDs are legal here (the lookup compares all 20 bytes)
-        if ((rc = kd_sort_side_into(ctx, (const u64*)kin, nullptr, ix->key, nullptr, ix->order, n, nullptr)))
+        if ((rc = kd_sort_side_into(ctx, (const u64*)kin, nullptr, ix->key, nullptr, ix->order, n, nullptr, nullptr)))
             return fail(rc);
         rc = launch(ctx, "k_sf_buckets", [&] {
             hipLaunchKernelGGL(k_sf_buckets, dim3(grid_for(ctx, n)), dim3(256), 0, ctx->stream, (const u64*)ix->key, n,

@@ -28,6 +28,7 @@
 // 4. k_gather_oid  OIDs permuted by the order (sorted k reads row order[k]; git-order leaves of one
 //                  64-entry leaf tree stay within ~1.3 KB, so the reads are near-coalesced).
 #include "kd_internal.h"
+#include "kd_walkkey.h"
 
 namespace kd {
 
@@ -55,6 +56,7 @@ struct SortPlan {
     u64 mask[RS_MAXRUNS];       // run r: (key >> lo[r]) & mask[r] -> compact bits at pos[r]
     u32 lo[RS_MAXRUNS], pos[RS_MAXRUNS];
     u32 nruns, bits;            // runs, compact key width
+    u64 out_xor;                // the last pass stores rs_expand(key) ^ out_xor (signed pks: the sign bit)
 };
 
 template <typename CK>
@@ -114,10 +116,11 @@ __global__ __launch_bounds__(256) void k_rs_bits(const u64* __restrict__ key, u6
 
 // ---- all passes' digit histograms in one read of the keys ----
 template <typename CK>
-__global__ __launch_bounds__(RS_HIST_NT) void k_sort_hist(const u64* __restrict__ key, u64 n, int npass, int width,
-                                                           SortPlan plan, u32* __restrict__ hist) {
+__global__ __launch_bounds__(RS_HIST_NT) void k_sort_hist(const u64* __restrict__ key, u64 ncap, const u64* __restrict__ dn,
+                                                           int npass, int width, SortPlan plan, u32* __restrict__ hist) {
     __shared__ u32 s_h[8 * RS_RD];
     const int tid = threadIdx.x;
+    const u64 n = dn ? min(*dn, ncap) : ncap;
     for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT) s_h[i] = 0;
     __syncthreads();
     const u32 dmask = (1u << width) - 1;
@@ -197,15 +200,19 @@ __device__ __forceinline__ u64 rs_load(const u64* p) {
     return __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One digit pass.  FIRST: input = the caller's 64-bit keys (compacted on load), value = the input
-// index.  LAST: output = full 64-bit keys (expanded) + the values (original indices).
-template <typename CK, int NT, int IPT, bool FIRST, bool LAST>
+// One digit pass.  FIRST: value = the input index; IN64: the input keys are the caller's 64-bit
+// keys (compacted on load), else compact keys already.  LAST: output = full 64-bit keys (expanded,
+// ^ plan.out_xor) + the values.  The grid is persistent: workgroups take tiles in order from an
+// atomic counter until the count (*dn when the caller's count lives on the device) is covered.
+template <typename CK, int NT, int IPT, bool FIRST, bool LAST, bool IN64>
 __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, const u32* __restrict__ vin,
-                                                  void* __restrict__ kout, u32* __restrict__ vout, u64 n, int shift,
-                                                  u32 dmask, const u32* __restrict__ gbase, u64* __restrict__ status, u32 epoch,
+                                                  void* __restrict__ kout, u32* __restrict__ vout, u64 ncap,
+                                                  const u64* __restrict__ dn, int shift, u32 dmask,
+                                                  const u32* __restrict__ gbase, u64* __restrict__ status, u32 epoch,
                                                   u32* __restrict__ tile_ctr, SortPlan plan) {
     constexpr int NW = NT / 64, TILE = NT * IPT, CPT = RS_RD * NW / NT;
     static_assert(NT >= RS_RD && (RS_RD * NW) % NT == 0, "tile shape");
+    static_assert(TILE <= 65535, "s_cnt holds tile-local starts in 16 bits");
     __shared__ u16 s_cnt[RS_RD * NW];  // [digit][wave]: item counts, then (after the scan) starts (<= TILE)
     __shared__ u32 s_hist[RS_RD];      // the tile's digit counts (early: published before the ranking)
     __shared__ CK s_key[TILE];
@@ -214,11 +221,15 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
     __shared__ u32 s_wsum[NW];
     __shared__ u32 s_tile;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u64 n = dn ? min(*dn, ncap) : ncap;
+    const u64 ntiles = (n + TILE - 1) / TILE;
+    while (true) {
     if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
     for (int i = tid; i < RS_RD * NW; i += NT) s_cnt[i] = 0;
     for (int i = tid; i < RS_RD; i += NT) s_hist[i] = 0;
     __syncthreads();
     const u32 tile = s_tile;
+    if ((u64)tile >= ntiles) break;
     const u64 t0 = (u64)tile * TILE;
     const u32 valid = (u32)min<u64>((u64)TILE, n - t0);
     const u64 wbase = t0 + (u64)wv * 64 * IPT + lane;
@@ -229,13 +240,10 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
     for (int i = 0; i < IPT; i++) {
         const u64 idx = wbase + (u64)i * 64;
         const bool ok = idx < n;
-        if (FIRST) {
-            c[i] = ok ? rs_compact<CK>(((const u64*)kin)[idx], plan) : (CK)0;
-            v[i] = (u32)idx;
-        } else {
-            c[i] = ok ? ((const CK*)kin)[idx] : (CK)0;
-            v[i] = ok ? vin[idx] : 0;
-        }
+        if (IN64) c[i] = ok ? rs_compact<CK>(((const u64*)kin)[idx], plan) : (CK)0;
+        else c[i] = ok ? ((const CK*)kin)[idx] : (CK)0;
+        if (FIRST) v[i] = (u32)idx;
+        else v[i] = ok ? vin[idx] : 0;
     }
     // ---- b. early counts: the tile's digit histogram, published before the ranking so that later
     //         tiles' look-backs find this tile's aggregate as early as possible ----
@@ -311,6 +319,7 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
             // RS_LBW earlier tiles' words per round trip (t-1, t-2, ...): their counts add up to the
             // first inclusive prefix; a word not yet published stops the round, and the next round
             // starts at it.  Tile 0 always publishes an inclusive prefix, so the walk ends there.
+            // (Every earlier tile's ticket belongs to a running workgroup: the wait always ends.)
             i64 t = (i64)tile - 1;
             while (true) {
                 u64 w[RS_LBW];
@@ -342,9 +351,11 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
         const CK k = s_key[j];
         const u32 x = s_val[j];
         const u32 dst = s_goff[(u32)(k >> shift) & dmask] + j;
-        if (LAST) ((u64*)kout)[dst] = rs_expand((u64)k, plan);
+        if (LAST) ((u64*)kout)[dst] = rs_expand((u64)k, plan) ^ plan.out_xor;
         else ((CK*)kout)[dst] = k;
         vout[dst] = x;
+    }
+    __syncthreads();  // the next tile reuses the LDS arrays
     }
 }
 
@@ -388,6 +399,74 @@ __global__ __launch_bounds__(256) void k_check_sorted(const u64* __restrict__ ke
     bool bad = false;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x + 1; i < n; i += (u64)gridDim.x * 256) bad |= key[i - 1] >= key[i];
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(dup, 1u);
+}
+
+// ---- deltas into pk order (DeltaDiff.sorted_items) ----
+// pk of each delta record (base key's, or the target key's for an insert), as a sortable unsigned
+// key (sign bit flipped), compacted by the plan; all passes' digit histograms.  n = *dn.
+template <typename CK>
+__global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict__ rec, u64 ncap, const u64* __restrict__ dn,
+                                                          const u64* __restrict__ kA, const u64* __restrict__ kB,
+                                                          int npass, int width, SortPlan plan, CK* __restrict__ out,
+                                                          u32* __restrict__ hist) {
+    __shared__ u32 s_h[8 * RS_RD];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT) s_h[i] = 0;
+    __syncthreads();
+    const u64 n = min(*dn, ncap);
+    const u32 dmask = (1u << width) - 1;
+    for (u64 r = (u64)blockIdx.x * RS_HIST_NT + tid; r < n; r += (u64)gridDim.x * RS_HIST_NT) {
+        const uint2 d = rec[r];
+        const u64 key = d.x != KD_NONE ? kA[d.x] : kB[d.y];
+        const u64 sk = (u64)wk::int_key_pk(key) ^ (1ull << 63);
+        const CK c = rs_compact<CK>(sk, plan);
+        out[r] = c;
+        for (int p = 0; p < npass; p++) atomicAdd(&s_h[p * RS_RD + ((u32)(c >> (p * width)) & dmask)], 1u);
+    }
+    __syncthreads();
+    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+// ---- segmented sort: keys ascending in their top bits (a hash side in walk order: the bucket)
+// ordered by the whole key inside each run of equal top bits.  One thread per entry: its rank among
+// its segment's keys (the segment scanned from global memory; segments average a few entries) is its
+// place.  err |= 1: a duplicate key or descending top bits; 4: a segment longer than RS_SEG_MAX (the
+// caller sorts with kd_sort_side_into instead).
+constexpr int RS_SEG_MAX = 512;
+__global__ __launch_bounds__(256) void k_seg_sort(const u64* __restrict__ key, u64 n, int shift, u64* __restrict__ kout,
+                                                  u32* __restrict__ order, u32* __restrict__ err) {
+    u32 bad = 0;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
+        const u64 k = key[i], seg = k >> shift;
+        u32 rank = 0, left = 0;
+        u64 j = i;
+        while (j > 0 && left < RS_SEG_MAX) {  // earlier entries of the segment
+            const u64 x = key[j - 1];
+            if ((x >> shift) != seg) {
+                bad |= (x >> shift) > seg ? 1u : 0u;
+                break;
+            }
+            rank += x < k;
+            bad |= x == k ? 1u : 0u;
+            left++;
+            j--;
+        }
+        if (left == RS_SEG_MAX) bad |= 4u;
+        u32 right = 0;
+        for (u64 q = i + 1; q < n && right < RS_SEG_MAX; q++, right++) {  // later entries
+            const u64 x = key[q];
+            if ((x >> shift) != seg) break;
+            rank += x < k;
+        }
+        if (right == RS_SEG_MAX) bad |= 4u;
+        const u64 dst = i - left + rank;
+        if (dst < n) {
+            kout[dst] = k;
+            order[dst] = (u32)i;
+        }
+    }
+    if (__ballot(bad != 0) && bad) atomicOr(err, bad);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -452,12 +531,31 @@ static int rs_epoch(kd_ctx* ctx, u64 status_bytes, SortState& S, u32* ep) {
     return KD_OK;
 }
 
-template <typename CK, bool FIRST, bool LAST>
-static int rs_launch_pass(kd_ctx* ctx, SortState& S, const void* kin, const u32* vin, void* kout, u32* vout, u64 n,
-                          int pass, int shift, int width, const SortPlan& plan) {
+// resident k_sort_pass workgroups per CU (persistent grid when the count lives on the device)
+template <typename CK, bool FIRST, bool LAST, bool IN64>
+static int rs_occupancy() {
+    constexpr int IPT = sizeof(CK) == 4 ? KD_RS_IPT32 : KD_RS_IPT64;
+    static int occ = 0;
+    if (!occ) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_sort_pass<CK, RS_NT, IPT, FIRST, LAST, IN64>,
+                                                         RS_NT, 0) != hipSuccess || nb <= 0)
+            nb = 1;
+        occ = nb;
+    }
+    return occ;
+}
+
+template <typename CK, bool FIRST, bool LAST, bool IN64>
+static int rs_launch_pass(kd_ctx* ctx, SortState& S, const void* kin, const u32* vin, void* kout, u32* vout, u64 ncap,
+                          const u64* dn, int pass, int shift, int width, const SortPlan& plan) {
     constexpr int IPT = sizeof(CK) == 4 ? KD_RS_IPT32 : KD_RS_IPT64;
     constexpr u64 TILE = (u64)RS_NT * IPT;
-    const u64 ntiles = (n + TILE - 1) / TILE;
+    const u64 ntiles = (ncap + TILE - 1) / TILE;
+    // host count: one workgroup per tile; device count: at most the resident workgroups, each
+    // taking tiles until the count is covered
+    const u64 grid = dn ? std::min<u64>(ntiles, (u64)ctx->n_cu * rs_occupancy<CK, FIRST, LAST, IN64>()) : ntiles;
+    if (grid == 0) return KD_OK;
     u32 ep;
     int rc = rs_epoch(ctx, ntiles * RS_RD * 8, S, &ep);
     if (rc) return rc;
@@ -465,76 +563,47 @@ static int rs_launch_pass(kd_ctx* ctx, SortState& S, const void* kin, const u32*
     u32* tc = S.tctr + pass;
     u64* status = S.status;
     return launch(ctx, "k_sort_pass", [&] {
-        hipLaunchKernelGGL((k_sort_pass<CK, RS_NT, IPT, FIRST, LAST>), dim3((unsigned)ntiles), dim3(RS_NT), 0,
-                           ctx->stream, kin, vin, kout, vout, n, shift,
-                           (u32)((1u << width) - 1), gb, status, ep, tc, plan);
+        hipLaunchKernelGGL((k_sort_pass<CK, RS_NT, IPT, FIRST, LAST, IN64>), dim3((unsigned)grid), dim3(RS_NT), 0,
+                           ctx->stream, kin, vin, kout, vout, ncap, dn, shift, (u32)((1u << width) - 1), gb, status, ep, tc,
+                           plan);
     });
 }
 
+// the digit passes: key_in = the caller's 64-bit keys (in64) or compact keys (the first pass's values
+// are then the input indices either way); the last pass writes 64-bit keys and the values
 template <typename CK>
-static int rs_passes(kd_ctx* ctx, SortState& S, const u64* key_in, u64* key_out, u32* order, u64 n, int npass,
-                     int width, const SortPlan& plan) {
+static int rs_passes(kd_ctx* ctx, SortState& S, const void* key_in, bool in64, u64* key_out, u32* order, u64 ncap,
+                     const u64* dn, int npass, int width, const SortPlan& plan) {
     int rc;
     void *kb[2], *vb[2];
     if (npass > 1) {
-        if ((rc = ensure(ctx, "rs.k0", n * sizeof(CK), &kb[0]))) return rc;
-        if ((rc = ensure(ctx, "rs.v0", n * 4, &vb[0]))) return rc;
+        if ((rc = ensure(ctx, "rs.k0", ncap * sizeof(CK), &kb[0]))) return rc;
+        if ((rc = ensure(ctx, "rs.v0", ncap * 4, &vb[0]))) return rc;
     }
     if (npass > 2) {
-        if ((rc = ensure(ctx, "rs.k1", n * sizeof(CK), &kb[1]))) return rc;
-        if ((rc = ensure(ctx, "rs.v1", n * 4, &vb[1]))) return rc;
+        if ((rc = ensure(ctx, "rs.k1", ncap * sizeof(CK), &kb[1]))) return rc;
+        if ((rc = ensure(ctx, "rs.v1", ncap * 4, &vb[1]))) return rc;
     }
     for (int p = 0; p < npass; p++) {
         const bool first = p == 0, last = p == npass - 1;
-        const void* kin = first ? (const void*)key_in : kb[(p - 1) & 1];
+        const void* kin = first ? key_in : kb[(p - 1) & 1];
         const u32* vin = first ? nullptr : (const u32*)vb[(p - 1) & 1];
         void* kout = last ? (void*)key_out : kb[p & 1];
         u32* vout = last ? order : (u32*)vb[p & 1];
         const int sh = p * width;
-        if (first && last) rc = rs_launch_pass<CK, true, true>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
-        else if (first) rc = rs_launch_pass<CK, true, false>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
-        else if (last) rc = rs_launch_pass<CK, false, true>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
-        else rc = rs_launch_pass<CK, false, false>(ctx, S, kin, vin, kout, vout, n, p, sh, width, plan);
+#define KD_RSP(F, L, I) rs_launch_pass<CK, F, L, I>(ctx, S, kin, vin, kout, vout, ncap, dn, p, sh, width, plan)
+        if (first && in64) rc = last ? KD_RSP(true, true, true) : KD_RSP(true, false, true);
+        else if (first) rc = last ? KD_RSP(true, true, false) : KD_RSP(true, false, false);
+        else rc = last ? KD_RSP(false, true, false) : KD_RSP(false, false, false);
+#undef KD_RSP
         if (rc) return rc;
     }
     return KD_OK;
 }
 
-// keys: key_in -> key_out (sorted), order[k] = input index of sorted entry k.  key_out may alias
-// key_in only when the sort takes two passes or more (the caller checks *passes_out first).
-static int sort_keys(kd_ctx* ctx, const u64* key_in, u64* key_out, u32* order, u64 n, bool inplace) {
-    int rc;
-    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 8));
-    void* bits;
-    if ((rc = ensure(ctx, "rs.bits", 16, &bits))) return rc;
-    // ---- which bits vary (one 8-byte read-back decides the passes) ----
-    KD_HIP(hipMemsetAsync(bits, 0, 16, ctx->stream));
-    rc = launch(ctx, "k_rs_bits", [&] {
-        hipLaunchKernelGGL(k_rs_bits, dim3(gs), dim3(256), 0, ctx->stream, key_in, n, (u64*)bits);
-    });
-    if (rc) return rc;
-    u64 hv[2] = {0, 0};
-    KD_HIP(hipMemcpyAsync(hv, bits, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KD_HIP(hipMemcpyAsync(hv + 1, key_in, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KD_HIP(hipStreamSynchronize(ctx->stream));
-    const u64 vary = hv[0];
-    if (vary == 0) {  // every key equal (n == 1, or duplicates): identity order
-        if (key_out != key_in) KD_HIP(hipMemcpyAsync(key_out, key_in, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        return launch(ctx, "k_iota", [&] {
-            hipLaunchKernelGGL(k_iota_u32, dim3(gs), dim3(256), 0, ctx->stream, order, n);
-        });
-    }
-    const SortPlan plan = make_plan(vary, hv[1]);
-    const int npass = (int)((plan.bits + RS_RB - 1) / RS_RB);
-    const int width = (int)((plan.bits + npass - 1) / npass);  // spread the bits evenly over the passes
-    if (inplace && npass == 1) {  // the single pass would read and write the caller's array
-        void* tmp;
-        if ((rc = ensure(ctx, "rs.kin", n * 8, &tmp))) return rc;
-        KD_HIP(hipMemcpyAsync(tmp, key_in, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        key_in = (const u64*)tmp;
-    }
-    SortState S;
+static int rs_state(kd_ctx* ctx, int npass, SortState& S) {
     void *tc, *hist, *gb;
+    int rc;
     if ((rc = ensure(ctx, "rs.tctr", 64, &tc))) return rc;
     if ((rc = ensure(ctx, "rs.hist", 8 * RS_RD * 4, &hist))) return rc;
     if ((rc = ensure(ctx, "rs.gbase", 8 * RS_RD * 4, &gb))) return rc;
@@ -543,24 +612,74 @@ static int sort_keys(kd_ctx* ctx, const u64* key_in, u64* key_out, u32* order, u
     S.gbase = (u32*)gb;
     KD_HIP(hipMemsetAsync(tc, 0, 64, ctx->stream));
     KD_HIP(hipMemsetAsync(hist, 0, (size_t)npass * RS_RD * 4, ctx->stream));
+    return KD_OK;
+}
+
+static void plan_passes(const SortPlan& plan, int* npass, int* width) {
+    *npass = (int)((plan.bits + RS_RB - 1) / RS_RB);
+    *width = *npass ? (int)((plan.bits + *npass - 1) / *npass) : 0;  // the bits spread evenly over the passes
+}
+
+// keys: key_in -> key_out (sorted), order[k] = input index of sorted entry k.  info (host, may be
+// NULL): which key bits vary (kd_keys_scan); without it one 16-byte read-back finds them.
+static int sort_keys(kd_ctx* ctx, const u64* key_in, u64* key_out, u32* order, u64 n, bool inplace,
+                     const kd_keys_info* info) {
+    int rc;
+    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 8));
+    u64 vary, k0;
+    if (info) {
+        vary = info->vary;
+        k0 = info->key0;
+    } else {
+        void* bits;
+        if ((rc = ensure(ctx, "rs.bits", 16, &bits))) return rc;
+        KD_HIP(hipMemsetAsync(bits, 0, 16, ctx->stream));
+        rc = launch(ctx, "k_rs_bits", [&] {
+            hipLaunchKernelGGL(k_rs_bits, dim3(gs), dim3(256), 0, ctx->stream, key_in, n, (u64*)bits);
+        });
+        if (rc) return rc;
+        u64 hv[2] = {0, 0};
+        KD_HIP(hipMemcpyAsync(hv, bits, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KD_HIP(hipMemcpyAsync(hv + 1, key_in, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KD_HIP(hipStreamSynchronize(ctx->stream));
+        vary = hv[0];
+        k0 = hv[1];
+    }
+    if (vary == 0) {  // every key equal (n == 1, or duplicates): identity order
+        if (key_out != key_in) KD_HIP(hipMemcpyAsync(key_out, key_in, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        return launch(ctx, "k_iota", [&] {
+            hipLaunchKernelGGL(k_iota_u32, dim3(gs), dim3(256), 0, ctx->stream, order, n);
+        });
+    }
+    const SortPlan plan = make_plan(vary, k0);
+    int npass, width;
+    plan_passes(plan, &npass, &width);
+    if (inplace && npass == 1) {  // the single pass would read and write the caller's array
+        void* tmp;
+        if ((rc = ensure(ctx, "rs.kin", n * 8, &tmp))) return rc;
+        KD_HIP(hipMemcpyAsync(tmp, key_in, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        key_in = (const u64*)tmp;
+    }
+    SortState S;
+    if ((rc = rs_state(ctx, npass, S))) return rc;
     const bool narrow = plan.bits <= 32;
     constexpr u64 HCH = (u64)RS_HIST_NT * RS_HIST_IPT;
     const unsigned hg = (unsigned)std::max<u64>(1, std::min<u64>((n + HCH - 1) / HCH, (u64)ctx->n_cu * 2));
     rc = launch(ctx, "k_sort_hist", [&] {
         if (narrow)
-            hipLaunchKernelGGL(k_sort_hist<u32>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, key_in, n, npass, width, plan,
-                               (u32*)hist);
+            hipLaunchKernelGGL(k_sort_hist<u32>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, key_in, n, (const u64*)nullptr,
+                               npass, width, plan, S.hist);
         else
-            hipLaunchKernelGGL(k_sort_hist<u64>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, key_in, n, npass, width, plan,
-                               (u32*)hist);
+            hipLaunchKernelGGL(k_sort_hist<u64>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, key_in, n, (const u64*)nullptr,
+                               npass, width, plan, S.hist);
     });
     if (rc) return rc;
     rc = launch(ctx, "k_sort_scan", [&] {
-        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(RS_RD), 0, ctx->stream, (const u32*)hist, npass, (u32*)gb);
+        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(RS_RD), 0, ctx->stream, (const u32*)S.hist, npass, S.gbase);
     });
     if (rc) return rc;
-    return narrow ? rs_passes<u32>(ctx, S, key_in, key_out, order, n, npass, width, plan)
-                  : rs_passes<u64>(ctx, S, key_in, key_out, order, n, npass, width, plan);
+    return narrow ? rs_passes<u32>(ctx, S, key_in, true, key_out, order, n, nullptr, npass, width, plan)
+                  : rs_passes<u64>(ctx, S, key_in, true, key_out, order, n, nullptr, npass, width, plan);
 }
 
 static int gather_and_check(kd_ctx* ctx, const u8* oid_in, u8* oid_out, const u32* order, const u64* key_sorted, u64 n,
@@ -583,12 +702,24 @@ static int gather_and_check(kd_ctx* ctx, const u8* oid_in, u8* oid_out, const u3
     return KD_OK;
 }
 
+// the plan of a pk sort: every pk lies in [lo, hi], so the sortable keys share the bits above the
+// highest bit in which lo and hi differ
+static SortPlan pk_plan(i64 lo, i64 hi) {
+    const u64 a = (u64)lo ^ (1ull << 63), b = (u64)hi ^ (1ull << 63);
+    const u64 d = a ^ b;
+    const u64 vary = d ? (d >> 63 ? ~0ull : ((1ull << (64 - __builtin_clzll(d))) - 1)) : 0;
+    SortPlan p = make_plan(vary, a);
+    p.out_xor = 1ull << 63;
+    return p;
+}
+
 }  // namespace kd
 
 using namespace kd;
 
 extern "C" int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oid_in, uint64_t* d_key_out,
-                                 uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup) {
+                                 uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup,
+                                 const kd_keys_info* info) {
     KD_CHECK(ctx && (n == 0 || (d_key_in && d_key_out && d_order)), "kd_sort_side_into: NULL");
     KD_CHECK(!d_oid_in == !d_oid_out, "kd_sort_side_into: OID input and output go together");
     KD_CHECK(n < 0xFFFFFFFFull, "kd_sort_side_into: side too large for uint32 indices");
@@ -600,7 +731,7 @@ extern "C" int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const ui
         if (d_dup) KD_HIP(hipMemsetAsync(d_dup, 0, 4, ctx->stream));
         return KD_OK;
     }
-    int rc = sort_keys(ctx, d_key_in, d_key_out, d_order, n, false);
+    int rc = sort_keys(ctx, d_key_in, d_key_out, d_order, n, false, info);
     if (rc) return rc;
     return gather_and_check(ctx, d_oid_in, d_oid_out, d_order, d_key_out, n, d_dup);
 }
@@ -612,7 +743,7 @@ extern "C" int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32
     KD_HIP(hipSetDevice(ctx->device));
     if (h_dup) *h_dup = 0;
     if (n == 0) return KD_OK;
-    int rc = sort_keys(ctx, d_key, d_key, d_order, n, true);
+    int rc = sort_keys(ctx, d_key, d_key, d_order, n, true, nullptr);
     if (rc) return rc;
     void *o2 = nullptr, *dup = nullptr;
     if (d_oid && (rc = ensure(ctx, "rs.oid", n * 20, &o2))) return rc;
@@ -624,4 +755,65 @@ extern "C" int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32
         KD_HIP(hipStreamSynchronize(ctx->stream));
     }
     return KD_OK;
+}
+
+extern "C" int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uint64_t* d_key_out, uint32_t* d_order,
+                                      uint64_t n, int seg_bits, uint32_t* d_err) {
+    KD_CHECK(ctx && d_err && (n == 0 || (d_key_in && d_key_out && d_order)), "kd_sort_segmented_into: NULL");
+    KD_CHECK(n < 0xFFFFFFFFull, "kd_sort_segmented_into: side too large for uint32 indices");
+    KD_CHECK(seg_bits > 0 && seg_bits < 64, "kd_sort_segmented_into: seg_bits %d", seg_bits);
+    KD_CHECK(n == 0 || (const void*)d_key_in != (const void*)d_key_out, "kd_sort_segmented_into: output aliases input");
+    KD_HIP(hipSetDevice(ctx->device));
+    if (n == 0) return KD_OK;
+    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 16));
+    return launch(ctx, "k_seg_sort", [&] {
+        hipLaunchKernelGGL(k_seg_sort, dim3(gs), dim3(256), 0, ctx->stream, d_key_in, n, 64 - seg_bits, d_key_out,
+                           d_order, d_err);
+    });
+}
+
+extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* d_delta,
+                                 uint64_t cap, const uint64_t* d_n, int64_t pk_lo, int64_t pk_hi, int64_t* d_pk,
+                                 uint32_t* d_perm) {
+    KD_CHECK(ctx && base && target && d_n && d_pk && d_perm && (cap == 0 || d_delta), "kd_delta_pk_order: NULL");
+    KD_CHECK(base->key_mode == KD_KEY_INT && target->key_mode == KD_KEY_INT, "kd_delta_pk_order: KD_KEY_INT sides only");
+    KD_CHECK(base->mem == KD_MEM_DEVICE && target->mem == KD_MEM_DEVICE, "kd_delta_pk_order: sides must be device memory");
+    KD_CHECK(pk_lo <= pk_hi, "kd_delta_pk_order: pk_lo > pk_hi");
+    KD_CHECK(cap < 0xFFFFFFFFull, "kd_delta_pk_order: too many deltas for uint32 indices");
+    KD_HIP(hipSetDevice(ctx->device));
+    if (cap == 0) return KD_OK;
+    int rc;
+    void* dz;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    const u64* kA = base->n ? base->key : (const u64*)dz;
+    const u64* kB = target->n ? target->key : (const u64*)dz;
+    SortPlan plan = pk_plan(pk_lo, pk_hi);
+    int npass, width;
+    plan_passes(plan, &npass, &width);
+    if (npass == 0) {  // a single pk value: at most one delta, in place already
+        plan.nruns = 1; plan.mask[0] = 1; plan.lo[0] = 0; plan.pos[0] = 0; plan.bits = 1;
+        plan.kconst = ((u64)pk_lo ^ (1ull << 63)) & ~1ull;
+        npass = width = 1;
+    }
+    const bool narrow = plan.bits <= 32;
+    void* ck;
+    if ((rc = ensure(ctx, "dpk.keys", cap * (narrow ? 4 : 8), &ck))) return rc;
+    SortState S;
+    if ((rc = rs_state(ctx, npass, S))) return rc;
+    const unsigned hg = (unsigned)std::max<u64>(1, std::min<u64>((cap + RS_HIST_NT - 1) / RS_HIST_NT, (u64)ctx->n_cu * 4));
+    rc = launch(ctx, "k_dpk_keys", [&] {
+        if (narrow)
+            hipLaunchKernelGGL(k_dpk_keys<u32>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n,
+                               kA, kB, npass, width, plan, (u32*)ck, S.hist);
+        else
+            hipLaunchKernelGGL(k_dpk_keys<u64>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n,
+                               kA, kB, npass, width, plan, (u64*)ck, S.hist);
+    });
+    if (rc) return rc;
+    rc = launch(ctx, "k_sort_scan", [&] {
+        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(RS_RD), 0, ctx->stream, (const u32*)S.hist, npass, S.gbase);
+    });
+    if (rc) return rc;
+    return narrow ? rs_passes<u32>(ctx, S, ck, false, (u64*)d_pk, d_perm, cap, d_n, npass, width, plan)
+                  : rs_passes<u64>(ctx, S, ck, false, (u64*)d_pk, d_perm, cap, d_n, npass, width, plan);
 }

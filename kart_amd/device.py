@@ -95,13 +95,21 @@ class DevSide:
 
 
 class _WalkSide:
-    """a side's arrays in walk order (what DevSide uploads)"""
+    """a side's arrays in another order (what DevSide uploads): keys, OIDs and (KD_KEY_HASH) the
+    filename arena with rows in that order"""
 
-    def __init__(self, key, oid):
-        self.key, self.oid = np.ascontiguousarray(key), np.ascontiguousarray(oid)
-        self.n = int(key.shape[0])
-        self.key_mode = N.KD_KEY_INT
-        self.name = None
+    def __init__(self, side, perm):
+        self.key, self.oid = np.ascontiguousarray(side.key[perm]), np.ascontiguousarray(side.oid[perm])
+        self.n = int(side.n)
+        self.key_mode = side.key_mode
+        self.name = self.name_off = None
+        if side.name is not None:
+            lens = (side.name_off[1:] - side.name_off[:-1])[perm]
+            off = np.zeros(self.n + 1, np.uint64)
+            np.cumsum(lens, out=off[1:])
+            src = side.name_off[:-1][perm].astype(np.int64)
+            idx = np.arange(int(off[-1]), dtype=np.int64) + np.repeat(src - off[:-1].astype(np.int64), lens.astype(np.int64))
+            self.name, self.name_off = np.ascontiguousarray(side.name[idx]), off
 
 
 class DevBlobs:
@@ -127,7 +135,19 @@ class DevBlobs:
 
 
 class DiffPipeline:
-    """classify2 + fielddiff over device-resident sides (one GPU), back to back on one stream.
+    """classify2 + fielddiff (+ the deltas in pk order) over device-resident sides (one GPU), back to
+    back on one stream.
+
+    The sides are as the tree walk lists them: for int pks that is ascending key order already
+    (kart_amd/walkkey.py), so a step is the join on the walk-order arrays, the field diff of its
+    updates and (``pk_order``) the radix sort of the delta and update records into pk order
+    (kd_delta_pk_order: DeltaDiff.sorted_items) — no side sort.
+
+    ``unsorted=(base_perm, target_perm)``: the fallback for a side whose walk order is not key order
+    (a leaf tree mixing pk wraps, or a hash-key side): the sides are held with rows ``side.key[perm]``
+    and every step first sorts their keys on the GPU (kd_sort_side_into, passes sized by
+    kd_keys_scan, no read-back); the join reads the OIDs (and filenames) through the sort orders
+    (kd_diff2_device_perm), or — ``late=False`` — the sort gathers the OIDs into key order.
 
     ``gather=(base_off, target_off)``: this GPU holds one bucket-range shard of a larger diff (its
     entries start at those global sorted indices); each step then runs kd_diff2_gather — the shard's
@@ -135,29 +155,27 @@ class DiffPipeline:
     the library's RCCL communicator (``engine.comm_init`` first) — and field-diffs the shard's own
     updates."""
 
-    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, ordered=True, gather=None, walk=None,
-                 late=True):
+    def __init__(self, engine, base, target, base_blobs, target_blobs, maps, ordered=True, gather=None, unsorted=None,
+                 late=True, pk_order=True):
+        from . import packing
+
         self.eng = engine
         self.flags = 0 if ordered else N.KD_DIFF_UNORDERED
         self.A = DevSide(engine, base)
         self.B = DevSide(engine, target)
-        # walk = (base_perm, target_perm): the sides are also held in walk (git tree) order —
-        # side.key[perm] — and every step first sorts them into the sorted side buffers above
-        # (kd_sort_side_into), as the drop-in does after packing the leaves it walked
-        # late (walk mode, single GPU): sort the keys only and let the join read the walk-order OIDs
-        # through the sort order (kd_diff2_device_perm) instead of permuting them (kd_sort_side_into's
-        # OID gather)
         self.walk = None
         self.late = bool(late) and gather is None
-        if walk is not None:
+        if unsorted is not None:
             self.walk = []
-            for side, perm in zip((base, target), walk):
-                w = _WalkSide(side.key[perm], side.oid[perm])
-                self.walk.append((DevSide(engine, w), DevBuf(engine, 4 * max(side.n, 1)), side.n))
+            for side, perm in zip((base, target), unsorted):
+                w = _WalkSide(side, perm)
+                info = packing.keys_scan(w.key, side.key_mode)
+                self.walk.append((DevSide(engine, w), DevBuf(engine, 4 * max(side.n, 1)), side.n, info))
         self.OB = DevBlobs(engine, *base_blobs)
         self.NB = DevBlobs(engine, *target_blobs)
         self.maps = maps
         cap = base.n + target.n + 1
+        self.cap = cap
         self.cap_upd = min(base.n, target.n)  # updates <= matched keys
         self.delta = DevBuf(engine, 8 * cap)
         self.upd = DevBuf(engine, 8 * cap)
@@ -169,6 +187,20 @@ class DiffPipeline:
         self._ob, self._nb = self.OB.kd_blobs(), self.NB.kd_blobs()
         self._km = maps.kd_maps()
         self._perm_sides = None
+        # pk order of the deltas and updates (KD_KEY_INT): the passes sized by the pk range
+        self.pk_order = bool(pk_order) and base.key_mode == N.KD_KEY_INT and gather is None
+        if self.pk_order:
+            lo, hi = [], []
+            for side in (base, target):
+                info = side.info if side.info is not None else packing.keys_scan(side.key, side.key_mode)
+                if side.n:
+                    lo.append(int(info.pk_min))
+                    hi.append(int(info.pk_max))
+            self.pk_range = (min(lo), max(hi)) if lo else (0, 0)
+            self.d_pk = DevBuf(engine, 8 * cap)
+            self.d_perm = DevBuf(engine, 4 * cap)
+            self.u_pk = DevBuf(engine, 8 * max(self.cap_upd, 1))
+            self.u_perm = DevBuf(engine, 4 * max(self.cap_upd, 1))
         self.gather = gather
         if gather is not None:
             self.world = engine.nranks
@@ -186,38 +218,40 @@ class DiffPipeline:
         self.all_delta = DevBuf(self.eng, 8 * self.all_cap)
 
     def sort_step(self):
-        """the two GPU side sorts (walk order -> the sorted side buffers), walk mode only"""
+        """(fallback) the two GPU side sorts into the sorted side buffers"""
         L, ctx = self.eng.L, self.eng.ctx
-        for (w, order, n), S in zip(self.walk, (self.A, self.B)):
+        for (w, order, n, info), S in zip(self.walk, (self.A, self.B)):
             if self.late:
-                N.check(L.kd_sort_side_into(ctx, w.key.ptr, None, S.key.ptr, None, order.ptr, n, None),
-                        "kd_sort_side_into")
+                N.check(L.kd_sort_side_into(ctx, w.key.ptr, None, S.key.ptr, None, order.ptr, n, None,
+                                            ctypes.byref(info)), "kd_sort_side_into")
             else:
-                N.check(L.kd_sort_side_into(ctx, w.key.ptr, w.oid.ptr, S.key.ptr, S.oid.ptr, order.ptr, n, None),
-                        "kd_sort_side_into")
+                N.check(L.kd_sort_side_into(ctx, w.key.ptr, w.oid.ptr, S.key.ptr, S.oid.ptr, order.ptr, n, None,
+                                            ctypes.byref(info)), "kd_sort_side_into")
 
     def orders(self):
-        """(walk mode) host copies of the two sort orders: walk index of sorted entry k"""
-        return [order.download(np.uint32, n) for _, order, n in self.walk]
+        """(fallback) host copies of the two sort orders: walk index of sorted entry k"""
+        return [order.download(np.uint32, n) for _, order, n, _ in self.walk]
 
     def step(self):
-        """one pass of the hot path: (walk mode) both side sorts, then the diff + field diff"""
+        """one pass of the hot path: (fallback) both side sorts, then the diff + field diff (+ pk order)"""
         if self.walk is not None:
             self.sort_step()
         self._diff(self.walk is not None and self.late)
 
     def diff_step(self):
-        """classify2 + fielddiff over the presorted side buffers (keys and OIDs in key order)"""
+        """classify2 + fielddiff (+ pk order) over the key-ordered side buffers"""
         self._diff(False)
 
     def _diff(self, perm):
         L, ctx = self.eng.L, self.eng.ctx
-        if perm:  # sorted keys, walk-order OIDs read through the sort orders
+        if perm:  # sorted keys; OIDs and filenames read through the sort orders from the walk-order rows
             if self._perm_sides is None:
                 self._perm_sides = []
-                for S, (w, _, _) in zip((self.A, self.B), self.walk):
+                for S, (w, _, _, _) in zip((self.A, self.B), self.walk):
                     k = S.kd_side()
                     k.oid = w.oid.ptr
+                    if w.name is not None:
+                        k.name, k.name_off = w.name.ptr, w.name_off.ptr
                     self._perm_sides.append(k)
             N.check(L.kd_diff2_device_perm(ctx, ctypes.byref(self._perm_sides[0]), ctypes.byref(self._perm_sides[1]),
                                            self.walk[0][1].ptr, self.walk[1][1].ptr, self.flags, self.delta.ptr,
@@ -234,6 +268,13 @@ class DiffPipeline:
         N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.ptr, self.cap_upd,
                                ctypes.cast(self.counts.ptr + 8, N.c_u64p), N.KD_MEM_DEVICE,
                                ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE), "kd_fielddiff")
+        if self.pk_order and self.flags == 0:
+            lo, hi = self.pk_range
+            N.check(L.kd_delta_pk_order(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.delta.ptr, self.cap,
+                                        self.counts.ptr + 24, lo, hi, self.d_pk.ptr, self.d_perm.ptr), "kd_delta_pk_order")
+            N.check(L.kd_delta_pk_order(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.upd.ptr,
+                                        max(self.cap_upd, 1), self.counts.ptr + 8, lo, hi, self.u_pk.ptr,
+                                        self.u_perm.ptr), "kd_delta_pk_order")
         if self.gather is not None:
             N.check(L.kd_diff2_gather_end(ctx, self.delta.ptr, self.all_delta.ptr, self.all_cap,
                                           self.h_counts.ctypes.data), "kd_diff2_gather_end")
@@ -249,6 +290,14 @@ class DiffPipeline:
         masks = self.masks.download(np.uint64, nu * self.maps.words).reshape(nu, self.maps.words)
         status = self.status.download(np.uint8, nu)
         return {"inserts": int(c[0]), "updates": nu, "deletes": int(c[2]), "deltas": nd}, delta, upd, masks, status
+
+    def pk_results(self):
+        """(pk_order) host copies: (pks of the deltas ascending, delta index of each), and the same for
+        the updates (update index: the row of masks / status)"""
+        c = self.counts.download(np.uint64, 8)
+        nd, nu = int(c[3]), int(c[1])
+        return (self.d_pk.download(np.int64, nd), self.d_perm.download(np.uint32, nd),
+                self.u_pk.download(np.int64, nu), self.u_perm.download(np.uint32, nu))
 
     def gathered(self):
         """(gather mode, after a step + sync) the whole diff: global delta records in key order and
@@ -360,31 +409,64 @@ class FilterPipeline:
 
 
 class MergePipeline:
-    """classify3 (three-way merge classification) over device-resident sides (one GPU)."""
+    """classify3 (three-way merge classification) over device-resident sides (one GPU).
 
-    def __init__(self, engine, ancestor, ours, theirs):
+    ``segmented``: KD_KEY_HASH sides in git tree order (what the walk lists: keys ascending in the
+    bucket bits, each leaf tree's few entries in filename order).  Every step first orders each bucket
+    (kd_sort_segmented_into, one kernel per side) and the merge reads OIDs and filenames through the
+    orders from the walk-order rows (kd_merge3_device_perm)."""
+
+    def __init__(self, engine, ancestor, ours, theirs, segmented=False):
+        from . import shard
+
         self.eng = engine
         self.S = [DevSide(engine, x) for x in (ancestor, ours, theirs)]
         self._s = [x.kd_side() for x in self.S]
+        self.segmented = bool(segmented)
+        if self.segmented:
+            self.seg_bits = shard.bucket_bits(ancestor.key_mode, ancestor.encoding)
+            self.skey = [DevBuf(engine, 8 * max(x.n, 1)) for x in (ancestor, ours, theirs)]
+            self.order = [DevBuf(engine, 4 * max(x.n, 1)) for x in (ancestor, ours, theirs)]
+            for k, sb in zip(self._s, self.skey):
+                k.key = sb.ptr
         na, no, nt = ancestor.n, ours.n, theirs.n
         self.conf = DevBuf(engine, 12 * (na + no + nt + 1))
         self.md = DevBuf(engine, 8 * (no + nt + 1))
-        self.counts = DevBuf(engine, 64)  # [0..3] counts, [4] error word
+        self.counts = DevBuf(engine, 64)  # [0..3] counts, [4] error word, [5] the segmented sorts' error word
         self.counts.zero()
         engine.sync()
 
+    def sort_step(self):
+        """(segmented) each side's buckets ordered by key"""
+        L, ctx = self.eng.L, self.eng.ctx
+        for S, sk, od in zip(self.S, self.skey, self.order):
+            N.check(L.kd_sort_segmented_into(ctx, S.key.ptr, sk.ptr, od.ptr, S.n, self.seg_bits, self.counts.ptr + 40),
+                    "kd_sort_segmented_into")
+
     def step(self):
         L, ctx = self.eng.L, self.eng.ctx
+        if self.segmented:
+            self.sort_step()
+            N.check(L.kd_merge3_device_perm(ctx, ctypes.byref(self._s[0]), ctypes.byref(self._s[1]),
+                                            ctypes.byref(self._s[2]), self.order[0].ptr, self.order[1].ptr,
+                                            self.order[2].ptr, 0, self.conf.ptr, self.md.ptr, self.counts.ptr,
+                                            self.counts.ptr + 32), "kd_merge3_device_perm")
+            return
         N.check(L.kd_merge3_device(ctx, ctypes.byref(self._s[0]), ctypes.byref(self._s[1]), ctypes.byref(self._s[2]), 0,
                                    self.conf.ptr, self.md.ptr, self.counts.ptr, self.counts.ptr + 32),
                 "kd_merge3_device")
 
     def results(self):
-        """host copies (synchronous): n_clean, conflicts [n,3], merge deltas [m,2]"""
+        """host copies (synchronous): n_clean, conflicts [n,3], merge deltas [m,2] (indices of the
+        key-ordered sides)"""
         c = self.counts.download(np.uint64, 8)
-        if c[4]:
-            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flag {int(c[4])}")
+        if c[4] or c[5]:
+            raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flags {int(c[4])}, {int(c[5])}")
         nc, nm = int(c[1]), int(c[2])
         conf = self.conf.download(np.uint32, 3 * nc).reshape(nc, 3)
         md = self.md.download(np.uint32, 2 * nm).reshape(nm, 2)
         return int(c[0]), conf, md
+
+    def orders(self):
+        """(segmented) walk row of sorted entry k, per side"""
+        return [o.download(np.uint32, S.n) for o, S in zip(self.order, self.S)]

@@ -142,6 +142,32 @@ class Engine:
         finally:
             L.kd_free(res)
 
+    def delta_pk_order(self, base, target, records):
+        """records uint32 [n, 2] (classify2's (base | NONE, target | NONE) deltas or updates) of two
+        KD_KEY_INT PackedSides -> (pks ascending int64 [n], record index of each uint32 [n]): the
+        order DeltaDiff.sorted_items yields (kd_delta_pk_order; the sides' keys are uploaded)"""
+        from . import packing
+        from .device import DevBuf, DevSide
+
+        records = np.ascontiguousarray(records, np.uint32).reshape(-1, 2)
+        n = records.shape[0]
+        if n == 0:
+            return np.zeros(0, np.int64), np.zeros(0, np.uint32)
+        lo, hi = [], []
+        for side in (base, target):
+            if side.n:
+                info = side.info if side.info is not None else packing.keys_scan(side.key, side.key_mode)
+                lo.append(int(info.pk_min))
+                hi.append(int(info.pk_max))
+        A, B = DevSide(self, base), DevSide(self, target)
+        sa, sb = A.kd_side(), B.kd_side()
+        d_rec = DevBuf.from_numpy(self, records.reshape(-1))
+        d_n = DevBuf.from_numpy(self, np.array([n], np.uint64))
+        d_pk, d_perm = DevBuf(self, 8 * n), DevBuf(self, 4 * n)
+        N.check(self.L.kd_delta_pk_order(self.ctx, ctypes.byref(sa), ctypes.byref(sb), d_rec.ptr, n, d_n.ptr, min(lo),
+                                         max(hi), d_pk.ptr, d_perm.ptr), "kd_delta_pk_order")
+        return d_pk.download(np.int64, n), d_perm.download(np.uint32, n)
+
     def fielddiff(self, old_data, old_off, new_data, new_off, pairs, maps):
         """Blob arenas (uint8 data, uint64 off[n+1]) per side; pairs uint32 [n, 2] (old blob,
         new blob) or None (blob u on both sides); maps: schema.FieldMaps.

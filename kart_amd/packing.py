@@ -5,13 +5,17 @@ A *side* is what ``RichBaseDataset.diff_feature`` hands to libgit2 implicitly: t
 become SoA arrays in join-key order (DESIGN.md "join key"):
 
 * ``KD_KEY_INT`` (IntPathEncoder, kart/dataset3_paths.py:283-299): the filename is
-  ``b64(msgpack([pk]))``; key = bucket24 | wrap34 | pk%64 — bijective with the pk, so equal keys
-  are equal paths and the pk is recovered from the key without touching the filename again.
+  ``b64(msgpack([pk]))``; key = rank24(bucket) | wrap34 | frank(pk) (kart_amd/walkkey.py) —
+  bijective with the pk, so equal keys are equal paths and the pk is recovered from the key without
+  touching the filename again, and ascending in git's tree order: the leaves the tree walk lists are
+  a key-ordered side already, with no sort (a leaf tree mixing 2**30 pk wraps is the exception:
+  kd_keys_scan reports it and the side is sorted).
 * ``KD_KEY_HASH`` (MsgpackHashPathEncoder, :202-215, and the 2x256 hex legacy layout): key = the
-  tree levels as a bucket number | FNV-1a bits of the filename; the GPU verifies filenames of
-  matched keys, a collision returns KD_EUNSUPPORTED.
+  tree levels as a (rank-mapped) bucket number | FNV-1a bits of the filename; the GPU verifies
+  filenames of matched keys, a collision returns KD_EUNSUPPORTED.  Walk order is ascending in the
+  bucket bits only: each bucket's few entries are sorted.
 
-Packing runs on the CPU in the native library (kd_pack_*), multithreaded.
+Packing runs on the CPU in the native library (kd_pack_*, kd_keys_scan), multithreaded.
 """
 import time
 from dataclasses import dataclass, field
@@ -77,6 +81,7 @@ class PackedSide:
     encoding: PathEncoding = field(default_factory=lambda: INT_PK_ENCODING)
     dev: Optional[tuple] = None  # (key, oid) DevBufs when the side was packed on the GPU
     timing: Optional[dict] = None  # pack_side's stage times (parse_s, sort_s, sort_on)
+    info: Optional[object] = None  # kd_keys_scan of the walk-order keys (_native.KdKeysInfo)
 
     @property
     def n(self):
@@ -130,6 +135,17 @@ def parse_keys(paths, off, encoding: PathEncoding):
     return keys
 
 
+def keys_scan(keys, key_mode):
+    """kd_keys_scan: (vary bits, key0, pk range, already strictly ascending?) of a key array"""
+    import ctypes
+
+    keys = np.ascontiguousarray(keys, np.uint64)
+    info = N.KdKeysInfo()
+    N.check(N.lib().kd_keys_scan(N.ptr(keys) if keys.size else N.ptr(_PAD), keys.shape[0], int(key_mode),
+                                 ctypes.byref(info)), "kd_keys_scan")
+    return info
+
+
 def sort_on_device(engine, keys, oids):
     """GPU pack: (arena-order keys, oids) -> device-resident sorted side (kd_sort_side, LDS-ranked
     LSD radix sort) + host copies (sorted keys, sorted oids, order).  PackError on duplicate keys."""
@@ -163,24 +179,32 @@ def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None, engine=None
     oids = np.ascontiguousarray(oids, np.uint8).reshape(n, 20)
     t0 = time.perf_counter()
     keys = parse_keys(paths, off, encoding)
+    info = keys_scan(keys, encoding.key_mode)
     t1 = time.perf_counter()
     dev = None
-    if engine is not None:
+    if info.ascending:  # git walk order is key order already (int keys of one pk wrap per leaf tree)
+        order = np.arange(n, dtype=np.int64)
+        sorted_oids = oids
+        sort_on = "none"
+    elif engine is not None:
         dk, do, dord = sort_on_device(engine, keys, oids)
         keys = dk.download(np.uint64, n)
         order = dord.download(np.uint32, n).astype(np.int64)
         sorted_oids = do.download(np.uint8, 20 * n).reshape(n, 20)
         dev = (dk, do)
+        sort_on = "gpu"
     else:
         order = np.argsort(keys, kind="stable")
         keys = keys[order]
         if n > 1 and not np.all(keys[1:] > keys[:-1]):
             raise PackError("duplicate join keys within one side")
         sorted_oids = oids[order]
+        sort_on = "host"
     side = PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(sorted_oids),
                       key_mode=encoding.key_mode, order=order.astype(np.int64), encoding=encoding)
     side.dev = dev
-    side.timing = {"parse_s": t1 - t0, "sort_s": time.perf_counter() - t1, "sort_on": "gpu" if dev else "host"}
+    side.info = info
+    side.timing = {"parse_s": t1 - t0, "sort_s": time.perf_counter() - t1, "sort_on": sort_on}
     if encoding.key_mode == N.KD_KEY_HASH:
         # sorted relative-path arena (needed for collision verification + pk decode)
         lens = (off[1:] - off[:-1])[order]
@@ -211,11 +235,10 @@ def int_keys_to_pks(keys):
 
 
 def pk_to_int_key(pk):
-    """Python-int pk -> KD_KEY_INT key (same formula as the native packer)."""
-    q = pk // 64
-    r = pk - q * 64
-    bucket = q % (1 << 24)
-    k = pk // (1 << 30) + (1 << 33)
-    if not 0 <= k < (1 << 34):
-        raise PackError(f"pk {pk} outside [-2**63, 2**63)")
-    return (bucket << 40) | (k << 6) | r
+    """Python-int pk -> KD_KEY_INT key (same formula as the native packer, kart_amd/walkkey.py)."""
+    from . import walkkey
+
+    try:
+        return walkkey.pk_to_int_key(pk)
+    except ValueError as e:
+        raise PackError(str(e)) from None

@@ -7,6 +7,9 @@ engine sees exactly what a Kart repo's trees would hand it.  Blob OIDs are synth
 64-bit mix of (pk, version)): equal content <=> equal OID, which is all classification relies on.
 No git repository is involved.
 
+Every side comes out in git tree order — the order the tree walk lists the leaves, which for
+int pks is ascending KD_KEY_INT key order (kart_amd/walkkey.py): no side needs a sort.
+
 Generation is vectorised numpy, fast enough for the 10M-point C2 layer in seconds.
 """
 from dataclasses import dataclass
@@ -15,7 +18,7 @@ import os
 
 import numpy as np
 
-from . import packing
+from . import packing, walkkey
 from .schema import Legend, Schema
 
 SEED = 0x4B415254
@@ -151,29 +154,28 @@ def point_blobs(pk, version, legend_hex, rng_seed=SEED):
 
 
 def points_layer(n, frac_update=0.01, frac_delete=0.01, frac_insert=0.01, seed=SEED, pk0=0):
-    """C2: n int-PK points (pks pk0..pk0+n-1); seeded 1% updates / deletes / inserts."""
+    """C2: n int-PK points (pks pk0..pk0+n-1); seeded 1% updates / deletes / inserts.  Both sides
+    in git tree (= key) order."""
     rng = np.random.default_rng(seed)
     schema = Schema.from_column_dicts(POINT_SCHEMA)
     legend = Legend(["c-fid"], [c["id"] for c in POINT_SCHEMA[1:]])
     lh = legend.hexhash()
-    pks = np.arange(pk0, pk0 + n, dtype=np.int64)
     n_upd, n_del, n_ins = int(n * frac_update), int(n * frac_delete), int(n * frac_insert)
-    perm = rng.permutation(n)
-    upd_i = np.sort(perm[:n_upd])
-    del_i = np.sort(perm[n_upd:n_upd + n_del])
+    perm = rng.permutation(n)  # edits picked by pk (index = pk - pk0)
+    tgt_ver = np.zeros(n + n_ins, np.uint64)
+    tgt_ver[perm[:n_upd]] = 1
+    tgt_ver[n:] = 2
+    keep = np.ones(n + n_ins, bool)
+    keep[perm[n_upd:n_upd + n_del]] = False
+    allp = walkkey.walk_order_range(pk0, pk0 + n + n_ins)  # every pk of either side, walk order
+    j = allp - pk0
+    pks = allp[j < n]
+    t_pk = allp[keep[j]]
+    t_ver = tgt_ver[t_pk - pk0]
     base_ver = np.zeros(n, np.uint64)
-    tgt_ver = base_ver.copy()
-    tgt_ver[upd_i] = 1
-    keep = np.ones(n, bool)
-    keep[del_i] = False
-    ins_pk = np.arange(pk0 + n, pk0 + n + n_ins, dtype=np.int64)
-    t_pk = np.concatenate([pks[keep], ins_pk])
-    t_ver = np.concatenate([tgt_ver[keep], np.full(n_ins, 2, np.uint64)])
-    keys_b = _int_keys(pks)
-    keys_t = _int_keys(t_pk)
-    base = packing.PackedSide(key=keys_b, oid=synth_oids(pks, base_ver), key_mode=0,
+    base = packing.PackedSide(key=walkkey.int_keys(pks), oid=synth_oids(pks, base_ver), key_mode=0,
                               order=np.arange(n, dtype=np.int64), encoding=packing.INT_PK_ENCODING)
-    target = packing.PackedSide(key=keys_t, oid=synth_oids(t_pk, t_ver), key_mode=0,
+    target = packing.PackedSide(key=walkkey.int_keys(t_pk), oid=synth_oids(t_pk, t_ver), key_mode=0,
                                 order=np.arange(t_pk.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
     bb = point_blobs(pks, base_ver, lh)
     tb = point_blobs(t_pk, t_ver, lh)
@@ -291,13 +293,13 @@ def c3_plan(pk, n, seed=C3_SEED):
     return np.where(h < 400, 1, np.where(h < 800, 2, np.where(h < 900, 3, 0))).astype(np.uint8)
 
 
-def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False, same_len=0.0):
+def polygons_layer(n, seed=SEED, shard=None, batch=1 << 20, delta_blobs=False, same_len=0.0):
     """C3: n int-PK MULTIPOLYGON features (pks 0..n-1) and n // 100 inserts (pks n..), 10 % edits =
     4 % geometry updates + 4 % attribute updates + 1 % deletes + 1 % inserts, edits
-    picked by a hash of the pk (c3_plan).
+    picked by a hash of the pk (c3_plan).  Both sides in git tree (= key) order.
 
-    ``lo, hi``: generate only the pks in [lo, hi) — a contiguous range of whole 64-pk leaf buckets
-    is one bucket-range shard of the same layer (bench.py --gpus N splits it this way).
+    ``shard=(rank, world)``: generate only that bucket-range shard of the same layer — a contiguous
+    run of the tree walk (shard_rank_range), as bench.py --gpus N splits it.
     Feature blobs are materialised for the updated features only (both versions): the diff reads no
     other blob — classification needs only keys and OIDs — so every other entry has a zero-length
     blob in the arena.  ``delta_blobs``: also the deleted features' base blobs and the inserted
@@ -307,26 +309,24 @@ def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False
     legend = Legend(["p-fid"], [c["id"] for c in POLYGON_SCHEMA[1:]])
     lh = legend.hexhash()
     n_ins = n // 100
-    hi = n + n_ins if hi is None else min(hi, n + n_ins)
-    lo = max(0, min(lo, hi))
-    pks = np.arange(lo, min(hi, n), dtype=np.int64)
-    plan = c3_plan(pks, n)
-    gver = (plan == 1).astype(np.uint8)
-    aver = (plan == 2).astype(np.uint8)
-    upd = plan == 1
-    upd |= plan == 2
-    keep = plan != 3
-    ins_pk = np.arange(max(lo, n), hi, dtype=np.int64)
-    t_pk = np.concatenate([pks[keep], ins_pk])
-    ver_b = np.zeros(pks.shape[0], np.uint64)
-    ver_t = np.concatenate([(gver.astype(np.uint64) | (aver.astype(np.uint64) << np.uint64(1)))[keep],
-                            np.full(ins_pk.shape[0], 4, np.uint64)])
-    base = packing.PackedSide(key=_int_keys(pks), oid=synth_oids(pks, ver_b), key_mode=0,
-                              order=np.arange(pks.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
-    target = packing.PackedSide(key=_int_keys(t_pk), oid=synth_oids(t_pk, ver_t), key_mode=0,
+    n_pks = n + n_ins
+    r_lo, r_hi = shard_rank_range(*shard, n_pks) if shard else (0, 1 << 24)
+    allp = walkkey.walk_order_pks(n_pks, r_lo, r_hi)  # every pk of either side in the shard, walk order
+    is_b = allp < n
+    plan = np.zeros(allp.shape[0], np.uint8)
+    plan[is_b] = c3_plan(allp[is_b], n)
+    in_t = ~is_b | (plan != 3)
+    bpos = np.cumsum(is_b) - 1  # base / target index of each walk position
+    tpos = np.cumsum(in_t) - 1
+    pks, t_pk = allp[is_b], allp[in_t]
+    gver = (plan == 1).astype(np.uint64)
+    aver = (plan == 2).astype(np.uint64)
+    ver_t = np.where(is_b, gver | (aver << np.uint64(1)), np.uint64(4))[in_t]
+    base = packing.PackedSide(key=walkkey.int_keys(pks), oid=synth_oids(pks, np.zeros(pks.shape[0], np.uint64)),
+                              key_mode=0, order=np.arange(pks.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
+    target = packing.PackedSide(key=walkkey.int_keys(t_pk), oid=synth_oids(t_pk, ver_t), key_mode=0,
                                 order=np.arange(t_pk.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
-    ub = np.nonzero(upd)[0]  # updated entries: base index; target index by search (target is pk-sorted)
-    ut = np.searchsorted(t_pk, pks[ub])
+    upd = (plan == 1) | (plan == 2)
 
     def blobs(idx_pk, gv, av):
         parts, offs = [], [np.zeros(1, np.uint64)]
@@ -336,31 +336,28 @@ def polygons_layer(n, seed=SEED, lo=0, hi=None, batch=1 << 20, delta_blobs=False
             offs.append(o[1:] + offs[-1][-1])
         return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), np.concatenate(offs)
 
-    bsel, tpk, tgv, tav = ub, pks[ub], gver[ub].astype(np.uint64), aver[ub].astype(np.uint64)
-    if delta_blobs:
-        bsel = np.nonzero(upd | (plan == 3))[0]
-        ti = np.concatenate([ut, np.arange(t_pk.shape[0] - ins_pk.shape[0], t_pk.shape[0])])
-        o = np.argsort(ti, kind="stable")
-        ut = ti[o]
-        z = np.zeros(ins_pk.shape[0], np.uint64)
-        tpk = np.concatenate([tpk, ins_pk])[o]
-        tgv = np.concatenate([tgv, z])[o]
-        tav = np.concatenate([tav, z])[o]
-    bd, bo = blobs(pks[bsel], np.zeros(bsel.size, np.uint64), np.zeros(bsel.size, np.uint64))
-    td, to = blobs(tpk, tgv, tav)
-    bb = _sparse_arena(pks.shape[0], bsel, bd, bo)
-    tb = _sparse_arena(t_pk.shape[0], ut, td, to)
-    return Layer(base, target, bb, tb, schema, {lh: legend}, int(ins_pk.shape[0]), int(ub.size),
+    bw = np.nonzero(upd | (plan == 3) if delta_blobs else upd)[0]  # walk positions with a base blob
+    tw = np.nonzero(upd | ~is_b if delta_blobs else upd)[0]  # ... with a target blob
+    bd, bo = blobs(allp[bw], np.zeros(bw.size, np.uint64), np.zeros(bw.size, np.uint64))
+    td, to = blobs(allp[tw], gver[tw], aver[tw])
+    bb = _sparse_arena(pks.shape[0], bpos[bw], bd, bo)
+    tb = _sparse_arena(t_pk.shape[0], tpos[tw], td, to)
+    return Layer(base, target, bb, tb, schema, {lh: legend}, int(np.count_nonzero(~is_b)), int(np.count_nonzero(upd)),
                  int(np.count_nonzero(plan == 3)))
 
 
-def shard_pk_range(rank, world, n_pks):
-    """[lo, hi) of rank's bucket-range shard of a layer with int pks 0..n_pks-1: whole 64-pk leaf
-    buckets (bucket = pk // 64 below 2**30), about n_pks / world pks each."""
-    if n_pks >= (1 << 30):
+def shard_rank_range(rank, world, n_pks):
+    """[lo, hi) of rank's bucket-range shard of a layer with int pks 0..n_pks-1, in rank-mapped bucket
+    space (the key's top 24 bits): a contiguous run of the tree walk holding about n_pks / world pks
+    in whole leaf trees.  Shards in rank order tile the walk."""
+    if n_pks > (1 << 30):
         raise ValueError("synthetic layer exceeds one bucket wrap (2**30 pks)")
     nb = (n_pks + 63) // 64
-    return 64 * (nb * rank // world), min(n_pks, 64 * (nb * (rank + 1) // world))
+    rk = np.sort(walkkey.rank_digits(np.arange(nb, dtype=np.uint64)))
+    a, b = nb * rank // world, nb * (rank + 1) // world
+    lo = 0 if rank == 0 else int(rk[a])
+    hi = (1 << 24) if rank == world - 1 else int(rk[b])
+    return lo, hi
 
 
 _B64 = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_", np.uint8)
@@ -404,69 +401,15 @@ def int_pk_paths(pk):
     return arena, off
 
 
-def walk_sort_keys(pk):
-    """u64 sort keys whose ascending order is git tree order (what kd_walk / `git ls-tree -r` lists,
-    kart/dataset3.py:225-231) of the IntPathEncoder paths of int pks in [0, 2**30): the four tree
-    characters (ASCII, big-endian) above the last base64 group of the filename.  Within one 64-pk
-    leaf tree every filename has the same length and differs only in that last group (the msgpack
-    width changes at 128 / 256 / 65536, multiples of 64), so the two fields order the paths exactly."""
-    pk = np.asarray(pk, np.int64)
-    n = pk.shape[0]
-    if n and (pk.min() < 0 or pk.max() >= (1 << 30)):
-        raise ValueError("walk_sort_keys: pks in [0, 2**30)")
-    t12 = _b64_pairs()
-    out = np.empty(n, np.uint64)
-    for s in range(0, n, 1 << 23):
-        p = pk[s:s + (1 << 23)]
-        bucket = p >> 6
-        tree = (t12[bucket >> 12] << np.uint64(16)) | t12[bucket & 4095]
-        # pk >= 65536: msgpack 91 ce b3 b2 b1 b0, the last group is (b2, b1, b0) = pk & 0xFFFFFF
-        v = p & 0xFFFFFF
-        last = (t12[v >> 12] << np.uint64(16)) | t12[v & 4095]
-        small = np.nonzero(p < 65536)[0]
-        if small.size:  # narrower msgpack ints: the general form (last group padded with '=')
-            q = p[small]
-            w = np.where(q < 128, 0, np.where(q < 256, 1, 2))
-            mlen = 2 + w
-            mp = np.zeros((q.shape[0], 6), np.int64)
-            mp[:, 0] = 0x91
-            mp[:, 1] = np.where(w == 0, q, np.where(w == 1, 0xCC, 0xCD))
-            for k in range(2):
-                mp[:, 2 + k] = np.where(k < w, (q >> np.maximum(8 * (w - 1 - k), 0)) & 0xFF, 0)
-            g = (mlen + 2) // 3 - 1  # index of the last 3-byte group
-            rows = np.arange(q.shape[0])
-            vv = mp[rows, 3 * g] << 16 | mp[rows, 3 * g + 1] << 8 | mp[rows, 3 * g + 2]
-            pad = (3 - mlen % 3) % 3  # '=' chars ending the name
-            ch = [_B64[(vv >> (18 - 6 * j)) & 63].astype(np.uint64) for j in range(4)]
-            ch[3] = np.where(pad >= 1, ord("="), ch[3]).astype(np.uint64)
-            ch[2] = np.where(pad >= 2, ord("="), ch[2]).astype(np.uint64)
-            last[small] = (ch[0] << np.uint64(24)) | (ch[1] << np.uint64(16)) | (ch[2] << np.uint64(8)) | ch[3]
-        out[s:s + p.shape[0]] = (tree << np.uint64(32)) | last
-    return out
-
-
-def _b64_pairs():
-    """[4096] u64: the two base64 chars (ASCII, big-endian) of a 12-bit value"""
-    v = np.arange(4096)
-    return (_B64[v >> 6].astype(np.uint64) << np.uint64(8)) | _B64[v & 63].astype(np.uint64)
-
-
 def walk_perm(keys):
-    """perm such that keys[perm] is the side in git tree (walk) order, for KD_KEY_INT keys of pks in
-    [0, 2**30) — the order the native walker hands the packer its leaves"""
-    keys = np.asarray(keys, np.uint64)
-    pk = (keys >> np.uint64(40)).astype(np.int64) * 64 + (keys & np.uint64(63)).astype(np.int64)
-    return np.argsort(walk_sort_keys(pk), kind="stable")
+    """perm such that keys[perm] is ascending: for a side in walk order this is the identity, except
+    where a leaf tree mixes pk wraps (the fallback sort's case); tests use it on shuffled sides"""
+    return np.argsort(np.asarray(keys, np.uint64), kind="stable")
 
 
 def _int_keys(pk):
-    """vectorised KD_KEY_INT (same formula as kd_pack_int_keys / packing.pk_to_int_key)"""
-    pk = np.asarray(pk, np.int64)
-    q = pk >> 6
-    r = (pk - (q << 6)).astype(np.uint64)
-    bucket = (q & ((1 << 24) - 1)).astype(np.uint64)
-    k = ((pk >> 30) + (1 << 33)).astype(np.uint64)
-    return np.ascontiguousarray((bucket << np.uint64(40)) | (k << np.uint64(6)) | r)
+    """vectorised KD_KEY_INT (kart_amd/walkkey.py; same keys as kd_pack_int_keys)"""
+    return walkkey.int_keys(pk)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -587,8 +530,10 @@ def _hash_paths(ids):
     return out
 
 
-def _pack_fixed(paths, oids):
-    """PackedSide (KD_KEY_HASH) of fixed-width relative paths [n, w] + OIDs [n, 20], vectorised"""
+def _pack_fixed(paths, oids, walk=False):
+    """PackedSide (KD_KEY_HASH) of fixed-width relative paths [n, w] + OIDs [n, 20], vectorised:
+    key-sorted, or (``walk``) in git tree order — the paths byte-sorted, as the tree walk lists them,
+    keys ascending only in their bucket bits (kd_sort_segmented_into's input)"""
     from . import _native as N
 
     n, w = paths.shape
@@ -599,10 +544,16 @@ def _pack_fixed(paths, oids):
     bad = N.lib().kd_pack_hash_keys(N.ptr(flat), N.ptr(off), n, 4, 0, N.ptr(keys), N.ptr(status))
     if bad:
         raise packing.PackError(f"{bad} synthetic paths not packable")
-    order = np.argsort(keys)  # (keys are distinct, checked below: any sort is stable)
-    keys = keys[order]
-    if n > 1 and not np.all(keys[1:] > keys[:-1]):
+    sk = np.sort(keys)
+    if n > 1 and not np.all(sk[1:] > sk[:-1]):
         raise packing.PackError("synthetic key collision")
+    if walk:
+        assert w % 8 == 0
+        cols = np.ascontiguousarray(paths).view(">u8").reshape(n, w // 8)
+        order = np.lexsort(tuple(cols[:, c] for c in range(w // 8 - 1, -1, -1)))
+    else:
+        order = np.argsort(keys)  # (keys are distinct: any sort is stable)
+    keys = keys[order]
     s = packing.PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(oids[order]),
                            key_mode=N.KD_KEY_HASH, order=order.astype(np.int64), encoding=packing.GENERAL_ENCODING)
     s.name = np.ascontiguousarray(paths[order]).reshape(-1)
@@ -610,10 +561,11 @@ def _pack_fixed(paths, oids):
     return s
 
 
-def table3_layers(n, seed=SEED, p_mod=0.02, p_del=0.005, p_ins=0.005, p_same=0.001, p_addadd=0.0005):
+def table3_layers(n, seed=SEED, p_mod=0.02, p_del=0.005, p_ins=0.005, p_same=0.001, p_addadd=0.0005, walk=False):
     """Ancestor of n string-PK rows and two independently edited descendants.  Per ancestor row each
     side keeps / modifies / deletes it; a fraction is modified identically on both (clean); both
-    sides insert new rows, some with the same pk on both (add/add, half identical)."""
+    sides insert new rows, some with the same pk on both (add/add, half identical).  ``walk``: the
+    sides in git tree order (as the walk lists them) instead of key order."""
     rng = np.random.default_rng(seed)
     ids = np.arange(n, dtype=np.int64)
     act = []  # per side: 0 keep, 1 modify, 2 delete
@@ -631,7 +583,7 @@ def table3_layers(n, seed=SEED, p_mod=0.02, p_del=0.005, p_ins=0.005, p_same=0.0
     aa_same = rng.random(n_aa) < 0.5
     paths_all = _hash_paths(np.concatenate([ids, ins_o, ins_t, aa]))
     P = lambda x: paths_all[x]  # ids are 0..total-1 in that order
-    anc = _pack_fixed(P(ids), synth_oids(ids, 0))
+    anc = _pack_fixed(P(ids), synth_oids(ids, 0), walk)
 
     def side(k, ins, ver):
         keep = act[k] != 2
@@ -642,7 +594,7 @@ def table3_layers(n, seed=SEED, p_mod=0.02, p_del=0.005, p_ins=0.005, p_same=0.0
         aav = np.where(aa_same, 3, ver).astype(np.uint64)
         sel = np.concatenate([rows, ins, aa])
         oids = np.concatenate([oid, synth_oids(ins, ver), synth_oids(aa, aav)])
-        return _pack_fixed(P(sel), oids)
+        return _pack_fixed(P(sel), oids, walk)
 
     ours = side(0, ins_o, 1)
     theirs = side(1, ins_t, 2)

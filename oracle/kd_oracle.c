@@ -60,6 +60,71 @@ int kdo_int_pk_key(int64_t pk_hi_sign, uint64_t pk_mag, uint64_t* key_out) {
 
 static const char B64URL[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
 
+/* urlsafe base64 of msgpack([pk]) (serialise_util.py:34-41,64-66 + dataset3_paths.py:164-165): the
+ * IntPathEncoder filename.  Returns its length. */
+static int int_pk_filename(int64_t pk, char* out) {
+    uint8_t m[10];
+    int L = 0, w = 0;
+    m[L++] = 0x91;
+    if (pk >= -32 && pk <= 127) m[L++] = (uint8_t)pk;
+    else if (pk > 0) {
+        if (pk <= 0xff) { m[L++] = 0xcc; w = 1; }
+        else if (pk <= 0xffff) { m[L++] = 0xcd; w = 2; }
+        else if (pk <= 0xffffffffll) { m[L++] = 0xce; w = 4; }
+        else { m[L++] = 0xcf; w = 8; }
+    } else {
+        if (pk >= -128) { m[L++] = 0xd0; w = 1; }
+        else if (pk >= -32768) { m[L++] = 0xd1; w = 2; }
+        else if (pk >= INT32_MIN) { m[L++] = 0xd2; w = 4; }
+        else { m[L++] = 0xd3; w = 8; }
+    }
+    for (int k = w - 1; k >= 0; k--) m[L++] = (uint8_t)((uint64_t)pk >> (8 * k));
+    int o = 0;
+    for (int i = 0; i < L; i += 3) {
+        uint32_t v = (uint32_t)m[i] << 16;
+        if (i + 1 < L) v |= (uint32_t)m[i + 1] << 8;
+        if (i + 2 < L) v |= m[i + 2];
+        out[o++] = B64URL[(v >> 18) & 63];
+        out[o++] = B64URL[(v >> 12) & 63];
+        out[o++] = i + 1 < L ? B64URL[(v >> 6) & 63] : '=';
+        out[o++] = i + 2 < L ? B64URL[v & 63] : '=';
+    }
+    return o;
+}
+
+static int ascii_rank(char c) {
+    int r = 0;
+    for (int i = 0; i < 64; i++) r += (unsigned char)B64URL[i] < (unsigned char)c;
+    return r;
+}
+
+static int name_cmp(const char* a, int na, const char* b, int nb) {
+    int n = na < nb ? na : nb;
+    int c = memcmp(a, b, (size_t)n);
+    return c ? c : (na > nb) - (na < nb);
+}
+
+/* The int-PK join key in git tree order, restated from its definition (DESIGN.md "join key"): the
+ * four tree characters of the IntPathEncoder path (dataset3_paths.py:292-299) as ASCII ranks, the
+ * pk's 2^30 wrap, and the filename's rank among the 64 filenames of its block [pk - pk%64, +64) —
+ * found by encoding and comparing all 64 names, as git's bytewise tree order would. */
+int kdo_int_walk_key(int64_t pk, uint64_t* key_out) {
+    i128 q = pyfloordiv((i128)pk, 64);
+    int64_t s = (int64_t)(q * 64);
+    i128 bucket = q - pyfloordiv(q, (i128)1 << 24) * ((i128)1 << 24);
+    uint64_t rb = 0;
+    for (int k = 3; k >= 0; k--) rb = (rb << 6) | (uint64_t)ascii_rank(B64URL[(int)(bucket >> (6 * k)) & 63]);
+    i128 wrap = pyfloordiv((i128)pk, (i128)1 << 30) + ((i128)1 << 33);
+    char me[16], other[16];
+    int nme = int_pk_filename(pk, me), rank = 0;
+    for (int j = 0; j < 64; j++) {
+        int no = int_pk_filename(s + j, other);
+        rank += name_cmp(other, no, me, nme) < 0;
+    }
+    *key_out = rb << 40 | (uint64_t)wrap << 6 | (uint64_t)rank;
+    return 0;
+}
+
 static int b64val(unsigned char c) {
     const char* p = (c == 0) ? NULL : strchr(B64URL, c);
     return p ? (int)(p - B64URL) : -1;
@@ -123,8 +188,8 @@ static uint64_t fnv1a64(const uint8_t* p, int n) {
 }
 
 /* Hashed-path join key (MsgpackHashPathEncoder, dataset3_paths.py:202-215): the tree levels
- * decoded as a bucket number (base64 alphabet index or hex), then 40/48 bits of FNV-1a of the
- * filename.  path = "c1/c2/c3/c4/<filename>" relative to feature/.  levels*bits_per_level
+ * as a bucket number in git's tree order (each base64 character's ASCII rank, or the hex digit),
+ * then 40/48 bits of FNV-1a of the filename.  path = "c1/c2/c3/c4/<filename>" relative to feature/.  levels*bits_per_level
  * bucket bits.  Returns -1 on malformed paths. */
 int kdo_hash_path_key(const uint8_t* path, int n, int levels, int hex, uint64_t* key_out) {
     uint64_t bucket = 0;
@@ -143,7 +208,8 @@ int kdo_hash_path_key(const uint8_t* path, int n, int levels, int hex, uint64_t*
             } else {
                 v = b64val(ch);
                 if (v < 0) return -1;
-                bucket = (bucket << 6) | (uint64_t)v; bits += 6;
+                /* git orders tree names bytewise: the digit's place in ASCII order */
+                bucket = (bucket << 6) | (uint64_t)ascii_rank((char)ch); bits += 6;
             }
         }
         if (pos >= n || path[pos] != '/') return -1;

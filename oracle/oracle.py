@@ -69,6 +69,8 @@ def C():
         L.kdo_point_envelope.argtypes = [_vp, ctypes.c_uint64, _vp]
         L.kdo_int_pk_key.restype = ctypes.c_int
         L.kdo_int_pk_key.argtypes = [ctypes.c_int64, ctypes.c_uint64, _vp]
+        L.kdo_int_walk_key.restype = ctypes.c_int
+        L.kdo_int_walk_key.argtypes = [ctypes.c_int64, _vp]
         L.kdo_decode_int_filename.restype = ctypes.c_int
         L.kdo_decode_int_filename.argtypes = [_vp, ctypes.c_int, _vp, _vp]
         L.kdo_hash_path_key.restype = ctypes.c_int

@@ -245,19 +245,21 @@ def test_gpu_env_overlap_vs_oracle(engine):
     (True, 1000, "points", "late"), (True, 3_000_000, "points", "late"), (False, 2_000_000, "polygons", "late"),
     (True, 1000, "points", "gather"), (True, 2_000_000, "polygons", "gather"),
     (True, 10_000_000, "points", False),    # C2 at its stated size (configs[1])
-    (True, 100_000_000, "polygons", "late"),  # C3 at its stated size (configs[2], the bench's default
-                                              # workload), from walk-order sides: both 100M sorts included
+    (True, 100_000_000, "polygons", False),  # C3 at its stated size (configs[2], the bench's default
+                                             # workload): walk-order sides, no sort, pk-order sorts included
+    (True, 20_000_000, "polygons", "late"),  # the fallback side sorts at 20M
     # C3v: 60 % of the geometry edits keep their length, so their payloads are compared byte by byte
     (True, 2_000_000, "polygons_same", False), (False, 2_000_000, "polygons_same", False),
     (True, 100_000_000, "polygons_same", False),
 ])
 def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
-    """the device-resident classify2 -> fielddiff pipeline bench.py times (both compaction modes),
-    on the C2 points layer and the C3 polygon layer (~370-B blobs: head + tail windows and the
-    cooperative payload compares); buffers from the library's own allocator.  walk: the sides start
-    in git tree order and every step sorts them on the GPU first (kd_sort_side_into): the sorted
-    keys and OIDs must equal the generator's key-ordered sides and the order must invert the walk
-    permutation (= a stable argsort of the walk-order keys), bit for bit"""
+    """the device-resident classify2 -> fielddiff -> pk-order pipeline bench.py times (both compaction
+    modes), on the C2 points layer and the C3 polygon layer (~370-B blobs: head + tail windows and the
+    cooperative payload compares); buffers from the library's own allocator.  The sides come in git
+    tree order, which is key order: no sort.  walk = "late" / "gather": the fallback for sides whose
+    walk order is not key order — the rows are scrambled and every step sorts them on the GPU first
+    (kd_sort_side_into): the sorted keys (and OIDs) must equal the generator's key-ordered sides and the
+    order must invert the scramble, bit for bit"""
     from kart_amd import synth
     from kart_amd.device import DiffPipeline
     from kart_amd.schema import FieldMaps
@@ -265,8 +267,9 @@ def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
     L = (synth.points_layer(n, seed=11) if layer == "points" else
          synth.polygons_layer(n, seed=12, same_len=0.6 if layer == "polygons_same" else 0.0))
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
-    perms = (synth.walk_perm(L.base.key), synth.walk_perm(L.target.key)) if walk else None
-    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered, walk=perms,
+    rng = np.random.default_rng(n)
+    perms = (rng.permutation(L.base.n), rng.permutation(L.target.n)) if walk else None
+    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered, unsorted=perms,
                         late=walk == "late")
     if walk:  # scramble the sorted buffers first: the sort (and, gathering, its OID permute) must rewrite them
         for S in (pipe.A, pipe.B):
@@ -291,6 +294,24 @@ def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
     assert (counts["inserts"], counts["updates"], counts["deletes"]) == (oc["inserts"], oc["updates"], oc["deletes"])
     om, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
     assert np.array_equal(masks, om) and np.array_equal(status, ost)
+    if pipe.pk_order and ordered:
+        check_pk_order(pipe, L.base.key, L.target.key, delta, upd)
+
+
+def check_pk_order(pipe, kA, kB, delta, upd):
+    """kd_delta_pk_order's outputs: the pks of the delta (and update) records ascending, and the
+    record index of each — a stable argsort of the records' pks (DeltaDiff.sorted_items order)"""
+    from kart_amd import walkkey
+
+    d_pk, d_perm, u_pk, u_perm = pipe.pk_results()
+    for rec, pk_out, perm_out in ((delta, d_pk, d_perm), (upd, u_pk, u_perm)):
+        a, b = rec[:, 0], rec[:, 1]
+        keys = np.where(a != 0xFFFFFFFF, kA[np.minimum(a, max(kA.size - 1, 0))] if kA.size else 0,
+                        kB[np.minimum(b, max(kB.size - 1, 0))] if kB.size else 0)
+        pks = walkkey.int_keys_to_pks(keys.astype(np.uint64))
+        want = np.argsort(pks, kind="stable")
+        assert np.array_equal(perm_out, want.astype(np.uint32))
+        assert np.array_equal(pk_out, pks[want])
 
 
 @pytest.mark.parametrize("n,seed", [(1000, 1), (2_000_000, 2)])
@@ -511,9 +532,10 @@ def test_gpu_sort_side_into_vs_argsort(engine, n, kind):
         rng.shuffle(keys)
     elif kind == "int30":
         keys = synth._int_keys(rng.permutation(n).astype(np.int64) * 5)
-    elif kind == "walk":
-        keys = synth._int_keys(np.arange(n, dtype=np.int64))
-        keys = keys[synth.walk_perm(keys)]
+    elif kind == "walk":  # a walk of pks mixing wraps in their leaf trees: not key order
+        p = np.arange(n, dtype=np.int64)
+        keys = synth._int_keys(np.where(p % 3 == 0, p + (1 << 30), p))
+        rng.shuffle(keys)
     elif kind == "runs5":
         spread = np.uint64(0)
         for b in (0, 1, 9, 10, 20, 33, 34, 35, 50, 63):
@@ -535,8 +557,12 @@ def test_gpu_sort_side_into_vs_argsort(engine, n, kind):
     oids = rng.integers(0, 256, size=(n, 20), dtype=np.uint8)
     dk, do = DevBuf.from_numpy(engine, keys), DevBuf.from_numpy(engine, oids.reshape(-1))
     ko, oo, order, dup = DevBuf(engine, 8 * n), DevBuf(engine, 20 * n), DevBuf(engine, 4 * n), DevBuf(engine, 4)
-    N.check(engine.L.kd_sort_side_into(engine.ctx, dk.ptr, do.ptr, ko.ptr, oo.ptr, order.ptr, n, dup.ptr),
-            "kd_sort_side_into")
+    info = None
+    if kind in ("int30", "walk", "runs5") and n > 0:  # the host scan sizes the passes: no read-back
+        from kart_amd import packing
+        info = packing.keys_scan(keys, 0 if kind != "runs5" else 1)
+    N.check(engine.L.kd_sort_side_into(engine.ctx, dk.ptr, do.ptr, ko.ptr, oo.ptr, order.ptr, n, dup.ptr,
+                                       ctypes.byref(info) if info is not None else None), "kd_sort_side_into")
     ref = np.argsort(keys, kind="stable")
     assert np.array_equal(order.download(np.uint32, n), ref.astype(np.uint32))
     assert np.array_equal(ko.download(np.uint64, n), keys[ref])
@@ -549,7 +575,7 @@ def test_gpu_sort_side_into_rejects_aliasing(engine):
     from kart_amd.device import DevBuf
 
     dk, do, order = DevBuf(engine, 80), DevBuf(engine, 200), DevBuf(engine, 40)
-    assert engine.L.kd_sort_side_into(engine.ctx, dk.ptr, do.ptr, dk.ptr, do.ptr, order.ptr, 10, None) == N.KD_EINVAL
+    assert engine.L.kd_sort_side_into(engine.ctx, dk.ptr, do.ptr, dk.ptr, do.ptr, order.ptr, 10, None, None) == N.KD_EINVAL
 
 
 def test_gpu_sort_side_duplicates_rejected(engine):
@@ -569,8 +595,11 @@ def test_gpu_pack_side_equals_host_pack(engine, n):
     L = synth.polygons_layer(n, seed=3)
     sides = []
     for S in (L.base, L.target):
-        pks = (S.key >> np.uint64(40)).astype(np.int64) * 64 + (S.key & np.uint64(63)).astype(np.int64)
-        perm = np.random.default_rng(n).permutation(S.n)  # leaves in another (walk) order
+        pks = packing.int_keys_to_pks(S.key)
+        walk = packing.pack_side(*synth.int_pk_paths(pks)[:1], S.oid, packing.INT_PK_ENCODING,
+                                 rel_off=synth.int_pk_paths(pks)[1], engine=engine)
+        assert walk.timing["sort_on"] == "none" and np.array_equal(walk.key, S.key)  # walk order: no sort
+        perm = np.random.default_rng(n).permutation(S.n)  # leaves in another order: sorted on the GPU
         arena, off = synth.int_pk_paths(pks[perm])
         host = packing.pack_side(arena, S.oid[perm], packing.INT_PK_ENCODING, rel_off=off)
         dev = packing.pack_side(arena, S.oid[perm], packing.INT_PK_ENCODING, rel_off=off, engine=engine)

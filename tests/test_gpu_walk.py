@@ -1,0 +1,149 @@
+"""-m gpu: the walk-order path — joins straight on the sides as the tree walk lists them, the deltas
+radix-sorted into pk order (kd_delta_pk_order), the hash sides' per-bucket sort
+(kd_sort_segmented_into) and the late-materialised three-way merge — against numpy, the oracle and the
+reference's own sorted_items order (tests/golden)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from fixtures import DIFF_FIXTURES, load, pk_of
+from oracle import oracle as O
+
+from kart_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _int_side(pks, rng):
+    from kart_amd import packing, walkkey
+
+    keys = np.sort(walkkey.int_keys(np.asarray(pks, np.int64)))
+    return packing.PackedSide(keys, rng.integers(0, 256, size=(keys.size, 20), dtype=np.uint8), 0, np.arange(keys.size))
+
+
+@pytest.mark.parametrize("case", ["small", "neg", "wide", "one", "empty_base", "dense"])
+def test_gpu_delta_pk_order_vs_numpy(engine, case):
+    """records of two int sides -> pks ascending + record index: any pk range (a few bits, the whole
+    signed 64-bit range: 64-bit compact keys, 8 passes), a single pk, an empty side"""
+    from kart_amd import walkkey
+
+    rng = np.random.default_rng(len(case))
+    if case == "small":
+        pa, pb = np.arange(0, 3000), np.arange(1500, 4000)
+    elif case == "neg":
+        pa, pb = np.arange(-70000, 5000, 3), np.arange(-80000, -20000, 2)
+    elif case == "wide":
+        u = np.unique(rng.integers(-2**63, 2**63 - 1, 60000, dtype=np.int64))
+        pa, pb = u[:40000], u[20000:]
+    elif case == "one":
+        pa, pb = np.array([77]), np.array([77])
+    elif case == "empty_base":
+        pa, pb = np.zeros(0, np.int64), np.arange(5, 50000)
+    else:
+        pa, pb = np.arange(0, 2_000_000), np.arange(1_000_000, 3_000_000)
+    A, B = _int_side(pa, rng), _int_side(pb, rng)
+    if case == "one":
+        B.oid[0] ^= 1
+    ka, kb = A.key, B.key
+    # the union as classify2 would list it (key order), every pair a record
+    allk = np.union1d(ka, kb)
+    ia = np.searchsorted(ka, allk)
+    ib = np.searchsorted(kb, allk)
+    has_a = (ia < ka.size) & (ka[np.minimum(ia, max(ka.size - 1, 0))] == allk) if ka.size else np.zeros(allk.size, bool)
+    has_b = (ib < kb.size) & (kb[np.minimum(ib, max(kb.size - 1, 0))] == allk) if kb.size else np.zeros(allk.size, bool)
+    rec = np.stack([np.where(has_a, ia, 0xFFFFFFFF), np.where(has_b, ib, 0xFFFFFFFF)], 1).astype(np.uint32)
+    pk, perm = engine.delta_pk_order(A, B, rec)
+    pks = walkkey.int_keys_to_pks(allk)
+    want = np.argsort(pks, kind="stable")
+    assert np.array_equal(perm, want.astype(np.uint32)) and np.array_equal(pk, pks[want])
+
+
+@pytest.mark.parametrize("name", [n for n in DIFF_FIXTURES])
+def test_gpu_pk_order_equals_reference_sorted_items(engine, name):
+    """The reference's own DeltaDiff.sorted_items order (the golden delta lists were written in it) ==
+    classify2's deltas put in pk order on the GPU, for every int-PK diff of the reference repos"""
+    from checks import delta_set, golden_set  # noqa: F401
+
+    fx = load(name)
+    for case in fx.cases("diff2"):
+        A, B = fx.packed(case["base"]), fx.packed(case["target"])
+        if A.key_mode != 0 or not case["deltas"]:
+            continue
+        r = engine.diff2(A, B)
+        pk, perm = engine.delta_pk_order(A, B, r.delta)
+        got = []
+        for p, i in zip(pk.tolist(), perm.tolist()):
+            a, b = r.delta[i]
+            got.append(("insert" if a == 0xFFFFFFFF else "delete" if b == 0xFFFFFFFF else "update", p))
+        want = [(d["type"], pk_of(d["old_pk"]) if d["old_pk"] is not None else pk_of(d["new_pk"])) for d in case["deltas"]]
+        assert got == want, (name, case["base"], case["target"])
+
+
+def _seg_sort(engine, keys, seg_bits=24):
+    from kart_amd.device import DevBuf
+
+    n = keys.size
+    dk = DevBuf.from_numpy(engine, keys if n else np.zeros(1, np.uint64))
+    ko, order, err = DevBuf(engine, 8 * max(n, 1)), DevBuf(engine, 4 * max(n, 1)), DevBuf(engine, 8)
+    err.zero()
+    N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk.ptr, ko.ptr, order.ptr, n, seg_bits, err.ptr),
+            "kd_sort_segmented_into")
+    return ko.download(np.uint64, n), order.download(np.uint32, n), int(err.download(np.uint32, 1)[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 1000, 400_000, 3_000_000])
+def test_gpu_segmented_sort_c4_walk_order(engine, n):
+    """the C4 string-PK sides in git tree order: buckets ascend, entries inside a bucket in filename
+    order; the per-bucket sort equals a full stable argsort of the keys"""
+    from kart_amd import synth
+
+    M = synth.table3_layers(max(n, 10), seed=3, walk=True)
+    for S in (M.ancestor, M.ours, M.theirs):
+        keys = S.key[:n]
+        k, order, err = _seg_sort(engine, keys)
+        ref = np.argsort(keys, kind="stable")
+        assert err == 0
+        assert np.array_equal(order, ref.astype(np.uint32)) and np.array_equal(k, keys[ref])
+
+
+def test_gpu_segmented_sort_flags(engine):
+    """duplicate keys and descending bucket bits set err 1; a bucket of more than 512 entries err 4"""
+    rng = np.random.default_rng(5)
+    base = np.sort(rng.integers(0, 2**63, 5000, dtype=np.uint64))
+    dup = base.copy()
+    dup[100] = dup[101]
+    assert _seg_sort(engine, dup)[2] & 1
+    desc = base.copy()
+    desc[10], desc[4000] = desc[4000], desc[10]
+    assert _seg_sort(engine, desc, seg_bits=24)[2] & 1
+    big = (np.uint64(7) << np.uint64(40)) | rng.permutation(2000).astype(np.uint64)
+    assert _seg_sort(engine, big)[2] & 4
+    ok = (np.uint64(7) << np.uint64(40)) | rng.permutation(500).astype(np.uint64)
+    k, order, err = _seg_sort(engine, ok)
+    assert err == 0 and np.array_equal(k, np.sort(ok))
+
+
+@pytest.mark.parametrize("n", [1000, 400_000, pytest.param(50_000_000, marks=pytest.mark.timeout(900))])
+def test_gpu_merge3_segmented_c4_walk_order(engine, n):
+    """C4 from the sides as the tree walk lists them: three per-bucket sorts, then the three-way merge
+    reading OIDs and filenames through the orders (kd_merge3_device_perm) — conflicts and merge deltas
+    bit-exact with the oracle on the key-sorted sides; 50M rows = C4 at its stated size"""
+    from kart_amd import packing, synth
+    from kart_amd.device import MergePipeline
+
+    M = synth.table3_layers(n, seed=n, walk=True)
+    pipe = MergePipeline(engine, M.ancestor, M.ours, M.theirs, segmented=True)
+    for _ in range(2):
+        pipe.step()
+    engine.sync()
+    n_clean, conf, md = pipe.results()
+    srt = []
+    for S, order in zip((M.ancestor, M.ours, M.theirs), pipe.orders()):
+        ref = np.argsort(S.key, kind="stable")
+        assert np.array_equal(order, ref.astype(np.uint32))
+        srt.append((S.key[ref], S.oid[ref]))
+    oc, om, ocl = O.classify3(*srt[0], *srt[1], *srt[2])
+    assert np.array_equal(conf, oc.reshape(-1, 3)) and np.array_equal(md, om.reshape(-1, 2)) and n_clean == ocl
+    assert conf.shape[0] == M.n_conflict
+    del packing

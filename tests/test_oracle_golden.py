@@ -67,19 +67,23 @@ def test_oracle_paths_golden():
     pks = packing.int_keys_to_pks(side.key)
     want = sorted(int(pk) for pk in uniq.values())
     assert sorted(pks.tolist()) == want
+    alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
     for pk_s, path in P["int"]:
         pk = int(pk_s)
         key = np.zeros(1, np.uint64)
-        rc = O.C().kdo_int_pk_key(1 if pk < 0 else 0, abs(pk), key.ctypes.data)
-        assert rc == 0
+        assert O.C().kdo_int_walk_key(pk, key.ctypes.data) == 0
         assert int(key[0]) == packing.pk_to_int_key(pk)
-        # the key's bucket is the IntPathEncoder tree path
+        # the key's bucket bits are the IntPathEncoder tree path, each character as its ASCII rank
         tree = path.rsplit("/", 1)[0].replace("/", "")
-        alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
-        bucket = 0
+        rank = 0
         for ch in tree:
-            bucket = bucket * 64 + alpha.index(ch)
-        assert int(key[0]) >> 40 == bucket
+            rank = rank * 64 + sorted(alpha).index(ch)
+        assert int(key[0]) >> 40 == rank
+    # these vectors mix 2**30 wraps in one leaf tree (0, 2**30, -2**30 all live in A/A/A/A): their
+    # git order is not key order, and the packer says so
+    paths = sorted(uniq, key=str.encode)
+    side = packing.pack_side(paths, np.zeros((len(paths), 20), np.uint8), packing.INT_PK_ENCODING)
+    assert side.info.ascending == 0 and side.timing["sort_on"] == "host"
     # hashed paths: packer == oracle, bucket bits == tree chars
     for enc, vecs, levels, hexm in ((packing.GENERAL_ENCODING, P["hash"], 4, 0),):
         rel = [p for _, p in vecs]
@@ -92,6 +96,67 @@ def test_oracle_paths_golden():
     leg = [p for pk, p in P["legacy"] if pk.startswith("s:")]
     side = packing.pack_side(leg, np.zeros((len(leg), 20), np.uint8), packing.LEGACY_ENCODING)
     assert side.n == len(leg)
+
+
+@pytest.mark.parametrize("name", [n for n in DIFF_FIXTURES if not n.startswith("synth")])
+def test_reference_repo_sides_need_no_sort(name):
+    """Every int-PK side of the reference's own repositories, in the order `git ls-tree -r` listed it
+    (the fixtures keep that order), packs to strictly ascending keys: no sort before the join."""
+    fx = load(name)
+    for key in fx.meta["sides"]:
+        side = fx.packed(key)
+        if side.key_mode == 0 and side.n:
+            assert side.timing["sort_on"] == "none", (name, key)
+
+
+def test_walk_key_oracle_vs_packer_random():
+    """The packer's table-driven keys (kd_walkkey.h / walkkey.py) equal the oracle's brute-force
+    restatement (every block's 64 filenames compared) on pks across every msgpack width and sign,
+    and the key inverts to the pk."""
+    from kart_amd import packing, walkkey
+
+    rng = np.random.default_rng(7)
+    edges = [0, 63, 64, 127, 128, 255, 256, 65535, 65536, 2**32 - 1, 2**32, 2**63 - 1, -1, -32, -33, -64, -65,
+             -128, -129, -32768, -32769, -2**31, -2**31 - 1, -2**63, 2**30 - 1, 2**30, -2**30, -2**30 - 1]
+    pks = np.concatenate([np.array(edges, np.int64), np.arange(-300, 300, dtype=np.int64),
+                          rng.integers(-2**63, 2**63 - 1, 3000, dtype=np.int64),
+                          rng.integers(-2**33, 2**33, 3000, dtype=np.int64)])
+    key = np.zeros(1, np.uint64)
+    got = walkkey.int_keys(pks)
+    for pk, k in zip(pks.tolist(), got.tolist()):
+        assert O.C().kdo_int_walk_key(pk, key.ctypes.data) == 0
+        assert int(key[0]) == k, pk
+    assert np.array_equal(packing.int_keys_to_pks(got), pks)
+    assert np.array_equal(walkkey.int_keys_to_pks(got), pks)
+
+
+def test_walk_key_order_is_git_path_order():
+    """Sorting IntPathEncoder paths bytewise (git's tree order) == sorting their keys, for pk ranges
+    whose leaf trees hold one 2**30 wrap (negative, small, msgpack width edges, the wrap's end)."""
+    from kart_amd import walkkey
+
+    alpha = walkkey.B64.decode()
+
+    def path(p):
+        b = (p // 64) % (1 << 24)
+        return ("/".join(alpha[(b >> (18 - 6 * k)) & 63] for k in range(4)) + "/" + walkkey.filename(p)).encode()
+
+    for lo, hi in [(-5000, 5000), (60000, 70000), (2**32 - 3000, 2**32 + 3000), (2**30 - 5000, 2**30),
+                   (-2**30, -2**30 + 5000), (-40000, -30000)]:
+        ps = np.arange(lo, hi, dtype=np.int64)
+        if lo < 0 < hi:  # negative and non-negative pks share no bucket here (|pk| < 2**29)
+            pass
+        by_path = sorted(ps.tolist(), key=path)
+        by_key = ps[np.argsort(walkkey.int_keys(ps))].tolist()
+        assert by_path == by_key, (lo, hi)
+    # a leaf tree mixing wraps (pk and pk + 2**30 share a bucket): the keys still invert, but the
+    # walk order can differ from key order — kd_keys_scan reports it and the side gets sorted
+    ps = np.array([5, 5 + 2**30, 6, 6 + 2**30], np.int64)
+    walk = sorted(ps.tolist(), key=path)
+    keys = walkkey.int_keys(np.array(walk, np.int64))
+    from kart_amd import packing
+    info = packing.keys_scan(keys, 0)
+    assert info.ascending == int(bool(np.all(keys[1:] > keys[:-1])))
 
 
 def _hexf(x):

@@ -37,20 +37,20 @@ def test_polygons_layer_plan_and_encoding():
 
 
 def test_polygons_layer_shards_concatenate():
-    """bucket-range slices (bench.py --gpus N) are exactly the whole layer's entries, in order"""
+    """bucket-range shards (bench.py --gpus N) are exactly the whole layer's entries, in order: each
+    a contiguous run of the tree walk"""
     n = 30_000
     whole = synth.polygons_layer(n, seed=9)
-    parts = [synth.polygons_layer(n, seed=9, lo=a, hi=b) for a, b in
-             (synth.shard_pk_range(r, 4, n + n // 100) for r in range(4))]
+    parts = [synth.polygons_layer(n, seed=9, shard=(r, 4)) for r in range(4)]
     for side in ("base", "target"):
         assert np.array_equal(np.concatenate([getattr(p, side).key for p in parts]), getattr(whole, side).key)
         assert np.array_equal(np.concatenate([getattr(p, side).oid for p in parts]), getattr(whole, side).oid)
     assert sum(p.n_update for p in parts) == whole.n_update
     assert sum(p.n_insert for p in parts) == whole.n_insert and sum(p.n_delete for p in parts) == whole.n_delete
-    # shard edges fall on 64-pk leaf buckets
-    for r in range(4):
-        lo, hi = synth.shard_pk_range(r, 4, n + n // 100)
-        assert lo % 64 == 0 and (hi % 64 == 0 or hi == n + n // 100)
+    # shard edges fall between whole leaf trees: no bucket in two shards
+    buckets = [set((p.base.key >> np.uint64(40)).tolist()) | set((p.target.key >> np.uint64(40)).tolist()) for p in parts]
+    assert all(not (buckets[i] & buckets[j]) for i in range(4) for j in range(i + 1, 4))
+    assert abs(parts[0].base.n - parts[3].base.n) < n // 40
 
 
 def test_int_pk_paths_match_reference_encoder():
@@ -72,19 +72,20 @@ def test_int_pk_paths_match_reference_encoder():
 
 
 def test_walk_order_is_git_path_order():
-    """synth.walk_perm puts a side in git tree order: the order `git ls-tree -r` / kd_walk lists the
-    IntPathEncoder paths (byte-wise path order), which the GPU sort starts from (bench.py's
-    value_with_sort, the walk-mode pipeline tests)"""
+    """A side's leaves as `git ls-tree -r` / kd_walk list them (bytewise path order) have ascending
+    KD_KEY_INT keys: the synthetic layers, generated in walk order, are key-ordered as they stand."""
     rng = np.random.default_rng(3)
     pks = np.unique(np.concatenate([np.arange(0, 400), np.arange(65_000, 66_000), np.arange(2**24 - 70, 2**24 + 70),
                                     rng.integers(0, 2**30, 30_000)]))
     rng.shuffle(pks)
     arena, off = synth.int_pk_paths(pks)
     paths = [arena[int(off[i]):int(off[i + 1])].tobytes() for i in range(pks.shape[0])]
-    want = sorted(range(pks.shape[0]), key=lambda i: paths[i])
-    keys = synth._int_keys(pks)
-    perm = synth.walk_perm(keys)
-    assert np.array_equal(perm, np.array(want))
-    # and the walk order is far from key order (what makes the GPU sort necessary)
-    w = keys[perm]
-    assert np.count_nonzero(w[1:] < w[:-1]) > pks.shape[0] // 20
+    walk = np.array(sorted(range(pks.shape[0]), key=lambda i: paths[i]))
+    keys = synth._int_keys(pks)[walk]
+    assert np.all(keys[1:] > keys[:-1])
+    L = synth.polygons_layer(10_000, seed=2)
+    for side in (L.base, L.target):
+        p = __import__("kart_amd.packing", fromlist=["x"]).int_keys_to_pks(side.key)
+        a, o = synth.int_pk_paths(p)
+        ps = [a[int(o[i]):int(o[i + 1])].tobytes() for i in range(p.shape[0])]
+        assert ps == sorted(ps)
