@@ -375,7 +375,8 @@ def run_diff(args, H, polygons):
 
 SORT_KERNELS = ("k_rs_bits", "k_sort_hist", "k_sort_scan", "k_sort_pass", "k_gather_oid")
 STEP_KERNELS = ("k_partition2", "k_join2", "k_gscan2", "k_place2", "k_fielddiff", "k_dpk_keys", "k_sort_scan",
-                "k_sort_pass")
+                "k_sort_pass", "k_pkm_mark", "k_pkm_scan", "k_pkm_place")
+PKM_MAX_BLOCKS = 1 << 26  # kd_delta_pk_order's bitmap path: pk ranges of at most this many 64-pk blocks
 RS_RB = 9  # digit bits per radix pass (kd_sort.hip RS_RB): passes = ceil(varying bits / 9)
 
 
@@ -397,22 +398,30 @@ def check_pk_order(pipe, L, delta, upd):
 
 
 def pk_sort_summary(pipe, parts, counts):
-    """the deltas' and updates' pk sorts (kd_delta_pk_order, two calls per step): algorithmic bytes
-    from the library's own pass count (the pk range's varying bits, 9-bit digits).  Per record: the
-    record read (8 B) + its key gathered (8 B) + the compact key written (4 B); per pass the compact
-    key + index read and written (16 B; the last pass writes the 8-B pk: 20 B)"""
+    """the deltas' and updates' pk order (kd_delta_pk_order, two calls per step).  A bounded pk range
+    takes the bitmap placement (one 64-bit mask per 64-pk block; every pk occurs once per list):
+    algorithmic bytes per record = the record (8 B) + its key (8 B) read, the pk (8 B) + the record
+    index (4 B) written; per block its mask written and read (16 B) and its in-chunk prefix (8 B).
+    Otherwise the radix path: the library's own pass count (the pk range's varying bits, 9-bit digits)."""
     lo, hi = pipe.pk_range
-    d = (lo ^ (1 << 63)) ^ (hi ^ (1 << 63)) if hi != lo else 0
-    bits = d.bit_length()
-    npass = max(1, radix_passes(bits))
-    ck = 4 if bits <= 32 else 8
-    per_rec = 8 + 8 + ck + sum((ck if p == 0 else ck + 4) + (12 if p == npass - 1 else ck + 4) for p in range(npass))
+    nb = (hi >> 6) - (lo >> 6) + 1
     recs = counts["deltas"] + counts["updates"]
-    ms = sum(parts[k][0] * parts[k][1] for k in ("k_dpk_keys", "k_sort_scan", "k_sort_pass") if k in parts) / 3
-    alg = per_rec * recs
-    return {"what": "deltas and updates radix-sorted by pk on the device (kd_delta_pk_order x2: k_dpk_keys + "
-                    "k_sort_scan + onesweep k_sort_pass per digit), the order DeltaDiff.sorted_items yields",
-            "records_per_step": recs, "varying_bits": bits, "passes_per_sort": npass,
+    if nb <= PKM_MAX_BLOCKS:
+        kk = ("k_pkm_mark", "k_pkm_scan", "k_pkm_place")
+        alg = 28 * recs + 2 * 24 * nb
+        how = {"path": "bitmap", "blocks": nb}
+    else:
+        d = (lo ^ (1 << 63)) ^ (hi ^ (1 << 63)) if hi != lo else 0
+        bits = d.bit_length()
+        npass = max(1, radix_passes(bits))
+        ck = 4 if bits <= 32 else 8
+        per_rec = 8 + 8 + ck + sum((ck if p == 0 else ck + 4) + (12 if p == npass - 1 else ck + 4) for p in range(npass))
+        kk = ("k_dpk_keys", "k_sort_scan", "k_sort_pass")
+        alg = per_rec * recs
+        how = {"path": "radix", "varying_bits": bits, "passes_per_sort": npass}
+    ms = sum(parts[k][0] * parts[k][1] for k in kk if k in parts) / 3
+    return {"what": "deltas and updates put in pk order on the device (kd_delta_pk_order x2), the order "
+                    "DeltaDiff.sorted_items yields", "records_per_step": recs, **how,
             "ms_per_step_events": round(ms, 4),
             "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": int(alg),
                          "achieved": round(alg / (ms * 1e-3) / 1e9, 1) if ms else None, "peak": HBM_PEAK_GBS,
@@ -447,8 +456,16 @@ def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
     sized by kd_keys_scan: no read-back), the join reading OIDs through the sort orders."""
     from kart_amd.device import DiffPipeline
 
-    rng = np.random.default_rng(1)
-    perms = (rng.permutation(L.base.n), rng.permutation(L.target.n))
+    def leaf_scramble(n, seed):
+        """rows shuffled inside each run of 64 (what a walk of leaf trees mixing pk wraps looks like:
+        key order broken inside leaf trees, kept between them)"""
+        r = np.random.default_rng(seed)
+        m = (n + 63) // 64
+        p = (np.arange(m * 64, dtype=np.int64).reshape(m, 64) + 0)
+        p = np.take_along_axis(p, np.argsort(r.random((m, 64)), axis=1), axis=1).reshape(-1)
+        return p[p < n]
+
+    perms = (leaf_scramble(L.base.n, 1), leaf_scramble(L.target.n, 2))
     fp = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, unsorted=perms,
                       late=not args.sort_gather, pk_order=not args.no_pk_order)
     for _ in range(max(1, args.warmup)):
@@ -480,7 +497,7 @@ def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
     eng.prof_enable(False)
     jp = kernel_times(eng, ("k_join2",))
     out = {"what": "the drop-in's fallback for sides whose walk order is not key order: each step sorts both "
-                   "(scrambled) sides on the GPU (kd_sort_side_into, onesweep LSD radix sort of the compacted varying "
+                   "sides (rows shuffled inside every 64-entry run, as a walk of leaf trees mixing pk wraps) on the GPU (kd_sort_side_into, onesweep LSD radix sort of the compacted varying "
                    "key bits, passes sized by the host kd_keys_scan) then classify2 + field diff + pk order; " +
                    ("the join reads the OIDs through the sort orders (kd_diff2_device_perm)" if fp.late else
                     "the OIDs are gathered into key order by the sort"),

@@ -223,7 +223,8 @@ int kd_env_overlap(kd_ctx* ctx, const uint8_t* enc, uint64_t n, int bits, const 
  * [m] (may be NULL = all are feature blobs: 1 when the object's path contains
  * "/.table-dataset/feature/" or "/.sno-dataset/feature/"), q = (w, s, e, n) of the filter;
  * result[i] = 0 MATCH (not a feature, not in the index, or the envelope overlaps), 1 NOT_MATCHED,
- * 2 ERROR (an inverted range: the reference aborts).  An inverted query latitude range is KD_EINVAL. */
+ * 2 ERROR (an inverted range reached by range_overlaps, per object as the reference decides it: a
+ * query with south > north errors only the objects whose longitude range overlaps). */
 typedef struct kd_sf_index kd_sf_index;
 int kd_sf_index_build(kd_ctx* ctx, const uint8_t* oid, const uint8_t* env, uint64_t n, int bits, uint32_t mem,
                       kd_sf_index** out);

@@ -190,8 +190,8 @@ int kd_sf_filter(kd_ctx* ctx, const kd_sf_index* ix, const uint8_t* oid, const u
                  const double q[4], uint8_t* result, uint32_t mem) {
     KD_CHECK(ctx && ix && q && result && (n == 0 || oid), "kd_sf_filter: NULL argument");
     KD_CHECK(ix->ctx == ctx, "kd_sf_filter: index built on another context");
-    // sf_init takes the rectangle as given; range_overlaps aborts on an inverted latitude range
-    KD_CHECK(q[1] <= q[3], "kd_sf_filter: query south %g > north %g", q[1], q[3]);
+    // sf_init takes the rectangle as given (an inverted latitude range included): range_overlaps
+    // rejects it per object, only for objects whose longitudes overlap (result 2, MR_ERROR)
     KD_HIP(hipSetDevice(ctx->device));
     if (n == 0) return KD_OK;
     int rc;

@@ -91,6 +91,30 @@ __device__ __forceinline__ u32 lanes_below(u64 m) {
     return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0));
 }
 
+// exclusive scan of one u32 per thread over the workgroup; *total <- the workgroup's sum
+template <int NT>
+__device__ __forceinline__ u32 block_scan_u32(u32 v, u32* s_wave, u32* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32 x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wv] = x;
+    __syncthreads();
+    u32 pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const u32 s = s_wave[w];
+        pre += w < wv ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
 // varying bits of the keys: OR of (key ^ key[0]) over all keys (16-B loads, four in flight per lane)
 __global__ __launch_bounds__(256) void k_rs_bits(const u64* __restrict__ key, u64 n, u64* __restrict__ out) {
     const u64 k0 = key[0];
@@ -426,6 +450,110 @@ __global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict
     __syncthreads();
     for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT)
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+// ---- deltas into pk order by bitmap placement (a bounded pk range) ----
+// Every pk occurs at most once in a record list, so the records of one 64-pk block [64b, 64b + 64)
+// are exactly the set bits of a 64-bit mask: a record's rank in pk order is the number of records
+// in earlier blocks (an exclusive scan of the masks' popcounts) plus the set bits below its own in
+// its block's mask.  Three streaming kernels instead of a radix sort's passes.
+//   k_pkm_mark   pk of each record (saved), its bit OR-ed into its block's mask: records of one
+//                leaf tree are adjacent in walk order, so a wave first ORs runs of equal blocks
+//                together (segmented shuffle reduction) and only each run's head lane does the atomic
+//   k_pkm_scan   per chunk of PKM_CH masks: the popcounts' exclusive prefix (u32) + the chunk total;
+//                the last workgroup to finish scans the chunk totals (one pass, no extra launch)
+//   k_pkm_place  record -> its rank: chunk prefix + in-chunk prefix + popcount(mask below its bit)
+constexpr int PKM_NT = 256, PKM_IPT = 8, PKM_CH = PKM_NT * PKM_IPT;
+
+__global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ rec, u64 ncap, const u64* __restrict__ dn,
+                                                     const u64* __restrict__ kA, const u64* __restrict__ kB, i64 lo_block,
+                                                     u64 nb, u64* __restrict__ masks, i64* __restrict__ pk_out) {
+    const u64 n = min(*dn, ncap);
+    const int lane = threadIdx.x & 63;
+    const u64 stride = (u64)gridDim.x * PKM_NT;
+    for (u64 base = (u64)blockIdx.x * PKM_NT + (threadIdx.x & ~63); base < n; base += stride) {
+        const u64 r = base + lane;
+        const bool ok = r < n;
+        i64 pk = 0;
+        if (ok) {
+            const uint2 d = rec[r];
+            pk = wk::int_key_pk(d.x != KD_NONE ? kA[d.x] : kB[d.y]);
+            pk_out[r] = pk;
+        }
+        const u64 b = (u64)((pk >> 6) - lo_block);
+        const bool inb = ok && b < nb;  // (a pk outside the caller's bounds is dropped, never written out of range)
+        u64 bit = inb ? 1ull << (pk & 63) : 0;
+        // runs of equal blocks among the wave's lanes: OR each run into its head lane
+        const u64 bprev = __shfl_up(b, 1, 64);
+        const bool head = inb && (lane == 0 || bprev != b);
+        const u64 heads = __ballot(head);
+        const u64 later = lane == 63 ? 0 : heads & (~0ull << (lane + 1));
+        const int seg_end = later ? __ffsll((long long)later) - 1 : 64;  // first lane of the next run
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u64 v = __shfl_down(bit, o, 64);
+            if (lane + o < seg_end) bit |= v;
+        }
+        if (head) atomicOr((unsigned long long*)(masks + b), (unsigned long long)bit);
+    }
+}
+
+__global__ __launch_bounds__(PKM_NT) void k_pkm_scan(const u64* __restrict__ masks, u64 nb, u32* __restrict__ local,
+                                                     u32* __restrict__ chunk_tot, u32* __restrict__ done_ctr,
+                                                     u32* __restrict__ chunk_pre) {
+    __shared__ u32 s_wave[PKM_NT / 64];
+    __shared__ u32 s_last;
+    const int tid = threadIdx.x;
+    const u64 c0 = (u64)blockIdx.x * PKM_CH + (u64)tid * PKM_IPT;
+    u32 cnt[PKM_IPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PKM_IPT; j++) {
+        cnt[j] = c0 + j < nb ? (u32)__popcll(masks[c0 + j]) : 0u;
+        sum += cnt[j];
+    }
+    u32 tot;
+    u32 ex = block_scan_u32<PKM_NT>(sum, s_wave, &tot);
+#pragma unroll
+    for (int j = 0; j < PKM_IPT; j++) {
+        if (c0 + j < nb) local[c0 + j] = ex;
+        ex += cnt[j];
+    }
+    if (tid == 0) {
+        chunk_tot[blockIdx.x] = tot;
+        __threadfence();
+        s_last = atomicAdd(done_ctr, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the last workgroup: exclusive scan of every chunk's total
+    __threadfence();
+    const u32 nch = gridDim.x;
+    u32 carry = 0;
+    for (u32 k0 = 0; k0 < nch; k0 += PKM_NT) {
+        const u32 k = k0 + tid;
+        const u32 v = k < nch ? __hip_atomic_load(chunk_tot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        u32 t2;
+        const u32 e = block_scan_u32<PKM_NT>(v, s_wave, &t2);
+        if (k < nch) chunk_pre[k] = carry + e;
+        carry += t2;
+    }
+    if (tid == 0) *done_ctr = 0;  // ready for the next call
+}
+
+__global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pks, u64 ncap, const u64* __restrict__ dn,
+                                                      i64 lo_block, u64 nb, const u64* __restrict__ masks,
+                                                      const u32* __restrict__ local, const u32* __restrict__ chunk_pre,
+                                                      i64* __restrict__ out_pk, u32* __restrict__ out_perm) {
+    const u64 n = min(*dn, ncap);
+    for (u64 r = (u64)blockIdx.x * PKM_NT + threadIdx.x; r < n; r += (u64)gridDim.x * PKM_NT) {
+        const i64 pk = pks[r];
+        const u64 b = (u64)((pk >> 6) - lo_block);
+        if (b >= nb) continue;
+        const u64 below = masks[b] & ((1ull << (pk & 63)) - 1);
+        const u32 pos = chunk_pre[b / PKM_CH] + local[b] + (u32)__popcll(below);
+        out_pk[pos] = pk;
+        out_perm[pos] = (u32)r;
+    }
 }
 
 // ---- segmented sort: keys ascending in their top bits (a hash side in walk order: the bucket)
@@ -787,6 +915,41 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
     if ((rc = device_zeros(ctx, &dz))) return rc;
     const u64* kA = base->n ? base->key : (const u64*)dz;
     const u64* kB = target->n ? target->key : (const u64*)dz;
+    // a bounded pk range: bitmap placement (one mask per 64-pk block)
+    const i64 lo_block = pk_lo >> 6, hi_block = pk_hi >> 6;
+    const u64 nb = (u64)hi_block - (u64)lo_block + 1;
+    static const u64 pkm_max = [] {
+        const char* e = getenv("KD_PKM_MAX_BLOCKS");  // tests force the radix path with 0
+        return e ? strtoull(e, nullptr, 10) : (u64)1 << 26;
+    }();
+    if (nb <= pkm_max && nb / PKM_CH < 0xFFFFFFFFull) {
+        void *masks, *local, *ctot, *cpre, *ctr, *tpk;
+        const u64 nch = (nb + PKM_CH - 1) / PKM_CH;
+        if ((rc = ensure(ctx, "pkm.masks", nb * 8, &masks))) return rc;
+        if ((rc = ensure(ctx, "pkm.local", nb * 4, &local))) return rc;
+        if ((rc = ensure(ctx, "pkm.ctot", nch * 4, &ctot))) return rc;
+        if ((rc = ensure(ctx, "pkm.cpre", nch * 4, &cpre))) return rc;
+        const bool fresh = ctx->bufs["pkm.ctr"].p == nullptr;
+        if ((rc = ensure(ctx, "pkm.ctr", 16, &ctr))) return rc;
+        if (fresh) KD_HIP(hipMemsetAsync(ctr, 0, 16, ctx->stream));
+        if ((rc = ensure(ctx, "pkm.pk", cap * 8, &tpk))) return rc;
+        KD_HIP(hipMemsetAsync(masks, 0, nb * 8, ctx->stream));
+        const unsigned g1 = (unsigned)std::max<u64>(1, std::min<u64>((cap + PKM_NT - 1) / PKM_NT, (u64)ctx->n_cu * 8));
+        rc = launch(ctx, "k_pkm_mark", [&] {
+            hipLaunchKernelGGL(k_pkm_mark, dim3(g1), dim3(PKM_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n, kA,
+                               kB, lo_block, nb, (u64*)masks, (i64*)tpk);
+        });
+        if (rc) return rc;
+        rc = launch(ctx, "k_pkm_scan", [&] {
+            hipLaunchKernelGGL(k_pkm_scan, dim3((unsigned)nch), dim3(PKM_NT), 0, ctx->stream, (const u64*)masks, nb,
+                               (u32*)local, (u32*)ctot, (u32*)ctr, (u32*)cpre);
+        });
+        if (rc) return rc;
+        return launch(ctx, "k_pkm_place", [&] {
+            hipLaunchKernelGGL(k_pkm_place, dim3(g1), dim3(PKM_NT), 0, ctx->stream, (const i64*)tpk, cap, d_n, lo_block,
+                               nb, (const u64*)masks, (const u32*)local, (const u32*)cpre, d_pk, d_perm);
+        });
+    }
     SortPlan plan = pk_plan(pk_lo, pk_hi);
     int npass, width;
     plan_passes(plan, &npass, &width);

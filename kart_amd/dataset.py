@@ -228,9 +228,12 @@ class DatasetVersion:
         self._remember_arena(idx, data, off)
         return data, off
 
+    ARENAS_KEPT = 2  # the latest batched reads (a field diff reads both sides once): a bounded cache
+
     def _remember_arena(self, idx, data, off):
         order = np.argsort(idx, kind="stable")
         self._arenas.append((idx[order], order, data, off))
+        del self._arenas[:-self.ARENAS_KEPT]
 
     def cached_blob(self, i):
         """leaf i's bytes from an arena blob_arena_leaves read, or None"""

@@ -89,17 +89,39 @@ class ObjectDB:
         self.n_opens = 0
         self.reopen()
 
-    def _pack_signature(self):
-        """what a reopen would see differently: the pack directory's files and the alternates"""
-        sig = []
-        for rel in ("objects/pack", "objects/info/alternates"):
-            path = os.path.join(self.gitdir, rel)
-            try:
-                st = os.stat(path)
-            except OSError:
-                sig.append(None)
+    def _alternate_dirs(self):
+        """objects directories named by objects/info/alternates (recursively, as git follows them)"""
+        out, todo, seen = [], [os.path.join(self.gitdir, "objects")], set()
+        while todo:
+            d = os.path.realpath(todo.pop())
+            if d in seen:
                 continue
-            sig.append((st.st_mtime_ns, st.st_size, tuple(sorted(os.listdir(path))) if os.path.isdir(path) else ()))
+            seen.add(d)
+            out.append(d)
+            try:
+                with open(os.path.join(d, "info", "alternates")) as f:
+                    for line in f:
+                        line = line.strip()
+                        if line and not line.startswith("#"):
+                            todo.append(line if os.path.isabs(line) else os.path.join(d, line))
+            except OSError:
+                pass
+        return out
+
+    def _pack_signature(self):
+        """what a reopen would see differently: every objects directory's pack files (this repository's
+        and each alternate's) and the alternates files themselves"""
+        sig = []
+        for d in self._alternate_dirs():
+            for rel in ("pack", "info/alternates"):
+                path = os.path.join(d, rel)
+                try:
+                    st = os.stat(path)
+                except OSError:
+                    sig.append((path, None))
+                    continue
+                sig.append((path, st.st_mtime_ns, st.st_size,
+                            tuple(sorted(os.listdir(path))) if os.path.isdir(path) else ()))
         return tuple(sig)
 
     def reopen(self):

@@ -304,13 +304,23 @@ FEATURE_PATH_MARKERS = ("/.sno-dataset/feature/", "/.table-dataset/feature/")
 SF_MATCH, SF_NOT_MATCHED, SF_ERROR = 0, 1, 2  # spatial_filter.cpp:154-158 (enum match_result)
 
 
+_NUM = re.compile(r"\s*([+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?)")
+
+
 def parse_filter_arg(filter_arg):
-    """sf_init's bounds argument (spatial_filter.cpp:268-285): '<w>,<s>,<e>,<n>' -> 4 floats"""
-    parts = [p for p in str(filter_arg).replace(",", " ").split()]
-    try:
-        rect = [float(p) for p in parts]
-    except ValueError:
-        rect = []
+    """sf_init's bounds argument (spatial_filter.cpp:266-285): `while (ss >> d) { push(d); if (peek
+    == ',') ignore(); }` — numbers with optional leading whitespace, each optionally followed by one
+    comma; the first thing that is not a number ends the list (trailing text is ignored); exactly
+    four numbers -> (w, s, e, n), else the reference's error."""
+    text, pos, rect = str(filter_arg), 0, []
+    while True:
+        m = _NUM.match(text, pos)
+        if m is None:
+            break
+        rect.append(float(m.group(1)))
+        pos = m.end()
+        if text[pos:pos + 1] == ",":
+            pos += 1
     if len(rect) != 4:
         raise ValueError("spatial-filter: Error: invalid bounds, expected '<lng_w>,<lat_s>,<lng_e>,<lat_n>'")
     return tuple(rect)

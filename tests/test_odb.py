@@ -324,6 +324,32 @@ def test_refresh_only_when_packs_change(tmp_path):
         r.close()
 
 
+def test_refresh_sees_packs_added_to_an_alternate(tmp_path):
+    """a pack written into an alternate object directory after the open changes the signature, so the
+    next miss reopens and finds the object (alternates' pack dirs were not watched)"""
+    from kart_amd.gitsource import GitRepo
+
+    alt = str(tmp_path / "alt.git")
+    subprocess.run(["git", "init", "-q", "--bare", alt], check=True)
+    _fast_import(alt, [("a", {"x/one": b"one"})])
+    gitdir = str(tmp_path / "main.git")
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    with open(os.path.join(gitdir, "objects", "info", "alternates"), "w") as f:
+        f.write(os.path.join(alt, "objects") + "\n")
+    r = GitRepo(gitdir)
+    try:
+        h = r.odb.n_opens
+        sig = r.odb._pack_signature()
+        _fast_import(alt, [("b", {"x/two": b"two, in the alternate's new pack"})])
+        _git(alt, "repack", "-adq")
+        assert r.odb._pack_signature() != sig
+        oid = _git(alt, "rev-parse", "b:x/two").decode().strip()
+        assert r.cat(oid) == b"two, in the alternate's new pack"
+        assert r.odb.n_opens == h + 1
+    finally:
+        r.close()
+
+
 def test_batch_reads_across_several_packs(tmp_path):
     """three fast-imports = three packs (each with its own delta chains): a shuffled batch over all
     of them, read in (pack, offset) order and stitched back, equals git cat-file object by object"""

@@ -122,7 +122,7 @@ def test_oracle_sf_filter_equals_reference_restatement():
     rng = np.random.default_rng(5)
     idx, env, qo, feat = _synthetic(rng, 3000, 5000)
     index = {bytes(o): bytes(e) for o, e in zip(idx, env)}
-    for q in QUERIES:
+    for q in QUERIES + [(170.0, -30.0, 180.0, -45.0)]:
         got = O.sf_filter_batch(idx, env, 20, qo, feat, q)
         want = [py_sf_filter_blob(index, o, f, q, 20) for o, f in zip(qo, feat)]
         assert got.tolist() == want
@@ -134,9 +134,16 @@ def test_oracle_sf_filter_equals_reference_restatement():
 
 
 def test_parse_filter_arg():
+    """std::istream >> double with one optional ',' after each number (sf_init, spatial_filter.cpp:
+    271-280): whitespace before a number is skipped, the first non-number ends the list"""
     assert SI.parse_filter_arg("174.5,-41.5,175,-41") == (174.5, -41.5, 175.0, -41.0)
     assert SI.parse_filter_arg("1 2 3 4") == (1.0, 2.0, 3.0, 4.0)
-    for bad in ("1,2,3", "1,2,3,4,5", "a,b,c,d", ""):
+    assert SI.parse_filter_arg("1, 2, 3, 4") == (1.0, 2.0, 3.0, 4.0)  # >> skips the space after the comma
+    assert SI.parse_filter_arg("1,2,3,4,garbage") == (1.0, 2.0, 3.0, 4.0)  # trailing text ignored
+    assert SI.parse_filter_arg("1,2,3,4xyz") == (1.0, 2.0, 3.0, 4.0)
+    assert SI.parse_filter_arg("+1e1,-.5,3.,4E-1") == (10.0, -0.5, 3.0, 0.4)
+    for bad in ("1,2,3", "1,2,3,4,5", "a,b,c,d", "", "nan,1,2,3", "1_0,2,3,4", "1,,2,3,4", "inf,0,1,1",
+                "0x1,2,3,4", "1 ,2,3,4"):
         with pytest.raises(ValueError):
             SI.parse_filter_arg(bad)
     assert SI.CloneFilter.feature_paths(["nz/.table-dataset/feature/A/A/A/A/kQ==", "nz/.table-dataset/meta/schema.json",
@@ -156,13 +163,17 @@ def test_gpu_sf_filter_vs_oracle(engine, tmp_path, n_idx, m):
     con.executemany("INSERT INTO feature_envelopes VALUES (?, ?);", ((o.tobytes(), e.tobytes()) for o, e in zip(idx, env)))
     con.commit()
     con.close()
-    for q in QUERIES[:3]:
+    # (the last query has south > north: the reference's range_overlaps rejects it for exactly the
+    # objects whose longitudes overlap: MR_ERROR per object, the rest decided as usual)
+    for q in QUERIES[:3] + [(170.0, -30.0, 180.0, -45.0)]:
         with SI.CloneFilter(engine, db, ",".join(map(str, q))) as cf:
             assert cf.n_index == idx.shape[0] and cf.bits == 20
             got = cf.filter(qo, is_feature=feat)
             want = O.sf_filter_batch(idx, env, 20, qo, feat, q)
             assert np.array_equal(got, want)
             assert 0 < np.count_nonzero(got == 1) < m or n_idx == 1
+            if q[1] > q[3]:
+                assert (got == 2).any() or n_idx == 1
             assert np.array_equal(cf.filter(qo), O.sf_filter_batch(idx, env, 20, qo, None, q))
     # no index database: nothing is omitted (sf_init's warning path)
     cf = SI.CloneFilter(engine, str(tmp_path / "absent.db"), "0,0,1,1")
