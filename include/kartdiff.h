@@ -167,6 +167,14 @@ int kd_diff2_device_perm(kd_ctx* ctx, const kd_side* base, const kd_side* target
                          const uint32_t* target_order, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
                          uint64_t* d_counts, uint32_t* d_err);
 
+/* kd_diff2_device / kd_diff2_device_perm with more outputs: base_order / target_order (both or
+ * NULL) as kd_diff2_device_perm; d_delta_key [cap] / d_upd_key [cap] (optional, device) <- the join key
+ * of every delta / update record, written beside the lists (what kd_delta_pk_order reads instead of
+ * gathering them from the sides). */
+int kd_diff2_device_ex(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* base_order,
+                       const uint32_t* target_order, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
+                       uint64_t* d_delta_key, uint64_t* d_upd_key, uint64_t* d_counts, uint32_t* d_err);
+
 /* -------- field diff -------- */
 /* For each update u: old blob = old->data[old->off[pu[2u]] ..], new blob = neu->...[pu[2u+1]]
  * (pu = the (base, target) update pairs, or NULL: blob u on both sides).  masks[u*words + w]
@@ -334,13 +342,16 @@ int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oi
 int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uint64_t* d_key_out, uint32_t* d_order,
                            uint64_t n, int seg_bits, uint32_t* d_err);
 /* The deltas in pk order (DeltaDiff.sorted_items, kart/diff_structs.py:442-458; classify2 emits them in
- * git walk order): for KD_KEY_INT device sides and a device delta list d_delta [cap] of (base | KD_NONE,
+ * git walk order): for KD_KEY_INT device sides and a device record list d_delta [cap] of (base | KD_NONE,
  * target | KD_NONE) records (classify2's deltas or updates) with *d_n of them, d_pk [cap] <- their pks
- * ascending, d_perm [cap] <- the record index of pk rank k.  pk_lo / pk_hi bound every pk of both sides
- * (kd_keys_scan's pk_min / pk_max): they size the radix passes, no read-back.  Stable, asynchronous. */
+ * ascending, d_perm [cap] <- the record index of pk rank k.  d_keys (optional, device): the records'
+ * keys as kd_diff2_device_ex wrote them (else each is gathered from the sides).  pk_lo / pk_hi bound
+ * every pk of both sides (kd_keys_scan's pk_min / pk_max): a range of at most 2^26 64-pk blocks is
+ * placed through a bitmap (one mask per block: every pk occurs once), a wider one radix-sorted with
+ * passes sized by the range — no read-back either way.  Stable, asynchronous. */
 int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* d_delta,
-                      uint64_t cap, const uint64_t* d_n, int64_t pk_lo, int64_t pk_hi, int64_t* d_pk,
-                      uint32_t* d_perm);
+                      const uint64_t* d_keys, uint64_t cap, const uint64_t* d_n, int64_t pk_lo, int64_t pk_hi,
+                      int64_t* d_pk, uint32_t* d_perm);
 
 /* -------- device memory and copies (no GPU framework needed by the caller) -------- */
 #define KD_COPY_H2D 1u

@@ -238,8 +238,12 @@ SIGNATURES = {
     "kd_sort_segmented_into": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
     "kd_delta_pk_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
-                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64,
-                                          ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "kd_diff2_device_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
     "kd_malloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "kd_mfree": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "kd_host_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),

@@ -436,6 +436,24 @@ int kd_diff2_device_perm(kd_ctx* ctx, const kd_side* base, const kd_side* target
                         base_order ? base_order : (const u32*)nullptr, target_order);
 }
 
+int kd_diff2_device_ex(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* base_order,
+                       const uint32_t* target_order, uint32_t flags, uint32_t* d_delta, uint32_t* d_upd,
+                       uint64_t* d_delta_key, uint64_t* d_upd_key, uint64_t* d_counts, uint32_t* d_err) {
+    KD_CHECK(ctx, "kd_diff2_device_ex: ctx NULL");
+    int rc;
+    if ((rc = check_side(base, "base")) || (rc = check_side(target, "target"))) return rc;
+    KD_CHECK(base->mem == KD_MEM_DEVICE && target->mem == KD_MEM_DEVICE, "kd_diff2_device_ex: sides must be device memory");
+    KD_CHECK(d_delta && d_counts && d_err, "kd_diff2_device_ex: NULL output");
+    KD_CHECK(!base_order == !target_order, "kd_diff2_device_ex: both orders or neither");
+    KD_CHECK(!d_upd_key || (d_upd && d_delta_key), "kd_diff2_device_ex: update keys need the update list and delta keys");
+    KD_HIP(hipSetDevice(ctx->device));
+    void* dz = nullptr;
+    if (base_order && (rc = device_zeros(ctx, &dz))) return rc;
+    const u32* oa = base_order ? (base->n ? base_order : (const u32*)dz) : nullptr;
+    const u32* ob = target_order ? (target->n ? target_order : (const u32*)dz) : nullptr;
+    return diff2_device(ctx, base, target, flags, d_delta, d_upd, d_counts, d_err, oa, ob, d_delta_key, d_upd_key);
+}
+
 int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t flags, kd_diff_result** out) {
     KD_CHECK(ctx && out, "kd_diff2: NULL");
     int rc;

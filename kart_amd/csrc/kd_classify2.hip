@@ -28,6 +28,12 @@ constexpr u64 C2_GROUP = 64;  // tiles per group sum (staged path: k_place2 offs
 // staging slot stride in records: one tile plus a pad, so the slots' hot first lines do not all
 // fall on the same HBM channels (a power-of-two stride would)
 constexpr u64 C2_STAGE = C2_TILE + KD_C2_STAGE_PAD;
+// PERM + KD_KEY_HASH: name rows staged beyond the tile's sorted range on each side (a per-bucket sort
+// moves an entry less than its bucket's length)
+#ifndef KD_J2_NAME_HALO
+#define KD_J2_NAME_HALO 64
+#endif
+constexpr u64 J2_NAME_HALO = KD_J2_NAME_HALO;
 #ifndef KD_PLACE_NT
 #define KD_PLACE_NT 64  // one wave per tile: up to 16 staged records per lane, all loads in flight
 #endif
@@ -153,6 +159,10 @@ struct Join2Args {
     u64* gsum;           // staged path: [2*ngroups] deltas | updates<<32, inserts | deletes<<32
     uint2* out_delta;    // final lists
     uint2* out_upd;
+    u64* stage_dkey;     // (optional) the join key of every staged delta / update record
+    u64* stage_ukey;
+    u64* out_dkey;       // (optional) the key of every delta / update, beside the final lists
+    u64* out_ukey;
     u64* counts;         // [4] inserts, updates, deletes, deltas
     u32* err;
     u64 ntiles;
@@ -324,16 +334,13 @@ __device__ __forceinline__ void tile_walk(const u64* sA, const u64* sB, const Ti
     }
 }
 
-// OID compare straight from HBM (keys-only LDS image): each thread loads the two 20-B OIDs of its own
-// matched pairs (consecutive items -> neighbouring entries across lanes), all loads issued before any
-// compare.  PERM (late materialisation after kd_sort_side_into without OIDs): the OIDs stay in the
-// order the walk produced them and sorted entry i's row is ord[i] — one more (coalesced) load round
-// trip instead of a 44-B-per-entry OID gather per side.  ra / rb <- the rows of the matched pairs.
+// Rows of the tile's matched pairs in the OID (and filename-offset) arrays: the sorted indices, or
+// (PERM: late materialisation after kd_sort_side_into / kd_sort_segmented_into without OIDs) the walk
+// rows ord[i] — one more (coalesced) load round trip instead of a 44-B-per-entry OID gather per side.
 template <int IPT, bool PERM>
-__device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGeo& q, u32 rec[IPT], u32 ra[IPT],
-                                                u32 rb[IPT]) {
+__device__ __forceinline__ void tile_rows(const Join2Args& g, const TileGeo& q, const u32 rec[IPT], u32 ra[IPT],
+                                          u32 rb[IPT]) {
     typedef const __attribute__((address_space(1))) u32* gp32;
-    u32 x[IPT][5], y[IPT][5];
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
         ra[k] = (u32)q.i0 + (rec[k] & 0xFFF);
@@ -349,6 +356,15 @@ __device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGe
             rb[k] = *ob;
         }
     }
+}
+
+// OID compare straight from HBM (keys-only LDS image): each thread loads the two 20-B OIDs of its own
+// matched pairs (consecutive items -> neighbouring entries across lanes), all loads issued before any
+// compare.
+template <int IPT>
+__device__ __forceinline__ void tile_oid_cmp(const Join2Args& g, u32 rec[IPT], const u32 ra[IPT], const u32 rb[IPT]) {
+    typedef const __attribute__((address_space(1))) u32* gp32;
+    u32 x[IPT][5], y[IPT][5];
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
         const bool m = (rec[k] >> 25) == R_MATCH;
@@ -364,6 +380,13 @@ __device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGe
         for (int w = 0; w < 5; w++) d |= x[k][w] ^ y[k][w];
         if ((rec[k] >> 25) == R_MATCH && d) rec[k] |= 1u << 24;
     }
+}
+
+template <int IPT, bool PERM>
+__device__ __forceinline__ void tile_oid_global(const Join2Args& g, const TileGeo& q, u32 rec[IPT], u32 ra[IPT],
+                                                u32 rb[IPT]) {
+    tile_rows<IPT, PERM>(g, q, rec, ra, rb);
+    tile_oid_cmp<IPT>(g, rec, ra, rb);
 }
 
 // KD_KEY_HASH: a matched key must also match the full filename (a 64-bit key collision between two
@@ -427,15 +450,22 @@ __device__ __forceinline__ TileCounts tile_counts(const u32 rec[IPT], u32* s_wav
 
 template <int IPT>
 __device__ __forceinline__ void tile_write(const u32 rec[IPT], const TileCounts& c, u64 i0, u64 j0,
-                                           uint2* __restrict__ sd, uint2* __restrict__ su) {
+                                           uint2* __restrict__ sd, uint2* __restrict__ su, const u64* sA, const u64* sB,
+                                           u64* __restrict__ kd, u64* __restrict__ ku) {
     u32 od = c.od, ou = c.ou;
     const u32 has_su = su != nullptr;
+    const bool keys = kd != nullptr;  // (uniform)
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
         const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
         const u32 isd = (c.fd >> k) & 1, isu = (c.fu >> k) & 1;
         const uint2 v = make_uint2(kind == R_INS ? KD_NONE : (u32)(i0 + ia), kind == R_DEL ? KD_NONE : (u32)(j0 + jb));
         if (isd) sd[od] = v;
+        if (keys && isd) {  // the record's key, from the tile's LDS image
+            const u64 key = kind == R_INS ? sB[jb] : sA[ia];
+            kd[od] = key;
+            if ((isu & has_su) && ku) ku[ou] = key;
+        }
         od += isd;
         if (isu & has_su) su[ou] = v;
         ou += isu;
@@ -453,8 +483,11 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // (HASH: filename checks compiled in; the int-key instantiation carries none of their registers)
     using LD = Join2Lds<NT, IPT>;
     static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
-    // filenames of matched pairs compared from LDS (KD_KEY_HASH, sorted-order name arenas)
-    constexpr bool LNAMES = HASH && !PERM;
+    // filenames of matched pairs compared from LDS (KD_KEY_HASH).  PERM: the name arenas are in walk
+    // order, and a per-bucket sort (kd_sort_segmented_into) moves an entry at most a bucket's length:
+    // the staged rows are the tile's sorted range widened by J2_NAME_HALO on each side, and a pair whose
+    // walk row falls outside them (a long bucket, or a full sort's order) is compared in HBM
+    constexpr bool LNAMES = HASH;
     // OL (large int-key joins): the tile's OIDs by LDS-DMA with the keys, so the matched pairs
     // compare from LDS with no global round trip after the walk (20.6 KB more LDS: 5 blocks per CU
     // instead of 8, which costs more than it saves on small joins)
@@ -472,9 +505,14 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // the tile's filename byte ranges: A [off[i0], off[i1]), B [off[j0], off[j1e]) (the lookahead
     // entry's name too: a match may pair with it) — loaded with the key DMA
     u64 nmA0 = 0, nmA1 = 0, nmB0 = 0, nmB1 = 0;
+    // staged name rows [rA0, rA1) / [rB0, rB1)
+    const u64 rA0 = PERM ? (q.i0 > J2_NAME_HALO ? q.i0 - J2_NAME_HALO : 0) : q.i0;
+    const u64 rA1 = PERM ? min(q.i1 + J2_NAME_HALO, g.nA) : q.i1;
+    const u64 rB0 = PERM ? (q.j0 > J2_NAME_HALO ? q.j0 - J2_NAME_HALO : 0) : q.j0;
+    const u64 rB1 = PERM ? min(q.j1e + J2_NAME_HALO, g.nB) : q.j1e;
     if (LNAMES) {
-        nmA0 = g.nameOffA[q.i0]; nmA1 = g.nameOffA[q.i1];
-        nmB0 = g.nameOffB[q.j0]; nmB1 = g.nameOffB[q.j1e];
+        nmA0 = g.nameOffA[rA0]; nmA1 = g.nameOffA[rA1];
+        nmB0 = g.nameOffB[rB0]; nmB1 = g.nameOffB[rB1];
     }
     // 64-chunk pieces (one wave-instruction each: wave-uniform source base and LDS base, lane l takes
     // chunk 64p + l), dealt round-robin to the waves across the two ranges: scalar address math
@@ -527,13 +565,14 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     // the matched pairs' name offsets, issued with the OID loads: low words only (differences of
     // offsets inside one tile's names fit 32 bits, and modular arithmetic gives them exactly)
     u32 oa0[IPT], oa1[IPT], ob0[IPT], ob1[IPT];
+    if (!LOIDS) tile_rows<IPT, PERM>(g, q, rec, ra, rb);
     if (LNAMES && lnames) {
         const u32* offA = (const u32*)g.nameOffA;
         const u32* offB = (const u32*)g.nameOffB;
 #pragma unroll
         for (int k = 0; k < IPT; k++) {
             const bool m = (rec[k] >> 25) == R_MATCH;
-            const u64 i = q.i0 + (m ? (rec[k] & 0xFFF) : 0), j = q.j0 + (m ? ((rec[k] >> 12) & 0xFFF) : 0);
+            const u64 i = m ? ra[k] : rA0, j = m ? rb[k] : rB0;
             oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
             ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
         }
@@ -552,7 +591,7 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
             if (m && d) rec[k] |= 1u << 24;
         }
     } else {
-        tile_oid_global<IPT, PERM>(g, q, rec, ra, rb);
+        tile_oid_cmp<IPT>(g, rec, ra, rb);
     }
     if (LNAMES && lnames) {
         __syncthreads();  // vmcnt(0) + barrier: every wave's share of the names DMA has landed
@@ -563,7 +602,10 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         for (int k = 0; k < IPT; k++) {
             if ((rec[k] >> 25) != R_MATCH) continue;
             const u32 la = oa1[k] - oa0[k], lb = ob1[k] - ob0[k];
-            ne |= la != lb || !lds_eq_bytes(baseA + (oa0[k] - (u32)nmA0), baseB + (ob0[k] - (u32)nmB0), la);
+            if (PERM && (ra[k] < rA0 || ra[k] >= rA1 || rb[k] < rB0 || rb[k] >= rB1))  // a row outside the staged names
+                ne |= !names_eq(g.nameA, g.nameOffA, ra[k], g.nameB, g.nameOffB, rb[k]);
+            else
+                ne |= la != lb || !lds_eq_bytes(baseA + (oa0[k] - (u32)nmA0), baseB + (ob0[k] - (u32)nmB0), la);
         }
         if (ne) atomicOr(g.err, 2u);
     } else if (HASH) {
@@ -572,6 +614,7 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
     if (bad) atomicOr(g.err, 1u);
     const TileCounts c = tile_counts<NT, IPT>(rec, s_wave);
     uint2 *sd, *su;
+    u64 *kd, *ku;
     if (UNORD) {
         // four lanes of wave 0 reserve in parallel: deltas, updates (offsets) + inserts, deletes
         if (tid < 4) {
@@ -583,11 +626,15 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         __syncthreads();
         sd = g.out_delta + s_base[0];
         su = g.out_upd ? g.out_upd + s_base[1] : nullptr;
+        kd = g.out_dkey ? g.out_dkey + s_base[0] : nullptr;
+        ku = g.out_dkey && g.out_upd ? g.out_ukey + s_base[1] : nullptr;
     } else {
         sd = g.stage_delta + tile * (u64)C2_STAGE;
         su = g.stage_upd + tile * (u64)C2_STAGE;
+        kd = g.stage_dkey ? g.stage_dkey + tile * (u64)C2_STAGE : nullptr;
+        ku = g.stage_dkey ? g.stage_ukey + tile * (u64)C2_STAGE : nullptr;
     }
-    tile_write<IPT>(rec, c, q.i0, q.j0, sd, su);
+    tile_write<IPT>(rec, c, q.i0, q.j0, sd, su, sA, sB, kd, ku);
     if (!UNORD && tid == 0) {
         u32* cc = g.tile_cnt + 4 * tile;
         const u32 tins = c.tnd - c.tnu - c.tdel;
@@ -656,7 +703,9 @@ __global__ __launch_bounds__(1024) void k_gscan2(const u64* __restrict__ gsum, u
 template <int NT>
 __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_delta, const uint2* __restrict__ stage_upd,
                                                const u32* __restrict__ tile_cnt, const u64* __restrict__ gpre,
-                                               int tile_items, uint2* __restrict__ out_delta, uint2* __restrict__ out_upd) {
+                                               int tile_items, uint2* __restrict__ out_delta, uint2* __restrict__ out_upd,
+                                               const u64* __restrict__ stage_dkey, const u64* __restrict__ stage_ukey,
+                                               u64* __restrict__ out_dkey, u64* __restrict__ out_ukey) {
     static_assert(NT == 64, "k_place2: one wave per tile");
     const int tid = threadIdx.x;
     const u64 t = blockIdx.x;
@@ -708,10 +757,17 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
             if (r < own.y) out_upd[pu + r] = v[j];
         }
     }
+    if (out_dkey) {  // the records' keys, when the caller asked for them
+        const u64* skd = stage_dkey + t * (u64)tile_items;
+        const u64* sku = stage_ukey + t * (u64)tile_items;
+        for (u32 r = tid; r < own.x; r += NT) out_dkey[pd + r] = skd[r];
+        if (out_upd)
+            for (u32 r = tid; r < own.y; r += NT) out_ukey[pu + r] = sku[r];
+    }
 }
 
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
-                 u64* d_counts, u32* d_err, const u32* ordA, const u32* ordB) {
+                 u64* d_counts, u32* d_err, const u32* ordA, const u32* ordB, u64* d_dkey, u64* d_ukey) {
     const bool unord = (flags & KD_DIFF_UNORDERED) != 0;
     const u64 nA = A->n, nB = B->n, total = nA + nB;
     KD_CHECK(nA < 0xFFFFFFFFull && nB < 0xFFFFFFFFull, "diff2: side too large for uint32 indices");
@@ -738,6 +794,11 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         if ((rc = ensure(ctx, "c2.sdel", ntiles * C2_STAGE * sizeof(uint2), &sdel))) return rc;
         if ((rc = ensure(ctx, "c2.supd", ntiles * C2_STAGE * sizeof(uint2), &supd))) return rc;
         zero = (u64*)gsum;
+    }
+    void *skd = nullptr, *sku = nullptr;
+    if (d_dkey && !unord) {
+        if ((rc = ensure(ctx, "c2.skd", ntiles * C2_STAGE * sizeof(u64), &skd))) return rc;
+        if ((rc = ensure(ctx, "c2.sku", ntiles * C2_STAGE * sizeof(u64), &sku))) return rc;
     }
     void* dz;
     if ((rc = device_zeros(ctx, &dz))) return rc;
@@ -775,6 +836,8 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
     g.tile_cnt = (u32*)tcnt; g.gsum = (u64*)gsum; g.err = d_err;
     g.out_delta = (uint2*)d_delta; g.out_upd = (uint2*)d_upd; g.counts = d_counts;
+    g.stage_dkey = (u64*)skd; g.stage_ukey = (u64*)sku;
+    g.out_dkey = d_dkey; g.out_ukey = d_upd ? d_ukey : nullptr;
     g.ntiles = ntiles;
     rc = launch(ctx, "k_join2", [&] {
 #define KD_J2(U, H, P) hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, U, H, P>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g)
@@ -800,7 +863,8 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     return launch(ctx, "k_place2", [&] {
         hipLaunchKernelGGL((k_place2<KD_PLACE_NT>), dim3((unsigned)ntiles), dim3(KD_PLACE_NT), 0, ctx->stream,
                            (const uint2*)sdel, (const uint2*)supd, (const u32*)tcnt, (const u64*)gpre,
-                           (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd);
+                           (int)C2_STAGE, (uint2*)d_delta, (uint2*)d_upd, (const u64*)skd, (const u64*)sku, d_dkey,
+                           d_upd ? d_ukey : nullptr);
     });
 }
 

@@ -137,8 +137,10 @@ void comm_release(kd_ctx* ctx);
 // ---- classify2 (device form), kd_classify.hip ----
 // ordA / ordB (both or neither): the sides' OIDs and filename offsets are in another order, row
 // ord[i] belongs to sorted entry i (kd_diff2_device_perm)
+// d_dkey / d_ukey (optional): the join key of every delta / update record, beside the lists
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
-                 u32* d_upd, u64* d_counts, u32* d_err, const u32* ordA = nullptr, const u32* ordB = nullptr);
+                 u32* d_upd, u64* d_counts, u32* d_err, const u32* ordA = nullptr, const u32* ordB = nullptr,
+                 u64* d_dkey = nullptr, u64* d_ukey = nullptr);
 #ifndef KD_C2_NT
 #define KD_C2_NT 256
 #endif

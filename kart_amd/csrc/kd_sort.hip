@@ -431,6 +431,7 @@ __global__ __launch_bounds__(256) void k_check_sorted(const u64* __restrict__ ke
 template <typename CK>
 __global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict__ rec, u64 ncap, const u64* __restrict__ dn,
                                                           const u64* __restrict__ kA, const u64* __restrict__ kB,
+                                                          const u64* __restrict__ rkey,
                                                           int npass, int width, SortPlan plan, CK* __restrict__ out,
                                                           u32* __restrict__ hist) {
     __shared__ u32 s_h[8 * RS_RD];
@@ -440,8 +441,12 @@ __global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict
     const u64 n = min(*dn, ncap);
     const u32 dmask = (1u << width) - 1;
     for (u64 r = (u64)blockIdx.x * RS_HIST_NT + tid; r < n; r += (u64)gridDim.x * RS_HIST_NT) {
-        const uint2 d = rec[r];
-        const u64 key = d.x != KD_NONE ? kA[d.x] : kB[d.y];
+        u64 key;
+        if (rkey) key = rkey[r];  // the join wrote the records' keys beside them
+        else {
+            const uint2 d = rec[r];
+            key = d.x != KD_NONE ? kA[d.x] : kB[d.y];
+        }
         const u64 sk = (u64)wk::int_key_pk(key) ^ (1ull << 63);
         const CK c = rs_compact<CK>(sk, plan);
         out[r] = c;
@@ -466,8 +471,9 @@ __global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict
 constexpr int PKM_NT = 256, PKM_IPT = 8, PKM_CH = PKM_NT * PKM_IPT;
 
 __global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ rec, u64 ncap, const u64* __restrict__ dn,
-                                                     const u64* __restrict__ kA, const u64* __restrict__ kB, i64 lo_block,
-                                                     u64 nb, u64* __restrict__ masks, i64* __restrict__ pk_out) {
+                                                     const u64* __restrict__ kA, const u64* __restrict__ kB,
+                                                     const u64* __restrict__ rkey, i64 lo_block, u64 nb,
+                                                     u64* __restrict__ masks, i64* __restrict__ pk_out) {
     const u64 n = min(*dn, ncap);
     const int lane = threadIdx.x & 63;
     const u64 stride = (u64)gridDim.x * PKM_NT;
@@ -476,8 +482,13 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ r
         const bool ok = r < n;
         i64 pk = 0;
         if (ok) {
-            const uint2 d = rec[r];
-            pk = wk::int_key_pk(d.x != KD_NONE ? kA[d.x] : kB[d.y]);
+            u64 key;
+            if (rkey) key = rkey[r];  // the join wrote the records' keys beside them
+            else {
+                const uint2 d = rec[r];
+                key = d.x != KD_NONE ? kA[d.x] : kB[d.y];
+            }
+            pk = wk::int_key_pk(key);
             pk_out[r] = pk;
         }
         const u64 b = (u64)((pk >> 6) - lo_block);
@@ -557,37 +568,74 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pk
 }
 
 // ---- segmented sort: keys ascending in their top bits (a hash side in walk order: the bucket)
-// ordered by the whole key inside each run of equal top bits.  One thread per entry: its rank among
-// its segment's keys (the segment scanned from global memory; segments average a few entries) is its
-// place.  err |= 1: a duplicate key or descending top bits; 4: a segment longer than RS_SEG_MAX (the
-// caller sorts with kd_sort_side_into instead).
+// ordered by the whole key inside each run of equal top bits.  One workgroup per tile of SEG_T
+// entries: the tile's keys plus SEG_H on each side go to LDS in one coalesced pass; each entry's
+// place = the start of its segment + the number of smaller keys in it, both found by scanning its
+// neighbours in LDS (segments average a few entries).  A segment reaching past the halo is scanned
+// in global memory instead.  err |= 1: a duplicate key or descending top bits; 4: a segment longer
+// than RS_SEG_MAX (the caller sorts with kd_sort_side_into instead).
 constexpr int RS_SEG_MAX = 512;
-__global__ __launch_bounds__(256) void k_seg_sort(const u64* __restrict__ key, u64 n, int shift, u64* __restrict__ kout,
-                                                  u32* __restrict__ order, u32* __restrict__ err) {
+constexpr int SEG_NT = 256, SEG_IPT = 8, SEG_T = SEG_NT * SEG_IPT, SEG_H = 64;
+__global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key, u64 n, int shift, u64* __restrict__ kout,
+                                                     u32* __restrict__ order, u32* __restrict__ err) {
+    __shared__ u64 s_k[SEG_T + 2 * SEG_H];
+    const int tid = threadIdx.x;
+    const u64 t0 = (u64)blockIdx.x * SEG_T;
+    const i64 g0 = (i64)t0 - SEG_H;  // global index of s_k[0]
+    const u64 glo = t0 >= (u64)SEG_H ? t0 - SEG_H : 0, ghi = min<u64>(n, t0 + SEG_T + SEG_H);
+    for (int x = tid; x < SEG_T + 2 * SEG_H; x += SEG_NT) {
+        const i64 g = g0 + x;
+        s_k[x] = (g >= 0 && (u64)g < n) ? key[g] : 0;
+    }
+    __syncthreads();
     u32 bad = 0;
-    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
-        const u64 k = key[i], seg = k >> shift;
-        u32 rank = 0, left = 0;
-        u64 j = i;
-        while (j > 0 && left < RS_SEG_MAX) {  // earlier entries of the segment
-            const u64 x = key[j - 1];
-            if ((x >> shift) != seg) {
-                bad |= (x >> shift) > seg ? 1u : 0u;
-                break;
+#pragma unroll 2
+    for (int j = 0; j < SEG_IPT; j++) {
+        const u64 i = t0 + (u64)j * SEG_NT + tid;  // consecutive lanes: consecutive entries
+        if (i >= n) break;
+        const int x = (int)(i - (u64)g0);
+        const u64 k = s_k[x], seg = k >> shift;
+        u32 rank = 0, left = 0, right = 0;
+        bool stop = false;
+        for (u64 p = i; p > glo && !stop; p--) {  // earlier entries of the segment, from LDS
+            const u64 v = s_k[(int)(p - 1 - (u64)g0)];
+            if ((v >> shift) != seg) {
+                bad |= (v >> shift) > seg ? 1u : 0u;
+                stop = true;
+            } else {
+                rank += v < k;
+                bad |= v == k ? 1u : 0u;
+                left++;
             }
-            rank += x < k;
-            bad |= x == k ? 1u : 0u;
-            left++;
-            j--;
         }
-        if (left == RS_SEG_MAX) bad |= 4u;
-        u32 right = 0;
-        for (u64 q = i + 1; q < n && right < RS_SEG_MAX; q++, right++) {  // later entries
-            const u64 x = key[q];
-            if ((x >> shift) != seg) break;
-            rank += x < k;
+        if (!stop && i - left > 0) {  // the segment runs on past the halo: continue in global memory
+            for (u64 p = i - left; p > 0 && left < RS_SEG_MAX; p--) {
+                const u64 v = key[p - 1];
+                if ((v >> shift) != seg) {
+                    bad |= (v >> shift) > seg ? 1u : 0u;
+                    break;
+                }
+                rank += v < k;
+                bad |= v == k ? 1u : 0u;
+                left++;
+            }
+            if (left >= RS_SEG_MAX) bad |= 4u;
         }
-        if (right == RS_SEG_MAX) bad |= 4u;
+        stop = false;
+        for (u64 q = i + 1; q < ghi && !stop; q++) {  // later entries, from LDS
+            const u64 v = s_k[(int)(q - (u64)g0)];
+            if ((v >> shift) != seg) stop = true;
+            else { rank += v < k; right++; }
+        }
+        if (!stop && i + 1 + right < n) {
+            for (u64 q = i + 1 + right; q < n && right < RS_SEG_MAX; q++) {
+                const u64 v = key[q];
+                if ((v >> shift) != seg) break;
+                rank += v < k;
+                right++;
+            }
+            if (right >= RS_SEG_MAX) bad |= 4u;
+        }
         const u64 dst = i - left + rank;
         if (dst < n) {
             kout[dst] = k;
@@ -893,17 +941,17 @@ extern "C" int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uin
     KD_CHECK(n == 0 || (const void*)d_key_in != (const void*)d_key_out, "kd_sort_segmented_into: output aliases input");
     KD_HIP(hipSetDevice(ctx->device));
     if (n == 0) return KD_OK;
-    const unsigned gs = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 16));
+    const u64 ntiles = (n + SEG_T - 1) / SEG_T;
     return launch(ctx, "k_seg_sort", [&] {
-        hipLaunchKernelGGL(k_seg_sort, dim3(gs), dim3(256), 0, ctx->stream, d_key_in, n, 64 - seg_bits, d_key_out,
-                           d_order, d_err);
+        hipLaunchKernelGGL(k_seg_sort, dim3((unsigned)ntiles), dim3(SEG_NT), 0, ctx->stream, d_key_in, n, 64 - seg_bits,
+                           d_key_out, d_order, d_err);
     });
 }
 
 extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side* target, const uint32_t* d_delta,
-                                 uint64_t cap, const uint64_t* d_n, int64_t pk_lo, int64_t pk_hi, int64_t* d_pk,
-                                 uint32_t* d_perm) {
-    KD_CHECK(ctx && base && target && d_n && d_pk && d_perm && (cap == 0 || d_delta), "kd_delta_pk_order: NULL");
+                                 const uint64_t* d_keys, uint64_t cap, const uint64_t* d_n, int64_t pk_lo, int64_t pk_hi,
+                                 int64_t* d_pk, uint32_t* d_perm) {
+    KD_CHECK(ctx && base && target && d_n && d_pk && d_perm && (cap == 0 || d_delta || d_keys), "kd_delta_pk_order: NULL");
     KD_CHECK(base->key_mode == KD_KEY_INT && target->key_mode == KD_KEY_INT, "kd_delta_pk_order: KD_KEY_INT sides only");
     KD_CHECK(base->mem == KD_MEM_DEVICE && target->mem == KD_MEM_DEVICE, "kd_delta_pk_order: sides must be device memory");
     KD_CHECK(pk_lo <= pk_hi, "kd_delta_pk_order: pk_lo > pk_hi");
@@ -937,7 +985,7 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
         const unsigned g1 = (unsigned)std::max<u64>(1, std::min<u64>((cap + PKM_NT - 1) / PKM_NT, (u64)ctx->n_cu * 8));
         rc = launch(ctx, "k_pkm_mark", [&] {
             hipLaunchKernelGGL(k_pkm_mark, dim3(g1), dim3(PKM_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n, kA,
-                               kB, lo_block, nb, (u64*)masks, (i64*)tpk);
+                               kB, d_keys, lo_block, nb, (u64*)masks, (i64*)tpk);
         });
         if (rc) return rc;
         rc = launch(ctx, "k_pkm_scan", [&] {
@@ -967,10 +1015,10 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
     rc = launch(ctx, "k_dpk_keys", [&] {
         if (narrow)
             hipLaunchKernelGGL(k_dpk_keys<u32>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n,
-                               kA, kB, npass, width, plan, (u32*)ck, S.hist);
+                               kA, kB, d_keys, npass, width, plan, (u32*)ck, S.hist);
         else
             hipLaunchKernelGGL(k_dpk_keys<u64>, dim3(hg), dim3(RS_HIST_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n,
-                               kA, kB, npass, width, plan, (u64*)ck, S.hist);
+                               kA, kB, d_keys, npass, width, plan, (u64*)ck, S.hist);
     });
     if (rc) return rc;
     rc = launch(ctx, "k_sort_scan", [&] {

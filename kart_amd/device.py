@@ -199,6 +199,10 @@ class DiffPipeline:
             self.pk_range = (min(lo), max(hi)) if lo else (0, 0)
             self.d_pk = DevBuf(engine, 8 * cap)
             self.d_perm = DevBuf(engine, 4 * cap)
+            # the join writes every delta's / update's key beside it (kd_diff2_device_ex): the pk
+            # order reads them in order instead of gathering them from the sides
+            self.dkey = DevBuf(engine, 8 * cap)
+            self.ukey = DevBuf(engine, 8 * cap)
             self.u_pk = DevBuf(engine, 8 * max(self.cap_upd, 1))
             self.u_perm = DevBuf(engine, 4 * max(self.cap_upd, 1))
         self.gather = gather
@@ -244,6 +248,7 @@ class DiffPipeline:
 
     def _diff(self, perm):
         L, ctx = self.eng.L, self.eng.ctx
+        keys = self.pk_order and self.flags == 0
         if perm:  # sorted keys; OIDs and filenames read through the sort orders from the walk-order rows
             if self._perm_sides is None:
                 self._perm_sides = []
@@ -253,12 +258,15 @@ class DiffPipeline:
                     if w.name is not None:
                         k.name, k.name_off = w.name.ptr, w.name_off.ptr
                     self._perm_sides.append(k)
-            N.check(L.kd_diff2_device_perm(ctx, ctypes.byref(self._perm_sides[0]), ctypes.byref(self._perm_sides[1]),
-                                           self.walk[0][1].ptr, self.walk[1][1].ptr, self.flags, self.delta.ptr,
-                                           self.upd.ptr, self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device_perm")
+            N.check(L.kd_diff2_device_ex(ctx, ctypes.byref(self._perm_sides[0]), ctypes.byref(self._perm_sides[1]),
+                                         self.walk[0][1].ptr, self.walk[1][1].ptr, self.flags, self.delta.ptr,
+                                         self.upd.ptr, self.dkey.ptr if keys else None, self.ukey.ptr if keys else None,
+                                         self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device_ex")
         elif self.gather is None:
-            N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.flags, self.delta.ptr,
-                                      self.upd.ptr, self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
+            N.check(L.kd_diff2_device_ex(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), None, None, self.flags,
+                                         self.delta.ptr, self.upd.ptr, self.dkey.ptr if keys else None,
+                                         self.ukey.ptr if keys else None, self.counts.ptr, self.counts.ptr + 32),
+                    "kd_diff2_device_ex")
         else:
             # the join, rebase and counts' all-gather; the field diff is queued before anything waits
             # for the counts, and the records' all-gather (communication stream) overlaps it
@@ -268,12 +276,13 @@ class DiffPipeline:
         N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.ptr, self.cap_upd,
                                ctypes.cast(self.counts.ptr + 8, N.c_u64p), N.KD_MEM_DEVICE,
                                ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE), "kd_fielddiff")
-        if self.pk_order and self.flags == 0:
+        if keys:
             lo, hi = self.pk_range
-            N.check(L.kd_delta_pk_order(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.delta.ptr, self.cap,
-                                        self.counts.ptr + 24, lo, hi, self.d_pk.ptr, self.d_perm.ptr), "kd_delta_pk_order")
+            N.check(L.kd_delta_pk_order(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.delta.ptr,
+                                        self.dkey.ptr, self.cap, self.counts.ptr + 24, lo, hi, self.d_pk.ptr,
+                                        self.d_perm.ptr), "kd_delta_pk_order")
             N.check(L.kd_delta_pk_order(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.upd.ptr,
-                                        max(self.cap_upd, 1), self.counts.ptr + 8, lo, hi, self.u_pk.ptr,
+                                        self.ukey.ptr, max(self.cap_upd, 1), self.counts.ptr + 8, lo, hi, self.u_pk.ptr,
                                         self.u_perm.ptr), "kd_delta_pk_order")
         if self.gather is not None:
             N.check(L.kd_diff2_gather_end(ctx, self.delta.ptr, self.all_delta.ptr, self.all_cap,

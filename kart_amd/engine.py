@@ -164,8 +164,8 @@ class Engine:
         d_rec = DevBuf.from_numpy(self, records.reshape(-1))
         d_n = DevBuf.from_numpy(self, np.array([n], np.uint64))
         d_pk, d_perm = DevBuf(self, 8 * n), DevBuf(self, 4 * n)
-        N.check(self.L.kd_delta_pk_order(self.ctx, ctypes.byref(sa), ctypes.byref(sb), d_rec.ptr, n, d_n.ptr, min(lo),
-                                         max(hi), d_pk.ptr, d_perm.ptr), "kd_delta_pk_order")
+        N.check(self.L.kd_delta_pk_order(self.ctx, ctypes.byref(sa), ctypes.byref(sb), d_rec.ptr, None, n, d_n.ptr,
+                                         min(lo), max(hi), d_pk.ptr, d_perm.ptr), "kd_delta_pk_order")
         return d_pk.download(np.int64, n), d_perm.download(np.uint32, n)
 
     def fielddiff(self, old_data, old_off, new_data, new_off, pairs, maps):

@@ -147,3 +147,29 @@ def test_gpu_merge3_segmented_c4_walk_order(engine, n):
     assert np.array_equal(conf, oc.reshape(-1, 3)) and np.array_equal(md, om.reshape(-1, 2)) and n_clean == ocl
     assert conf.shape[0] == M.n_conflict
     del packing
+
+
+@pytest.mark.parametrize("n,flags", [(1000, 0), (300_000, 0), (300_000, 1), (2_000_000, 0)])
+def test_gpu_diff2_ex_record_keys(engine, n, flags):
+    """kd_diff2_device_ex writes every delta's and update's join key beside it (the key the pk order
+    reads): equal to the side key the record points at, in both compaction modes"""
+    from kart_amd import synth
+    from kart_amd.device import DevBuf, DevSide
+
+    L = synth.points_layer(n, seed=31)
+    A, B = DevSide(engine, L.base), DevSide(engine, L.target)
+    sa, sb = A.kd_side(), B.kd_side()
+    cap = L.base.n + L.target.n + 1
+    d, u, dk, uk, c = (DevBuf(engine, 8 * cap) for _ in range(5))
+    c.zero()
+    N.check(engine.L.kd_diff2_device_ex(engine.ctx, ctypes.byref(sa), ctypes.byref(sb), None, None, flags, d.ptr, u.ptr,
+                                        dk.ptr, uk.ptr, c.ptr, c.ptr + 32), "kd_diff2_device_ex")
+    cnt = c.download(np.uint64, 8)
+    assert cnt[4] == 0
+    nd, nu = int(cnt[3]), int(cnt[1])
+    for rec, keys, m in ((d, dk, nd), (u, uk, nu)):
+        r = rec.download(np.uint32, 2 * m).reshape(m, 2)
+        k = keys.download(np.uint64, m)
+        want = np.where(r[:, 0] != 0xFFFFFFFF, L.base.key[np.minimum(r[:, 0], L.base.n - 1)],
+                        L.target.key[np.minimum(r[:, 1], L.target.n - 1)])
+        assert np.array_equal(k, want)
