@@ -202,27 +202,48 @@ class GitRepo:
             return subprocess.run(["git", "write-tree"], env=env, check=True, capture_output=True).stdout.decode().strip()
 
     # ---- dataset versions -----------------------------------------------------------------------
+    def tree_at(self, spec, path):
+        """the OID of the tree at ``path`` in revision ``spec``, or None"""
+        tree = self.rev_tree(spec)
+        for part in [p for p in path.split("/") if p]:
+            nxt = None
+            for _, typ, oid, name in self.odb.tree_entries(tree):
+                if name == part and typ == "tree":
+                    nxt = oid
+                    break
+            if nxt is None:
+                return None
+            tree = nxt
+        return tree
+
     def _meta(self, spec, ds_path):
+        """(meta items, legends, schema, path structure) of a dataset version: the meta tree's files
+        read once; the items as Dataset3.meta_items yields them (kart_amd/meta.py), the
+        ``metadata.xml`` attachment taken from the dataset's own tree"""
+        from . import meta as M
+
         inner = f"{ds_path}/{DATASET_DIRNAME}/meta"
         (lv,) = self.walk([spec], inner)
         if not lv.present or lv.n == 0:
             return None
-        meta, legends, schema, path_structure = {}, {}, None, None
+        files, legends, schema, path_structure = {}, {}, None, None
         for rel, oid in lv.items():
             data = self.cat(oid)
             if rel.startswith("legend/"):
                 legends[rel[len("legend/"):]] = Legend.loads(data)
-            elif rel == "schema.json":
-                cols = json.loads(data)
-                schema = Schema.from_column_dicts(cols)
-                meta[rel] = cols
+                continue
+            files[rel] = data
+            if rel == "schema.json":
+                schema = Schema.from_column_dicts(json.loads(data))
             elif rel == "path-structure.json":
                 path_structure = json.loads(data)
-            elif rel.endswith(".json"):
-                meta[rel] = json.loads(data)
-            else:
-                meta[rel] = data.decode()
-        return meta, legends, schema, path_structure
+        attachments = {}
+        ds_tree = self.tree_at(spec, ds_path)
+        if ds_tree is not None:
+            for _, typ, oid, name in self.odb.tree_entries(ds_tree):
+                if typ == "blob" and name in M.ATTACHMENT_META_ITEMS:
+                    attachments[name] = self.cat(oid)
+        return M.meta_items(files, attachments), legends, schema, path_structure
 
     def _version(self, ds_path, m, leaves, partial):
         meta, legends, schema, path_structure = m

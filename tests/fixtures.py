@@ -19,7 +19,7 @@ from kart_amd import packing  # noqa: E402
 from kart_amd.schema import Legend, Schema  # noqa: E402
 
 DIFF_FIXTURES = ["repo_points", "repo_polygons", "repo_table", "repo_string_pks", "conflicts_points",
-                 "conflicts_polygons", "conflicts_table", "synth_int", "synth_int_same", "synth_str"]
+                 "conflicts_polygons", "conflicts_table", "synth_int", "synth_int_same", "synth_str", "meta_edits"]
 MERGE_FIXTURES = ["conflicts_points", "conflicts_polygons", "conflicts_table"]
 
 
@@ -71,6 +71,13 @@ class Fixture:
                 o = self.a[f"{key}_name_off"].astype(np.uint64)
                 self._packed[key] = packing.pack_side(d, self.oids(key), enc, rel_off=o)
         return self._packed[key]
+
+    def meta_files(self, key):
+        """{path relative to the meta tree: bytes} of a side (legends apart), as the repo holds them"""
+        return {k: bytes.fromhex(v) for k, v in self.meta["sides"][key].get("meta_files", {}).items()}
+
+    def attachments(self, key):
+        return {k: bytes.fromhex(v) for k, v in self.meta["sides"][key].get("attachments", {}).items()}
 
     def sorted_names(self, key):
         names = self.names(key)

@@ -110,6 +110,7 @@ class Side:
 
     def __init__(self, repo, spec, ds_path):
         self.spec = spec
+        self.repo = repo
         self.ds = refshim.dataset3(repo, spec, ds_path) if spec else None
         self.names, self.oids = [], []
         if self.ds is not None:
@@ -122,6 +123,20 @@ class Side:
         if self.ds is None:
             return None
         return self.ds.get_meta_item("schema.json")
+
+    def meta_files(self):
+        """{path relative to the meta tree: raw bytes} (legends left out: they are stored apart)"""
+        if self.ds is None:
+            return None
+        pre = f"{self.ds.path}/.table-dataset/meta/"
+        return {p[len(pre):]: self.repo.blob_data(o) for p, o in self.repo.ls_tree_r(self.spec, pre)
+                if not p[len(pre):].startswith("legend/")}
+
+    def attachments(self):
+        """{name: raw bytes} of the blobs beside .table-dataset (the metadata.xml attachment)"""
+        if self.ds is None:
+            return None
+        return {b.name: bytes(b.data) for b in self.ds.tree if b.type_str == "blob"}
 
     def path_structure(self):
         if self.ds is None:
@@ -175,6 +190,8 @@ class Fixture:
             "n": len(names),
             "schema": side.schema_json(),
             "path_structure": side.path_structure(),
+            "meta_files": {k: v.hex() for k, v in (side.meta_files() or {}).items()},
+            "attachments": {k: v.hex() for k, v in (side.attachments() or {}).items()},
         }
 
     def save(self):
@@ -198,6 +215,8 @@ def golden_diff2(fx, base_key, target_key, base_side, target_side, ds_path, with
         base_ds, target_ds = target_ds, base_ds
         params["reverse"] = True
     ds_diff = base_ds.diff(target_ds, **params)
+    # diff_meta (kart/rich_base_dataset.py:183-195): the meta items' DeltaDiff, (key, old, new)
+    meta_diff = sorted([k, d.old_value, d.new_value] for k, d in ds_diff.get("meta", {}).items())
     fdiff = ds_diff.get("feature")
     deltas = []
     counts = {}
@@ -223,6 +242,7 @@ def golden_diff2(fx, base_key, target_key, base_side, target_side, ds_path, with
             "target": target_key,
             "counts": counts,
             "deltas": deltas,
+            "meta": meta_diff,
         }
     )
     return deltas
@@ -767,9 +787,91 @@ def path_goldens():
     print("  wrote paths.json")
 
 
+WKT_A = ('GEOGCS["WGS 84",DATUM["WGS_1984", SPHEROID["WGS 84",6378137,298.257223563,AUTHORITY["EPSG","7030"]],'
+         'AUTHORITY["EPSG","6326"]],\n  PRIMEM["Greenwich",0,AUTHORITY["EPSG","8901"]],UNIT["degree",0.0174532925199433,'
+         'AUTHORITY["EPSG","9122"]],AXIS["Latitude",NORTH],AXIS["Longitude",EAST],AUTHORITY["EPSG","4326"]]')
+WKT_B = ('PROJCS["NZGD2000 / New Zealand Transverse Mercator 2000",GEOGCS["NZGD2000",DATUM["New_Zealand_Geodetic_Datum_2000",'
+         'SPHEROID["GRS 1980",6378137,298.257222101]],PRIMEM["Greenwich",0],UNIT["degree",0.0174532925199433]],'
+         'PROJECTION["Transverse_Mercator"],PARAMETER["latitude_of_origin",0],PARAMETER["central_meridian",173],'
+         'PARAMETER["scale_factor",0.9996],PARAMETER["false_easting",1600000],PARAMETER["false_northing",10000000],'
+         'UNIT["metre",1],AUTHORITY["EPSG","2193"]]')
+
+
+WKT_CASES = ['GEOGCS["a",DATUM["b"]]', '  A [ 1 ,2.5e3, "x""y" ] ', 'A[B[1],C[2,D[3]],E]', 'A[1,]]',
+             'A[1,]]\nB[2,C[3]]', 'x\r\ny', '1.5.3,[$', '\n\nA(1 , -0.5E+3 ,B("q"))\n\n', 'A[007,-0,1e5]', WKT_A, WKT_B,
+             'A["unterminated, B[1]]', 'Ω[1,Ж[2]]', '\ufeffA[1]', '\tA[\t1,\r2]']
+
+
+def wkt_goldens():
+    """crs_util.normalise_wkt (kart/crs_util.py:204-209) on crafted WKT: whitespace, nesting, error
+    characters, unbalanced brackets, newlines, non-ASCII keywords"""
+    cu = refshim.ref("crs_util")
+    out = [[w, cu.normalise_wkt(w)] for w in WKT_CASES]
+    with open(os.path.join(OUT, "wkt.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"  wrote wkt.json: {len(out)} cases")
+
+
+def meta_edits():
+    """A dataset whose meta items change: title, description, CRS definitions (odd whitespace,
+    nested, added, removed), the metadata.xml attachment, a schema.json that only changes its
+    formatting (normalised: no item change), and non-standard meta files (never items)."""
+    schema = schema_m.Schema.from_column_dicts([
+        {"id": "m-fid", "name": "fid", "dataType": "integer", "primaryKeyIndex": 0, "size": 64},
+        {"id": "m-geom", "name": "geom", "dataType": "geometry", "geometryType": "POINT", "geometryCRS": "EPSG:4326"},
+        {"id": "m-name", "name": "name", "dataType": "text", "length": None},
+    ])
+    enc = paths_m.PathEncoder.INT_PK_ENCODER
+    ds = "mds"
+    inner = f"{ds}/.table-dataset"
+    base = _ds_meta_files(ds, schema, enc)
+    raw_schema = json.loads(schema.dumps())
+    feats = {}
+    rng = random.Random(11)
+    for pk in range(20):
+        feats[f"{inner}/feature/{enc.encode_pks_to_path([pk])}"] = su.msg_pack(
+            [schema.legend.hexhash(), [_point(rng), f"n{pk}"]])
+    c0 = dict(base, **feats)
+    c0[f"{inner}/meta/title"] = b"Title A"
+    c0[f"{inner}/meta/crs/EPSG:4326.wkt"] = WKT_A.encode()
+    c0[f"{inner}/meta/custom.json"] = b'{"x": 1}'
+    c0[f"{ds}/metadata.xml"] = b"<gmd:MD_Metadata>one</gmd:MD_Metadata>"
+    c1 = {
+        f"{inner}/meta/title": b"Title B",
+        f"{inner}/meta/description": "A longer description \u2014 with non-ASCII".encode(),
+        f"{inner}/meta/crs/EPSG:4326.wkt": (WKT_A.replace(",", ",  ") + "\r\n").encode(),  # same tokens
+        f"{inner}/meta/crs/EPSG:2193.wkt": WKT_B.encode(),
+        f"{inner}/meta/custom.json": b'{"x": 2}',
+        f"{ds}/metadata.xml": b"<gmd:MD_Metadata>two</gmd:MD_Metadata>",
+        # the same columns with explicit nulls and another key order: normalised to the same item
+        f"{inner}/meta/schema.json": json.dumps([dict(reversed(list(c.items())), extra=None) for c in raw_schema]).encode(),
+    }
+    c2 = {
+        f"{inner}/meta/title": b"",
+        f"{inner}/meta/crs/EPSG:4326.wkt": None,
+        f"{inner}/meta/crs/nested/EPSG:3857.wkt": b'PROJCS["Pseudo",GEOGCS["WGS 84"],UNIT["metre",1]]',
+        f"{ds}/metadata.xml": None,
+        f"{inner}/meta/description": None,
+    }
+    gitdir = os.path.join(WORK, "meta_edits.git")
+    _fast_import(gitdir, [("c0", c0), ("c1", c1), ("c2", c2)])
+    repo = refshim.GitRepo(gitdir)
+    fx = Fixture("meta_edits", repo)
+    fx.meta["ds_path"] = ds
+    sides = {k: Side(repo, f"c{i}", ds) for i, k in enumerate(("c0", "c1", "c2"))}
+    sides["empty"] = Side(repo, None, ds)
+    for k, sd in sides.items():
+        fx.add_side(k, sd)
+    for a, b in (("c0", "c1"), ("c1", "c2"), ("c0", "c2"), ("c2", "c0"), ("empty", "c0"), ("c1", "empty")):
+        golden_diff2(fx, a, b, sides[a], sides[b], ds)
+    (c01,) = [c for c in fx.meta["cases"] if c["base"] == "c0" and c["target"] == "c1"]
+    assert {k for k, _, _ in c01["meta"]} == {"title", "description", "crs/EPSG:2193.wkt", "metadata.xml"}, c01["meta"]
+    fx.save()
+
+
 if __name__ == "__main__":
     os.makedirs(WORK, exist_ok=True)
-    which = sys.argv[1:] or ["paths", "envelopes", "real", "conflicts", "synth"]
+    which = sys.argv[1:] or ["paths", "envelopes", "real", "conflicts", "synth", "meta"]
     if "paths" in which:
         path_goldens()
     if "envelopes" in which:
@@ -782,3 +884,6 @@ if __name__ == "__main__":
         synthetic_int(True)
         synthetic_int(False)
         synthetic_str()
+    if "meta" in which:
+        meta_edits()
+        wkt_goldens()

@@ -47,9 +47,16 @@ def version(fx, key):
     if fx.n(key) == 0:
         return None
     idx = fx.a[f"{key}_blob"]
+    from kart_amd import meta as M
+
     return D.DatasetVersion(fx.meta["ds_path"], fx.schema(key), fx.legends, fx.encoding(key), fx.a[f"{key}_names"],
                             fx.a[f"{key}_name_off"].astype(np.uint64), fx.oids(key), lambda i: fx.blob(int(idx[i])),
-                            meta={"schema.json": fx.meta["sides"][key]["schema"]})
+                            meta=M.meta_items(fx.meta_files(key), fx.attachments(key)))
+
+
+def meta_diff_rows(ds):
+    """a DatasetDiff's meta DeltaDiff as sorted [key, old, new] rows (the golden form)"""
+    return sorted([k, d.old_value, d.new_value] for k, d in ds.get("meta", {}).items())
 
 
 def _jv(v):
@@ -75,7 +82,10 @@ def test_get_dataset_diff_golden(eng, name):
     for case in fx.cases("diff2"):
         base, target = version(fx, case["base"]), version(fx, case["target"])
         ds = D.get_dataset_diff(eng, base, target)
-        fd = ds.get("feature", {})
+        # diff_meta: the meta items' DeltaDiff equals the reference's (normalised schema.json and CRS
+        # WKT, the metadata.xml attachment, non-standard meta files left out)
+        assert meta_diff_rows(ds) == case["meta"], (name, case["base"], case["target"])
+        fd = ds.get("feature") or structs().DeltaDiff()
         got = {(d.type, d.old_key, d.new_key) for d in fd.values()}
         want = {(d["type"], pk_of(d["old_pk"]), pk_of(d["new_pk"])) for d in case["deltas"]}
         assert got == want
