@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--arena", action="store_true",
                     help="c5: filter from the blob arenas (kd_geom_filter) instead of the geometry heads")
+    ap.add_argument("--per-entry", action="store_true",
+                    help="c5: the heads kernel straight on the per-entry heads (no delta-order gather)")
+    ap.add_argument("--c3-layer", action="store_true",
+                    help="c5: the C3 polygon layer instead of SURVEY's C5 mix (points, straddles, wide, EMPTY, edge)")
     ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
     ap.add_argument("--no-delta-order", action="store_true",
                     help="c5: skip timing the heads kernel on the drop-in's delta-order layout")
@@ -648,14 +652,15 @@ def run_c5(args, H):
 
     n, bits = args.n, 20
     t0 = time.time()
-    L = synth.polygons_layer(n, shard=(H.rank, H.world) if H.world > 1 else None, delta_blobs=True)
+    shard = (H.rank, H.world) if H.world > 1 else None
+    L = synth.polygons_layer(n, shard=shard, delta_blobs=True) if args.c3_layer else synth.c5_layer(n, shard=shard)
     log(f"[rank {H.rank}] generated {L.base.n}+{L.target.n} entries in {time.time() - t0:.1f}s")
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     cols = GeomCols(ver, ver, "geom", "geom")
     eng = engine_for(H)
     heads = not args.arena
     pipe = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits,
-                          heads=heads)
+                          heads=heads, delta_order=heads and not args.per_entry)
     for _ in range(max(1, args.warmup)):
         pipe.step()
     eng.sync()
@@ -666,7 +671,7 @@ def run_c5(args, H):
         # size-independent: kept = deltas with a side that may match, in delta order; codes in range
         may = ((codes >= 1) & (codes <= 3)).any(axis=1)
         assert np.array_equal(keep, np.nonzero(may)[0]), "kept deltas differ from the per-delta codes"
-        assert codes.max() <= 4 and not (codes == 3).any(), "fallback codes on synthetic polygons"
+        assert codes.max() <= 4 and not (codes == 3).any(), "fallback codes left (the blob fallback runs in the step)"
         assert ((delta[:, 0] == 0xFFFFFFFF) == (codes[:, 0] == 4)).all() and \
             ((delta[:, 1] == 0xFFFFFFFF) == (codes[:, 1] == 4)).all()
     kname = "k_gf_heads" if heads else "k_gf_match"
@@ -676,15 +681,31 @@ def run_c5(args, H):
     elapsed = timed(H, eng, pipe.step, args.steps)
     eng.prof_enable(False)
     kern = kernel_times(eng, ("k_partition2", "k_join2", "k_place2", kname, "k_gf_scan", "k_gf_place"))
+    eng.prof_reset()
+    eng.prof_select(None)
+    eng.prof_enable(True)
+    for _ in range(3):
+        pipe.step()
+    eng.sync()
+    eng.prof_enable(False)
+    parts = kernel_times(eng, ("k_partition2", "k_join2", "k_gscan2", "k_place2", "k_gh_gather", kname, "k_gf_scan",
+                               "k_gf_place"))
     n_pairs = L.base.n + L.n_insert
     total_pairs = sum(H.allgather(n_pairs))
     nd = counts["deltas"]
     ob_off, nb_off = L.base_blobs[1], L.target_blobs[1]
+    pres = int((delta[:, 0] != 0xFFFFFFFF).sum() + (delta[:, 1] != 0xFFFFFFFF).sum())
+    gather = None
     if heads:
         # algorithmic bytes per k_gf_heads launch: the delta pairs (8 B), one 48-B head per present
         # side, codes (2 B) + index envelope (bits/2 + 1 B) written per delta
-        pres = int((delta[:, 0] != 0xFFFFFFFF).sum() + (delta[:, 1] != 0xFFFFFFFF).sum())
         alg = 8 * nd + 48 * pres + nd * (2 + bits // 2 + 1)
+        if pipe.delta_order and "k_gh_gather" in parts:  # the gather: pairs read, heads read + written, pairs written
+            galg = 8 * nd + 96 * pres + 8 * nd
+            gms = parts["k_gh_gather"][1]
+            gather = {"what": "k_gh_gather: the deltas' 48-B heads copied into delta order (one per present side)",
+                      "avg_launch_ms": round(gms, 5), "algorithmic_bytes_per_launch": galg,
+                      "frac": round(galg / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     else:
         # per k_gf_match launch: the delta pairs (8 B); per present side its offsets (16 B) and the
         # blob head up to the end of the GPKG envelope (<= 96 B); codes + index envelope written
@@ -763,17 +784,22 @@ def run_c5(args, H):
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong" if H.world > 1 else "weak", "vs_baseline": None,
         "dtype": "u8/u64 (integer join) + f64 (envelopes, EnvelopeEncoder)",
-        "data": "synthetic (the C3 MULTIPOLYGON layer; blobs materialised for every delta's old/new version)",
+        "data": ("synthetic (the C3 MULTIPOLYGON layer" if args.c3_layer else
+                 "synthetic (SURVEY §8d's C5 mix: 30% points incl. EMPTY, polygons with straddling / >=180-degree-wide / "
+                 "filter-edge / XYZ envelopes, EPSG:4326") + "; blobs materialised for every delta's old/new version)",
         "config": {"workload": f"C5: spatially filtered diff of ONE {n}-feature polygon layer"
                                f"{f' split into {H.world} bucket-range shards' if H.world > 1 else ''}: classify2 + "
                                "per-delta geometry envelope filter + EnvelopeEncoder of the new side" +
-                               (" (from the 48-B geometry heads the blob reader extracts on the host: kd_geom_heads)"
+                               ((" (from the 48-B geometry heads the blob reader extracts on the host: kd_geom_heads; "
+                                 "gathered into delta order on the device, blob fallback in the step)" if pipe.delta_order
+                                 else " (from the 48-B per-entry geometry heads)")
                                 if heads else " (msgpack walk of the blob arenas on the GPU)"),
                    "features": n, "pairs_per_step": total_pairs, "deltas_per_step": sum(H.allgather(nd)),
                    "kept_per_step": sum(H.allgather(counts["kept"])), "bits": bits, "filter": list(synth.C5_FILTER),
                    "parallelism": f"bucket-range shards x{H.world} (counts per rank, no exchange)"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
-        "roofline": roof, "cpu_baseline": cpu,
+        "step_kernels_avg_ms": {k: round(v[1], 5) for k, v in parts.items()},
+        "roofline": roof, "cpu_baseline": cpu, "heads_gather": gather,
     }
     if heads:
         blobs = int(np.count_nonzero(np.diff(L.base_blobs[1])) + np.count_nonzero(np.diff(L.target_blobs[1])))

@@ -293,6 +293,18 @@ int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_
                          const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
                          uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem);
 
+/* kd_geom_filter_heads over classify2's delta list on the device (all buffers device memory, the delta
+ * count *d_n on the device, cap the list's capacity): the heads of the deltas' old and new blobs are
+ * first gathered into delta order (the layout the drop-in's blob reader produces: it reads the
+ * deltas' blobs after classification), then filtered from those contiguous heads; a geometry whose
+ * head cannot decide it is read from old_blobs / new_blobs at the delta's own blob (the pairs).
+ * heads_old [n_old] / heads_new [n_new] are indexed like the arenas (per entry).  Outputs as
+ * kd_geom_filter_heads (match [cap * 2], keep [cap], n_keep, enc, enc_ok: device). */
+int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_old, const kd_geom_head* heads_new,
+                          uint64_t n_new, const kd_blobs* old_blobs, const kd_blobs* new_blobs, const uint32_t* pairs,
+                          uint64_t cap, const uint64_t* d_n, const double filt_env[4], uint32_t flags, int bits,
+                          uint8_t* match, uint32_t* keep, uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok);
+
 /* -------- writer formatting -------- */
 #define KD_HEX_BYTES 0u    /* bytes.hex(v): lowercase hex of every byte of every blob                */
 #define KD_HEX_GPKG_WKB 1u /* gpkg_geom_to_hex_wkb: uppercase hex of the WKB after the GPKG header   */

@@ -208,6 +208,12 @@ SIGNATURES = {
          ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c_u64p, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_uint32],
     ),
+    "kd_geom_filter_deltas": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(KdBlobs),
+         ctypes.POINTER(KdBlobs), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, c_dblp, ctypes.c_uint32, ctypes.c_int,
+         ctypes.c_void_p, ctypes.c_void_p, c_u64p, ctypes.c_void_p, ctypes.c_void_p],
+    ),
     "kd_shard_cuts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kd_sf_index_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,

@@ -386,6 +386,8 @@ struct GfHeadArgs {
     const u8* data[2];  // the arenas the heads came from (null: no slow path, such sides FALLBACK)
     const u64* off[2];
     const u8* zeros;    // >= 48 readable zero bytes: the source of an absent side's head loads
+    const uint2* bpairs;  // (optional) the blob of each delta side in the arenas, when the heads are
+                          // not indexed like the arenas (delta-order heads over per-entry arenas)
 };
 
 struct HeadLd {
@@ -406,7 +408,7 @@ __device__ __forceinline__ HeadLd load_head(const GfHeadArgs& g, int s, u32 bi) 
 }
 
 __device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g, int s, u32 bi, const HeadLd& L,
-                                            GHit& h) {
+                                            GHit& h, u64 d) {
     h.r = -1;
     h.pc = -1;
     h.empty = false;
@@ -422,7 +424,9 @@ __device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g
     const bool fast = env_fast(r, glen, h.r, h.e, h.pc, h.pe);
     if (!fast) {  // XYZ/XYM/XYZM envelope or a NaN one: the byte-wise decode on the blob
         if (!g.data[s]) { h.code = GF_FALLBACK; h.r = -1; return; }
-        const u8* gp = g.data[s] + g.off[s][bi] + (v2.w & 0xFFFFFFu);
+        const u32 blob = g.bpairs ? (s ? g.bpairs[d].y : g.bpairs[d].x) : bi;
+        if (blob == KD_NONE || (u64)blob >= a.nblob[s]) { h.code = GF_FALLBACK; h.r = -1; return; }
+        const u8* gp = g.data[s] + g.off[s][blob] + (v2.w & 0xFFFFFFu);
         h.r = gpkg_env(gp, glen, h.e);
         h.pc = -1;
         if (h.r == 0 || h.r == 2) h.pc = point_env(gp, glen, h.pe);
@@ -470,9 +474,9 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
             for (int k = 0; k < nb; k++) wenc[lane * nb + k] = 0;
         if (d < n) {
             GHit h;
-            decode_head(a, g, 0, pr.x, L0, h);
+            decode_head(a, g, 0, pr.x, L0, h, d);
             const int co = h.code;
-            decode_head(a, g, 1, pr.y, L1, h);
+            decode_head(a, g, 1, pr.y, L1, h, d);
             const int cn = h.code;
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
@@ -572,6 +576,35 @@ __global__ __launch_bounds__(GF_NT) void k_gf_place(const u8* __restrict__ match
     }
 }
 
+
+// Delta-order heads: delta d's old and new heads copied to slot d of two contiguous arrays (the
+// layout the drop-in's blob reader hands over: it reads the deltas' blobs after classification), and
+// its pair rewritten to (d | NONE, d | NONE).  One lane per delta, three 16-B loads and stores per side.
+__global__ __launch_bounds__(256) void k_gh_gather(const kd_geom_head* __restrict__ ho, u64 no, const kd_geom_head* __restrict__ hn,
+                                                   u64 nn, const uint2* __restrict__ pairs, u64 cap, const u64* __restrict__ d_n,
+                                                   kd_geom_head* __restrict__ oo, kd_geom_head* __restrict__ on,
+                                                   uint2* __restrict__ opairs) {
+    const u64 n = d_n ? min(*d_n, cap) : cap;
+    for (u64 d = (u64)blockIdx.x * 256 + threadIdx.x; d < n; d += (u64)gridDim.x * 256) {
+        const uint2 p = pairs[d];
+        const bool a = p.x != KD_NONE && (u64)p.x < no, b = p.y != KD_NONE && (u64)p.y < nn;
+        if (a) {
+            const u32x4* src = (const u32x4*)(ho + p.x);
+            u32x4* dst = (u32x4*)(oo + d);
+            const u32x4 x0 = src[0], x1 = src[1], x2 = src[2];
+            dst[0] = x0; dst[1] = x1; dst[2] = x2;
+        }
+        if (b) {
+            const u32x4* src = (const u32x4*)(hn + p.y);
+            u32x4* dst = (u32x4*)(on + d);
+            const u32x4 y0 = src[0], y1 = src[1], y2 = src[2];
+            dst[0] = y0; dst[1] = y1; dst[2] = y2;
+        }
+        // a side without a head in range keeps an index past the heads: the filter's FALLBACK
+        opairs[d] = make_uint2(p.x == KD_NONE ? KD_NONE : a ? (u32)d : 0xFFFFFFFEu,
+                               p.y == KD_NONE ? KD_NONE : b ? (u32)d : 0xFFFFFFFEu);
+    }
+}
 
 // the launches and result copies shared by kd_geom_filter (arenas) and kd_geom_filter_heads (heads)
 static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* pairs, uint64_t n, const uint64_t* d_n,
@@ -757,4 +790,54 @@ extern "C" int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, 
     a.nblob[0] = n_old;
     a.nblob[1] = n_new;
     return gf_run(ctx, a, &g, pairs, n, d_n, pairs_mem, filt_env, flags, bits, match, keep, n_keep, enc, enc_ok, out_mem);
+}
+
+extern "C" int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_old,
+                                     const kd_geom_head* heads_new, uint64_t n_new, const kd_blobs* old_blobs,
+                                     const kd_blobs* new_blobs, const uint32_t* pairs, uint64_t cap, const uint64_t* d_n,
+                                     const double filt_env[4], uint32_t flags, int bits, uint8_t* match, uint32_t* keep,
+                                     uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok) {
+    KD_CHECK(ctx && filt_env && match && keep && n_keep && d_n && (cap == 0 || pairs), "kd_geom_filter_deltas: NULL argument");
+    KD_CHECK((n_old == 0 || heads_old) && (n_new == 0 || heads_new), "kd_geom_filter_deltas: heads NULL");
+    KD_CHECK(filt_env[0] <= filt_env[1] && filt_env[2] <= filt_env[3], "kd_geom_filter_deltas: inverted filter envelope");
+    KD_CHECK(!enc || (enc_ok && bits >= 2 && bits <= 32 && bits % 2 == 0),
+             "kd_geom_filter_deltas: bits must be even and <= 32");
+    KD_CHECK(!old_blobs == !new_blobs, "kd_geom_filter_deltas: both arenas or neither");
+    KD_CHECK(cap < 0xFFFFFFF0ull, "kd_geom_filter_deltas: too many deltas");
+    KD_CHECK(((u64)heads_old & 15) == 0 && ((u64)heads_new & 15) == 0, "kd_geom_filter_deltas: heads must be 16-byte aligned");
+    KD_HIP(hipSetDevice(ctx->device));
+    static_assert(sizeof(kd_geom_head) == 48, "kd_geom_head is 48 bytes");
+    int rc;
+    void *go, *gn, *gp, *dz;
+    if ((rc = ensure(ctx, "gd.ho", (cap + 1) * sizeof(kd_geom_head), &go))) return rc;
+    if ((rc = ensure(ctx, "gd.hn", (cap + 1) * sizeof(kd_geom_head), &gn))) return rc;
+    if ((rc = ensure(ctx, "gd.pairs", (cap + 1) * 8, &gp))) return rc;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    if (cap) {
+        const unsigned grid = (unsigned)std::max<u64>(1, std::min<u64>((cap + 255) / 256, (u64)ctx->n_cu * 16));
+        rc = launch(ctx, "k_gh_gather", [&] {
+            hipLaunchKernelGGL(k_gh_gather, dim3(grid), dim3(256), 0, ctx->stream, n_old ? heads_old : (const kd_geom_head*)dz,
+                               n_old, n_new ? heads_new : (const kd_geom_head*)dz, n_new, (const uint2*)pairs, cap, d_n,
+                               (kd_geom_head*)go, (kd_geom_head*)gn, (uint2*)gp);
+        });
+        if (rc) return rc;
+    }
+    GfArgs a{};
+    GfHeadArgs g{};
+    g.head[0] = (const kd_geom_head*)go;
+    g.head[1] = (const kd_geom_head*)gn;
+    g.nhead[0] = g.nhead[1] = cap;
+    g.zeros = (const u8*)dz;
+    g.bpairs = (const uint2*)pairs;
+    if (old_blobs) {
+        const kd_blobs* bl[2] = {old_blobs, new_blobs};
+        for (int s = 0; s < 2; s++) {
+            KD_CHECK(bl[s]->mem == KD_MEM_DEVICE, "kd_geom_filter_deltas: arenas must be device memory");
+            g.data[s] = bl[s]->data;
+            g.off[s] = bl[s]->off;
+            a.nblob[s] = bl[s]->n;
+        }
+    }
+    return gf_run(ctx, a, &g, (const uint32_t*)gp, cap, d_n, KD_MEM_DEVICE, filt_env, flags, bits, match, keep, n_keep,
+                  enc, enc_ok, KD_MEM_DEVICE);
 }

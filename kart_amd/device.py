@@ -340,7 +340,10 @@ class FilterPipeline:
     whole layer in one stream."""
 
     def __init__(self, engine, base, target, base_blobs, target_blobs, geom_cols, filt_env, rectangle=False, bits=20,
-                 heads=False):
+                 heads=False, delta_order=False):
+        """heads: filter from 48-B geometry heads (the blob reader's host pass) instead of the blob
+        arenas; delta_order (with heads): every step first gathers the deltas' heads into delta order
+        on the device (kd_geom_filter_deltas: the drop-in's layout), the blob fallback included"""
         import ctypes as _c
 
         self.eng = engine
@@ -367,6 +370,7 @@ class FilterPipeline:
         self.heads = None
         self.heads_s = None
         self.heads_host = None
+        self.delta_order = bool(delta_order) and heads
         if heads:  # the blob reader's host pass, then 48 bytes per blob in HBM (kd_geom_filter_heads)
             import time
 
@@ -386,6 +390,14 @@ class FilterPipeline:
         L, ctx = self.eng.L, self.eng.ctx
         N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), 0, self.delta.ptr, self.upd.ptr,
                                   self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
+        if self.delta_order:
+            (ho, no), (hn, nn) = self.heads
+            N.check(L.kd_geom_filter_deltas(ctx, ho.ptr, no, hn.ptr, nn, ctypes.byref(self._ob), ctypes.byref(self._nb),
+                                            self.delta.ptr, self.cap, ctypes.cast(self.counts.ptr + 24, N.c_u64p),
+                                            self._fe, self.flags, self.bits, self.match.ptr, self.keep.ptr,
+                                            ctypes.cast(self.n_keep.ptr, N.c_u64p), self.enc.ptr if self.enc else None,
+                                            self.enc_ok.ptr if self.enc_ok else None), "kd_geom_filter_deltas")
+            return
         if self.heads is not None:
             (ho, no), (hn, nn) = self.heads
             N.check(L.kd_geom_filter_heads(ctx, ho.ptr, no, hn.ptr, nn, N.KD_MEM_DEVICE, ctypes.byref(self._ob),

@@ -475,6 +475,174 @@ def geometry_layer(n, seed=SEED, frac_point=0.3):
 
 
 # ---------------------------------------------------------------------------------------------
+# C5 as SURVEY §8(d) defines it: the filtered diff of a 100M-feature layer of mixed geometries
+MIXED_SCHEMA = [
+    {"id": "g-fid", "name": "id", "dataType": "integer", "primaryKeyIndex": 0, "size": 64},
+    {"id": "g-geom", "name": "geom", "dataType": "geometry", "geometryType": "GEOMETRY", "geometryCRS": "EPSG:4326"},
+    {"id": "g-date", "name": "date_adjusted", "dataType": "timestamp"},
+    {"id": "g-sid", "name": "survey_reference", "dataType": "text", "length": 50},
+    {"id": "g-adj", "name": "adjusted_nodes", "dataType": "integer", "size": 32},
+]
+
+
+def _concat_segments(segs, n):
+    """rows of variable-length byte segments -> (arena, off[n+1]): segs = [(mat [n, W], len [n]), ...]"""
+    lens = np.zeros(n, np.int64)
+    for _, ln in segs:
+        lens += ln
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    arena = np.zeros(int(off[-1]), np.uint8)
+    pos = off[:-1].astype(np.int64).copy()
+    for mat, ln in segs:
+        W = mat.shape[1]
+        if W:
+            cols = np.arange(W, dtype=np.int64)[None, :]
+            m = cols < ln[:, None]
+            arena[(pos[:, None] + cols)[m]] = mat[m]
+        pos += ln
+    return arena, off
+
+
+def mixed_blobs(pk, gver, aver, legend_hex, rng_seed=SEED):
+    """C5 feature blobs: values = [geom, date_adjusted, survey_reference, adjusted_nodes]; the
+    geometry (a function of (pk, gver)) is, by a hash of the pk, a point (30 %: 8-B GPKG header + 21-B
+    WKB, no stored envelope; 0.1 % of them EMPTY) or a MULTIPOLYGON (8-B header + XY envelope + a
+    5..24-point ring; 0.2 % carry an XYZ envelope, which the geometry heads cannot decide: the filter's
+    blob fallback).  lon U[-180, 180), lat U[-85, 85]; polygon widths and heights log-U[1e-6, 10]
+    degrees; 1 % straddle +180, 0.1 % are >= 180 degrees wide, 1 % start exactly on the filter's east
+    edge."""
+    pk = np.asarray(pk, np.int64)
+    n = pk.shape[0]
+    u = pk.view(np.uint64)
+    hk = splitmix64(u ^ np.uint64(rng_seed ^ 0xC5C5))  # per feature, fixed across versions
+    hg = splitmix64(u ^ (np.asarray(gver, np.uint64) << np.uint64(48)) ^ np.uint64(rng_seed ^ 0x6706))
+    hg2 = splitmix64(hg)
+    ha = splitmix64(u ^ (np.asarray(aver, np.uint64) << np.uint64(48)) ^ np.uint64(rng_seed ^ 0xA77A))
+    ha2 = splitmix64(ha)
+    is_pt = (hk % np.uint64(1000)) < np.uint64(300)
+    f = lambda h, sh: ((h >> np.uint64(sh)) & np.uint64(0xFFFFFF)).astype(np.float64) / float(1 << 24)
+    lon = -180.0 + f(hg, 0) * 360.0
+    lat = -85.0 + f(hg, 24) * 170.0
+    w = 10.0 ** (-6.0 + 7.0 * f(hg2, 0))
+    hh = 10.0 ** (-6.0 + 7.0 * f(hg2, 24))
+    cls = (hg2 >> np.uint64(48)) % np.uint64(10000)
+    straddle, wide = cls < 100, (cls >= 100) & (cls < 110)
+    edge, xyz = (cls >= 110) & (cls < 210), (cls >= 210) & (cls < 230)
+    empty = is_pt & ((hk >> np.uint64(20)) % np.uint64(1000) == 0)
+    minx = np.where(straddle, 180.0 - w / 2, np.where(edge, C5_FILTER[1], lon))
+    w = np.where(wide, 180.0 + 10.0 * f(hg2, 8), w)
+    env = np.stack([minx, minx + w, lat, np.minimum(lat + hh, 90.0)], 1)
+    npts = (5 + (hg >> np.uint64(58)) % np.uint64(20)).astype(np.int64)
+    # geometry value: GPKG header [+ envelope] + WKB
+    elen = np.where(is_pt, 0, np.where(xyz, 48, 32))
+    glen = np.where(is_pt, 29, 8 + elen + 22 + 16 * npts)
+    G = np.zeros((n, 8 + 48 + 22), np.uint8)  # header + envelope + WKB head (the ring's xy follow)
+    G[:, 0], G[:, 1] = ord("G"), ord("P")
+    G[:, 3] = np.where(is_pt, np.where(empty, 0x11, 0x01), np.where(xyz, 0x05, 0x03))
+    G[:, 4:8] = np.array([4326], "<i4").view(np.uint8)
+    pxy = np.stack([lon, lat], 1)
+    pxy[empty] = np.nan
+    ptw = np.concatenate([np.frombuffer(b"\x01\x01\x00\x00\x00", np.uint8)[None, :].repeat(n, 0),
+                          pxy.astype("<f8").view(np.uint8).reshape(n, 16)], 1)
+    envb = env.astype("<f8").view(np.uint8).reshape(n, 32)
+    zb = np.stack([np.zeros(n), np.ones(n)], 1).astype("<f8").view(np.uint8).reshape(n, 16)
+    G[:, 8:40] = np.where(is_pt[:, None], 0, envb)
+    G[:, 40:56] = np.where(xyz[:, None], zb, 0)
+    wk = np.zeros((n, 22), np.uint8)
+    wk[:, :18] = np.frombuffer(b"\x01\x06\x00\x00\x00\x01\x00\x00\x00\x01\x03\x00\x00\x00\x01\x00\x00\x00", np.uint8)
+    wk[:, 18:22] = npts.astype("<u4").view(np.uint8).reshape(n, 4)
+    # points: the WKB right after the 8-B header; polygons: after the envelope
+    head = np.zeros((n, 78), np.uint8)
+    head[:, :8] = G[:, :8]
+    head[:, 8:29] = np.where(is_pt[:, None], ptw, 0)
+    pe = (8 + elen)
+    cols = np.arange(78)[None, :]
+    for k in range(48):  # polygon envelope bytes
+        sel = ~is_pt & (k < elen)
+        head[sel, 8 + k] = G[sel, 8 + k]
+    for k in range(22):
+        sel = ~is_pt
+        head[np.nonzero(sel)[0], (pe[sel] + k)] = wk[sel, k]
+    hlen = np.where(is_pt, 29, pe + 22)
+    maxp = int(npts.max()) if n else 0
+    kk = np.arange(2 * maxp, dtype=np.float64)[None, :]
+    ring = np.where(kk % 2 == 0, env[:, 0:1] + (env[:, 1:2] - env[:, 0:1]) * ((kk * 0.37) % 1.0),
+                    env[:, 2:3] + (env[:, 3:4] - env[:, 2:3]) * ((kk * 0.61) % 1.0))
+    ringb = ring.astype("<f8").view(np.uint8).reshape(n, 16 * maxp)
+    rlen = np.where(is_pt, 0, 16 * npts)
+    ext = np.zeros((n, 4), np.uint8)
+    small = glen <= 255
+    ext[:, 0] = np.where(small, 0xC7, 0xC8)
+    ext[:, 1] = np.where(small, glen, glen >> 8).astype(np.uint8)
+    ext[:, 2] = np.where(small, 0x47, glen & 0xFF).astype(np.uint8)
+    ext[:, 3] = 0x47
+    extlen = np.where(small, 3, 4)
+    # attributes (as polygon_blobs): date string, survey reference str|nil, adjusted_nodes u32
+    yy = 2000 + (ha % np.uint64(25)).astype(np.int64)
+    mo = 1 + ((ha >> np.uint64(8)) % np.uint64(12)).astype(np.int64)
+    dd = 1 + ((ha >> np.uint64(16)) % np.uint64(28)).astype(np.int64)
+    dig = lambda v, w_: [(v // 10 ** (w_ - 1 - j)) % 10 + 48 for j in range(w_)]
+    date = np.stack([np.full(n, 0xB4)] + dig(yy, 4) + [np.full(n, 45)] + dig(mo, 2) + [np.full(n, 45)] + dig(dd, 2) +
+                    [np.full(n, ord(c)) for c in "T12:00:00Z"], 1).astype(np.uint8)
+    has_ref = ((ha2 >> np.uint64(7)) & np.uint64(3)) != 0
+    rl = (8 + (ha2 >> np.uint64(20)) % np.uint64(9)).astype(np.int64)
+    ref = np.zeros((n, 17), np.uint8)
+    ref[:, 0] = np.where(has_ref, 0xA0 | rl, 0xC0)
+    ref[:, 1:] = (splitmix64(ha2[:, None] ^ np.arange(16, dtype=np.uint64)[None, :]) % np.uint64(26)).astype(np.uint8) + 65
+    reflen = np.where(has_ref, 1 + rl, 1)
+    nodes = np.concatenate([np.full((n, 1), 0xCE, np.uint8),
+                            ((ha2 >> np.uint64(32)) & np.uint64(0xFFFFF)).astype(">u4").view(np.uint8).reshape(n, 4)], 1)
+    lead = np.frombuffer(b"\x92\xd9\x28" + legend_hex.encode() + b"\x94", np.uint8)[None, :].repeat(n, 0)
+    return _concat_segments([(lead, np.full(n, 44)), (ext, extlen), (head, hlen), (ringb, rlen),
+                             (date, np.full(n, 21)), (ref, reflen), (nodes, np.full(n, 5))], n)
+
+
+def c5_layer(n, seed=SEED, shard=None, batch=1 << 20):
+    """C5: n int-PK features of mixed geometries (mixed_blobs) and n // 100 inserts, the C3 edit plan
+    (4 % geometry + 4 % attribute updates, 1 % deletes, 1 % inserts); both sides in git tree (= key)
+    order; blobs materialised for every delta's old and new version (what the filtered diff reads)."""
+    schema = Schema.from_column_dicts(MIXED_SCHEMA)
+    legend = Legend(["g-fid"], [c["id"] for c in MIXED_SCHEMA[1:]])
+    lh = legend.hexhash()
+    n_ins = n // 100
+    n_pks = n + n_ins
+    r_lo, r_hi = shard_rank_range(*shard, n_pks) if shard else (0, 1 << 24)
+    allp = walkkey.walk_order_pks(n_pks, r_lo, r_hi)
+    is_b = allp < n
+    plan = np.zeros(allp.shape[0], np.uint8)
+    plan[is_b] = c3_plan(allp[is_b], n)
+    in_t = ~is_b | (plan != 3)
+    bpos, tpos = np.cumsum(is_b) - 1, np.cumsum(in_t) - 1
+    pks, t_pk = allp[is_b], allp[in_t]
+    gver = (plan == 1).astype(np.uint64)
+    aver = (plan == 2).astype(np.uint64)
+    ver_t = np.where(is_b, gver | (aver << np.uint64(1)), np.uint64(4))[in_t]
+    base = packing.PackedSide(key=walkkey.int_keys(pks), oid=synth_oids(pks, np.zeros(pks.shape[0], np.uint64)),
+                              key_mode=0, order=np.arange(pks.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
+    target = packing.PackedSide(key=walkkey.int_keys(t_pk), oid=synth_oids(t_pk, ver_t), key_mode=0,
+                                order=np.arange(t_pk.shape[0], dtype=np.int64), encoding=packing.INT_PK_ENCODING)
+    upd = (plan == 1) | (plan == 2)
+
+    def blobs(idx_pk, gv, av):
+        parts, offs = [], [np.zeros(1, np.uint64)]
+        for s in range(0, idx_pk.shape[0], batch):
+            d, o = mixed_blobs(idx_pk[s:s + batch], gv[s:s + batch], av[s:s + batch], lh, seed)
+            parts.append(d)
+            offs.append(o[1:] + offs[-1][-1])
+        return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), np.concatenate(offs)
+
+    bw = np.nonzero(upd | (plan == 3))[0]
+    tw = np.nonzero(upd | ~is_b)[0]
+    bd, bo = blobs(allp[bw], np.zeros(bw.size, np.uint64), np.zeros(bw.size, np.uint64))
+    td, to = blobs(allp[tw], gver[tw], aver[tw])
+    bb = _sparse_arena(pks.shape[0], bpos[bw], bd, bo)
+    tb = _sparse_arena(t_pk.shape[0], tpos[tw], td, to)
+    return Layer(base, target, bb, tb, schema, {lh: legend}, int(np.count_nonzero(~is_b)), int(np.count_nonzero(upd)),
+                 int(np.count_nonzero(plan == 3)))
+
+
+# ---------------------------------------------------------------------------------------------
 # C4: string-PK attribute table, three-way merge (ancestor / ours / theirs)
 # ---------------------------------------------------------------------------------------------
 @dataclass

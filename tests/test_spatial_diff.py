@@ -271,6 +271,41 @@ def test_gpu_filter_pipeline_device_resident(engine, n, heads):
     assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [200_000, 3_000_000, pytest.param(100_000_000, marks=pytest.mark.timeout(900))])
+def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n):
+    """C5 as SURVEY §8(d) defines it (synth.c5_layer: 30 % points, EMPTY points, polygons straddling
+    +180, >= 180 degrees wide, starting on the filter's edge, XYZ envelopes the heads cannot decide):
+    classify2, the deltas' heads gathered into delta order on the device, the filter from them with
+    the blob fallback (kd_geom_filter_deltas) — codes, kept list and index envelopes bit-exact with
+    the oracle; the arena kernel gives the same answer"""
+    import types
+
+    from kart_amd import synth
+    from kart_amd.device import FilterPipeline
+
+    L = synth.c5_layer(n, seed=13)
+    ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
+    gc = S.GeomCols(ver, ver, "geom", "geom")
+    pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, gc, synth.C5_FILTER, False, 20,
+                          heads=True, delta_order=True)
+    pipe.step()
+    pipe.step()
+    counts, delta, codes, keep, enc, ok = pipe.results()
+    assert (counts["inserts"], counts["updates"], counts["deletes"]) == (L.n_insert, L.n_update, L.n_delete)
+    cols = {h: 0 for h in L.legends}  # the geometry is the first non-pk value
+    (od, oo), (nd, no) = L.base_blobs, L.target_blobs
+    oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta, cols, cols, synth.C5_FILTER, False, 20)
+    assert np.array_equal(codes, oc) and np.array_equal(keep, okeep) and counts["kept"] == len(okeep)
+    assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1])
+    # the mix reaches every branch: candidates, points, and heads that needed their blob
+    heads = pipe.heads_host
+    st = [h["goff_status"] >> 24 for h in heads]
+    assert 0 < len(keep) and (oc == 1).any()
+    flags = np.concatenate([h["gpkg"][:, 3][s == 0] for h, s in zip(heads, st)])
+    assert (flags == 0x01).any() and (flags == 0x11).any() and (flags == 0x05).any()
+
+
 @pytest.mark.parametrize("bits", [20, 16])
 def test_oracle_geom_filter_c_equals_python(bits):
     """the C restatement of the filtered diff's per-side decision (kdo_geom_filter, what the
