@@ -1,10 +1,18 @@
-/* kd_pystr.c — CPython helper for the writer formatting path (host code, no GPU): the per-value
- * str objects of one ASCII output buffer (kd_hex_encode's hex), built straight from the buffer
- * with PyUnicode_New + memcpy — no decode of the whole buffer into one str and no slice object per
- * value.  ascii_slices(buf, lo, hi) -> [buf[lo[i]:hi[i]] as str for every i]; lo / hi are int64
- * buffers of equal length, every range inside buf, every byte < 0x80 (the hex alphabet). */
+/* kd_pystr.c — CPython helpers of the drop-in's host side (no GPU):
+ *
+ * ascii_slices(buf, lo, hi) — the writer formatting path: the per-value str objects of one ASCII
+ *   output buffer (kd_hex_encode's hex), built straight from the buffer with PyUnicode_New + memcpy
+ *   — no decode of the whole buffer into one str and no slice object per value.  lo / hi are int64
+ *   buffers of equal length, every range inside buf, every byte < 0x80 (the hex alphabet).
+ *
+ * build_deltas(...) — the object side of RichBaseDataset.diff_feature (kart/rich_base_dataset.py:
+ *   240-300) for a whole delta list at once: per delta the lazy blob of each present side, the
+ *   promise partial(get_feature_from_blob, blob) (kart/base_dataset.py:506-507: no blob is read and
+ *   get_feature is not called here), the two KeyValue halves and the Delta
+ *   (kart/diff_structs.py:12-40,47-80), built in C with the slots filled directly. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <structmember.h>
 #include <string.h>
 
 static PyObject* ascii_slices(PyObject* self, PyObject* args) {
@@ -44,8 +52,245 @@ done:
     return out;
 }
 
+/* the byte offset of a __slots__ member of a Python class (its member descriptor) */
+static Py_ssize_t slot_offset(PyObject* type, const char* name) {
+    PyObject* d = PyObject_GetAttrString(type, name);
+    if (!d) return -1;
+    Py_ssize_t off = -1;
+    if (Py_TYPE(d) == &PyMemberDescr_Type) off = ((PyMemberDescrObject*)d)->d_member->offset;
+    else PyErr_Format(PyExc_TypeError, "%s is not a __slots__ member", name);
+    Py_DECREF(d);
+    return off;
+}
+
+static inline void set_slot(PyObject* obj, Py_ssize_t off, PyObject* v) {  /* steals v */
+    PyObject** p = (PyObject**)((char*)obj + off);
+    PyObject* old = *p;
+    *p = v;
+    Py_XDECREF(old);
+}
+
+/* functools.partial(fn, arg) built directly: the partial's func / args / keywords members (their
+ * member-descriptor offsets) and its vectorcall entry (the type's tp_vectorcall_offset) filled as
+ * partial_new fills them, copied from a template made by the constructor for the same fn. */
+typedef struct {
+    PyTypeObject* type;
+    Py_ssize_t fn, args, kwoff, vc;
+    void* vcfunc;
+    PyObject* kw;  /* the keywords dict all direct partials of one call share: empty, never written
+                    * (Kart reads .keywords of a promise nowhere; partial_call copies it when non-empty) */
+    int direct;
+} PartialMaker;
+
+static int partial_maker_init(PartialMaker* m, PyObject* pt, PyObject* fn) {
+    memset(m, 0, sizeof(*m));
+    m->type = (PyTypeObject*)pt;
+    if (!fn || fn == Py_None) return 0;
+    PyObject* tmpl = PyObject_CallFunctionObjArgs(pt, fn, Py_None, NULL);
+    if (!tmpl) return -1;
+    m->fn = slot_offset(pt, "func");
+    m->args = slot_offset(pt, "args");
+    m->kwoff = slot_offset(pt, "keywords");
+    if (m->fn < 0 || m->args < 0 || m->kwoff < 0) {
+        PyErr_Clear();  /* not CPython's partial layout: go through the constructor */
+        Py_DECREF(tmpl);
+        return 0;
+    }
+    m->vc = m->type->tp_vectorcall_offset;
+    PyObject** f = (PyObject**)((char*)tmpl + m->fn);
+    PyObject** a = (PyObject**)((char*)tmpl + m->args);
+    PyObject** k = (PyObject**)((char*)tmpl + m->kwoff);
+    m->direct = Py_TYPE(tmpl) == m->type && *f == fn && PyTuple_CheckExact(*a) && PyTuple_GET_SIZE(*a) == 1 &&
+                PyTuple_GET_ITEM(*a, 0) == Py_None && PyDict_CheckExact(*k) && PyDict_GET_SIZE(*k) == 0 &&
+                m->type->tp_dictoffset >= 0;
+    if (m->vc > 0) m->vcfunc = *(void**)((char*)tmpl + m->vc);
+    Py_DECREF(tmpl);
+    if (m->direct && !(m->kw = PyDict_New())) return -1;
+    return 0;
+}
+
+static PyObject* partial_make(const PartialMaker* m, PyObject* fn, PyObject* arg) {
+    if (!m->direct) return PyObject_CallFunctionObjArgs((PyObject*)m->type, fn, arg, NULL);
+    PyObject* args = PyTuple_Pack(1, arg);
+    PyObject* p = m->type->tp_alloc(m->type, 0);
+    if (!args || !p) {
+        Py_XDECREF(args); Py_XDECREF(p);
+        return NULL;
+    }
+    PyObject* kw = m->kw;
+    Py_INCREF(kw);
+    Py_INCREF(fn);
+    set_slot(p, m->fn, fn);
+    set_slot(p, m->args, args);
+    set_slot(p, m->kwoff, kw);
+    if (m->vc > 0) *(void**)((char*)p + m->vc) = m->vcfunc;
+    return p;
+}
+
+/* pk i of an int64 buffer or a list */
+static PyObject* pk_at(PyObject* list, const long long* arr, Py_ssize_t i) {
+    if (list) {
+        PyObject* x = PyList_GET_ITEM(list, i);
+        Py_INCREF(x);
+        return x;
+    }
+    return PyLong_FromLongLong(arr[i]);
+}
+
+/* build_deltas(delta_type, kv_type, blob_type, partial_type, old_get, new_get, old_src, new_src,
+ *              old_leaf, new_leaf, old_pk, new_pk, own)
+ * old_leaf / new_leaf: int64 buffers of n leaf indices (-1: the side is absent); old_pk / new_pk: int64
+ * buffers or lists of n pks (entries of absent sides unused).  own: delta_type / kv_type are
+ * kart_amd.deltas' own classes (Delta filled field by field, KeyValue's slots directly), else the
+ * halves are (pk, promise) tuples passed to delta_type(old, new).  blob_type is kart_amd.dataset's
+ * LazyBlob (slots _src, _i, _data).
+ * Returns (keys, deltas, upd_rows, upd_deltas, upd_keys): the key of each delta (old pk, else new pk)
+ * and the delta, and the updates' row numbers, deltas and keys. */
+static PyObject* build_deltas(PyObject* self, PyObject* args) {
+    PyObject *dt, *kvt, *bt, *pt, *og, *ng, *os_, *ns, *ol_o, *nl_o, *op_o, *np_o;
+    int own;
+    if (!PyArg_ParseTuple(args, "OOOOOOOOOOOOp", &dt, &kvt, &bt, &pt, &og, &ng, &os_, &ns, &ol_o, &nl_o, &op_o, &np_o, &own))
+        return NULL;
+    Py_buffer ol = {0}, nl = {0}, opb = {0}, npb = {0};
+    PyObject *keys = NULL, *dl = NULL, *urows = NULL, *udl = NULL, *ukeys = NULL, *ret = NULL;
+    PyObject *t_ins = NULL, *t_upd = NULL, *t_del = NULL;
+    PartialMaker pm[2];
+    memset(pm, 0, sizeof(pm));
+    PyObject *zero = NULL;
+    if (PyObject_GetBuffer(ol_o, &ol, PyBUF_C_CONTIGUOUS) < 0) goto fail;
+    if (PyObject_GetBuffer(nl_o, &nl, PyBUF_C_CONTIGUOUS) < 0) goto fail;
+    const Py_ssize_t n = ol.len / 8;
+    if (ol.len != nl.len || ol.len % 8) { PyErr_SetString(PyExc_ValueError, "build_deltas: leaf arrays"); goto fail; }
+    PyObject* op_list = PyList_Check(op_o) ? op_o : NULL;
+    PyObject* np_list = PyList_Check(np_o) ? np_o : NULL;
+    if (!op_list && PyObject_GetBuffer(op_o, &opb, PyBUF_C_CONTIGUOUS) < 0) goto fail;
+    if (!np_list && PyObject_GetBuffer(np_o, &npb, PyBUF_C_CONTIGUOUS) < 0) goto fail;
+    if ((op_list ? PyList_GET_SIZE(op_list) : opb.len / 8) != n || (np_list ? PyList_GET_SIZE(np_list) : npb.len / 8) != n) {
+        PyErr_SetString(PyExc_ValueError, "build_deltas: pk arrays");
+        goto fail;
+    }
+    const long long* olp = (const long long*)ol.buf;
+    const long long* nlp = (const long long*)nl.buf;
+    const long long* opp = (const long long*)opb.buf;
+    const long long* npp = (const long long*)npb.buf;
+    const Py_ssize_t b_src = slot_offset(bt, "_src"), b_i = slot_offset(bt, "_i"), b_data = slot_offset(bt, "_data");
+    if (b_src < 0 || b_i < 0 || b_data < 0) goto fail;
+    Py_ssize_t kv_key = -1, kv_val = -1, d_old = -1, d_new = -1, d_type = -1, d_flags = -1;
+    if (own) {
+        kv_key = slot_offset(kvt, "key");
+        kv_val = slot_offset(kvt, "value");
+        d_old = slot_offset(dt, "old");
+        d_new = slot_offset(dt, "new");
+        d_type = slot_offset(dt, "type");
+        d_flags = slot_offset(dt, "flags");
+        if (kv_key < 0 || kv_val < 0 || d_old < 0 || d_new < 0 || d_type < 0 || d_flags < 0) goto fail;
+    }
+    if (partial_maker_init(&pm[0], pt, og) < 0 || partial_maker_init(&pm[1], pt, ng) < 0) goto fail;
+    t_ins = PyUnicode_InternFromString("insert"); t_upd = PyUnicode_InternFromString("update");
+    t_del = PyUnicode_InternFromString("delete");
+    zero = PyLong_FromLong(0);
+    if (!t_ins || !t_upd || !t_del || !zero) goto fail;
+    keys = PyList_New(n); dl = PyList_New(n);
+    urows = PyList_New(0); udl = PyList_New(0); ukeys = PyList_New(0);
+    if (!keys || !dl || !urows || !udl || !ukeys) goto fail;
+    PyTypeObject* BT = (PyTypeObject*)bt;
+    PyTypeObject* KT = (PyTypeObject*)kvt;
+    PyTypeObject* DT = (PyTypeObject*)dt;
+    for (Py_ssize_t i = 0; i < n; i++) {
+        PyObject* half[2] = {NULL, NULL};
+        PyObject* pkv[2] = {NULL, NULL};
+        const long long leaf[2] = {olp[i], nlp[i]};
+        if (leaf[0] < 0 && leaf[1] < 0) {
+            PyErr_Format(PyExc_ValueError, "build_deltas: row %zd has neither side (Empty Delta)", i);
+            goto fail;
+        }
+        for (int s = 0; s < 2; s++) {
+            if (leaf[s] < 0) continue;
+            PyObject* pk;
+            if (s && pkv[0] && !np_list && !op_list && npp[i] == opp[i]) {  /* an update: one int for both keys */
+                pk = pkv[0];
+                Py_INCREF(pk);
+            } else {
+                pk = pk_at(s ? np_list : op_list, s ? npp : opp, i);
+            }
+            PyObject* blob = BT->tp_alloc(BT, 0);
+            PyObject* li = PyLong_FromLongLong(leaf[s]);
+            if (!pk || !blob || !li) { Py_XDECREF(pk); Py_XDECREF(blob); Py_XDECREF(li); goto item_fail; }
+            PyObject* src = s ? ns : os_;
+            Py_INCREF(src);
+            set_slot(blob, b_src, src);
+            set_slot(blob, b_i, li);
+            Py_INCREF(Py_None);
+            set_slot(blob, b_data, Py_None);
+            PyObject* promise = partial_make(&pm[s], s ? ng : og, blob);
+            Py_DECREF(blob);
+            if (!promise) { Py_DECREF(pk); goto item_fail; }
+            pkv[s] = pk;
+            if (own) {
+                PyObject* kv = KT->tp_alloc(KT, 0);
+                if (!kv) { Py_DECREF(promise); goto item_fail; }
+                Py_INCREF(pk);
+                set_slot(kv, kv_key, pk);
+                set_slot(kv, kv_val, promise);
+                half[s] = kv;
+            } else {
+                half[s] = PyTuple_Pack(2, pk, promise);
+                Py_DECREF(promise);
+                if (!half[s]) goto item_fail;
+            }
+            continue;
+        item_fail:
+            Py_XDECREF(half[0]); Py_XDECREF(half[1]); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]);
+            goto fail;
+        }
+        PyObject* d;
+        if (own) {
+            d = DT->tp_alloc(DT, 0);
+            if (!d) { Py_XDECREF(half[0]); Py_XDECREF(half[1]); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]); goto fail; }
+            PyObject* ty = !half[0] ? t_ins : !half[1] ? t_del : t_upd;
+            Py_INCREF(ty);
+            set_slot(d, d_type, ty);
+            Py_INCREF(zero);
+            set_slot(d, d_flags, zero);
+            set_slot(d, d_old, half[0] ? half[0] : (Py_INCREF(Py_None), Py_None));
+            set_slot(d, d_new, half[1] ? half[1] : (Py_INCREF(Py_None), Py_None));
+            half[0] = half[1] = NULL;  /* owned by the delta now */
+        } else {
+            d = PyObject_CallFunctionObjArgs(dt, half[0] ? half[0] : Py_None, half[1] ? half[1] : Py_None, NULL);
+            if (!d) { Py_XDECREF(half[0]); Py_XDECREF(half[1]); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]); goto fail; }
+        }
+        Py_XDECREF(half[0]);
+        Py_XDECREF(half[1]);
+        PyObject* key = pkv[0] ? pkv[0] : pkv[1];
+        Py_INCREF(key);
+        PyList_SET_ITEM(keys, i, key);
+        Py_INCREF(d);
+        PyList_SET_ITEM(dl, i, d);
+        if (pkv[0] && pkv[1]) {
+            PyObject* r = PyLong_FromSsize_t(i);
+            int e = !r || PyList_Append(urows, r) < 0 || PyList_Append(udl, d) < 0 || PyList_Append(ukeys, pkv[0]) < 0;
+            Py_XDECREF(r);
+            if (e) { Py_DECREF(d); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]); goto fail; }
+        }
+        Py_DECREF(d);
+        Py_XDECREF(pkv[0]);
+        Py_XDECREF(pkv[1]);
+    }
+    ret = PyTuple_Pack(5, keys, dl, urows, udl, ukeys);
+fail:
+    Py_XDECREF(keys); Py_XDECREF(dl); Py_XDECREF(urows); Py_XDECREF(udl); Py_XDECREF(ukeys);
+    Py_XDECREF(t_ins); Py_XDECREF(t_upd); Py_XDECREF(t_del); Py_XDECREF(zero);
+    Py_XDECREF(pm[0].kw); Py_XDECREF(pm[1].kw);
+    if (ol.obj) PyBuffer_Release(&ol);
+    if (nl.obj) PyBuffer_Release(&nl);
+    if (opb.obj) PyBuffer_Release(&opb);
+    if (npb.obj) PyBuffer_Release(&npb);
+    return ret;
+}
+
 static PyMethodDef methods[] = {
     {"ascii_slices", ascii_slices, METH_VARARGS, "str per [lo, hi) range of an ASCII buffer"},
+    {"build_deltas", build_deltas, METH_VARARGS, "Delta objects with lazy promises for a whole delta list"},
     {NULL, NULL, 0, NULL},
 };
 

@@ -619,7 +619,6 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
                 bad |= v == k ? 1u : 0u;
                 left++;
             }
-            if (left >= RS_SEG_MAX) bad |= 4u;
         }
         stop = false;
         for (u64 q = i + 1; q < ghi && !stop; q++) {  // later entries, from LDS
@@ -634,8 +633,8 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
                 rank += v < k;
                 right++;
             }
-            if (right >= RS_SEG_MAX) bad |= 4u;
         }
+        if (left + right >= (u32)RS_SEG_MAX) bad |= 4u;  // the segment is longer than RS_SEG_MAX
         const u64 dst = i - left + rank;
         if (dst < n) {
             kout[dst] = k;

@@ -52,7 +52,11 @@ class KeyValue:
 
 
 class Delta:
-    """old -> new change of one object; either side may be None (insert / delete)."""
+    """old -> new change of one object; either side may be None (insert / delete).  The fields are
+    slots (filled directly by the native delta builder, kart_amd/csrc/kd_pystr.c); ``__dict__`` keeps
+    other attributes settable as on the reference's class."""
+
+    __slots__ = ("old", "new", "type", "flags", "changed_fields", "__dict__")
 
     def __init__(self, old, new):
         self.old = old = KeyValue.of(old)

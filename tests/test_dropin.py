@@ -358,3 +358,81 @@ def test_gc_pause_leaves_collector_state():
     finally:
         gc.enable()
     assert len(built) == len(more) == 1000
+
+
+def _delta_view(fd):
+    out = {}
+    for k, d in fd.items():
+        halves = []
+        for kv in (d.old, d.new):
+            if kv is None:
+                halves.append(None)
+                continue
+            blob = kv.value.args[0]
+            halves.append((kv.key, type(blob).__name__, blob._i, blob._src is not None, kv.value.func.__name__))
+        out[k] = (d.type, d.flags, tuple(halves))
+    return out
+
+
+@pytest.mark.parametrize("name", ["repo_points", "repo_string_pks", "synth_str", "conflicts_table"])
+def test_native_delta_builder_matches_python_loop(eng, name, monkeypatch):
+    """the C delta builder (kart_amd/csrc/kd_pystr.c build_deltas) yields the deltas the Python
+    loop builds: same keys, types, flags, KeyValue halves, partial(get_feature_from_blob, LazyBlob)
+    promises over the same leaves and the same update batch; values equal and stay lazy"""
+    assert D._pystr is not None, "kart_amd/_kd_pystr was not built (make -C kart_amd/csrc)"
+    fx = load(name)
+    for case in fx.cases("diff2")[:3]:
+        got = {}
+        for native in (True, False):
+            if not native:
+                monkeypatch.setattr(D, "_pystr", None)
+            base, target = version(fx, case["base"]), version(fx, case["target"])
+            ds = D.get_dataset_diff(eng, base, target)
+            fd = ds.get("feature") or structs().DeltaDiff()
+            b = getattr(fd, "_kd_updates", None)
+            got[native] = (_delta_view(fd), [(k, d.old_value, d.new_value) for k, d in fd.sorted_items()][:50],
+                           None if b is None else (b.keys, [id(x) in {id(y) for y in fd.values()} for x in b.deltas],
+                                                   b.old_leaf.tolist(), b.new_leaf.tolist(), b.n_total))
+            monkeypatch.undo()
+        assert got[True] == got[False]
+    # generator form (diff_feature without _collect) and reverse through the builder
+    old, new = version(fx, fx.cases("diff2")[0]["base"]), version(fx, fx.cases("diff2")[0]["target"])
+    if old is not None and new is not None:
+        fwd = structs().DeltaDiff(D.diff_feature(eng, old, new))
+        rev = structs().DeltaDiff(D.diff_feature(eng, new, old, reverse=True))
+        assert _delta_view(fwd) == _delta_view(rev)
+
+
+def test_native_delta_builder_kart_structs_path(monkeypatch):
+    """own=False: halves handed to the Delta constructor as (pk, promise) tuples, as for
+    kart.diff_structs"""
+    import functools
+
+    from kart_amd import _kd_pystr as P
+    from kart_amd import deltas as DL
+
+    calls = []
+
+    class KD:
+        def __init__(self, old, new):
+            calls.append((old, new))
+            self.old, self.new = old, new
+
+    class V:
+        def get_feature_from_blob(self, blob):
+            return blob._i
+
+    ov, nv = V(), V()
+    ol = np.array([3, -1, 5], np.int64)
+    nl = np.array([-1, 4, 6], np.int64)
+    r = P.build_deltas(KD, DL.KeyValue, D.LazyBlob, functools.partial, ov.get_feature_from_blob,
+                       nv.get_feature_from_blob, ov, nv, ol, nl, ["a", None, "c"], [None, "b", "c"], False)
+    keys, deltas, rows, upd, ukeys = r
+    assert keys == ["a", "b", "c"] and rows == [2] and ukeys == ["c"] and upd == [deltas[2]]
+    assert calls[0][1] is None and calls[1][0] is None
+    assert [c[0][0] if c[0] else None for c in calls] == ["a", None, "c"]
+    assert [c[1][1]() if c[1] else None for c in calls] == [None, 4, 6]
+    with pytest.raises(ValueError):
+        P.build_deltas(DL.Delta, DL.KeyValue, D.LazyBlob, functools.partial, None, None, ov, nv,
+                       np.array([-1], np.int64), np.array([-1], np.int64), np.zeros(1, np.int64),
+                       np.zeros(1, np.int64), True)
