@@ -118,6 +118,7 @@ class Harness:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.dist = None
+        self.comm = None  # set by engine_for
         if self.world > 1:
             import torch.distributed as dist
 
@@ -162,6 +163,15 @@ def engine_for(H):
     if H.world > 1:  # the library's own RCCL communicator; the id travels over the harness
         uid = H.bcast(Engine.comm_unique_id() if H.rank == 0 else None)
         eng.comm_init(H.world, H.rank, uid)
+        # the communicator's own count (ncclCommCount) and every rank's (rank, device) as RCCL sees
+        # them: the JSON line shows that N ranks joined one communicator
+        info = eng.comm_info()
+        views = H.allgather((info["count"], info["rank"], info["device"]))
+        H.comm = {"backend": "rccl", "ncclCommCount": info["count"],
+                  "ranks": [v[1] for v in views], "devices": [v[2] for v in views],
+                  "all_ranks_agree": all(v[0] == H.world for v in views)}
+    else:
+        H.comm = {"backend": None, "ncclCommCount": None, "ranks": [0]}
     return eng
 
 
@@ -344,7 +354,7 @@ def run_diff(args, H, polygons):
         "metric": METRIC,
         "value": round(total_pairs * args.steps / elapsed / 1e6, 2),
         "unit": "M feature-pairs/s",
-        "n_gpus": world,
+        "n_gpus": world, "rccl_comm": H.comm,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -780,7 +790,7 @@ def run_c5(args, H):
     eng.close()
     out = {
         "metric": METRIC, "value": round(total_pairs * args.steps / elapsed / 1e6, 2), "unit": "M feature-pairs/s",
-        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": H.world, "rccl_comm": H.comm, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong" if H.world > 1 else "weak", "vs_baseline": None,
         "dtype": "u8/u64 (integer join) + f64 (envelopes, EnvelopeEncoder)",
@@ -947,7 +957,7 @@ def run_c5env(args, H):
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M geometries/s",
-        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": H.world, "rccl_comm": H.comm, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64 (envelopes, EnvelopeEncoder) + u8",
         "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
@@ -1117,7 +1127,7 @@ def run_c6(args, H):
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M geometries/s",
-        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": H.world, "rccl_comm": H.comm, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded GPKG geometries: 30% points, 70% multipolygons, EPSG:4326)",
@@ -1239,7 +1249,7 @@ def run_c4(args, H):
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M entries/s",
-        "n_gpus": H.world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": H.world, "rccl_comm": H.comm, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8/u64 (integer)",
         "data": "synthetic (seeded string-PK table: MsgpackHashPathEncoder paths in git tree order, synthetic OIDs)",

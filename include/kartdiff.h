@@ -385,6 +385,9 @@ int kd_device_sync(kd_ctx* ctx);                           /* hipDeviceSynchroni
 int kd_comm_unique_id(uint8_t id[KD_COMM_ID_BYTES]);
 int kd_comm_init(kd_ctx* ctx, int nranks, int rank, const uint8_t id[KD_COMM_ID_BYTES]);
 int kd_comm_fini(kd_ctx* ctx);
+/* the communicator's own view, from RCCL: out[0] = ncclCommCount (ranks that joined), out[1] =
+ * ncclCommUserRank, out[2] = ncclCommCuDevice (the HIP device it drives) */
+int kd_comm_info(kd_ctx* ctx, int32_t out[3]);
 /* d_recv[nranks * n] <- every rank's d_send[n] (device buffers, context stream) */
 int kd_allgather_u64(kd_ctx* ctx, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);
 /* One rank's step of a sharded diff: kd_diff2_device on this rank's shard (device sides holding

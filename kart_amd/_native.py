@@ -260,6 +260,7 @@ SIGNATURES = {
     "kd_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "kd_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "kd_comm_fini": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "kd_allgather_u64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "kd_diff2_gather": (
         ctypes.c_int,

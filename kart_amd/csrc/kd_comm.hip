@@ -25,6 +25,9 @@ struct Rccl {
     decltype(&ncclGroupStart) groupStart = nullptr;
     decltype(&ncclGroupEnd) groupEnd = nullptr;
     decltype(&ncclGetErrorString) errorString = nullptr;
+    decltype(&ncclCommCount) commCount = nullptr;
+    decltype(&ncclCommUserRank) commUserRank = nullptr;
+    decltype(&ncclCommCuDevice) commDevice = nullptr;
 };
 static Rccl g_rccl;
 static std::mutex g_rccl_m;
@@ -45,9 +48,13 @@ static int rccl(Rccl** out) {
         KD_SYM(groupStart, "ncclGroupStart");
         KD_SYM(groupEnd, "ncclGroupEnd");
         KD_SYM(errorString, "ncclGetErrorString");
+        KD_SYM(commCount, "ncclCommCount");
+        KD_SYM(commUserRank, "ncclCommUserRank");
+        KD_SYM(commDevice, "ncclCommCuDevice");
 #undef KD_SYM
         if (!g_rccl.getUniqueId || !g_rccl.commInitRank || !g_rccl.commInitAll || !g_rccl.commDestroy ||
-            !g_rccl.allGather || !g_rccl.groupStart || !g_rccl.groupEnd || !g_rccl.errorString) {
+            !g_rccl.allGather || !g_rccl.groupStart || !g_rccl.groupEnd || !g_rccl.errorString || !g_rccl.commCount ||
+            !g_rccl.commUserRank || !g_rccl.commDevice) {
             set_error("RCCL: missing symbols");
             dlclose(g_rccl.h);
             g_rccl.h = nullptr;
@@ -206,6 +213,22 @@ int kd_comm_init(kd_ctx* ctx, int nranks, int rank, const uint8_t id[KD_COMM_ID_
     ctx->comm = c;
     ctx->nranks = nranks;
     ctx->rank = rank;
+    return KD_OK;
+}
+
+int kd_comm_info(kd_ctx* ctx, int32_t out[3]) {
+    KD_CHECK(ctx && out, "kd_comm_info: NULL");
+    KD_CHECK(ctx->comm, "kd_comm_info: no communicator (kd_comm_init)");
+    Rccl* R;
+    int rc;
+    if ((rc = rccl(&R))) return rc;
+    int count = 0, rank = -1, dev = -1;
+    KD_NCCL(R, R->commCount((ncclComm_t)ctx->comm, &count));
+    KD_NCCL(R, R->commUserRank((ncclComm_t)ctx->comm, &rank));
+    KD_NCCL(R, R->commDevice((ncclComm_t)ctx->comm, &dev));
+    out[0] = count;
+    out[1] = rank;
+    out[2] = dev;
     return KD_OK;
 }
 

@@ -85,6 +85,13 @@ class Engine:
         N.check(self.L.kd_comm_init(self.ctx, int(nranks), int(rank), buf), "kd_comm_init")
         self.nranks, self.rank = int(nranks), int(rank)
 
+    def comm_info(self):
+        """{"count": ncclCommCount, "rank": ncclCommUserRank, "device": ncclCommCuDevice} of the
+        library's communicator"""
+        out = (ctypes.c_int32 * 3)()
+        N.check(self.L.kd_comm_info(self.ctx, out), "kd_comm_info")
+        return {"count": int(out[0]), "rank": int(out[1]), "device": int(out[2])}
+
     def comm_fini(self):
         N.check(self.L.kd_comm_fini(self.ctx), "kd_comm_fini")
 
