@@ -25,6 +25,7 @@
 //      shift), and ORs the changed keys into the owners' masks in LDS.
 // Payloads of unequal length are "changed" without reading them.  Tables too large for LDS take
 // k_fielddiff_g (one lane per update, everything from global memory).
+#include <cstdlib>
 #include <type_traits>
 
 #include "kd_internal.h"
@@ -583,7 +584,7 @@ __device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb
     const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
     if (oa != ~0u && ob != ~0u) return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
     const u64 xa = A.start + pa, xb = B.start + pb;
-    if (key < 64) {
+    if (q.cap && key < 64) {
         const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (t < q.cap) {
             q.task[3 * t] = xa;
@@ -820,7 +821,15 @@ constexpr u32 FD_TAB_LDS_MAX = 16384;
 #define KD_FD_SHAPE_S 32, 8, 3, 1, 16, 2  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
 #endif
 template <int UPR, int NH, int NTL, int TM, int TG, int TS>
-constexpr int fd_upr(const void*) { return UPR; }  // tables up to this size are copied into each block's LDS
+constexpr int fd_upr(const void*) { return UPR; }
+#ifndef KD_FD_SSHAPE
+#define KD_FD_SSHAPE 32, 16384  // streamed kernel: updates per tile, LDS bytes per side
+#endif
+#ifndef KD_FD_STREAM_DEFAULT
+#define KD_FD_STREAM_DEFAULT 0
+#endif
+template <int T, int CAPB>
+constexpr int fd_stream_t() { return T; }  // tables up to this size are copied into each block's LDS
 typedef __attribute__((address_space(3))) void* fd_lds_vp;
 typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 
@@ -1029,6 +1038,97 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
     }
 }
 
+// ================================================================================================
+// streamed variant (k_fielddiff_s): the updates' blobs lie back to back in update order (no pairs),
+// so a tile of T consecutive updates owns one contiguous byte span per side.  Each workgroup (one
+// wave) copies both spans whole into LDS by LDS-DMA — 16 B per lane, 1 KiB per instruction, the
+// bytes of the arena read exactly once — and every lane then parses its update straight from LDS:
+// headers, values and the payload compares, with no per-blob window descriptors, no offsets ->
+// window round trip and no payload re-read from HBM.  A tile whose span exceeds the buffer keeps
+// its first CAP bytes in LDS; the blobs past them are read from global memory.
+// ================================================================================================
+// one blob inside the tile image (or, past the buffer, in global memory only)
+struct SBlob {
+    u64 start;
+    u32 len;
+    u32 s0;    // start & 15: blob position p is at offset x = p + s0 from its aligned chunk
+    u32 img;   // LDS byte address of that chunk
+    bool res;  // every byte lies in the loaded part of the image
+    __device__ __forceinline__ u32 win(u32 x, u32) const { return res ? x : ~0u; }
+};
+
+template <int T, int CAPB>
+__global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od, const u64* __restrict__ ooff,
+                                                       const u8* __restrict__ nd, const u64* __restrict__ noff,
+                                                       u64 n_upd_host, const u64* __restrict__ n_upd_dev,
+                                                       FdTab tg, FdTabOff to, const u8* __restrict__ tab_base,
+                                                       u64* __restrict__ masks, u8* __restrict__ status) {
+    static_assert(T <= FD_NT && CAPB % 1024 == 0, "stream shape");
+    constexpr u32 CAPC = CAPB / 16;             // chunks loaded per side at most
+    __shared__ u32x4 s_img[2 * CAPC + 8];        // old span, new span (+ slack: reads past a blob's end)
+    __shared__ u32 s_dummy;
+    extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
+    const int lane = threadIdx.x;
+    const u64 n_upd = n_upd_dev ? min(*n_upd_dev, n_upd_host ? n_upd_host : ~0ull) : n_upd_host;
+    const u64 ntiles = (n_upd + T - 1) / T;
+    if ((u64)blockIdx.x >= ntiles) return;  // wave-uniform
+    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp128)(tab_base + i);
+    mp_tab_to_lds();
+    FdTabT<3> tb;
+    tb.n_keys = tg.n_keys; tb.words = tg.words; tb.n_lo = tg.n_lo; tb.n_ln = tg.n_ln; tb.maxv = tg.maxv;
+    typedef __attribute__((address_space(3))) u8* l8;
+    const l8 lt = (l8)s_tab;
+    tb.leg_o = (typename ASP<3, u32>::type)(lt + to.leg_o);
+    tb.leg_n = (typename ASP<3, u32>::type)(lt + to.leg_n);
+    tb.map_o = (typename ASP<3, i16>::type)(lt + to.map_o);
+    tb.map_n = (typename ASP<3, i16>::type)(lt + to.map_n);
+    tb.cmp = (typename ASP<3, u64>::type)(lt + to.cmp);
+    tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
+    tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
+    const FdQueue none{(lds_u64p) nullptr, (lds_u32p)&s_dummy, 0};  // payloads compare in place
+    const u32 img_o = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img;
+    const u32 img_n = img_o + 16 * CAPC;
+    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const u64 u0 = tile * T, ue = min(u0 + T, n_upd);
+        const u64 u = u0 + lane;
+        const bool act = lane < T && u < ue;
+        // the span of each side, and this lane's blob
+        const u64 so0 = ooff[u0], so1 = ooff[ue], sn0 = noff[u0], sn1 = noff[ue];
+        u64 os = 0, oe = 0, ns = 0, ne = 0;
+        if (act) {
+            os = ooff[u]; oe = ooff[u + 1];
+            ns = noff[u]; ne = noff[u + 1];
+        }
+        const u64 co = ((u64)od + so0) & ~(u64)15, cn = ((u64)nd + sn0) & ~(u64)15;
+        const u32 nco = (u32)min<u64>((((u64)od + so1) - co + 15) >> 4, CAPC);
+        const u32 ncn = (u32)min<u64>((((u64)nd + sn1) - cn + 15) >> 4, CAPC);
+        for (u32 k = 0; k < nco; k += FD_NT)
+            if (k + lane < nco)
+                __builtin_amdgcn_global_load_lds((fd_glb_vp)(co + 16ull * (k + lane)), (fd_lds_vp)(s_img + k), 16, 0, 0);
+        for (u32 k = 0; k < ncn; k += FD_NT)
+            if (k + lane < ncn)
+                __builtin_amdgcn_global_load_lds((fd_glb_vp)(cn + 16ull * (k + lane)), (fd_lds_vp)(s_img + CAPC + k), 16, 0, 0);
+        __syncthreads();  // vmcnt(0) + barrier: the spans have landed
+        if (act) {
+            SBlob A, B;
+            A.start = (u64)od + os; A.len = (u32)(oe - os); A.s0 = (u32)(A.start & 15);
+            A.img = img_o + (u32)((A.start & ~(u64)15) - co);
+            A.res = A.start + A.len <= co + 16ull * nco;
+            B.start = (u64)nd + ns; B.len = (u32)(ne - ns); B.s0 = (u32)(B.start & 15);
+            B.img = img_n + (u32)((B.start & ~(u64)15) - cn);
+            B.res = B.start + B.len <= cn + 16ull * ncn;
+            u64* m = masks + u * tb.words;
+            for (int w = 4; w < tb.words; w++) m[w] = 0;
+            u64 mk[4] = {0, 0, 0, 0};
+            u8 st = diff_one_w(A, B, tb, mk, m, none);
+            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+            store_masks(m, tb.words, mk, st);
+            status[u] = st;
+        }
+        __syncthreads();  // the image is free for the next tile
+    }
+}
+
 // Fallback for tables too large for LDS: one lane per update, blobs parsed straight from global
 // memory.
 __global__ __launch_bounds__(FD_NT) void k_fielddiff_g(const u8* __restrict__ od, const u64* __restrict__ ooff,
@@ -1172,9 +1272,15 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     // window shape from the typical blob: small features (points, ~90-150 B) fit a long head window
     // whole; larger ones (polygons) get head + tail windows around their geometry
     const bool small = typ <= 144;
+    // the streamed kernel: contiguous update arenas (no pairs) of larger blobs; KD_FD_STREAM=0/1
+    // forces it off / on (A/B)
+    const char* stream_e = getenv("KD_FD_STREAM");
+    const int stream_env = stream_e ? atoi(stream_e) : -1;
+    const bool stream = lds_tab && d_pu == nullptr && (stream_env >= 0 ? stream_env > 0 : !small && KD_FD_STREAM_DEFAULT);
     // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
     // calculator for this launch's LDS), capped at the measured optimum.
-    const void* kern = !lds_tab ? (const void*)k_fielddiff_g
+    const void* kern = stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE>
+                       : !lds_tab ? (const void*)k_fielddiff_g
                        : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
     int per_cu = 0;
     KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FD_NT, lds_tab ? o_end : 0));
@@ -1182,8 +1288,8 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
 #ifndef KD_FD_CAP
 #define KD_FD_CAP 12  // C2 points: 10 / 12 blocks per CU = 36.8 / 35.1 us (C3 is LDS-bound at 8)
 #endif
-    per_cu = std::max(1, std::min(per_cu, KD_FD_CAP));
-    const u64 upr = !lds_tab ? FD_NT : small ? fd_upr<KD_FD_SHAPE_S>(nullptr) : fd_upr<KD_FD_SHAPE_L>(nullptr);
+    per_cu = std::max(1, std::min(per_cu, stream ? 16 : KD_FD_CAP));
+    const u64 upr = stream ? (u64)fd_stream_t<KD_FD_SSHAPE>() : !lds_tab ? FD_NT : small ? fd_upr<KD_FD_SHAPE_S>(nullptr) : fd_upr<KD_FD_SHAPE_L>(nullptr);
     unsigned blocks = (unsigned)std::min<u64>((work + upr - 1) / upr, (u64)ctx->n_cu * (u64)per_cu);
     if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
@@ -1192,7 +1298,11 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
                                tb, to, (const u8*)dt, d_masks, d_status);
         };
-        if (!lds_tab)
+        if (stream)
+            hipLaunchKernelGGL(k_fielddiff_s<KD_FD_SSHAPE>, dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
+                               (const u64*)d_ooff, (const u8*)d_nd, (const u64*)d_noff, n_upd, d_n_upd, tb, to,
+                               (const u8*)dt, d_masks, d_status);
+        else if (!lds_tab)
             hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks,
                                d_status);

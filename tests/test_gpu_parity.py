@@ -669,3 +669,69 @@ def test_gpu_diff2_perm_equals_sorted(engine, kind, n):
     assert np.array_equal(outs[0][1], outs[1][1]) and np.array_equal(outs[0][2], outs[1][2])
     od, _ = O.classify2(A.key, A.oid, B.key, B.oid)
     assert np.array_equal(outs[0][1].reshape(-1, 2), od)
+
+
+def _gather_arena(data, off, idx):
+    """the blobs ``idx`` of an arena, back to back (contiguous in idx order)"""
+    idx = np.asarray(idx, np.int64)
+    lo, hi = off[idx].astype(np.int64), off[idx + 1].astype(np.int64)
+    lens = hi - lo
+    out_off = np.zeros(idx.size + 1, np.uint64)
+    np.cumsum(lens, out=out_off[1:])
+    pos = np.repeat(lo - out_off[:-1].astype(np.int64), lens) + np.arange(int(lens.sum()), dtype=np.int64)
+    return np.ascontiguousarray(data[pos]), out_off
+
+
+def _grow_geometry(blob, extra, rng):
+    """the feature blob with its geometry payload lengthened by ``extra`` bytes (field diff compares
+    geometry payloads as bytes)"""
+    import msgpack
+
+    from kart_amd.dataset import Geometry, msg_unpack
+
+    leg, vals = msg_unpack(blob)
+    vals = [Geometry(bytes(v) + rng.integers(0, 256, extra, dtype=np.uint8).tobytes()) if isinstance(v, Geometry)
+            else v for v in vals]
+    return msgpack.packb([leg, vals], use_bin_type=True, strict_types=True,
+                         default=lambda g: msgpack.ExtType(ord("G"), bytes(g)))
+
+
+@pytest.mark.parametrize("stream", ["0", "1"])
+@pytest.mark.parametrize("case", ["c3", "c3v", "huge", "ragged", "points", "one"])
+def test_gpu_fielddiff_contiguous_vs_oracle(engine, monkeypatch, stream, case):
+    """kd_fielddiff on update arenas laid back to back (no pairs: the drop-in's and the bench's form),
+    through the streamed kernel (KD_FD_STREAM=1: whole tile spans into LDS) and the windowed one:
+    C3 / C3v polygons, a tile whose span overflows the LDS buffer (blobs of 20-60 KB, read from
+    global memory past it), update counts that end inside a tile, point features"""
+    from kart_amd import synth
+    from kart_amd.schema import FieldMaps
+
+    monkeypatch.setenv("KD_FD_STREAM", stream)
+    rng = np.random.default_rng(7)
+    if case == "points":
+        L = synth.points_layer(300_000, seed=3)
+    else:
+        L = synth.polygons_layer(400_000 if case in ("c3", "c3v", "huge") else 30_011, seed=5,
+                                 same_len=0.6 if case in ("c3v", "huge") else 0.0)
+    r = engine.diff2(L.base, L.target)
+    upd = r.upd
+    if case == "one":
+        upd = upd[:1]
+    od, oo = _gather_arena(*L.base_blobs, upd[:, 0])
+    nd, no = _gather_arena(*L.target_blobs, upd[:, 1])
+    if case == "huge":  # rows 40..79 and 2000..2004: geometries of 20-60 KB on both sides
+        rows = list(range(40, 80)) + list(range(2000, 2005))
+        ob = [od[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(upd.shape[0])]
+        nb = [nd[int(no[i]):int(no[i + 1])].tobytes() for i in range(upd.shape[0])]
+        for i in rows:
+            extra = int(rng.integers(20_000, 60_000))
+            ob[i] = _grow_geometry(ob[i], extra, np.random.default_rng(i))
+            nb[i] = _grow_geometry(nb[i], extra, np.random.default_rng(i if i % 2 else i + 1))
+        from kart_amd.packing import _arena
+
+        (od, oo), (nd, no) = _arena(ob), _arena(nb)
+    maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    gm, gs = engine.fielddiff(od, oo, nd, no, None, maps)
+    om, ost = O.fielddiff(od, oo, nd, no, None, maps)
+    assert np.array_equal(gm, om) and np.array_equal(gs, ost)
+    assert not gs.any()
