@@ -11,6 +11,8 @@
 // classify3 replaces libgit2 git_merge_trees (kart/merge.py:99-100): key-range tiles cut on the
 // ancestor∪ours merge path, theirs split by lower_bound; per item LDS binary searches find the
 // (ancestor, ours, theirs) triple and the libgit2 OID rule classifies it.
+#include <cstdlib>
+
 #include "kd_join.h"
 
 namespace kd {
@@ -341,6 +343,11 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     const bool perm = pA || pO || pT;
     int rc;
     const u64 nA = A.n, nO = O.n, nT = T.n;
+    // the one-pass join (k_join3) unless the union is empty (then only the ancestor's order check
+    // remains) or KD_MERGE3_JOIN=0 selects the two-step path (classify2 + k_resolve3) for an A/B
+    const char* j3e = getenv("KD_MERGE3_JOIN");
+    if (nO + nT > 0 && !(j3e && atoi(j3e) == 0))
+        return merge3_join_device(ctx, A, O, T, d_conf, d_md, counts, derr, pA, pO, pT);
     const u64 nchunk = (nO + nT) / C3_CH + 2;
     void *cand, *c2, *desc, *aux, *dz;
     if ((rc = ensure(ctx, "c3.cand", (nO + nT + 1) * 8, &cand))) return rc;

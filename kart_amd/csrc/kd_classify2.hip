@@ -652,8 +652,11 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
 // Staged path, step 1: one block scans the C2_GROUP-tile group sums (exclusive prefix of deltas and
 // updates per group) and writes the totals — so each k_place2 tile reads one prefix instead of
 // summing every earlier group (which made k_place2 O(tiles x groups): 0.30 ms at C3's 195k tiles).
+// layout 0 (classify2): counts = inserts, updates, deletes, deltas; layout 1 (k_join3, where the
+// "deltas" are conflicts, the "updates" merge deltas and the "inserts" clean paths): counts = clean,
+// conflicts, merge deltas, 0
 __global__ __launch_bounds__(1024) void k_gscan2(const u64* __restrict__ gsum, u64 ngroups, u64* __restrict__ gpre,
-                                                 u64* __restrict__ counts) {
+                                                 u64* __restrict__ counts, int layout) {
     __shared__ u64 s_w[4][16];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     u64 cd = 0, cu = 0, ci = 0, cx = 0;
@@ -691,9 +694,9 @@ __global__ __launch_bounds__(1024) void k_gscan2(const u64* __restrict__ gsum, u
     }
     if (tid == 0) {
         counts[0] = ci;
-        counts[1] = cu;
-        counts[2] = cx;
-        counts[3] = cd;
+        counts[1] = layout ? cd : cu;
+        counts[2] = layout ? cu : cx;
+        counts[3] = layout ? 0 : cd;
     }
 }
 
@@ -764,6 +767,440 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
         if (out_upd)
             for (u32 r = tid; r < own.y; r += NT) out_ukey[pu + r] = sku[r];
     }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// k_join3: the three-way merge (libgit2 git_merge_trees, kart/merge.py:99-100) in one pass over
+// the three sorted sides.  The O∪T key union is cut into k_join2's merge-path tiles; the ancestor
+// entries of each tile's key range — [apart[t], apart[t+1]) plus one lookahead entry, apart[t] =
+// lower_bound(ancestor, first key of tile t) (k_apart3) — are staged in LDS with the tile's keys.
+// The tile walk pairs ours with theirs as k_join2 does; every path where they differ (one side only,
+// or different OIDs) finds its ancestor entry by an LDS binary search, loads the (at most three)
+// OIDs and applies the libgit2 rule: o == t -> clean; a == o -> theirs (merge delta); a == t ->
+// ours (clean); else conflict.  Conflicts and merge deltas are staged per tile and placed in path
+// order (k_gscan2 layout 1, k_place3).  The ancestor's keys are read once, in order, and its OIDs
+// only where ours and theirs differ; the order checks of all three sides ride along.
+// ---------------------------------------------------------------------------------------------
+struct Join3Args {
+    Join2Args j;          // A = ours, B = theirs (k_join2's two sides)
+    const u64* K;         // the ancestor: keys, OIDs, filenames, walk rows (PERM)
+    const u8* oidK;
+    const u8* nameK;
+    const u64* nameOffK;
+    const u32* ordK;
+    u64 nK;
+    const u64* apart;     // [ntiles + 1]
+    u32* stage_conf;      // per tile C2_STAGE slots of (a, o, t)
+    uint2* stage_md;      // per tile C2_STAGE slots of (o, t)
+};
+#ifndef KD_J3_ACAP
+#define KD_J3_ACAP 1024   // ancestor keys of a tile staged in LDS (a longer range is searched in HBM)
+#endif
+constexpr int J3_ACAP = KD_J3_ACAP;
+
+// smallest p in [lo, hi] with p == hi || K[p] >= key, by groups of PW lanes (PW-ary search)
+template <int PW>
+__device__ __forceinline__ u64 lb_search(const u64* __restrict__ K, u64 key, u64 lo, u64 hi) {
+    const int lane = threadIdx.x & 63, sub = lane % PW, grp = lane / PW;
+    while (hi > lo) {
+        const u64 step = (hi - lo + PW - 1) / PW;
+        const u64 probe = lo + step * (u64)(sub + 1) - 1;
+        bool p = true;
+        if (probe < hi) p = K[probe] >= key;
+        const unsigned long long bal = (__ballot(p) >> (grp * PW)) & ((PW == 64) ? ~0ull : ((1ull << PW) - 1));
+        if (bal == 0) return hi;
+        const int f = __ffsll(bal) - 1;
+        const u64 nh = lo + step * (u64)(f + 1) - 1;
+        lo = lo + step * (u64)f;
+        hi = nh < hi ? nh : hi;
+        if (step == 1) return hi;
+    }
+    return lo;
+}
+
+// the same from a guess: PW probes `step` apart around it bracket the answer (or bound one side)
+template <int PW>
+__device__ __forceinline__ u64 lb_guided(const u64* __restrict__ K, u64 n, u64 key, u64 guess, u64 step) {
+    const int lane = threadIdx.x & 63, sub = lane % PW, grp = lane / PW;
+    const u64 span = step * (PW / 2);
+    const u64 g0 = guess > span ? guess - span : 0;
+    u64 probe = g0 + step * (u64)sub;
+    if (probe > n) probe = n;
+    const bool p = probe >= n || K[probe] >= key;
+    const unsigned long long bal = (__ballot(p) >> (grp * PW)) & ((PW == 64) ? ~0ull : ((1ull << PW) - 1));
+    const int f = bal ? __ffsll(bal) - 1 : PW;
+    const u64 pf = f < PW ? (g0 + step * (u64)f < n ? g0 + step * (u64)f : n) : n;
+    const u64 pl = f > 0 ? (g0 + step * (u64)(f - 1) < n ? g0 + step * (u64)(f - 1) : n) : 0;
+    const u64 nlo = f > 0 ? pl + 1 : 0;
+    return lb_search<PW>(K, key, nlo < pf ? nlo : pf, pf);
+}
+
+// apart[t] for t in [0, ntiles]: 8 lanes per split, guided by the proportional position
+__global__ __launch_bounds__(256) void k_apart3(const u64* __restrict__ O, u64 nO, const u64* __restrict__ T, u64 nT,
+                                                const u64* __restrict__ part, u64 ntiles, const u64* __restrict__ K,
+                                                u64 nK, u64* __restrict__ apart) {
+    const u64 t = ((u64)blockIdx.x * 256 + threadIdx.x) / 8;
+    if (t > ntiles) return;  // (whole 8-lane groups)
+    u64 r;
+    if (t == 0) r = 0;
+    else if (t == ntiles) r = nK;
+    else {
+        const u64 i = part[t], d = t * (u64)C2_TILE, j = d - i;
+        const u64 a = i < nO ? O[i] : ~0ull, b = j < nT ? T[j] : ~0ull;
+        const u64 key = a < b ? a : b;
+        const u64 guess = (u64)((double)d / (double)(nO + nT) * (double)nK);
+        r = lb_guided<8>(K, nK, key, guess < nK ? guess : nK, 16);
+    }
+    if ((threadIdx.x & 7) == 0) apart[t] = r;
+}
+
+// a byte range into LDS by LDS-DMA: 64-chunk pieces dealt round-robin to the waves, continuing the
+// deal of earlier ranges (q0 = pieces dealt so far); returns the new count
+template <int NT>
+__device__ __forceinline__ u32 dma_range(const Range& R, u32x4* dst, u32 q0) {
+    constexpr int NW = NT / 64;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const u32 np = (R.nch + 63) >> 6;
+    for (u32 p = (u32)(wid + NW - (int)(q0 % NW)) % NW; p < np; p += NW) {
+        const u32 c = 64 * p + lane;
+        if (c < R.nch) __builtin_amdgcn_global_load_lds((glb_vp)(R.base + 16ull * c), (lds_vp)(dst + 64 * p), 16, 0, 0);
+    }
+    return q0 + np;
+}
+
+template <int NT, int IPT, bool HASH, bool PERM>
+__global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
+    const Join2Args& g = g3.j;
+    using LD = Join2Lds<NT, IPT>;
+    static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
+    constexpr int KCH = (8 * (J3_ACAP + 2) + 16 + 15) / 16 + 4;
+    __shared__ u32x4 s_ch[LD::CHK];
+    __shared__ u32x4 s_k[KCH];
+    __shared__ u32x4 s_nm[HASH ? LD::NMCH : 1];
+    __shared__ u32 s_wave[3 * NT / 64];
+    typedef const __attribute__((address_space(1))) u32* gp32;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 tile = blockIdx.x;
+    const TileGeo q = tile_geo(g, tile, LD::TILE);
+    bool bad = !q.ok;
+    const TileRanges r = tile_ranges(g, q);
+    // the ancestor entries of the tile's key range [k0, k1) (+ the lookahead entry k1: a match of ours'
+    // last entry with theirs' lookahead has the next tile's first key) and the lookbehind key
+    const u64 k0 = uni64(g3.apart[tile]), kend = uni64(g3.apart[tile + 1]);
+    const bool kok = kend >= k0 && kend <= g3.nK;
+    bad |= !kok;
+    const u64 k1 = kok ? kend : k0;
+    const u64 k1e = k1 < g3.nK ? k1 + 1 : k1;
+    const bool has_lbK = k0 > 0;
+    const bool lk = k1e - k0 <= (u64)J3_ACAP;
+    Range rk{};
+    if (lk) rk = mk_range(g3.K, 8 * (k0 - has_lbK), 8 * k1e);
+    u64 nmA0 = 0, nmA1 = 0, nmB0 = 0, nmB1 = 0;
+    const u64 rA0 = PERM ? (q.i0 > J2_NAME_HALO ? q.i0 - J2_NAME_HALO : 0) : q.i0;
+    const u64 rA1 = PERM ? min(q.i1 + J2_NAME_HALO, g.nA) : q.i1;
+    const u64 rB0 = PERM ? (q.j0 > J2_NAME_HALO ? q.j0 - J2_NAME_HALO : 0) : q.j0;
+    const u64 rB1 = PERM ? min(q.j1e + J2_NAME_HALO, g.nB) : q.j1e;
+    if (HASH) {
+        nmA0 = g.nameOffA[rA0]; nmA1 = g.nameOffA[rA1];
+        nmB0 = g.nameOffB[rB0]; nmB1 = g.nameOffB[rB1];
+    }
+    u32 qq = dma_range<NT>(r.ka, s_ch, 0);
+    qq = dma_range<NT>(r.kb, s_ch + r.c1, qq);
+    if (lk) qq = dma_range<NT>(rk, s_k, qq);
+    __syncthreads();  // vmcnt(0) + barrier: the keys have landed
+    Range rnA{}, rnB{};
+    bool lnames = false;
+    if (HASH) {
+        nmA0 = uni64(nmA0); nmA1 = uni64(nmA1); nmB0 = uni64(nmB0); nmB1 = uni64(nmB1);
+        rnA = mk_range(g.nameA, nmA0, nmA1);
+        rnB = mk_range(g.nameB, nmB0, nmB1);
+        lnames = nmA1 >= nmA0 && nmB1 >= nmB0 && (u64)rnA.nch + rnB.nch <= (u64)LD::NMCH;
+        if (lnames) dma_range<NT>(rnB, s_nm + rnA.nch, dma_range<NT>(rnA, s_nm, 0));
+    }
+    const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
+    const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
+    const u64* sK = (const u64*)((const u8*)s_k + rk.skew) + has_lbK;
+    u32 rec[IPT];
+    tile_walk<NT, IPT>(sA, sB, q, rec, bad);
+    for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
+    for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
+    // the ancestor strictly ascending: every adjacent pair (x-1, x) with x in [k0, k1) once over all tiles
+    if (lk) {
+        for (int x = tid; x < (int)(k1 - k0); x += NT) bad |= (x > 0 || has_lbK) && sK[x - 1] >= sK[x];
+    } else {
+        for (u64 x = k0 + tid; x < k1; x += NT) bad |= x > 0 && g3.K[x - 1] >= g3.K[x];
+    }
+    u32 ra[IPT], rb[IPT];
+    u32 oa0[IPT], oa1[IPT], ob0[IPT], ob1[IPT];
+    tile_rows<IPT, PERM>(g, q, rec, ra, rb);
+    if (HASH && lnames) {
+        const u32* offA = (const u32*)g.nameOffA;
+        const u32* offB = (const u32*)g.nameOffB;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const bool m = (rec[k] >> 25) == R_MATCH;
+            const u64 i = m ? ra[k] : rA0, j = m ? rb[k] : rB0;
+            oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
+            ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
+        }
+    }
+    tile_oid_cmp<IPT>(g, rec, ra, rb);
+    bool ne = false;
+    if (HASH && lnames) {
+        __syncthreads();  // vmcnt(0) + barrier: the names DMA has landed
+        const u32 nm = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_nm;
+        const u32 baseA = nm + rnA.skew, baseB = nm + 16 * rnA.nch + rnB.skew;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            if ((rec[k] >> 25) != R_MATCH) continue;
+            const u32 la = oa1[k] - oa0[k], lb = ob1[k] - ob0[k];
+            if (PERM && (ra[k] < rA0 || ra[k] >= rA1 || rb[k] < rB0 || rb[k] >= rB1))
+                ne |= !names_eq(g.nameA, g.nameOffA, ra[k], g.nameB, g.nameOffB, rb[k]);
+            else
+                ne |= la != lb || !lds_eq_bytes(baseA + (oa0[k] - (u32)nmA0), baseB + (ob0[k] - (u32)nmB0), la);
+        }
+    } else if (HASH) {
+        u32 act = 0;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
+        ne |= names_ne_batch<IPT, 8>(g.nameA, g.nameOffA, ra, g.nameB, g.nameOffB, rb, act) != 0;
+    }
+    // ---- the paths where ours and theirs differ: their ancestor entries ----
+    u32 dif = 0, clean = 0;
+    u64 key[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
+        const bool d = kind == R_DEL || kind == R_INS || (kind == R_MATCH && chg);
+        dif |= (u32)d << k;
+        clean += kind == R_MATCH && !chg;  // ours == theirs: clean, nothing to record
+        key[k] = kind == R_INS ? sB[jb] : sA[ia];
+    }
+    u64 pos[IPT];
+    const u64 nk = k1e - k0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) pos[k] = 0;
+    if (__syncthreads_or(dif != 0)) {
+        const int rounds = nk ? 64 - __clzll((long long)nk) : 0;  // wave-uniform
+        u64 lo[IPT], hi[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; k++) { lo[k] = 0; hi[k] = (dif >> k) & 1 ? nk : 0; }
+        for (int it = 0; it < rounds; it++) {
+            u64 v[IPT], m[IPT];
+#pragma unroll
+            for (int k = 0; k < IPT; k++) {
+                m[k] = (lo[k] + hi[k]) >> 1;
+                const u64 mi = m[k] < nk ? m[k] : (nk ? nk - 1 : 0);
+                v[k] = lk ? sK[mi] : g3.K[k0 + mi];
+            }
+#pragma unroll
+            for (int k = 0; k < IPT; k++) {
+                const bool act = lo[k] < hi[k], lt = v[k] < key[k];
+                lo[k] = act && lt ? m[k] + 1 : lo[k];
+                hi[k] = act && !lt ? m[k] : hi[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; k++) pos[k] = lo[k];
+    }
+    u32 ik[IPT], io[IPT], itt[IPT], rk3[IPT], ro[IPT], rt[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
+        const bool d = (dif >> k) & 1;
+        const bool found = d && pos[k] < nk && (lk ? sK[pos[k]] : g3.K[k0 + pos[k]]) == key[k];
+        ik[k] = found ? (u32)(k0 + pos[k]) : KD_NONE;
+        io[k] = d && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
+        itt[k] = d && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
+    }
+    // rows of the differing paths in the OID / filename arrays (PERM: through the walk orders)
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        rk3[k] = ik[k]; ro[k] = io[k]; rt[k] = itt[k];
+        if (PERM) {
+            rk3[k] = ik[k] != KD_NONE ? *(gp32)(g3.ordK + ik[k]) : KD_NONE;
+            ro[k] = io[k] != KD_NONE ? *(gp32)(g.ordA + io[k]) : KD_NONE;
+            rt[k] = itt[k] != KD_NONE ? *(gp32)(g.ordB + itt[k]) : KD_NONE;
+        }
+    }
+    u32 xk[IPT][5], xo[IPT][5], xt[IPT][5];
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const gp32 pk = rk3[k] != KD_NONE ? (gp32)(g3.oidK + 20ull * rk3[k]) : (gp32)g.dummy;
+        const gp32 po = ro[k] != KD_NONE ? (gp32)(g.oidA + 20ull * ro[k]) : (gp32)g.dummy;
+        const gp32 pt = rt[k] != KD_NONE ? (gp32)(g.oidB + 20ull * rt[k]) : (gp32)g.dummy;
+#pragma unroll
+        for (int w = 0; w < 5; w++) { xk[k][w] = pk[w]; xo[k][w] = po[w]; xt[k][w] = pt[w]; }
+    }
+    if (HASH) {  // a matched ancestor path must carry the same filename (ours', else theirs')
+        u32 act_o = 0, act_t = 0;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            act_o |= (u32)(ik[k] != KD_NONE && io[k] != KD_NONE) << k;
+            act_t |= (u32)(ik[k] != KD_NONE && itt[k] != KD_NONE && io[k] == KD_NONE) << k;
+        }
+        if (act_o | act_t)
+            ne |= (names_ne_batch<IPT, 8>(g3.nameK, g3.nameOffK, rk3, g.nameA, g.nameOffA, ro, act_o) |
+                   names_ne_batch<IPT, 8>(g3.nameK, g3.nameOffK, rk3, g.nameB, g.nameOffB, rt, act_t)) != 0;
+    }
+    // libgit2's rule where ours != theirs: a == o -> theirs (merge delta), a == t -> ours, else conflict
+    u32 fc = 0, fm = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const bool pa = ik[k] != KD_NONE, po = io[k] != KD_NONE, pt = itt[k] != KD_NONE;
+        u32 dko = 0, dkt = 0;
+#pragma unroll
+        for (int w = 0; w < 5; w++) { dko |= xk[k][w] ^ xo[k][w]; dkt |= xk[k][w] ^ xt[k][w]; }
+        const bool a_eq_o = pa == po && (!pa || dko == 0);
+        const bool a_eq_t = pa == pt && (!pa || dkt == 0);
+        const bool d = (dif >> k) & 1;
+        const bool md = d && a_eq_o, cf = d && !a_eq_o && !a_eq_t;
+        fm |= (u32)md << k;
+        fc |= (u32)cf << k;
+        clean += (d && !a_eq_o && a_eq_t && po) || (md && pt);
+    }
+    if (ne) atomicOr(g.err, 2u);
+    if (bad) atomicOr(g.err, 1u);
+    // ---- tile compaction: per item-slot ballots, wave totals exchanged once ----
+    u32 oc = 0, om = 0, wc = 0, wm = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u64 bc = __ballot((fc >> k) & 1), bm = __ballot((fm >> k) & 1);
+        oc += __builtin_amdgcn_mbcnt_hi((u32)(bc >> 32), __builtin_amdgcn_mbcnt_lo((u32)bc, 0));
+        om += __builtin_amdgcn_mbcnt_hi((u32)(bm >> 32), __builtin_amdgcn_mbcnt_lo((u32)bm, 0));
+        wc += __popcll(bc);
+        wm += __popcll(bm);
+    }
+    u32 wcl = clean;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wcl += __shfl_xor(wcl, o, 64);
+    if (lane == 0) { s_wave[wid] = wc; s_wave[NT / 64 + wid] = wm; s_wave[2 * NT / 64 + wid] = wcl; }
+    __syncthreads();
+    u32 tc = 0, tm = 0, tcl = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const u32 a = s_wave[w], b = s_wave[NT / 64 + w];
+        if (w < wid) { oc += a; om += b; }
+        tc += a;
+        tm += b;
+        tcl += s_wave[2 * NT / 64 + w];
+    }
+    u32* sc = g3.stage_conf + tile * (u64)C2_STAGE * 3;
+    uint2* sm = g3.stage_md + tile * (u64)C2_STAGE;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        if ((fc >> k) & 1) {
+            sc[3 * oc] = ik[k]; sc[3 * oc + 1] = io[k]; sc[3 * oc + 2] = itt[k];
+            oc++;
+        }
+        if ((fm >> k) & 1) {
+            sm[om] = make_uint2(io[k], itt[k]);
+            om++;
+        }
+    }
+    if (tid == 0) {
+        u32* cc = g.tile_cnt + 4 * tile;
+        cc[0] = tcl; cc[1] = tm; cc[2] = 0; cc[3] = tc;
+        u64* gs = g.gsum + 2 * (tile / C2_GROUP);
+        atomicAdd((unsigned long long*)gs, (unsigned long long)(tc | (u64)tm << 32));
+        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)tcl);
+    }
+}
+
+// staged conflicts / merge deltas -> final path-ordered positions; one wave per tile
+__global__ __launch_bounds__(64) void k_place3(const u32* __restrict__ stage_conf, const uint2* __restrict__ stage_md,
+                                               const u32* __restrict__ tile_cnt, const u64* __restrict__ gpre,
+                                               u32* __restrict__ out_conf, uint2* __restrict__ out_md) {
+    const int tid = threadIdx.x;
+    const u64 t = blockIdx.x, grp = t / C2_GROUP, t_lo = grp * C2_GROUP;
+    u64 pc = 0, pm = 0;
+    if (tid < (int)(t - t_lo)) {
+        const uint4 c = *(const uint4*)(tile_cnt + 4 * (t_lo + tid));
+        pc = c.w;
+        pm = c.y;
+    }
+    const uint4 own = *(const uint4*)(tile_cnt + 4 * t);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { pc += __shfl_xor(pc, o, 64); pm += __shfl_xor(pm, o, 64); }
+    pc += gpre[2 * grp];
+    pm += gpre[2 * grp + 1];
+    const u32* scp = stage_conf + t * (u64)C2_STAGE * 3;
+    const uint2* smp = stage_md + t * (u64)C2_STAGE;
+    for (u32 x = tid; x < 3 * own.w; x += 64) out_conf[3 * pc + x] = scp[x];
+    for (u32 x = tid; x < own.y; x += 64) out_md[pm + x] = smp[x];
+}
+
+// the three-way merge through k_join3 (sides device-resident; ord* non-null: late materialisation)
+int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
+                       u64* d_counts, u32* d_err, const u32* ordK, const u32* ordO, const u32* ordT) {
+    const u64 nK = K.n, nO = O.n, nT = T.n, total = nO + nT;
+    const bool hash = K.key_mode == KD_KEY_HASH;
+    const bool perm = ordK || ordO || ordT;
+    if (hash) KD_CHECK((nK == 0 || (K.name && K.name_off)) && (nO == 0 || (O.name && O.name_off)) &&
+                       (nT == 0 || (T.name && T.name_off)), "merge3: KD_KEY_HASH needs filenames");
+    const u64 ntiles = (total + C2_TILE - 1) / C2_TILE;
+    const u64 n_zero = 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
+    void *part, *apart, *tcnt, *gsum, *gpre, *sconf, *smd, *dz;
+    int rc;
+    if ((rc = ensure(ctx, "c2.part", (ntiles + 1) * sizeof(u64), &part))) return rc;
+    if ((rc = ensure(ctx, "c3.apart", (ntiles + 1) * sizeof(u64), &apart))) return rc;
+    if ((rc = ensure(ctx, "c2.tcnt", ntiles * 4 * sizeof(u32), &tcnt))) return rc;
+    if ((rc = ensure(ctx, "c2.gsum", n_zero * sizeof(u64), &gsum))) return rc;
+    if ((rc = ensure(ctx, "c2.gpre", n_zero * sizeof(u64), &gpre))) return rc;
+    if ((rc = ensure(ctx, "c3.sconf", ntiles * C2_STAGE * 12, &sconf))) return rc;
+    if ((rc = ensure(ctx, "c3.smd", ntiles * C2_STAGE * sizeof(uint2), &smd))) return rc;
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    auto P = [&](const void* p, u64 n) { return n && p ? p : (const void*)dz; };
+    const u64* kO = (const u64*)P(O.key, nO);
+    const u64* kT = (const u64*)P(T.key, nT);
+    const u64* kK = (const u64*)P(K.key, nK);
+    rc = launch(ctx, "k_partition2", [&] {
+        unsigned nb = (unsigned)((ntiles + C2_PG - 1) / C2_PG);
+        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kO, nO, kT, nT, ntiles, (u64*)part,
+                           d_counts, d_err, (u64*)gsum, n_zero);
+    });
+    if (rc) return rc;
+    rc = launch(ctx, "k_apart3", [&] {
+        const u64 lanes = 8 * (ntiles + 1);
+        hipLaunchKernelGGL(k_apart3, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, ctx->stream, kO, nO, kT, nT,
+                           (const u64*)part, ntiles, kK, nK, (u64*)apart);
+    });
+    if (rc) return rc;
+    Join3Args a;
+    Join2Args& g = a.j;
+    g.A = kO; g.oidA = (const u8*)P(O.oid, nO); g.nA = nO;
+    g.B = kT; g.oidB = (const u8*)P(T.oid, nT); g.nB = nT;
+    g.part = (const u64*)part;
+    g.nameA = (const u8*)P(O.name, nO); g.nameOffA = (const u64*)P(O.name_off, nO);
+    g.nameB = (const u8*)P(T.name, nT); g.nameOffB = (const u64*)P(T.name_off, nT);
+    g.hash_mode = hash ? 1 : 0;
+    g.dummy = (const u8*)dz;
+    g.ordA = (const u32*)P(ordO, nO); g.ordB = (const u32*)P(ordT, nT);
+    g.stage_delta = g.stage_upd = nullptr;
+    g.tile_cnt = (u32*)tcnt; g.gsum = (u64*)gsum; g.err = d_err;
+    g.out_delta = g.out_upd = nullptr; g.counts = d_counts;
+    g.stage_dkey = g.stage_ukey = g.out_dkey = g.out_ukey = nullptr;
+    g.ntiles = ntiles;
+    a.K = kK; a.oidK = (const u8*)P(K.oid, nK); a.nameK = (const u8*)P(K.name, nK);
+    a.nameOffK = (const u64*)P(K.name_off, nK); a.ordK = (const u32*)P(ordK, nK); a.nK = nK;
+    a.apart = (const u64*)apart; a.stage_conf = (u32*)sconf; a.stage_md = (uint2*)smd;
+    rc = launch(ctx, "k_join3", [&] {
+#define KD_J3(H, PM) hipLaunchKernelGGL((k_join3<C2_NT, C2_IPT, H, PM>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
+        if (hash) { if (perm) KD_J3(true, true); else KD_J3(true, false); }
+        else { if (perm) KD_J3(false, true); else KD_J3(false, false); }
+#undef KD_J3
+    });
+    if (rc) return rc;
+    rc = launch(ctx, "k_gscan2", [&] {
+        hipLaunchKernelGGL(k_gscan2, dim3(1), dim3(1024), 0, ctx->stream, (const u64*)gsum, (u64)(n_zero / 2),
+                           (u64*)gpre, d_counts, 1);
+    });
+    if (rc) return rc;
+    return launch(ctx, "k_place3", [&] {
+        hipLaunchKernelGGL(k_place3, dim3((unsigned)ntiles), dim3(64), 0, ctx->stream, (const u32*)sconf,
+                           (const uint2*)smd, (const u32*)tcnt, (const u64*)gpre, d_conf, d_md);
+    });
 }
 
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,
@@ -857,7 +1294,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     if (rc || unord) return rc;
     rc = launch(ctx, "k_gscan2", [&] {
         hipLaunchKernelGGL(k_gscan2, dim3(1), dim3(1024), 0, ctx->stream, (const u64*)gsum, (u64)(n_zero / 2),
-                           (u64*)gpre, d_counts);
+                           (u64*)gpre, d_counts, 0);
     });
     if (rc) return rc;
     return launch(ctx, "k_place2", [&] {

@@ -138,6 +138,11 @@ void comm_release(kd_ctx* ctx);
 // ordA / ordB (both or neither): the sides' OIDs and filename offsets are in another order, row
 // ord[i] belongs to sorted entry i (kd_diff2_device_perm)
 // d_dkey / d_ukey (optional): the join key of every delta / update record, beside the lists
+// three-way merge in one pass (k_join3): conflicts (a, o, t) and merge deltas (o, t) in path order,
+// counts = clean, conflicts, merge deltas, 0; ord*: late materialisation (walk rows of sorted entries)
+int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
+                       u64* d_counts, u32* d_err, const u32* ordK = nullptr, const u32* ordO = nullptr,
+                       const u32* ordT = nullptr);
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta,
                  u32* d_upd, u64* d_counts, u32* d_err, const u32* ordA = nullptr, const u32* ordB = nullptr,
                  u64* d_dkey = nullptr, u64* d_ukey = nullptr);
