@@ -94,6 +94,37 @@ class DevSide:
         return s
 
 
+class DevPermSide:
+    """A side packed on the GPU for the late-materialised join (packing.pack_side with an engine, when
+    the walk order is not key order): keys sorted in HBM, OIDs and (KD_KEY_HASH) the filename arena
+    left in walk order, ``order[k]`` = walk row of sorted entry k — what kd_diff2_device_perm /
+    kd_merge3_device_perm read through (bench.py's fallback_sort times the same path)."""
+
+    def __init__(self, engine, n, key_mode, key, oid, order, name=None, name_off=None):
+        self.n, self.key_mode = int(n), key_mode
+        self.key, self.oid, self.order, self.name, self.name_off = key, oid, order, name, name_off
+
+    def kd_side(self):
+        s = N.KdSide()
+        s.n = self.n
+        s.key, s.oid = self.key.ptr, self.oid.ptr
+        s.name = self.name.ptr if self.name is not None else None
+        s.name_off = self.name_off.ptr if self.name_off is not None else None
+        s.mem = N.KD_MEM_DEVICE
+        s.key_mode = self.key_mode
+        return s
+
+
+def perm_dev(engine, side):
+    """(kd_side, order DevBuf, keep-alive) of a PackedSide for the *_perm entry points: its DevPermSide,
+    or a sorted-form side uploaded with an identity order"""
+    if side.dperm is not None:
+        return side.dperm.kd_side(), side.dperm.order, side.dperm
+    ds = DevSide(engine, side)
+    order = DevBuf.from_numpy(engine, np.arange(max(side.n, 1), dtype=np.uint32))
+    return ds.kd_side(), order, (ds, order)
+
+
 class _WalkSide:
     """a side's arrays in another order (what DevSide uploads): keys, OIDs and (KD_KEY_HASH) the
     filename arena with rows in that order"""

@@ -117,7 +117,11 @@ class Engine:
 
     # ---------------------------------------------------------------------------------------
     def diff2(self, base, target, flags=0) -> Diff2Result:
-        """base/target: PackedSide (host) -> key-ordered delta set (kd_diff2)."""
+        """base/target: PackedSide (host) -> key-ordered delta set (kd_diff2).  A side packed on the
+        GPU with its rows in walk order (PackedSide.dperm) joins through its order on the device
+        (kd_diff2_device_perm: no OID or filename gather)."""
+        if base.walk_rows or target.walk_rows:
+            return self._diff2_perm(base, target, flags)
         sa, sb = base.kd_side(), target.kd_side()
         res = ctypes.POINTER(N.KdDiffResult)()
         N.check(self.L.kd_diff2(self.ctx, ctypes.byref(sa), ctypes.byref(sb), flags, ctypes.byref(res)), "kd_diff2")
@@ -129,6 +133,44 @@ class Engine:
             return Diff2Result(int(r.n_insert), nu, int(r.n_delete), delta, upd)
         finally:
             self.L.kd_free(res)
+
+    def _diff2_perm(self, base, target, flags):
+        from .device import DevBuf, perm_dev
+
+        (sa, oa, ka), (sb, ob, kb) = perm_dev(self, base), perm_dev(self, target)
+        n = base.n + target.n
+        d_delta, d_upd, d_c = DevBuf(self, 8 * (n + 1)), DevBuf(self, 8 * (n + 1)), DevBuf(self, 64)
+        N.check(self.L.kd_diff2_device_perm(self.ctx, ctypes.byref(sa), ctypes.byref(sb), oa.ptr, ob.ptr, flags,
+                                            d_delta.ptr, d_upd.ptr, d_c.ptr, d_c.ptr + 32), "kd_diff2_device_perm")
+        c = d_c.download(np.uint64, 5)
+        err = int(c[4]) & 0xFFFFFFFF
+        if err:
+            raise N.Unsupported("kd_diff2: " + ("side keys not strictly ascending" if err & 1 else
+                                               "hash key collision between different filenames"))
+        nd, nu = int(c[3]), int(c[1])
+        delta = d_delta.download(np.uint32, 2 * nd).reshape(nd, 2)
+        upd = d_upd.download(np.uint32, 2 * nu).reshape(nu, 2)
+        del ka, kb
+        return Diff2Result(int(c[0]), nu, int(c[2]), delta, upd)
+
+    def _merge3_perm(self, ancestor, ours, theirs, flags):
+        from .device import DevBuf, perm_dev
+
+        ds = [perm_dev(self, s) for s in (ancestor, ours, theirs)]
+        n = ancestor.n + ours.n + theirs.n
+        d_conf, d_md, d_c = DevBuf(self, 12 * (n + 1)), DevBuf(self, 8 * (ours.n + theirs.n + 1)), DevBuf(self, 64)
+        N.check(self.L.kd_merge3_device_perm(self.ctx, *(ctypes.byref(d[0]) for d in ds), *(d[1].ptr for d in ds),
+                                             flags, d_conf.ptr, d_md.ptr, d_c.ptr, d_c.ptr + 32),
+                "kd_merge3_device_perm")
+        c = d_c.download(np.uint64, 5)
+        err = int(c[4]) & 0xFFFFFFFF
+        if err:
+            raise N.Unsupported("kd_merge3: err=0x%x (%s)" % (err, "keys not strictly ascending" if err & 1 else
+                                                               "hash key collision" if err & 2 else "tile overflow"))
+        nc, nm = int(c[1]), int(c[2])
+        conf = d_conf.download(np.uint32, 3 * nc).reshape(nc, 3)
+        md = d_md.download(np.uint32, 2 * nm).reshape(nm, 2)
+        return Merge3Result(int(c[0]), conf, md)
 
     @staticmethod
     def diff2_sharded(engines, base, target, bucket_bits, flags=0) -> Diff2Result:
@@ -203,6 +245,10 @@ class Engine:
         return masks[:n], status[:n]
 
     def merge3(self, ancestor, ours, theirs, flags=0) -> Merge3Result:
+        """three PackedSides -> conflicts / merge deltas in path order (kd_merge3; sides packed on the
+        GPU with walk-order rows through kd_merge3_device_perm)"""
+        if ancestor.walk_rows or ours.walk_rows or theirs.walk_rows:
+            return self._merge3_perm(ancestor, ours, theirs, flags)
         sa, so, st = ancestor.kd_side(), ours.kd_side(), theirs.kd_side()
         res = ctypes.POINTER(N.KdMergeResult)()
         N.check(self.L.kd_merge3(self.ctx, ctypes.byref(sa), ctypes.byref(so), ctypes.byref(st), flags,

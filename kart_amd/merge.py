@@ -155,10 +155,10 @@ class MergeIndex:
 
 
 # ---------------------------------------------------------------------------------------------
-def _side(version, encoding):
+def _side(version, encoding, engine=None):
     if version is None or version.n == 0:
         return packing.empty_side(encoding)
-    return version.packed
+    return version.pack(engine)
 
 
 def merge_trees(engine, ancestor, ours, theirs, prefix="", ours_all=None):
@@ -173,7 +173,7 @@ def merge_trees(engine, ancestor, ours, theirs, prefix="", ours_all=None):
     if present is None:
         return MergeIndex({}, {})
     vers = (ancestor, ours, theirs)
-    sides = [_side(v, present.encoding) for v in vers]
+    sides = [_side(v, present.encoding, engine) for v in vers]
     r = engine.merge3(*sides)
 
     def entry(s, i):

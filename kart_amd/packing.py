@@ -82,12 +82,23 @@ class PackedSide:
     dev: Optional[tuple] = None  # (key, oid) DevBufs when the side was packed on the GPU
     timing: Optional[dict] = None  # pack_side's stage times (parse_s, sort_s, sort_on)
     info: Optional[object] = None  # kd_keys_scan of the walk-order keys (_native.KdKeysInfo)
+    # GPU pack of a side whose walk order is not key order: keys sorted (``key``, and in HBM), but
+    # ``oid`` / ``name`` / ``name_off`` still in walk order (row ``order[k]`` for sorted entry k) and
+    # the join reads them through the order (device.DevPermSide)
+    dperm: Optional[object] = None
+
+    @property
+    def walk_rows(self):
+        return self.dperm is not None
 
     @property
     def n(self):
         return int(self.key.shape[0])
 
     def kd_side(self):
+        if self.walk_rows:
+            raise ValueError("a late-materialised side joins through its order (engine *_perm paths); "
+                             "materialised() gives the sorted form")
         s = N.KdSide()
         s.n = self.n
         if self.dev is not None and self.key_mode == N.KD_KEY_INT:  # already in HBM (GPU pack)
@@ -104,8 +115,20 @@ class PackedSide:
 
     def rel_path(self, k):
         """relative path ('c/c/c/c/<filename>') of sorted entry k (KD_KEY_HASH sides)"""
-        a, b = int(self.name_off[k]), int(self.name_off[k + 1])
+        r = int(self.order[k]) if self.walk_rows else k
+        a, b = int(self.name_off[r]), int(self.name_off[r + 1])
         return self.name[a:b].tobytes().decode()
+
+    def materialised(self):
+        """the sorted form of a late-materialised side (OIDs and filenames gathered into key order),
+        for the host-form entry points (sharding, kd_diff2 / kd_merge3 on host arrays)"""
+        if not self.walk_rows:
+            return self
+        out = PackedSide(key=self.key, oid=np.ascontiguousarray(self.oid[self.order]), key_mode=self.key_mode,
+                         order=self.order, encoding=self.encoding, timing=self.timing, info=self.info)
+        if self.name is not None:
+            out.name, out.name_off = _gather_names(self.name, self.name_off, self.order)
+        return out
 
 
 class PackError(ValueError):
@@ -146,6 +169,56 @@ def keys_scan(keys, key_mode):
     return info
 
 
+def _gather_names(paths, off, order):
+    """the filename arena with rows in ``order`` (one vectorised gather)"""
+    n = order.shape[0]
+    lens = (off[1:] - off[:-1])[order]
+    noff = np.zeros(n + 1, np.uint64)
+    noff[1:] = np.cumsum(lens)
+    idx = np.arange(int(noff[-1]), dtype=np.int64) + np.repeat(off[:-1][order].astype(np.int64) - noff[:-1].astype(np.int64),
+                                                                lens.astype(np.int64))
+    return (np.ascontiguousarray(paths[idx]) if n else np.zeros(0, np.uint8)), noff
+
+
+def sort_on_device_perm(engine, keys, oids, info, encoding, paths, off):
+    """GPU pack of a side whose walk order is not key order, late-materialised as bench.py times it:
+    KD_KEY_HASH sides take the per-bucket sort (kd_sort_segmented_into, one kernel), falling back to
+    the full radix sort of the keys when a bucket is long or the buckets descend; KD_KEY_INT sides
+    the radix sort of the compacted varying key bits (kd_sort_side_into, passes from the host's
+    kd_keys_scan, no OIDs moved).  Returns (DevPermSide, sorted keys, order) — OIDs and filenames
+    stay in walk order.  PackError on duplicate keys."""
+    import ctypes
+
+    from . import shard
+    from .device import DevBuf, DevPermSide
+
+    n = keys.shape[0]
+    dk_in = DevBuf.from_numpy(engine, keys)
+    dk, dord, flag = DevBuf(engine, 8 * n), DevBuf(engine, 4 * n), DevBuf(engine, 8)
+    sorted_ok = False
+    if encoding.key_mode == N.KD_KEY_HASH:
+        flag.zero()
+        N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk_in.ptr, dk.ptr, dord.ptr, n,
+                                                shard.bucket_bits(encoding.key_mode, encoding), flag.ptr),
+                "kd_sort_segmented_into")
+        sorted_ok = int(flag.download(np.uint32, 1)[0]) == 0
+    if not sorted_ok:
+        flag.zero()
+        N.check(engine.L.kd_sort_side_into(engine.ctx, dk_in.ptr, None, dk.ptr, None, dord.ptr, n, flag.ptr,
+                                           ctypes.byref(info)), "kd_sort_side_into")
+        if int(flag.download(np.uint32, 1)[0]):
+            raise PackError("duplicate join keys within one side")
+    dk_in.free()
+    flag.free()
+    do = DevBuf.from_numpy(engine, oids.reshape(-1))
+    name = name_off = None
+    if encoding.key_mode == N.KD_KEY_HASH:
+        name = DevBuf.from_numpy(engine, paths if paths.size else np.zeros(1, np.uint8))
+        name_off = DevBuf.from_numpy(engine, off)
+    dp = DevPermSide(engine, n, encoding.key_mode, dk, do, dord, name, name_off)
+    return dp, dk.download(np.uint64, n), dord.download(np.uint32, n).astype(np.int64)
+
+
 def sort_on_device(engine, keys, oids):
     """GPU pack: (arena-order keys, oids) -> device-resident sorted side (kd_sort_side, LDS-ranked
     LSD radix sort) + host copies (sorted keys, sorted oids, order).  PackError on duplicate keys."""
@@ -181,17 +254,15 @@ def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None, engine=None
     keys = parse_keys(paths, off, encoding)
     info = keys_scan(keys, encoding.key_mode)
     t1 = time.perf_counter()
-    dev = None
+    dev = dperm = None
     if info.ascending:  # git walk order is key order already (int keys of one pk wrap per leaf tree)
         order = np.arange(n, dtype=np.int64)
         sorted_oids = oids
         sort_on = "none"
     elif engine is not None:
-        dk, do, dord = sort_on_device(engine, keys, oids)
-        keys = dk.download(np.uint64, n)
-        order = dord.download(np.uint32, n).astype(np.int64)
-        sorted_oids = do.download(np.uint8, 20 * n).reshape(n, 20)
-        dev = (dk, do)
+        # late materialisation: only the keys are sorted, OIDs and filenames stay in walk order
+        dperm, keys, order = sort_on_device_perm(engine, keys, oids, info, encoding, paths, off)
+        sorted_oids = oids
         sort_on = "gpu"
     else:
         order = np.argsort(keys, kind="stable")
@@ -205,6 +276,11 @@ def pack_side(rel_paths, oids, encoding: PathEncoding, rel_off=None, engine=None
     side.dev = dev
     side.info = info
     side.timing = {"parse_s": t1 - t0, "sort_s": time.perf_counter() - t1, "sort_on": sort_on}
+    if sort_on == "gpu":
+        side.dperm = dperm
+        if encoding.key_mode == N.KD_KEY_HASH:  # the walk-order arena: the join reads it through the order
+            side.name, side.name_off = paths, off
+        return side
     if encoding.key_mode == N.KD_KEY_HASH:
         # sorted relative-path arena (needed for collision verification + pk decode)
         lens = (off[1:] - off[:-1])[order]

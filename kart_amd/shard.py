@@ -56,6 +56,7 @@ def shard_side(side, lo, hi):
     """view of a PackedSide restricted to sorted entries [lo, hi) (indices re-based at 0)"""
     from .packing import PackedSide
 
+    side = side.materialised()
     s = PackedSide(key=side.key[lo:hi], oid=side.oid[lo:hi], key_mode=side.key_mode, order=side.order[lo:hi],
                    encoding=side.encoding)
     if side.name is not None:
