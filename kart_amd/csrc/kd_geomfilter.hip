@@ -388,6 +388,8 @@ struct GfHeadArgs {
     const u8* zeros;    // >= 48 readable zero bytes: the source of an absent side's head loads
     const uint2* bpairs;  // (optional) the blob of each delta side in the arenas, when the heads are
                           // not indexed like the arenas (delta-order heads over per-entry arenas)
+    u32* fb_list;         // (optional) deltas whose head needs its blob are listed here and left to
+    u32* fb_count;        // k_gf_fb, so the streaming pass never waits on a byte-wise blob decode
 };
 
 struct HeadLd {
@@ -407,25 +409,27 @@ __device__ __forceinline__ HeadLd load_head(const GfHeadArgs& g, int s, u32 bi) 
     return L;
 }
 
-__device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g, int s, u32 bi, const HeadLd& L,
-                                            GHit& h, u64 d) {
+// returns false when the geometry needs its blob and the caller defers it (g.fb_list): code FALLBACK
+__device__ __forceinline__ bool decode_head(const GfArgs& a, const GfHeadArgs& g, int s, u32 bi, const HeadLd& L,
+                                            GHit& h, u64 d, bool defer) {
     h.r = -1;
     h.pc = -1;
     h.empty = false;
-    if (bi == KD_NONE) { h.code = GF_NONE; return; }
-    if ((u64)bi >= g.nhead[s]) { h.code = GF_FALLBACK; return; }
+    if (bi == KD_NONE) { h.code = GF_NONE; return true; }
+    if ((u64)bi >= g.nhead[s]) { h.code = GF_FALLBACK; return true; }
     const u32x4 v0 = L.v0, v1 = L.v1, v2 = L.v2;
     const u32 st = v2.w >> 24;
-    if (st == KD_GH_NULL) { h.code = GF_MATCH; return; }
-    if (st != KD_GH_GEOM) { h.code = GF_FALLBACK; return; }
+    if (st == KD_GH_NULL) { h.code = GF_MATCH; return true; }
+    if (st != KD_GH_GEOM) { h.code = GF_FALLBACK; return true; }
     const u32 glen = v2.z;
     const u32 r[11] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, 0u};
     u8 hflags = (u8)(v0.x >> 24);
     const bool fast = env_fast(r, glen, h.r, h.e, h.pc, h.pe);
     if (!fast) {  // XYZ/XYM/XYZM envelope or a NaN one: the byte-wise decode on the blob
-        if (!g.data[s]) { h.code = GF_FALLBACK; h.r = -1; return; }
+        if (!g.data[s]) { h.code = GF_FALLBACK; h.r = -1; return true; }
+        if (defer) { h.code = GF_FALLBACK; h.r = -1; return false; }
         const u32 blob = g.bpairs ? (s ? g.bpairs[d].y : g.bpairs[d].x) : bi;
-        if (blob == KD_NONE || (u64)blob >= a.nblob[s]) { h.code = GF_FALLBACK; h.r = -1; return; }
+        if (blob == KD_NONE || (u64)blob >= a.nblob[s]) { h.code = GF_FALLBACK; h.r = -1; return true; }
         const u8* gp = g.data[s] + g.off[s][blob] + (v2.w & 0xFFFFFFu);
         h.r = gpkg_env(gp, glen, h.e);
         h.pc = -1;
@@ -436,6 +440,7 @@ __device__ __forceinline__ void decode_head(const GfArgs& a, const GfHeadArgs& g
         h.e[0] = h.pe[0]; h.e[1] = h.pe[1]; h.e[2] = h.pe[2]; h.e[3] = h.pe[3];
     }
     h.code = geom_code(a, h, hflags);
+    return true;
 }
 
 // k_gf_match over heads: the same tiles, codes, kept counts and index envelopes.
@@ -472,19 +477,31 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
         u8 ok = 0;
         if (a.enc)
             for (int k = 0; k < nb; k++) wenc[lane * nb + k] = 0;
+        bool deferred = false;
         if (d < n) {
             GHit h;
-            decode_head(a, g, 0, pr.x, L0, h, d);
+            const bool defer = g.fb_list != nullptr;
+            deferred = !decode_head(a, g, 0, pr.x, L0, h, d, defer);
             const int co = h.code;
-            decode_head(a, g, 1, pr.y, L1, h, d);
+            deferred |= !decode_head(a, g, 1, pr.y, L1, h, d, defer);
             const int cn = h.code;
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
-            if (a.enc && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
+            if (a.enc && !deferred && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
                 ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { wenc[lane * nb + k] = v; });
             if (a.enc) a.enc_ok[d] = ok;
         }
         kept += (u32)__popcll(__ballot(keep));
+        {  // deferred deltas: one atomic per wave, slots in lane order
+            const u64 bd = __ballot(deferred);
+            if (bd) {
+                u32 base = 0;
+                if (lane == 0) base = atomicAdd(g.fb_count, (u32)__popcll(bd));
+                base = __shfl(base, 0);
+                if (deferred)
+                    g.fb_list[base + __builtin_amdgcn_mbcnt_hi((u32)(bd >> 32), __builtin_amdgcn_mbcnt_lo((u32)bd, 0))] = (u32)d;
+            }
+        }
         if (a.enc) {
             __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations stay in program order)
             const u64 w0 = d0 + 64ull * wid;
@@ -511,6 +528,36 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
         u32 t = 0;
         for (int w = 0; w < GF_NT / 64; w++) t += s_wc[w];
         a.tile_cnt[blockIdx.x] = t;
+    }
+}
+
+// The deferred deltas (a head that needs its blob: XYZ/XYM/XYZM or NaN envelopes): both sides decoded
+// again with the blob path, codes and the index envelope rewritten, and the tile's kept count
+// corrected — k_gf_heads counted them as kept (FALLBACK), the final codes may not be.
+__global__ __launch_bounds__(256) void k_gf_fb(GfArgs a, GfHeadArgs g) {
+    const u32 cnt = *g.fb_count;
+    const int nb = a.bits / 2;
+    const double vmax = (double)((1ull << a.bits) - 1);
+    for (u32 x = blockIdx.x * 256 + threadIdx.x; x < cnt; x += gridDim.x * 256) {
+        const u64 d = g.fb_list[x];
+        const uint2 pr = ((const uint2*)a.pairs)[d];
+        const HeadLd L0 = load_head(g, 0, pr.x), L1 = load_head(g, 1, pr.y);
+        GHit h;
+        decode_head(a, g, 0, pr.x, L0, h, d, false);
+        const int co = h.code;
+        decode_head(a, g, 1, pr.y, L1, h, d, false);
+        const int cn = h.code;
+        const bool keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
+        *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
+        if (a.enc) {
+            u8* e = a.enc + d * nb;
+            for (int k = 0; k < nb; k++) e[k] = 0;
+            u8 ok = 0;
+            if (cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
+                ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { e[k] = v; });
+            a.enc_ok[d] = ok;
+        }
+        if (!keep) atomicSub(a.tile_cnt + d / GF_TILE, 1u);
     }
 }
 
@@ -638,11 +685,28 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
     a.enc_ok = enc ? dok : nullptr;
     a.tile_cnt = (u32*)t_cnt;
     KD_HIP(hipMemsetAsync(t_nk, 0, 8, ctx->stream));
+    GfHeadArgs gh{};
+    if (g) {
+        gh = *g;
+        // with blob arenas, heads that need their blob are deferred to k_gf_fb
+        if (gh.data[0] && gh.data[1] && n) {
+            void *fl, *fc;
+            if ((rc = ensure(ctx, "gf.fblist", n * 4 + 4, &fl)) || (rc = ensure(ctx, "gf.fbcnt", 16, &fc))) return rc;
+            gh.fb_list = (u32*)fl;
+            gh.fb_count = (u32*)fc;
+            KD_HIP(hipMemsetAsync(fc, 0, 4, ctx->stream));
+        }
+    }
     if (tiles) {
         if (g) {
             if ((rc = launch(ctx, "k_gf_heads", [&] {
-                     hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a, *g);
+                     hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a, gh);
                  })))
+                return rc;
+            if (gh.fb_list && (rc = launch(ctx, "k_gf_fb", [&] {
+                                   const unsigned grid = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 2));
+                                   hipLaunchKernelGGL(k_gf_fb, dim3(grid), dim3(256), 0, ctx->stream, a, gh);
+                               })))
                 return rc;
         } else if ((rc = launch(ctx, "k_gf_match", [&] {
                         hipLaunchKernelGGL(k_gf_match, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a);
