@@ -388,6 +388,8 @@ def run_diff(args, H, polygons):
 
 
 SORT_KERNELS = ("k_rs_bits", "k_sort_hist", "k_sort_scan", "k_sort_pass", "k_gather_oid")
+C4_KERNELS = ("k_seg_sort", "k_sorted3", "k_partition2", "k_apart3", "k_join2", "k_join3", "k_gscan2", "k_place2",
+              "k_place3", "k_resolve3")
 STEP_KERNELS = ("k_partition2", "k_join2", "k_gscan2", "k_place2", "k_fielddiff", "k_dpk_keys", "k_sort_scan",
                 "k_sort_pass", "k_pkm_mark", "k_pkm_scan", "k_pkm_place")
 PKM_MAX_BLOCKS = 1 << 26  # kd_delta_pk_order's bitmap path: pk ranges of at most this many 64-pk blocks
@@ -1172,13 +1174,13 @@ def run_c4(args, H):
     if not args.no_check:  # the generator's own plan (libgit2 rule over planned edits)
         assert conf.shape[0] == M.n_conflict, (conf.shape[0], M.n_conflict)
     eng.prof_reset()
-    eng.prof_select(None if args.time_all else ["k_join2"])
+    eng.prof_select(None if args.time_all else ["k_join2", "k_join3"])
     eng.prof_enable(not args.no_events)
     elapsed = timed(H, eng, pipe.step, args.steps)
     eng.prof_enable(False)
     nall = A.n + O_.n + T.n
     total = sum(H.allgather(nall))
-    kern = kernel_times(eng, ("k_seg_sort", "k_sorted3", "k_partition2", "k_join2", "k_place2", "k_resolve3"))
+    kern = kernel_times(eng, C4_KERNELS)
     eng.prof_reset()
     eng.prof_select(None)
     eng.prof_enable(True)
@@ -1186,16 +1188,21 @@ def run_c4(args, H):
         pipe.step()
     eng.sync()
     eng.prof_enable(False)
-    parts = kernel_times(eng, ("k_seg_sort", "k_sorted3", "k_partition2", "k_join2", "k_gscan2", "k_place2", "k_resolve3"))
-    # classify3 = classify2(ours, theirs) + k_resolve3 over the paths where they differ.
-    # Dominant kernel k_join2, algorithmic bytes per launch: every ours/theirs key + OID once (28 B),
-    # every ours/theirs filename once (hash keys are verified against the names) and one 8-B record
-    # per differing path; with the OIDs in walk order, one 4-B order entry per matched pair
+    parts = kernel_times(eng, C4_KERNELS)
+    # classify3 in one pass (k_join3): dominant kernel k_join3, algorithmic bytes per
+    # launch: every ours/theirs key + OID once (28 B), every ours/theirs filename once (hash keys are
+    # verified against the names), every ancestor key once (8 B), and per differing path its ancestor
+    # OID (20 B) + the staged record (12 B); with the OIDs in walk order, one 4-B order entry per
+    # matched pair.  (KD_MERGE3_JOIN=0: the two-step path, k_join2 + k_resolve3, k_join2 dominant.)
     (kO, oO, _), (kT, oT, _) = srt[1], srt[2]
     _, io, it = np.intersect1d(kO, kT, assume_unique=True, return_indices=True)
     n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((oO[io] != oT[it]).any(axis=1)))
-    alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand + 8 * io.size
-    roof = roofline(kern, "k_join2", alg, args.traffic_json, n, "c4" if H.world == 1 else None)
+    j3 = "k_join3" in kern
+    if j3:
+        alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * A.n + 32 * n_cand + 4 * io.size
+    else:
+        alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand + 8 * io.size
+    roof = roofline(kern, "k_join3" if j3 else "k_join2", alg, args.traffic_json, n, "c4" if H.world == 1 else None)
     seg_alg = 20 * nall  # per entry: the key read, key + 4-B order written (neighbours hit the cache)
     seg = {"what": "kd_sort_segmented_into x3: each bucket's entries (git filename order) ordered by key",
            "ms_per_step_events": round(parts["k_seg_sort"][0] * parts["k_seg_sort"][1] / 3, 4) if "k_seg_sort" in parts else None,

@@ -878,6 +878,9 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
     __shared__ u32x4 s_ch[LD::CHK];
     __shared__ u32x4 s_k[KCH];
     __shared__ u32x4 s_nm[HASH ? LD::NMCH : 1];
+    // the tile's differing paths (their walk records) in path order: in hash mode the filename buffer
+    // holds them (the names are compared before), else a buffer of their own
+    __shared__ u32 s_drec_own[HASH ? 1 : LD::TILE];
     __shared__ u32 s_wave[3 * NT / 64];
     typedef const __attribute__((address_space(1))) u32* gp32;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -966,139 +969,106 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
         for (int k = 0; k < IPT; k++) act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
         ne |= names_ne_batch<IPT, 8>(g.nameA, g.nameOffA, ra, g.nameB, g.nameOffB, rb, act) != 0;
     }
-    // ---- the paths where ours and theirs differ: their ancestor entries ----
-    u32 dif = 0, clean = 0;
-    u64 key[IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
-        const bool d = kind == R_DEL || kind == R_INS || (kind == R_MATCH && chg);
-        dif |= (u32)d << k;
-        clean += kind == R_MATCH && !chg;  // ours == theirs: clean, nothing to record
-        key[k] = kind == R_INS ? sB[jb] : sA[ia];
-    }
-    u64 pos[IPT];
-    const u64 nk = k1e - k0;
-#pragma unroll
-    for (int k = 0; k < IPT; k++) pos[k] = 0;
-    if (__syncthreads_or(dif != 0)) {
-        const int rounds = nk ? 64 - __clzll((long long)nk) : 0;  // wave-uniform
-        u64 lo[IPT], hi[IPT];
-#pragma unroll
-        for (int k = 0; k < IPT; k++) { lo[k] = 0; hi[k] = (dif >> k) & 1 ? nk : 0; }
-        for (int it = 0; it < rounds; it++) {
-            u64 v[IPT], m[IPT];
-#pragma unroll
-            for (int k = 0; k < IPT; k++) {
-                m[k] = (lo[k] + hi[k]) >> 1;
-                const u64 mi = m[k] < nk ? m[k] : (nk ? nk - 1 : 0);
-                v[k] = lk ? sK[mi] : g3.K[k0 + mi];
-            }
-#pragma unroll
-            for (int k = 0; k < IPT; k++) {
-                const bool act = lo[k] < hi[k], lt = v[k] < key[k];
-                lo[k] = act && lt ? m[k] + 1 : lo[k];
-                hi[k] = act && !lt ? m[k] : hi[k];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < IPT; k++) pos[k] = lo[k];
-    }
-    u32 ik[IPT], io[IPT], itt[IPT], rk3[IPT], ro[IPT], rt[IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        const u32 kind = rec[k] >> 25, ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
-        const bool d = (dif >> k) & 1;
-        const bool found = d && pos[k] < nk && (lk ? sK[pos[k]] : g3.K[k0 + pos[k]]) == key[k];
-        ik[k] = found ? (u32)(k0 + pos[k]) : KD_NONE;
-        io[k] = d && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
-        itt[k] = d && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
-    }
-    // rows of the differing paths in the OID / filename arrays (PERM: through the walk orders)
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        rk3[k] = ik[k]; ro[k] = io[k]; rt[k] = itt[k];
-        if (PERM) {
-            rk3[k] = ik[k] != KD_NONE ? *(gp32)(g3.ordK + ik[k]) : KD_NONE;
-            ro[k] = io[k] != KD_NONE ? *(gp32)(g.ordA + io[k]) : KD_NONE;
-            rt[k] = itt[k] != KD_NONE ? *(gp32)(g.ordB + itt[k]) : KD_NONE;
-        }
-    }
-    u32 xk[IPT][5], xo[IPT][5], xt[IPT][5];
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        const gp32 pk = rk3[k] != KD_NONE ? (gp32)(g3.oidK + 20ull * rk3[k]) : (gp32)g.dummy;
-        const gp32 po = ro[k] != KD_NONE ? (gp32)(g.oidA + 20ull * ro[k]) : (gp32)g.dummy;
-        const gp32 pt = rt[k] != KD_NONE ? (gp32)(g.oidB + 20ull * rt[k]) : (gp32)g.dummy;
-#pragma unroll
-        for (int w = 0; w < 5; w++) { xk[k][w] = pk[w]; xo[k][w] = po[w]; xt[k][w] = pt[w]; }
-    }
-    if (HASH) {  // a matched ancestor path must carry the same filename (ours', else theirs')
-        u32 act_o = 0, act_t = 0;
-#pragma unroll
-        for (int k = 0; k < IPT; k++) {
-            act_o |= (u32)(ik[k] != KD_NONE && io[k] != KD_NONE) << k;
-            act_t |= (u32)(ik[k] != KD_NONE && itt[k] != KD_NONE && io[k] == KD_NONE) << k;
-        }
-        if (act_o | act_t)
-            ne |= (names_ne_batch<IPT, 8>(g3.nameK, g3.nameOffK, rk3, g.nameA, g.nameOffA, ro, act_o) |
-                   names_ne_batch<IPT, 8>(g3.nameK, g3.nameOffK, rk3, g.nameB, g.nameOffB, rt, act_t)) != 0;
-    }
-    // libgit2's rule where ours != theirs: a == o -> theirs (merge delta), a == t -> ours, else conflict
-    u32 fc = 0, fm = 0;
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        const bool pa = ik[k] != KD_NONE, po = io[k] != KD_NONE, pt = itt[k] != KD_NONE;
-        u32 dko = 0, dkt = 0;
-#pragma unroll
-        for (int w = 0; w < 5; w++) { dko |= xk[k][w] ^ xo[k][w]; dkt |= xk[k][w] ^ xt[k][w]; }
-        const bool a_eq_o = pa == po && (!pa || dko == 0);
-        const bool a_eq_t = pa == pt && (!pa || dkt == 0);
-        const bool d = (dif >> k) & 1;
-        const bool md = d && a_eq_o, cf = d && !a_eq_o && !a_eq_t;
-        fm |= (u32)md << k;
-        fc |= (u32)cf << k;
-        clean += (d && !a_eq_o && a_eq_t && po) || (md && pt);
-    }
-    if (ne) atomicOr(g.err, 2u);
     if (bad) atomicOr(g.err, 1u);
-    // ---- tile compaction: per item-slot ballots, wave totals exchanged once ----
-    u32 oc = 0, om = 0, wc = 0, wm = 0;
+    // ---- the paths where ours and theirs differ (one side only, or different OIDs): compacted into
+    //      LDS in path order, then resolved one per thread — a few per tile, so the per-item arrays
+    //      of the join do not carry ancestor state ----
+    u32 dif = 0, clean = 0;
 #pragma unroll
     for (int k = 0; k < IPT; k++) {
-        const u64 bc = __ballot((fc >> k) & 1), bm = __ballot((fm >> k) & 1);
-        oc += __builtin_amdgcn_mbcnt_hi((u32)(bc >> 32), __builtin_amdgcn_mbcnt_lo((u32)bc, 0));
-        om += __builtin_amdgcn_mbcnt_hi((u32)(bm >> 32), __builtin_amdgcn_mbcnt_lo((u32)bm, 0));
-        wc += __popcll(bc);
-        wm += __popcll(bm);
+        const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1;
+        dif |= (u32)(kind == R_DEL || kind == R_INS || (kind == R_MATCH && chg)) << k;
+        clean += kind == R_MATCH && !chg;  // ours == theirs: clean, nothing to record
     }
-    u32 wcl = clean;
+    static_assert(!HASH || LD::NMCH * 16 >= 4 * LD::TILE, "the differing paths fit the name buffer");
+    u32* const s_drec = HASH ? (u32*)s_nm : s_drec_own;
+    u32 od = 0, wd = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wcl += __shfl_xor(wcl, o, 64);
-    if (lane == 0) { s_wave[wid] = wc; s_wave[NT / 64 + wid] = wm; s_wave[2 * NT / 64 + wid] = wcl; }
+    for (int k = 0; k < IPT; k++) {
+        const u64 bd = __ballot((dif >> k) & 1);
+        od += __builtin_amdgcn_mbcnt_hi((u32)(bd >> 32), __builtin_amdgcn_mbcnt_lo((u32)bd, 0));
+        wd += __popcll(bd);
+    }
+    if (lane == 0) s_wave[wid] = wd;
     __syncthreads();
-    u32 tc = 0, tm = 0, tcl = 0;
+    u32 ndif = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) {
-        const u32 a = s_wave[w], b = s_wave[NT / 64 + w];
-        if (w < wid) { oc += a; om += b; }
-        tc += a;
-        tm += b;
-        tcl += s_wave[2 * NT / 64 + w];
+        const u32 x = s_wave[w];
+        if (w < wid) od += x;
+        ndif += x;
     }
+#pragma unroll
+    for (int k = 0; k < IPT; k++)
+        if ((dif >> k) & 1) s_drec[od++] = rec[k];
+    __syncthreads();  // (s_wave reused below)
+    const u64 nk = k1e - k0;
+    const int rounds = nk ? 64 - __clzll((long long)nk) : 0;  // wave-uniform
+    u32 tc = 0, tm = 0;  // running conflict / merge-delta counts of the tile
     u32* sc = g3.stage_conf + tile * (u64)C2_STAGE * 3;
     uint2* sm = g3.stage_md + tile * (u64)C2_STAGE;
+    for (u32 c0 = 0; c0 < ndif; c0 += NT) {  // block-uniform
+        const u32 x = c0 + tid;
+        const bool act = x < ndif;
+        const u32 r0 = act ? s_drec[x] : 0u;
+        const u32 kind = r0 >> 25, ia = r0 & 0xFFF, jb = (r0 >> 12) & 0xFFF;
+        const u64 key = kind == R_INS ? sB[jb] : sA[ia];
+        // the ancestor entry: lower bound in the tile's range (LDS, or HBM for a long range)
+        u64 lo = 0, hi = act ? nk : 0;
+        for (int it = 0; it < rounds; it++) {
+            const u64 m = (lo + hi) >> 1;
+            const u64 mi = m < nk ? m : (nk ? nk - 1 : 0);
+            const u64 v = lk ? sK[mi] : g3.K[k0 + mi];
+            const bool on = lo < hi, lt = v < key;
+            lo = on && lt ? m + 1 : lo;
+            hi = on && !lt ? m : hi;
+        }
+        const bool found = act && lo < nk && (lk ? sK[lo] : g3.K[k0 + lo]) == key;
+        const u32 ik = found ? (u32)(k0 + lo) : KD_NONE;
+        const u32 io = act && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
+        const u32 itt = act && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
+        u32 rk3 = ik, ro = io, rt = itt;  // rows in the OID / filename arrays (PERM: through the orders)
+        if (PERM) {
+            rk3 = ik != KD_NONE ? *(gp32)(g3.ordK + ik) : KD_NONE;
+            ro = io != KD_NONE ? *(gp32)(g.ordA + io) : KD_NONE;
+            rt = itt != KD_NONE ? *(gp32)(g.ordB + itt) : KD_NONE;
+        }
+        const gp32 pk = rk3 != KD_NONE ? (gp32)(g3.oidK + 20ull * rk3) : (gp32)g.dummy;
+        const gp32 po = ro != KD_NONE ? (gp32)(g.oidA + 20ull * ro) : (gp32)g.dummy;
+        const gp32 pt = rt != KD_NONE ? (gp32)(g.oidB + 20ull * rt) : (gp32)g.dummy;
+        u32 dko = 0, dkt = 0;
 #pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        if ((fc >> k) & 1) {
-            sc[3 * oc] = ik[k]; sc[3 * oc + 1] = io[k]; sc[3 * oc + 2] = itt[k];
-            oc++;
+        for (int w = 0; w < 5; w++) {
+            const u32 xk = pk[w];
+            dko |= xk ^ po[w];
+            dkt |= xk ^ pt[w];
         }
-        if ((fm >> k) & 1) {
-            sm[om] = make_uint2(io[k], itt[k]);
-            om++;
+        if (HASH) {  // a matched ancestor path must carry the same filename (ours', else theirs')
+            const u32 act_o = ik != KD_NONE && io != KD_NONE;
+            const u32 act_t = ik != KD_NONE && itt != KD_NONE && io == KD_NONE;
+            const u32 rr[1] = {rk3}, oo[1] = {ro}, tt[1] = {rt};
+            if (__syncthreads_or((int)(act_o | act_t)))
+                ne |= (names_ne_batch<1, 8>(g3.nameK, g3.nameOffK, rr, g.nameA, g.nameOffA, oo, act_o) |
+                       names_ne_batch<1, 8>(g3.nameK, g3.nameOffK, rr, g.nameB, g.nameOffB, tt, act_t)) != 0;
         }
+        // libgit2's rule where ours != theirs: a == o -> theirs (merge delta), a == t -> ours, else conflict
+        const bool pa = ik != KD_NONE, pO = io != KD_NONE, pT = itt != KD_NONE;
+        const bool a_eq_o = pa == pO && (!pa || dko == 0);
+        const bool a_eq_t = pa == pT && (!pa || dkt == 0);
+        const bool md = act && a_eq_o, cf = act && !a_eq_o && !a_eq_t;
+        clean += (act && !a_eq_o && a_eq_t && pO) || (md && pT);
+        u32 tot;
+        const u32 off = block_excl_scan<NT>((u32)cf | (u32)md << 16, s_wave, &tot);
+        if (cf) {
+            u32* o = sc + 3 * (tc + (off & 0xFFFF));
+            o[0] = ik; o[1] = io; o[2] = itt;
+        }
+        if (md) sm[tm + (off >> 16)] = make_uint2(io, itt);
+        tc += tot & 0xFFFF;
+        tm += tot >> 16;
     }
+    if (ne) atomicOr(g.err, 2u);
+    const u32 tcl = block_sum<NT>(clean, s_wave);
     if (tid == 0) {
         u32* cc = g.tile_cnt + 4 * tile;
         cc[0] = tcl; cc[1] = tm; cc[2] = 0; cc[3] = tc;
