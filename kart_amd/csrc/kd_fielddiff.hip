@@ -566,6 +566,16 @@ __device__ bool glb_bytes_eq(u64 a, u64 b, u32 n) {
     return true;
 }
 
+#ifndef KD_FD_PROBE_NOPARSE
+#define KD_FD_PROBE_NOPARSE 0
+#endif
+#ifndef KD_FD_PROBE_NOCMP
+#define KD_FD_PROBE_NOCMP 0
+#endif
+#ifndef KD_FD_PROBE_NOLDSCMP
+#define KD_FD_PROBE_NOLDSCMP 0  // timing probe only (results invalid): in-LDS payload compares skipped
+#endif
+
 // Per-round queue of payloads compared cooperatively after the parse (in LDS).
 typedef __attribute__((address_space(3))) u64* lds_u64p;
 typedef __attribute__((address_space(3))) u32* lds_u32p;
@@ -582,7 +592,10 @@ template <class BL>
 __device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb, u32 n, int key, const FdQueue& q) {
     const u32 ya = pa + A.s0, yb = pb + B.s0;  // offsets from the head bases
     const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
-    if (oa != ~0u && ob != ~0u) return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
+    if (oa != ~0u && ob != ~0u) {
+        if (KD_FD_PROBE_NOLDSCMP) return 0u;
+        return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
+    }
     const u64 xa = A.start + pa, xb = B.start + pb;
     if (q.cap && key < 64) {
         const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -800,12 +813,6 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
     for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
 }
 
-#ifndef KD_FD_PROBE_NOPARSE
-#define KD_FD_PROBE_NOPARSE 0
-#endif
-#ifndef KD_FD_PROBE_NOCMP
-#define KD_FD_PROBE_NOCMP 0
-#endif
 constexpr u32 FD_TAB_LDS_MAX = 16384;
 // window shapes (updates per round, head chunks, tail chunks): small features / larger ones
 #ifndef KD_FD_SHAPE_L
@@ -1120,7 +1127,12 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od
             u64* m = masks + u * tb.words;
             for (int w = 4; w < tb.words; w++) m[w] = 0;
             u64 mk[4] = {0, 0, 0, 0};
+#if KD_FD_PROBE_NOPARSE  // timing probe only (results invalid)
+            u8 st = 0;
+            (void)none;
+#else
             u8 st = diff_one_w(A, B, tb, mk, m, none);
+#endif
             if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
             store_masks(m, tb.words, mk, st);
             status[u] = st;
