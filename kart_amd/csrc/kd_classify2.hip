@@ -849,8 +849,11 @@ __global__ __launch_bounds__(256) void k_apart3(const u64* __restrict__ O, u64 n
         const u64 i = part[t], d = t * (u64)C2_TILE, j = d - i;
         const u64 a = i < nO ? O[i] : ~0ull, b = j < nT ? T[j] : ~0ull;
         const u64 key = a < b ? a : b;
-        const u64 guess = (u64)((double)d / (double)(nO + nT) * (double)nK);
-        r = lb_guided<8>(K, nK, key, guess < nK ? guess : nK, 16);
+        // ours is the ancestor with a few edits: its index i is the ancestor rank up to the edits'
+        // running balance (a random walk of ~sqrt(edits) entries), so probes 256 apart around it
+        // bracket the answer; without ours, the proportional position
+        const u64 guess = nO ? (u64)((double)i / (double)nO * (double)nK) : (u64)((double)d / (double)(nO + nT) * (double)nK);
+        r = lb_guided<8>(K, nK, key, guess < nK ? guess : nK, 256);
     }
     if ((threadIdx.x & 7) == 0) apart[t] = r;
 }
