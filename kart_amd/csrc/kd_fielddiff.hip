@@ -832,6 +832,9 @@ constexpr int fd_upr(const void*) { return UPR; }
 #ifndef KD_FD_SSHAPE
 #define KD_FD_SSHAPE 32, 16384  // streamed kernel: updates per tile, LDS bytes per side
 #endif
+#ifndef KD_FD_SDB
+#define KD_FD_SDB false  // streamed kernel: double-buffered spans
+#endif
 #ifndef KD_FD_STREAM_DEFAULT
 #define KD_FD_STREAM_DEFAULT 0
 #endif
@@ -1064,7 +1067,14 @@ struct SBlob {
     __device__ __forceinline__ u32 win(u32 x, u32) const { return res ? x : ~0u; }
 };
 
-template <int T, int CAPB>
+// one tile's spans and this lane's blob offsets (loads issued, values used later)
+struct FdTile {
+    u64 u, co, cn, os, oe, ns, ne;
+    u32 nco, ncn;
+    bool act;
+};
+
+template <int T, int CAPB, bool DB>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                        const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                        u64 n_upd_host, const u64* __restrict__ n_upd_dev,
@@ -1072,7 +1082,8 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od
                                                        u64* __restrict__ masks, u8* __restrict__ status) {
     static_assert(T <= FD_NT && CAPB % 1024 == 0, "stream shape");
     constexpr u32 CAPC = CAPB / 16;             // chunks loaded per side at most
-    __shared__ u32x4 s_img[2 * CAPC + 8];        // old span, new span (+ slack: reads past a blob's end)
+    constexpr int NB = DB ? 2 : 1;              // DB: tile t+1's spans land while tile t is parsed
+    __shared__ u32x4 s_img[NB][2 * CAPC + 8];   // old span, new span (+ slack: reads past a blob's end)
     __shared__ u32 s_dummy;
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
     const int lane = threadIdx.x;
@@ -1093,51 +1104,88 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od
     tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
     tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
     const FdQueue none{(lds_u64p) nullptr, (lds_u32p)&s_dummy, 0};  // payloads compare in place
-    const u32 img_o = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img;
-    const u32 img_n = img_o + 16 * CAPC;
-    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    auto load_tile = [&](u64 tile) {
+        FdTile f;
         const u64 u0 = tile * T, ue = min(u0 + T, n_upd);
-        const u64 u = u0 + lane;
-        const bool act = lane < T && u < ue;
-        // the span of each side, and this lane's blob
+        f.u = u0 + lane;
+        f.act = lane < T && f.u < ue;
         const u64 so0 = ooff[u0], so1 = ooff[ue], sn0 = noff[u0], sn1 = noff[ue];
-        u64 os = 0, oe = 0, ns = 0, ne = 0;
-        if (act) {
-            os = ooff[u]; oe = ooff[u + 1];
-            ns = noff[u]; ne = noff[u + 1];
+        f.os = f.oe = f.ns = f.ne = 0;
+        if (f.act) {
+            f.os = ooff[f.u]; f.oe = ooff[f.u + 1];
+            f.ns = noff[f.u]; f.ne = noff[f.u + 1];
         }
-        const u64 co = ((u64)od + so0) & ~(u64)15, cn = ((u64)nd + sn0) & ~(u64)15;
-        const u32 nco = (u32)min<u64>((((u64)od + so1) - co + 15) >> 4, CAPC);
-        const u32 ncn = (u32)min<u64>((((u64)nd + sn1) - cn + 15) >> 4, CAPC);
-        for (u32 k = 0; k < nco; k += FD_NT)
-            if (k + lane < nco)
-                __builtin_amdgcn_global_load_lds((fd_glb_vp)(co + 16ull * (k + lane)), (fd_lds_vp)(s_img + k), 16, 0, 0);
-        for (u32 k = 0; k < ncn; k += FD_NT)
-            if (k + lane < ncn)
-                __builtin_amdgcn_global_load_lds((fd_glb_vp)(cn + 16ull * (k + lane)), (fd_lds_vp)(s_img + CAPC + k), 16, 0, 0);
-        __syncthreads();  // vmcnt(0) + barrier: the spans have landed
-        if (act) {
-            SBlob A, B;
-            A.start = (u64)od + os; A.len = (u32)(oe - os); A.s0 = (u32)(A.start & 15);
-            A.img = img_o + (u32)((A.start & ~(u64)15) - co);
-            A.res = A.start + A.len <= co + 16ull * nco;
-            B.start = (u64)nd + ns; B.len = (u32)(ne - ns); B.s0 = (u32)(B.start & 15);
-            B.img = img_n + (u32)((B.start & ~(u64)15) - cn);
-            B.res = B.start + B.len <= cn + 16ull * ncn;
-            u64* m = masks + u * tb.words;
-            for (int w = 4; w < tb.words; w++) m[w] = 0;
-            u64 mk[4] = {0, 0, 0, 0};
+        f.co = ((u64)od + so0) & ~(u64)15;
+        f.cn = ((u64)nd + sn0) & ~(u64)15;
+        f.nco = (u32)min<u64>((((u64)od + so1) - f.co + 15) >> 4, CAPC);
+        f.ncn = (u32)min<u64>((((u64)nd + sn1) - f.cn + 15) >> 4, CAPC);
+        return f;
+    };
+    // the spans by LDS-DMA, 16 B per lane, 1 KiB per instruction
+    auto stage = [&](const FdTile& f, int b) {
+        for (u32 k = 0; k < f.nco; k += FD_NT)
+            if (k + lane < f.nco)
+                __builtin_amdgcn_global_load_lds((fd_glb_vp)(f.co + 16ull * (k + lane)), (fd_lds_vp)(s_img[b] + k), 16, 0, 0);
+        for (u32 k = 0; k < f.ncn; k += FD_NT)
+            if (k + lane < f.ncn)
+                __builtin_amdgcn_global_load_lds((fd_glb_vp)(f.cn + 16ull * (k + lane)), (fd_lds_vp)(s_img[b] + CAPC + k), 16, 0, 0);
+    };
+    auto parse = [&](const FdTile& f, int b) {
+        if (!f.act) return;
+        const u32 img_o = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img[b];
+        const u32 img_n = img_o + 16 * CAPC;
+        SBlob A, B;
+        A.start = (u64)od + f.os; A.len = (u32)(f.oe - f.os); A.s0 = (u32)(A.start & 15);
+        A.img = img_o + (u32)((A.start & ~(u64)15) - f.co);
+        A.res = A.start + A.len <= f.co + 16ull * f.nco;
+        B.start = (u64)nd + f.ns; B.len = (u32)(f.ne - f.ns); B.s0 = (u32)(B.start & 15);
+        B.img = img_n + (u32)((B.start & ~(u64)15) - f.cn);
+        B.res = B.start + B.len <= f.cn + 16ull * f.ncn;
+        u64* m = masks + f.u * tb.words;
+        for (int w = 4; w < tb.words; w++) m[w] = 0;
+        u64 mk[4] = {0, 0, 0, 0};
 #if KD_FD_PROBE_NOPARSE  // timing probe only (results invalid)
-            u8 st = 0;
-            (void)none;
+        u8 st = 0;
+        (void)none;
 #else
-            u8 st = diff_one_w(A, B, tb, mk, m, none);
+        u8 st = diff_one_w(A, B, tb, mk, m, none);
 #endif
-            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
-            store_masks(m, tb.words, mk, st);
-            status[u] = st;
+        if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+        store_masks(m, tb.words, mk, st);
+        status[f.u] = st;
+    };
+    if (!DB) {
+        for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+            const FdTile f = load_tile(tile);
+            stage(f, 0);
+            __syncthreads();  // vmcnt(0) + barrier: the spans have landed
+            parse(f, 0);
+            __syncthreads();  // the image is free for the next tile
         }
-        __syncthreads();  // the image is free for the next tile
+        return;
+    }
+    // Double-buffered (one wave per block): tile t+1's offsets are loaded while tile t's spans are in
+    // flight, and its spans are staged before tile t is parsed.  Waiting for t+1's offsets (the
+    // compiler's wait on their registers, ahead of the DMA that uses them) also waits for t's spans,
+    // issued before them: vector-memory loads return in order.
+    u64 tile = blockIdx.x;
+    FdTile cur = load_tile(tile);
+    stage(cur, 0);
+    u64 nt = tile + gridDim.x;
+    FdTile nxt = load_tile(nt < ntiles ? nt : tile);
+    for (int it = 0;; it++) {
+        const int b = it & 1;
+        const bool more = nt < ntiles;  // wave-uniform
+        if (more) stage(nxt, b ^ 1);
+        else __syncthreads();           // vmcnt(0): the last tile's spans have landed
+        const u64 nn = nt + gridDim.x;
+        FdTile after = cur;
+        if (more) after = load_tile(nn < ntiles ? nn : nt);
+        parse(cur, b);
+        if (!more) break;
+        cur = nxt;
+        nxt = after;
+        nt = nn;
     }
 }
 
@@ -1291,7 +1339,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     const bool stream = lds_tab && d_pu == nullptr && (stream_env >= 0 ? stream_env > 0 : !small && KD_FD_STREAM_DEFAULT);
     // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
     // calculator for this launch's LDS), capped at the measured optimum.
-    const void* kern = stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE>
+    const void* kern = stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SDB>
                        : !lds_tab ? (const void*)k_fielddiff_g
                        : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
     int per_cu = 0;
@@ -1311,7 +1359,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
                                tb, to, (const u8*)dt, d_masks, d_status);
         };
         if (stream)
-            hipLaunchKernelGGL(k_fielddiff_s<KD_FD_SSHAPE>, dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
+            hipLaunchKernelGGL((k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SDB>), dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
                                (const u64*)d_ooff, (const u8*)d_nd, (const u64*)d_noff, n_upd, d_n_upd, tb, to,
                                (const u8*)dt, d_masks, d_status);
         else if (!lds_tab)
