@@ -98,6 +98,7 @@ __device__ __forceinline__ u64 mp_search_guided(const u64* __restrict__ A, const
 #define KD_PTOP 16  // lanes per top-level split search
 #endif
 constexpr int C2_PG = 32, C2_PNT = 256;  // tiles per group; threads (8 lanes per inner split)
+template <int TILE>
 __global__ __launch_bounds__(C2_PNT) void k_partition2(const u64* __restrict__ A, u64 nA, const u64* __restrict__ B,
                                                        u64 nB, u64 ntiles, u64* __restrict__ part,
                                                        u64* __restrict__ zero_counts, u32* __restrict__ zero_err,
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(C2_PNT) void k_partition2(const u64* __restrict__ A
     const u64 t0 = (u64)blockIdx.x * C2_PG, t1 = t0 + C2_PG < ntiles ? t0 + C2_PG : ntiles;
     if (tid < 2 * KD_PTOP) {  // wave 0: the group's end splits t0 and t1 (guided: ~3 rounds)
         const u64 t = tid < KD_PTOP ? t0 : t1;
-        u64 d = t * (u64)C2_TILE;
+        u64 d = t * (u64)TILE;
         if (d > total) d = total;
         const u64 guess = (u64)((double)d * (double)nA / (double)(total ? total : 1));
         const u64 i = mp_search_guided<KD_PTOP>(A, B, d, d > nB ? d - nB : 0, d < nA ? d : nA, guess, 2048 / KD_PTOP);
@@ -119,13 +120,13 @@ __global__ __launch_bounds__(C2_PNT) void k_partition2(const u64* __restrict__ A
     }
     __syncthreads();
     const u64 i0 = s_end[0], i1 = s_end[1];
-    const u64 d0 = t0 * (u64)C2_TILE, d1 = t1 * (u64)C2_TILE < total ? t1 * (u64)C2_TILE : total;
+    const u64 d0 = t0 * (u64)TILE, d1 = t1 * (u64)TILE < total ? t1 * (u64)TILE : total;
     const u64 j0 = d0 - i0, j1 = d1 - i1;
     if (tid == 0) part[t0] = i0;
     if (tid == 1 && t1 == ntiles) part[ntiles] = i1;
     const u64 t = t0 + 1 + (u64)(tid / 8);  // 8 lanes per inner split
     if (t < t1) {
-        const u64 d = t * (u64)C2_TILE;
+        const u64 d = t * (u64)TILE;
         const u64 lo = (d > j1 && d - j1 > i0) ? d - j1 : i0, hi = i1 < d - j0 ? i1 : d - j0;
         // proportional guess inside the group's box
         const u64 guess = d1 > d0 ? i0 + (u64)((double)(d - d0) * (double)(i1 - i0) / (double)(d1 - d0)) : lo;
@@ -798,6 +799,14 @@ struct Join3Args {
 #define KD_J3_ACAP 1024   // ancestor keys of a tile staged in LDS (a longer range is searched in HBM)
 #endif
 constexpr int J3_ACAP = KD_J3_ACAP;
+#ifndef KD_J3_IPT
+#define KD_J3_IPT 3  // 768-item tiles: with the ancestor keys, four 256-thread blocks fit a CU's LDS
+#endif
+constexpr int J3_IPT = KD_J3_IPT;
+constexpr int J3_TILE = C2_NT * J3_IPT;
+#ifndef KD_J3_NAME_CH
+#define KD_J3_NAME_CH 1425  // filename bytes of a tile in LDS (C4's 24-B names of a 768-item tile + halo: ~22 KB)
+#endif
 
 // smallest p in [lo, hi] with p == hi || K[p] >= key, by groups of PW lanes (PW-ary search)
 template <int PW>
@@ -838,15 +847,15 @@ __device__ __forceinline__ u64 lb_guided(const u64* __restrict__ K, u64 n, u64 k
 
 // apart[t] for t in [0, ntiles]: 8 lanes per split, guided by the proportional position
 __global__ __launch_bounds__(256) void k_apart3(const u64* __restrict__ O, u64 nO, const u64* __restrict__ T, u64 nT,
-                                                const u64* __restrict__ part, u64 ntiles, const u64* __restrict__ K,
-                                                u64 nK, u64* __restrict__ apart) {
+                                                const u64* __restrict__ part, u64 ntiles, int tile_items,
+                                                const u64* __restrict__ K, u64 nK, u64* __restrict__ apart) {
     const u64 t = ((u64)blockIdx.x * 256 + threadIdx.x) / 8;
     if (t > ntiles) return;  // (whole 8-lane groups)
     u64 r;
     if (t == 0) r = 0;
     else if (t == ntiles) r = nK;
     else {
-        const u64 i = part[t], d = t * (u64)C2_TILE, j = d - i;
+        const u64 i = part[t], d = t * (u64)tile_items, j = d - i;
         const u64 a = i < nO ? O[i] : ~0ull, b = j < nT ? T[j] : ~0ull;
         const u64 key = a < b ? a : b;
         // ours is the ancestor with a few edits: its index i is the ancestor rank up to the edits'
@@ -880,7 +889,8 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
     constexpr int KCH = (8 * (J3_ACAP + 2) + 16 + 15) / 16 + 4;
     __shared__ u32x4 s_ch[LD::CHK];
     __shared__ u32x4 s_k[KCH];
-    __shared__ u32x4 s_nm[HASH ? LD::NMCH : 1];
+    constexpr int NMCH = KD_J3_NAME_CH;
+    __shared__ u32x4 s_nm[HASH ? NMCH : 1];
     // the tile's differing paths (their walk records) in path order: in hash mode the filename buffer
     // holds them (the names are compared before), else a buffer of their own
     __shared__ u32 s_drec_own[HASH ? 1 : LD::TILE];
@@ -921,7 +931,7 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
         nmA0 = uni64(nmA0); nmA1 = uni64(nmA1); nmB0 = uni64(nmB0); nmB1 = uni64(nmB1);
         rnA = mk_range(g.nameA, nmA0, nmA1);
         rnB = mk_range(g.nameB, nmB0, nmB1);
-        lnames = nmA1 >= nmA0 && nmB1 >= nmB0 && (u64)rnA.nch + rnB.nch <= (u64)LD::NMCH;
+        lnames = nmA1 >= nmA0 && nmB1 >= nmB0 && (u64)rnA.nch + rnB.nch <= (u64)NMCH;
         if (lnames) dma_range<NT>(rnB, s_nm + rnA.nch, dma_range<NT>(rnA, s_nm, 0));
     }
     const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
@@ -983,7 +993,7 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
         dif |= (u32)(kind == R_DEL || kind == R_INS || (kind == R_MATCH && chg)) << k;
         clean += kind == R_MATCH && !chg;  // ours == theirs: clean, nothing to record
     }
-    static_assert(!HASH || LD::NMCH * 16 >= 4 * LD::TILE, "the differing paths fit the name buffer");
+    static_assert(!HASH || NMCH * 16 >= 4 * LD::TILE, "the differing paths fit the name buffer");
     u32* const s_drec = HASH ? (u32*)s_nm : s_drec_own;
     u32 od = 0, wd = 0;
 #pragma unroll
@@ -1110,9 +1120,10 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     const u64 nK = K.n, nO = O.n, nT = T.n, total = nO + nT;
     const bool hash = K.key_mode == KD_KEY_HASH;
     const bool perm = ordK || ordO || ordT;
+    constexpr int TILE = J3_TILE;
     if (hash) KD_CHECK((nK == 0 || (K.name && K.name_off)) && (nO == 0 || (O.name && O.name_off)) &&
                        (nT == 0 || (T.name && T.name_off)), "merge3: KD_KEY_HASH needs filenames");
-    const u64 ntiles = (total + C2_TILE - 1) / C2_TILE;
+    const u64 ntiles = (total + TILE - 1) / TILE;
     const u64 n_zero = 2 * ((ntiles + C2_GROUP - 1) / C2_GROUP);
     void *part, *apart, *tcnt, *gsum, *gpre, *sconf, *smd, *dz;
     int rc;
@@ -1130,14 +1141,14 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     const u64* kK = (const u64*)P(K.key, nK);
     rc = launch(ctx, "k_partition2", [&] {
         unsigned nb = (unsigned)((ntiles + C2_PG - 1) / C2_PG);
-        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kO, nO, kT, nT, ntiles, (u64*)part,
-                           d_counts, d_err, (u64*)gsum, n_zero);
+        hipLaunchKernelGGL(k_partition2<TILE>, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kO, nO, kT, nT, ntiles,
+                           (u64*)part, d_counts, d_err, (u64*)gsum, n_zero);
     });
     if (rc) return rc;
     rc = launch(ctx, "k_apart3", [&] {
         const u64 lanes = 8 * (ntiles + 1);
         hipLaunchKernelGGL(k_apart3, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, ctx->stream, kO, nO, kT, nT,
-                           (const u64*)part, ntiles, kK, nK, (u64*)apart);
+                           (const u64*)part, ntiles, TILE, kK, nK, (u64*)apart);
     });
     if (rc) return rc;
     Join3Args a;
@@ -1159,7 +1170,7 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     a.nameOffK = (const u64*)P(K.name_off, nK); a.ordK = (const u32*)P(ordK, nK); a.nK = nK;
     a.apart = (const u64*)apart; a.stage_conf = (u32*)sconf; a.stage_md = (uint2*)smd;
     rc = launch(ctx, "k_join3", [&] {
-#define KD_J3(H, PM) hipLaunchKernelGGL((k_join3<C2_NT, C2_IPT, H, PM>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
+#define KD_J3(H, PM) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, H, PM>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
         if (hash) { if (perm) KD_J3(true, true); else KD_J3(true, false); }
         else { if (perm) KD_J3(false, true); else KD_J3(false, false); }
 #undef KD_J3
@@ -1217,8 +1228,8 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     const u8* empty_oid = (const u8*)dz;
     rc = launch(ctx, "k_partition2", [&] {
         unsigned nb = (unsigned)((ntiles + C2_PG - 1) / C2_PG);
-        hipLaunchKernelGGL(k_partition2, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kA, nA, kB, nB, ntiles, (u64*)part,
-                           d_counts, d_err, zero, n_zero);
+        hipLaunchKernelGGL(k_partition2<C2_TILE>, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kA, nA, kB, nB, ntiles,
+                           (u64*)part, d_counts, d_err, zero, n_zero);
     });
     if (rc) return rc;
     Join2Args g;

@@ -9,7 +9,7 @@ for v in s16db s32db; do
   rc=$?; tail -2 gpurun_out/r4h_parity_$v.log; [ $rc -eq 0 ] || exit $rc
 done
 for wl in c3 c3v; do
-  for v in base s32 s32np s32nc s16np s64np s16db s32db s16dbnp; do
+  for v in base s32 s32np s16np s16db s32db s16dbnp; do
     if [ $v = base ]; then lib=kart_amd/libkartdiff.so; else lib=kart_amd/probe/libkartdiff_$v.so; fi
     KART_AMD_LIB=$lib timeout -k 10 300 python -u bench.py --workload $wl --n 20000000 --steps 10 --no-cpu-baseline \
         --no-host-timing --no-sort --no-check > gpurun_out/r4h_${wl}_$v.json 2> gpurun_out/r4h_${wl}_$v.err
