@@ -455,8 +455,11 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
     const u64 n = a.d_n ? *a.d_n : a.cap;
     const int nb = a.bits / 2;
     const double vmax = (double)((1ull << a.bits) - 1);
-    const u64 t0 = (u64)blockIdx.x * GF_TILE;
     u8* const wenc = (u8*)(s_encw + 64 * 4 * wid);  // this wave's slice
+    // persistent: the grid is the resident set, tiles taken grid-stride (no partial last wave of blocks)
+    const u64 ntiles = (n + GF_TILE - 1) / GF_TILE;
+    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const u64 t0 = tile * GF_TILE;
     u32 kept = 0;
     auto ld_pair = [&](u64 d) {  // (unconditional load, clamped index)
         const uint2 v = *(n ? (const uint2*)a.pairs + (d < n ? d : n - 1) : (const uint2*)g.zeros);
@@ -527,7 +530,9 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
     if (tid == 0) {
         u32 t = 0;
         for (int w = 0; w < GF_NT / 64; w++) t += s_wc[w];
-        a.tile_cnt[blockIdx.x] = t;
+        a.tile_cnt[tile] = t;
+    }
+    __syncthreads();  // s_wc is rewritten by the next tile
     }
 }
 
@@ -699,8 +704,15 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
     }
     if (tiles) {
         if (g) {
+            static int occ_heads = 0;  // resident k_gf_heads workgroups per CU
+            if (occ_heads <= 0) {
+                int nb_ = 0;
+                KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_, (const void*)k_gf_heads, GF_NT, 0));
+                occ_heads = nb_ > 0 ? nb_ : 1;
+            }
+            const u64 hgrid = std::min<u64>(tiles, (u64)ctx->n_cu * (u64)occ_heads);
             if ((rc = launch(ctx, "k_gf_heads", [&] {
-                     hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a, gh);
+                     hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)hgrid), dim3(GF_NT), 0, ctx->stream, a, gh);
                  })))
                 return rc;
             if (gh.fb_list && (rc = launch(ctx, "k_gf_fb", [&] {
