@@ -399,6 +399,7 @@ __device__ __forceinline__ u32 mp_entry(u32 t) {
 // is bounded by the blob length.
 template <int NH, int NTL>
 struct WBlob {
+    static constexpr bool lds_only = false;
     u64 start;  // device address of byte 0
     u32 len;
     u32 s0;     // start - hb (0..15): blob position p is at offset x = p + s0 from hb
@@ -425,7 +426,7 @@ __device__ __forceinline__ void rd12(const BL& b, u32 p, u32& x0, u32& x1, u32& 
     const u32 x = p + b.s0, x4 = x & ~3u, s = x & 3;
     u32 w0, w1, w2, w3;
     const u32 o = b.win(x4, 16);
-    if (o != ~0u) {
+    if (BL::lds_only || o != ~0u) {
         const u32 q = b.img + o;
         w0 = lds_u32(q); w1 = lds_u32(q + 4); w2 = lds_u32(q + 8); w3 = lds_u32(q + 12);
     } else {  // outside both windows: aligned dwords holding a blob byte, from global memory
@@ -447,7 +448,7 @@ __device__ __forceinline__ void rd_legend(const BL& b, u32 lp, u32 h[10]) {
     const u32 x = lp + b.s0, x4 = x & ~3u, s = x & 3;
     u32 w[11];
     const u32 o = b.win(x4, 44);
-    if (o != ~0u) {
+    if (BL::lds_only || o != ~0u) {
 #pragma unroll
         for (int i = 0; i < 11; i++) w[i] = lds_u32(b.img + o + 4 * i);
     } else {
@@ -592,7 +593,7 @@ template <class BL>
 __device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb, u32 n, int key, const FdQueue& q) {
     const u32 ya = pa + A.s0, yb = pb + B.s0;  // offsets from the head bases
     const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
-    if (oa != ~0u && ob != ~0u) {
+    if (BL::lds_only || (oa != ~0u && ob != ~0u)) {
         if (KD_FD_PROBE_NOLDSCMP) return 0u;
         return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
     }
@@ -832,8 +833,8 @@ constexpr int fd_upr(const void*) { return UPR; }
 #ifndef KD_FD_SSHAPE
 #define KD_FD_SSHAPE 32, 16384  // streamed kernel: updates per tile, LDS bytes per side
 #endif
-#ifndef KD_FD_SDB
-#define KD_FD_SDB false  // streamed kernel: double-buffered spans
+#ifndef KD_FD_SPF
+#define KD_FD_SPF false  // streamed kernel: the next tile's spans prefetched into registers
 #endif
 #ifndef KD_FD_STREAM_DEFAULT
 #define KD_FD_STREAM_DEFAULT 0
@@ -1058,32 +1059,59 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
 // its first CAP bytes in LDS; the blobs past them are read from global memory.
 // ================================================================================================
 // one blob inside the tile image (or, past the buffer, in global memory only)
-struct SBlob {
+// LDS: every byte of the blob lies in the loaded part of the image (the decoder is compiled without
+// global-memory paths, so no wait on other loads in flight lands in the parse); else HBM only
+template <bool LDS>
+struct SBlobT {
+    static constexpr bool lds_only = LDS;
     u64 start;
     u32 len;
     u32 s0;    // start & 15: blob position p is at offset x = p + s0 from its aligned chunk
     u32 img;   // LDS byte address of that chunk
-    bool res;  // every byte lies in the loaded part of the image
-    __device__ __forceinline__ u32 win(u32 x, u32) const { return res ? x : ~0u; }
+    __device__ __forceinline__ u32 win(u32 x, u32) const { return LDS ? x : ~0u; }
 };
 
-// one tile's spans and this lane's blob offsets (loads issued, values used later)
+// one tile: its first update, both spans (aligned base, chunk counts) and this lane's blob offsets
 struct FdTile {
     u64 u, co, cn, os, oe, ns, ne;
     u32 nco, ncn;
     bool act;
 };
 
-template <int T, int CAPB, bool DB>
+template <int T, u32 CAPC>
+__device__ __forceinline__ void fd_load_tile(FdTile& f, u64 tile, u64 n_upd, const u8* od, const u64* ooff, const u8* nd,
+                                             const u64* noff) {
+    const int lane = threadIdx.x;
+    const u64 u0 = tile * T, ue = min(u0 + T, n_upd);
+    f.u = u0 + lane;
+    f.act = lane < T && f.u < ue;
+    const u64 so0 = ooff[u0], so1 = ooff[ue], sn0 = noff[u0], sn1 = noff[ue];
+    f.os = f.oe = f.ns = f.ne = 0;
+    if (f.act) {
+        f.os = ooff[f.u]; f.oe = ooff[f.u + 1];
+        f.ns = noff[f.u]; f.ne = noff[f.u + 1];
+    }
+    f.co = ((u64)od + so0) & ~(u64)15;
+    f.cn = ((u64)nd + sn0) & ~(u64)15;
+    f.nco = (u32)min<u64>((((u64)od + so1) - f.co + 15) >> 4, CAPC);
+    f.ncn = (u32)min<u64>((((u64)nd + sn1) - f.cn + 15) >> 4, CAPC);
+}
+
+// PF: the spans of the next tile are loaded into registers (PL chunks per lane: the old span's
+// chunks, then the new span's) while the current tile is parsed from LDS, and written to LDS after
+// it — plain loads, so no wait on them precedes the parse's LDS reads (an LDS-DMA in flight makes
+// the compiler drain every load before any LDS read).  Without PF: LDS-DMA, then the parse.
+template <int T, int CAPB, bool PF>
 __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                        const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                        u64 n_upd_host, const u64* __restrict__ n_upd_dev,
                                                        FdTab tg, FdTabOff to, const u8* __restrict__ tab_base,
                                                        u64* __restrict__ masks, u8* __restrict__ status) {
-    static_assert(T <= FD_NT && CAPB % 1024 == 0, "stream shape");
+    static_assert(T <= FD_NT && CAPB % 512 == 0, "stream shape");
     constexpr u32 CAPC = CAPB / 16;             // chunks loaded per side at most
-    constexpr int NB = DB ? 2 : 1;              // DB: tile t+1's spans land while tile t is parsed
-    __shared__ u32x4 s_img[NB][2 * CAPC + 8];   // old span, new span (+ slack: reads past a blob's end)
+    constexpr int PL = (int)(2 * CAPC / FD_NT);  // PF: chunks per lane
+    static_assert(!PF || PL * FD_NT == 2 * CAPC, "stream shape");
+    __shared__ u32x4 s_img[2 * CAPC + 8];        // old span, new span (+ slack: reads past a blob's end)
     __shared__ u32 s_dummy;
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
     const int lane = threadIdx.x;
@@ -1104,88 +1132,103 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od
     tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
     tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
     const FdQueue none{(lds_u64p) nullptr, (lds_u32p)&s_dummy, 0};  // payloads compare in place
-    auto load_tile = [&](u64 tile) {
-        FdTile f;
-        const u64 u0 = tile * T, ue = min(u0 + T, n_upd);
-        f.u = u0 + lane;
-        f.act = lane < T && f.u < ue;
-        const u64 so0 = ooff[u0], so1 = ooff[ue], sn0 = noff[u0], sn1 = noff[ue];
-        f.os = f.oe = f.ns = f.ne = 0;
-        if (f.act) {
-            f.os = ooff[f.u]; f.oe = ooff[f.u + 1];
-            f.ns = noff[f.u]; f.ne = noff[f.u + 1];
-        }
-        f.co = ((u64)od + so0) & ~(u64)15;
-        f.cn = ((u64)nd + sn0) & ~(u64)15;
-        f.nco = (u32)min<u64>((((u64)od + so1) - f.co + 15) >> 4, CAPC);
-        f.ncn = (u32)min<u64>((((u64)nd + sn1) - f.cn + 15) >> 4, CAPC);
-        return f;
-    };
-    // the spans by LDS-DMA, 16 B per lane, 1 KiB per instruction
-    auto stage = [&](const FdTile& f, int b) {
-        for (u32 k = 0; k < f.nco; k += FD_NT)
-            if (k + lane < f.nco)
-                __builtin_amdgcn_global_load_lds((fd_glb_vp)(f.co + 16ull * (k + lane)), (fd_lds_vp)(s_img[b] + k), 16, 0, 0);
-        for (u32 k = 0; k < f.ncn; k += FD_NT)
-            if (k + lane < f.ncn)
-                __builtin_amdgcn_global_load_lds((fd_glb_vp)(f.cn + 16ull * (k + lane)), (fd_lds_vp)(s_img[b] + CAPC + k), 16, 0, 0);
-    };
-    auto parse = [&](const FdTile& f, int b) {
-        if (!f.act) return;
-        const u32 img_o = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img[b];
-        const u32 img_n = img_o + 16 * CAPC;
-        SBlob A, B;
-        A.start = (u64)od + f.os; A.len = (u32)(f.oe - f.os); A.s0 = (u32)(A.start & 15);
-        A.img = img_o + (u32)((A.start & ~(u64)15) - f.co);
-        A.res = A.start + A.len <= f.co + 16ull * f.nco;
-        B.start = (u64)nd + f.ns; B.len = (u32)(f.ne - f.ns); B.s0 = (u32)(B.start & 15);
-        B.img = img_n + (u32)((B.start & ~(u64)15) - f.cn);
-        B.res = B.start + B.len <= f.cn + 16ull * f.ncn;
-        u64* m = masks + f.u * tb.words;
-        for (int w = 4; w < tb.words; w++) m[w] = 0;
-        u64 mk[4] = {0, 0, 0, 0};
-#if KD_FD_PROBE_NOPARSE  // timing probe only (results invalid)
-        u8 st = 0;
-        (void)none;
-#else
-        u8 st = diff_one_w(A, B, tb, mk, m, none);
-#endif
-        if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
-        store_masks(m, tb.words, mk, st);
-        status[f.u] = st;
-    };
-    if (!DB) {
-        for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-            const FdTile f = load_tile(tile);
-            stage(f, 0);
-            __syncthreads();  // vmcnt(0) + barrier: the spans have landed
-            parse(f, 0);
-            __syncthreads();  // the image is free for the next tile
-        }
-        return;
-    }
-    // Double-buffered (one wave per block): tile t+1's offsets are loaded while tile t's spans are in
-    // flight, and its spans are staged before tile t is parsed.  Waiting for t+1's offsets (the
-    // compiler's wait on their registers, ahead of the DMA that uses them) also waits for t's spans,
-    // issued before them: vector-memory loads return in order.
+    const u32 img_o = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img;
+    const u32 img_n = img_o + 16 * CAPC;
+    typedef __attribute__((address_space(3))) u32x4* l128;
     u64 tile = blockIdx.x;
-    FdTile cur = load_tile(tile);
-    stage(cur, 0);
+    FdTile cur, nxt;
+    fd_load_tile<T, CAPC>(cur, tile, n_upd, od, ooff, nd, noff);
+    u32x4 buf[PF ? PL : 1];
+    if (PF) {  // the first tile's spans through registers too
+#pragma unroll
+        for (int p = 0; p < PL; p++) {
+            const u32 i = 64 * p + lane;
+            const bool o = i < cur.nco, n = !o && i < cur.nco + cur.ncn;
+            const u64 src = o ? cur.co + 16ull * i : cur.cn + 16ull * (i - cur.nco);
+            if (o || n) buf[p] = *(gp128)src;
+        }
+#pragma unroll
+        for (int p = 0; p < PL; p++) {
+            const u32 i = 64 * p + lane;
+            const bool o = i < cur.nco, n = !o && i < cur.nco + cur.ncn;
+            if (o || n) *(l128)(size_t)(o ? img_o + 16 * i : img_n + 16 * (i - cur.nco)) = buf[p];
+        }
+    }
     u64 nt = tile + gridDim.x;
-    FdTile nxt = load_tile(nt < ntiles ? nt : tile);
-    for (int it = 0;; it++) {
-        const int b = it & 1;
-        const bool more = nt < ntiles;  // wave-uniform
-        if (more) stage(nxt, b ^ 1);
-        else __syncthreads();           // vmcnt(0): the last tile's spans have landed
-        const u64 nn = nt + gridDim.x;
-        FdTile after = cur;
-        if (more) after = load_tile(nn < ntiles ? nn : nt);
-        parse(cur, b);
+    if (PF && nt < ntiles) fd_load_tile<T, CAPC>(nxt, nt, n_upd, od, ooff, nd, noff);
+    for (;;) {
+        const bool more = PF && nt < ntiles;  // wave-uniform
+        if (PF) {
+            // the next tile's spans into registers (its offsets were loaded during the last tile)
+            if (more) {
+#pragma unroll
+                for (int p = 0; p < PL; p++) {
+                    const u32 i = 64 * p + lane;
+                    const bool o = i < nxt.nco, n = !o && i < nxt.nco + nxt.ncn;
+                    const u64 src = o ? nxt.co + 16ull * i : nxt.cn + 16ull * (i - nxt.nco);
+                    if (o || n) buf[p] = *(gp128)src;
+                }
+            }
+        } else {
+            for (u32 k = 0; k < cur.nco; k += FD_NT)
+                if (k + lane < cur.nco)
+                    __builtin_amdgcn_global_load_lds((fd_glb_vp)(cur.co + 16ull * (k + lane)), (fd_lds_vp)(s_img + k), 16, 0, 0);
+            for (u32 k = 0; k < cur.ncn; k += FD_NT)
+                if (k + lane < cur.ncn)
+                    __builtin_amdgcn_global_load_lds((fd_glb_vp)(cur.cn + 16ull * (k + lane)), (fd_lds_vp)(s_img + CAPC + k), 16, 0, 0);
+            __syncthreads();  // vmcnt(0) + barrier: the spans have landed
+        }
+        if (cur.act) {
+            SBlobT<true> A, B;
+            A.start = (u64)od + cur.os; A.len = (u32)(cur.oe - cur.os); A.s0 = (u32)(A.start & 15);
+            A.img = img_o + (u32)((A.start & ~(u64)15) - cur.co);
+            B.start = (u64)nd + cur.ns; B.len = (u32)(cur.ne - cur.ns); B.s0 = (u32)(B.start & 15);
+            B.img = img_n + (u32)((B.start & ~(u64)15) - cur.cn);
+            const bool res = A.start + A.len <= cur.co + 16ull * cur.nco && B.start + B.len <= cur.cn + 16ull * cur.ncn;
+            u64* m = masks + cur.u * tb.words;
+            for (int w = 4; w < tb.words; w++) m[w] = 0;
+            u64 mk[4] = {0, 0, 0, 0};
+#if KD_FD_PROBE_NOPARSE  // timing probe only (results invalid)
+            u8 st = 0;
+            (void)none;
+            (void)res;
+#else
+            u8 st;
+            if (res) {
+                st = diff_one_w(A, B, tb, mk, m, none);
+            } else {  // a tile whose span outgrew the buffer: this update from HBM
+                SBlobT<false> GA, GB;
+                GA.start = A.start; GA.len = A.len; GA.s0 = A.s0; GA.img = 0;
+                GB.start = B.start; GB.len = B.len; GB.s0 = B.s0; GB.img = 0;
+                st = diff_one_w(GA, GB, tb, mk, m, none);
+            }
+#endif
+            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+            store_masks(m, tb.words, mk, st);
+            status[cur.u] = st;
+        }
+        if (!PF) {
+            __syncthreads();  // the image is free for the next tile
+            tile += gridDim.x;
+            if (tile >= ntiles) break;
+            fd_load_tile<T, CAPC>(cur, tile, n_upd, od, ooff, nd, noff);
+            continue;
+        }
         if (!more) break;
+        // the parse is done with the image (one wave: its LDS operations stay in order): the next
+        // tile's spans go in, and the tile after it has its offsets loaded
+        const u64 nn = nt + gridDim.x;
+        FdTile aft;
+        if (nn < ntiles) fd_load_tile<T, CAPC>(aft, nn, n_upd, od, ooff, nd, noff);
+#pragma unroll
+        for (int p = 0; p < PL; p++) {
+            const u32 i = 64 * p + lane;
+            const bool o = i < nxt.nco, n = !o && i < nxt.nco + nxt.ncn;
+            if (o || n) *(l128)(size_t)(o ? img_o + 16 * i : img_n + 16 * (i - nxt.nco)) = buf[p];
+        }
         cur = nxt;
-        nxt = after;
         nt = nn;
+        if (nn < ntiles) nxt = aft;
     }
 }
 
@@ -1339,7 +1382,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     const bool stream = lds_tab && d_pu == nullptr && (stream_env >= 0 ? stream_env > 0 : !small && KD_FD_STREAM_DEFAULT);
     // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
     // calculator for this launch's LDS), capped at the measured optimum.
-    const void* kern = stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SDB>
+    const void* kern = stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SPF>
                        : !lds_tab ? (const void*)k_fielddiff_g
                        : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
     int per_cu = 0;
@@ -1359,7 +1402,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
                                tb, to, (const u8*)dt, d_masks, d_status);
         };
         if (stream)
-            hipLaunchKernelGGL((k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SDB>), dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
+            hipLaunchKernelGGL((k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SPF>), dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
                                (const u64*)d_ooff, (const u8*)d_nd, (const u64*)d_noff, n_upd, d_n_upd, tb, to,
                                (const u8*)dt, d_masks, d_status);
         else if (!lds_tab)
