@@ -54,6 +54,7 @@ struct Resolve3Args {
     const u64 *noA, *noO, *noT;
     int hash_mode;
     const uint2* cand;      // classify2(ours, theirs) delta list: (ours | NONE, theirs | NONE)
+    const u32* cand3;       // HAVE_A: k_join3's differing paths with their ancestor entry (a, o, t)
     const u64* c2;          // its counts: inserts, updates, deletes, deltas
     const u32 *pA, *pO, *pT;  // PERM: row of sorted entry i in the side's OID / filename arrays
     u64* desc;              // look-back descriptors [2][nchunk]
@@ -108,7 +109,9 @@ __device__ __forceinline__ u64 half_lower_bound(const u64* __restrict__ X, u64 n
     return lo;
 }
 
-template <int NT, bool PERM>
+// HAVE_A: the candidates come from k_join3 (split form) with the ancestor entry found in its LDS:
+// no bracket, sample or search; c2 = the join's counts (clean paths where ours == theirs, candidates)
+template <int NT, bool PERM, bool HAVE_A>
 __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
     constexpr int PT = C3_CH / NT;
     constexpr int NS = C3_SAMPLES;
@@ -117,13 +120,13 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
     __shared__ u64 s_ex[2];
     __shared__ u64 s_smp[NS];  // ancestor keys at NS evenly spaced bracket positions
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const u64 n = g.c2[3];
+    const u64 n = HAVE_A ? g.c2[1] : g.c2[3];
     while (true) {
         if (tid == 0) s_b[0] = atomicAdd(g.aux, 1u);
         __syncthreads();
         const u64 t = s_b[0];
         if (t == 0 && tid == 0) {  // paths where ours == theirs: clean, and the ancestor-order check
-            atomicAdd((unsigned long long*)g.counts, (unsigned long long)(g.nO - g.c2[1] - g.c2[2]));
+            atomicAdd((unsigned long long*)g.counts, (unsigned long long)(HAVE_A ? g.c2[0] : g.nO - g.c2[1] - g.c2[2]));
             if (g.aux[1]) { atomicOr(g.err, 1u); g.aux[1] = 0; }  // consumed: k_sorted3 only sets it
         }
         const u64 base = t * C3_CH;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
         const u32 cnt = (u32)(n - base < (u64)C3_CH ? n - base : (u64)C3_CH);
         auto key_of = [&](uint2 r) { return *(r.x != KD_NONE ? g.O + r.x : g.T + r.y); };  // one load
         // the chunk's ancestor bracket: [lower_bound(first key), lower_bound(last key) + 1)
-        if (wid == 0) {
+        if (!HAVE_A && wid == 0) {
             const u64 k = key_of(g.cand[base + (lane < 32 ? 0 : cnt - 1)]);
             const u64 p = half_lower_bound(g.A, g.nA, k);
             if (lane == 0) s_b[1] = p;
@@ -139,14 +142,27 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
         }
         uint2 rec[PT];
         u64 key[PT];
+        u32 ia3[PT];
 #pragma unroll
         for (int j = 0; j < PT; j++) {
             const u32 r = tid * PT + j;
-            rec[j] = r < cnt ? g.cand[base + r] : make_uint2(KD_NONE, KD_NONE);
+            if (HAVE_A) {
+                const u32* c3 = g.cand3 + 3 * (base + r);
+                ia3[j] = r < cnt ? c3[0] : KD_NONE;
+                rec[j] = r < cnt ? make_uint2(c3[1], c3[2]) : make_uint2(KD_NONE, KD_NONE);
+            } else {
+                rec[j] = r < cnt ? g.cand[base + r] : make_uint2(KD_NONE, KD_NONE);
+            }
         }
 #pragma unroll
-        for (int j = 0; j < PT; j++) key[j] = (tid * PT + j < cnt) ? key_of(rec[j]) : 0;
+        for (int j = 0; j < PT; j++) key[j] = (!HAVE_A && tid * PT + j < cnt) ? key_of(rec[j]) : 0;
         __syncthreads();
+        u32 lo[PT], hi[PT];
+        bool found[PT];
+        if (HAVE_A) {
+#pragma unroll
+            for (int j = 0; j < PT; j++) { found[j] = ia3[j] != KD_NONE; lo[j] = hi[j] = ia3[j]; }
+        } else {
         const u32 blo = (u32)s_b[1], bhi = (u32)s_b[2];
         const u32 span = bhi - blo;
         // sample level: NS keys at positions blo + s*span/NS in LDS (one gather), each key's
@@ -160,8 +176,6 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
 #endif
         }
         __syncthreads();
-        u32 lo[PT], hi[PT];
-        bool found[PT];
 #pragma unroll
         for (int j = 0; j < PT; j++) {
             // c = number of samples < key: lower_bound lies in (pos(c-1), pos(c)]
@@ -204,6 +218,7 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
                 hi[j] = act && !lt ? m[j] : hi[j];
             }
         }
+        }  // (!HAVE_A)
         // every OID of the chunk's paths loaded before any compare
         u32 ia[PT], io[PT], itt[PT];
         u32 ra[PT], ro[PT], rt[PT];  // their rows in the OID / filename arrays
@@ -305,6 +320,52 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
 
 using namespace kd;
 
+int kd::resolve3_have_a(kd_ctx* ctx, const kd_side& A, const kd_side& O, const kd_side& T, const u32* cand3,
+                        const u64* c2, u32* d_conf, uint2* d_md, u64* counts, u32* derr, const u32* pA, const u32* pO,
+                        const u32* pT) {
+    const bool perm = pA || pO || pT;
+    int rc;
+    const u64 nA = A.n, nO = O.n, nT = T.n;
+    const u64 nchunk = (nO + nT) / C3_CH + 2;
+    void *desc, *aux, *dz;
+    if ((rc = ensure(ctx, "c3.desc", 2 * nchunk * 8, &desc))) return rc;
+    const bool fresh_aux = ctx->bufs["c3.aux"].p == nullptr;
+    if ((rc = ensure(ctx, "c3.aux", 64, &aux))) return rc;
+    if (fresh_aux) KD_HIP(hipMemsetAsync(aux, 0, 64, ctx->stream));
+    if ((rc = device_zeros(ctx, &dz))) return rc;
+    // the resolve's counters and look-back words cleared (no ancestor scan: k_join3 checked its order)
+    rc = launch(ctx, "k_sorted3", [&] {
+        const u64 blocks = std::min<u64>((2 * nchunk + 255) / 256, (u64)ctx->n_cu * 8);
+        hipLaunchKernelGGL(k_sorted3, dim3((unsigned)std::max<u64>(blocks, 1)), dim3(256), 0, ctx->stream,
+                           (const u64*)dz, (u64)0, (u64*)desc, 2 * nchunk, (u32*)aux, counts);
+    });
+    if (rc) return rc;
+    static int occ_r3a[2] = {0, 0};
+    if (occ_r3a[perm] <= 0) {
+        int nb = 0;
+        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, perm ? (const void*)k_resolve3<C3_NT, true, true> : (const void*)k_resolve3<C3_NT, false, true>, C3_NT, 0));
+        occ_r3a[perm] = nb > 0 ? nb : 1;
+    }
+    auto ptr = [&](const void* p, u64 n) { return n && p ? p : (const void*)dz; };
+    Resolve3Args g{};
+    g.A = (const u64*)dz; g.O = (const u64*)ptr(O.key, nO); g.T = (const u64*)ptr(T.key, nT);
+    g.oA = (const u32*)ptr(A.oid, nA); g.oO = (const u32*)ptr(O.oid, nO); g.oT = (const u32*)ptr(T.oid, nT);
+    g.nA = nA; g.nO = nO;
+    g.nmA = (const u8*)ptr(A.name, nA); g.nmO = (const u8*)ptr(O.name, nO); g.nmT = (const u8*)ptr(T.name, nT);
+    g.noA = (const u64*)ptr(A.name_off, nA); g.noO = (const u64*)ptr(O.name_off, nO); g.noT = (const u64*)ptr(T.name_off, nT);
+    g.hash_mode = A.key_mode == KD_KEY_HASH;
+    g.cand = nullptr; g.cand3 = cand3; g.c2 = c2;
+    g.pA = (const u32*)ptr(pA, nA); g.pO = (const u32*)ptr(pO, nO); g.pT = (const u32*)ptr(pT, nT);
+    g.desc = (u64*)desc; g.nchunk = nchunk; g.aux = (u32*)aux;
+    g.out_conf = d_conf; g.out_md = d_md; g.counts = counts; g.err = derr;
+    const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)occ_r3a[perm]);
+    return launch(ctx, "k_resolve3", [&] {
+        if (perm) hipLaunchKernelGGL((k_resolve3<C3_NT, true, true>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
+        else hipLaunchKernelGGL((k_resolve3<C3_NT, false, true>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
+    });
+}
+
 // --------------------------------------------------------------------------------------------
 // host-form helpers
 int kd::stage_side(kd_ctx* ctx, const kd_side* s, const char* tag, kd_side* dev) {
@@ -373,7 +434,7 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     if (occ_r3[perm] <= 0) {
         int nb = 0;
         KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, perm ? (const void*)k_resolve3<C3_NT, true> : (const void*)k_resolve3<C3_NT, false>, C3_NT, 0));
+            &nb, perm ? (const void*)k_resolve3<C3_NT, true, false> : (const void*)k_resolve3<C3_NT, false, false>, C3_NT, 0));
         occ_r3[perm] = nb > 0 ? nb : 1;
     }
     ctx->occ_resolve3 = occ_r3[perm];
@@ -395,8 +456,8 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     // clean count when there are no differing paths)
     const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)ctx->occ_resolve3);
     return launch(ctx, "k_resolve3", [&] {
-        if (perm) hipLaunchKernelGGL((k_resolve3<C3_NT, true>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
-        else hipLaunchKernelGGL((k_resolve3<C3_NT, false>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
+        if (perm) hipLaunchKernelGGL((k_resolve3<C3_NT, true, false>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
+        else hipLaunchKernelGGL((k_resolve3<C3_NT, false, false>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
     });
 }
 

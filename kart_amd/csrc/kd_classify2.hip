@@ -17,6 +17,8 @@
 // completion order, key order inside each tile); no k_place2.
 // (Earlier variants — a persistent register-prefetched join, a decoupled look-back and a per-wave
 // run merge — were measured slower and removed; their numbers are in DESIGN.md §3.1.)
+#include <cstdlib>
+
 #include "kd_join.h"
 
 namespace kd {
@@ -881,7 +883,10 @@ __device__ __forceinline__ u32 dma_range(const Range& R, u32x4* dst, u32 q0) {
     return q0 + np;
 }
 
-template <int NT, int IPT, bool HASH, bool PERM>
+// SPLIT: every differing path is staged with its ancestor entry as a candidate (a, o, t) and the
+// rule is applied by k_resolve3<HAVE_A> over the placed list (many paths per thread: the OID and
+// filename loads of the few differing paths of a tile no longer hold the tile's LDS)
+template <int NT, int IPT, bool HASH, bool PERM, bool SPLIT>
 __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
     const Join2Args& g = g3.j;
     using LD = Join2Lds<NT, IPT>;
@@ -1040,6 +1045,10 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
         const u32 ik = found ? (u32)(k0 + lo) : KD_NONE;
         const u32 io = act && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
         const u32 itt = act && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
+        bool md = false, cf = false;
+        if constexpr (SPLIT) {
+            cf = act;  // a candidate, resolved by k_resolve3
+        } else {
         u32 rk3 = ik, ro = io, rt = itt;  // rows in the OID / filename arrays (PERM: through the orders)
         if (PERM) {
             rk3 = ik != KD_NONE ? *(gp32)(g3.ordK + ik) : KD_NONE;
@@ -1068,8 +1077,10 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
         const bool pa = ik != KD_NONE, pO = io != KD_NONE, pT = itt != KD_NONE;
         const bool a_eq_o = pa == pO && (!pa || dko == 0);
         const bool a_eq_t = pa == pT && (!pa || dkt == 0);
-        const bool md = act && a_eq_o, cf = act && !a_eq_o && !a_eq_t;
+        md = act && a_eq_o;
+        cf = act && !a_eq_o && !a_eq_t;
         clean += (act && !a_eq_o && a_eq_t && pO) || (md && pT);
+        }
         u32 tot;
         const u32 off = block_excl_scan<NT>((u32)cf | (u32)md << 16, s_wave, &tot);
         if (cf) {
@@ -1169,22 +1180,40 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     a.K = kK; a.oidK = (const u8*)P(K.oid, nK); a.nameK = (const u8*)P(K.name, nK);
     a.nameOffK = (const u64*)P(K.name_off, nK); a.ordK = (const u32*)P(ordK, nK); a.nK = nK;
     a.apart = (const u64*)apart; a.stage_conf = (u32*)sconf; a.stage_md = (uint2*)smd;
+    // split (default): the join stages candidates (a, o, t) and k_resolve3 applies the rule;
+    // KD_MERGE3_SPLIT=0 resolves inside the join
+    const char* se = getenv("KD_MERGE3_SPLIT");
+    const bool split = !(se && atoi(se) == 0);
+    void *cand3 = nullptr, *c2 = nullptr;
+    if (split) {
+        if ((rc = ensure(ctx, "c3.cand3", (total + 1) * 12, &cand3))) return rc;
+        if ((rc = ensure(ctx, "c3.c2j", 64, &c2))) return rc;
+    }
     rc = launch(ctx, "k_join3", [&] {
-#define KD_J3(H, PM) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, H, PM>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
-        if (hash) { if (perm) KD_J3(true, true); else KD_J3(true, false); }
-        else { if (perm) KD_J3(false, true); else KD_J3(false, false); }
+#define KD_J3(H, PM, S) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, H, PM, S>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
+        if (split) {
+            if (hash) { if (perm) KD_J3(true, true, true); else KD_J3(true, false, true); }
+            else { if (perm) KD_J3(false, true, true); else KD_J3(false, false, true); }
+        } else {
+            if (hash) { if (perm) KD_J3(true, true, false); else KD_J3(true, false, false); }
+            else { if (perm) KD_J3(false, true, false); else KD_J3(false, false, false); }
+        }
 #undef KD_J3
     });
     if (rc) return rc;
+    u64* jcounts = split ? (u64*)c2 : d_counts;
     rc = launch(ctx, "k_gscan2", [&] {
         hipLaunchKernelGGL(k_gscan2, dim3(1), dim3(1024), 0, ctx->stream, (const u64*)gsum, (u64)(n_zero / 2),
-                           (u64*)gpre, d_counts, 1);
+                           (u64*)gpre, jcounts, 1);
     });
     if (rc) return rc;
-    return launch(ctx, "k_place3", [&] {
+    rc = launch(ctx, "k_place3", [&] {
         hipLaunchKernelGGL(k_place3, dim3((unsigned)ntiles), dim3(64), 0, ctx->stream, (const u32*)sconf,
-                           (const uint2*)smd, (const u32*)tcnt, (const u64*)gpre, d_conf, d_md);
+                           (const uint2*)smd, (const u32*)tcnt, (const u64*)gpre, split ? (u32*)cand3 : d_conf, d_md);
     });
+    if (rc || !split) return rc;
+    return resolve3_have_a(ctx, K, O, T, (const u32*)cand3, (const u64*)c2, d_conf, d_md, d_counts, d_err, ordK, ordO,
+                           ordT);
 }
 
 int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32* d_delta, u32* d_upd,

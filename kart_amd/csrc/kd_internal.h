@@ -140,6 +140,10 @@ void comm_release(kd_ctx* ctx);
 // d_dkey / d_ukey (optional): the join key of every delta / update record, beside the lists
 // three-way merge in one pass (k_join3): conflicts (a, o, t) and merge deltas (o, t) in path order,
 // counts = clean, conflicts, merge deltas, 0; ord*: late materialisation (walk rows of sorted entries)
+// k_resolve3 over k_join3's candidates (a, o, t) with the ancestor entries already found
+int resolve3_have_a(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd_side& T, const u32* cand3, const u64* c2,
+                    u32* d_conf, uint2* d_md, u64* d_counts, u32* d_err, const u32* ordK, const u32* ordO,
+                    const u32* ordT);
 int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
                        u64* d_counts, u32* d_err, const u32* ordK = nullptr, const u32* ordO = nullptr,
                        const u32* ordT = nullptr);
