@@ -456,8 +456,10 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
     const int nb = a.bits / 2;
     const double vmax = (double)((1ull << a.bits) - 1);
     u8* const wenc = (u8*)(s_encw + 64 * 4 * wid);  // this wave's slice
-    // persistent: the grid is the resident set, tiles taken grid-stride (no partial last wave of blocks)
-    const u64 ntiles = (n + GF_TILE - 1) / GF_TILE;
+    // persistent: the grid is the resident set, tiles taken grid-stride (no partial last wave of
+    // blocks).  Every tile of the capacity is visited: k_gf_scan reads all their kept counts, and a
+    // tile past the device count writes 0
+    const u64 ntiles = (a.cap + GF_TILE - 1) / GF_TILE;
     for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const u64 t0 = tile * GF_TILE;
     u32 kept = 0;
