@@ -1191,15 +1191,14 @@ def run_c4(args, H):
     parts = kernel_times(eng, C4_KERNELS)
     # classify3 in one pass (k_join3): dominant kernel k_join3, algorithmic bytes per
     # launch: every ours/theirs key + OID once (28 B), every ours/theirs filename once (hash keys are
-    # verified against the names), every ancestor key once (8 B), and per differing path its ancestor
-    # OID (20 B) + the staged record (12 B); with the OIDs in walk order, one 4-B order entry per
-    # matched pair.  (KD_MERGE3_JOIN=0: the two-step path, k_join2 + k_resolve3, k_join2 dominant.)
+    # verified against the names), every ancestor key once (8 B), and per differing path the staged
+    # candidate (a, o, t) (12 B); with the OIDs in walk order, one 4-B order entry per matched pair.  (KD_MERGE3_JOIN=0: the two-step path, k_join2 + k_resolve3, k_join2 dominant.)
     (kO, oO, _), (kT, oT, _) = srt[1], srt[2]
     _, io, it = np.intersect1d(kO, kT, assume_unique=True, return_indices=True)
     n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((oO[io] != oT[it]).any(axis=1)))
     j3 = "k_join3" in kern
-    if j3:
-        alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * A.n + 32 * n_cand + 4 * io.size
+    if j3:  # (split form: the join stages a 12-B candidate per differing path, k_resolve3 reads its OIDs)
+        alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * A.n + 12 * n_cand + 4 * io.size
     else:
         alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand + 8 * io.size
     roof = roofline(kern, "k_join3" if j3 else "k_join2", alg, args.traffic_json, n, "c4" if H.world == 1 else None)

@@ -12,4 +12,4 @@ python3 -c "import json;d=json.load(open('gpurun_out/r4m_bench_c4.json'));print(
 KD_MERGE3_SPLIT=0 timeout -k 10 400 python -u bench.py --workload c4 --steps 20 --no-cpu-baseline > gpurun_out/r4m_bench_c4_nosplit.json 2> gpurun_out/r4m_bench_c4_nosplit.err
 rc=$?; tail -1 gpurun_out/r4m_bench_c4_nosplit.err; [ $rc -eq 0 ] || exit $rc
 python3 -c "import json;d=json.load(open('gpurun_out/r4m_bench_c4_nosplit.json'));print(d['ms_per_step'], d['step_kernels_avg_ms'], d['presorted'])"
-bash scripts/gpu_r4_i.sh
+echo "m done"
