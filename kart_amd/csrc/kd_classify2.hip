@@ -411,7 +411,14 @@ struct TileCounts {
     u32 tnd, tnu, tdel;  // tile totals: deltas, updates, deletes
 };
 
-template <int NT, int IPT>
+// a workgroup barrier for LDS only: waits for this wave's LDS operations, not for its global loads
+// in flight (__syncthreads' release fence would drain those: the prefetch of a persistent kernel)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt at their maxima (no wait)
+    __builtin_amdgcn_s_barrier();
+}
+
+template <int NT, int IPT, bool LB = false>
 __device__ __forceinline__ TileCounts tile_counts(const u32 rec[IPT], u32* s_wave) {
     TileCounts c;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -437,7 +444,8 @@ __device__ __forceinline__ TileCounts tile_counts(const u32 rec[IPT], u32* s_wav
         wx += __popcll(bx);
     }
     if (lane == 0) { s_wave[wid] = wd; s_wave[NT / 64 + wid] = wu; s_wave[2 * NT / 64 + wid] = wx; }
-    __syncthreads();
+    if (LB) lds_barrier();
+    else __syncthreads();
     u32 tnd = 0, tnu = 0, tdel = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) {
@@ -649,6 +657,144 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         u64* gs = g.gsum + 2 * (tile / C2_GROUP);
         atomicAdd((unsigned long long*)gs, (unsigned long long)(c.tnd | (u64)c.tnu << 32));
         atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)c.tdel << 32));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_join2r: the large int-key join, persistent with the next tile prefetched into registers.
+// A resident grid walks the tiles grid-stride; while tile t is walked, compared and written out
+// from LDS, tile t+1's keys and OIDs (keys + OIDs of both sides, ~28 KB) are in flight as plain
+// 16-B loads into registers (P per thread), and tile t+2's split points too.  After tile t the
+// registers go to LDS.  The barriers inside a tile are LDS-only (lds_barrier), so nothing in the
+// tile's own work waits for the prefetch — an LDS-DMA double buffer (tried in round 2) makes the
+// compiler drain every load before each LDS read.
+// ---------------------------------------------------------------------------------------------
+template <int NT, int IPT>
+struct J2RTile {
+    TileGeo q;
+    TileRanges r;
+    Range oa, ob;
+    u32 n0, n1, n2, n3;  // cumulative chunk counts: keys A, keys B, OIDs A, OIDs B
+};
+
+template <int NT, int IPT>
+__device__ __forceinline__ void j2r_plan(const Join2Args& g, u64 tile, u64 p0, u64 p1, J2RTile<NT, IPT>& T) {
+    using LD = Join2Lds<NT, IPT>;
+    T.q = tile_geo_from(g, tile, LD::TILE, p0, p1);
+    T.r = tile_ranges(g, T.q);
+    T.oa = mk_range(g.oidA, 20 * T.q.i0, 20 * T.q.i1);
+    T.ob = mk_range(g.oidB, 20 * T.q.j0, 20 * T.q.j1e);
+    T.n0 = T.r.ka.nch;
+    T.n1 = T.n0 + T.r.kb.nch;
+    T.n2 = T.n1 + T.oa.nch;
+    T.n3 = T.n2 + T.ob.nch;
+}
+
+template <int NT, int IPT>
+__global__ __launch_bounds__(NT) void k_join2r(Join2Args g) {
+    using LD = Join2Lds<NT, IPT>;
+    static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
+    constexpr int P = (LD::CHK + LD::OCH + NT - 1) / NT;  // prefetched chunks per thread
+    __shared__ u32x4 s_ch[LD::CHK];
+    __shared__ u32x4 s_oid[LD::OCH];
+    __shared__ u32 s_wave[3 * NT / 64];
+    typedef __attribute__((address_space(3))) u32x4* l128;
+    typedef const __attribute__((address_space(1))) u32x4* g128;
+    const int tid = threadIdx.x;
+    const u64 ntiles = g.ntiles;
+    u64 tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    J2RTile<NT, IPT> cur, nxt;
+    u32x4 buf[P];
+    auto fetch = [&](const J2RTile<NT, IPT>& T) {
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            const u32 c = tid + NT * p;
+            u64 src = 0;
+            if (c < T.n0) src = T.r.ka.base + 16ull * c;
+            else if (c < T.n1) src = T.r.kb.base + 16ull * (c - T.n0);
+            else if (c < T.n2) src = T.oa.base + 16ull * (c - T.n1);
+            else if (c < T.n3) src = T.ob.base + 16ull * (c - T.n2);
+            if (c < T.n3) buf[p] = *(g128)src;
+        }
+    };
+    auto deposit = [&](const J2RTile<NT, IPT>& T) {
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            const u32 c = tid + NT * p;
+            if (c < T.n0) *(l128)(s_ch + c) = buf[p];
+            else if (c < T.n1) *(l128)(s_ch + T.r.c1 + (c - T.n0)) = buf[p];
+            else if (c < T.n2) *(l128)(s_oid + (c - T.n1)) = buf[p];
+            else if (c < T.n3) *(l128)(s_oid + T.oa.nch + (c - T.n2)) = buf[p];
+        }
+    };
+    j2r_plan<NT, IPT>(g, tile, g.part[tile], g.part[tile + 1], cur);
+    fetch(cur);
+    deposit(cur);
+    u64 nt = tile + gridDim.x;
+    u64 np0 = 0, np1 = 0;
+    if (nt < ntiles) { np0 = g.part[nt]; np1 = g.part[nt + 1]; }
+    lds_barrier();
+    for (;;) {
+        const bool more = nt < ntiles;  // block-uniform
+        if (more) {
+            j2r_plan<NT, IPT>(g, nt, np0, np1, nxt);
+            fetch(nxt);  // in flight under this tile's work
+        }
+        const u64 nn = nt + gridDim.x;
+        u64 ap0 = 0, ap1 = 0;
+        if (more && nn < ntiles) { ap0 = g.part[nn]; ap1 = g.part[nn + 1]; }
+        // ---- tile `tile` from LDS ----
+        const TileGeo& q = cur.q;
+        if (!q.ok && tid == 0) atomicOr(g.err, 1u);
+        const u64* sA = (const u64*)((const u8*)s_ch + cur.r.ka.skew) + q.has_lbA;
+        const u64* sB = (const u64*)((const u8*)(s_ch + cur.r.c1) + cur.r.kb.skew) + q.has_lbB;
+        u32 rec[IPT];
+        bool bad = false;
+        tile_walk<NT, IPT>(sA, sB, q, rec, bad);
+        for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
+        for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
+        {
+            typedef const __attribute__((address_space(3))) u32* l32;
+            const u32 ob = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_oid;
+            const u32 baseA = ob + cur.oa.skew, baseB = ob + 16 * cur.oa.nch + cur.ob.skew;
+#pragma unroll
+            for (int k = 0; k < IPT; k++) {
+                const bool m = (rec[k] >> 25) == R_MATCH;
+                const u32 pa = baseA + 20 * (m ? (rec[k] & 0xFFF) : 0), pb = baseB + 20 * (m ? ((rec[k] >> 12) & 0xFFF) : 0);
+                u32 d = 0;
+#pragma unroll
+                for (int w = 0; w < 5; w++) d |= *(l32)(size_t)(pa + 4 * w) ^ *(l32)(size_t)(pb + 4 * w);
+                if (m && d) rec[k] |= 1u << 24;
+            }
+        }
+        if (bad) atomicOr(g.err, 1u);
+        const TileCounts c = tile_counts<NT, IPT, true>(rec, s_wave);
+        uint2* sd = g.stage_delta + tile * (u64)C2_STAGE;
+        uint2* su = g.stage_upd + tile * (u64)C2_STAGE;
+        u64* kd = g.stage_dkey ? g.stage_dkey + tile * (u64)C2_STAGE : nullptr;
+        u64* ku = g.stage_dkey ? g.stage_ukey + tile * (u64)C2_STAGE : nullptr;
+        tile_write<IPT>(rec, c, q.i0, q.j0, sd, su, sA, sB, kd, ku);
+        if (tid == 0) {
+            u32* cc = g.tile_cnt + 4 * tile;
+            const u32 tins = c.tnd - c.tnu - c.tdel;
+            cc[0] = tins;
+            cc[1] = c.tnu;
+            cc[2] = c.tdel;
+            cc[3] = c.tnd;
+            u64* gs = g.gsum + 2 * (tile / C2_GROUP);
+            atomicAdd((unsigned long long*)gs, (unsigned long long)(c.tnd | (u64)c.tnu << 32));
+            atomicAdd((unsigned long long*)gs + 1, (unsigned long long)(tins | (u64)c.tdel << 32));
+        }
+        if (!more) break;
+        lds_barrier();  // every thread is done with the tile's LDS (and s_wave)
+        deposit(nxt);
+        lds_barrier();
+        cur = nxt;
+        tile = nt;
+        nt = nn;
+        np0 = ap0;
+        np1 = ap1;
     }
 }
 
@@ -1180,10 +1326,10 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     a.K = kK; a.oidK = (const u8*)P(K.oid, nK); a.nameK = (const u8*)P(K.name, nK);
     a.nameOffK = (const u64*)P(K.name_off, nK); a.ordK = (const u32*)P(ordK, nK); a.nK = nK;
     a.apart = (const u64*)apart; a.stage_conf = (u32*)sconf; a.stage_md = (uint2*)smd;
-    // split (default): the join stages candidates (a, o, t) and k_resolve3 applies the rule;
-    // KD_MERGE3_SPLIT=0 resolves inside the join
+    // KD_MERGE3_SPLIT=1: the join stages candidates (a, o, t) and k_resolve3 applies the rule (C4,
+    // r4n: 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
     const char* se = getenv("KD_MERGE3_SPLIT");
-    const bool split = !(se && atoi(se) == 0);
+    const bool split = se && atoi(se) == 1;
     void *cand3 = nullptr, *c2 = nullptr;
     if (split) {
         if ((rc = ensure(ctx, "c3.cand3", (total + 1) * 12, &cand3))) return rc;
@@ -1281,6 +1427,18 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         return e ? strtoull(e, nullptr, 10) : (u64)1 << 26;
     }();
     const bool oid_lds = nA + nB >= oid_lds_min;
+    // the persistent register-prefetched form of the large int-key join (KD_J2R=0: one tile per
+    // workgroup)
+    static const bool j2r = [] {
+        const char* e = getenv("KD_J2R");
+        return !(e && atoi(e) == 0);
+    }();
+    static int j2r_occ = 0;
+    if (j2r && j2r_occ <= 0) {
+        int nb = 0;
+        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_join2r<C2_NT, C2_IPT>, C2_NT, 0));
+        j2r_occ = nb > 0 ? nb : 1;
+    }
     g.ordA = nA && ordA ? ordA : (const u32*)dz;
     g.ordB = nB && ordB ? ordB : (const u32*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;
@@ -1292,17 +1450,21 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     rc = launch(ctx, "k_join2", [&] {
 #define KD_J2(U, H, P) hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, U, H, P>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g)
 #define KD_J2OL(U) hipLaunchKernelGGL((k_join2<C2_NT, C2_IPT, U, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, g)
+#define KD_J2R() hipLaunchKernelGGL((k_join2r<C2_NT, C2_IPT>), dim3((unsigned)std::min<u64>(ntiles, (u64)ctx->n_cu * j2r_occ)), dim3(C2_NT), 0, ctx->stream, g)
         if (perm) {
             if (unord) { if (hash) KD_J2(true, true, true); else KD_J2(true, false, true); }
             else { if (hash) KD_J2(false, true, true); else KD_J2(false, false, true); }
         } else if (!hash && oid_lds) {
-            if (unord) KD_J2OL(true); else KD_J2OL(false);
+            if (unord) KD_J2OL(true);
+            else if (j2r) KD_J2R();
+            else KD_J2OL(false);
         } else {
             if (unord) { if (hash) KD_J2(true, true, false); else KD_J2(true, false, false); }
             else { if (hash) KD_J2(false, true, false); else KD_J2(false, false, false); }
         }
 #undef KD_J2
 #undef KD_J2OL
+#undef KD_J2R
     });
     if (rc || unord) return rc;
     rc = launch(ctx, "k_gscan2", [&] {
