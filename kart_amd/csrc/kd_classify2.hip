@@ -1427,11 +1427,12 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         return e ? strtoull(e, nullptr, 10) : (u64)1 << 26;
     }();
     const bool oid_lds = nA + nB >= oid_lds_min;
-    // the persistent register-prefetched form of the large int-key join (KD_J2R=0: one tile per
-    // workgroup)
+    // KD_J2R=1: the persistent register-prefetched form of the large int-key join (C3, r4o: k_join2
+    // 1.93 vs 1.18 ms — three resident tiles per CU prefetching hold fewer bytes in flight than five
+    // one-shot tiles; one tile per workgroup stays the default)
     static const bool j2r = [] {
         const char* e = getenv("KD_J2R");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) == 1;
     }();
     static int j2r_occ = 0;
     if (j2r && j2r_occ <= 0) {
