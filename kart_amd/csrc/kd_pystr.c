@@ -137,6 +137,111 @@ static PyObject* pk_at(PyObject* list, const long long* arr, Py_ssize_t i) {
     return PyLong_FromLongLong(arr[i]);
 }
 
+/* ---- Promise: partial(get_feature_from_blob, blob) with the blob made on first use ----
+ * What a delta half's value is (kart/base_dataset.py:506-507 promise, base_diff_writer.py:506 reads
+ * `value.args[0]`): calling it returns func(blob); .args = (blob,), .func, .keywords as a partial
+ * has.  The LazyBlob (blob_type(src, i)) is created the first time the value or .args is used, so a
+ * diff builds one object per delta half here instead of three (blob, partial, args tuple) plus the
+ * leaf-index int. */
+typedef struct {
+    PyObject_HEAD
+    PyObject* func;
+    PyObject* src;
+    PyObject* blob_type;
+    PyObject* blob;
+    long long i;
+} Promise;
+
+static PyTypeObject PromiseType;
+
+static PyObject* promise_blob(Promise* p) {
+    if (!p->blob) p->blob = PyObject_CallFunction(p->blob_type, "OL", p->src, p->i);
+    return p->blob;  /* borrowed; NULL on error */
+}
+
+static PyObject* promise_call(PyObject* self, PyObject* args, PyObject* kw) {
+    Promise* p = (Promise*)self;
+    PyObject* blob = promise_blob(p);
+    if (!blob) return NULL;
+    const Py_ssize_t na = PyTuple_GET_SIZE(args);
+    if (na == 0 && (!kw || PyDict_GET_SIZE(kw) == 0)) return PyObject_CallOneArg(p->func, blob);
+    PyObject* all = PyTuple_New(na + 1);
+    if (!all) return NULL;
+    Py_INCREF(blob);
+    PyTuple_SET_ITEM(all, 0, blob);
+    for (Py_ssize_t k = 0; k < na; k++) {
+        PyObject* x = PyTuple_GET_ITEM(args, k);
+        Py_INCREF(x);
+        PyTuple_SET_ITEM(all, k + 1, x);
+    }
+    PyObject* r = PyObject_Call(p->func, all, kw);
+    Py_DECREF(all);
+    return r;
+}
+
+static PyObject* promise_get_args(PyObject* self, void* c) {
+    PyObject* blob = promise_blob((Promise*)self);
+    return blob ? PyTuple_Pack(1, blob) : NULL;
+}
+
+static PyObject* promise_get_func(PyObject* self, void* c) {
+    Py_INCREF(((Promise*)self)->func);
+    return ((Promise*)self)->func;
+}
+
+static PyObject* promise_get_keywords(PyObject* self, void* c) { return PyDict_New(); }
+
+static PyObject* promise_repr(PyObject* self) {
+    PyObject* blob = promise_blob((Promise*)self);
+    if (!blob) return NULL;
+    return PyUnicode_FromFormat("functools.partial(%R, %R)", ((Promise*)self)->func, blob);
+}
+
+static int promise_traverse(PyObject* self, visitproc visit, void* arg) {
+    Promise* p = (Promise*)self;
+    Py_VISIT(p->func);
+    Py_VISIT(p->src);
+    Py_VISIT(p->blob_type);
+    Py_VISIT(p->blob);
+    return 0;
+}
+
+static int promise_clear(PyObject* self) {
+    Promise* p = (Promise*)self;
+    Py_CLEAR(p->func);
+    Py_CLEAR(p->src);
+    Py_CLEAR(p->blob_type);
+    Py_CLEAR(p->blob);
+    return 0;
+}
+
+static void promise_dealloc(PyObject* self) {
+    PyObject_GC_UnTrack(self);
+    promise_clear(self);
+    Py_TYPE(self)->tp_free(self);
+}
+
+static PyGetSetDef promise_getset[] = {
+    {"args", promise_get_args, NULL, "(blob,): the promise's one argument", NULL},
+    {"func", promise_get_func, NULL, "the getter the blob is passed to", NULL},
+    {"keywords", promise_get_keywords, NULL, "always empty", NULL},
+    {NULL, NULL, NULL, NULL, NULL},
+};
+
+static PyTypeObject PromiseType = {
+    PyVarObject_HEAD_INIT(NULL, 0)
+    .tp_name = "kart_amd._kd_pystr.Promise",
+    .tp_basicsize = sizeof(Promise),
+    .tp_dealloc = promise_dealloc,
+    .tp_repr = promise_repr,
+    .tp_call = promise_call,
+    .tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC,
+    .tp_doc = "partial(get_feature_from_blob, blob) whose blob is made on first use",
+    .tp_traverse = promise_traverse,
+    .tp_clear = promise_clear,
+    .tp_getset = promise_getset,
+};
+
 /* build_deltas(delta_type, kv_type, blob_type, partial_type, old_get, new_get, old_src, new_src,
  *              old_leaf, new_leaf, old_pk, new_pk, own)
  * old_leaf / new_leaf: int64 buffers of n leaf indices (-1: the side is absent); old_pk / new_pk: int64
@@ -185,7 +290,8 @@ static PyObject* build_deltas(PyObject* self, PyObject* args) {
         d_flags = slot_offset(dt, "flags");
         if (kv_key < 0 || kv_val < 0 || d_old < 0 || d_new < 0 || d_type < 0 || d_flags < 0) goto fail;
     }
-    if (partial_maker_init(&pm[0], pt, og) < 0 || partial_maker_init(&pm[1], pt, ng) < 0) goto fail;
+    const int promise_mode = pt == (PyObject*)&PromiseType;  /* lazy-blob promises, else functools.partial */
+    if (!promise_mode && (partial_maker_init(&pm[0], pt, og) < 0 || partial_maker_init(&pm[1], pt, ng) < 0)) goto fail;
     t_ins = PyUnicode_InternFromString("insert"); t_upd = PyUnicode_InternFromString("update");
     t_del = PyUnicode_InternFromString("delete");
     zero = PyLong_FromLong(0);
@@ -213,18 +319,30 @@ static PyObject* build_deltas(PyObject* self, PyObject* args) {
             } else {
                 pk = pk_at(s ? np_list : op_list, s ? npp : opp, i);
             }
-            PyObject* blob = BT->tp_alloc(BT, 0);
-            PyObject* li = PyLong_FromLongLong(leaf[s]);
-            if (!pk || !blob || !li) { Py_XDECREF(pk); Py_XDECREF(blob); Py_XDECREF(li); goto item_fail; }
             PyObject* src = s ? ns : os_;
-            Py_INCREF(src);
-            set_slot(blob, b_src, src);
-            set_slot(blob, b_i, li);
-            Py_INCREF(Py_None);
-            set_slot(blob, b_data, Py_None);
-            PyObject* promise = partial_make(&pm[s], s ? ng : og, blob);
-            Py_DECREF(blob);
-            if (!promise) { Py_DECREF(pk); goto item_fail; }
+            PyObject* promise;
+            if (promise_mode) {
+                Promise* pr = pk ? (Promise*)PromiseType.tp_alloc(&PromiseType, 0) : NULL;
+                if (!pr) { Py_XDECREF(pk); goto item_fail; }
+                PyObject* fn = s ? ng : og;
+                Py_INCREF(fn); pr->func = fn;
+                Py_INCREF(src); pr->src = src;
+                Py_INCREF(bt); pr->blob_type = bt;
+                pr->i = leaf[s];
+                promise = (PyObject*)pr;
+            } else {
+                PyObject* blob = BT->tp_alloc(BT, 0);
+                PyObject* li = PyLong_FromLongLong(leaf[s]);
+                if (!pk || !blob || !li) { Py_XDECREF(pk); Py_XDECREF(blob); Py_XDECREF(li); goto item_fail; }
+                Py_INCREF(src);
+                set_slot(blob, b_src, src);
+                set_slot(blob, b_i, li);
+                Py_INCREF(Py_None);
+                set_slot(blob, b_data, Py_None);
+                promise = partial_make(&pm[s], s ? ng : og, blob);
+                Py_DECREF(blob);
+                if (!promise) { Py_DECREF(pk); goto item_fail; }
+            }
             pkv[s] = pk;
             if (own) {
                 PyObject* kv = KT->tp_alloc(KT, 0);
@@ -296,4 +414,15 @@ static PyMethodDef methods[] = {
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_kd_pystr", NULL, -1, methods};
 
-PyMODINIT_FUNC PyInit__kd_pystr(void) { return PyModule_Create(&module); }
+PyMODINIT_FUNC PyInit__kd_pystr(void) {
+    if (PyType_Ready(&PromiseType) < 0) return NULL;
+    PyObject* m = PyModule_Create(&module);
+    if (!m) return NULL;
+    Py_INCREF(&PromiseType);
+    if (PyModule_AddObject(m, "Promise", (PyObject*)&PromiseType) < 0) {
+        Py_DECREF(&PromiseType);
+        Py_DECREF(m);
+        return NULL;
+    }
+    return m;
+}

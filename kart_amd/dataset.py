@@ -20,6 +20,7 @@ import functools
 import gc
 import operator
 import os
+import time
 
 import msgpack
 import numpy as np
@@ -36,6 +37,15 @@ except ImportError:  # pragma: no cover - the helper is optional host code
     _pystr = None
 
 FEATURE_PATH = "feature/"
+# stage timings of the last dataset_diff when set to a dict (scripts/e2e_repo_bench.py reads them)
+STAGE_TIMES = None
+
+
+def _lap(name, t0):
+    t1 = time.perf_counter()
+    if STAGE_TIMES is not None:
+        STAGE_TIMES[name] = STAGE_TIMES.get(name, 0.0) + (t1 - t0)
+    return t1
 GPU_SORT_MIN = 1 << 20  # sides at least this long are sorted on the GPU when an engine is at hand
 
 
@@ -293,10 +303,13 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
     if present is None:
         return
     S = structs()
+    t = time.perf_counter()
     empty = packing.empty_side(present.encoding)
     A = base.pack(engine) if base is not None else empty
     B = target.pack(engine) if target is not None else empty
+    t = _lap("pack", t)
     res = engine.diff2(A, B)
+    t = _lap("classify2", t)
     old_v, new_v = (target, base) if reverse else (base, target)
     d = res.delta
     if reverse:
@@ -311,6 +324,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
     old_leaf[ia] = A.order[a_idx[ia]]
     new_leaf[ib] = B.order[b_idx[ib]]
     old_pks, new_pks = _pk_column(old_v, a_idx, ia, n), _pk_column(new_v, b_idx, ib, n)
+    t = _lap("pks", t)
     match_all = feature_filter is None or getattr(feature_filter, "match_all", False)
     # this module's own Delta / KeyValue: built field by field (the constructor's argument
     # normalisation is most of a delta's host cost); Kart's classes through their constructor
@@ -320,10 +334,13 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
     if match_all and _pystr is not None:
         # the whole delta list built in C (kart_amd/csrc/kd_pystr.c build_deltas): the same lazy
         # blobs, partial promises, KeyValue halves and Delta objects the loop below builds
+        # (the promises are _kd_pystr.Promise: partial(get_feature_from_blob, LazyBlob(version, leaf))
+        # with the blob made on first use — one object per half instead of blob + partial + args)
         keys, dl, upd_rows, upd_deltas, upd_keys = _pystr.build_deltas(
-            S.Delta, _deltas.KeyValue, LazyBlob, functools.partial, old_get, new_get, old_v, new_v,
+            S.Delta, _deltas.KeyValue, LazyBlob, _pystr.Promise, old_get, new_get, old_v, new_v,
             old_leaf, new_leaf, old_pks, new_pks, own)
         n_total = len(dl)
+        t = _lap("build_deltas", t)
         if _collect is not None:
             _collect[0].extend(keys)
             _collect[1].extend(dl)
@@ -393,9 +410,11 @@ def _pk_column(version, idx, present, n):
 def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
     """RichBaseDataset.diff (kart/rich_base_dataset.py:170-181): {"meta": dict diff, "feature": DeltaDiff}"""
     S = structs()
+    t = time.perf_counter()
     out = S.DatasetDiff()
     old, new = (target, base) if reverse else (base, target)
     out["meta"] = S.DeltaDiff.diff_dicts(old.meta_items() if old else {}, new.meta_items() if new else {})
+    t = _lap("meta", t)
     ffilter = None
     if ds_filter is not None and not getattr(ds_filter, "match_all", False):
         # a filter without a "feature" entry matches no feature (the reference falls back to an empty
@@ -408,8 +427,10 @@ def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
             for _ in diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch,
                                   _collect=(keys, deltas)):
                 pass
+            t = time.perf_counter()
             fd = S.DeltaDiff()
             fd.data.update(zip(keys, deltas))
+            _lap("dict", t)
         else:
             fd = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch))
     fd._kd_updates = batch

@@ -210,8 +210,11 @@ def main():
             stages["pack_parse_s"] = pa.timing["parse_s"] + pb.timing["parse_s"]
             stages["pack_sort_s"] = pa.timing["sort_s"] + pb.timing["sort_s"]
             stages["sort_on"] = pa.timing["sort_on"]
+            D.STAGE_TIMES = {}
             t, ds = timed(lambda: D.get_dataset_diff(eng, old, new))
             stages["diff_s"] = t
+            stages["diff_parts_s"] = {k: round(v, 4) for k, v in D.STAGE_TIMES.items()}
+            D.STAGE_TIMES = None
             fd = ds["feature"]
             fds = {}
             t, nu = timed(lambda: D.field_diff(eng, fd, old, new, stats=fds))

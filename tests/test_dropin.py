@@ -436,3 +436,41 @@ def test_native_delta_builder_kart_structs_path(monkeypatch):
         P.build_deltas(DL.Delta, DL.KeyValue, D.LazyBlob, functools.partial, None, None, ov, nv,
                        np.array([-1], np.int64), np.array([-1], np.int64), np.zeros(1, np.int64),
                        np.zeros(1, np.int64), True)
+
+
+def test_promise_acts_as_partial():
+    """_kd_pystr.Promise: partial(func, LazyBlob(src, i)) with the blob made on first use — called
+    once per value access, .args[0] the same blob object every time, .func / .keywords as a partial,
+    extra call arguments passed after the blob"""
+    import functools
+
+    from kart_amd import _kd_pystr as P
+    from kart_amd import deltas as DL
+
+    made = []
+
+    class Blob(D.LazyBlob):
+        __slots__ = ()
+
+        def __init__(self, src, i):
+            made.append(i)
+            super().__init__(src, i)
+
+    class V:
+        def get(self, blob, *extra, **kw):
+            return ("feat", blob._i, extra, kw)
+
+    v = V()
+    _, deltas, *_ = P.build_deltas(DL.Delta, DL.KeyValue, Blob, P.Promise, v.get, v.get, v, v,
+                                   np.array([7, -1], np.int64), np.array([9, 4], np.int64),
+                                   np.array([1, 0], np.int64), np.array([1, 2], np.int64), True)
+    assert made == []  # nothing materialised by the diff
+    pr = deltas[0].old.value
+    assert pr() == ("feat", 7, (), {}) and made == [7]
+    assert pr.args[0] is pr.args[0] and pr.args[0]._i == 7 and made == [7]
+    assert pr.func == v.get and pr.keywords == {}
+    assert pr(1, k=2) == ("feat", 7, (1,), {"k": 2})
+    assert repr(pr).startswith("functools.partial(")
+    ref = functools.partial(v.get, Blob(v, 9))
+    assert deltas[0].new.value() == ref() and deltas[1].new.value.args[0]._i == 4
+    assert deltas[0].old_value == ("feat", 7, (), {})  # KeyValue.get_lazy_value caches
