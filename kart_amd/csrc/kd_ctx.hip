@@ -185,6 +185,10 @@ int kd_abi_version(void) { return KD_ABI_VERSION; }
 
 const char* kd_last_error(void) { return kd::g_err; }
 
+// one empty launch at context creation: the library's code object is loaded then, not inside the
+// first diff a process runs
+__global__ void k_load_probe() {}
+
 int kd_init(int device_ordinal, kd_ctx** out) {
     KD_CHECK(out != nullptr, "kd_init: out is NULL");
     int n = 0;
@@ -203,6 +207,13 @@ int kd_init(int device_ordinal, kd_ctx** out) {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) == hipSuccess && cu > 0)
         c->n_cu = cu;
+    hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        set_error("kd_init: %s", hipGetErrorString(e));
+        return KD_EHIP;
+    }
     *out = c;
     return KD_OK;
 }

@@ -250,12 +250,19 @@ static PyTypeObject PromiseType = {
  * halves are (pk, promise) tuples passed to delta_type(old, new).  blob_type is kart_amd.dataset's
  * LazyBlob (slots _src, _i, _data).
  * Returns (keys, deltas, upd_rows, upd_deltas, upd_keys): the key of each delta (old pk, else new pk)
- * and the delta, and the updates' row numbers, deltas and keys. */
+ * and the delta, and the updates' row numbers, deltas and keys.  out (optional dict): each delta is
+ * also stored there at its key (a DeltaDiff's dict filled in place). */
 static PyObject* build_deltas(PyObject* self, PyObject* args) {
-    PyObject *dt, *kvt, *bt, *pt, *og, *ng, *os_, *ns, *ol_o, *nl_o, *op_o, *np_o;
+    PyObject *dt, *kvt, *bt, *pt, *og, *ng, *os_, *ns, *ol_o, *nl_o, *op_o, *np_o, *out = Py_None;
     int own;
-    if (!PyArg_ParseTuple(args, "OOOOOOOOOOOOp", &dt, &kvt, &bt, &pt, &og, &ng, &os_, &ns, &ol_o, &nl_o, &op_o, &np_o, &own))
+    if (!PyArg_ParseTuple(args, "OOOOOOOOOOOOp|O", &dt, &kvt, &bt, &pt, &og, &ng, &os_, &ns, &ol_o, &nl_o, &op_o, &np_o, &own,
+                          &out))
         return NULL;
+    if (out != Py_None && !PyDict_Check(out)) {
+        PyErr_SetString(PyExc_TypeError, "build_deltas: out must be a dict");
+        return NULL;
+    }
+    PyObject* const out_dict = out != Py_None ? out : NULL;
     Py_buffer ol = {0}, nl = {0}, opb = {0}, npb = {0};
     PyObject *keys = NULL, *dl = NULL, *urows = NULL, *udl = NULL, *ukeys = NULL, *ret = NULL;
     PyObject *t_ins = NULL, *t_upd = NULL, *t_del = NULL;
@@ -380,6 +387,10 @@ static PyObject* build_deltas(PyObject* self, PyObject* args) {
         Py_XDECREF(half[0]);
         Py_XDECREF(half[1]);
         PyObject* key = pkv[0] ? pkv[0] : pkv[1];
+        if (out_dict && PyDict_SetItem(out_dict, key, d) < 0) {
+            Py_DECREF(d); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]);
+            goto fail;
+        }
         Py_INCREF(key);
         PyList_SET_ITEM(keys, i, key);
         Py_INCREF(d);

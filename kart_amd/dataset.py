@@ -297,7 +297,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
 
     base / target: DatasetVersion or None (a missing dataset diffs against the empty tree).
     updates: an UpdateBatch that receives the yielded update deltas (set once the generator is
-    exhausted).  _collect=(keys, deltas): the deltas are appended there with their keys instead of
+    exhausted).  _collect=dict: the deltas are stored there at their keys instead of
     yielded (dataset_diff's bulk path)."""
     present = base if base is not None else target
     if present is None:
@@ -338,13 +338,10 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
         # with the blob made on first use — one object per half instead of blob + partial + args)
         keys, dl, upd_rows, upd_deltas, upd_keys = _pystr.build_deltas(
             S.Delta, _deltas.KeyValue, LazyBlob, _pystr.Promise, old_get, new_get, old_v, new_v,
-            old_leaf, new_leaf, old_pks, new_pks, own)
+            old_leaf, new_leaf, old_pks, new_pks, own, _collect)
         n_total = len(dl)
         t = _lap("build_deltas", t)
-        if _collect is not None:
-            _collect[0].extend(keys)
-            _collect[1].extend(dl)
-        else:
+        if _collect is None:
             yield from dl
     else:
         if isinstance(old_pks, np.ndarray):
@@ -352,7 +349,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
         if isinstance(new_pks, np.ndarray):
             new_pks = new_pks.tolist()
         upd_rows, upd_deltas, upd_keys, n_total = [], [], [], 0
-        keys_append, deltas_append = (_collect[0].append, _collect[1].append) if _collect is not None else (None, None)
+        store = _collect.__setitem__ if _collect is not None else None
         Delta, KeyValue, new_obj, partial = _deltas.Delta, _deltas.KeyValue, object.__new__, functools.partial
         olist, nlist = old_leaf.tolist(), new_leaf.tolist()
         for i in range(n):
@@ -380,8 +377,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
             if _collect is None:
                 yield delta
             else:
-                keys_append(opk if ob is not None else npk)
-                deltas_append(delta)
+                store(opk if ob is not None else npk, delta)
     if updates is not None:
         rows = np.asarray(upd_rows, np.int64)
         updates.old_v, updates.new_v = old_v, new_v
@@ -422,15 +418,10 @@ def dataset_diff(engine, base, target, ds_filter=None, reverse=False):
         ffilter = ds_filter.get("feature", _NoKeys())
     batch = UpdateBatch()
     with _gc_paused():
-        if S.DeltaDiff is _deltas.DeltaDiff:  # this module's own DeltaDiff: one dict update from the lists
-            keys, deltas = [], []
-            for _ in diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch,
-                                  _collect=(keys, deltas)):
-                pass
-            t = time.perf_counter()
+        if S.DeltaDiff is _deltas.DeltaDiff:  # this module's own DeltaDiff: its dict filled in place
             fd = S.DeltaDiff()
-            fd.data.update(zip(keys, deltas))
-            _lap("dict", t)
+            for _ in diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch, _collect=fd.data):
+                pass
         else:
             fd = S.DeltaDiff(diff_feature(engine, base, target, ffilter, reverse=reverse, updates=batch))
     fd._kd_updates = batch

@@ -193,7 +193,9 @@ def main():
     n_git = out.count(b"\n")
     res = {"n": a.n, "changed_paths": n_git, "git_diff_tree_s": round(t_git, 4),
            "reference_path_s_estimate": round((a.n + a.n // 100) / REFERENCE_RATE, 2)}
+    t_eng = time.perf_counter()
     with Engine(0) as eng:
+        res["engine_init_s"] = round(time.perf_counter() - t_eng, 4)  # context + the library's code object
         # the first run of a process also loads the GPU code objects and sizes the workspaces:
         # reported as "cold", the repeat as "warm"
         for label, pruned in (("pruned walk (cold)", True), ("pruned walk (warm)", True), ("full walk", False)):
