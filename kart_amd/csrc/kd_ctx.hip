@@ -18,6 +18,8 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
+constexpr size_t SLAB_BYTES = (size_t)64 << 20, SLAB_PIECE_MAX = (size_t)8 << 20;
+
 int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out) {
     DevBuf& b = ctx->bufs[slot];
     if (bytes == 0) bytes = 16;
@@ -25,13 +27,29 @@ int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out) {
         if (b.p) {
             hipError_t e = hipStreamSynchronize(ctx->stream);
             if (e != hipSuccess) { set_error("sync before realloc: %s", hipGetErrorString(e)); return KD_EHIP; }
-            KD_HIP(hipFree(b.p));
+            if (!b.slab) KD_HIP(hipFree(b.p));  // (a slab piece is abandoned)
             b.p = nullptr;
             b.bytes = 0;
+            b.slab = false;
         }
-        size_t want = bytes + bytes / 8;  // headroom
-        KD_HIP(hipMalloc(&b.p, want));
-        b.bytes = want;
+        const size_t want = (bytes + bytes / 8 + 255) & ~(size_t)255;  // headroom, 256-B aligned
+        if (want <= SLAB_PIECE_MAX) {
+            if (!ctx->slab) {
+                void* s = nullptr;
+                if (hipMalloc(&s, SLAB_BYTES) == hipSuccess) ctx->slab = (char*)s;
+                ctx->slab_used = 0;
+            }
+            if (ctx->slab && ctx->slab_used + want <= SLAB_BYTES) {
+                b.p = ctx->slab + ctx->slab_used;
+                ctx->slab_used += want;
+                b.bytes = want;
+                b.slab = true;
+            }
+        }
+        if (!b.p) {
+            KD_HIP(hipMalloc(&b.p, want));
+            b.bytes = want;
+        }
     }
     *out = b.p;
     return KD_OK;
@@ -207,8 +225,14 @@ int kd_init(int device_ordinal, kd_ctx** out) {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) == hipSuccess && cu > 0)
         c->n_cu = cu;
+    {   // the workspace slab too (ensure() carves it; a failure here is retried there)
+        void* s = nullptr;
+        if (hipMalloc(&s, SLAB_BYTES) == hipSuccess) c->slab = (char*)s;
+        c->slab_used = 0;
+    }
     hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        if (c->slab) (void)hipFree(c->slab);
         (void)hipStreamDestroy(c->own_stream);
         delete c;
         set_error("kd_init: %s", hipGetErrorString(e));
@@ -226,7 +250,8 @@ int kd_fini(kd_ctx* ctx) {
     comm_release(ctx);
     gather_release(ctx);
     for (auto& kv : ctx->bufs)
-        if (kv.second.p) (void)hipFree(kv.second.p);
+        if (kv.second.p && !kv.second.slab) (void)hipFree(kv.second.p);
+    if (ctx->slab) (void)hipFree(ctx->slab);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;

@@ -46,6 +46,7 @@ void set_error(const char* fmt, ...);
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool slab = false;  // carved from the context's slab (never freed on its own)
 };
 
 struct ProfStat {
@@ -89,6 +90,10 @@ struct kd_ctx {
     uint64_t gather_send_cap = 0;  // records the last _begin's d_delta holds (base.n + target.n + 1)
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
     uint32_t rs_epoch = 0;  // kd_sort: epoch of the last pass's look-back words (kd_sort.hip)
+    // small workspaces come from one slab (one hipMalloc instead of one per slot on a process's
+    // first calls); grown slots take a fresh piece, the slab is freed with the context
+    char* slab = nullptr;
+    size_t slab_used = 0;
 };
 
 namespace kd {
