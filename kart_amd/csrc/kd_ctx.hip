@@ -231,6 +231,11 @@ int kd_init(int device_ordinal, kd_ctx** out) {
         c->slab_used = 0;
     }
     hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
+    if (c->slab) {  // and one pageable round trip: the runtime sets up its staging buffers now
+        static thread_local char page[4096];
+        (void)hipMemcpyAsync(c->slab, page, sizeof page, hipMemcpyHostToDevice, c->stream);
+        (void)hipMemcpyAsync(page, c->slab, sizeof page, hipMemcpyDeviceToHost, c->stream);
+    }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         if (c->slab) (void)hipFree(c->slab);
         (void)hipStreamDestroy(c->own_stream);
