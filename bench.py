@@ -81,19 +81,24 @@ def parse():
     ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
     ap.add_argument("--no-delta-order", action="store_true",
                     help="c5: skip timing the heads kernel on the drop-in's delta-order layout")
-    ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/traffic_<wl>.json)")
+    ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/r04/traffic_<wl>.json, else profiles/traffic_<wl>.json)")
     ap.add_argument("--no-heads-path", action="store_true", help="c5env: skip the indexer's heads-path timing")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--time-all", action="store_true",
                     help="HIP events around every kernel of a step (default: only the dominant kernel, "
                          "so the events do not inflate the step time)")
+    ap.add_argument("--ab", default="",
+                    help="c5 A/B: comma-separated VAR=value library switches (read per call), each timed after the "
+                         "main run in the same process on the same layer")
     a = ap.parse_args()
     if not a.n:
         a.n = {"c2": 10_000_000, "c3": 100_000_000, "c3v": 100_000_000, "c4": 50_000_000, "c5": 100_000_000, "c5env": 20_000_000,
                "c6": 20_000_000}[a.workload]
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
+        a.traffic_json = os.path.join(ROOT, "profiles", "r04", f"traffic_{a.workload}.json")  # this round's PMC passes
+        if not os.path.exists(a.traffic_json):
+            a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
     return a
 
 
@@ -187,13 +192,13 @@ def timed(H, eng, step, steps):
     return H.max(time.perf_counter() - t0)
 
 
-ROCPROF_STATS = {"c3": "profiles/r03/c3_kernel_stats.csv", "c3v": "profiles/r03/c3v_kernel_stats.csv", "c4": "profiles/r03/c4_kernel_stats.csv",
-                 "c5": "profiles/r03/c5_kernel_stats.csv"}
+ROCPROF_STATS = {"c3": "profiles/r04/c3_kernel_stats.csv", "c3v": "profiles/r03/c3v_kernel_stats.csv", "c4": "profiles/r04/c4_kernel_stats.csv",
+                 "c5": "profiles/r04/c5_kernel_stats.csv"}
 
 
 def rocprof_avg_ms(workload, kernel):
     """the kernel's average duration in the committed `rocprofv3 --kernel-trace --stats` summary of
-    this workload (profiles/r03), or None"""
+    this workload (profiles/r04; C3v profiles/r03), or None"""
     path = os.path.join(ROOT, ROCPROF_STATS.get(workload, "-"))
     try:
         import csv
@@ -727,6 +732,33 @@ def run_c5(args, H):
             head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
         alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
     roof = roofline(kern, kname, alg, args.traffic_json, n, "c5" if heads and H.world == 1 else None)
+    ab = None
+    if args.ab:  # library switches read per call (os.environ reaches getenv): same process, same layer
+        ab = {}
+        for spec in args.ab.split(","):
+            var, val = spec.split("=", 1)
+            old_v = os.environ.get(var)
+            os.environ[var] = val
+            for _ in range(max(1, args.warmup)):
+                pipe.step()
+            eng.sync()
+            if not args.no_check:
+                c2, d2, codes2, keep2, enc2, ok2 = pipe.results()
+                assert np.array_equal(codes2, codes) and np.array_equal(keep2, keep) and np.array_equal(enc2, enc) \
+                    and np.array_equal(ok2, enc_ok), f"{spec}: results differ"
+            eng.prof_reset()
+            eng.prof_select([kname])
+            eng.prof_enable(True)
+            el = timed(H, eng, pipe.step, args.steps)
+            eng.prof_enable(False)
+            kk = kernel_times(eng, (kname,))
+            ab[spec] = {"ms_per_step": round(el / args.steps * 1e3, 4),
+                        "kernel_ms": round(kk[kname][1], 5) if kname in kk else None}
+            if old_v is None:
+                del os.environ[var]
+            else:
+                os.environ[var] = old_v
+        log(f"[rank {H.rank}] A/B: {ab}")
     delta_order = None
     if heads and H.world == 1 and not args.no_delta_order and not pipe.delta_order:
         # (--per-entry steps only: the delta-order step already times this layout) the drop-in's layout: the blob reader reads the deltas' blobs after classification, so the
@@ -822,6 +854,8 @@ def run_c5(args, H):
                                f"{host_cores()} threads) that leaves 48 B per blob for the GPU; outside the timed step"}
         out["arena_path"] = arena_path
         out["heads_delta_order"] = delta_order
+    if ab:
+        out["ab"] = ab
     return out
 
 

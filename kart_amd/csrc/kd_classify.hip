@@ -553,10 +553,10 @@ int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t f
     r->delta = (u32*)(r + 1);
     r->upd = r->delta + 2 * nd;
     if (nd) {
-        hipError_t e = hipMemcpyAsync(r->delta, dd, nd * 8, hipMemcpyDeviceToHost, ctx->stream);
-        if (e == hipSuccess && nu) e = hipMemcpyAsync(r->upd, du, nu * 8, hipMemcpyDeviceToHost, ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e != hipSuccess) { std::free(r); set_error("kd_diff2 D2H: %s", hipGetErrorString(e)); return KD_EHIP; }
+        if ((rc = stage_d2h(ctx, r->delta, dd, nd * 8)) || (nu && (rc = stage_d2h(ctx, r->upd, du, nu * 8)))) {
+            std::free(r);
+            return rc;
+        }
     }
     prof_flush(ctx);
     *out = r;
@@ -599,11 +599,10 @@ int kd_merge3(kd_ctx* ctx, const kd_side* anc, const kd_side* ours, const kd_sid
     r->n_clean = hc[0]; r->n_conflict = nc; r->n_mdelta = nm;
     r->conflict = (u32*)(r + 1);
     r->mdelta = r->conflict + 3 * nc;
-    hipError_t e = hipSuccess;
-    if (nc) e = hipMemcpyAsync(r->conflict, oc, nc * 12, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && nm) e = hipMemcpyAsync(r->mdelta, om, nm * 8, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) { std::free(r); set_error("kd_merge3 D2H: %s", hipGetErrorString(e)); return KD_EHIP; }
+    if ((nc && (rc = stage_d2h(ctx, r->conflict, oc, nc * 12))) || (nm && (rc = stage_d2h(ctx, r->mdelta, om, nm * 8)))) {
+        std::free(r);
+        return rc;
+    }
     prof_flush(ctx);
     *out = r;
     return KD_OK;

@@ -2,6 +2,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <algorithm>
 #include <thread>
 
 #include "kd_internal.h"
@@ -72,8 +74,52 @@ int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem
     void* d = nullptr;
     int rc = ensure(ctx, slot, bytes, &d);
     if (rc) return rc;
-    KD_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = stage_h2d(ctx, d, p, bytes))) return rc;
     *dev = d;
+    return KD_OK;
+}
+
+constexpr size_t PIN_CHUNK = (size_t)4 << 20, PIN_MIN = (size_t)64 << 10;
+
+int stage_h2d(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (bytes < PIN_MIN || !ctx->pin[1]) {
+        KD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));  // (pageable: staged by the runtime)
+        return KD_OK;
+    }
+    // chunk i's host copy overlaps chunk i-1's DMA; a chunk buffer is refilled once its DMA is done
+    for (size_t o = 0; o < bytes; o += PIN_CHUNK) {
+        const int j = ctx->pin_next;
+        ctx->pin_next ^= 1;
+        const size_t c = std::min(PIN_CHUNK, bytes - o);
+        KD_HIP(hipEventSynchronize(ctx->pin_ev[j]));
+        std::memcpy(ctx->pin[j], (const char*)src + o, c);
+        KD_HIP(hipMemcpyAsync((char*)dst + o, ctx->pin[j], c, hipMemcpyHostToDevice, ctx->stream));
+        KD_HIP(hipEventRecord(ctx->pin_ev[j], ctx->stream));
+    }
+    return KD_OK;
+}
+
+int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (bytes < PIN_MIN || !ctx->pin[1]) {
+        KD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        KD_HIP(hipStreamSynchronize(ctx->stream));
+        return KD_OK;
+    }
+    // DMA of chunk i+1 is queued before chunk i is copied out of its buffer
+    const size_t n = (bytes + PIN_CHUNK - 1) / PIN_CHUNK;
+    auto issue = [&](size_t i) -> hipError_t {
+        const size_t o = i * PIN_CHUNK, c = std::min(PIN_CHUNK, bytes - o);
+        hipError_t e = hipMemcpyAsync(ctx->pin[i & 1], (const char*)src + o, c, hipMemcpyDeviceToHost, ctx->stream);
+        return e == hipSuccess ? hipEventRecord(ctx->pin_ev[i & 1], ctx->stream) : e;
+    };
+    KD_HIP(issue(0));
+    for (size_t i = 0; i < n; i++) {
+        if (i + 1 < n) KD_HIP(issue(i + 1));
+        KD_HIP(hipEventSynchronize(ctx->pin_ev[i & 1]));
+        const size_t o = i * PIN_CHUNK;
+        std::memcpy((char*)dst + o, ctx->pin[i & 1], std::min(PIN_CHUNK, bytes - o));
+    }
+    ctx->pin_next = 0;
     return KD_OK;
 }
 
@@ -231,13 +277,21 @@ int kd_init(int device_ordinal, kd_ctx** out) {
         c->slab_used = 0;
     }
     hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
-    if (c->slab) {  // and one pageable round trip: the runtime sets up its staging buffers now
-        static thread_local char page[4096];
-        (void)hipMemcpyAsync(c->slab, page, sizeof page, hipMemcpyHostToDevice, c->stream);
-        (void)hipMemcpyAsync(page, c->slab, sizeof page, hipMemcpyDeviceToHost, c->stream);
+    for (int j = 0; j < 2; j++) {  // the pinned staging chunks (without them: pageable copies)
+        void* h = nullptr;
+        if (hipHostMalloc(&h, PIN_CHUNK, hipHostMallocDefault) != hipSuccess) break;
+        if (hipEventCreateWithFlags(&c->pin_ev[j], hipEventDisableTiming) != hipSuccess) {
+            (void)hipHostFree(h);
+            break;
+        }
+        c->pin[j] = (char*)h;
     }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         if (c->slab) (void)hipFree(c->slab);
+        for (int j = 0; j < 2; j++) {
+            if (c->pin[j]) (void)hipHostFree(c->pin[j]);
+            if (c->pin_ev[j]) (void)hipEventDestroy(c->pin_ev[j]);
+        }
         (void)hipStreamDestroy(c->own_stream);
         delete c;
         set_error("kd_init: %s", hipGetErrorString(e));
@@ -257,6 +311,10 @@ int kd_fini(kd_ctx* ctx) {
     for (auto& kv : ctx->bufs)
         if (kv.second.p && !kv.second.slab) (void)hipFree(kv.second.p);
     if (ctx->slab) (void)hipFree(ctx->slab);
+    for (int j = 0; j < 2; j++) {
+        if (ctx->pin[j]) (void)hipHostFree(ctx->pin[j]);
+        if (ctx->pin_ev[j]) (void)hipEventDestroy(ctx->pin_ev[j]);
+    }
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;

@@ -1414,9 +1414,7 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     });
     if (rc) return rc;
     if (out_mem == KD_MEM_HOST) {
-        KD_HIP(hipMemcpyAsync(masks, d_masks, n_upd * W * 8, hipMemcpyDeviceToHost, ctx->stream));
-        KD_HIP(hipMemcpyAsync(status, d_status, n_upd, hipMemcpyDeviceToHost, ctx->stream));
-        KD_HIP(hipStreamSynchronize(ctx->stream));
+        if ((rc = stage_d2h(ctx, masks, d_masks, n_upd * W * 8)) || (rc = stage_d2h(ctx, status, d_status, n_upd))) return rc;
         prof_flush(ctx);
     }
     return KD_OK;

@@ -25,6 +25,7 @@
 // 112 bytes from each blob start (7 dwordx4, realigned with v_alignbyte) and decodes the common
 // shape — [legend str8(40), fixarray|array16 values, geometry first as ext8/16/32 'G'] — from
 // registers; anything else takes the byte-wise decoder on global memory.
+#include <cstdlib>
 #include <type_traits>
 
 #include "kd_geom.h"
@@ -32,7 +33,10 @@
 namespace kd {
 
 constexpr int GF_NT = 256;
-constexpr int GF_ROUNDS = 16;
+#ifndef KD_GF_ROUNDS
+#define KD_GF_ROUNDS 16
+#endif
+constexpr int GF_ROUNDS = KD_GF_ROUNDS;  // (probe builds may change it)
 constexpr int GF_TILE = GF_NT * GF_ROUNDS;
 constexpr int GF_MAXLEG = 64;  // legends per side held in LDS
 
@@ -390,6 +394,8 @@ struct GfHeadArgs {
                           // not indexed like the arenas (delta-order heads over per-entry arenas)
     u32* fb_list;         // (optional) deltas whose head needs its blob are listed here and left to
     u32* fb_count;        // k_gf_fb, so the streaming pass never waits on a byte-wise blob decode
+    int dense;            // heads indexed by delta (slot d holds delta d's head; the pairs say only
+                          // which sides are present): k_gf_dense, no pair -> head dependency
 };
 
 struct HeadLd {
@@ -485,11 +491,18 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
         bool deferred = false;
         if (d < n) {
             GHit h;
+#ifdef KD_GF_PROBE_NODECODE  // profiling variant: the loads and stores alone
+            const u32 x = L0.v0.x ^ L0.v1.y ^ L0.v2.w ^ L1.v0.z ^ L1.v1.w ^ L1.v2.x;
+            const int co = (int)(x & 3), cn = (int)((x >> 2) & 3);
+            h.r = -1;
+            (void)g;
+#else
             const bool defer = g.fb_list != nullptr;
             deferred = !decode_head(a, g, 0, pr.x, L0, h, d, defer);
             const int co = h.code;
             deferred |= !decode_head(a, g, 1, pr.y, L1, h, d, defer);
             const int cn = h.code;
+#endif
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
             if (a.enc && !deferred && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
@@ -535,6 +548,127 @@ __global__ __launch_bounds__(GF_NT) void k_gf_heads(GfArgs a, GfHeadArgs g) {
         a.tile_cnt[tile] = t;
     }
     __syncthreads();  // s_wc is rewritten by the next tile
+    }
+}
+
+// k_gf_heads for dense heads (kd_geom_filter_deltas: the device gather put delta d's heads in
+// slot d).  Head addresses follow from the delta index, so nothing waits on the pairs before its
+// loads are issued.  Each wave owns 64-delta chunks (grid-stride over chunks, so the persistent
+// grid ends within one chunk of balance) and keeps PF chunks of loads in flight beyond the one it
+// decodes.  TR: a chunk's 2 x 3 KB of heads are read as lane-contiguous 16-B pieces (each load
+// instruction one 1-KB run) and transposed through the wave's LDS slice; else three 16-B loads
+// per lane and side at the 48-B head stride.  Kept counts go to the chunk's tile by one atomic per
+// wave (tile_cnt zeroed before the launch).
+struct DenseLd {
+    u32x4 h[6];  // TR: pieces k of side s at [3s + k]; else side s head dwords at [3s + k]
+    uint2 pr;
+};
+
+template <bool TR>
+__device__ __forceinline__ DenseLd dense_load(const GfArgs& a, const GfHeadArgs& g, u64 c, u64 nchunk, u64 n, int lane) {
+    typedef const __attribute__((address_space(1))) u32x4* gx4;
+    DenseLd L;
+    const u64 cc = c < nchunk ? c : (nchunk ? nchunk - 1 : 0);  // (past the end: a clamped, unused load)
+    const u64 d = cc * 64 + lane;
+    // (the slots are allocated in whole 64-delta chunks: every chunk below nchunk is readable)
+    const u64 o = TR ? cc * 3072 + (u64)lane * 16 : d * 48;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const u64 base = (u64)g.head[s] + o;
+#pragma unroll
+        for (int k = 0; k < 3; k++) L.h[3 * s + k] = *(gx4)(base + (TR ? 1024 : 16) * k);
+    }
+    const u64 dp = n ? (d < n ? d : n - 1) : 0;
+    const uint2 v = *(n ? (const uint2*)a.pairs + dp : (const uint2*)g.zeros);
+    L.pr = d < n ? v : make_uint2(KD_NONE, KD_NONE);
+    return L;
+}
+
+template <int PF, bool TR>
+__global__ __launch_bounds__(GF_NT) __attribute__((amdgpu_waves_per_eu(PF == 1 && !TR ? 4 : 3))) void k_gf_dense(GfArgs a, GfHeadArgs g) {
+    static_assert(PF == 1 || PF == 2, "prefetch depth");
+    __shared__ u32 s_encw[GF_NT * 4];  // 16 B per lane: nb <= 16 index-envelope bytes
+    __shared__ u32x4 s_tr[TR ? (GF_NT / 64) * 6 * 64 : 1];  // 6 KB per wave
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 n = a.d_n ? *a.d_n : a.cap;
+    const u64 nchunk = (n + 63) / 64;
+    const int nb = a.bits / 2;
+    const double vmax = (double)((1ull << a.bits) - 1);
+    u8* const wenc = (u8*)(s_encw + 64 * 4 * wid);
+    u32x4* const wtr = s_tr + (TR ? wid * 6 * 64 : 0);
+    const u64 wstride = (u64)gridDim.x * (GF_NT / 64);
+    u64 c = (u64)blockIdx.x * (GF_NT / 64) + wid;
+    DenseLd A = dense_load<TR>(a, g, c, nchunk, n, lane);
+    DenseLd B;
+    if (PF == 2) B = dense_load<TR>(a, g, c + wstride, nchunk, n, lane);
+    for (; c < nchunk; c += wstride) {  // wave-uniform
+        // the load PF chunks ahead first, so this chunk's wait leaves it in flight
+        DenseLd Nx = dense_load<TR>(a, g, c + PF * wstride, nchunk, n, lane);
+        const u64 d = c * 64 + lane;
+        HeadLd L0, L1;
+        if (TR) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) wtr[k * 64 + lane] = A.h[k];  // piece (s, k) = index (3s + k) * 64 + lane
+            __builtin_amdgcn_wave_barrier();
+            // side s, head of this lane: bytes [lane * 48, +48) of the side's 3 KB = pieces lane*3 + j
+            L0.v0 = wtr[lane * 3 + 0]; L0.v1 = wtr[lane * 3 + 1]; L0.v2 = wtr[lane * 3 + 2];
+            L1.v0 = wtr[192 + lane * 3 + 0]; L1.v1 = wtr[192 + lane * 3 + 1]; L1.v2 = wtr[192 + lane * 3 + 2];
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            L0.v0 = A.h[0]; L0.v1 = A.h[1]; L0.v2 = A.h[2];
+            L1.v0 = A.h[3]; L1.v1 = A.h[4]; L1.v2 = A.h[5];
+        }
+        const uint2 pr = A.pr;
+        bool keep = false, deferred = false;
+        u8 ok = 0;
+        if (a.enc)
+            for (int k = 0; k < nb; k++) wenc[lane * nb + k] = 0;
+        if (d < n) {
+            GHit h;
+            const bool defer = g.fb_list != nullptr;
+            deferred = !decode_head(a, g, 0, pr.x, L0, h, d, defer);
+            const int co = h.code;
+            deferred |= !decode_head(a, g, 1, pr.y, L1, h, d, defer);
+            const int cn = h.code;
+            keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
+            *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
+            if (a.enc && !deferred && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
+                ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { wenc[lane * nb + k] = v; });
+            if (a.enc) a.enc_ok[d] = ok;
+        }
+        const u32 kept = (u32)__popcll(__ballot(keep));
+        if (lane == 0 && kept) atomicAdd(a.tile_cnt + (c * 64) / GF_TILE, kept);
+        {
+            const u64 bd = __ballot(deferred);
+            if (bd) {
+                u32 base = 0;
+                if (lane == 0) base = atomicAdd(g.fb_count, (u32)__popcll(bd));
+                base = __shfl(base, 0);
+                if (deferred)
+                    g.fb_list[base + __builtin_amdgcn_mbcnt_hi((u32)(bd >> 32), __builtin_amdgcn_mbcnt_lo((u32)bd, 0))] = (u32)d;
+            }
+        }
+        if (a.enc) {
+            __builtin_amdgcn_wave_barrier();
+            const u64 w0 = c * 64;
+            const u32 cnt = (u32)(n - w0 < 64 ? n - w0 : 64);
+            u8* dst = a.enc + w0 * nb;
+            const u32 bytes = cnt * nb;
+            if ((((u64)dst) & 3) == 0) {
+                const u32 nw = bytes >> 2;
+                for (u32 k = lane; k < nw; k += 64) ((u32*)dst)[k] = ((const u32*)wenc)[k];
+                for (u32 k = 4 * nw + lane; k < bytes; k += 64) dst[k] = wenc[k];
+            } else {
+                for (u32 k = lane; k < bytes; k += 64) dst[k] = wenc[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (PF == 2) {
+            A = B;
+            B = Nx;
+        } else {
+            A = Nx;
+        }
     }
 }
 
@@ -705,14 +839,44 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
         }
     }
     if (tiles) {
-        if (g) {
+        if (g && gh.dense) {
+            // KD_GFD (A/B): prefetch depth 1 / 2, 't' = transposed loads; default "1t"
+            const char* v = std::getenv("KD_GFD");
+            const int pf = v && v[0] == '2' ? 2 : 1;
+            const bool tr = !(v && v[0] && v[1] == 's');
+            KD_HIP(hipMemsetAsync(t_cnt, 0, tiles * 4, ctx->stream));
+            const void* fn = pf == 2 ? (tr ? (const void*)k_gf_dense<2, true> : (const void*)k_gf_dense<2, false>)
+                                     : (tr ? (const void*)k_gf_dense<1, true> : (const void*)k_gf_dense<1, false>);
+            static int occ_dense[4] = {0, 0, 0, 0};
+            int& occ = occ_dense[(pf - 1) * 2 + (tr ? 1 : 0)];
+            if (occ <= 0) {
+                int nb_ = 0;
+                KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_, fn, GF_NT, 0));
+                occ = nb_ > 0 ? nb_ : 1;
+            }
+            const u64 nchunk = (n + 63) / 64;
+            const u64 grid = std::max<u64>(1, std::min<u64>((nchunk + 3) / 4, (u64)ctx->n_cu * (u64)occ));
+            if ((rc = launch(ctx, "k_gf_heads", [&] {
+                     if (pf == 2 && tr) hipLaunchKernelGGL((k_gf_dense<2, true>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
+                     else if (pf == 2) hipLaunchKernelGGL((k_gf_dense<2, false>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
+                     else if (tr) hipLaunchKernelGGL((k_gf_dense<1, true>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
+                     else hipLaunchKernelGGL((k_gf_dense<1, false>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
+                 })))
+                return rc;
+            if (gh.fb_list && (rc = launch(ctx, "k_gf_fb", [&] {
+                                   const unsigned fgrid = (unsigned)std::max<u64>(1, std::min<u64>((n + 255) / 256, (u64)ctx->n_cu * 2));
+                                   hipLaunchKernelGGL(k_gf_fb, dim3(fgrid), dim3(256), 0, ctx->stream, a, gh);
+                               })))
+                return rc;
+        } else if (g) {
             static int occ_heads = 0;  // resident k_gf_heads workgroups per CU
             if (occ_heads <= 0) {
                 int nb_ = 0;
                 KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_, (const void*)k_gf_heads, GF_NT, 0));
                 occ_heads = nb_ > 0 ? nb_ : 1;
             }
-            const u64 hgrid = std::min<u64>(tiles, (u64)ctx->n_cu * (u64)occ_heads);
+            const char* np_ = std::getenv("KD_GF_NOPERSIST");  // (A/B: one block per tile)
+            const u64 hgrid = np_ && np_[0] == '1' ? tiles : std::min<u64>(tiles, (u64)ctx->n_cu * (u64)occ_heads);
             if ((rc = launch(ctx, "k_gf_heads", [&] {
                      hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)hgrid), dim3(GF_NT), 0, ctx->stream, a, gh);
                  })))
@@ -887,8 +1051,9 @@ extern "C" int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old,
     static_assert(sizeof(kd_geom_head) == 48, "kd_geom_head is 48 bytes");
     int rc;
     void *go, *gn, *gp, *dz;
-    if ((rc = ensure(ctx, "gd.ho", (cap + 1) * sizeof(kd_geom_head), &go))) return rc;
-    if ((rc = ensure(ctx, "gd.hn", (cap + 1) * sizeof(kd_geom_head), &gn))) return rc;
+    const u64 slots = (cap + 63) / 64 * 64 + 1;  // whole 64-delta chunks (k_gf_dense's loads)
+    if ((rc = ensure(ctx, "gd.ho", slots * sizeof(kd_geom_head), &go))) return rc;
+    if ((rc = ensure(ctx, "gd.hn", slots * sizeof(kd_geom_head), &gn))) return rc;
     if ((rc = ensure(ctx, "gd.pairs", (cap + 1) * 8, &gp))) return rc;
     if ((rc = device_zeros(ctx, &dz))) return rc;
     if (cap) {
@@ -907,6 +1072,7 @@ extern "C" int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old,
     g.nhead[0] = g.nhead[1] = cap;
     g.zeros = (const u8*)dz;
     g.bpairs = (const uint2*)pairs;
+    g.dense = std::getenv("KD_GF_DENSE") && std::getenv("KD_GF_DENSE")[0] == '0' ? 0 : 1;  // (A/B: 0 = k_gf_heads)
     if (old_blobs) {
         const kd_blobs* bl[2] = {old_blobs, new_blobs};
         for (int s = 0; s < 2; s++) {

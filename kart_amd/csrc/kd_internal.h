@@ -94,6 +94,12 @@ struct kd_ctx {
     // first calls); grown slots take a fresh piece, the slab is freed with the context
     char* slab = nullptr;
     size_t slab_used = 0;
+    // host inputs / results cross PCIe through two pinned chunks (stage_h2d / stage_d2h): a
+    // pageable hipMemcpy pins the caller's pages on first use, which a one-shot process pays for
+    // every buffer it hands over
+    char* pin[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    int pin_next = 0;
 };
 
 namespace kd {
@@ -102,6 +108,10 @@ namespace kd {
 // kd_reserve() has sized it.
 void gather_release(kd_ctx* ctx);  // kd_comm.hip: kd_diff2_gather_begin/_end resources
 int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out);
+// host -> device on ctx->stream through the pinned chunks (returns when src may be reused);
+// device -> host, blocking (the stream is synchronised)
+int stage_h2d(kd_ctx* ctx, void* dst, const void* src, size_t bytes);
+int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 // 256 zero bytes of device memory: what empty inputs point at, and the target of loads issued by
 // masked-off lanes in branch-free load batches (never a host address)

@@ -306,6 +306,37 @@ def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n):
     assert (flags == 0x01).any() and (flags == 0x11).any() and (flags == 0x05).any()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1000, 3_000_000])
+def test_gpu_filter_dense_variants_agree(engine, n, monkeypatch):
+    """k_gf_dense (delta-order heads, kd_geom_filter_deltas): every prefetch depth / load form and
+    the pair-indexed k_gf_heads give the oracle's codes, kept list and index envelopes"""
+    import types
+
+    from kart_amd import synth
+    from kart_amd.device import FilterPipeline
+
+    L = synth.c5_layer(n, seed=21)
+    ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
+    gc = S.GeomCols(ver, ver, "geom", "geom")
+    pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, gc, synth.C5_FILTER, False, 20,
+                          heads=True, delta_order=True)
+    cols = {h: 0 for h in L.legends}
+    (od, oo), (nd, no) = L.base_blobs, L.target_blobs
+    ref = None
+    for var, val in (("KD_GFD", "1s"), ("KD_GFD", "1t"), ("KD_GFD", "2s"), ("KD_GFD", "2t"), ("KD_GF_DENSE", "0")):
+        monkeypatch.setenv(var, val)
+        pipe.step()
+        counts, delta, codes, keep, enc, ok = pipe.results()
+        monkeypatch.delenv(var)
+        if ref is None:
+            oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta, cols, cols, synth.C5_FILTER, False, 20)
+            ref = (oc, okeep, oenc, ook)
+        oc, okeep, oenc, ook = ref
+        assert np.array_equal(codes, oc) and np.array_equal(keep, okeep) and counts["kept"] == len(okeep), (var, val)
+        assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1]), (var, val)
+
+
 @pytest.mark.parametrize("bits", [20, 16])
 def test_oracle_geom_filter_c_equals_python(bits):
     """the C restatement of the filtered diff's per-side decision (kdo_geom_filter, what the
