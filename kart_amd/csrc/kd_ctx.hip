@@ -276,7 +276,6 @@ int kd_init(int device_ordinal, kd_ctx** out) {
         if (hipMalloc(&s, SLAB_BYTES) == hipSuccess) c->slab = (char*)s;
         c->slab_used = 0;
     }
-    hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
     for (int j = 0; j < 2; j++) {  // the pinned staging chunks (without them: pageable copies)
         void* h = nullptr;
         if (hipHostMalloc(&h, PIN_CHUNK, hipHostMallocDefault) != hipSuccess) break;
@@ -285,6 +284,16 @@ int kd_init(int device_ordinal, kd_ctx** out) {
             break;
         }
         c->pin[j] = (char*)h;
+    }
+    hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
+    if (c->slab) {  // the runtime's fill / copy kernels load on their first use: a memset, a device
+                    // copy and a pinned round trip here, not inside the first diff
+        (void)hipMemsetAsync(c->slab, 0, 512, c->stream);
+        (void)hipMemcpyAsync(c->slab + 256, c->slab, 256, hipMemcpyDeviceToDevice, c->stream);
+        if (c->pin[0]) {
+            (void)hipMemcpyAsync(c->slab, c->pin[0], 256, hipMemcpyHostToDevice, c->stream);
+            (void)hipMemcpyAsync(c->pin[0], c->slab + 256, 256, hipMemcpyDeviceToHost, c->stream);
+        }
     }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         if (c->slab) (void)hipFree(c->slab);
