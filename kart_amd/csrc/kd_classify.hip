@@ -527,16 +527,20 @@ int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t f
     int rc;
     if ((rc = check_side(base, "base")) || (rc = check_side(target, "target"))) return rc;
     KD_HIP(hipSetDevice(ctx->device));
+    host_mark(ctx, nullptr);
     kd_side A, B;
     if ((rc = stage_side(ctx, base, "in.a", &A)) || (rc = stage_side(ctx, target, "in.b", &B))) return rc;
+    host_mark(ctx, "kd_diff2 stage");
     u64 total = base->n + target->n;
     void *dd, *du, *dc;
     if ((rc = ensure(ctx, "out.delta", (total + 1) * 8, &dd))) return rc;
     if ((rc = ensure(ctx, "out.upd", (total + 1) * 8, &du))) return rc;
     if ((rc = ensure(ctx, "out.counts", 64, &dc))) return rc;
+    host_mark(ctx, "kd_diff2 ensure");
     u64* counts = (u64*)dc;
     u32* derr = (u32*)(counts + 4);
     if ((rc = diff2_device(ctx, &A, &B, flags, (u32*)dd, (u32*)du, counts, derr))) return rc;
+    host_mark(ctx, "kd_diff2 kernels");
     u64 hc[5];
     KD_HIP(hipMemcpyAsync(hc, dc, 40, hipMemcpyDeviceToHost, ctx->stream));
     KD_HIP(hipStreamSynchronize(ctx->stream));
@@ -546,6 +550,7 @@ int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t f
         return KD_EUNSUPPORTED;
     }
     u64 nd = hc[3], nu = hc[1];
+    host_mark(ctx, "kd_diff2 counts");
     size_t bytes = sizeof(kd_diff_result) + (nd + nu) * 8 + 16;
     kd_diff_result* r = (kd_diff_result*)std::malloc(bytes);
     KD_CHECK(r, "kd_diff2: out of host memory");
@@ -558,6 +563,7 @@ int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t f
             return rc;
         }
     }
+    host_mark(ctx, "kd_diff2 results");
     prof_flush(ctx);
     *out = r;
     return KD_OK;

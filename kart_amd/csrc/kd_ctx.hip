@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <chrono>
 #include <thread>
 
 #include "kd_internal.h"
@@ -79,10 +80,13 @@ int stage_in(kd_ctx* ctx, const char* slot, const void* p, size_t bytes, u32 mem
     return KD_OK;
 }
 
-constexpr size_t PIN_CHUNK = (size_t)4 << 20, PIN_MIN = (size_t)64 << 10;
+// Pinned staging for small / middling transfers: a pageable copy pins the caller's pages, which a
+// one-shot process pays for every buffer.  From PIN_MAX up the runtime's own pinning of the caller's
+// pages (no host copy) is the faster path (10M-entry sides: 48 vs 25 GB/s, r4w).
+constexpr size_t PIN_CHUNK = (size_t)4 << 20, PIN_MIN = (size_t)64 << 10, PIN_MAX = (size_t)32 << 20;
 
 int stage_h2d(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
-    if (bytes < PIN_MIN || !ctx->pin[1]) {
+    if (bytes < PIN_MIN || bytes >= PIN_MAX || !ctx->pin[1]) {
         KD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));  // (pageable: staged by the runtime)
         return KD_OK;
     }
@@ -100,7 +104,7 @@ int stage_h2d(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
 }
 
 int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
-    if (bytes < PIN_MIN || !ctx->pin[1]) {
+    if (bytes < PIN_MIN || bytes >= PIN_MAX || !ctx->pin[1]) {
         KD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
         KD_HIP(hipStreamSynchronize(ctx->stream));
         return KD_OK;
@@ -121,6 +125,16 @@ int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
     }
     ctx->pin_next = 0;
     return KD_OK;
+}
+
+void host_mark(kd_ctx* ctx, const char* name) {
+    static const int on = [] { const char* v = std::getenv("KD_TRACE_HOST"); return v && v[0] == '1'; }();
+    static thread_local std::chrono::steady_clock::time_point t0;
+    if (!on) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    const auto t = std::chrono::steady_clock::now();
+    if (name) std::fprintf(stderr, "[kd] %-22s %9.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
 }
 
 void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a) {
@@ -286,14 +300,31 @@ int kd_init(int device_ordinal, kd_ctx** out) {
         c->pin[j] = (char*)h;
     }
     hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
-    if (c->slab) {  // the runtime's fill / copy kernels load on their first use: a memset, a device
-                    // copy and a pinned round trip here, not inside the first diff
-        (void)hipMemsetAsync(c->slab, 0, 512, c->stream);
-        (void)hipMemcpyAsync(c->slab + 256, c->slab, 256, hipMemcpyDeviceToDevice, c->stream);
-        if (c->pin[0]) {
-            (void)hipMemcpyAsync(c->slab, c->pin[0], 256, hipMemcpyHostToDevice, c->stream);
-            (void)hipMemcpyAsync(c->pin[0], c->slab + 256, 256, hipMemcpyDeviceToHost, c->stream);
-        }
+    if (c->slab) {
+        // What a process's first diff would otherwise pay (r4x: 16 ms of a 17-ms first kd_diff2 on
+        // 60k-entry sides): the runtime's fill / copy kernels and DMA queues come up on first use,
+        // and the pinned chunks' pages on first touch — a memset, a device copy and a full-chunk
+        // pinned round trip each way here; then one 1 + 1-entry classify2, the first launch of each
+        // of its kernels.  The slab's first pieces are the scratch (re-carved by later ensure()s).
+        (void)hipMemsetAsync(c->slab, 0, 1024, c->stream);
+        (void)hipMemcpyAsync(c->slab + 512, c->slab, 256, hipMemcpyDeviceToDevice, c->stream);
+        for (int j = 0; j < 2; j++)
+            if (c->pin[j]) {
+                std::memset(c->pin[j], 0, PIN_CHUNK);
+                (void)hipMemcpyAsync(c->slab + 4096, c->pin[j], PIN_CHUNK, hipMemcpyHostToDevice, c->stream);
+                (void)hipMemcpyAsync(c->pin[j], c->slab + 4096, PIN_CHUNK, hipMemcpyDeviceToHost, c->stream);
+            }
+        kd_side A{};
+        A.n = 1;
+        A.key = (const u64*)c->slab;  // zero key, zero OID on both sides: one unchanged pair
+        A.oid = (const u8*)c->slab;
+        A.mem = KD_MEM_DEVICE;
+        A.key_mode = KD_KEY_INT;
+        u32* out = (u32*)(c->slab + 512);
+        c->slab_used = (size_t)8 << 20;  // the join's own workspaces past the scratch above
+        (void)diff2_device(c, &A, &A, 0, out, out + 8, (u64*)(c->slab + 768), (u32*)(c->slab + 800));
+        c->slab_used = 0;  // (every ensure() piece above is released with the warm-up)
+        c->bufs.clear();
     }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         if (c->slab) (void)hipFree(c->slab);

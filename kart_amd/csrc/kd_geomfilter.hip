@@ -840,10 +840,11 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
     }
     if (tiles) {
         if (g && gh.dense) {
-            // KD_GFD (A/B): prefetch depth 1 / 2, 't' = transposed loads; default "1t"
+            // KD_GFD (A/B): prefetch depth 1 / 2, 's' strided / 't' transposed loads; default "1s"
+            // (r4w on the C5 mix: 1s 0.320, 2s 0.334, 2t 0.338, 1t 0.346 ms; k_gf_heads 0.355)
             const char* v = std::getenv("KD_GFD");
             const int pf = v && v[0] == '2' ? 2 : 1;
-            const bool tr = !(v && v[0] && v[1] == 's');
+            const bool tr = v && v[0] && v[1] == 't';
             KD_HIP(hipMemsetAsync(t_cnt, 0, tiles * 4, ctx->stream));
             const void* fn = pf == 2 ? (tr ? (const void*)k_gf_dense<2, true> : (const void*)k_gf_dense<2, false>)
                                      : (tr ? (const void*)k_gf_dense<1, true> : (const void*)k_gf_dense<1, false>);

@@ -111,6 +111,9 @@ int ensure(kd_ctx* ctx, const char* slot, size_t bytes, void** out);
 // host -> device on ctx->stream through the pinned chunks (returns when src may be reused);
 // device -> host, blocking (the stream is synchronised)
 int stage_h2d(kd_ctx* ctx, void* dst, const void* src, size_t bytes);
+// KD_TRACE_HOST=1: stream sync + wall time since the previous mark to stderr (diagnosis only;
+// name nullptr starts a sequence)
+void host_mark(kd_ctx* ctx, const char* name);
 int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 // 256 zero bytes of device memory: what empty inputs point at, and the target of loads issued by

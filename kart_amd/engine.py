@@ -5,11 +5,16 @@ pipelines (bench.py) keep their buffers in HBM through the library's own allocat
 (``kart_amd.device``).
 """
 import ctypes
+import os
+import sys
+import time
 from dataclasses import dataclass
 
 import numpy as np
 
 from . import _native as N
+
+_TRACE = os.environ.get("KD_TRACE_HOST") == "1"  # (diagnosis: host phase times to stderr)
 
 # placeholder a native call gets for an empty host array: a module-level array, alive for every call
 _PAD = np.zeros(16, np.uint8)
@@ -122,9 +127,14 @@ class Engine:
         (kd_diff2_device_perm: no OID or filename gather)."""
         if base.walk_rows or target.walk_rows:
             return self._diff2_perm(base, target, flags)
+        t0 = time.perf_counter() if _TRACE else 0
         sa, sb = base.kd_side(), target.kd_side()
         res = ctypes.POINTER(N.KdDiffResult)()
+        if _TRACE:
+            print(f"[kd] engine.diff2 kd_side    {1e3 * (time.perf_counter() - t0):9.3f} ms", file=sys.stderr)
         N.check(self.L.kd_diff2(self.ctx, ctypes.byref(sa), ctypes.byref(sb), flags, ctypes.byref(res)), "kd_diff2")
+        if _TRACE:
+            print(f"[kd] engine.diff2 call       {1e3 * (time.perf_counter() - t0):9.3f} ms", file=sys.stderr)
         try:
             r = res.contents
             nd, nu = int(r.n_delta), int(r.n_update)
