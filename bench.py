@@ -196,17 +196,24 @@ ROCPROF_STATS = {"c3": "profiles/r04/c3_kernel_stats.csv", "c3v": "profiles/r03/
                  "c5": "profiles/r04/c5_kernel_stats.csv"}
 
 
+# the HIP-event name a role is timed under -> the kernel symbols rocprof lists for it
+# (kd_geom_filter_deltas times k_gf_dense, the dense-heads form, under "k_gf_heads")
+KERNEL_SYMBOLS = {"k_gf_heads": ("k_gf_dense", "k_gf_heads")}
+
+
 def rocprof_avg_ms(workload, kernel):
     """the kernel's average duration in the committed `rocprofv3 --kernel-trace --stats` summary of
     this workload (profiles/r04; C3v profiles/r03), or None"""
     path = os.path.join(ROOT, ROCPROF_STATS.get(workload, "-"))
+    names = KERNEL_SYMBOLS.get(kernel, (kernel,))
     try:
         import csv
 
         with open(path) as f:
-            for r in csv.DictReader(f):
-                if r["Name"].split("(")[0].split("<")[0] == kernel:
-                    return float(r["AverageNs"]) / 1e6, os.path.relpath(path, ROOT)
+            rows = {r["Name"].split("(")[0].split("<")[0]: r for r in csv.DictReader(f)}
+        for name in names:
+            if name in rows:
+                return float(rows[name]["AverageNs"]) / 1e6, os.path.relpath(path, ROOT)
     except (OSError, KeyError, ValueError):
         pass
     return None
@@ -223,7 +230,7 @@ def roofline(kern, dom, alg_bytes, traffic_json, n_units, workload=None):
     try:
         with open(traffic_json) as f:
             tj = json.load(f)
-        if tj.get("kernel") == dom and int(tj.get("n_units", tj.get("n_points", -1))) == n_units:
+        if tj.get("kernel") in KERNEL_SYMBOLS.get(dom, (dom,)) and int(tj.get("n_units", tj.get("n_points", -1))) == n_units:
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError, TypeError):
         pass

@@ -554,6 +554,7 @@ int kd_diff2(kd_ctx* ctx, const kd_side* base, const kd_side* target, uint32_t f
     size_t bytes = sizeof(kd_diff_result) + (nd + nu) * 8 + 16;
     kd_diff_result* r = (kd_diff_result*)std::malloc(bytes);
     KD_CHECK(r, "kd_diff2: out of host memory");
+    host_mark(ctx, "kd_diff2 malloc");
     r->n_insert = hc[0]; r->n_update = hc[1]; r->n_delete = hc[2]; r->n_delta = nd;
     r->delta = (u32*)(r + 1);
     r->upd = r->delta + 2 * nd;

@@ -103,6 +103,16 @@ int stage_h2d(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
     return KD_OK;
 }
 
+// device -> pinned host chunk by the library's own kernel (16-B stores over the fabric): the
+// runtime's first device-to-host copy of a process waited 8 ms whatever was warmed at init (r4z2)
+__global__ __launch_bounds__(256) void k_to_host(const u8* __restrict__ src, u8* __restrict__ dst, u64 bytes) {
+    const u64 n16 = bytes / 16;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n16; i += (u64)gridDim.x * 256)
+        ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    const u64 t = 16 * n16 + (u64)blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x == 0 && t < bytes) dst[t] = src[t];
+}
+
 int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (bytes < PIN_MIN || bytes >= PIN_MAX || !ctx->pin[1]) {
         KD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -111,17 +121,28 @@ int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
     }
     // DMA of chunk i+1 is queued before chunk i is copied out of its buffer
     const size_t n = (bytes + PIN_CHUNK - 1) / PIN_CHUNK;
+    const bool aligned = ((uintptr_t)src & 15) == 0 && ctx->pin_dev[1];
     auto issue = [&](size_t i) -> hipError_t {
         const size_t o = i * PIN_CHUNK, c = std::min(PIN_CHUNK, bytes - o);
-        hipError_t e = hipMemcpyAsync(ctx->pin[i & 1], (const char*)src + o, c, hipMemcpyDeviceToHost, ctx->stream);
+        hipError_t e;
+        if (aligned) {
+            const unsigned grid = (unsigned)std::min<size_t>((c / 16 + 255) / 256 + 1, 1024);
+            hipLaunchKernelGGL(k_to_host, dim3(grid), dim3(256), 0, ctx->stream, (const u8*)src + o,
+                               (u8*)ctx->pin_dev[i & 1], (u64)c);
+            e = hipGetLastError();
+        } else {
+            e = hipMemcpyAsync(ctx->pin[i & 1], (const char*)src + o, c, hipMemcpyDeviceToHost, ctx->stream);
+        }
         return e == hipSuccess ? hipEventRecord(ctx->pin_ev[i & 1], ctx->stream) : e;
     };
     KD_HIP(issue(0));
     for (size_t i = 0; i < n; i++) {
         if (i + 1 < n) KD_HIP(issue(i + 1));
         KD_HIP(hipEventSynchronize(ctx->pin_ev[i & 1]));
+        host_mark(ctx, "d2h chunk wait");
         const size_t o = i * PIN_CHUNK;
         std::memcpy((char*)dst + o, ctx->pin[i & 1], std::min(PIN_CHUNK, bytes - o));
+        host_mark(ctx, "d2h chunk copy-out");
     }
     ctx->pin_next = 0;
     return KD_OK;
@@ -292,12 +313,14 @@ int kd_init(int device_ordinal, kd_ctx** out) {
     }
     for (int j = 0; j < 2; j++) {  // the pinned staging chunks (without them: pageable copies)
         void* h = nullptr;
-        if (hipHostMalloc(&h, PIN_CHUNK, hipHostMallocDefault) != hipSuccess) break;
+        if (hipHostMalloc(&h, PIN_CHUNK, hipHostMallocMapped) != hipSuccess) break;
         if (hipEventCreateWithFlags(&c->pin_ev[j], hipEventDisableTiming) != hipSuccess) {
             (void)hipHostFree(h);
             break;
         }
         c->pin[j] = (char*)h;
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess) c->pin_dev[j] = dp;
     }
     hipLaunchKernelGGL(k_load_probe, dim3(1), dim3(64), 0, c->stream);
     if (c->slab) {
@@ -312,7 +335,11 @@ int kd_init(int device_ordinal, kd_ctx** out) {
             if (c->pin[j]) {
                 std::memset(c->pin[j], 0, PIN_CHUNK);
                 (void)hipMemcpyAsync(c->slab + 4096, c->pin[j], PIN_CHUNK, hipMemcpyHostToDevice, c->stream);
-                (void)hipMemcpyAsync(c->pin[j], c->slab + 4096, PIN_CHUNK, hipMemcpyDeviceToHost, c->stream);
+                if (c->pin_dev[j])
+                    hipLaunchKernelGGL(k_to_host, dim3(64), dim3(256), 0, c->stream, (const u8*)(c->slab + 4096),
+                                       (u8*)c->pin_dev[j], (u64)PIN_CHUNK);
+                (void)hipEventRecord(c->pin_ev[j], c->stream);  // (and a blocking wait on each event)
+                (void)hipEventSynchronize(c->pin_ev[j]);
             }
         kd_side A{};
         A.n = 1;

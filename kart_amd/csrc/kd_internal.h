@@ -98,6 +98,7 @@ struct kd_ctx {
     // pageable hipMemcpy pins the caller's pages on first use, which a one-shot process pays for
     // every buffer it hands over
     char* pin[2] = {nullptr, nullptr};
+    void* pin_dev[2] = {nullptr, nullptr};  // the chunks' device-side addresses (k_to_host writes them)
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
     int pin_next = 0;
 };
