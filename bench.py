@@ -180,8 +180,19 @@ def engine_for(H):
     return eng
 
 
+# The warmup ends with untimed steps for at least this long directly before the timed bracket: the
+# GPU clocks down while the host checks the warmup's results, and the first ~20 ms after an idle
+# spell run slow (r4pw: C5-envelopes 1.51 -> 0.73 ms per step over 20 steps, C3 3.46 -> 3.41)
+PREWARM_S = float(os.environ.get("BENCH_PREWARM_S", "0.1"))
+
+
 def timed(H, eng, step, steps):
     """barrier + device sync, K steps, device sync + barrier; the max-over-ranks seconds"""
+    if PREWARM_S > 0:  # untimed steps right before the bracket, for at least PREWARM_S seconds
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < PREWARM_S:
+            step()
+            eng.sync()
     H.barrier()
     eng.device_sync()
     t0 = time.perf_counter()
