@@ -133,6 +133,8 @@ typedef struct kd_merge_result {
 /* -------- context -------- */
 int kd_abi_version(void);
 const char* kd_last_error(void);
+/* Creates the context and warms the first-diff path (runtime copy kernels, DMA queues, the pinned
+ * staging chunks, one 1 + 1-entry classify2), so a one-shot process's first diff runs warm. */
 int kd_init(int device_ordinal, kd_ctx** out);
 int kd_fini(kd_ctx* ctx);
 /* Launch on an external HIP stream (e.g. torch's current stream); NULL = the context's own. */
