@@ -468,7 +468,10 @@ __global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict
 //   k_pkm_scan   per chunk of PKM_CH masks: the popcounts' exclusive prefix (u32) + the chunk total;
 //                the last workgroup to finish scans the chunk totals (one pass, no extra launch)
 //   k_pkm_place  record -> its rank: chunk prefix + in-chunk prefix + popcount(mask below its bit)
-constexpr int PKM_NT = 256, PKM_IPT = 8, PKM_CH = PKM_NT * PKM_IPT;
+#ifndef KD_PKM_IPT
+#define KD_PKM_IPT 16  // masks per scan thread (r4pk, C3: 2 / 4 / 8 / 16 -> scan 0.111 / 0.074 / 0.052 / 0.038 ms)
+#endif
+constexpr int PKM_NT = 256, PKM_IPT = KD_PKM_IPT, PKM_CH = PKM_NT * PKM_IPT;
 
 __global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ rec, u64 ncap, const u64* __restrict__ dn,
                                                      const u64* __restrict__ kA, const u64* __restrict__ kB,
@@ -536,9 +539,29 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_scan(const u64* __restrict__ mas
     }
     __syncthreads();
     if (!s_last) return;
-    // the last workgroup: exclusive scan of every chunk's total
+    // the last workgroup: exclusive scan of every chunk's total.  Up to 8 per thread: each thread a
+    // contiguous run, all its loads issued together (one L2 round trip instead of one per 256
+    // totals: the serial tail was most of this kernel, r4pk)
     __threadfence();
     const u32 nch = gridDim.x;
+    if (nch <= 8 * PKM_NT) {
+        const u32 per = (nch + PKM_NT - 1) / PKM_NT, k0 = tid * per;
+        u32 v[8], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            v[j] = (u32)j < per && k0 + j < nch ? __hip_atomic_load(chunk_tot + k0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            sum += v[j];
+        }
+        u32 t2;
+        u32 e = block_scan_u32<PKM_NT>(sum, s_wave, &t2);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if ((u32)j < per && k0 + j < nch) chunk_pre[k0 + j] = e;
+            e += v[j];
+        }
+        if (tid == 0) *done_ctr = 0;
+        return;
+    }
     u32 carry = 0;
     for (u32 k0 = 0; k0 < nch; k0 += PKM_NT) {
         const u32 k = k0 + tid;

@@ -22,7 +22,7 @@ def _int_side(pks, rng):
     return packing.PackedSide(keys, rng.integers(0, 256, size=(keys.size, 20), dtype=np.uint8), 0, np.arange(keys.size))
 
 
-@pytest.mark.parametrize("case", ["small", "neg", "wide", "one", "empty_base", "dense"])
+@pytest.mark.parametrize("case", ["small", "neg", "wide", "one", "empty_base", "dense", "spread", "range_1e9"])
 def test_gpu_delta_pk_order_vs_numpy(engine, case):
     """records of two int sides -> pks ascending + record index: any pk range (a few bits, the whole
     signed 64-bit range: 64-bit compact keys, 8 passes), a single pk, an empty side"""
@@ -40,6 +40,12 @@ def test_gpu_delta_pk_order_vs_numpy(engine, case):
         pa, pb = np.array([77]), np.array([77])
     elif case == "empty_base":
         pa, pb = np.zeros(0, np.int64), np.arange(5, 50000)
+    elif case == "spread":  # bitmap path, hundreds of scan chunks (the one-round-trip tail scan)
+        u = np.unique(rng.integers(0, 200_000_000, 1_200_000, dtype=np.int64))
+        pa, pb = u[: 2 * u.size // 3], u[u.size // 3:]
+    elif case == "range_1e9":  # bitmap path past the tail scan's register run (its looped form)
+        u = np.unique(rng.integers(0, 1_500_000_000, 600_000, dtype=np.int64))
+        pa, pb = u[: 2 * u.size // 3], u[u.size // 3:]
     else:
         pa, pb = np.arange(0, 2_000_000), np.arange(1_000_000, 3_000_000)
     A, B = _int_side(pa, rng), _int_side(pb, rng)
