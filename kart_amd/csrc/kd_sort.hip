@@ -492,7 +492,7 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ r
                 key = d.x != KD_NONE ? kA[d.x] : kB[d.y];
             }
             pk = wk::int_key_pk(key);
-            pk_out[r] = pk;
+            if (!rkey) pk_out[r] = pk;  // (with the record keys, k_pkm_place recomputes it: no write)
         }
         const u64 b = (u64)((pk >> 6) - lo_block);
         const bool inb = ok && b < nb;  // (a pk outside the caller's bounds is dropped, never written out of range)
@@ -574,13 +574,14 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_scan(const u64* __restrict__ mas
     if (tid == 0) *done_ctr = 0;  // ready for the next call
 }
 
-__global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pks, u64 ncap, const u64* __restrict__ dn,
-                                                      i64 lo_block, u64 nb, const u64* __restrict__ masks,
-                                                      const u32* __restrict__ local, const u32* __restrict__ chunk_pre,
-                                                      i64* __restrict__ out_pk, u32* __restrict__ out_perm) {
+__global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pks, const u64* __restrict__ rkey, u64 ncap,
+                                                      const u64* __restrict__ dn, i64 lo_block, u64 nb,
+                                                      const u64* __restrict__ masks, const u32* __restrict__ local,
+                                                      const u32* __restrict__ chunk_pre, i64* __restrict__ out_pk,
+                                                      u32* __restrict__ out_perm) {
     const u64 n = min(*dn, ncap);
     for (u64 r = (u64)blockIdx.x * PKM_NT + threadIdx.x; r < n; r += (u64)gridDim.x * PKM_NT) {
-        const i64 pk = pks[r];
+        const i64 pk = rkey ? wk::int_key_pk(rkey[r]) : pks[r];
         const u64 b = (u64)((pk >> 6) - lo_block);
         if (b >= nb) continue;
         const u64 below = masks[b] & ((1ull << (pk & 63)) - 1);
@@ -1016,8 +1017,8 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
         });
         if (rc) return rc;
         return launch(ctx, "k_pkm_place", [&] {
-            hipLaunchKernelGGL(k_pkm_place, dim3(g1), dim3(PKM_NT), 0, ctx->stream, (const i64*)tpk, cap, d_n, lo_block,
-                               nb, (const u64*)masks, (const u32*)local, (const u32*)cpre, d_pk, d_perm);
+            hipLaunchKernelGGL(k_pkm_place, dim3(g1), dim3(PKM_NT), 0, ctx->stream, (const i64*)tpk, d_keys, cap, d_n,
+                               lo_block, nb, (const u64*)masks, (const u32*)local, (const u32*)cpre, d_pk, d_perm);
         });
     }
     SortPlan plan = pk_plan(pk_lo, pk_hi);
