@@ -625,11 +625,17 @@ __global__ __launch_bounds__(GF_NT) __attribute__((amdgpu_waves_per_eu(PF == 1 &
             for (int k = 0; k < nb; k++) wenc[lane * nb + k] = 0;
         if (d < n) {
             GHit h;
+#ifdef KD_GF_PROBE_NODECODE  // profiling variant: the loads and stores alone
+            const u32 x = L0.v0.x ^ L0.v1.y ^ L0.v2.w ^ L1.v0.z ^ L1.v1.w ^ L1.v2.x ^ pr.x ^ pr.y;
+            const int co = (int)(x & 3), cn = (int)((x >> 2) & 3);
+            h.r = -1;
+#else
             const bool defer = g.fb_list != nullptr;
             deferred = !decode_head(a, g, 0, pr.x, L0, h, d, defer);
             const int co = h.code;
             deferred |= !decode_head(a, g, 1, pr.y, L1, h, d, defer);
             const int cn = h.code;
+#endif
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
             if (a.enc && !deferred && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
