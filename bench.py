@@ -21,9 +21,13 @@ torch is not imported at all.
 
 --workload c2 (configs[1]): a 10M-point layer per GPU, 1 % upd/del/ins (weak scaling at N>1);
 c4 (configs[3]): 50M-row string-PK three-way merge classification; c5 (configs[4]): the spatially
-filtered diff of the 100M-feature polygon layer (classify2 + per-delta geometry envelope filter +
-EnvelopeEncoder); c5env: the envelope kernels alone over a raw geometry arena; c6:
+filtered diff of a 100M-feature layer on SURVEY §8(d)'s mix (classify2 + the deltas' geometry heads
+gathered into delta order + per-delta envelope filter + EnvelopeEncoder + the blob fallback); c5env: the envelope kernels alone over a raw geometry arena; c6:
 hex WKB of every geometry.
+
+Timing: W untimed warmup steps (their results checked), then — after a burst of untimed steps of at
+least BENCH_PREWARM_S = 0.1 s, so the clocks are up after the host's checks — a barrier + device
+sync, exactly K timed steps, device sync + barrier; the max over ranks.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c5env|c6] [--n UNITS]
                        [--no-cpu-baseline] [--no-host-timing]
