@@ -584,8 +584,11 @@ __device__ __forceinline__ DenseLd dense_load(const GfArgs& a, const GfHeadArgs&
     return L;
 }
 
+#ifndef KD_GFD_WAVES
+#define KD_GFD_WAVES 4  // k_gf_dense<1, false>: waves per SIMD the register budget is cut for
+#endif
 template <int PF, bool TR>
-__global__ __launch_bounds__(GF_NT) __attribute__((amdgpu_waves_per_eu(PF == 1 && !TR ? 4 : 3))) void k_gf_dense(GfArgs a, GfHeadArgs g) {
+__global__ __launch_bounds__(GF_NT) __attribute__((amdgpu_waves_per_eu(PF == 1 && !TR ? KD_GFD_WAVES : 3))) void k_gf_dense(GfArgs a, GfHeadArgs g) {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
     __shared__ u32 s_encw[GF_NT * 4];  // 16 B per lane: nb <= 16 index-envelope bytes
     __shared__ u32x4 s_tr[TR ? (GF_NT / 64) * 6 * 64 : 1];  // 6 KB per wave
