@@ -192,11 +192,18 @@ PREWARM_S = float(os.environ.get("BENCH_PREWARM_S", "0.1"))
 
 def timed(H, eng, step, steps):
     """barrier + device sync, K steps, device sync + barrier; the max-over-ranks seconds"""
-    if PREWARM_S > 0:  # untimed steps right before the bracket, for at least PREWARM_S seconds
+    if PREWARM_S > 0:
+        # untimed steps right before the bracket for at least PREWARM_S seconds.  A step may hold
+        # collectives (the gathered records at N > 1), so every rank runs the same count: one step
+        # timed on each rank, the count from the slowest
+        H.barrier()
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < PREWARM_S:
+        step()
+        eng.sync()
+        one = H.max(time.perf_counter() - t0)
+        for _ in range(min(10_000, int(PREWARM_S / max(one, 1e-6)))):
             step()
-            eng.sync()
+        eng.sync()
     H.barrier()
     eng.device_sync()
     t0 = time.perf_counter()
