@@ -25,9 +25,10 @@ filtered diff of a 100M-feature layer on SURVEY §8(d)'s mix (classify2 + the de
 gathered into delta order + per-delta envelope filter + EnvelopeEncoder + the blob fallback); c5env: the envelope kernels alone over a raw geometry arena; c6:
 hex WKB of every geometry.
 
-Timing: W untimed warmup steps (their results checked), then — after a burst of untimed steps of at
-least BENCH_PREWARM_S = 0.1 s, so the clocks are up after the host's checks — a barrier + device
-sync, exactly K timed steps, device sync + barrier; the max over ranks.
+Timing: W untimed warmup steps (their results checked), then — after a burst of untimed steps worth
+BENCH_PREWARM_S = 0.1 s (the count from one timed step, the slowest rank's, so every rank runs the
+same steps), so the clocks are up after the host's checks — a barrier + device sync, exactly K timed
+steps, device sync + barrier; the max over ranks.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c5env|c6] [--n UNITS]
                        [--no-cpu-baseline] [--no-host-timing]
