@@ -307,7 +307,7 @@ def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1000, 3_000_000])
+@pytest.mark.parametrize("n", [40, 130, 1000, 3_000_000])  # (1 and 13 deltas: one partial chunk)
 def test_gpu_filter_dense_variants_agree(engine, n, monkeypatch):
     """k_gf_dense (delta-order heads, kd_geom_filter_deltas): every prefetch depth / load form and
     the pair-indexed k_gf_heads give the oracle's codes, kept list and index envelopes"""
