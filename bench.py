@@ -215,7 +215,7 @@ def timed(H, eng, step, steps):
     return H.max(time.perf_counter() - t0)
 
 
-ROCPROF_STATS = {"c3": "profiles/r04/c3_kernel_stats.csv", "c3v": "profiles/r03/c3v_kernel_stats.csv", "c4": "profiles/r04/c4_kernel_stats.csv",
+ROCPROF_STATS = {"c3": "profiles/r04/c3_kernel_stats.csv", "c3v": "profiles/r04/c3v_kernel_stats.csv", "c4": "profiles/r04/c4_kernel_stats.csv",
                  "c5": "profiles/r04/c5_kernel_stats.csv"}
 
 
@@ -226,7 +226,7 @@ KERNEL_SYMBOLS = {"k_gf_heads": ("k_gf_dense", "k_gf_heads")}
 
 def rocprof_avg_ms(workload, kernel):
     """the kernel's average duration in the committed `rocprofv3 --kernel-trace --stats` summary of
-    this workload (profiles/r04; C3v profiles/r03), or None"""
+    this workload (profiles/r04), or None"""
     path = os.path.join(ROOT, ROCPROF_STATS.get(workload, "-"))
     names = KERNEL_SYMBOLS.get(kernel, (kernel,))
     try:
