@@ -1032,10 +1032,14 @@ __device__ __forceinline__ u32 dma_range(const Range& R, u32x4* dst, u32 q0) {
 // SPLIT: every differing path is staged with its ancestor entry as a candidate (a, o, t) and the
 // rule is applied by k_resolve3<HAVE_A> over the placed list (many paths per thread: the OID and
 // filename loads of the few differing paths of a tile no longer hold the tile's LDS)
-template <int NT, int IPT, bool HASH, bool PERM, bool SPLIT>
+template <int NT, int IPT, bool HASH, bool PERM, bool SPLIT, bool OL = false>
 __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
     const Join2Args& g = g3.j;
     using LD = Join2Lds<NT, IPT>;
+    // OL (A/B, sorted-form sides only): ours' and theirs' OIDs of the tile by LDS-DMA with the keys,
+    // so the matched pairs compare from LDS (one HBM round trip less per tile, 15 KB more LDS)
+    constexpr bool LOIDS = OL && !PERM;
+    __shared__ u32x4 s_oid[LOIDS ? LD::OCH : 1];
     static_assert(LD::TILE <= 4095, "per-item records hold 12-bit local indices");
     constexpr int KCH = (8 * (J3_ACAP + 2) + 16 + 15) / 16 + 4;
     __shared__ u32x4 s_ch[LD::CHK];
@@ -1075,6 +1079,13 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
     u32 qq = dma_range<NT>(r.ka, s_ch, 0);
     qq = dma_range<NT>(r.kb, s_ch + r.c1, qq);
     if (lk) qq = dma_range<NT>(rk, s_k, qq);
+    Range roA{}, roB{};
+    if (LOIDS) {
+        roA = mk_range(g.oidA, 20 * q.i0, 20 * q.i1);
+        roB = mk_range(g.oidB, 20 * q.j0, 20 * q.j1e);
+        qq = dma_range<NT>(roA, s_oid, qq);
+        qq = dma_range<NT>(roB, s_oid + roA.nch, qq);
+    }
     __syncthreads();  // vmcnt(0) + barrier: the keys have landed
     Range rnA{}, rnB{};
     bool lnames = false;
@@ -1112,7 +1123,22 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
             ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
         }
     }
-    tile_oid_cmp<IPT>(g, rec, ra, rb);
+    if (LOIDS) {  // matched pairs' OIDs from LDS (both tile ranges landed with the keys)
+        typedef const __attribute__((address_space(3))) u32* l32;
+        const u32 ob = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_oid;
+        const u32 baseA = ob + roA.skew, baseB = ob + 16 * roA.nch + roB.skew;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const bool m = (rec[k] >> 25) == R_MATCH;
+            const u32 pa = baseA + 20 * (m ? (rec[k] & 0xFFF) : 0), pb = baseB + 20 * (m ? ((rec[k] >> 12) & 0xFFF) : 0);
+            u32 d = 0;
+#pragma unroll
+            for (int w = 0; w < 5; w++) d |= *(l32)(size_t)(pa + 4 * w) ^ *(l32)(size_t)(pb + 4 * w);
+            if (m && d) rec[k] |= 1u << 24;
+        }
+    } else {
+        tile_oid_cmp<IPT>(g, rec, ra, rb);
+    }
     bool ne = false;
     if (HASH && lnames) {
         __syncthreads();  // vmcnt(0) + barrier: the names DMA has landed
@@ -1330,6 +1356,8 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     // r4n: 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
     const char* se = getenv("KD_MERGE3_SPLIT");
     const bool split = se && atoi(se) == 1;
+    const char* oe = getenv("KD_J3_OL");  // (A/B: sorted-form sides' OIDs staged with the keys)
+    const bool j3_ol = oe && atoi(oe) == 1;
     void *cand3 = nullptr, *c2 = nullptr;
     if (split) {
         if ((rc = ensure(ctx, "c3.cand3", (total + 1) * 12, &cand3))) return rc;
@@ -1340,6 +1368,9 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
         if (split) {
             if (hash) { if (perm) KD_J3(true, true, true); else KD_J3(true, false, true); }
             else { if (perm) KD_J3(false, true, true); else KD_J3(false, false, true); }
+        } else if (j3_ol && !perm) {
+            if (hash) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, true, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a);
+            else hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, false, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a);
         } else {
             if (hash) { if (perm) KD_J3(true, true, false); else KD_J3(true, false, false); }
             else { if (perm) KD_J3(false, true, false); else KD_J3(false, false, false); }
