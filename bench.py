@@ -621,6 +621,42 @@ def cpu_baseline_diff(L, maps, seconds, tag):
             "reference_path": REFERENCE_CPU_PATH}
 
 
+def cpu_sharded(work, parts, seconds):
+    """A CPU baseline on the host cores: ``work(s)`` processes shard s of ``parts`` (the oracle's C
+    code, which releases the GIL) and returns its units.  All cores run every shard repeatedly for
+    ``seconds``; then shard 0 alone on one thread for ``seconds / 2``.  Returns
+    (cores, units per rep, reps, seconds, shard-0 units, its reps, its seconds)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    cores = host_cores()
+    with ThreadPoolExecutor(cores) as ex:
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            units = sum(ex.map(work, range(parts)))
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    reps1 = 0
+    while True:
+        u1 = work(0)
+        reps1 += 1
+        if time.perf_counter() - t0 >= seconds / 2:
+            break
+    return cores, units, reps, dt, u1, reps1, time.perf_counter() - t0
+
+
+def cpu_line(res, unit, what, tag):
+    """the cpu_baseline object of a cpu_sharded result"""
+    cores, units, reps, dt, u1, reps1, dt1 = res
+    return {"value": round(units * reps / dt / 1e6, 3), "unit": unit, "cores": cores, "kind": "port",
+            "sample": f"the full {tag} ({units} units) x {reps} reps in {dt:.1f}s: {what} on {cores} threads",
+            "one_thread": {"value": round(u1 * reps1 / dt1 / 1e6, 3), "unit": unit, "cores": 1,
+                           "sample": f"one shard ({u1} units) x {reps1} reps in {dt1:.1f}s"}}
+
+
 def host_timing(eng, L, h2d_s, h2d_bytes):
     """What the drop-in path spends outside the timed device step, for the same layer:
     * pack: the base side's relative leaf paths ('c/c/c/c/<b64(msgpack([pk]))>', in the order the tree
@@ -1003,24 +1039,25 @@ def run_c5env(args, H):
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         O = oracle()
-        m = min(n, 2_000_000)
-        h_enc = enc.download(np.uint8, m * nb).reshape(m, nb)
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            om, oe, okk, _ = O.envelope_batch(data[: int(off[m])], off[: m + 1], synth.C5_FILTER, bits)
-            if reps == 0 and not args.no_check:  # the baseline's sample doubles as a bit-exact check
-                assert np.array_equal(h_match[:m], om), "k_envelopes match flags differ from the oracle"
-                assert np.array_equal(h_ok[:m], okk), "k_envelopes enc_ok differs from the oracle"
-                assert np.array_equal(h_enc, oe), "EnvelopeEncoder bytes differ"
-                t0 = time.perf_counter()
-            reps += 1
-            if time.perf_counter() - t0 >= min(args.cpu_seconds, 5.0):
-                break
-        dt = time.perf_counter() - t0
-        cpu = {"value": round(m * reps / dt / 1e6, 3), "unit": "M geometries/s", "cores": 1, "kind": "port",
-               "sample": f"first {m} geometries of the same layer x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
-                         f"envelope batch (bbox test + index envelope + EnvelopeEncoder), 1 thread"}
+        parts = 4 * host_cores()
+        cut = np.linspace(0, n, parts + 1).astype(np.int64)
+        h_enc = enc.download(np.uint8, n * nb).reshape(n, nb)
+        got = [None] * parts
+
+        def work(s):
+            a, b = int(cut[s]), int(cut[s + 1])
+            o0 = int(off[a])
+            got[s] = O.envelope_batch(data[o0:int(off[b])], off[a:b + 1] - np.uint64(o0), synth.C5_FILTER, bits)
+            return b - a
+
+        res = cpu_sharded(work, parts, min(args.cpu_seconds, 10.0))
+        if not args.no_check:  # the baseline's last run doubles as a bit-exact check of the whole layer
+            assert np.array_equal(h_match, np.concatenate([g[0] for g in got])), "k_envelopes flags differ from the oracle"
+            assert np.array_equal(h_ok, np.concatenate([g[2] for g in got])), "k_envelopes enc_ok differs from the oracle"
+            assert np.array_equal(h_enc, np.concatenate([g[1] for g in got])), "EnvelopeEncoder bytes differ"
+        del got, h_enc
+        cpu = cpu_line(res, "M geometries/s", "oracle/kd_oracle.c envelope batch (bbox test + index envelope + "
+                                              f"EnvelopeEncoder) over {parts} geometry ranges", f"layer ({n} geometries)")
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M geometries/s",
@@ -1152,18 +1189,30 @@ def run_c6(args, H):
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         m = min(n, 200_000)
         blobs = [data[int(off[i]):int(off[i + 1])].tobytes() for i in range(m)]
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            for b in blobs:
-                O.hex_wkb(b)
-            reps += 1
-            if time.perf_counter() - t0 >= min(args.cpu_seconds, 5.0):
-                break
-        dt = time.perf_counter() - t0
-        cpu = {"value": round(m * reps / dt / 1e6, 3), "unit": "M geometries/s", "cores": 1, "kind": "port",
-               "sample": f"first {m} geometries of the same layer x {reps} reps in {dt:.1f}s: oracle.hex_wkb "
-                         f"(the reference's gpkg_geom_to_hex_wkb restated: slice + hexlify + upper), 1 thread"}
+        parts = 4 * host_cores()
+        cut = np.linspace(0, n, parts + 1).astype(np.int64)
+        first = {}
+
+        def work(s):
+            a, b = int(cut[s]), int(cut[s + 1])
+            hx, st = O.hex_wkb_batch(data, off[a:b + 1])
+            if s == 0:
+                first["hex"], first["st"] = hx, st
+            return b - a
+
+        res = cpu_sharded(work, parts, min(args.cpu_seconds, 10.0))
+        if not args.no_check:  # shard 0 of the C restatement equals the kernel's hex bytes
+            b0 = int(cut[1])
+            st0 = start.download(np.uint32, b0)
+            gh = hexbuf.download(np.uint8, 2 * int(off[b0]))
+            assert not first["st"].any()
+            for i in range(b0):
+                a, e = 2 * (int(off[i]) + int(st0[i])), 2 * int(off[i + 1])
+                if not np.array_equal(gh[a:e], first["hex"][a:e]):
+                    raise AssertionError(f"hex of geometry {i} differs from the C restatement")
+        cpu = cpu_line(res, "M geometries/s", "oracle/kd_oracle.c kdo_hex_wkb_batch (gpkg_geom_to_hex_wkb "
+                                              f"restated: slice + uppercase hex) over {parts} geometry ranges",
+                       f"layer ({n} geometries)")
         # the drop-in as Kart would call it: host values in, Python strs out (arena join, H2D, kernel,
         # D2H, one decode + numpy-bounded slicing), against a per-value binascii.hexlify loop
         import binascii
@@ -1212,8 +1261,9 @@ def run_c4(args, H):
     """C4 (configs[3]): three-way merge classification of a 50M-row string-PK table.  The sides come as
     the tree walk lists them (git tree order: buckets ascending, each leaf tree's few entries in
     filename order, not FNV-key order); one step = the three per-bucket sorts
-    (kd_sort_segmented_into) + classify2(ours, theirs) + k_resolve3, OIDs and filenames read through the
-    orders (kd_merge3_device_perm).  Beside it (``presorted``) the same merge over key-sorted sides."""
+    (kd_sort_segmented_into) + the one-pass three-way join (k_partition2, k_apart3, k_join3, k_place3),
+    OIDs and filenames read through the orders (kd_merge3_device_perm).  The table is SURVEY §8(d)'s
+    mix (synth.table3_layers).  Beside it (``presorted``) the same merge over key-sorted sides."""
     from kart_amd import synth
     from kart_amd.device import MergePipeline
 
@@ -1280,13 +1330,7 @@ def run_c4(args, H):
         for S, (k, o, order) in zip((A, O_, T), srt):
             P = packing.PackedSide(np.ascontiguousarray(k), np.ascontiguousarray(o), S.key_mode, np.arange(S.n),
                                    encoding=S.encoding)
-            lens = (S.name_off[1:] - S.name_off[:-1])[order]
-            off = np.zeros(S.n + 1, np.uint64)
-            np.cumsum(lens, out=off[1:])
-            w = int(lens[0]) if S.n else 0
-            assert np.all(lens == w)
-            P.name = np.ascontiguousarray(S.name.reshape(S.n, w)[order]).reshape(-1)
-            P.name_off = off
+            P.name, P.name_off = packing._gather_names(S.name, S.name_off, order)
             ks.append(P)
         del pipe
         pp = MergePipeline(eng, *ks)
@@ -1302,31 +1346,49 @@ def run_c4(args, H):
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         Orc = oracle()
         (kA, oA, _), (kO, oO, _), (kT, oT, _) = srt
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            oc, om, ocl = Orc.classify3(kA, oA, kO, oO, kT, oT)
-            if reps == 0 and not args.no_check:  # the baseline's run doubles as a bit-exact check
-                assert np.array_equal(conf, oc.reshape(-1, 3)), "classify3 conflicts differ from the oracle"
-                assert np.array_equal(md, om.reshape(-1, 2)), "classify3 merge deltas differ from the oracle"
-                t0 = time.perf_counter()
-            reps += 1
-            if time.perf_counter() - t0 >= min(args.cpu_seconds, 10.0):
-                break
-        dt = time.perf_counter() - t0
-        cpu = {"value": round(nall * reps / dt / 1e6, 3), "unit": "M entries/s", "cores": 1, "kind": "port",
-               "sample": f"the full C4 layer ({nall} entries, key-sorted) x {reps} reps in {dt:.1f}s: oracle/kd_oracle.c "
-                         f"classify3, 1 thread"}
+        parts = 4 * host_cores()
+        # bucket-range shards (keys ascend in their bucket bits): cut at ancestor key quantiles
+        ck = kA[np.linspace(0, A.n, parts + 1).astype(np.int64)[1:-1]] if A.n else np.zeros(0, np.uint64)
+        bnd = [np.concatenate([[0], np.searchsorted(k, ck), [k.shape[0]]]).astype(np.int64) for k in (kA, kO, kT)]
+        got = [None] * parts
+
+        def work(s):
+            sl = [slice(int(bd[s]), int(bd[s + 1])) for bd in bnd]
+            got[s] = Orc.classify3(kA[sl[0]], oA[sl[0]], kO[sl[1]], oO[sl[1]], kT[sl[2]], oT[sl[2]])
+            return sum(x.stop - x.start for x in sl)
+
+        res = cpu_sharded(work, parts, min(args.cpu_seconds, 10.0))
+        if not args.no_check:  # the baseline's last run, re-based to whole-side indices, is a bit-exact check
+            NONE = np.uint32(0xFFFFFFFF)
+
+            def rebase(rows, s, cols):
+                rows = rows.copy()
+                for c, side in enumerate(cols):
+                    m = rows[:, c] != NONE
+                    rows[m, c] += np.uint32(bnd[side][s])
+                return rows
+
+            oc = np.concatenate([rebase(got[s][0], s, (0, 1, 2)) for s in range(parts)])
+            om = np.concatenate([rebase(got[s][1], s, (1, 2)) for s in range(parts)])
+            assert np.array_equal(conf, oc), "classify3 conflicts differ from the oracle"
+            assert np.array_equal(md, om), "classify3 merge deltas differ from the oracle"
+            assert n_clean == sum(got[s][2] for s in range(parts))
+        del got
+        cpu = cpu_line(res, "M entries/s", f"oracle/kd_oracle.c classify3 over {parts} bucket-range shards",
+                       f"C4 layer ({nall} entries, key-sorted)")
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M entries/s",
         "n_gpus": H.world, "rccl_comm": H.comm, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8/u64 (integer)",
-        "data": "synthetic (seeded string-PK table: MsgpackHashPathEncoder paths in git tree order, synthetic OIDs)",
-        "config": {"workload": f"C4: {n}-row string-PK table per GPU, three-way merge classification "
-                               "(ancestor/ours/theirs join + libgit2 conflict rule) from walk-order sides",
-                   "rows_per_gpu": n, "entries_per_step": total, "conflicts": int(conf.shape[0]),
+        "data": "synthetic (seeded text-PK table: MsgpackHashPathEncoder paths in git tree order, synthetic OIDs)",
+        "config": {"workload": f"C4: {n}-row string-PK table per GPU (SURVEY 8(d) mix: 12-24-char text pks, 5% "
+                               "multibyte UTF-8; per side 5% updates, 0.5% inserts, 0.5% deletes from independent "
+                               "seeds; +0.5% rows edited differently on both sides, +0.5% identically; add/add), "
+                               "three-way merge classification (ancestor/ours/theirs join + libgit2 conflict rule) "
+                               "from walk-order sides",
+                   "rows_per_gpu": n, "entries_per_step": total, "mix": M.plan, "conflicts": int(conf.shape[0]),
                    "merge_deltas": int(md.shape[0]), "differing_paths": n_cand,
                    "parallelism": f"independent shards x{H.world}"},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},

@@ -340,13 +340,8 @@ int kd::resolve3_have_a(kd_ctx* ctx, const kd_side& A, const kd_side& O, const k
                            (const u64*)dz, (u64)0, (u64*)desc, 2 * nchunk, (u32*)aux, counts);
     });
     if (rc) return rc;
-    static int occ_r3a[2] = {0, 0};
-    if (occ_r3a[perm] <= 0) {
-        int nb = 0;
-        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, perm ? (const void*)k_resolve3<C3_NT, true, true> : (const void*)k_resolve3<C3_NT, false, true>, C3_NT, 0));
-        occ_r3a[perm] = nb > 0 ? nb : 1;
-    }
+    const int occ_r3a = occupancy(ctx, perm ? (const void*)k_resolve3<C3_NT, true, true> : (const void*)k_resolve3<C3_NT, false, true>,
+                                  C3_NT, 0);
     auto ptr = [&](const void* p, u64 n) { return n && p ? p : (const void*)dz; };
     Resolve3Args g{};
     g.A = (const u64*)dz; g.O = (const u64*)ptr(O.key, nO); g.T = (const u64*)ptr(T.key, nT);
@@ -359,7 +354,7 @@ int kd::resolve3_have_a(kd_ctx* ctx, const kd_side& A, const kd_side& O, const k
     g.pA = (const u32*)ptr(pA, nA); g.pO = (const u32*)ptr(pO, nO); g.pT = (const u32*)ptr(pT, nT);
     g.desc = (u64*)desc; g.nchunk = nchunk; g.aux = (u32*)aux;
     g.out_conf = d_conf; g.out_md = d_md; g.counts = counts; g.err = derr;
-    const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)occ_r3a[perm]);
+    const u64 grid = std::min<u64>((nO + nT) / C3_CH + 1, (u64)ctx->n_cu * (u64)occ_r3a);
     return launch(ctx, "k_resolve3", [&] {
         if (perm) hipLaunchKernelGGL((k_resolve3<C3_NT, true, true>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
         else hipLaunchKernelGGL((k_resolve3<C3_NT, false, true>), dim3((unsigned)grid), dim3(C3_NT), 0, ctx->stream, g);
@@ -430,14 +425,8 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     if ((rc = diff2_device(ctx, &O, &T, 0, (u32*)cand, nullptr, (u64*)c2, derr, perm ? pO : nullptr,
                            perm ? pT : nullptr)))
         return rc;
-    static int occ_r3[2] = {0, 0};  // resident k_resolve3 workgroups per CU, per instantiation
-    if (occ_r3[perm] <= 0) {
-        int nb = 0;
-        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, perm ? (const void*)k_resolve3<C3_NT, true, false> : (const void*)k_resolve3<C3_NT, false, false>, C3_NT, 0));
-        occ_r3[perm] = nb > 0 ? nb : 1;
-    }
-    ctx->occ_resolve3 = occ_r3[perm];
+    ctx->occ_resolve3 = occupancy(ctx, perm ? (const void*)k_resolve3<C3_NT, true, false> : (const void*)k_resolve3<C3_NT, false, false>,
+                                  C3_NT, 0);
     // an empty side (or an absent filename arena) points at device zeros: lanes without an entry
     // load from index 0 of every array instead of branching, so each array must be readable
     auto ptr = [&](const void* p, u64 n) { return n && p ? p : (const void*)dz; };

@@ -638,7 +638,7 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
         sd = g.out_delta + s_base[0];
         su = g.out_upd ? g.out_upd + s_base[1] : nullptr;
         kd = g.out_dkey ? g.out_dkey + s_base[0] : nullptr;
-        ku = g.out_dkey && g.out_upd ? g.out_ukey + s_base[1] : nullptr;
+        ku = g.out_dkey && g.out_upd && g.out_ukey ? g.out_ukey + s_base[1] : nullptr;  // each key list optional
     } else {
         sd = g.stage_delta + tile * (u64)C2_STAGE;
         su = g.stage_upd + tile * (u64)C2_STAGE;
@@ -913,7 +913,7 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
         const u64* skd = stage_dkey + t * (u64)tile_items;
         const u64* sku = stage_ukey + t * (u64)tile_items;
         for (u32 r = tid; r < own.x; r += NT) out_dkey[pd + r] = skd[r];
-        if (out_upd)
+        if (out_upd && out_ukey)
             for (u32 r = tid; r < own.y; r += NT) out_ukey[pu + r] = sku[r];
     }
 }
@@ -1465,12 +1465,7 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
         const char* e = getenv("KD_J2R");
         return e && atoi(e) == 1;
     }();
-    static int j2r_occ = 0;
-    if (j2r && j2r_occ <= 0) {
-        int nb = 0;
-        KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_join2r<C2_NT, C2_IPT>, C2_NT, 0));
-        j2r_occ = nb > 0 ? nb : 1;
-    }
+    const int j2r_occ = j2r ? occupancy(ctx, (const void*)k_join2r<C2_NT, C2_IPT>, C2_NT, 0) : 1;
     g.ordA = nA && ordA ? ordA : (const u32*)dz;
     g.ordB = nB && ordB ? ordB : (const u32*)dz;
     g.stage_delta = (uint2*)sdel; g.stage_upd = (uint2*)supd;

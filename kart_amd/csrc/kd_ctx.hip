@@ -278,6 +278,20 @@ static inline u64 fnv1a64(const u8* p, u64 n) {
 
 using namespace kd;
 
+namespace kd {
+int occupancy(kd_ctx* ctx, const void* kernel, int block, size_t lds) {
+    const auto key = std::make_pair(kernel, lds);
+    auto it = ctx->occ.find(key);
+    if (it != ctx->occ.end()) return it->second;
+    int nb = 0;
+    if (hipSetDevice(ctx->device) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, lds) != hipSuccess || nb <= 0)
+        nb = 1;
+    ctx->occ[key] = nb;
+    return nb;
+}
+}  // namespace kd
+
 extern "C" {
 
 int kd_abi_version(void) { return KD_ABI_VERSION; }
@@ -351,6 +365,8 @@ int kd_init(int device_ordinal, kd_ctx** out) {
         c->slab_used = (size_t)8 << 20;  // the join's own workspaces past the scratch above
         (void)diff2_device(c, &A, &A, 0, out, out + 8, (u64*)(c->slab + 768), (u32*)(c->slab + 800));
         c->slab_used = 0;  // (every ensure() piece above is released with the warm-up)
+        for (auto& kv : c->bufs)  // a piece that did not fit the slab came from hipMalloc (hipFree waits for the join)
+            if (!kv.second.slab && kv.second.p) (void)hipFree(kv.second.p);
         c->bufs.clear();
     }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {

@@ -857,13 +857,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
             KD_HIP(hipMemsetAsync(t_cnt, 0, tiles * 4, ctx->stream));
             const void* fn = pf == 2 ? (tr ? (const void*)k_gf_dense<2, true> : (const void*)k_gf_dense<2, false>)
                                      : (tr ? (const void*)k_gf_dense<1, true> : (const void*)k_gf_dense<1, false>);
-            static int occ_dense[4] = {0, 0, 0, 0};
-            int& occ = occ_dense[(pf - 1) * 2 + (tr ? 1 : 0)];
-            if (occ <= 0) {
-                int nb_ = 0;
-                KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_, fn, GF_NT, 0));
-                occ = nb_ > 0 ? nb_ : 1;
-            }
+            const int occ = occupancy(ctx, fn, GF_NT, 0);
             const u64 nchunk = (n + 63) / 64;
             const u64 grid = std::max<u64>(1, std::min<u64>((nchunk + 3) / 4, (u64)ctx->n_cu * (u64)occ));
             if ((rc = launch(ctx, "k_gf_heads", [&] {
@@ -879,12 +873,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
                                })))
                 return rc;
         } else if (g) {
-            static int occ_heads = 0;  // resident k_gf_heads workgroups per CU
-            if (occ_heads <= 0) {
-                int nb_ = 0;
-                KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_, (const void*)k_gf_heads, GF_NT, 0));
-                occ_heads = nb_ > 0 ? nb_ : 1;
-            }
+            const int occ_heads = occupancy(ctx, (const void*)k_gf_heads, GF_NT, 0);  // resident workgroups per CU
             const char* np_ = std::getenv("KD_GF_NOPERSIST");  // (A/B: one block per tile)
             const u64 hgrid = np_ && np_[0] == '1' ? tiles : std::min<u64>(tiles, (u64)ctx->n_cu * (u64)occ_heads);
             if ((rc = launch(ctx, "k_gf_heads", [&] {

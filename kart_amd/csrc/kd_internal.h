@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <utility>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -89,6 +90,8 @@ struct kd_ctx {
     int h_counts_ranks = 0;
     uint64_t gather_send_cap = 0;  // records the last _begin's d_delta holds (base.n + target.n + 1)
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
+    // resident workgroups per CU by (kernel, dynamic LDS): asked once per context (kd::occupancy)
+    std::map<std::pair<const void*, size_t>, int> occ;
     uint32_t rs_epoch = 0;  // kd_sort: epoch of the last pass's look-back words (kd_sort.hip)
     // small workspaces come from one slab (one hipMalloc instead of one per slot on a process's
     // first calls); grown slots take a fresh piece, the slab is freed with the context
@@ -120,6 +123,10 @@ int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes);
 // 256 zero bytes of device memory: what empty inputs point at, and the target of loads issued by
 // masked-off lanes in branch-free load batches (never a host address)
 int device_zeros(kd_ctx* ctx, void** out);
+
+// resident workgroups per CU of `kernel` at `block` threads and `lds` dynamic LDS bytes on the
+// context's device (>= 1), from the occupancy calculator once per context
+int occupancy(kd_ctx* ctx, const void* kernel, int block, size_t lds);
 
 // profiling wrappers around a launch on ctx->stream
 void prof_begin(kd_ctx* ctx, const char* name, hipEvent_t* a);

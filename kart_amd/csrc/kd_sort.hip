@@ -732,17 +732,9 @@ static int rs_epoch(kd_ctx* ctx, u64 status_bytes, SortState& S, u32* ep) {
 
 // resident k_sort_pass workgroups per CU (persistent grid when the count lives on the device)
 template <typename CK, bool FIRST, bool LAST, bool IN64>
-static int rs_occupancy() {
+static int rs_occupancy(kd_ctx* ctx) {
     constexpr int IPT = sizeof(CK) == 4 ? KD_RS_IPT32 : KD_RS_IPT64;
-    static int occ = 0;
-    if (!occ) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_sort_pass<CK, RS_NT, IPT, FIRST, LAST, IN64>,
-                                                         RS_NT, 0) != hipSuccess || nb <= 0)
-            nb = 1;
-        occ = nb;
-    }
-    return occ;
+    return occupancy(ctx, (const void*)k_sort_pass<CK, RS_NT, IPT, FIRST, LAST, IN64>, RS_NT, 0);
 }
 
 template <typename CK, bool FIRST, bool LAST, bool IN64>
@@ -753,7 +745,7 @@ static int rs_launch_pass(kd_ctx* ctx, SortState& S, const void* kin, const u32*
     const u64 ntiles = (ncap + TILE - 1) / TILE;
     // host count: one workgroup per tile; device count: at most the resident workgroups, each
     // taking tiles until the count is covered
-    const u64 grid = dn ? std::min<u64>(ntiles, (u64)ctx->n_cu * rs_occupancy<CK, FIRST, LAST, IN64>()) : ntiles;
+    const u64 grid = dn ? std::min<u64>(ntiles, (u64)ctx->n_cu * rs_occupancy<CK, FIRST, LAST, IN64>(ctx)) : ntiles;
     if (grid == 0) return KD_OK;
     u32 ep;
     int rc = rs_epoch(ctx, ntiles * RS_RD * 8, S, &ep);

@@ -153,6 +153,7 @@ class DatasetVersion:
         self._read_blobs = read_blobs
         self.meta = dict(meta or {})
         self._packed = None
+        self._packed_by = None  # the engine whose buffers a GPU-packed side holds
         self._arenas = []
 
     @property
@@ -165,14 +166,21 @@ class DatasetVersion:
 
     def pack(self, engine=None):
         """the side packed for the join (cached).  With a GPU engine and a large side the sort runs
-        on the GPU (kd_sort_side); the host parses the keys either way."""
+        on the GPU (kd_sort_side); the host parses the keys either way.  A GPU-packed side holds device
+        buffers of the engine that packed it: another engine, or that engine once closed, re-packs."""
+        if self._packed is not None and self._packed.dperm is not None and engine is not None:
+            own = self._packed_by
+            if own is not engine or not getattr(own, "ctx", None):
+                self._packed = None
         if self._packed is None:
+            self._packed_by = None
             if self.n == 0:
                 self._packed = packing.empty_side(self.encoding)
             else:
                 gpu = engine if self.n >= GPU_SORT_MIN and hasattr(engine, "ctx") else None
                 self._packed = packing.pack_side(self.rel_paths, self.oids, self.encoding, rel_off=self.rel_off,
                                                  engine=gpu)
+                self._packed_by = gpu
         return self._packed
 
     # ---- Dataset3 API used by the diff path ----------------------------------------------------

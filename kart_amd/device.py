@@ -73,6 +73,11 @@ class DevSide:
     """A PackedSide's arrays in HBM."""
 
     def __init__(self, engine, side):
+        if getattr(side, "walk_rows", False):
+            # (sorted keys beside walk-order OIDs / filenames: uploaded as one side, each key would be
+            # paired with another entry's OID — such sides join through their order, DevPermSide)
+            raise ValueError("DevSide needs a key-ordered side; a late-materialised side joins through its order "
+                             "(side.materialised() gives the sorted form)")
         self.n = side.n
         self.key_mode = side.key_mode
         self.key = DevBuf.from_numpy(engine, _nonempty(side.key, np.uint64))

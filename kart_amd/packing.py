@@ -169,15 +169,22 @@ def keys_scan(keys, key_mode):
     return info
 
 
-def _gather_names(paths, off, order):
-    """the filename arena with rows in ``order`` (one vectorised gather)"""
+def _gather_names(paths, off, order, chunk=1 << 20):
+    """the filename arena with rows in ``order`` (vectorised gathers, ``chunk`` rows at a time so
+    the byte index stays small)"""
     n = order.shape[0]
     lens = (off[1:] - off[:-1])[order]
     noff = np.zeros(n + 1, np.uint64)
     noff[1:] = np.cumsum(lens)
-    idx = np.arange(int(noff[-1]), dtype=np.int64) + np.repeat(off[:-1][order].astype(np.int64) - noff[:-1].astype(np.int64),
-                                                                lens.astype(np.int64))
-    return (np.ascontiguousarray(paths[idx]) if n else np.zeros(0, np.uint8)), noff
+    out = np.empty(int(noff[-1]), np.uint8)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        ln = lens[a:b].astype(np.int64)
+        base = int(noff[a])
+        idx = np.arange(int(noff[b]) - base, dtype=np.int64) + np.repeat(
+            off[:-1][order[a:b]].astype(np.int64) - (noff[a:b].astype(np.int64) - base), ln)
+        out[base:int(noff[b])] = paths[idx]
+    return out, noff
 
 
 def sort_on_device_perm(engine, keys, oids, info, encoding, paths, off):

@@ -651,122 +651,186 @@ class Merge3Layer:
     ours: packing.PackedSide
     theirs: packing.PackedSide
     n_conflict: int  # libgit2 rule over the generator's plan (o == t -> o; a == o -> t; a == t -> o)
+    plan: dict = None  # the edit mix as generated (counts per kind)
 
 
-def _sha256_prefixes(rows):
-    """the first 3 bytes of sha256 of each 12-byte record"""
-    import hashlib
-
-    return b"".join(hashlib.sha256(rows[i:i + 12]).digest()[:3] for i in range(0, len(rows), 12))
+PK_W = 36  # text pks up to 24 characters, 3 of them up to 4 B: 33 bytes (36 with slack)
+PATH_W = 8 + 52  # 'c/c/c/c/' + the longest filename (4 * ceil((3 + PK_W) / 3))
+_SYNTH = None
 
 
-def _hash_paths(ids):
-    """MsgpackHashPathEncoder paths (dataset3_paths.py:202-215, 4 levels x 64 branches, base64) of the
-    string pks 'R%09d' % id: 'c/c/c/c/' + urlsafe_b64(msgpack([pk])) — 24 bytes each, [n, 24] uint8."""
-    import base64
-    import hashlib
+def _synth_lib():
+    """libkdsynth.so (kart_amd/csrc/kd_synth.cpp): host-only generator helpers, not the product ABI"""
+    global _SYNTH
+    if _SYNTH is None:
+        import ctypes
 
-    ids = np.asarray(ids, np.int64)
+        L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkdsynth.so"))
+        P, U, I, D = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_double
+        L.kds_text_pks.argtypes = [P, U, U, I, I, D, P, I, P, I]
+        L.kds_text_pk_paths.argtypes = [P, P, U, I, P, I, P, I]
+        L.kds_walk_order.argtypes = [P, U, I, P, I]
+        L.kds_gather_paths.argtypes = [P, I, P, P, U, P, P, I]
+        L.kds_gather_paths.restype = None
+        _SYNTH = L
+    return _SYNTH
+
+
+def _threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _p(a):
+    return a.ctypes.data_as(__import__("ctypes").c_void_p)
+
+
+def text_pks(ids, seed=SEED, lmin=12, lmax=24, p_mb=0.05):
+    """The C4 table's text pks: 12–24 characters, 5 % of the rows holding 1–3
+    multibyte UTF-8 characters (2-, 3- and 4-byte).  Characters 0–4 are a bijective base-62
+    scramble of the row id (pks are distinct), the rest seeded filler (kds_text_pks).
+    -> (UTF-8 bytes [n, PK_W] zero-padded, byte lengths [n])"""
+    ids = np.ascontiguousarray(ids, np.int64)
     n = ids.size
-    digits = np.char.zfill(ids.astype("U9"), 9)
-    packed = np.zeros((n, 12), np.uint8)  # 91 aa 'R' + 9 digits  == msgpack(['R%09d'])
-    packed[:, 0], packed[:, 1], packed[:, 2] = 0x91, 0xAA, ord("R")
-    packed[:, 3:] = np.frombuffer("".join(digits.tolist()).encode(), np.uint8).reshape(n, 9)
-    alpha = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_", np.uint8)
-    # filename: urlsafe base64 of 12 bytes = 16 chars, vectorised (4 groups of 3 bytes)
-    g = packed.reshape(n, 4, 3).astype(np.uint32)
-    v = g[:, :, 0] << 16 | g[:, :, 1] << 8 | g[:, :, 2]
-    fn = np.stack([(v >> 18) & 63, (v >> 12) & 63, (v >> 6) & 63, v & 63], 2).reshape(n, 16)
-    out = np.empty((n, 24), np.uint8)
-    out[:, 8:] = alpha[fn]
-    # tree: first 24 bits of sha256(packed) as 4 base64 chars (b64hash, serialise_util.py:82-85)
-    rows = packed.tobytes()
-    if n >= 1 << 21:  # large layers: the digests on a process pool
-        from multiprocessing import Pool
-
-        nproc = max(1, min(16, os.cpu_count() or 1))
-        cuts = np.linspace(0, n, 4 * nproc + 1).astype(np.int64)
-        with Pool(nproc) as pool:
-            parts = pool.map(_sha256_prefixes, [rows[12 * a:12 * b] for a, b in zip(cuts[:-1], cuts[1:])])
-        h = np.frombuffer(b"".join(parts), np.uint8).reshape(n, 3).astype(np.uint32)
-    else:
-        h = np.frombuffer(_sha256_prefixes(rows), np.uint8).reshape(n, 3).astype(np.uint32)
-    hv = h[:, 0] << 16 | h[:, 1] << 8 | h[:, 2]
-    for k in range(4):
-        out[:, 2 * k] = alpha[(hv >> (18 - 6 * k)) & 63]
-        out[:, 2 * k + 1] = ord("/")
-    return out
+    out = np.empty((n, PK_W), np.uint8)
+    nb = np.empty(n, np.int64)
+    if _synth_lib().kds_text_pks(_p(ids), n, seed & (2**64 - 1), lmin, lmax, p_mb, _p(out), PK_W, _p(nb), _threads()):
+        raise ValueError("bad text-pk shape")
+    return out, nb
 
 
-def _pack_fixed(paths, oids, walk=False):
-    """PackedSide (KD_KEY_HASH) of fixed-width relative paths [n, w] + OIDs [n, 20], vectorised:
-    key-sorted, or (``walk``) in git tree order — the paths byte-sorted, as the tree walk lists them,
-    keys ascending only in their bucket bits (kd_sort_segmented_into's input)"""
+def text_pk_paths(pkb, nb):
+    """MsgpackHashPathEncoder paths (kart/dataset3_paths.py:202-215) of text pks given as UTF-8
+    bytes: packed = msgpack([pk]) (fixstr up to 31 B, else str8; serialise_util.py:34-41), tree =
+    the first 24 bits of sha256(packed) as 4 base64 chars (b64hash, serialise_util.py:82-85), one
+    per level, filename = urlsafe_b64(packed) with '=' padding (:64-66); kds_text_pk_paths.
+    -> (paths [n, PATH_W] zero-padded, path lengths [n])"""
+    pkb = np.ascontiguousarray(pkb, np.uint8)
+    nb = np.ascontiguousarray(nb, np.int64)
+    n = pkb.shape[0]
+    paths = np.empty((n, PATH_W), np.uint8)
+    plen = np.empty(n, np.int64)
+    if _synth_lib().kds_text_pk_paths(_p(pkb), _p(nb), n, pkb.shape[1], _p(paths), PATH_W, _p(plen), _threads()):
+        raise ValueError("a text pk's path does not fit")
+    return paths, plen
+
+
+def _hash_keys(paths, plen):
+    """KD_KEY_HASH join keys of padded paths (kd_pack_hash_keys over the packed arena)"""
     from . import _native as N
 
-    n, w = paths.shape
-    flat = np.ascontiguousarray(paths).reshape(-1)
-    off = np.arange(n + 1, dtype=np.uint64) * np.uint64(w)
+    n = paths.shape[0]
+    arena, off = _arena(paths, plen, np.arange(n, dtype=np.int64))
     keys = np.empty(n, np.uint64)
     status = np.empty(n, np.uint8)
-    bad = N.lib().kd_pack_hash_keys(N.ptr(flat), N.ptr(off), n, 4, 0, N.ptr(keys), N.ptr(status))
+    bad = N.lib().kd_pack_hash_keys(N.ptr(arena), N.ptr(off), n, 4, 0, N.ptr(keys), N.ptr(status))
     if bad:
         raise packing.PackError(f"{bad} synthetic paths not packable")
-    sk = np.sort(keys)
-    if n > 1 and not np.all(sk[1:] > sk[:-1]):
-        raise packing.PackError("synthetic key collision")
-    if walk:
-        assert w % 8 == 0
-        cols = np.ascontiguousarray(paths).view(">u8").reshape(n, w // 8)
-        order = np.lexsort(tuple(cols[:, c] for c in range(w // 8 - 1, -1, -1)))
-    else:
-        order = np.argsort(keys)  # (keys are distinct: any sort is stable)
-    keys = keys[order]
-    s = packing.PackedSide(key=np.ascontiguousarray(keys), oid=np.ascontiguousarray(oids[order]),
-                           key_mode=N.KD_KEY_HASH, order=order.astype(np.int64), encoding=packing.GENERAL_ENCODING)
-    s.name = np.ascontiguousarray(paths[order]).reshape(-1)
-    s.name_off = off
+    return keys
+
+
+def _arena(paths, plen, rows):
+    """the name arena (rows' paths back to back) + offsets [len(rows)+1] (kds_gather_paths)"""
+    rows = np.ascontiguousarray(rows, np.int64)
+    m = rows.shape[0]
+    off = np.zeros(m + 1, np.uint64)
+    np.cumsum(plen[rows], out=off[1:])
+    arena = np.empty(int(off[-1]), np.uint8)
+    _synth_lib().kds_gather_paths(_p(paths), paths.shape[1], _p(plen), _p(rows), m, _p(off), _p(arena), _threads())
+    return arena, off
+
+
+def _walk_order(paths):
+    """git tree order of the padded paths 'c/c/c/c/<filename>': the four one-character tree
+    levels, then the filename bytes, a shorter name that is a prefix of another first
+    (kds_walk_order: counting sort on the trees, memcmp inside each leaf tree)"""
+    n = paths.shape[0]
+    order = np.empty(n, np.int64)
+    if _synth_lib().kds_walk_order(_p(np.ascontiguousarray(paths)), n, paths.shape[1], _p(order), _threads()):
+        raise packing.PackError("two synthetic paths are equal")
+    return order
+
+
+def _side(keys, paths, plen, oid_of, rows_mask, order):
+    """PackedSide of the rows of ``rows_mask``, in ``order`` (walk order or key order)"""
+    from . import _native as N
+
+    rows = order[rows_mask[order]]
+    s = packing.PackedSide(key=np.ascontiguousarray(keys[rows]), oid=np.ascontiguousarray(oid_of(rows)),
+                           key_mode=N.KD_KEY_HASH, order=rows.astype(np.int64), encoding=packing.GENERAL_ENCODING)
+    s.name, s.name_off = _arena(paths, plen, rows)
     return s
 
 
-def table3_layers(n, seed=SEED, p_mod=0.02, p_del=0.005, p_ins=0.005, p_same=0.001, p_addadd=0.0005, walk=False):
-    """Ancestor of n string-PK rows and two independently edited descendants.  Per ancestor row each
-    side keeps / modifies / deletes it; a fraction is modified identically on both (clean); both
-    sides insert new rows, some with the same pk on both (add/add, half identical).  ``walk``: the
-    sides in git tree order (as the walk lists them) instead of key order."""
+def table3_layers(n, seed=SEED, p_mod=0.05, p_del=0.005, p_ins=0.005, p_conflict=0.005, p_same=0.005,
+                  p_addadd=0.0005, walk=False, pks=None):
+    """C4 as SURVEY §8(d) states it: an ancestor of n text-pk rows (12–24 characters, 5 % with
+    multibyte UTF-8; MsgpackHashPathEncoder paths, kart/dataset3_paths.py:202-215) and two
+    descendants edited from independent seeds — each side updates 5 %, deletes 0.5 % and inserts
+    0.5 % new rows — plus 0.5 % of the rows edited differently on both sides (conflicts), 0.5 %
+    edited identically on both (clean), and 0.05 % new pks added on both sides (add/add, half with
+    the same content).  ``walk``: the sides in git tree order (as the tree walk lists them) instead
+    of key order.  ``pks``: override the ancestor's pks (list of str), e.g. the reference's KATs."""
     rng = np.random.default_rng(seed)
-    ids = np.arange(n, dtype=np.int64)
-    act = []  # per side: 0 keep, 1 modify, 2 delete
+    n_ins, n_aa = int(n * p_ins), int(n * p_addadd)
+    total = n + 2 * n_ins + n_aa
+    gid = np.arange(total, dtype=np.int64)
+    pkb, nb = text_pks(gid, seed)
+    if pks is not None:
+        for i, p in enumerate(pks):
+            e = p.encode()
+            if len(e) > PK_W:
+                raise ValueError("pk too long for the generator")
+            pkb[i] = 0
+            pkb[i, :len(e)], nb[i] = np.frombuffer(e, np.uint8), len(e)
+    paths, plen = text_pk_paths(pkb, nb)
+    keys = _hash_keys(paths, plen)
+    sk = np.sort(keys)
+    if total > 1 and not np.all(sk[1:] > sk[:-1]):
+        raise packing.PackError("synthetic key collision")
+    del sk
+    order = _walk_order(paths) if walk else np.argsort(keys)
+
+    # the edit plan over ancestor rows: per side 0 keep, 1 modify, 2 delete (independent draws)
+    act = []
     for _ in range(2):
         u = rng.random(n)
         act.append(np.where(u < p_mod, 1, np.where(u < p_mod + p_del, 2, 0)).astype(np.int8))
-    same = rng.random(n) < p_same  # both modify to the same new content
-    act[0][same] = 1
-    act[1][same] = 1
-    n_ins = int(n * p_ins)
-    n_aa = int(n * p_addadd)
-    ins_o = n + np.arange(n_ins)
-    ins_t = n + n_ins + np.arange(n_ins)
-    aa = n + 2 * n_ins + np.arange(n_aa)  # inserted on both sides
+    u = rng.random(n)
+    planted = u < p_conflict  # modified differently on both sides
+    same = (u >= p_conflict) & (u < p_conflict + p_same)  # modified identically on both sides
+    for k in range(2):
+        act[k][planted | same] = 1
+    ver = np.zeros((2, total), np.uint64)  # content version per side; 0 = the ancestor's
+    ver[0, :n] = np.where(act[0] == 1, 1, 0)
+    ver[1, :n] = np.where(act[1] == 1, 2, 0)
+    ver[:, :n][:, same] = 3
+    ins_o = np.arange(n, n + n_ins)
+    ins_t = np.arange(n + n_ins, n + 2 * n_ins)
+    aa = np.arange(n + 2 * n_ins, total)
     aa_same = rng.random(n_aa) < 0.5
-    paths_all = _hash_paths(np.concatenate([ids, ins_o, ins_t, aa]))
-    P = lambda x: paths_all[x]  # ids are 0..total-1 in that order
-    anc = _pack_fixed(P(ids), synth_oids(ids, 0), walk)
+    ver[0, ins_o], ver[1, ins_t] = 1, 2
+    ver[0, aa] = np.where(aa_same, 3, 1)
+    ver[1, aa] = np.where(aa_same, 3, 2)
 
-    def side(k, ins, ver):
-        keep = act[k] != 2
-        v = np.where(act[k] == 1, ver, 0).astype(np.uint64)
-        v[same] = 3
-        rows = ids[keep]
-        oid = synth_oids(rows, v[keep])
-        aav = np.where(aa_same, 3, ver).astype(np.uint64)
-        sel = np.concatenate([rows, ins, aa])
-        oids = np.concatenate([oid, synth_oids(ins, ver), synth_oids(aa, aav)])
-        return _pack_fixed(P(sel), oids, walk)
-
-    ours = side(0, ins_o, 1)
-    theirs = side(1, ins_t, 2)
+    mem_a = gid < n
+    mem_o = np.zeros(total, bool)
+    mem_o[:n] = act[0] != 2
+    mem_o[ins_o] = mem_o[aa] = True
+    mem_t = np.zeros(total, bool)
+    mem_t[:n] = act[1] != 2
+    mem_t[ins_t] = mem_t[aa] = True
+    anc = _side(keys, paths, plen, lambda r: synth_oids(r, 0), mem_a, order)
+    ours = _side(keys, paths, plen, lambda r: synth_oids(r, ver[0, r]), mem_o, order)
+    theirs = _side(keys, paths, plen, lambda r: synth_oids(r, ver[1, r]), mem_t, order)
     a0, a1 = act
     conflict_rows = ((a0 == 1) & (a1 == 1) & ~same) | ((a0 == 1) & (a1 == 2)) | ((a0 == 2) & (a1 == 1))
     n_conflict = int(conflict_rows.sum()) + int((~aa_same).sum())
-    return Merge3Layer(anc, ours, theirs, n_conflict)
+    plan = {"rows": n, "pk_chars": "12-24", "pk_multibyte_rows": int(np.count_nonzero((pkb[:n] >= 0x80).any(axis=1))),
+            "ours_updates": int(np.count_nonzero(a0 == 1)), "ours_deletes": int(np.count_nonzero(a0 == 2)),
+            "theirs_updates": int(np.count_nonzero(a1 == 1)), "theirs_deletes": int(np.count_nonzero(a1 == 2)),
+            "inserts_each": n_ins, "add_add": n_aa, "planted_conflicts": int(planted.sum()),
+            "identical_edits": int(same.sum()), "conflicts": n_conflict}
+    lens = plen[:n]
+    plan["path_bytes_min_mean_max"] = [int(lens.min()) if n else 0, round(float(lens.mean()), 2) if n else 0,
+                                       int(lens.max()) if n else 0]
+    return Merge3Layer(anc, ours, theirs, n_conflict, plan)

@@ -893,3 +893,30 @@ int64_t kdo_geom_filter(uint64_t n, const uint8_t* od, const uint64_t* ooff, con
     }
     return kept;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* writer formatting: gpkg_geom_to_hex_wkb over a geometry arena                               */
+/* ------------------------------------------------------------------------------------------ */
+
+/* kart/geometry.py:346-375 (gpkg_geom_to_hex_wkb) + :227-252 (header, envelope sizes): the WKB
+ * after the GPKG header and envelope, as uppercase hex.  For blob i, status[i] = 0 with its hex at
+ * hex[2 * (off[i] + start)] (start = 8 + envelope size, the layout kd_hex_encode writes), 1 for a
+ * null (empty) value, 3 where the reference goes through OGR (big-endian WKB) or raises (invalid
+ * GPKG, extended bit, unknown envelope, empty WKB). */
+void kdo_hex_wkb_batch(uint64_t n, const uint8_t* data, const uint64_t* off, uint8_t* hex, uint8_t* status) {
+    static const int env_size[8] = {0, 32, 48, 48, 64, -1, -1, -1};
+    static const char digits[] = "0123456789ABCDEF";
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* g = data + off[i];
+        const uint64_t len = off[i + 1] - off[i];
+        if (len == 0) { status[i] = 1; continue; }
+        if (len < 8 || g[0] != 'G' || g[1] != 'P' || g[2] != 0 || (g[3] & 0x20)) { status[i] = 3; continue; }
+        const int es = env_size[(g[3] >> 1) & 7];
+        if (es < 0 || len <= (uint64_t)(8 + es) || g[8 + es] == 0) { status[i] = 3; continue; }
+        for (uint64_t p = off[i] + 8 + es; p < off[i + 1]; p++) {
+            hex[2 * p] = (uint8_t)digits[data[p] >> 4];
+            hex[2 * p + 1] = (uint8_t)digits[data[p] & 15];
+        }
+        status[i] = 0;
+    }
+}

@@ -75,6 +75,8 @@ def C():
         L.kdo_decode_int_filename.argtypes = [_vp, ctypes.c_int, _vp, _vp]
         L.kdo_hash_path_key.restype = ctypes.c_int
         L.kdo_hash_path_key.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]
+        L.kdo_hex_wkb_batch.restype = None
+        L.kdo_hex_wkb_batch.argtypes = [ctypes.c_uint64, _vp, _vp, _vp, _vp]
         _lib = L
     return _lib
 
@@ -362,3 +364,16 @@ def hex_wkb(gpkg):
     if len(wkb) == 0 or wkb[0] == 0:
         return "fallback"
     return wkb.hex().upper()
+
+
+def hex_wkb_batch(data, off):
+    """kdo_hex_wkb_batch: (hex buffer [2 * off[-1]] with blob i's WKB hex at 2 * (off[i] + start),
+    status [n]: 0 ok, 1 null, 3 fallback).  ``off`` may start past 0 (a shard of an arena)."""
+    n = off.shape[0] - 1
+    base = int(off[0]) if n >= 0 else 0
+    loc = np.ascontiguousarray(off - np.uint64(base), np.uint64)
+    seg = np.ascontiguousarray(data[base:int(off[-1])]) if n > 0 else np.zeros(1, np.uint8)
+    hexb = np.zeros(max(1, 2 * int(loc[-1])), np.uint8)
+    status = np.zeros(max(1, n), np.uint8)
+    C().kdo_hex_wkb_batch(n, _p(seg if seg.size else np.zeros(1, np.uint8)), _p(loc), _p(hexb), _p(status))
+    return hexb[:2 * int(loc[-1])], status[:n]

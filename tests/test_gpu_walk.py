@@ -179,3 +179,33 @@ def test_gpu_diff2_ex_record_keys(engine, n, flags):
         want = np.where(r[:, 0] != 0xFFFFFFFF, L.base.key[np.minimum(r[:, 0], L.base.n - 1)],
                         L.target.key[np.minimum(r[:, 1], L.target.n - 1)])
         assert np.array_equal(k, want)
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+def test_gpu_diff2_ex_delta_keys_only(engine, flags):
+    """each key list is optional on its own: delta keys with the update list but no update
+    keys writes the delta keys and leaves the update list correct (no store through the NULL list)"""
+    from kart_amd import synth
+    from kart_amd.device import DevBuf, DevSide
+
+    L = synth.points_layer(300_000, seed=32)
+    A, B = DevSide(engine, L.base), DevSide(engine, L.target)
+    sa, sb = A.kd_side(), B.kd_side()
+    cap = L.base.n + L.target.n + 1
+    d, u, dk, c = (DevBuf(engine, 8 * cap) for _ in range(4))
+    c.zero()
+    N.check(engine.L.kd_diff2_device_ex(engine.ctx, ctypes.byref(sa), ctypes.byref(sb), None, None, flags, d.ptr, u.ptr,
+                                        dk.ptr, None, c.ptr, c.ptr + 32), "kd_diff2_device_ex")
+    cnt = c.download(np.uint64, 8)
+    assert cnt[4] == 0
+    nd, nu = int(cnt[3]), int(cnt[1])
+    od, oc = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
+    r = d.download(np.uint32, 2 * nd).reshape(nd, 2)
+    ru = u.download(np.uint32, 2 * nu).reshape(nu, 2)
+    key = lambda x: sorted(map(tuple, x.tolist()))
+    assert key(r) == key(od) and nu == oc["updates"]
+    k = dk.download(np.uint64, nd)
+    want = np.where(r[:, 0] != 0xFFFFFFFF, L.base.key[np.minimum(r[:, 0], L.base.n - 1)],
+                    L.target.key[np.minimum(r[:, 1], L.target.n - 1)])
+    assert np.array_equal(k, want)
+    assert set(map(tuple, ru.tolist())) <= set(map(tuple, r.tolist()))

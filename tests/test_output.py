@@ -91,6 +91,27 @@ def test_oracle_hexwkb_edges():
     assert O.hex_wkb(b"GP\x00\x01\x00\x00\x00\x00") == "fallback"
 
 
+def test_oracle_hex_batch_equals_per_value():
+    """the C batch restatement (bench.py's all-cores C6 baseline) equals oracle.hex_wkb per value"""
+    geoms = [g for g, _ in _golden_geoms()] + _mixed_geoms(np.random.default_rng(9), 3000)
+    lens = np.array([0 if g is None else len(g) for g in geoms], np.uint64)
+    off = np.zeros(len(geoms) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = np.frombuffer(b"".join(g or b"" for g in geoms), np.uint8)
+    for a, b in ((0, len(geoms)), (5, 1234)):  # the whole arena, and a shard starting past 0
+        hexb, st = O.hex_wkb_batch(data, off[a:b + 1])
+        for i in range(a, b):
+            want = O.hex_wkb(geoms[i])
+            code = int(st[i - a])
+            if want is None:
+                assert code == 1
+            elif want == "fallback":
+                assert code == 3
+            else:
+                lo = 2 * (int(off[i + 1] - off[a])) - len(want)
+                assert code == 0 and hexb[lo:2 * int(off[i + 1] - off[a])].tobytes().decode() == want
+
+
 # ---------------------------------------------------------------- GPU: kd_hex_encode
 @pytest.mark.gpu
 def test_gpu_hexwkb_golden(engine):
