@@ -80,12 +80,13 @@ def parse():
     ap.add_argument("--arena", action="store_true",
                     help="c5: filter from the blob arenas (kd_geom_filter) instead of the geometry heads")
     ap.add_argument("--per-entry", action="store_true",
-                    help="c5: the heads kernel straight on the per-entry heads (no delta-order gather)")
+                    help="c5: the heads kernel straight on the per-entry heads (pair-indexed k_gf_heads)")
+    ap.add_argument("--gh-gather", action="store_true",
+                    help="c5: gather the per-entry heads into delta order on the device inside every step "
+                         "(k_gh_gather) instead of the blob reader's delta-order heads")
     ap.add_argument("--c3-layer", action="store_true",
                     help="c5: the C3 polygon layer instead of SURVEY's C5 mix (points, straddles, wide, EMPTY, edge)")
     ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
-    ap.add_argument("--no-delta-order", action="store_true",
-                    help="c5: skip timing the heads kernel on the drop-in's delta-order layout")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/r04/traffic_<wl>.json, else profiles/traffic_<wl>.json)")
     ap.add_argument("--no-heads-path", action="store_true", help="c5env: skip the indexer's heads-path timing")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
@@ -93,17 +94,15 @@ def parse():
     ap.add_argument("--time-all", action="store_true",
                     help="HIP events around every kernel of a step (default: only the dominant kernel, "
                          "so the events do not inflate the step time)")
-    ap.add_argument("--ab", default="",
-                    help="c5 A/B: comma-separated VAR=value library switches (read per call), each timed after the "
-                         "main run in the same process on the same layer")
     a = ap.parse_args()
     if not a.n:
         a.n = {"c2": 10_000_000, "c3": 100_000_000, "c3v": 100_000_000, "c4": 50_000_000, "c5": 100_000_000, "c5env": 20_000_000,
                "c6": 20_000_000}[a.workload]
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", "r04", f"traffic_{a.workload}.json")  # this round's PMC passes
-        if not os.path.exists(a.traffic_json):
-            a.traffic_json = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
+        for d in ("r05", "r04", ""):  # the newest PMC passes of the workload
+            a.traffic_json = os.path.join(ROOT, "profiles", d, f"traffic_{a.workload}.json")
+            if os.path.exists(a.traffic_json):
+                break
     return a
 
 
@@ -743,7 +742,7 @@ def run_c5(args, H):
     eng = engine_for(H)
     heads = not args.arena
     pipe = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits,
-                          heads=heads, delta_order=heads and not args.per_entry)
+                          heads=heads, delta_order=heads and not args.per_entry, gather=args.gh_gather)
     for _ in range(max(1, args.warmup)):
         pipe.step()
     eng.sync()
@@ -783,7 +782,7 @@ def run_c5(args, H):
         # algorithmic bytes per k_gf_heads launch: the delta pairs (8 B), one 48-B head per present
         # side, codes (2 B) + index envelope (bits/2 + 1 B) written per delta
         alg = 8 * nd + 48 * pres + nd * (2 + bits // 2 + 1)
-        if pipe.delta_order and "k_gh_gather" in parts:  # the gather: pairs read, heads read + written, pairs written
+        if pipe.gather and "k_gh_gather" in parts:  # the gather: pairs read, heads read + written, pairs written
             galg = 8 * nd + 96 * pres + 8 * nd
             gms = parts["k_gh_gather"][1]
             gather = {"what": "k_gh_gather: the deltas' 48-B heads copied into delta order (one per present side)",
@@ -798,78 +797,6 @@ def run_c5(args, H):
             head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
         alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
     roof = roofline(kern, kname, alg, args.traffic_json, n, "c5" if heads and H.world == 1 else None)
-    ab = None
-    if args.ab:  # library switches read per call (os.environ reaches getenv): same process, same layer
-        ab = {}
-        for spec in args.ab.split(","):
-            var, val = spec.split("=", 1)
-            old_v = os.environ.get(var)
-            os.environ[var] = val
-            for _ in range(max(1, args.warmup)):
-                pipe.step()
-            eng.sync()
-            if not args.no_check:
-                c2, d2, codes2, keep2, enc2, ok2 = pipe.results()
-                assert np.array_equal(codes2, codes) and np.array_equal(keep2, keep) and np.array_equal(enc2, enc) \
-                    and np.array_equal(ok2, enc_ok), f"{spec}: results differ"
-            eng.prof_reset()
-            eng.prof_select([kname])
-            eng.prof_enable(True)
-            el = timed(H, eng, pipe.step, args.steps)
-            eng.prof_enable(False)
-            kk = kernel_times(eng, (kname,))
-            ab[spec] = {"ms_per_step": round(el / args.steps * 1e3, 4),
-                        "kernel_ms": round(kk[kname][1], 5) if kname in kk else None}
-            if old_v is None:
-                del os.environ[var]
-            else:
-                os.environ[var] = old_v
-        log(f"[rank {H.rank}] A/B: {ab}")
-    delta_order = None
-    if heads and H.world == 1 and not args.no_delta_order and not pipe.delta_order:
-        # (--per-entry steps only: the delta-order step already times this layout) the drop-in's layout: the blob reader reads the deltas' blobs after classification, so the
-        # heads lie in delta order (spatial.filtered_ds_feature_deltas); kd_geom_filter_heads alone on
-        # that layout, over the same deltas
-        import ctypes
-
-        from kart_amd import _native as N
-        from kart_amd.device import DevBuf
-        hs, pc = [], np.full(delta.shape, 0xFFFFFFFF, np.uint32)
-        for s_ in range(2):  # a head depends on its blob only: the per-entry heads, gathered into delta order
-            col = delta[:, s_]
-            pres = np.nonzero(col != 0xFFFFFFFF)[0]
-            hs.append(np.ascontiguousarray(pipe.heads_host[s_][col[pres].astype(np.int64)]))
-            pc[pres, s_] = np.arange(pres.size, dtype=np.uint32)
-        dh = [DevBuf.from_numpy(eng, h.view(np.uint8).reshape(-1)) for h in hs]
-        dp = DevBuf.from_numpy(eng, pc.reshape(-1))
-        m2, kp, nk = DevBuf(eng, 2 * nd + 2), DevBuf(eng, 4 * nd + 4), DevBuf(eng, 8)
-        e2, ok2 = DevBuf(eng, nd * (bits // 2) + 4), DevBuf(eng, nd + 4)
-        fe = (ctypes.c_double * 4)(*[float(x) for x in synth.C5_FILTER])
-
-        def filt():
-            N.check(eng.L.kd_geom_filter_heads(eng.ctx, dh[0].ptr, hs[0].size, dh[1].ptr, hs[1].size, N.KD_MEM_DEVICE,
-                                               None, None, dp.ptr, nd, None, N.KD_MEM_DEVICE, fe, 0, bits, m2.ptr,
-                                               kp.ptr, ctypes.cast(nk.ptr, N.c_u64p), e2.ptr, ok2.ptr, N.KD_MEM_DEVICE),
-                    "kd_geom_filter_heads")
-
-        filt()
-        eng.sync()
-        if not args.no_check:
-            m2h = m2.download(np.uint8, 2 * nd).reshape(nd, 2)  # (3 = the blob fallback, not run here)
-            assert np.array_equal(np.where(m2h == 3, codes, m2h), codes), "delta-order heads differ"
-        eng.prof_reset()
-        eng.prof_select(["k_gf_heads"])
-        eng.prof_enable(True)
-        el_d = timed(H, eng, filt, args.steps)
-        eng.prof_enable(False)
-        kd = kernel_times(eng, ("k_gf_heads",))
-        alg_d = 8 * nd + 48 * (hs[0].size + hs[1].size) + nd * (2 + bits // 2 + 1)
-        delta_order = {"what": "kd_geom_filter_heads alone over the same deltas with the heads in delta order (the "
-                               "drop-in's layout: the blob reader reads the deltas' blobs after classification)",
-                       "ms_per_call": round(el_d / args.steps * 1e3, 4),
-                       "roofline": roofline(kd, "k_gf_heads", alg_d, "", -1)}
-        for b in dh + [dp, m2, kp, nk, e2, ok2]:
-            b.free()
     arena_path = None
     if heads and not args.no_arena_timing:  # the same step through kd_geom_filter (blob arenas, msgpack walk)
         pa = FilterPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, cols, synth.C5_FILTER, False, bits)
@@ -901,9 +828,11 @@ def run_c5(args, H):
         "config": {"workload": f"C5: spatially filtered diff of ONE {n}-feature polygon layer"
                                f"{f' split into {H.world} bucket-range shards' if H.world > 1 else ''}: classify2 + "
                                "per-delta geometry envelope filter + EnvelopeEncoder of the new side" +
-                               ((" (from the 48-B geometry heads the blob reader extracts on the host: kd_geom_heads; "
-                                 "gathered into delta order on the device, blob fallback in the step)" if pipe.delta_order
-                                 else " (from the 48-B per-entry geometry heads)")
+                               ((" (from the 48-B geometry heads the blob reader extracts on the host, kd_geom_heads, "
+                                 "in delta order as the reader leaves them after classification; blob fallback through "
+                                 "the step's delta pairs)" if pipe.delta_order and not pipe.gather else
+                                 " (from the 48-B per-entry geometry heads, gathered into delta order on the device in "
+                                 "the step)" if pipe.gather else " (from the 48-B per-entry geometry heads)")
                                 if heads else " (msgpack walk of the blob arenas on the GPU)"),
                    "features": n, "pairs_per_step": total_pairs, "deltas_per_step": sum(H.allgather(nd)),
                    "kept_per_step": sum(H.allgather(counts["kept"])), "bits": bits, "filter": list(synth.C5_FILTER),
@@ -916,12 +845,12 @@ def run_c5(args, H):
         blobs = int(np.count_nonzero(np.diff(L.base_blobs[1])) + np.count_nonzero(np.diff(L.target_blobs[1])))
         out["host"] = {"geom_heads_s": round(pipe.heads_s, 4), "blobs": blobs,
                        "geom_heads_M_blobs_per_s": round(blobs / pipe.heads_s / 1e6, 2),
+                       "delta_heads_s": round(pipe.delta_heads_s, 4) if pipe.delta_heads_s is not None else None,
                        "note": "kd_geom_heads: the blob reader's host pass (msgpack walk of every materialised blob, "
-                               f"{host_cores()} threads) that leaves 48 B per blob for the GPU; outside the timed step"}
+                               f"{host_cores()} threads) that leaves 48 B per blob for the GPU; delta_heads_s: those "
+                               "heads laid out in delta order (the reader reads the deltas' blobs after "
+                               "classification); both outside the timed step, per pass over the layer"}
         out["arena_path"] = arena_path
-        out["heads_delta_order"] = delta_order
-    if ab:
-        out["ab"] = ab
     return out
 
 
@@ -1039,10 +968,10 @@ def run_c5env(args, H):
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         O = oracle()
-        parts = 4 * host_cores()
-        cut = np.linspace(0, n, parts + 1).astype(np.int64)
+        nsh = 4 * host_cores()
+        cut = np.linspace(0, n, nsh + 1).astype(np.int64)
         h_enc = enc.download(np.uint8, n * nb).reshape(n, nb)
-        got = [None] * parts
+        got = [None] * nsh
 
         def work(s):
             a, b = int(cut[s]), int(cut[s + 1])
@@ -1050,14 +979,14 @@ def run_c5env(args, H):
             got[s] = O.envelope_batch(data[o0:int(off[b])], off[a:b + 1] - np.uint64(o0), synth.C5_FILTER, bits)
             return b - a
 
-        res = cpu_sharded(work, parts, min(args.cpu_seconds, 10.0))
+        res = cpu_sharded(work, nsh, min(args.cpu_seconds, 10.0))
         if not args.no_check:  # the baseline's last run doubles as a bit-exact check of the whole layer
             assert np.array_equal(h_match, np.concatenate([g[0] for g in got])), "k_envelopes flags differ from the oracle"
             assert np.array_equal(h_ok, np.concatenate([g[2] for g in got])), "k_envelopes enc_ok differs from the oracle"
             assert np.array_equal(h_enc, np.concatenate([g[1] for g in got])), "EnvelopeEncoder bytes differ"
         del got, h_enc
         cpu = cpu_line(res, "M geometries/s", "oracle/kd_oracle.c envelope batch (bbox test + index envelope + "
-                                              f"EnvelopeEncoder) over {parts} geometry ranges", f"layer ({n} geometries)")
+                                              f"EnvelopeEncoder) over {nsh} geometry ranges", f"layer ({n} geometries)")
     eng.close()
     return {
         "metric": METRIC, "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "M geometries/s",
@@ -1189,8 +1118,8 @@ def run_c6(args, H):
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         m = min(n, 200_000)
         blobs = [data[int(off[i]):int(off[i + 1])].tobytes() for i in range(m)]
-        parts = 4 * host_cores()
-        cut = np.linspace(0, n, parts + 1).astype(np.int64)
+        nsh = 4 * host_cores()
+        cut = np.linspace(0, n, nsh + 1).astype(np.int64)
         first = {}
 
         def work(s):
@@ -1200,7 +1129,7 @@ def run_c6(args, H):
                 first["hex"], first["st"] = hx, st
             return b - a
 
-        res = cpu_sharded(work, parts, min(args.cpu_seconds, 10.0))
+        res = cpu_sharded(work, nsh, min(args.cpu_seconds, 10.0))
         if not args.no_check:  # shard 0 of the C restatement equals the kernel's hex bytes
             b0 = int(cut[1])
             st0 = start.download(np.uint32, b0)
@@ -1211,7 +1140,7 @@ def run_c6(args, H):
                 if not np.array_equal(gh[a:e], first["hex"][a:e]):
                     raise AssertionError(f"hex of geometry {i} differs from the C restatement")
         cpu = cpu_line(res, "M geometries/s", "oracle/kd_oracle.c kdo_hex_wkb_batch (gpkg_geom_to_hex_wkb "
-                                              f"restated: slice + uppercase hex) over {parts} geometry ranges",
+                                              f"restated: slice + uppercase hex) over {nsh} geometry ranges",
                        f"layer ({n} geometries)")
         # the drop-in as Kart would call it: host values in, Python strs out (arena join, H2D, kernel,
         # D2H, one decode + numpy-bounded slicing), against a per-value binascii.hexlify loop
@@ -1346,18 +1275,18 @@ def run_c4(args, H):
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         Orc = oracle()
         (kA, oA, _), (kO, oO, _), (kT, oT, _) = srt
-        parts = 4 * host_cores()
+        nsh = 4 * host_cores()
         # bucket-range shards (keys ascend in their bucket bits): cut at ancestor key quantiles
-        ck = kA[np.linspace(0, A.n, parts + 1).astype(np.int64)[1:-1]] if A.n else np.zeros(0, np.uint64)
+        ck = kA[np.linspace(0, A.n, nsh + 1).astype(np.int64)[1:-1]] if A.n else np.zeros(0, np.uint64)
         bnd = [np.concatenate([[0], np.searchsorted(k, ck), [k.shape[0]]]).astype(np.int64) for k in (kA, kO, kT)]
-        got = [None] * parts
+        got = [None] * nsh
 
         def work(s):
             sl = [slice(int(bd[s]), int(bd[s + 1])) for bd in bnd]
             got[s] = Orc.classify3(kA[sl[0]], oA[sl[0]], kO[sl[1]], oO[sl[1]], kT[sl[2]], oT[sl[2]])
             return sum(x.stop - x.start for x in sl)
 
-        res = cpu_sharded(work, parts, min(args.cpu_seconds, 10.0))
+        res = cpu_sharded(work, nsh, min(args.cpu_seconds, 10.0))
         if not args.no_check:  # the baseline's last run, re-based to whole-side indices, is a bit-exact check
             NONE = np.uint32(0xFFFFFFFF)
 
@@ -1368,13 +1297,13 @@ def run_c4(args, H):
                     rows[m, c] += np.uint32(bnd[side][s])
                 return rows
 
-            oc = np.concatenate([rebase(got[s][0], s, (0, 1, 2)) for s in range(parts)])
-            om = np.concatenate([rebase(got[s][1], s, (1, 2)) for s in range(parts)])
+            oc = np.concatenate([rebase(got[s][0], s, (0, 1, 2)) for s in range(nsh)])
+            om = np.concatenate([rebase(got[s][1], s, (1, 2)) for s in range(nsh)])
             assert np.array_equal(conf, oc), "classify3 conflicts differ from the oracle"
             assert np.array_equal(md, om), "classify3 merge deltas differ from the oracle"
-            assert n_clean == sum(got[s][2] for s in range(parts))
+            assert n_clean == sum(got[s][2] for s in range(nsh))
         del got
-        cpu = cpu_line(res, "M entries/s", f"oracle/kd_oracle.c classify3 over {parts} bucket-range shards",
+        cpu = cpu_line(res, "M entries/s", f"oracle/kd_oracle.c classify3 over {nsh} bucket-range shards",
                        f"C4 layer ({nall} entries, key-sorted)")
     eng.close()
     return {

@@ -139,6 +139,19 @@ int kd_init(int device_ordinal, kd_ctx** out);
 int kd_fini(kd_ctx* ctx);
 /* Launch on an external HIP stream (e.g. torch's current stream); NULL = the context's own. */
 int kd_set_stream(kd_ctx* ctx, void* hip_stream);
+/* Tuning options of a context (A/B switches of the measured alternatives; defaults are the measured
+ * optima).  kd_init seeds each from the environment variable in brackets, once; kd_set_option changes
+ * it for later calls on the context.  Unknown names: KD_EINVAL.
+ *   merge3_join    [KD_MERGE3_JOIN]    1: one-pass three-way join (k_join3); 0: classify2 + k_resolve3
+ *   merge3_split   [KD_MERGE3_SPLIT]   1: k_join3 stages candidates, k_resolve3 applies the rule
+ *   j3_ol          [KD_J3_OL]          1: k_join3 stages ours'/theirs' OIDs in LDS (sorted-form sides)
+ *   j2_oidlds_min  [KD_J2_OIDLDS_MIN]  k_join2 stages OIDs in LDS from this many entries (2^26)
+ *   j2r            [KD_J2R]            1: the persistent register-prefetched int-key join
+ *   fd_stream      [KD_FD_STREAM]      -1 auto, 0 windowed, 1 streamed field diff (contiguous arenas)
+ *   pkm_max_blocks [KD_PKM_MAX_BLOCKS] largest pk range (64-pk blocks) kd_delta_pk_order places by bitmap
+ *   trace_host     [KD_TRACE_HOST]     1: stream-synced wall-clock marks of host phases to stderr */
+int kd_set_option(kd_ctx* ctx, const char* name, int64_t value);
+int kd_get_option(kd_ctx* ctx, const char* name, int64_t* value);
 int kd_sync(kd_ctx* ctx);
 /* Pre-size device workspaces so the first timed call does not allocate. */
 int kd_reserve(kd_ctx* ctx, uint64_t max_entries_per_side, uint64_t max_updates);
@@ -257,6 +270,12 @@ int kd_sf_index_free(kd_sf_index* index);
  * per delta — classify2's delta list with the arenas indexed by sorted entry.  With d_n the count
  * is read on the device (pairs and outputs device memory, n = capacity).  match must be 2-B aligned. */
 #define KD_GF_RECT 0x1u /* the filter geometry is its own envelope (an axis-aligned rectangle) */
+/* kd_geom_filter_heads / kd_geom_filter_deltas: the heads are already in delta order — heads_old[d] /
+ * heads_new[d] belong to delta d (an absent side's slot is never read), as the drop-in's blob reader
+ * lays them out after classification; pairs then give each side's presence and its blob in the
+ * arenas (the slow path).  n_old and n_new must each cover whole 64-delta chunks of the capacity
+ * (>= ceil(n / 64) * 64; heads device memory in kd_geom_filter_deltas). */
+#define KD_GF_DELTA_HEADS 0x2u
 typedef struct kd_geom_cols {
     int32_t n_leg_old, n_leg_new;
     const uint8_t* leg_old_hex; /* [n_leg_old*40] legend hexhashes (host memory) */
@@ -296,12 +315,12 @@ int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_
                          uint64_t* n_keep, uint8_t* enc, uint8_t* enc_ok, uint32_t out_mem);
 
 /* kd_geom_filter_heads over classify2's delta list on the device (all buffers device memory, the delta
- * count *d_n on the device, cap the list's capacity): the heads of the deltas' old and new blobs are
- * first gathered into delta order (the layout the drop-in's blob reader produces: it reads the
- * deltas' blobs after classification), then filtered from those contiguous heads; a geometry whose
- * head cannot decide it is read from old_blobs / new_blobs at the delta's own blob (the pairs).
- * heads_old [n_old] / heads_new [n_new] are indexed like the arenas (per entry).  Outputs as
- * kd_geom_filter_heads (match [cap * 2], keep [cap], n_keep, enc, enc_ok: device). */
+ * count *d_n on the device, cap the list's capacity): filtered from heads in delta order (the layout
+ * the drop-in's blob reader produces: it reads the deltas' blobs after classification); a geometry
+ * whose head cannot decide it is read from old_blobs / new_blobs at the delta's own blob (the pairs).
+ * With KD_GF_DELTA_HEADS in flags the heads are given in delta order; without it heads_old [n_old] /
+ * heads_new [n_new] are indexed like the arenas (per entry) and first gathered into delta order.
+ * Outputs as kd_geom_filter_heads (match [cap * 2], keep [cap], n_keep, enc, enc_ok: device). */
 int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old, uint64_t n_old, const kd_geom_head* heads_new,
                           uint64_t n_new, const kd_blobs* old_blobs, const kd_blobs* new_blobs, const uint32_t* pairs,
                           uint64_t cap, const uint64_t* d_n, const double filt_env[4], uint32_t flags, int bits,

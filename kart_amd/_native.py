@@ -30,6 +30,7 @@ KD_COPY_D2D = 3
 KD_COMM_ID_BYTES = 128
 KD_GH_GEOM, KD_GH_NULL, KD_GH_FALLBACK = 0, 2, 3
 KD_GF_RECT = 0x1
+KD_GF_DELTA_HEADS = 0x2  # the geometry heads are in delta order (slot d = delta d)
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -154,6 +155,8 @@ SIGNATURES = {
     "kd_init": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "kd_fini": (ctypes.c_int, [ctypes.c_void_p]),
     "kd_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "kd_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),
+    "kd_get_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "kd_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "kd_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "kd_free": (None, [ctypes.c_void_p]),

@@ -400,9 +400,8 @@ static int merge3_device(kd_ctx* ctx, const kd_side& A, const kd_side& O, const 
     int rc;
     const u64 nA = A.n, nO = O.n, nT = T.n;
     // the one-pass join (k_join3) unless the union is empty (then only the ancestor's order check
-    // remains) or KD_MERGE3_JOIN=0 selects the two-step path (classify2 + k_resolve3) for an A/B
-    const char* j3e = getenv("KD_MERGE3_JOIN");
-    if (nO + nT > 0 && !(j3e && atoi(j3e) == 0))
+    // remains) or the merge3_join option selects the two-step path (classify2 + k_resolve3)
+    if (nO + nT > 0 && ctx->opt.merge3_join)
         return merge3_join_device(ctx, A, O, T, d_conf, d_md, counts, derr, pA, pO, pT);
     const u64 nchunk = (nO + nT) / C3_CH + 2;
     void *cand, *c2, *desc, *aux, *dz;

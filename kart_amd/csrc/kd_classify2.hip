@@ -1352,12 +1352,10 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     a.K = kK; a.oidK = (const u8*)P(K.oid, nK); a.nameK = (const u8*)P(K.name, nK);
     a.nameOffK = (const u64*)P(K.name_off, nK); a.ordK = (const u32*)P(ordK, nK); a.nK = nK;
     a.apart = (const u64*)apart; a.stage_conf = (u32*)sconf; a.stage_md = (uint2*)smd;
-    // KD_MERGE3_SPLIT=1: the join stages candidates (a, o, t) and k_resolve3 applies the rule (C4,
-    // r4n: 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
-    const char* se = getenv("KD_MERGE3_SPLIT");
-    const bool split = se && atoi(se) == 1;
-    const char* oe = getenv("KD_J3_OL");  // (A/B: sorted-form sides' OIDs staged with the keys)
-    const bool j3_ol = oe && atoi(oe) == 1;
+    // merge3_split: the join stages candidates (a, o, t) and k_resolve3 applies the rule (C4, r4n:
+    // 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
+    const bool split = ctx->opt.merge3_split == 1;
+    const bool j3_ol = ctx->opt.j3_ol == 1;  // (sorted-form sides' OIDs staged with the keys)
     void *cand3 = nullptr, *c2 = nullptr;
     if (split) {
         if ((rc = ensure(ctx, "c3.cand3", (total + 1) * 12, &cand3))) return rc;
@@ -1452,19 +1450,12 @@ int diff2_device(kd_ctx* ctx, const kd_side* A, const kd_side* B, u32 flags, u32
     g.dummy = (const u8*)dz;
     const bool perm = ordA != nullptr || ordB != nullptr;
     // OIDs staged in LDS from this many entries on (C3's 200M: k_join2 1.28 -> 1.20 ms; C2's 20M:
-    // 0.131 -> 0.136, profiles/r03/join2_oid_lds_ab.jsonl); KD_J2_OIDLDS_MIN overrides (tests)
-    static const u64 oid_lds_min = [] {
-        const char* e = getenv("KD_J2_OIDLDS_MIN");
-        return e ? strtoull(e, nullptr, 10) : (u64)1 << 26;
-    }();
-    const bool oid_lds = nA + nB >= oid_lds_min;
-    // KD_J2R=1: the persistent register-prefetched form of the large int-key join (C3, r4o: k_join2
-    // 1.93 vs 1.18 ms — three resident tiles per CU prefetching hold fewer bytes in flight than five
-    // one-shot tiles; one tile per workgroup stays the default)
-    static const bool j2r = [] {
-        const char* e = getenv("KD_J2R");
-        return e && atoi(e) == 1;
-    }();
+    // 0.131 -> 0.136, profiles/r03/join2_oid_lds_ab.jsonl); the j2_oidlds_min option overrides (tests)
+    const bool oid_lds = nA + nB >= ctx->opt.j2_oidlds_min;
+    // j2r: the persistent register-prefetched form of the large int-key join (C3, r4o: k_join2 1.93 vs
+    // 1.18 ms — three resident tiles per CU prefetching hold fewer bytes in flight than five one-shot
+    // tiles; one tile per workgroup stays the default)
+    const bool j2r = ctx->opt.j2r == 1;
     const int j2r_occ = j2r ? occupancy(ctx, (const void*)k_join2r<C2_NT, C2_IPT>, C2_NT, 0) : 1;
     g.ordA = nA && ordA ? ordA : (const u32*)dz;
     g.ordB = nB && ordB ? ordB : (const u32*)dz;

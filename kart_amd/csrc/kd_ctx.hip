@@ -149,9 +149,8 @@ int stage_d2h(kd_ctx* ctx, void* dst, const void* src, size_t bytes) {
 }
 
 void host_mark(kd_ctx* ctx, const char* name) {
-    static const int on = [] { const char* v = std::getenv("KD_TRACE_HOST"); return v && v[0] == '1'; }();
     static thread_local std::chrono::steady_clock::time_point t0;
-    if (!on) return;
+    if (!ctx->opt.trace_host) return;
     (void)hipStreamSynchronize(ctx->stream);
     const auto t = std::chrono::steady_clock::now();
     if (name) std::fprintf(stderr, "[kd] %-22s %9.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t0).count());
@@ -302,6 +301,51 @@ const char* kd_last_error(void) { return kd::g_err; }
 // first diff a process runs
 __global__ void k_load_probe() {}
 
+// the option table: name, KD_* environment variable (read once by kd_init), field
+namespace {
+struct OptDef {
+    const char* name;
+    const char* env;
+    int64_t kd_opts::*i64;
+    int kd_opts::*i32;
+    uint64_t kd_opts::*u64;
+};
+const OptDef OPTS[] = {
+    {"merge3_join", "KD_MERGE3_JOIN", nullptr, &kd_opts::merge3_join, nullptr},
+    {"merge3_split", "KD_MERGE3_SPLIT", nullptr, &kd_opts::merge3_split, nullptr},
+    {"j3_ol", "KD_J3_OL", nullptr, &kd_opts::j3_ol, nullptr},
+    {"j2_oidlds_min", "KD_J2_OIDLDS_MIN", nullptr, nullptr, &kd_opts::j2_oidlds_min},
+    {"j2r", "KD_J2R", nullptr, &kd_opts::j2r, nullptr},
+    {"fd_stream", "KD_FD_STREAM", nullptr, &kd_opts::fd_stream, nullptr},
+    {"pkm_max_blocks", "KD_PKM_MAX_BLOCKS", nullptr, nullptr, &kd_opts::pkm_max_blocks},
+    {"trace_host", "KD_TRACE_HOST", nullptr, &kd_opts::trace_host, nullptr},
+};
+void opt_set(kd_opts& o, const OptDef& d, int64_t v) {
+    if (d.i32) o.*(d.i32) = (int)v;
+    else if (d.u64) o.*(d.u64) = (uint64_t)v;
+}
+}  // namespace
+
+int kd_set_option(kd_ctx* ctx, const char* name, int64_t value) {
+    KD_CHECK(ctx && name, "kd_set_option: NULL");
+    for (const OptDef& d : OPTS)
+        if (!strcmp(d.name, name)) {
+            opt_set(ctx->opt, d, value);
+            return KD_OK;
+        }
+    KD_CHECK(false, "kd_set_option: unknown option '%s'", name);
+}
+
+int kd_get_option(kd_ctx* ctx, const char* name, int64_t* value) {
+    KD_CHECK(ctx && name && value, "kd_get_option: NULL");
+    for (const OptDef& d : OPTS)
+        if (!strcmp(d.name, name)) {
+            *value = d.i32 ? (int64_t)(ctx->opt.*(d.i32)) : (int64_t)(ctx->opt.*(d.u64));
+            return KD_OK;
+        }
+    KD_CHECK(false, "kd_get_option: unknown option '%s'", name);
+}
+
 int kd_init(int device_ordinal, kd_ctx** out) {
     KD_CHECK(out != nullptr, "kd_init: out is NULL");
     int n = 0;
@@ -310,6 +354,8 @@ int kd_init(int device_ordinal, kd_ctx** out) {
     KD_HIP(hipSetDevice(device_ordinal));
     kd_ctx* c = new kd_ctx();
     c->device = device_ordinal;
+    for (const OptDef& d : OPTS)  // init-time settings: the KD_* environment, read once here
+        if (const char* v = std::getenv(d.env)) opt_set(c->opt, d, strtoll(v, nullptr, 10));
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;

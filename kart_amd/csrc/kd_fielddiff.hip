@@ -1375,10 +1375,9 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     // window shape from the typical blob: small features (points, ~90-150 B) fit a long head window
     // whole; larger ones (polygons) get head + tail windows around their geometry
     const bool small = typ <= 144;
-    // the streamed kernel: contiguous update arenas (no pairs) of larger blobs; KD_FD_STREAM=0/1
-    // forces it off / on (A/B)
-    const char* stream_e = getenv("KD_FD_STREAM");
-    const int stream_env = stream_e ? atoi(stream_e) : -1;
+    // the streamed kernel: contiguous update arenas (no pairs) of larger blobs; the fd_stream option
+    // 0 / 1 forces it off / on
+    const int stream_env = ctx->opt.fd_stream;
     const bool stream = lds_tab && d_pu == nullptr && (stream_env >= 0 ? stream_env > 0 : !small && KD_FD_STREAM_DEFAULT);
     // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
     // calculator for this launch's LDS), capped at the measured optimum.

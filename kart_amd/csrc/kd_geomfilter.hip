@@ -396,7 +396,15 @@ struct GfHeadArgs {
     u32* fb_count;        // k_gf_fb, so the streaming pass never waits on a byte-wise blob decode
     int dense;            // heads indexed by delta (slot d holds delta d's head; the pairs say only
                           // which sides are present): k_gf_dense, no pair -> head dependency
+    int pres_only;        // (dense) the pairs are the deltas' blob rows (bpairs == pairs): a present
+                          // side's head is at slot d
 };
+
+// (dense) the head slots of delta d's sides from its pair
+__device__ __forceinline__ uint2 head_slots(const GfHeadArgs& g, uint2 p, u64 d) {
+    if (!g.pres_only) return p;
+    return make_uint2(p.x == KD_NONE ? KD_NONE : (u32)d, p.y == KD_NONE ? KD_NONE : (u32)d);
+}
 
 struct HeadLd {
     u32x4 v0, v1, v2;
@@ -580,10 +588,16 @@ __device__ __forceinline__ DenseLd dense_load(const GfArgs& a, const GfHeadArgs&
     }
     const u64 dp = n ? (d < n ? d : n - 1) : 0;
     const uint2 v = *(n ? (const uint2*)a.pairs + dp : (const uint2*)g.zeros);
-    L.pr = d < n ? v : make_uint2(KD_NONE, KD_NONE);
+    L.pr = d < n ? head_slots(g, v, d) : make_uint2(KD_NONE, KD_NONE);
     return L;
 }
 
+#ifndef KD_GFD_PF
+#define KD_GFD_PF 1  // k_gf_dense prefetch depth (chunks ahead)
+#endif
+#ifndef KD_GFD_TR
+#define KD_GFD_TR false  // k_gf_dense: heads loaded as lane-contiguous runs, transposed through LDS
+#endif
 #ifndef KD_GFD_WAVES
 #define KD_GFD_WAVES 4  // k_gf_dense<1, false>: waves per SIMD the register budget is cut for
 #endif
@@ -690,7 +704,7 @@ __global__ __launch_bounds__(256) void k_gf_fb(GfArgs a, GfHeadArgs g) {
     const double vmax = (double)((1ull << a.bits) - 1);
     for (u32 x = blockIdx.x * 256 + threadIdx.x; x < cnt; x += gridDim.x * 256) {
         const u64 d = g.fb_list[x];
-        const uint2 pr = ((const uint2*)a.pairs)[d];
+        const uint2 pr = head_slots(g, ((const uint2*)a.pairs)[d], d);
         const HeadLd L0 = load_head(g, 0, pr.x), L1 = load_head(g, 1, pr.y);
         GHit h;
         decode_head(a, g, 0, pr.x, L0, h, d, false);
@@ -838,6 +852,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
     GfHeadArgs gh{};
     if (g) {
         gh = *g;
+        if (gh.pres_only) gh.bpairs = (const uint2*)dp;  // the blob of each side: the pairs themselves
         // with blob arenas, heads that need their blob are deferred to k_gf_fb
         if (gh.data[0] && gh.data[1] && n) {
             void *fl, *fc;
@@ -849,22 +864,14 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
     }
     if (tiles) {
         if (g && gh.dense) {
-            // KD_GFD (A/B): prefetch depth 1 / 2, 's' strided / 't' transposed loads; default "1s"
-            // (r4w on the C5 mix: 1s 0.320, 2s 0.334, 2t 0.338, 1t 0.346 ms; k_gf_heads 0.355)
-            const char* v = std::getenv("KD_GFD");
-            const int pf = v && v[0] == '2' ? 2 : 1;
-            const bool tr = v && v[0] && v[1] == 't';
+            // prefetch depth 1, strided loads (r4w on the C5 mix: 1-deep strided 0.320 ms, 2-deep 0.334,
+            // 2-deep transposed through LDS 0.338, 1-deep transposed 0.346; k_gf_heads 0.355)
             KD_HIP(hipMemsetAsync(t_cnt, 0, tiles * 4, ctx->stream));
-            const void* fn = pf == 2 ? (tr ? (const void*)k_gf_dense<2, true> : (const void*)k_gf_dense<2, false>)
-                                     : (tr ? (const void*)k_gf_dense<1, true> : (const void*)k_gf_dense<1, false>);
-            const int occ = occupancy(ctx, fn, GF_NT, 0);
+            const int occ = occupancy(ctx, (const void*)k_gf_dense<KD_GFD_PF, KD_GFD_TR>, GF_NT, 0);
             const u64 nchunk = (n + 63) / 64;
             const u64 grid = std::max<u64>(1, std::min<u64>((nchunk + 3) / 4, (u64)ctx->n_cu * (u64)occ));
             if ((rc = launch(ctx, "k_gf_heads", [&] {
-                     if (pf == 2 && tr) hipLaunchKernelGGL((k_gf_dense<2, true>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
-                     else if (pf == 2) hipLaunchKernelGGL((k_gf_dense<2, false>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
-                     else if (tr) hipLaunchKernelGGL((k_gf_dense<1, true>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
-                     else hipLaunchKernelGGL((k_gf_dense<1, false>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
+                     hipLaunchKernelGGL((k_gf_dense<KD_GFD_PF, KD_GFD_TR>), dim3((unsigned)grid), dim3(GF_NT), 0, ctx->stream, a, gh);
                  })))
                 return rc;
             if (gh.fb_list && (rc = launch(ctx, "k_gf_fb", [&] {
@@ -874,8 +881,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
                 return rc;
         } else if (g) {
             const int occ_heads = occupancy(ctx, (const void*)k_gf_heads, GF_NT, 0);  // resident workgroups per CU
-            const char* np_ = std::getenv("KD_GF_NOPERSIST");  // (A/B: one block per tile)
-            const u64 hgrid = np_ && np_[0] == '1' ? tiles : std::min<u64>(tiles, (u64)ctx->n_cu * (u64)occ_heads);
+            const u64 hgrid = std::min<u64>(tiles, (u64)ctx->n_cu * (u64)occ_heads);  // (one block per tile: 0.345 vs 0.353 ms, r4v)
             if ((rc = launch(ctx, "k_gf_heads", [&] {
                      hipLaunchKernelGGL(k_gf_heads, dim3((unsigned)hgrid), dim3(GF_NT), 0, ctx->stream, a, gh);
                  })))
@@ -1013,12 +1019,20 @@ extern "C" int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, 
         if ((rc = device_zeros(ctx, &dz))) return rc;  // 256 zero bytes
         g.zeros = (const u8*)dz;
     }
+    const bool dh = (flags & KD_GF_DELTA_HEADS) != 0;
+    if (dh) {  // heads in delta order: slot d is delta d's; the pairs give presence and the blobs
+        const u64 slots = (n + 63) / 64 * 64;
+        KD_CHECK(nh[0] >= slots && nh[1] >= slots, "kd_geom_filter_heads: KD_GF_DELTA_HEADS needs %llu head slots per side",
+                 (unsigned long long)slots);
+        g.dense = 1;
+        g.pres_only = 1;
+    }
     if (old_blobs) {
         const kd_blobs* bl[2] = {old_blobs, new_blobs};
         const char* tag[2][2] = {{"gf.od", "gf.oo"}, {"gf.nd", "gf.no"}};
         for (int s = 0; s < 2; s++) {
             const kd_blobs* B = bl[s];
-            KD_CHECK(B->n == nh[s], "kd_geom_filter_heads: arena %d holds %llu blobs, %llu heads", s,
+            KD_CHECK(dh || B->n == nh[s], "kd_geom_filter_heads: arena %d holds %llu blobs, %llu heads", s,
                      (unsigned long long)B->n, (unsigned long long)nh[s]);
             const void *dd, *doff;
             const u64 bytes = B->mem == KD_MEM_HOST ? (B->n ? B->off[B->n] : 0) : 0;
@@ -1028,8 +1042,8 @@ extern "C" int kd_geom_filter_heads(kd_ctx* ctx, const kd_geom_head* heads_old, 
             g.off[s] = (const u64*)doff;
         }
     }
-    a.nblob[0] = n_old;
-    a.nblob[1] = n_new;
+    a.nblob[0] = dh && old_blobs ? old_blobs->n : n_old;
+    a.nblob[1] = dh && new_blobs ? new_blobs->n : n_new;
     return gf_run(ctx, a, &g, pairs, n, d_n, pairs_mem, filt_env, flags, bits, match, keep, n_keep, enc, enc_ok, out_mem);
 }
 
@@ -1049,29 +1063,42 @@ extern "C" int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old,
     KD_HIP(hipSetDevice(ctx->device));
     static_assert(sizeof(kd_geom_head) == 48, "kd_geom_head is 48 bytes");
     int rc;
-    void *go, *gn, *gp, *dz;
-    const u64 slots = (cap + 63) / 64 * 64 + 1;  // whole 64-delta chunks (k_gf_dense's loads)
-    if ((rc = ensure(ctx, "gd.ho", slots * sizeof(kd_geom_head), &go))) return rc;
-    if ((rc = ensure(ctx, "gd.hn", slots * sizeof(kd_geom_head), &gn))) return rc;
-    if ((rc = ensure(ctx, "gd.pairs", (cap + 1) * 8, &gp))) return rc;
+    void* dz;
     if ((rc = device_zeros(ctx, &dz))) return rc;
-    if (cap) {
-        const unsigned grid = (unsigned)std::max<u64>(1, std::min<u64>((cap + 255) / 256, (u64)ctx->n_cu * 16));
-        rc = launch(ctx, "k_gh_gather", [&] {
-            hipLaunchKernelGGL(k_gh_gather, dim3(grid), dim3(256), 0, ctx->stream, n_old ? heads_old : (const kd_geom_head*)dz,
-                               n_old, n_new ? heads_new : (const kd_geom_head*)dz, n_new, (const uint2*)pairs, cap, d_n,
-                               (kd_geom_head*)go, (kd_geom_head*)gn, (uint2*)gp);
-        });
-        if (rc) return rc;
-    }
     GfArgs a{};
     GfHeadArgs g{};
-    g.head[0] = (const kd_geom_head*)go;
-    g.head[1] = (const kd_geom_head*)gn;
-    g.nhead[0] = g.nhead[1] = cap;
     g.zeros = (const u8*)dz;
-    g.bpairs = (const uint2*)pairs;
-    g.dense = std::getenv("KD_GF_DENSE") && std::getenv("KD_GF_DENSE")[0] == '0' ? 0 : 1;  // (A/B: 0 = k_gf_heads)
+    g.dense = 1;
+    const uint32_t* fpairs = pairs;  // the pairs the filter reads
+    const u64 slots = (cap + 63) / 64 * 64;  // whole 64-delta chunks (k_gf_dense's loads)
+    if (flags & KD_GF_DELTA_HEADS) {  // heads already in delta order (the blob reader's layout)
+        KD_CHECK(n_old >= slots && n_new >= slots, "kd_geom_filter_deltas: KD_GF_DELTA_HEADS needs %llu head slots per side",
+                 (unsigned long long)slots);
+        g.head[0] = heads_old;
+        g.head[1] = heads_new;
+        g.nhead[0] = n_old;
+        g.nhead[1] = n_new;
+        g.pres_only = 1;  // (bpairs = the pairs, set by gf_run)
+    } else {  // per-entry heads: gathered into delta order first (k_gh_gather)
+        void *go, *gn, *gp;
+        if ((rc = ensure(ctx, "gd.ho", (slots + 1) * sizeof(kd_geom_head), &go))) return rc;
+        if ((rc = ensure(ctx, "gd.hn", (slots + 1) * sizeof(kd_geom_head), &gn))) return rc;
+        if ((rc = ensure(ctx, "gd.pairs", (cap + 1) * 8, &gp))) return rc;
+        if (cap) {
+            const unsigned grid = (unsigned)std::max<u64>(1, std::min<u64>((cap + 255) / 256, (u64)ctx->n_cu * 16));
+            rc = launch(ctx, "k_gh_gather", [&] {
+                hipLaunchKernelGGL(k_gh_gather, dim3(grid), dim3(256), 0, ctx->stream, n_old ? heads_old : (const kd_geom_head*)dz,
+                                   n_old, n_new ? heads_new : (const kd_geom_head*)dz, n_new, (const uint2*)pairs, cap, d_n,
+                                   (kd_geom_head*)go, (kd_geom_head*)gn, (uint2*)gp);
+            });
+            if (rc) return rc;
+        }
+        g.head[0] = (const kd_geom_head*)go;
+        g.head[1] = (const kd_geom_head*)gn;
+        g.nhead[0] = g.nhead[1] = cap;
+        g.bpairs = (const uint2*)pairs;
+        fpairs = (const uint32_t*)gp;
+    }
     if (old_blobs) {
         const kd_blobs* bl[2] = {old_blobs, new_blobs};
         for (int s = 0; s < 2; s++) {
@@ -1081,6 +1108,6 @@ extern "C" int kd_geom_filter_deltas(kd_ctx* ctx, const kd_geom_head* heads_old,
             a.nblob[s] = bl[s]->n;
         }
     }
-    return gf_run(ctx, a, &g, (const uint32_t*)gp, cap, d_n, KD_MEM_DEVICE, filt_env, flags, bits, match, keep, n_keep,
-                  enc, enc_ok, KD_MEM_DEVICE);
+    return gf_run(ctx, a, &g, fpairs, cap, d_n, KD_MEM_DEVICE, filt_env, flags, bits, match, keep, n_keep, enc, enc_ok,
+                  KD_MEM_DEVICE);
 }

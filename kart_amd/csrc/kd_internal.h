@@ -62,8 +62,22 @@ struct PendingEv {
 
 }  // namespace kd
 
+// Tuning options of a context (kd_set_option; kd_init seeds them once from the KD_* environment
+// variables of the same names, documented in kartdiff.h).  Defaults are the measured optima.
+struct kd_opts {
+    int merge3_join = 1;             // KD_MERGE3_JOIN: 0 = round 3's two-step merge (classify2 + k_resolve3)
+    int merge3_split = 0;            // KD_MERGE3_SPLIT: 1 = k_join3 stages candidates, k_resolve3 applies the rule
+    int j3_ol = 0;                   // KD_J3_OL: 1 = k_join3 stages ours'/theirs' OIDs in LDS (sorted-form sides)
+    uint64_t j2_oidlds_min = 1ull << 26;  // KD_J2_OIDLDS_MIN: k_join2 stages OIDs in LDS from this many entries
+    int j2r = 0;                     // KD_J2R: 1 = the persistent register-prefetched k_join2r
+    int fd_stream = -1;              // KD_FD_STREAM: -1 auto, 0 windowed k_fielddiff, 1 streamed k_fielddiff_s
+    uint64_t pkm_max_blocks = 1ull << 26;  // KD_PKM_MAX_BLOCKS: largest pk range (64-pk blocks) of the bitmap pk order
+    int trace_host = 0;              // KD_TRACE_HOST: 1 = stream-synced wall-clock marks to stderr
+};
+
 struct kd_ctx {
     int device = 0;
+    kd_opts opt;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     std::map<std::string, kd::DevBuf> bufs;

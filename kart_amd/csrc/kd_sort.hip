@@ -981,10 +981,7 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
     // a bounded pk range: bitmap placement (one mask per 64-pk block)
     const i64 lo_block = pk_lo >> 6, hi_block = pk_hi >> 6;
     const u64 nb = (u64)hi_block - (u64)lo_block + 1;
-    static const u64 pkm_max = [] {
-        const char* e = getenv("KD_PKM_MAX_BLOCKS");  // tests force the radix path with 0
-        return e ? strtoull(e, nullptr, 10) : (u64)1 << 26;
-    }();
+    const u64 pkm_max = ctx->opt.pkm_max_blocks;  // (tests force the radix path with 0)
     if (nb <= pkm_max && nb / PKM_CH < 0xFFFFFFFFull) {
         void *masks, *local, *ctot, *cpre, *ctr, *tpk;
         const u64 nch = (nb + PKM_CH - 1) / PKM_CH;

@@ -72,7 +72,15 @@ def _nonempty(a, dtype, width=1):
 class DevSide:
     """A PackedSide's arrays in HBM."""
 
-    def __init__(self, engine, side):
+    def __init__(self, engine, side, keys_only=False):
+        """keys_only: only the keys go to HBM (OIDs / filenames: a zero placeholder), for entry points
+        that read keys alone (kd_delta_pk_order) — any side form"""
+        if keys_only:
+            self.n, self.key_mode = side.n, side.key_mode
+            self.key = DevBuf.from_numpy(engine, _nonempty(side.key, np.uint64))
+            self.oid = DevBuf.from_numpy(engine, np.zeros(20, np.uint8))
+            self.name = self.name_off = None
+            return
         if getattr(side, "walk_rows", False):
             # (sorted keys beside walk-order OIDs / filenames: uploaded as one side, each key would be
             # paired with another entry's OID — such sides join through their order, DevPermSide)
@@ -376,10 +384,14 @@ class FilterPipeline:
     whole layer in one stream."""
 
     def __init__(self, engine, base, target, base_blobs, target_blobs, geom_cols, filt_env, rectangle=False, bits=20,
-                 heads=False, delta_order=False):
+                 heads=False, delta_order=False, gather=False):
         """heads: filter from 48-B geometry heads (the blob reader's host pass) instead of the blob
-        arenas; delta_order (with heads): every step first gathers the deltas' heads into delta order
-        on the device (kd_geom_filter_deltas: the drop-in's layout), the blob fallback included"""
+        arenas; delta_order (with heads): the heads in delta order, as the drop-in's blob reader lays
+        them out after classification (it reads the deltas' blobs) — built once on the host from the
+        deltas of a first diff (``delta_heads_s``), then every step is classify2 + the filter over them
+        (kd_geom_filter_deltas, KD_GF_DELTA_HEADS; the blob fallback through the step's delta pairs);
+        gather (with delta_order): the per-entry heads are instead gathered into delta order on the
+        device inside every step (k_gh_gather)"""
         import ctypes as _c
 
         self.eng = engine
@@ -407,6 +419,9 @@ class FilterPipeline:
         self.heads_s = None
         self.heads_host = None
         self.delta_order = bool(delta_order) and heads
+        self.gather = bool(gather) and self.delta_order
+        self.dheads = None
+        self.delta_heads_s = None
         if heads:  # the blob reader's host pass, then 48 bytes per blob in HBM (kd_geom_filter_heads)
             import time
 
@@ -421,16 +436,49 @@ class FilterPipeline:
                           for h in hs]
         engine.reserve(max(base.n, target.n))
         engine.sync()
+        if self.delta_order and not self.gather:
+            self._build_delta_heads()
 
-    def step(self):
+    def _classify(self):
         L, ctx = self.eng.L, self.eng.ctx
         N.check(L.kd_diff2_device(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), 0, self.delta.ptr, self.upd.ptr,
                                   self.counts.ptr, self.counts.ptr + 32), "kd_diff2_device")
+
+    def _build_delta_heads(self):
+        """the deltas' heads in delta order (slot d: delta d's old / new head, absent sides zero), as
+        the blob reader leaves them when it reads the deltas' blobs after classification: from the
+        per-entry heads of the host pass and the deltas of one classify2 (host work, outside a step)"""
+        import time
+
+        self._classify()
+        c = self.counts.download(np.uint64, 8)
+        nd = int(c[3])
+        delta = self.delta.download(np.uint32, 2 * nd).reshape(nd, 2)
+        t0 = time.perf_counter()
+        slots = max((self.cap + 63) // 64 * 64, 64)
+        self.dheads = []
+        for s in range(2):
+            col = delta[:, s]
+            pres = np.nonzero(col != N.KD_NONE)[0]
+            h = np.zeros(slots, self.heads_host[s].dtype)
+            h[pres] = self.heads_host[s][col[pres].astype(np.int64)]
+            self.dheads.append((DevBuf.from_numpy(self.eng, h.view(np.uint8).reshape(-1)), slots))
+        self.delta_heads_s = time.perf_counter() - t0
+        self.eng.sync()
+
+    def step(self):
+        L, ctx = self.eng.L, self.eng.ctx
+        self._classify()
         if self.delta_order:
-            (ho, no), (hn, nn) = self.heads
+            if self.gather:  # per-entry heads gathered into delta order on the device
+                (ho, no), (hn, nn) = self.heads
+                flags = self.flags
+            else:
+                (ho, no), (hn, nn) = self.dheads
+                flags = self.flags | N.KD_GF_DELTA_HEADS
             N.check(L.kd_geom_filter_deltas(ctx, ho.ptr, no, hn.ptr, nn, ctypes.byref(self._ob), ctypes.byref(self._nb),
                                             self.delta.ptr, self.cap, ctypes.cast(self.counts.ptr + 24, N.c_u64p),
-                                            self._fe, self.flags, self.bits, self.match.ptr, self.keep.ptr,
+                                            self._fe, flags, self.bits, self.match.ptr, self.keep.ptr,
                                             ctypes.cast(self.n_keep.ptr, N.c_u64p), self.enc.ptr if self.enc else None,
                                             self.enc_ok.ptr if self.enc_ok else None), "kd_geom_filter_deltas")
             return

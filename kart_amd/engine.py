@@ -50,6 +50,15 @@ class Engine:
         N.check(self.L.kd_init(int(device), ctypes.byref(self.ctx)), "kd_init")
         self.device = device
 
+    def set_option(self, name, value):
+        """a tuning option of the context (kd_set_option: the A/B switches of kartdiff.h)"""
+        N.check(self.L.kd_set_option(self.ctx, name.encode(), int(value)), "kd_set_option")
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        N.check(self.L.kd_get_option(self.ctx, name.encode(), ctypes.byref(v)), "kd_get_option")
+        return int(v.value)
+
     def close(self):
         if self.ctx:
             self.L.kd_fini(self.ctx)
@@ -218,7 +227,7 @@ class Engine:
                 info = side.info if side.info is not None else packing.keys_scan(side.key, side.key_mode)
                 lo.append(int(info.pk_min))
                 hi.append(int(info.pk_max))
-        A, B = DevSide(self, base), DevSide(self, target)
+        A, B = DevSide(self, base, keys_only=True), DevSide(self, target, keys_only=True)  # (the pass reads keys only)
         sa, sb = A.kd_side(), B.kd_side()
         d_rec = DevBuf.from_numpy(self, records.reshape(-1))
         d_n = DevBuf.from_numpy(self, np.array([n], np.uint64))

@@ -292,10 +292,13 @@ def geom_heads(data, off, hexarr, gidx, n_leg, threads=0):
     return out[:n]
 
 
-def geom_filter_heads(engine, old_heads, new_heads, pairs, filt_env, rectangle=False, bits=0, arenas=None):
+def geom_filter_heads(engine, old_heads, new_heads, pairs, filt_env, rectangle=False, bits=0, arenas=None,
+                      delta_heads=False):
     """kd_geom_filter_heads over host heads: (codes uint8 [n, 2], keep uint32 [k], enc, enc_ok).
     ``arenas`` ((od, oo), (nd, no)) for the geometries whose decode needs more than their head;
-    without them such sides come back 3 (FALLBACK: the host decides)."""
+    without them such sides come back 3 (FALLBACK: the host decides).  ``delta_heads``: the heads are
+    in delta order (row d = delta d's, ceil(n / 64) * 64 rows per side: KD_GF_DELTA_HEADS, the dense
+    kernel); else the pairs index them."""
     pairs = np.ascontiguousarray(pairs, np.uint32).reshape(-1, 2)
     n = pairs.shape[0]
     hs = [np.ascontiguousarray(h, GEOM_HEAD) for h in (old_heads, new_heads)]
@@ -319,7 +322,7 @@ def geom_filter_heads(engine, old_heads, new_heads, pairs, filt_env, rectangle=F
         engine.ctx, hs[0].ctypes.data if hs[0].size else None, hs[0].shape[0], hs[1].ctypes.data if hs[1].size else None,
         hs[1].shape[0], N.KD_MEM_HOST, ctypes.byref(blobs[0]) if blobs[0] else None,
         ctypes.byref(blobs[1]) if blobs[1] else None, N.ptr(pairs), n, None, N.KD_MEM_HOST, fe,
-        N.KD_GF_RECT if rectangle else 0, int(bits), N.ptr(match), N.ptr(keep), ctypes.byref(nk), N.ptr(enc), N.ptr(ok),
+        (N.KD_GF_RECT if rectangle else 0) | (N.KD_GF_DELTA_HEADS if delta_heads else 0), int(bits), N.ptr(match), N.ptr(keep), ctypes.byref(nk), N.ptr(enc), N.ptr(ok),
         N.KD_MEM_HOST), "kd_geom_filter_heads")
     k = int(nk.value)
     return match[:n], keep[:k], (enc[:n] if bits else None), (ok[:n] if bits else None)
@@ -379,7 +382,16 @@ def filtered_ds_feature_deltas(engine, ds_diff, old_version, new_version, spatia
     # geometry whose decode needs more comes back FALLBACK and is decided below on the host)
     heads = [geom_heads(sides[0][0], sides[0][1], cols.old_hex, cols.old_gidx, len(cols.old_map)),
              geom_heads(sides[1][0], sides[1][1], cols.new_hex, cols.new_gidx, len(cols.new_map))]
-    codes, keep, _, _ = geom_filter_heads(engine, heads[0], heads[1], pairs, env, rect)
+    # laid out in delta order (row i = delta i's head; an absent side's row is never read): the dense
+    # kernel reads its heads without a pair -> head dependency
+    slots = (n + 63) // 64 * 64
+    dense = []
+    for s, h in enumerate(heads):
+        d = np.zeros(slots, GEOM_HEAD)
+        pres = np.nonzero(pairs[:, s] != N.KD_NONE)[0]
+        d[pres] = h[pairs[pres, s].astype(np.int64)]
+        dense.append(d)
+    codes, keep, _, _ = geom_filter_heads(engine, dense[0], dense[1], pairs, env, rect, delta_heads=True)
     kept = np.zeros(n, bool)
     kept[keep] = True
     for i, (key, d) in enumerate(items):

@@ -110,7 +110,7 @@ def test_gpu_merge_trees_uses_device_pack(engine, monkeypatch):
     from kart_amd import merge as M
 
     monkeypatch.setattr(D, "GPU_SORT_MIN", 1)
-    W = synth.table3_layers(3000, seed=4, walk=True)
+    W = synth.table3_layers(30_000, seed=4, walk=True)  # (enough rows that some leaf trees hold several)
 
     def version(side):
         return D.DatasetVersion("ds", None, {}, packing.GENERAL_ENCODING, side.name, side.name_off, side.oid,

@@ -701,15 +701,16 @@ def _grow_geometry(blob, extra, rng):
 
 @pytest.mark.parametrize("stream", ["0", "1"])
 @pytest.mark.parametrize("case", ["c3", "c3v", "huge", "ragged", "points", "one"])
-def test_gpu_fielddiff_contiguous_vs_oracle(engine, monkeypatch, stream, case):
+def test_gpu_fielddiff_contiguous_vs_oracle(engine, request, stream, case):
     """kd_fielddiff on update arenas laid back to back (no pairs: the drop-in's and the bench's form),
-    through the streamed kernel (KD_FD_STREAM=1: whole tile spans into LDS) and the windowed one:
+    through the streamed kernel (fd_stream option 1: whole tile spans into LDS) and the windowed one:
     C3 / C3v polygons, a tile whose span overflows the LDS buffer (blobs of 20-60 KB, read from
     global memory past it), update counts that end inside a tile, point features"""
     from kart_amd import synth
     from kart_amd.schema import FieldMaps
 
-    monkeypatch.setenv("KD_FD_STREAM", stream)
+    engine.set_option("fd_stream", int(stream))
+    request.addfinalizer(lambda: engine.set_option("fd_stream", -1))
     rng = np.random.default_rng(7)
     if case == "points":
         L = synth.points_layer(300_000, seed=3)

@@ -272,13 +272,15 @@ def test_gpu_filter_pipeline_device_resident(engine, n, heads):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [200_000, 3_000_000, pytest.param(100_000_000, marks=pytest.mark.timeout(900))])
-def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n):
+@pytest.mark.parametrize("n,gather", [(200_000, False), (200_000, True), (3_000_000, False), (3_000_000, True),
+                                      pytest.param(100_000_000, False, marks=pytest.mark.timeout(900))])
+def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n, gather):
     """C5 as SURVEY §8(d) defines it (synth.c5_layer: 30 % points, EMPTY points, polygons straddling
     +180, >= 180 degrees wide, starting on the filter's edge, XYZ envelopes the heads cannot decide):
-    classify2, the deltas' heads gathered into delta order on the device, the filter from them with
-    the blob fallback (kd_geom_filter_deltas) — codes, kept list and index envelopes bit-exact with
-    the oracle; the arena kernel gives the same answer"""
+    classify2, then the filter from the deltas' heads in delta order with the blob fallback through
+    the step's delta pairs (kd_geom_filter_deltas: heads laid out in delta order by the host as the
+    blob reader leaves them, KD_GF_DELTA_HEADS; or ``gather``: per-entry heads gathered into delta
+    order on the device) — codes, kept list and index envelopes bit-exact with the oracle"""
     import types
 
     from kart_amd import synth
@@ -288,7 +290,7 @@ def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n):
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     gc = S.GeomCols(ver, ver, "geom", "geom")
     pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, gc, synth.C5_FILTER, False, 20,
-                          heads=True, delta_order=True)
+                          heads=True, delta_order=True, gather=gather)
     pipe.step()
     pipe.step()
     counts, delta, codes, keep, enc, ok = pipe.results()
@@ -308,9 +310,10 @@ def test_gpu_filter_pipeline_c5_mix_delta_order(engine, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [40, 130, 1000, 3_000_000])  # (1 and 13 deltas: one partial chunk)
-def test_gpu_filter_dense_variants_agree(engine, n, monkeypatch):
-    """k_gf_dense (delta-order heads, kd_geom_filter_deltas): every prefetch depth / load form and
-    the pair-indexed k_gf_heads give the oracle's codes, kept list and index envelopes"""
+def test_gpu_filter_head_layouts_agree(engine, n):
+    """k_gf_dense over delta-order heads (prebuilt: KD_GF_DELTA_HEADS; or gathered on the device) and
+    the pair-indexed k_gf_heads over per-entry heads give the oracle's codes, kept list and index
+    envelopes"""
     import types
 
     from kart_amd import synth
@@ -319,22 +322,20 @@ def test_gpu_filter_dense_variants_agree(engine, n, monkeypatch):
     L = synth.c5_layer(n, seed=21)
     ver = types.SimpleNamespace(schema=L.schema, legends=L.legends)
     gc = S.GeomCols(ver, ver, "geom", "geom")
-    pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, gc, synth.C5_FILTER, False, 20,
-                          heads=True, delta_order=True)
     cols = {h: 0 for h in L.legends}
     (od, oo), (nd, no) = L.base_blobs, L.target_blobs
     ref = None
-    for var, val in (("KD_GFD", "1s"), ("KD_GFD", "1t"), ("KD_GFD", "2s"), ("KD_GFD", "2t"), ("KD_GF_DENSE", "0")):
-        monkeypatch.setenv(var, val)
+    for mode in ({"delta_order": True}, {"delta_order": True, "gather": True}, {"delta_order": False}):
+        pipe = FilterPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, gc, synth.C5_FILTER, False, 20,
+                              heads=True, **mode)
         pipe.step()
         counts, delta, codes, keep, enc, ok = pipe.results()
-        monkeypatch.delenv(var)
         if ref is None:
-            oc, okeep, oenc, ook = O.geom_filter(od, oo, nd, no, delta, cols, cols, synth.C5_FILTER, False, 20)
-            ref = (oc, okeep, oenc, ook)
+            ref = O.geom_filter(od, oo, nd, no, delta, cols, cols, synth.C5_FILTER, False, 20)
         oc, okeep, oenc, ook = ref
-        assert np.array_equal(codes, oc) and np.array_equal(keep, okeep) and counts["kept"] == len(okeep), (var, val)
-        assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1]), (var, val)
+        assert np.array_equal(codes, oc) and np.array_equal(keep, okeep) and counts["kept"] == len(okeep), mode
+        assert np.array_equal(ok, ook) and np.array_equal(enc[ok == 1], oenc[ook == 1]), mode
+        del pipe
 
 
 @pytest.mark.parametrize("bits", [20, 16])
