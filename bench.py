@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--no-sort", action="store_true",
                     help="c2/c3: skip timing the fallback steps (sides in a non-key order: both GPU side sorts in "
                          "the step); c4: skip the presorted comparison")
+    ap.add_argument("--no-radix", action="store_true", help="c2/c3: skip timing the radix-sort fallback beside the "
+                                                             "per-leaf-tree one")
     ap.add_argument("--no-pk-order", action="store_true",
                     help="c2/c3: leave the deltas in walk (key) order (no kd_delta_pk_order in the step)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -500,28 +502,31 @@ def sort_bytes(info, n, gather_oids):
     return b, npass
 
 
-def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
-    """The fallback the drop-in takes for a side whose walk order is not key order (a leaf tree
-    mixing 2**30 pk wraps): the same step from scrambled sides, both GPU side sorts inside it (passes
-    sized by kd_keys_scan: no read-back), the join reading OIDs through the sort orders."""
+def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs, radix=False):
+    """The fallback the drop-in takes for a side whose walk order is not key order (leaf trees mixing
+    2**30 pk wraps): the same step from sides whose rows are shuffled inside every leaf tree, both GPU
+    side sorts inside it — per leaf tree (kd_sort_segmented_into: the walk lists each leaf tree's
+    entries together, so only they are out of order; planned from the host's kd_keys_scan, no
+    read-back) or, ``radix`` (a leaf tree longer than 512 entries), the onesweep radix sort of the
+    compacted varying key bits — then the join reading OIDs through the sort orders."""
     from kart_amd.device import DiffPipeline
 
-    def leaf_scramble(n, seed):
-        """rows shuffled inside each run of 64 (what a walk of leaf trees mixing pk wraps looks like:
-        key order broken inside leaf trees, kept between them)"""
+    def leaf_scramble(keys, seed):
+        """rows shuffled inside each leaf tree (the entries sharing the key's top 24 bucket bits): what
+        a walk of leaf trees mixing pk wraps looks like — key order broken inside leaf trees, kept
+        between them"""
         r = np.random.default_rng(seed)
-        m = (n + 63) // 64
-        p = (np.arange(m * 64, dtype=np.int64).reshape(m, 64) + 0)
-        p = np.take_along_axis(p, np.argsort(r.random((m, 64)), axis=1), axis=1).reshape(-1)
-        return p[p < n]
+        b = keys >> np.uint64(40)
+        return np.lexsort((r.random(keys.shape[0]), b))  # stable by bucket, random inside
 
-    perms = (leaf_scramble(L.base.n, 1), leaf_scramble(L.target.n, 2))
+    perms = (leaf_scramble(L.base.key, 1), leaf_scramble(L.target.key, 2))
     fp = DiffPipeline(eng, L.base, L.target, L.base_blobs, L.target_blobs, maps, unsorted=perms,
-                      late=not args.sort_gather, pk_order=not args.no_pk_order)
+                      late=not args.sort_gather, pk_order=not args.no_pk_order, radix=radix)
     for _ in range(max(1, args.warmup)):
         fp.step()
     eng.sync()
     if not args.no_check:
+        fp.results()  # (raises on a device error flag: the join's order checks, the per-leaf-tree sort's)
         for S, side, perm, order in zip((fp.A, fp.B), (L.base, L.target), perms, fp.orders()):
             assert np.array_equal(S.key.download(np.uint64, side.n), side.key), "sorted keys differ"
             assert np.array_equal(perm[order], np.arange(side.n)), "sort order differs"
@@ -535,9 +540,13 @@ def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
         fp.sort_step()
     eng.sync()
     eng.prof_enable(False)
-    sk = kernel_times(eng, SORT_KERNELS)
+    sk = kernel_times(eng, SORT_KERNELS + ("k_seg_sort",))
     ms_sorts = sum(v[0] * v[1] for v in sk.values()) / 3
-    (bb, pb), (bt, pt) = [sort_bytes(w[3], w[2], not fp.late) for w in fp.walk]
+    if fp.segmented:  # per entry: the key read, the key + 4-B order written (the leaf tree's neighbours hit the cache)
+        bb, bt = 20 * L.base.n, 20 * L.target.n
+        pb = pt = 0
+    else:
+        (bb, pb), (bt, pt) = [sort_bytes(w[3], w[2], not fp.late) for w in fp.walk]
     eng.prof_reset()
     eng.prof_select(["k_join2"])
     eng.prof_enable(True)
@@ -546,9 +555,12 @@ def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
     eng.sync()
     eng.prof_enable(False)
     jp = kernel_times(eng, ("k_join2",))
+    how = ("per leaf tree (kd_sort_segmented_into: one kernel per side, planned from the host kd_keys_scan's "
+           "seg_max)" if fp.segmented else "by the onesweep LSD radix sort of the compacted varying key bits "
+           "(kd_sort_side_into, passes sized by the host kd_keys_scan)")
     out = {"what": "the drop-in's fallback for sides whose walk order is not key order: each step sorts both "
-                   "sides (rows shuffled inside every 64-entry run, as a walk of leaf trees mixing pk wraps) on the GPU (kd_sort_side_into, onesweep LSD radix sort of the compacted varying "
-                   "key bits, passes sized by the host kd_keys_scan) then classify2 + field diff + pk order; " +
+                   "sides (rows shuffled inside every leaf tree, as a walk of leaf trees mixing pk wraps) on the GPU "
+                   + how + ", then classify2 + field diff + pk order; " +
                    ("the join reads the OIDs through the sort orders (kd_diff2_device_perm)" if fp.late else
                     "the OIDs are gathered into key order by the sort"),
            "value": round(total_pairs * args.steps / el / 1e6, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -561,7 +573,11 @@ def fallback_sort(args, H, eng, L, maps, elapsed, total_pairs):
                         "achieved": round((bb + bt) / (ms_sorts * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round((bb + bt) / (ms_sorts * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
     assert out["kernel_launches_per_step"].get("k_sort_pass", 0) == pb + pt, "pass accounting differs from launches"
+    if fp.segmented:
+        assert out["kernel_launches_per_step"].get("k_seg_sort", 0) == 2, "one per-leaf-tree sort per side"
     del fp
+    if not radix and not args.no_radix:  # the radix path beside it (a leaf tree longer than 512 entries)
+        out["radix"] = fallback_sort(args, H, eng, L, maps, elapsed, total_pairs, radix=True)
     return out
 
 

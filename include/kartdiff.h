@@ -347,13 +347,16 @@ int kd_hex_encode(kd_ctx* ctx, const kd_blobs* blobs, uint32_t mode, uint8_t* he
 int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32_t* d_order, uint64_t n, uint32_t* h_dup);
 /* What a sort needs to know about a side's keys (host scan, kd_keys_scan): the bits that vary
  * (OR of key[i] ^ key[0]) and key[0]; whether the keys are strictly ascending already (a walk-order
- * KD_KEY_INT side usually is: no sort); for KD_KEY_INT the smallest and largest pk. */
+ * KD_KEY_INT side usually is: no sort); for KD_KEY_INT the smallest and largest pk; seg_max: the
+ * longest run of consecutive keys sharing their top 24 bits (the leaf tree: a walk lists each leaf
+ * tree's entries together), or -1 when those bits descend somewhere — a side with 0 < seg_max <= 512
+ * that is not ascending sorts per leaf tree (kd_sort_segmented_into, seg_bits 24). */
 typedef struct kd_keys_info {
     uint64_t vary;
     uint64_t key0;
     int64_t pk_min, pk_max; /* KD_KEY_INT only */
     int32_t ascending;
-    int32_t reserved;
+    int32_t seg_max;
 } kd_keys_info;
 int kd_keys_scan(const uint64_t* keys, uint64_t n, uint32_t key_mode, kd_keys_info* out);
 /* Out-of-place form (what a device pipeline runs): d_key_in / d_oid_in hold the side in walk order
@@ -366,8 +369,9 @@ int kd_keys_scan(const uint64_t* keys, uint64_t n, uint32_t key_mode, kd_keys_in
  * side whose walk order is not key order (a leaf tree mixing pk wraps). */
 int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oid_in, uint64_t* d_key_out,
                       uint8_t* d_oid_out, uint32_t* d_order, uint64_t n, uint32_t* d_dup, const kd_keys_info* info);
-/* A KD_KEY_HASH side in walk order (its keys ascend in the top seg_bits bucket bits; inside a leaf
- * tree the leaves are in filename order, not FNV order): each bucket's entries ordered by key.
+/* A side in walk order whose keys ascend in their top seg_bits bucket bits (KD_KEY_HASH: inside a leaf
+ * tree the leaves are in filename order, not FNV order; KD_KEY_INT: a leaf tree mixing pk wraps):
+ * each bucket's entries ordered by key.
  * d_key_out [n] <- keys ascending, d_order [n] <- walk index of sorted entry k (the OIDs and
  * filenames stay in walk order: kd_diff2_device_perm / kd_merge3_device_perm read through it).
  * *d_err |= 1 on a duplicate key or descending bucket bits, 4 on a bucket of more than 512 entries

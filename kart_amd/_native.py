@@ -123,7 +123,7 @@ class KdKeysInfo(ctypes.Structure):
         ("pk_min", ctypes.c_int64),
         ("pk_max", ctypes.c_int64),
         ("ascending", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("seg_max", ctypes.c_int32),  # longest run of keys sharing their top 24 (bucket) bits; -1: buckets descend
     ]
 
 

@@ -575,7 +575,14 @@ int kd_keys_scan(const uint64_t* keys, uint64_t n, uint32_t key_mode, kd_keys_in
     unsigned nt = std::thread::hardware_concurrency();
     nt = nt == 0 ? 1 : nt > 32 ? 32 : nt;
     if (n < 65536) nt = 1;
-    struct Part { u64 vary = 0; i64 lo = INT64_MAX, hi = INT64_MIN; bool asc = true; };
+    // per part: the runs of equal top-24-bit buckets (first and last run, longest inside) and
+    // whether the buckets are non-decreasing
+    struct Part {
+        u64 vary = 0;
+        i64 lo = INT64_MAX, hi = INT64_MIN;
+        bool asc = true, basc = true;
+        u64 b0 = 0, b1 = 0, pre = 0, suf = 0, mx = 0, len = 0;
+    };
     std::vector<Part> part(nt);
     std::vector<std::thread> th;
     const u64 chunk = (n + nt - 1) / nt;
@@ -584,27 +591,65 @@ int kd_keys_scan(const uint64_t* keys, uint64_t n, uint32_t key_mode, kd_keys_in
         if (a >= b) break;
         th.emplace_back([&, t, a, b] {
             Part p;
+            p.len = b - a;
+            p.b0 = keys[a] >> 40;
+            u64 run = 0, prev = p.b0;
+            bool first = true;
             for (u64 i = a; i < b; i++) {
                 const u64 k = keys[i];
                 p.vary |= k ^ k0;
                 if (i > 0) p.asc &= keys[i - 1] < k;
+                const u64 bk = k >> 40;
+                if (bk != prev) {
+                    p.basc &= bk > prev;
+                    if (first) p.pre = run;
+                    first = false;
+                    p.mx = run > p.mx ? run : p.mx;
+                    run = 0;
+                    prev = bk;
+                }
+                run++;
                 if (key_mode == KD_KEY_INT) {
                     const i64 pk = wk::int_key_pk(k);
                     p.lo = pk < p.lo ? pk : p.lo;
                     p.hi = pk > p.hi ? pk : p.hi;
                 }
             }
+            if (first) p.pre = run;
+            p.suf = run;
+            p.b1 = prev;
+            p.mx = run > p.mx ? run : p.mx;
             part[t] = p;
         });
     }
     for (auto& t : th) t.join();
     i64 lo = INT64_MAX, hi = INT64_MIN;
+    bool basc = true, have = false;
+    u64 cur_b = 0, cur_run = 0, seg = 0;  // the run still open at the end of the parts combined so far
     for (auto& p : part) {
+        if (!p.len) continue;
         out->vary |= p.vary;
         out->ascending &= p.asc ? 1 : 0;
         lo = p.lo < lo ? p.lo : lo;
         hi = p.hi > hi ? p.hi : hi;
+        basc &= p.basc;
+        const bool one = p.pre == p.len;  // the whole part is one bucket
+        if (have && p.b0 == cur_b) {
+            cur_run += p.pre;
+        } else {
+            if (have) { basc &= p.b0 > cur_b; seg = cur_run > seg ? cur_run : seg; }
+            cur_run = p.pre;
+        }
+        if (!one) {
+            seg = cur_run > seg ? cur_run : seg;
+            seg = p.mx > seg ? p.mx : seg;
+            cur_run = p.suf;
+        }
+        cur_b = p.b1;
+        have = true;
     }
+    seg = cur_run > seg ? cur_run : seg;
+    out->seg_max = !basc ? -1 : (int32_t)(seg > 0x7fffffffull ? 0x7fffffff : seg);
     out->key0 = k0;
     out->pk_min = key_mode == KD_KEY_INT ? lo : 0;
     out->pk_max = key_mode == KD_KEY_INT ? hi : 0;

@@ -200,7 +200,10 @@ class DiffPipeline:
     updates."""
 
     def __init__(self, engine, base, target, base_blobs, target_blobs, maps, ordered=True, gather=None, unsorted=None,
-                 late=True, pk_order=True):
+                 late=True, pk_order=True, radix=False):
+        """``unsorted`` (the fallback): both sides in that row order instead, sorted on the device inside
+        every step — per leaf tree (kd_sort_segmented_into) when the host's kd_keys_scan finds the
+        leaf trees short, else (or ``radix``) the onesweep radix sort (kd_sort_side_into)"""
         from . import packing
 
         self.eng = engine
@@ -209,12 +212,18 @@ class DiffPipeline:
         self.B = DevSide(engine, target)
         self.walk = None
         self.late = bool(late) and gather is None
+        self.seg_err = None
         if unsorted is not None:
             self.walk = []
             for side, perm in zip((base, target), unsorted):
                 w = _WalkSide(side, perm)
                 info = packing.keys_scan(w.key, side.key_mode)
                 self.walk.append((DevSide(engine, w), DevBuf(engine, 4 * max(side.n, 1)), side.n, info))
+            # per leaf tree when every side's leaf trees are short (no read-back: the plan is the host scan's)
+            self.segmented = self.late and not radix and all(0 < x[3].seg_max <= packing.SEG_SORT_MAX for x in self.walk)
+            if self.segmented:
+                self.seg_err = DevBuf(engine, 8)
+                self.seg_err.zero()
         self.OB = DevBlobs(engine, *base_blobs)
         self.NB = DevBlobs(engine, *target_blobs)
         self.maps = maps
@@ -269,7 +278,10 @@ class DiffPipeline:
         """(fallback) the two GPU side sorts into the sorted side buffers"""
         L, ctx = self.eng.L, self.eng.ctx
         for (w, order, n, info), S in zip(self.walk, (self.A, self.B)):
-            if self.late:
+            if self.segmented:
+                N.check(L.kd_sort_segmented_into(ctx, w.key.ptr, S.key.ptr, order.ptr, n, 24, self.seg_err.ptr),
+                        "kd_sort_segmented_into")
+            elif self.late:
                 N.check(L.kd_sort_side_into(ctx, w.key.ptr, None, S.key.ptr, None, order.ptr, n, None,
                                             ctypes.byref(info)), "kd_sort_side_into")
             else:
@@ -337,6 +349,8 @@ class DiffPipeline:
         c = self.counts.download(np.uint64, 8)
         if c[4]:
             raise N.Unsupported(N.KD_EUNSUPPORTED, f"device error flag {int(c[4])}")
+        if self.seg_err is not None and int(self.seg_err.download(np.uint32, 1)[0]):
+            raise N.Unsupported(N.KD_EUNSUPPORTED, "per-leaf-tree sort flagged a long or descending leaf tree")
         nd, nu = int(c[3]), int(c[1])
         delta = self.delta.download(np.uint32, 2 * nd).reshape(nd, 2)
         upd = self.upd.download(np.uint32, 2 * nu).reshape(nu, 2)

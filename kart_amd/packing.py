@@ -187,13 +187,18 @@ def _gather_names(paths, off, order, chunk=1 << 20):
     return out, noff
 
 
+SEG_SORT_MAX = 512  # the longest leaf tree kd_sort_segmented_into orders (err 4 beyond)
+
+
 def sort_on_device_perm(engine, keys, oids, info, encoding, paths, off):
     """GPU pack of a side whose walk order is not key order, late-materialised as bench.py times it:
-    KD_KEY_HASH sides take the per-bucket sort (kd_sort_segmented_into, one kernel), falling back to
-    the full radix sort of the keys when a bucket is long or the buckets descend; KD_KEY_INT sides
-    the radix sort of the compacted varying key bits (kd_sort_side_into, passes from the host's
-    kd_keys_scan, no OIDs moved).  Returns (DevPermSide, sorted keys, order) — OIDs and filenames
-    stay in walk order.  PackError on duplicate keys."""
+    the per-leaf-tree sort (kd_sort_segmented_into, one kernel) — KD_KEY_HASH sides always try it (a
+    leaf tree lists its entries in filename order, not FNV order), KD_KEY_INT sides when the host's
+    kd_keys_scan finds their leaf trees short (seg_max <= 512: a walk mixing pk wraps inside leaf
+    trees) — else, or when a bucket is long or the buckets descend, the full radix sort of the
+    compacted varying key bits (kd_sort_side_into, passes from kd_keys_scan, no OIDs moved).
+    Returns (DevPermSide, sorted keys, order) — OIDs and filenames stay in walk order.  PackError on
+    duplicate keys."""
     import ctypes
 
     from . import shard
@@ -203,7 +208,7 @@ def sort_on_device_perm(engine, keys, oids, info, encoding, paths, off):
     dk_in = DevBuf.from_numpy(engine, keys)
     dk, dord, flag = DevBuf(engine, 8 * n), DevBuf(engine, 4 * n), DevBuf(engine, 8)
     sorted_ok = False
-    if encoding.key_mode == N.KD_KEY_HASH:
+    if encoding.key_mode == N.KD_KEY_HASH or 0 < info.seg_max <= SEG_SORT_MAX:
         flag.zero()
         N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk_in.ptr, dk.ptr, dord.ptr, n,
                                                 shard.bucket_bits(encoding.key_mode, encoding), flag.ptr),

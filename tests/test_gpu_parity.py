@@ -248,6 +248,9 @@ def test_gpu_env_overlap_vs_oracle(engine):
     (True, 100_000_000, "polygons", False),  # C3 at its stated size (configs[2], the bench's default
                                              # workload): walk-order sides, no sort, pk-order sorts included
     (True, 20_000_000, "polygons", "late"),  # the fallback side sorts at 20M
+    # rows shuffled inside each leaf tree (a walk mixing pk wraps): the per-leaf-tree sort
+    (True, 1000, "points", "leaf"), (True, 3_000_000, "points", "leaf"), (False, 2_000_000, "polygons", "leaf"),
+    (True, 20_000_000, "polygons", "leaf"),
     # C3v: 60 % of the geometry edits keep their length, so their payloads are compared byte by byte
     (True, 2_000_000, "polygons_same", False), (False, 2_000_000, "polygons_same", False),
     (True, 100_000_000, "polygons_same", False),
@@ -268,9 +271,14 @@ def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
          synth.polygons_layer(n, seed=12, same_len=0.6 if layer == "polygons_same" else 0.0))
     maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
     rng = np.random.default_rng(n)
-    perms = (rng.permutation(L.base.n), rng.permutation(L.target.n)) if walk else None
+    if walk == "leaf":  # shuffled inside each leaf tree (the key's top 24 bits), in order between them
+        perms = tuple(np.lexsort((rng.random(S.n), S.key >> np.uint64(40))) for S in (L.base, L.target))
+    else:
+        perms = (rng.permutation(L.base.n), rng.permutation(L.target.n)) if walk else None
     pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps, ordered=ordered, unsorted=perms,
-                        late=walk == "late")
+                        late=walk in ("late", "leaf"))
+    if walk:
+        assert pipe.segmented == (walk == "leaf")
     if walk:  # scramble the sorted buffers first: the sort (and, gathering, its OID permute) must rewrite them
         for S in (pipe.A, pipe.B):
             N.check(engine.L.kd_memset(engine.ctx, S.key.ptr, 0xA5, S.key.nbytes), "kd_memset")

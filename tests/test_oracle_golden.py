@@ -268,3 +268,35 @@ def test_oracle_fielddiff_vs_python_semantics():
         old = O.py_feature(ob, [pk], lo, sa)
         new = O.py_feature(nb, [pk], ln, sb)
         assert maps.changed_names(masks[u]) == O.py_changed_fields(old, new)
+
+
+def _seg_max_ref(keys):
+    b = keys >> np.uint64(40)
+    if keys.size == 0:
+        return 0
+    if np.any(b[1:] < b[:-1]):
+        return -1
+    edges = np.flatnonzero(np.diff(b)) + 1
+    runs = np.diff(np.concatenate([[0], edges, [keys.size]]))
+    return int(runs.max())
+
+
+def test_keys_scan_seg_max():
+    """kd_keys_scan's seg_max (the longest run of keys in one leaf tree, -1 when the tree bits descend)
+    equals a numpy restatement — threaded parts included (runs crossing the part boundaries)"""
+    from kart_amd import packing
+
+    rng = np.random.default_rng(1)
+    for n in (0, 1, 5, 1000, 70_000, 300_000):
+        for kind in ("asc", "runs", "onebucket", "desc"):
+            if kind == "asc":
+                k = np.sort(rng.integers(0, 2**63, n, dtype=np.uint64))
+            elif kind == "runs":  # buckets ascending, each bucket's entries scrambled (a walk mixing wraps)
+                b = np.sort(rng.integers(0, 1 << 12, n, dtype=np.uint64))
+                k = (b << np.uint64(40)) | rng.integers(0, 1 << 40, n, dtype=np.uint64)
+            elif kind == "onebucket":
+                k = (np.uint64(7) << np.uint64(40)) | rng.permutation(n).astype(np.uint64)
+            else:
+                k = rng.integers(0, 2**63, n, dtype=np.uint64)
+            info = packing.keys_scan(k, 0 if kind != "onebucket" else 1)
+            assert info.seg_max == _seg_max_ref(k), (n, kind)
