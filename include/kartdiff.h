@@ -145,6 +145,7 @@ int kd_set_stream(kd_ctx* ctx, void* hip_stream);
  *   merge3_join    [KD_MERGE3_JOIN]    1: one-pass three-way join (k_join3); 0: classify2 + k_resolve3
  *   merge3_split   [KD_MERGE3_SPLIT]   1: k_join3 stages candidates, k_resolve3 applies the rule
  *   j3_ol          [KD_J3_OL]          1: k_join3 stages ours'/theirs' OIDs in LDS (sorted-form sides)
+ *   j3_v           [KD_J3_V]           1: k_join3b (every tile range in one LDS-DMA batch); 0: k_join3
  *   j2_oidlds_min  [KD_J2_OIDLDS_MIN]  k_join2 stages OIDs in LDS from this many entries (2^26)
  *   j2r            [KD_J2R]            1: the persistent register-prefetched int-key join
  *   fd_stream      [KD_FD_STREAM]      -1 auto, 0 windowed, 1 streamed field diff (contiguous arenas)

@@ -942,6 +942,7 @@ struct Join3Args {
     const u64* apart;     // [ntiles + 1]
     u32* stage_conf;      // per tile C2_STAGE slots of (a, o, t)
     uint2* stage_md;      // per tile C2_STAGE slots of (o, t)
+    const u64* nsplit;    // (k_join3b, KD_KEY_HASH) [4 * (ntiles + 1)]: name offsets around each split
 };
 #ifndef KD_J3_ACAP
 #define KD_J3_ACAP 1024   // ancestor keys of a tile staged in LDS (a longer range is searched in HBM)
@@ -1297,13 +1298,367 @@ __global__ __launch_bounds__(64) void k_place3(const u32* __restrict__ stage_con
     for (u32 x = tid; x < own.y; x += 64) out_md[pm + x] = smp[x];
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_join3b: the three-way join with every tile-sized range staged in one LDS-DMA round trip
+// ---------------------------------------------------------------------------------------------
+// k_join3 chains six to eight dependent memory round trips per tile (split points, then keys and
+// name bounds, then names, walk rows, OIDs and name offsets, then the differing paths' ancestor
+// rows, OIDs and names), and its 22-KB name buffer overflows on SURVEY's C4 names (12-24-character
+// text pks: ~36-B paths), sending every filename compare to HBM.  k_join3b cuts the chain to five:
+//   1. the tile's two split records (k_apart3b: merge-path split, ancestor lower bound and the name
+//      arena offsets around the split, so no round trip waits on a split point to find its names);
+//   2. ONE LDS-DMA batch: ours' / theirs' / the ancestor's keys, (PERM) the three walk-row ranges
+//      of the tile's sorted entries, and ours' / theirs' filename bytes of the tile's rows (PERM: the
+//      rows widened by a halo of J3B_HALO on each side — a per-leaf-tree sort moves an entry less than
+//      its leaf tree's length; a row outside them is compared in HBM);
+//   3. the matched pairs' OIDs and name offsets (rows from LDS), then OIDs and names compared;
+//   4. per differing path (one per thread, after compaction; ancestor found by binary search in
+//      LDS, its row from LDS): the three OIDs and the ancestor's / the path's name offsets;
+//   5. the ancestor's filename (HBM window) against the path's name (LDS).
+// Results are k_join3's (same staging, same k_place3).
+#ifndef KD_J3B_IPT
+#define KD_J3B_IPT 2  // 512-item tiles: C4's ~36-B names of a tile (+ halo) fit 22.5 KB of LDS
+#endif
+constexpr int J3B_IPT = KD_J3B_IPT;
+constexpr int J3B_TILE = C2_NT * J3B_IPT;
+#ifndef KD_J3B_ACAP
+#define KD_J3B_ACAP (J3B_TILE + 128)  // ancestor keys staged (a tile's range is ~half its items)
+#endif
+constexpr int J3B_ACAP = KD_J3B_ACAP;
+#ifndef KD_J3B_NAME_CH
+#define KD_J3B_NAME_CH 1408
+#endif
+#ifndef KD_J3B_HALO
+#define KD_J3B_HALO 16
+#endif
+constexpr u64 J3B_HALO = KD_J3B_HALO;
+
+// apart[t] and (nsplit) the name-arena offsets around split t: ours rows i_t -/+ halo, theirs rows
+// j_t - halo and j_t + 1 + halo (clamped), j_t = min(t * tile, nO + nT) - i_t
+__global__ __launch_bounds__(256) void k_apart3b(const u64* __restrict__ O, u64 nO, const u64* __restrict__ T, u64 nT,
+                                                 const u64* __restrict__ part, u64 ntiles, int tile_items,
+                                                 const u64* __restrict__ K, u64 nK, u64* __restrict__ apart,
+                                                 const u64* __restrict__ offO, const u64* __restrict__ offT, u64 halo,
+                                                 u64* __restrict__ nsplit) {
+    const u64 t = ((u64)blockIdx.x * 256 + threadIdx.x) / 8;
+    if (t > ntiles) return;  // (whole 8-lane groups)
+    const int sub = threadIdx.x & 7;
+    const u64 i = part[t];
+    const u64 d = min(t * (u64)tile_items, nO + nT), j = d - i;
+    if (nsplit && sub < 4) {
+        u64 v;
+        if (sub == 0) v = offO[i > halo ? i - halo : 0];
+        else if (sub == 1) v = offO[min(i + halo, nO)];
+        else if (sub == 2) v = offT[j > halo ? j - halo : 0];
+        else v = offT[min(j + 1 + halo, nT)];
+        nsplit[4 * t + sub] = v;
+    }
+    u64 r;
+    if (t == 0) r = 0;
+    else if (t == ntiles) r = nK;
+    else {
+        const u64 a = i < nO ? O[i] : ~0ull, b = j < nT ? T[j] : ~0ull;
+        const u64 key = a < b ? a : b;
+        const u64 guess = nO ? (u64)((double)i / (double)nO * (double)nK) : (u64)((double)d / (double)(nO + nT) * (double)nK);
+        r = lb_guided<8>(K, nK, key, guess < nK ? guess : nK, 256);
+    }
+    if (sub == 0) apart[t] = r;
+}
+
+// a filename in HBM (bytes [a0, a0 + len)) against one in LDS (byte address lb)
+__device__ __forceinline__ bool glb_lds_name_eq(const u8* __restrict__ na, u64 a0, u32 len, u32 lb) {
+    typedef const __attribute__((address_space(3))) u32* l32;
+    const u32 sa = (u32)(a0 & 3), sb = lb & 3;
+    const u32* wa = (const u32*)(na + (a0 - sa));
+    const u32 nwa = (sa + len + 3) >> 2;
+    const u32 wb = lb - sb;
+    if (nwa <= 16) {  // one window of 16 dwords, all loads issued together
+        u32 x[17], y[17];
+#pragma unroll
+        for (int w = 0; w < 16; w++) x[w] = (u32)w < nwa ? wa[w] : 0u;
+        x[16] = 0;
+#pragma unroll
+        for (int w = 0; w < 17; w++) y[w] = *(l32)(size_t)(wb + 4 * w);
+        u32 diff = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            const u32 rem = len > 4u * w ? len - 4u * w : 0u;
+            const u32 m = rem >= 4 ? 0xFFFFFFFFu : ((1u << (8 * rem)) - 1u);
+            diff |= (__builtin_amdgcn_alignbyte(x[w + 1], x[w], sa) ^ __builtin_amdgcn_alignbyte(y[w + 1], y[w], sb)) & m;
+        }
+        return diff == 0;
+    }
+    typedef const __attribute__((address_space(3))) u8* l8;
+    for (u32 k = 0; k < len; k++)
+        if (na[a0 + k] != *(l8)(size_t)(lb + k)) return false;
+    return true;
+}
+
+template <int NT, int IPT, bool HASH, bool PERM>
+__global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
+    const Join2Args& g = g3.j;
+    using LD = Join2Lds<NT, IPT>;
+    constexpr int TILE = LD::TILE;
+    static_assert(TILE <= 4095, "per-item records hold 12-bit local indices");
+    constexpr int KCH = (8 * (J3B_ACAP + 2) + 16 + 15) / 16 + 4;
+    // walk rows: ours [i0, i1) + theirs [j0, j1e) (<= TILE + 1 entries) and the ancestor's [k0, k1e)
+    constexpr int ORDCH = PERM ? (4 * (TILE + 1) + 15) / 16 + 4 + (4 * (J3B_ACAP + 1) + 15) / 16 + 2 : 1;
+    constexpr int NMCH = HASH ? KD_J3B_NAME_CH : 1;
+    __shared__ u32x4 s_ch[LD::CHK];
+    __shared__ u32x4 s_k[KCH];
+    __shared__ u32x4 s_ord[ORDCH];
+    __shared__ u32x4 s_nm[NMCH];
+    __shared__ u32 s_drec[TILE];
+    __shared__ u32 s_wave[3 * NT / 64];
+    typedef const __attribute__((address_space(1))) u32* gp32;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64 tile = blockIdx.x;
+    // ---- 1. split records of both tile ends ----
+    const u64 p0 = g.part[tile], p1 = g.part[tile + 1];
+    const u64 a0 = g3.apart[tile], a1 = g3.apart[tile + 1];
+    u64 nmA0 = 0, nmA1 = 0, nmB0 = 0, nmB1 = 0;
+    if (HASH) {
+        nmA0 = g3.nsplit[4 * tile]; nmB0 = g3.nsplit[4 * tile + 2];
+        nmA1 = g3.nsplit[4 * tile + 5]; nmB1 = g3.nsplit[4 * tile + 7];
+    }
+    const TileGeo q = tile_geo_from(g, tile, TILE, p0, p1);
+    bool bad = !q.ok;
+    const TileRanges r = tile_ranges(g, q);
+    const u64 k0 = uni64(a0), kend = uni64(a1);
+    const bool kok = kend >= k0 && kend <= g3.nK;
+    bad |= !kok;
+    const u64 k1 = kok ? kend : k0;
+    const u64 k1e = k1 < g3.nK ? k1 + 1 : k1;
+    const bool has_lbK = k0 > 0;
+    const bool lk = k1e - k0 <= (u64)J3B_ACAP;
+    // the staged name rows (PERM: the sorted ranges widened by the halo)
+    const u64 H = PERM ? J3B_HALO : 0;
+    const u64 rA0 = q.i0 > H ? q.i0 - H : 0, rA1 = min(q.i1 + H, g.nA);
+    const u64 rB0 = q.j0 > H ? q.j0 - H : 0, rB1 = min(q.j1 + 1 + H, g.nB);
+    // ---- 2. one DMA batch ----
+    u32 qq = dma_range<NT>(r.ka, s_ch, 0);
+    qq = dma_range<NT>(r.kb, s_ch + r.c1, qq);
+    Range rk{};
+    if (lk) {
+        rk = mk_range(g3.K, 8 * (k0 - has_lbK), 8 * k1e);
+        qq = dma_range<NT>(rk, s_k, qq);
+    }
+    Range roO{}, roT{}, roK{};
+    if (PERM) {
+        roO = mk_range(g.ordA, 4 * q.i0, 4 * q.i1);
+        roT = mk_range(g.ordB, 4 * q.j0, 4 * q.j1e);
+        qq = dma_range<NT>(roO, s_ord, qq);
+        qq = dma_range<NT>(roT, s_ord + roO.nch, qq);
+        if (lk) {
+            roK = mk_range(g3.ordK, 4 * k0, 4 * k1e);
+            qq = dma_range<NT>(roK, s_ord + roO.nch + roT.nch, qq);
+        }
+    }
+    Range rnA{}, rnB{};
+    bool lnames = false;
+    if (HASH) {
+        nmA0 = uni64(nmA0); nmA1 = uni64(nmA1); nmB0 = uni64(nmB0); nmB1 = uni64(nmB1);
+        rnA = mk_range(g.nameA, nmA0, nmA1);
+        rnB = mk_range(g.nameB, nmB0, nmB1);
+        lnames = q.ok && nmA1 >= nmA0 && nmB1 >= nmB0 && (u64)rnA.nch + rnB.nch <= (u64)NMCH;
+        if (lnames) {
+            qq = dma_range<NT>(rnA, s_nm, qq);
+            qq = dma_range<NT>(rnB, s_nm + rnA.nch, qq);
+        }
+    }
+    __syncthreads();  // vmcnt(0) + barrier: everything staged has landed
+    const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
+    const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
+    const u64* sK = (const u64*)((const u8*)s_k + rk.skew) + has_lbK;
+    const u32* sOrdO = (const u32*)((const u8*)s_ord + roO.skew);
+    const u32* sOrdT = (const u32*)((const u8*)(s_ord + roO.nch) + roT.skew);
+    const u32* sOrdK = (const u32*)((const u8*)(s_ord + roO.nch + roT.nch) + roK.skew);
+    u32 rec[IPT];
+    tile_walk<NT, IPT>(sA, sB, q, rec, bad);
+    for (int x = tid; x < q.na; x += NT) bad |= (x > 0 || q.has_lbA) && sA[x - 1] >= sA[x];
+    for (int x = tid; x < q.nb; x += NT) bad |= (x > 0 || q.has_lbB) && sB[x - 1] >= sB[x];
+    if (lk) {
+        for (int x = tid; x < (int)(k1 - k0); x += NT) bad |= (x > 0 || has_lbK) && sK[x - 1] >= sK[x];
+    } else {
+        for (u64 x = k0 + tid; x < k1; x += NT) bad |= x > 0 && g3.K[x - 1] >= g3.K[x];
+    }
+    // ---- 3. matched pairs: rows from LDS, then OIDs and name offsets ----
+    u32 ra[IPT], rb[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const bool m = (rec[k] >> 25) == R_MATCH;
+        const u32 ia = rec[k] & 0xFFF, jb = (rec[k] >> 12) & 0xFFF;
+        ra[k] = PERM ? (m ? sOrdO[ia] : 0u) : (u32)q.i0 + ia;
+        rb[k] = PERM ? (m ? sOrdT[jb] : 0u) : (u32)q.j0 + jb;
+    }
+    u32 oa0[IPT], oa1[IPT], ob0[IPT], ob1[IPT];
+    if (HASH && lnames) {
+        const u32* offA = (const u32*)g.nameOffA;
+        const u32* offB = (const u32*)g.nameOffB;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const bool m = (rec[k] >> 25) == R_MATCH;
+            const u64 i = m ? ra[k] : rA0, j = m ? rb[k] : rB0;
+            oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
+            ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
+        }
+    }
+    tile_oid_cmp<IPT>(g, rec, ra, rb);
+    bool ne = false;
+    if (HASH && lnames) {
+        const u32 nm = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_nm;
+        const u32 baseA = nm + rnA.skew, baseB = nm + 16 * rnA.nch + rnB.skew;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            if ((rec[k] >> 25) != R_MATCH) continue;
+            const u32 la = oa1[k] - oa0[k], lb = ob1[k] - ob0[k];
+            if (PERM && (ra[k] < rA0 || ra[k] >= rA1 || rb[k] < rB0 || rb[k] >= rB1))
+                ne |= !names_eq(g.nameA, g.nameOffA, ra[k], g.nameB, g.nameOffB, rb[k]);
+            else
+                ne |= la != lb || !lds_eq_bytes(baseA + (oa0[k] - (u32)nmA0), baseB + (ob0[k] - (u32)nmB0), la);
+        }
+    } else if (HASH) {
+        u32 act = 0;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
+        ne |= names_ne_batch<IPT, 8>(g.nameA, g.nameOffA, ra, g.nameB, g.nameOffB, rb, act) != 0;
+    }
+    if (bad) atomicOr(g.err, 1u);
+    // ---- the paths where ours and theirs differ, compacted in path order ----
+    u32 dif = 0, clean = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u32 kind = rec[k] >> 25, chg = (rec[k] >> 24) & 1;
+        dif |= (u32)(kind == R_DEL || kind == R_INS || (kind == R_MATCH && chg)) << k;
+        clean += kind == R_MATCH && !chg;
+    }
+    u32 od = 0, wd = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const u64 bd = __ballot((dif >> k) & 1);
+        od += __builtin_amdgcn_mbcnt_hi((u32)(bd >> 32), __builtin_amdgcn_mbcnt_lo((u32)bd, 0));
+        wd += __popcll(bd);
+    }
+    if (lane == 0) s_wave[wid] = wd;
+    __syncthreads();
+    u32 ndif = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const u32 x = s_wave[w];
+        if (w < wid) od += x;
+        ndif += x;
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; k++)
+        if ((dif >> k) & 1) s_drec[od++] = rec[k];
+    __syncthreads();  // (s_wave reused below)
+    const u64 nk = k1e - k0;
+    const int rounds = nk ? 64 - __clzll((long long)nk) : 0;  // wave-uniform
+    u32 tc = 0, tm = 0;
+    u32* sc = g3.stage_conf + tile * (u64)C2_STAGE * 3;
+    uint2* sm = g3.stage_md + tile * (u64)C2_STAGE;
+    const u32 nmb = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_nm;
+    for (u32 c0 = 0; c0 < ndif; c0 += NT) {  // block-uniform
+        const u32 x = c0 + tid;
+        const bool act = x < ndif;
+        const u32 r0 = act ? s_drec[x] : 0u;
+        const u32 kind = r0 >> 25, ia = r0 & 0xFFF, jb = (r0 >> 12) & 0xFFF;
+        const u64 key = kind == R_INS ? sB[jb] : sA[ia];
+        u64 lo = 0, hi = act ? nk : 0;
+        for (int it = 0; it < rounds; it++) {
+            const u64 m = (lo + hi) >> 1;
+            const u64 mi = m < nk ? m : (nk ? nk - 1 : 0);
+            const u64 v = lk ? sK[mi] : g3.K[k0 + mi];
+            const bool on = lo < hi, lt = v < key;
+            lo = on && lt ? m + 1 : lo;
+            hi = on && !lt ? m : hi;
+        }
+        const bool found = act && lo < nk && (lk ? sK[lo] : g3.K[k0 + lo]) == key;
+        const u32 ik = found ? (u32)(k0 + lo) : KD_NONE;
+        const u32 io = act && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
+        const u32 itt = act && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
+        // ---- 4. rows (LDS), then the three OIDs and the name offsets ----
+        u32 rk3 = ik, ro = io, rt = itt;
+        if (PERM) {
+            rk3 = ik != KD_NONE ? (lk ? sOrdK[lo] : *(gp32)(g3.ordK + ik)) : KD_NONE;
+            ro = io != KD_NONE ? sOrdO[ia] : KD_NONE;
+            rt = itt != KD_NONE ? sOrdT[jb] : KD_NONE;
+        }
+        const gp32 pk = rk3 != KD_NONE ? (gp32)(g3.oidK + 20ull * rk3) : (gp32)g.dummy;
+        const gp32 po = ro != KD_NONE ? (gp32)(g.oidA + 20ull * ro) : (gp32)g.dummy;
+        const gp32 pt = rt != KD_NONE ? (gp32)(g.oidB + 20ull * rt) : (gp32)g.dummy;
+        // (HASH) a matched ancestor path must carry the same filename as ours' (else theirs')
+        const bool chk = HASH && ik != KD_NONE && (io != KD_NONE || itt != KD_NONE);
+        const bool side_o = io != KD_NONE;
+        const u32 srow = side_o ? ro : rt;
+        u64 kn0 = 0, kn1 = 0, sn0 = 0, sn1 = 0;
+        if (HASH) {
+            const u64* offS = side_o ? g.nameOffA : g.nameOffB;
+            kn0 = g3.nameOffK[chk ? rk3 : 0]; kn1 = g3.nameOffK[chk ? rk3 + 1 : 0];
+            sn0 = offS[chk ? srow : 0]; sn1 = offS[chk ? srow + 1 : 0];
+        }
+        u32 dko = 0, dkt = 0;
+#pragma unroll
+        for (int w = 0; w < 5; w++) {
+            const u32 xk = pk[w];
+            dko |= xk ^ po[w];
+            dkt |= xk ^ pt[w];
+        }
+        // ---- 5. the ancestor's name (HBM) against the path's (LDS, else HBM) ----
+        if (HASH && chk) {
+            const u32 len = (u32)(kn1 - kn0);
+            if (len != (u32)(sn1 - sn0)) {
+                ne = true;
+            } else {
+                const bool in_lds = lnames && (side_o ? (srow >= rA0 && srow < rA1) : (srow >= rB0 && srow < rB1));
+                if (in_lds) {
+                    const u32 sb = side_o ? nmb + rnA.skew + (u32)(sn0 - nmA0) : nmb + 16 * rnA.nch + rnB.skew + (u32)(sn0 - nmB0);
+                    ne |= !glb_lds_name_eq(g3.nameK, kn0, len, sb);
+                } else {
+                    ne |= !names_eq(g3.nameK, g3.nameOffK, rk3, side_o ? g.nameA : g.nameB, side_o ? g.nameOffA : g.nameOffB,
+                                    srow);
+                }
+            }
+        }
+        const bool pa = ik != KD_NONE, pO = io != KD_NONE, pT = itt != KD_NONE;
+        const bool a_eq_o = pa == pO && (!pa || dko == 0);
+        const bool a_eq_t = pa == pT && (!pa || dkt == 0);
+        const bool md = act && a_eq_o;
+        const bool cf = act && !a_eq_o && !a_eq_t;
+        clean += (act && !a_eq_o && a_eq_t && pO) || (md && pT);
+        u32 tot;
+        const u32 off = block_excl_scan<NT>((u32)cf | (u32)md << 16, s_wave, &tot);
+        if (cf) {
+            u32* o = sc + 3 * (tc + (off & 0xFFFF));
+            o[0] = ik; o[1] = io; o[2] = itt;
+        }
+        if (md) sm[tm + (off >> 16)] = make_uint2(io, itt);
+        tc += tot & 0xFFFF;
+        tm += tot >> 16;
+    }
+    if (ne) atomicOr(g.err, 2u);
+    const u32 tcl = block_sum<NT>(clean, s_wave);
+    if (tid == 0) {
+        u32* cc = g.tile_cnt + 4 * tile;
+        cc[0] = tcl; cc[1] = tm; cc[2] = 0; cc[3] = tc;
+        u64* gs = g.gsum + 2 * (tile / C2_GROUP);
+        atomicAdd((unsigned long long*)gs, (unsigned long long)(tc | (u64)tm << 32));
+        atomicAdd((unsigned long long*)gs + 1, (unsigned long long)tcl);
+    }
+}
+
 // the three-way merge through k_join3 (sides device-resident; ord* non-null: late materialisation)
 int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd_side& T, u32* d_conf, uint2* d_md,
                        u64* d_counts, u32* d_err, const u32* ordK, const u32* ordO, const u32* ordT) {
     const u64 nK = K.n, nO = O.n, nT = T.n, total = nO + nT;
     const bool hash = K.key_mode == KD_KEY_HASH;
     const bool perm = ordK || ordO || ordT;
-    constexpr int TILE = J3_TILE;
+    // merge3_split: the join stages candidates (a, o, t) and k_resolve3 applies the rule (C4, r4n:
+    // 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
+    const bool split = ctx->opt.merge3_split == 1;
+    const bool j3_ol = ctx->opt.j3_ol == 1;  // (sorted-form sides' OIDs staged with the keys)
+    const bool v2 = ctx->opt.j3_v != 0 && !split && !(j3_ol && !perm);  // k_join3b
+    const int TILE = v2 ? J3B_TILE : J3_TILE;
     if (hash) KD_CHECK((nK == 0 || (K.name && K.name_off)) && (nO == 0 || (O.name && O.name_off)) &&
                        (nT == 0 || (T.name && T.name_off)), "merge3: KD_KEY_HASH needs filenames");
     const u64 ntiles = (total + TILE - 1) / TILE;
@@ -1324,14 +1679,23 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     const u64* kK = (const u64*)P(K.key, nK);
     rc = launch(ctx, "k_partition2", [&] {
         unsigned nb = (unsigned)((ntiles + C2_PG - 1) / C2_PG);
-        hipLaunchKernelGGL(k_partition2<TILE>, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kO, nO, kT, nT, ntiles,
-                           (u64*)part, d_counts, d_err, (u64*)gsum, n_zero);
+        if (v2) hipLaunchKernelGGL(k_partition2<J3B_TILE>, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kO, nO, kT, nT, ntiles,
+                                   (u64*)part, d_counts, d_err, (u64*)gsum, n_zero);
+        else hipLaunchKernelGGL(k_partition2<J3_TILE>, dim3(nb), dim3(C2_PNT), 0, ctx->stream, kO, nO, kT, nT, ntiles,
+                                (u64*)part, d_counts, d_err, (u64*)gsum, n_zero);
     });
     if (rc) return rc;
+    void* nsplit = nullptr;
+    if (v2 && hash && (rc = ensure(ctx, "c3.nsplit", 4 * (ntiles + 1) * sizeof(u64), &nsplit))) return rc;
     rc = launch(ctx, "k_apart3", [&] {
         const u64 lanes = 8 * (ntiles + 1);
-        hipLaunchKernelGGL(k_apart3, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, ctx->stream, kO, nO, kT, nT,
-                           (const u64*)part, ntiles, TILE, kK, nK, (u64*)apart);
+        if (v2)
+            hipLaunchKernelGGL(k_apart3b, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, ctx->stream, kO, nO, kT, nT,
+                               (const u64*)part, ntiles, TILE, kK, nK, (u64*)apart, (const u64*)P(O.name_off, nO),
+                               (const u64*)P(T.name_off, nT), perm ? J3B_HALO : (u64)0, (u64*)nsplit);
+        else
+            hipLaunchKernelGGL(k_apart3, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, ctx->stream, kO, nO, kT, nT,
+                               (const u64*)part, ntiles, TILE, kK, nK, (u64*)apart);
     });
     if (rc) return rc;
     Join3Args a;
@@ -1352,10 +1716,7 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     a.K = kK; a.oidK = (const u8*)P(K.oid, nK); a.nameK = (const u8*)P(K.name, nK);
     a.nameOffK = (const u64*)P(K.name_off, nK); a.ordK = (const u32*)P(ordK, nK); a.nK = nK;
     a.apart = (const u64*)apart; a.stage_conf = (u32*)sconf; a.stage_md = (uint2*)smd;
-    // merge3_split: the join stages candidates (a, o, t) and k_resolve3 applies the rule (C4, r4n:
-    // 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
-    const bool split = ctx->opt.merge3_split == 1;
-    const bool j3_ol = ctx->opt.j3_ol == 1;  // (sorted-form sides' OIDs staged with the keys)
+    a.nsplit = (const u64*)nsplit;
     void *cand3 = nullptr, *c2 = nullptr;
     if (split) {
         if ((rc = ensure(ctx, "c3.cand3", (total + 1) * 12, &cand3))) return rc;
@@ -1366,6 +1727,11 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
         if (split) {
             if (hash) { if (perm) KD_J3(true, true, true); else KD_J3(true, false, true); }
             else { if (perm) KD_J3(false, true, true); else KD_J3(false, false, true); }
+        } else if (v2) {
+#define KD_J3B(H, PM) hipLaunchKernelGGL((k_join3b<C2_NT, J3B_IPT, H, PM>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
+            if (hash) { if (perm) KD_J3B(true, true); else KD_J3B(true, false); }
+            else { if (perm) KD_J3B(false, true); else KD_J3B(false, false); }
+#undef KD_J3B
         } else if (j3_ol && !perm) {
             if (hash) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, true, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a);
             else hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, false, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a);

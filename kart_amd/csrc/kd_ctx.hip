@@ -314,6 +314,7 @@ const OptDef OPTS[] = {
     {"merge3_join", "KD_MERGE3_JOIN", nullptr, &kd_opts::merge3_join, nullptr},
     {"merge3_split", "KD_MERGE3_SPLIT", nullptr, &kd_opts::merge3_split, nullptr},
     {"j3_ol", "KD_J3_OL", nullptr, &kd_opts::j3_ol, nullptr},
+    {"j3_v", "KD_J3_V", nullptr, &kd_opts::j3_v, nullptr},
     {"j2_oidlds_min", "KD_J2_OIDLDS_MIN", nullptr, nullptr, &kd_opts::j2_oidlds_min},
     {"j2r", "KD_J2R", nullptr, &kd_opts::j2r, nullptr},
     {"fd_stream", "KD_FD_STREAM", nullptr, &kd_opts::fd_stream, nullptr},

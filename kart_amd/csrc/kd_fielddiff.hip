@@ -624,6 +624,73 @@ __device__ __forceinline__ u32 payload_eq(const WVal& a, const BL& A, u32 pa, co
     return range_eq(A, pa + a.hdr(), B, pb + b.hdr(), n, key, q);
 }
 
+// ---- the lockstep fast path: a value's size and class from its type byte alone ----
+// Two encodings of one msgpack type byte are equal values (Python ==) exactly when their bytes are
+// equal — for nil, bool, every int width, str, bin and ext — except floats (NaN != NaN, -0.0 ==
+// 0.0); and two byte-like values (str / bin / ext) of different payload lengths always differ.
+// Those cases — nearly every column of every update — are settled from the raw bytes, without the
+// number / payload extraction of decode_w; the rest (mixed type bytes: int vs float, str8 vs fixstr,
+// ext8 vs bin8 of one length) take decode_w + scalar_eq.
+struct FVal {
+    u32 t;     // type byte
+    u32 cls;   // MpTab class (7 = not a field value)
+    u32 hdr;   // header bytes
+    u32 len;   // payload length (numbers: their width)
+    u32 used;  // hdr + len, 0 = invalid (nested value, truncated, or an ext 'G' that is no GeoPackage)
+    u64 be;    // bytes 1..8 big-endian (float bits)
+};
+
+__device__ __forceinline__ FVal fast_decode(u32 x0, u32 x1, u32 x2, u32 avail) {
+    FVal f;
+    f.t = x0 & 0xff;
+    const u32 e = mp_entry(f.t);
+    f.cls = e & 7;
+    f.hdr = (e >> 3) & 7;
+    const u32 plen = (e >> 6) & 31, lenw = (e >> 11) & 7;
+    const u64 lo = (u64)x0 | (u64)x1 << 32;
+    f.be = __builtin_bswap64((lo >> 8) | (u64)x2 << 56);
+    f.len = lenw ? (u32)(f.be >> (64 - 8 * lenw)) : plen;
+    const u64 used = (u64)f.hdr + f.len;
+    bool ok = f.cls != 7 && used <= avail;
+    if (f.cls == V_EXT) {  // ext 'G': b"" -> None; else it must start "GP" (Geometry())
+        const u32 et = (u32)(lo >> (8 * (f.hdr - 1))) & 0xff;
+        const u32 g0 = (u32)(lo >> (8 * f.hdr)) & 0xff, g1 = (u32)(lo >> (8 * f.hdr + 8)) & 0xff;
+        ok = ok && (et != 'G' || f.len == 0 || (f.len >= 2 && g0 == 'G' && g1 == 'P'));
+    }
+    f.used = ok ? (u32)used : 0u;
+    return f;
+}
+
+// bytes [0, n) of two 12-byte windows differ (n <= 12)
+__device__ __forceinline__ bool win_ne(u32 a0, u32 a1, u32 a2, u32 b0, u32 b1, u32 b2, u32 n) {
+    const u32 m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1;
+    const u32 m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1;
+    const u32 m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1;
+    return (((a0 ^ b0) & m0) | ((a1 ^ b1) & m1) | ((a2 ^ b2) & m2)) != 0;
+}
+
+// the fast comparison when it applies: 0 equal, 1 changed, 3 queued; 2 = not settled here
+template <class BL>
+__device__ __forceinline__ u32 fast_eq(const FVal& a, u32 a0, u32 a1, u32 a2, const BL& A, u32 pa, const FVal& b, u32 b0,
+                                       u32 b1, u32 b2, const BL& B, u32 pb, int key, const FdQueue& q) {
+    const bool byt_a = a.cls == V_STR || a.cls == V_BYTES || a.cls == V_EXT;
+    const bool byt_b = b.cls == V_STR || b.cls == V_BYTES || b.cls == V_EXT;
+    if (a.t != b.t) return byt_a && byt_b && a.len != b.len ? 1u : 2u;
+    if (a.cls == V_FLOAT) {  // same width: equal bits and not NaN, or both zeros
+        const u32 w = a.len;  // 4 or 8
+        const u64 xa = a.be >> (64 - 8 * w), xb = b.be >> (64 - 8 * w);
+        const u64 mag = w == 8 ? 0x7FFFFFFFFFFFFFFFull : 0x7FFFFFFFull;
+        const u64 inf = w == 8 ? 0x7FF0000000000000ull : 0x7F800000ull;
+        const bool nan = (xa & mag) > inf;
+        return (xa == xb && !nan) || ((xa | xb) & mag) == 0 ? 0u : 1u;
+    }
+    if (byt_a && a.len != b.len) return 1u;
+    if (a.used <= 12) return win_ne(a0, a1, a2, b0, b1, b2, a.used) ? 1u : 0u;
+    // a long payload: the equal headers (type, length, ext code) are in the windows; the payloads
+    if (win_ne(a0, a1, a2, b0, b1, b2, a.hdr)) return 1u;
+    return range_eq(A, pa + a.hdr, B, pb + a.hdr, a.len, key, q);
+}
+
 template <class BL>
 __device__ __forceinline__ u32 rd_decode(const BL& b, u32 p, WVal& v) {
     u32 x0, x1, x2;
@@ -688,17 +755,25 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
         const auto kov = tb.key_of_val + (u64)li_o * tb.maxv;
         u32 pa = po, pb = pn;
         for (u32 v = 0; v < cvo; v++) {
-            WVal a, b;
-            const u32 ca = rd_decode(A, pa, a), cb = rd_decode(B, pb, b);
-            if (!ca || !cb) return 4;
+            u32 a0, a1, a2, b0, b1, b2;
+            rd12(A, pa, a0, a1, a2);
+            rd12(B, pb, b0, b1, b2);
+            const FVal fa = fast_decode(a0, a1, a2, A.len - pa), fb = fast_decode(b0, b1, b2, B.len - pb);
+            if (!fa.used || !fb.used) return 4;
             const int k = v < (u32)tb.maxv ? kov[v] : -1;
             if (k >= 0) {
-                u32 r = scalar_eq(a, b);
-                if (r == 2) r = payload_eq(a, A, pa, b, B, pb, k, q);
+                u32 r = fast_eq(fa, a0, a1, a2, A, pa, fb, b0, b1, b2, B, pb, k, q);
+                if (r == 2) {  // mixed type bytes: the full decode
+                    WVal a, b;
+                    decode_w(a0, a1, a2, A.len - pa, a);
+                    decode_w(b0, b1, b2, B.len - pb, b);
+                    r = scalar_eq(a, b);
+                    if (r == 2) r = payload_eq(a, A, pa, b, B, pb, k, q);
+                }
                 if (r == 1) set_bit(mk, m, k);
             }
-            pa += ca;
-            pb += cb;
+            pa += fa.used;
+            pb += fb.used;
         }
         if (pa != A.len || pb != B.len) return 4;  // trailing bytes: unpackb raises ExtraData
         return 0;

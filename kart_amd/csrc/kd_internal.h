@@ -68,6 +68,7 @@ struct kd_opts {
     int merge3_join = 1;             // KD_MERGE3_JOIN: 0 = round 3's two-step merge (classify2 + k_resolve3)
     int merge3_split = 0;            // KD_MERGE3_SPLIT: 1 = k_join3 stages candidates, k_resolve3 applies the rule
     int j3_ol = 0;                   // KD_J3_OL: 1 = k_join3 stages ours'/theirs' OIDs in LDS (sorted-form sides)
+    int j3_v = 1;                    // KD_J3_V: 1 = k_join3b (one DMA batch per tile), 0 = k_join3
     uint64_t j2_oidlds_min = 1ull << 26;  // KD_J2_OIDLDS_MIN: k_join2 stages OIDs in LDS from this many entries
     int j2r = 0;                     // KD_J2R: 1 = the persistent register-prefetched k_join2r
     int fd_stream = -1;              // KD_FD_STREAM: -1 auto, 0 windowed k_fielddiff, 1 streamed k_fielddiff_s

@@ -591,79 +591,127 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pk
     }
 }
 
-// ---- segmented sort: keys ascending in their top bits (a hash side in walk order: the bucket)
+// ---- segmented sort: keys ascending in their top bits (a side in walk order: the leaf tree's bucket)
 // ordered by the whole key inside each run of equal top bits.  One workgroup per tile of SEG_T
-// entries: the tile's keys plus SEG_H on each side go to LDS in one coalesced pass; each entry's
-// place = the start of its segment + the number of smaller keys in it, both found by scanning its
-// neighbours in LDS (segments average a few entries).  A segment reaching past the halo is scanned
-// in global memory instead.  err |= 1: a duplicate key or descending top bits; 4: a segment longer
-// than RS_SEG_MAX (the caller sorts with kd_sort_side_into instead).
+// entries: the tile's keys plus SEG_H = RS_SEG_MAX on each side go to LDS in one coalesced pass (so
+// every run of at most RS_SEG_MAX entries that touches the tile lies inside); the runs' bounds come
+// from a block-wide max-scan of the run heads and a min-scan of the next heads; each entry's place
+// = its run's start + the number of smaller keys in the run, counted with independent LDS reads (the
+// lanes of one run read the same word: a broadcast).  err |= 1: a duplicate key or descending top
+// bits; 4: a run longer than RS_SEG_MAX (the caller sorts with kd_sort_side_into instead).
+// (Round 4's form scanned each entry's neighbours one dependent LDS read at a time: 0.33 ms per 50M
+// C4 side of ~3-entry leaf trees, but 4.2 ms per 100M C3 side of ~64-entry ones.)
 constexpr int RS_SEG_MAX = 512;
-constexpr int SEG_NT = 256, SEG_IPT = 8, SEG_T = SEG_NT * SEG_IPT, SEG_H = 64;
+constexpr int SEG_NT = 256, SEG_IPT = 8, SEG_T = SEG_NT * SEG_IPT, SEG_H = RS_SEG_MAX;
+constexpr int SEG_E = SEG_T + 2 * SEG_H, SEG_EPT = SEG_E / SEG_NT;  // staged entries, per thread (contiguous)
+static_assert(SEG_E % SEG_NT == 0 && SEG_E < 65536, "segmented-sort tile shape");
+
+// block-wide inclusive scan (op = max or min) of one u32 per thread, in thread order
+template <bool MAX>
+__device__ __forceinline__ u32 seg_block_scan(u32 v, u32* s_w, bool reverse) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int NW = SEG_NT / 64;
+    u32 x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = reverse ? __shfl_down(x, o, 64) : __shfl_up(x, o, 64);
+        const bool in = reverse ? lane + o < 64 : lane >= o;
+        if (in) x = MAX ? (y > x ? y : x) : (y < x ? y : x);
+    }
+    if (lane == (reverse ? 0 : 63)) s_w[wv] = x;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const u32 y = s_w[w];
+        if (reverse ? w > wv : w < wv) x = MAX ? (y > x ? y : x) : (y < x ? y : x);
+    }
+    __syncthreads();
+    return x;
+}
+
 __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key, u64 n, int shift, u64* __restrict__ kout,
                                                      u32* __restrict__ order, u32* __restrict__ err) {
-    __shared__ u64 s_k[SEG_T + 2 * SEG_H];
+    __shared__ u64 s_k[SEG_E];
+    __shared__ u16 s_st[SEG_E];  // start of the entry's run (LDS index)
+    __shared__ u16 s_en[SEG_E];  // end (exclusive; SEG_E fits 16 bits)
+    __shared__ u32 s_w[SEG_NT / 64];
     const int tid = threadIdx.x;
     const u64 t0 = (u64)blockIdx.x * SEG_T;
     const i64 g0 = (i64)t0 - SEG_H;  // global index of s_k[0]
-    const u64 glo = t0 >= (u64)SEG_H ? t0 - SEG_H : 0, ghi = min<u64>(n, t0 + SEG_T + SEG_H);
-    for (int x = tid; x < SEG_T + 2 * SEG_H; x += SEG_NT) {
-        const i64 g = g0 + x;
-        s_k[x] = (g >= 0 && (u64)g < n) ? key[g] : 0;
+    const int vlo = g0 < 0 ? (int)(-g0) : 0;                                   // valid LDS entries: [vlo, vhi)
+    const int vhi = (int)min<i64>((i64)SEG_E, (i64)n - g0);
+    for (int x = tid; x < SEG_E; x += SEG_NT) s_k[x] = (x >= vlo && x < vhi) ? key[g0 + x] : 0;
+    __syncthreads();
+    // run heads: an entry whose top bits differ from its predecessor's (or the first valid entry);
+    // invalid entries are runs of their own.  Starts: the last head at or before the entry (a max-scan
+    // of head index + 1, 0 = none yet); ends: the first head after it (a min-scan from the right)
+    auto is_head = [&](int x) {
+        return !(x >= vlo && x < vhi) || x == vlo || (s_k[x] >> shift) != (s_k[x - 1] >> shift);
+    };
+    const int x0 = tid * SEG_EPT;
+    u32 st_loc[SEG_EPT], en_loc[SEG_EPT];
+    u32 runp1 = 0;
+    bool bad1 = false;
+#pragma unroll
+    for (int j = 0; j < SEG_EPT; j++) {
+        const int x = x0 + j;
+        const bool head = is_head(x);
+        if (head) runp1 = (u32)x + 1;
+        st_loc[j] = runp1;
+        // descending top bits: checked at the heads of the tile's own range (each boundary once)
+        if (head && x > vlo && x < vhi && x >= SEG_H && x < SEG_H + SEG_T)
+            bad1 |= (s_k[x] >> shift) < (s_k[x - 1] >> shift);
+    }
+    u32 nxt = SEG_E;
+#pragma unroll
+    for (int j = SEG_EPT - 1; j >= 0; j--) {
+        en_loc[j] = nxt;
+        if (is_head(x0 + j)) nxt = (u32)(x0 + j);
+    }
+    __shared__ u32 s_inc[SEG_NT];
+    const u32 fwd = seg_block_scan<true>(runp1, s_w, false);
+    s_inc[tid] = fwd;
+    __syncthreads();
+    const u32 before = tid ? s_inc[tid - 1] : 0u;  // the last head before this thread's chunk (+1)
+    __syncthreads();
+    const u32 bwd = seg_block_scan<false>(nxt, s_w, true);
+    s_inc[tid] = bwd;
+    __syncthreads();
+    const u32 after = tid + 1 < SEG_NT ? s_inc[tid + 1] : (u32)SEG_E;  // the first head after the chunk
+#pragma unroll
+    for (int j = 0; j < SEG_EPT; j++) {
+        s_st[x0 + j] = (u16)((st_loc[j] ? st_loc[j] : before) - 1);
+        s_en[x0 + j] = (u16)(en_loc[j] != (u32)SEG_E ? en_loc[j] : after);
     }
     __syncthreads();
-    u32 bad = 0;
+    // ranks of the tile's own entries
+    u32 bad = bad1 ? 1u : 0u;
 #pragma unroll 2
     for (int j = 0; j < SEG_IPT; j++) {
-        const u64 i = t0 + (u64)j * SEG_NT + tid;  // consecutive lanes: consecutive entries
-        if (i >= n) break;
-        const int x = (int)(i - (u64)g0);
-        const u64 k = s_k[x], seg = k >> shift;
-        u32 rank = 0, left = 0, right = 0;
-        bool stop = false;
-        for (u64 p = i; p > glo && !stop; p--) {  // earlier entries of the segment, from LDS
-            const u64 v = s_k[(int)(p - 1 - (u64)g0)];
-            if ((v >> shift) != seg) {
-                bad |= (v >> shift) > seg ? 1u : 0u;
-                stop = true;
-            } else {
-                rank += v < k;
-                bad |= v == k ? 1u : 0u;
-                left++;
-            }
+        const int x = SEG_H + j * SEG_NT + tid;  // consecutive lanes: consecutive entries
+        if (x >= vhi) break;
+        const u64 k = s_k[x];
+        const u32 s0 = s_st[x], e0 = s_en[x];
+        if ((s0 == 0 && g0 > 0) || (e0 == (u32)SEG_E && g0 + SEG_E < (i64)n) || e0 - s0 > (u32)RS_SEG_MAX) {
+            bad |= 4u;  // a run longer than RS_SEG_MAX (or reaching past the halo)
+            continue;
         }
-        if (!stop && i - left > 0) {  // the segment runs on past the halo: continue in global memory
-            for (u64 p = i - left; p > 0 && left < RS_SEG_MAX; p--) {
-                const u64 v = key[p - 1];
-                if ((v >> shift) != seg) {
-                    bad |= (v >> shift) > seg ? 1u : 0u;
-                    break;
-                }
-                rank += v < k;
-                bad |= v == k ? 1u : 0u;
-                left++;
-            }
+        u32 rank = 0, dup = 0;
+        u32 y = s0;
+        for (; y + 4 <= e0; y += 4) {
+            const u64 a = s_k[y], b = s_k[y + 1], c = s_k[y + 2], d = s_k[y + 3];
+            rank += (a < k) + (b < k) + (c < k) + (d < k);
+            dup += (a == k) + (b == k) + (c == k) + (d == k);
         }
-        stop = false;
-        for (u64 q = i + 1; q < ghi && !stop; q++) {  // later entries, from LDS
-            const u64 v = s_k[(int)(q - (u64)g0)];
-            if ((v >> shift) != seg) stop = true;
-            else { rank += v < k; right++; }
+        for (; y < e0; y++) {
+            const u64 a = s_k[y];
+            rank += a < k;
+            dup += a == k;
         }
-        if (!stop && i + 1 + right < n) {
-            for (u64 q = i + 1 + right; q < n && right < RS_SEG_MAX; q++) {
-                const u64 v = key[q];
-                if ((v >> shift) != seg) break;
-                rank += v < k;
-                right++;
-            }
-        }
-        if (left + right >= (u32)RS_SEG_MAX) bad |= 4u;  // the segment is longer than RS_SEG_MAX
-        const u64 dst = i - left + rank;
-        if (dst < n) {
-            kout[dst] = k;
-            order[dst] = (u32)i;
-        }
+        bad |= dup > 1 ? 1u : 0u;
+        const u64 dst = (u64)(g0 + (i64)s0) + rank;
+        kout[dst] = k;
+        order[dst] = (u32)(g0 + x);
     }
     if (__ballot(bad != 0) && bad) atomicOr(err, bad);
 }

@@ -1,11 +1,12 @@
 """End-to-end `kart diff HEAD^ HEAD` of a Kart-shaped git repository through the drop-in path:
 object store + walk (gitsource) -> key packing -> kd_diff2 -> Delta objects -> batched blob read +
 kd_fielddiff, timed stage by stage, next to `git diff-tree -r` (the tree diff libgit2 does for the
-reference) and the reference's own Python path rate (0.54 M feature-pairs/s).
+reference).  The reference's own Python path is measured apart, in the build container
+(scripts/ref_path_bench.py, on repositories built by this script's build_parallel).
 
 The repository: N points features (IntPathEncoder paths, the reference's feature blob encoding,
-EPSG:4326), a second commit with 1 % updates / deletes / inserts.  Prints one JSON object.
-usage: python scripts/e2e_repo_bench.py [--n 1000000] [--out FILE]   (GPU needed for the diff)
+EPSG:4326), a second commit with --edits update / delete / insert fractions.  Prints one JSON object.
+usage: python scripts/e2e_repo_bench.py [--n 1000000] [--edits 0.08,0.01,0.01] [--out FILE]   (GPU needed)
 """
 import argparse
 import hashlib
@@ -24,7 +25,6 @@ from kart_amd import synth  # noqa: E402
 from kart_amd.schema import Legend  # noqa: E402
 
 DS = "nz_points"
-REFERENCE_RATE = 0.54e6  # the reference diff hot path, feature pairs / s, 1 core
 
 
 def _import_blobs(args):
@@ -59,18 +59,20 @@ def _blob_ids(gitdir, data, off, procs):
     return np.frombuffer(b"".join(ids), np.uint8).reshape(n, 20)
 
 
-def build_parallel(gitdir, n, seed=3, procs=16):
+def build_parallel(gitdir, n, seed=3, procs=16, edits=(0.01, 0.01, 0.01)):
     """the same repository as build(), with the blobs written by parallel fast-imports (packs of
-    blobs) and the two commits by one fast-import referencing them by id: for 10M features"""
+    blobs) and the two commits by one fast-import referencing them by id: for 10M features.
+    edits = (update, delete, insert) fractions of n"""
     subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
     legend = Legend(["c-fid"], [c["id"] for c in synth.POINT_SCHEMA[1:]])
     lh = legend.hexhash()
     rng = np.random.default_rng(seed)
     pks = np.arange(1, n + 1, dtype=np.int64)
     perm = rng.permutation(n)
-    k = n // 100
-    upd, dele = np.sort(perm[:k]), np.sort(perm[k:2 * k])
-    ins = np.arange(n + 1, n + 1 + k, dtype=np.int64)
+    ku, kd, ki = (int(n * f) for f in edits)
+    upd, dele = np.sort(perm[:ku]), np.sort(perm[ku:ku + kd])
+    ins = np.arange(n + 1, n + 1 + ki, dtype=np.int64)
+    k = kd
     inner = f"{DS}/.table-dataset"
     meta = _meta(inner, lh, legend)
     t0 = time.perf_counter()
@@ -115,7 +117,7 @@ def build_parallel(gitdir, n, seed=3, procs=16):
     finally:
         done.set()
     print(f"  commits written in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
-    return k
+    return ku + kd + ki
 
 
 def _meta(inner, lh, legend):
@@ -166,6 +168,34 @@ def build(gitdir, n, seed=3):
     return k
 
 
+def fielddiff_split(eng, od, oo, nd, no, old, new):
+    """kd_fielddiff on the update arenas split into its parts: H2D of both arenas (pinned staging by
+    the library), the device call on resident arenas (synchronised), D2H of the masks"""
+    import ctypes
+
+    from kart_amd import _native as N
+    from kart_amd.device import DevBlobs, DevBuf
+    from kart_amd.schema import FieldMaps
+
+    maps = FieldMaps(old.schema, old.legends, new.schema, new.legends)
+    n = int(oo.shape[0]) - 1
+    eng.sync()
+    t0 = time.perf_counter()
+    OB, NB = DevBlobs(eng, od, oo), DevBlobs(eng, nd, no)
+    eng.sync()
+    t1 = time.perf_counter()
+    masks, status = DevBuf(eng, 8 * max(n, 1) * maps.words), DevBuf(eng, max(n, 1))
+    ob, nb, km = OB.kd_blobs(), NB.kd_blobs(), maps.kd_maps()
+    N.check(eng.L.kd_fielddiff(eng.ctx, ctypes.byref(ob), ctypes.byref(nb), None, n, None, N.KD_MEM_DEVICE,
+                               ctypes.byref(km), masks.ptr, status.ptr, N.KD_MEM_DEVICE), "kd_fielddiff")
+    eng.sync()
+    t2 = time.perf_counter()
+    masks.download(np.uint64, n * maps.words)
+    t3 = time.perf_counter()
+    return {"h2d_s": round(t1 - t0, 4), "device_s": round(t2 - t1, 4), "d2h_s": round(t3 - t2, 4),
+            "arena_bytes": int(od.size + nd.size), "updates": n}
+
+
 def timed(fn):
     t0 = time.perf_counter()
     r = fn()
@@ -178,10 +208,13 @@ def main():
     ap.add_argument("--repo", default=None)
     ap.add_argument("--out", default=None)
     ap.add_argument("--procs", type=int, default=16, help="parallel blob writers when building the repository")
+    ap.add_argument("--edits", default="0.01,0.01,0.01",
+                    help="update,delete,insert fractions of n in the second commit (C3's mix: 0.08,0.01,0.01)")
     a = ap.parse_args()
-    gitdir = a.repo or f"/tmp/kart_e2e_{a.n}.git"
+    edits = tuple(float(x) for x in a.edits.split(","))
+    gitdir = a.repo or f"/tmp/kart_e2e_{a.n}_{a.edits.replace(',', '_')}.git"
     if not os.path.isdir(gitdir):
-        t, k = timed(lambda: build_parallel(gitdir, a.n, procs=a.procs))
+        t, k = timed(lambda: build_parallel(gitdir, a.n, procs=a.procs, edits=edits))
         print(f"built {gitdir} in {t:.1f} s", file=sys.stderr, flush=True)
     from kart_amd import dataset as D
     from kart_amd.engine import Engine
@@ -191,8 +224,10 @@ def main():
     t_git, out = timed(lambda: subprocess.run(["git", "--git-dir", gitdir, "diff-tree", "-r", "--name-only",
                                                "main^", "main", "--", feat], capture_output=True, check=True).stdout)
     n_git = out.count(b"\n")
-    res = {"n": a.n, "changed_paths": n_git, "git_diff_tree_s": round(t_git, 4),
-           "reference_path_s_estimate": round((a.n + a.n // 100) / REFERENCE_RATE, 2)}
+    res = {"n": a.n, "edits_update_delete_insert": list(edits), "changed_paths": n_git,
+           "git_diff_tree_s": round(t_git, 4),
+           "reference_path": "measured in the build container by scripts/ref_path_bench.py (the reference's own "
+                             "Dataset3.diff_feature + get_feature loop) at 1M and 3M: profiles/r05/ref_path_*.json"}
     t_eng = time.perf_counter()
     with Engine(0) as eng:
         res["engine_init_s"] = round(time.perf_counter() - t_eng, 4)  # context + the library's code object
@@ -223,14 +258,19 @@ def main():
             stages["field_diff_s"] = t
             stages["field_diff_parts_s"] = {k: round(v, 4) for k, v in fds.items()}
             total = time.perf_counter() - t0
+            # the field diff's kernel call split (outside total_s): H2D of the two update arenas, the
+            # device call on resident arenas, the masks' D2H
+            batch = D._live_batch(fd, old, new)
+            if batch is not None and batch.deltas:
+                (od, oo), (nd, no) = D._arena_pair(old, new, batch.old_leaf, batch.new_leaf)
+                stages["field_diff_split_s"] = fielddiff_split(eng, od, oo, nd, no, old, new)
             counts = fd.type_counts()
             assert sum(counts.values()) == n_git, (counts, n_git)
             assert all(d.changed_fields for d in fd.values() if d.type == "update")
             repo.close()
             res[label] = {**{k: round(v, 4) if isinstance(v, float) else v for k, v in stages.items()},
                           "total_s": round(total, 4),
-                          "counts": counts, "leaves": [int(old.n), int(new.n)],
-                          "speedup_vs_reference_path": round(res["reference_path_s_estimate"] / total, 1)}
+                          "counts": counts, "leaves": [int(old.n), int(new.n)]}
     s = json.dumps(res, indent=1)
     print(s)
     if a.out:

@@ -101,6 +101,8 @@ class GitRepo:
         self.gitdir = gitdir
         self.env = dict(os.environ, GIT_DIR=gitdir, GIT_INDEX_FILE=index_file)
         self._trees = {}
+        self._maps = {}
+        self._children = {}
         self._blobs = {}
         self._cat = None
 
@@ -115,6 +117,26 @@ class GitRepo:
 
     def tree(self, spec):
         return Tree(self, self.rev(spec + "^{tree}"), "")
+
+    def entry_map(self, oid):
+        """{name: entry} of a tree (libgit2 finds an entry by binary search in C; a dict keeps the shim's
+        lookups from dominating timings of the reference path)"""
+        m = self._maps.get(oid)
+        if m is None:
+            m = self._maps[oid] = {e[0]: e for e in self.ls_tree(oid)}
+        return m
+
+    def child(self, tree_oid, name):
+        """the Tree / Blob object of entry ``name`` of a tree, made once (pygit2 hands out C-backed
+        objects; the shim keeps its Python ones so a path lookup costs dict hits, not object builds)"""
+        key = (tree_oid, name)
+        c = self._children.get(key)
+        if c is None:
+            ent = self.entry_map(tree_oid).get(name)
+            if ent is None:
+                return None
+            c = self._children[key] = (Tree(self, ent[2], name) if ent[1] == "tree" else Blob(self, ent[2], name))
+        return c
 
     def ls_tree(self, oid):
         if oid not in self._trees:
@@ -255,12 +277,10 @@ class Tree:
         for part in [p for p in str(path).split("/") if p]:
             if not isinstance(node, Tree):
                 raise KeyError(path)
-            for ent in node._entries():
-                if ent[0] == part:
-                    node = node._child(ent)
-                    break
-            else:
+            nxt = node.repo.child(node.id, part)
+            if nxt is None:
                 raise KeyError(path)
+            node = nxt
         return node
 
     def diff_to_tree(self, other=None, flags=0, swap=False):
