@@ -376,9 +376,10 @@ int kd_sort_side_into(kd_ctx* ctx, const uint64_t* d_key_in, const uint8_t* d_oi
  * d_key_out [n] <- keys ascending, d_order [n] <- walk index of sorted entry k (the OIDs and
  * filenames stay in walk order: kd_diff2_device_perm / kd_merge3_device_perm read through it).
  * *d_err |= 1 on a duplicate key or descending bucket bits, 4 on a bucket of more than 512 entries
- * (then sort with kd_sort_side_into).  One kernel, no host sync. */
+ * (then sort with kd_sort_side_into).  max_seg: the longest bucket the caller knows of (kd_keys_scan's
+ * seg_max; 0 = unknown): at most 128 stages a smaller halo per tile.  One kernel, no host sync. */
 int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uint64_t* d_key_out, uint32_t* d_order,
-                           uint64_t n, int seg_bits, uint32_t* d_err);
+                           uint64_t n, int seg_bits, int max_seg, uint32_t* d_err);
 /* The deltas in pk order (DeltaDiff.sorted_items, kart/diff_structs.py:442-458; classify2 emits them in
  * git walk order): for KD_KEY_INT device sides and a device record list d_delta [cap] of (base | KD_NONE,
  * target | KD_NONE) records (classify2's deltas or updates) with *d_n of them, d_pk [cap] <- their pks

@@ -245,7 +245,7 @@ SIGNATURES = {
                                           ctypes.POINTER(KdKeysInfo)]),
     "kd_keys_scan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(KdKeysInfo)]),
     "kd_sort_segmented_into": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                               ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
+                                               ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "kd_delta_pk_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(KdSide), ctypes.POINTER(KdSide),
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),

@@ -592,6 +592,35 @@ __device__ __forceinline__ DenseLd dense_load(const GfArgs& a, const GfHeadArgs&
     return L;
 }
 
+// PP: the pairs run one chunk ahead of the heads, so a side the pair marks absent (an insert's old
+// side, a delete's new side: ~20 % of C5's delta sides) is loaded from the zero block, not from its
+// slot — those bytes never leave the cache
+__device__ __forceinline__ uint2 dense_pair(const GfArgs& a, const GfHeadArgs& g, u64 c, u64 n, int lane) {
+    const u64 d = c * 64 + lane;
+    const u64 dp = n ? (d < n ? d : n - 1) : 0;
+    const uint2 v = *(n ? (const uint2*)a.pairs + dp : (const uint2*)g.zeros);
+    return d < n ? head_slots(g, v, d) : make_uint2(KD_NONE, KD_NONE);
+}
+
+__device__ __forceinline__ DenseLd dense_load_pp(const GfHeadArgs& g, u64 c, u64 nchunk, uint2 pr, int lane) {
+    typedef const __attribute__((address_space(1))) u32x4* gx4;
+    DenseLd L;
+    const u64 cc = c < nchunk ? c : (nchunk ? nchunk - 1 : 0);
+    const u64 o = (cc * 64 + lane) * 48;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const bool pres = (s ? pr.y : pr.x) != KD_NONE;
+        const u64 base = pres ? (u64)g.head[s] + o : (u64)g.zeros;
+#pragma unroll
+        for (int k = 0; k < 3; k++) L.h[3 * s + k] = *(gx4)(base + 16 * k);
+    }
+    L.pr = pr;
+    return L;
+}
+
+#ifndef KD_GFD_PP
+#define KD_GFD_PP 1
+#endif
 #ifndef KD_GFD_PF
 #define KD_GFD_PF 1  // k_gf_dense prefetch depth (chunks ahead)
 #endif
@@ -615,12 +644,27 @@ __global__ __launch_bounds__(GF_NT) __attribute__((amdgpu_waves_per_eu(PF == 1 &
     u32x4* const wtr = s_tr + (TR ? wid * 6 * 64 : 0);
     const u64 wstride = (u64)gridDim.x * (GF_NT / 64);
     u64 c = (u64)blockIdx.x * (GF_NT / 64) + wid;
-    DenseLd A = dense_load<TR>(a, g, c, nchunk, n, lane);
+    constexpr bool PP = KD_GFD_PP && PF == 1 && !TR;
+    uint2 pr1 = make_uint2(KD_NONE, KD_NONE);
+    DenseLd A;
+    if (PP) {
+        A = dense_load_pp(g, c, nchunk, dense_pair(a, g, c, n, lane), lane);
+        pr1 = dense_pair(a, g, c + wstride, n, lane);
+    } else {
+        A = dense_load<TR>(a, g, c, nchunk, n, lane);
+    }
     DenseLd B;
     if (PF == 2) B = dense_load<TR>(a, g, c + wstride, nchunk, n, lane);
     for (; c < nchunk; c += wstride) {  // wave-uniform
         // the load PF chunks ahead first, so this chunk's wait leaves it in flight
-        DenseLd Nx = dense_load<TR>(a, g, c + PF * wstride, nchunk, n, lane);
+        DenseLd Nx;
+        if (PP) {
+            const uint2 pr2 = dense_pair(a, g, c + 2 * wstride, n, lane);
+            Nx = dense_load_pp(g, c + wstride, nchunk, pr1, lane);
+            pr1 = pr2;
+        } else {
+            Nx = dense_load<TR>(a, g, c + PF * wstride, nchunk, n, lane);
+        }
         const u64 d = c * 64 + lane;
         HeadLd L0, L1;
         if (TR) {

@@ -602,9 +602,9 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pk
 // (Round 4's form scanned each entry's neighbours one dependent LDS read at a time: 0.33 ms per 50M
 // C4 side of ~3-entry leaf trees, but 4.2 ms per 100M C3 side of ~64-entry ones.)
 constexpr int RS_SEG_MAX = 512;
-constexpr int SEG_NT = 256, SEG_IPT = 8, SEG_T = SEG_NT * SEG_IPT, SEG_H = RS_SEG_MAX;
-constexpr int SEG_E = SEG_T + 2 * SEG_H, SEG_EPT = SEG_E / SEG_NT;  // staged entries, per thread (contiguous)
-static_assert(SEG_E % SEG_NT == 0 && SEG_E < 65536, "segmented-sort tile shape");
+// halo SEG_H: RS_SEG_MAX, or 128 when the caller knows every run is at most that long (C4's ~3-entry
+// leaf trees: 0.34 vs 0.46 ms per 50M side; C3's ~64-entry ones likewise)
+constexpr int SEG_NT = 256, SEG_IPT = 8, SEG_T = SEG_NT * SEG_IPT, SEG_HS = 128;
 
 // block-wide inclusive scan (op = max or min) of one u32 per thread, in thread order
 template <bool MAX>
@@ -629,8 +629,11 @@ __device__ __forceinline__ u32 seg_block_scan(u32 v, u32* s_w, bool reverse) {
     return x;
 }
 
+template <int SEG_H>
 __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key, u64 n, int shift, u64* __restrict__ kout,
                                                      u32* __restrict__ order, u32* __restrict__ err) {
+    constexpr int SEG_E = SEG_T + 2 * SEG_H, SEG_EPT = SEG_E / SEG_NT;  // staged entries, per thread (contiguous)
+    static_assert(SEG_E % SEG_NT == 0 && SEG_E < 65536, "segmented-sort tile shape");
     __shared__ u64 s_k[SEG_E];
     __shared__ u16 s_st[SEG_E];  // start of the entry's run (LDS index)
     __shared__ u16 s_en[SEG_E];  // end (exclusive; SEG_E fits 16 bits)
@@ -997,7 +1000,7 @@ extern "C" int kd_sort_side(kd_ctx* ctx, uint64_t* d_key, uint8_t* d_oid, uint32
 }
 
 extern "C" int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uint64_t* d_key_out, uint32_t* d_order,
-                                      uint64_t n, int seg_bits, uint32_t* d_err) {
+                                      uint64_t n, int seg_bits, int max_seg, uint32_t* d_err) {
     KD_CHECK(ctx && d_err && (n == 0 || (d_key_in && d_key_out && d_order)), "kd_sort_segmented_into: NULL");
     KD_CHECK(n < 0xFFFFFFFFull, "kd_sort_segmented_into: side too large for uint32 indices");
     KD_CHECK(seg_bits > 0 && seg_bits < 64, "kd_sort_segmented_into: seg_bits %d", seg_bits);
@@ -1005,9 +1008,14 @@ extern "C" int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uin
     KD_HIP(hipSetDevice(ctx->device));
     if (n == 0) return KD_OK;
     const u64 ntiles = (n + SEG_T - 1) / SEG_T;
+    const bool small = max_seg > 0 && max_seg <= SEG_HS;
     return launch(ctx, "k_seg_sort", [&] {
-        hipLaunchKernelGGL(k_seg_sort, dim3((unsigned)ntiles), dim3(SEG_NT), 0, ctx->stream, d_key_in, n, 64 - seg_bits,
-                           d_key_out, d_order, d_err);
+        if (small)
+            hipLaunchKernelGGL(k_seg_sort<SEG_HS>, dim3((unsigned)ntiles), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
+                               64 - seg_bits, d_key_out, d_order, d_err);
+        else
+            hipLaunchKernelGGL(k_seg_sort<RS_SEG_MAX>, dim3((unsigned)ntiles), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
+                               64 - seg_bits, d_key_out, d_order, d_err);
     });
 }
 

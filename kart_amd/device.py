@@ -279,7 +279,7 @@ class DiffPipeline:
         L, ctx = self.eng.L, self.eng.ctx
         for (w, order, n, info), S in zip(self.walk, (self.A, self.B)):
             if self.segmented:
-                N.check(L.kd_sort_segmented_into(ctx, w.key.ptr, S.key.ptr, order.ptr, n, 24, self.seg_err.ptr),
+                N.check(L.kd_sort_segmented_into(ctx, w.key.ptr, S.key.ptr, order.ptr, n, 24, info.seg_max, self.seg_err.ptr),
                         "kd_sort_segmented_into")
             elif self.late:
                 N.check(L.kd_sort_side_into(ctx, w.key.ptr, None, S.key.ptr, None, order.ptr, n, None,
@@ -543,7 +543,12 @@ class MergePipeline:
         self._s = [x.kd_side() for x in self.S]
         self.segmented = bool(segmented)
         if self.segmented:
+            from . import packing
+
             self.seg_bits = shard.bucket_bits(ancestor.key_mode, ancestor.encoding)
+            # the longest leaf tree of each side (the host's key scan; a halo plan, not a check)
+            self.seg_max = [packing.keys_scan(x.key, x.key_mode).seg_max if self.seg_bits == 24 else 0
+                            for x in (ancestor, ours, theirs)]
             self.skey = [DevBuf(engine, 8 * max(x.n, 1)) for x in (ancestor, ours, theirs)]
             self.order = [DevBuf(engine, 4 * max(x.n, 1)) for x in (ancestor, ours, theirs)]
             for k, sb in zip(self._s, self.skey):
@@ -558,8 +563,8 @@ class MergePipeline:
     def sort_step(self):
         """(segmented) each side's buckets ordered by key"""
         L, ctx = self.eng.L, self.eng.ctx
-        for S, sk, od in zip(self.S, self.skey, self.order):
-            N.check(L.kd_sort_segmented_into(ctx, S.key.ptr, sk.ptr, od.ptr, S.n, self.seg_bits, self.counts.ptr + 40),
+        for S, sk, od, segmax in zip(self.S, self.skey, self.order, self.seg_max):
+            N.check(L.kd_sort_segmented_into(ctx, S.key.ptr, sk.ptr, od.ptr, S.n, self.seg_bits, segmax, self.counts.ptr + 40),
                     "kd_sort_segmented_into")
 
     def step(self):

@@ -210,8 +210,9 @@ def sort_on_device_perm(engine, keys, oids, info, encoding, paths, off):
     sorted_ok = False
     if encoding.key_mode == N.KD_KEY_HASH or 0 < info.seg_max <= SEG_SORT_MAX:
         flag.zero()
-        N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk_in.ptr, dk.ptr, dord.ptr, n,
-                                                shard.bucket_bits(encoding.key_mode, encoding), flag.ptr),
+        bits = shard.bucket_bits(encoding.key_mode, encoding)
+        N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk_in.ptr, dk.ptr, dord.ptr, n, bits,
+                                                info.seg_max if bits == 24 else 0, flag.ptr),
                 "kd_sort_segmented_into")
         sorted_ok = int(flag.download(np.uint32, 1)[0]) == 0
     if not sorted_ok:

@@ -120,6 +120,91 @@ def build_parallel(gitdir, n, seed=3, procs=16, edits=(0.01, 0.01, 0.01)):
     return ku + kd + ki
 
 
+def _subtree_import(args):
+    """one worker: the entries of one two-level path prefix ('A/B/') as a commit of their own whose
+    root tree is that prefix's subtree; returns (prefix, tree id)"""
+    gitdir, ref, prefix, pks, ids = args
+    arena, off = synth.int_pk_paths(pks)
+    hexes = ids.tobytes().hex()
+    lines = [b"commit %s\ncommitter t <t@t> 1600000000 +0000\ndata 1\ns\n" % ref.encode()]
+    for i in range(pks.shape[0]):
+        path = arena[int(off[i]):int(off[i + 1])].tobytes()
+        assert path[:4] == prefix
+        lines.append(b"M 100644 %s %s\n" % (hexes[40 * i:40 * i + 40].encode(), path[4:]))
+    lines.append(b"\n")
+    env = dict(os.environ, GIT_DIR=gitdir)
+    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=env, check=True)
+    tree = subprocess.run(["git", "rev-parse", ref + "^{tree}"], env=env, check=True, capture_output=True).stdout.strip()
+    return prefix, tree.decode()
+
+
+def build_sharded(gitdir, n, seed=3, procs=16, edits=(0.08, 0.01, 0.01)):
+    """build_parallel for tens of millions of features: the blobs by parallel fast-imports as there,
+    and each commit's feature tree too — one fast-import per two-level path prefix (its subtree, as a
+    commit of its own; ~4k leaf trees each), the commits then placing those subtrees by id (M 040000).
+    One fast-import building a 10M-entry tree alone took ~240 s."""
+    from multiprocessing import Pool
+
+    subprocess.run(["git", "init", "-q", "--bare", gitdir], check=True)
+    legend = Legend(["c-fid"], [c["id"] for c in synth.POINT_SCHEMA[1:]])
+    lh = legend.hexhash()
+    rng = np.random.default_rng(seed)
+    pks = np.arange(1, n + 1, dtype=np.int64)
+    perm = rng.permutation(n)
+    ku, kd, ki = (int(n * f) for f in edits)
+    upd, dele = np.sort(perm[:ku]), np.sort(perm[ku:ku + kd])
+    ins = np.arange(n + 1, n + 1 + ki, dtype=np.int64)
+    inner = f"{DS}/.table-dataset"
+    meta = _meta(inner, lh, legend)
+    t0 = time.perf_counter()
+    ids = []
+    for p, ver in ((pks, 0), (pks[upd], 1), (ins, 2)):
+        data, boff = synth.point_blobs(p, np.full(p.shape[0], ver, np.uint64), lh)
+        ids.append(_blob_ids(gitdir, data, boff, procs))
+        del data, boff
+        print(f"  blobs of version {ver}: {p.shape[0]} in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    # the two commits' entries: (pks ascending, blob ids)
+    keep = np.ones(n, bool)
+    keep[dele] = False
+    ids2 = ids[0].copy()
+    ids2[upd] = ids[1]
+    c1 = (pks, ids[0])
+    c2 = (np.concatenate([pks[keep], ins]), np.concatenate([ids2[keep], ids[2]]))
+    commits = []
+    alpha = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
+    for ci, (cp, cid) in enumerate((c1, c2)):
+        group = ((cp // 64) % (1 << 24)) >> 12  # the first two path levels (positive pks)
+        order = np.argsort(group, kind="stable")
+        g_sorted = group[order]
+        cuts = np.flatnonzero(np.diff(g_sorted)) + 1
+        starts = np.concatenate([[0], cuts])
+        ends = np.concatenate([cuts, [g_sorted.shape[0]]])
+        jobs = []
+        for a, b in zip(starts, ends):
+            g = int(g_sorted[a])
+            prefix = bytes([alpha[g >> 6], ord("/"), alpha[g & 63], ord("/")])
+            rows = order[a:b]
+            jobs.append((gitdir, f"refs/heads/s{ci}_{g}", prefix, cp[rows], cid[rows]))
+        with Pool(procs) as pool:
+            subtrees = pool.map(_subtree_import, jobs)
+        commits.append(subtrees)
+        print(f"  commit {ci}: {len(subtrees)} subtrees in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    lines = []
+    for ci, subtrees in enumerate(commits):
+        lines.append(b"commit refs/heads/main\ncommitter t <t@t> %d +0000\ndata 1\nx\n" % (1600000000 + ci))
+        if ci:
+            lines.append(b"deleteall\n")
+        for path, d in meta.items():
+            lines.append(b"M 100644 inline %s\ndata %d\n%s\n" % (path.encode(), len(d), d))
+        for prefix, tree in subtrees:
+            lines.append(b"M 040000 %s %s/feature/%s\n" % (tree.encode(), inner.encode(), prefix[:3]))
+        lines.append(b"\n")
+    subprocess.run(["git", "fast-import", "--quiet"], input=b"".join(lines), env=dict(os.environ, GIT_DIR=gitdir),
+                   check=True)
+    print(f"  commits written in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    return ku + kd + ki
+
+
 def _meta(inner, lh, legend):
     return {f"{inner}/meta/schema.json": json.dumps(synth.POINT_SCHEMA).encode(),
             f"{inner}/meta/path-structure.json": json.dumps(
@@ -214,7 +299,8 @@ def main():
     edits = tuple(float(x) for x in a.edits.split(","))
     gitdir = a.repo or f"/tmp/kart_e2e_{a.n}_{a.edits.replace(',', '_')}.git"
     if not os.path.isdir(gitdir):
-        t, k = timed(lambda: build_parallel(gitdir, a.n, procs=a.procs, edits=edits))
+        build = build_sharded if a.n > 5_000_000 else build_parallel
+        t, k = timed(lambda: build(gitdir, a.n, procs=a.procs, edits=edits))
         print(f"built {gitdir} in {t:.1f} s", file=sys.stderr, flush=True)
     from kart_amd import dataset as D
     from kart_amd.engine import Engine

@@ -86,14 +86,14 @@ def test_gpu_pk_order_equals_reference_sorted_items(engine, name):
         assert got == want, (name, case["base"], case["target"])
 
 
-def _seg_sort(engine, keys, seg_bits=24):
+def _seg_sort(engine, keys, seg_bits=24, max_seg=0):
     from kart_amd.device import DevBuf
 
     n = keys.size
     dk = DevBuf.from_numpy(engine, keys if n else np.zeros(1, np.uint64))
     ko, order, err = DevBuf(engine, 8 * max(n, 1)), DevBuf(engine, 4 * max(n, 1)), DevBuf(engine, 8)
     err.zero()
-    N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk.ptr, ko.ptr, order.ptr, n, seg_bits, err.ptr),
+    N.check(engine.L.kd_sort_segmented_into(engine.ctx, dk.ptr, ko.ptr, order.ptr, n, seg_bits, max_seg, err.ptr),
             "kd_sort_segmented_into")
     return ko.download(np.uint64, n), order.download(np.uint32, n), int(err.download(np.uint32, 1)[0])
 
@@ -104,13 +104,35 @@ def test_gpu_segmented_sort_c4_walk_order(engine, n):
     order; the per-bucket sort equals a full stable argsort of the keys"""
     from kart_amd import synth
 
+    from kart_amd import packing
+
     M = synth.table3_layers(max(n, 10), seed=3, walk=True)
     for S in (M.ancestor, M.ours, M.theirs):
         keys = S.key[:n]
-        k, order, err = _seg_sort(engine, keys)
         ref = np.argsort(keys, kind="stable")
-        assert err == 0
-        assert np.array_equal(order, ref.astype(np.uint32)) and np.array_equal(k, keys[ref])
+        # the full halo, and the small one the host's scan allows (seg_max <= 128)
+        for max_seg in (0, packing.keys_scan(keys, S.key_mode).seg_max):
+            k, order, err = _seg_sort(engine, keys, max_seg=max_seg)
+            assert err == 0
+            assert np.array_equal(order, ref.astype(np.uint32)) and np.array_equal(k, keys[ref])
+
+
+@pytest.mark.parametrize("run", [60, 200, 500])
+def test_gpu_segmented_sort_long_runs(engine, run):
+    """runs of 60 / 200 / 500 entries crossing tile boundaries: exact with the full halo; with a
+    hint of 128 a longer run that crosses a tile edge is flagged (err 4), never mis-sorted"""
+    rng = np.random.default_rng(run)
+    nb = 40_000 // run
+    b = np.repeat(np.arange(nb, dtype=np.uint64), run)
+    keys = (b << np.uint64(40)) | rng.permutation(b.size).astype(np.uint64)
+    ref = np.argsort(keys, kind="stable")
+    k, order, err = _seg_sort(engine, keys, max_seg=0)
+    assert err == 0 and np.array_equal(order, ref.astype(np.uint32)) and np.array_equal(k, keys[ref])
+    k, order, err = _seg_sort(engine, keys, max_seg=128)
+    if run <= 128:
+        assert err == 0 and np.array_equal(order, ref.astype(np.uint32))
+    else:
+        assert err & 4
 
 
 def test_gpu_segmented_sort_flags(engine):
