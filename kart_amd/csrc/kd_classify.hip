@@ -118,7 +118,7 @@ __global__ __launch_bounds__(NT) void k_resolve3(Resolve3Args g) {
     __shared__ u32 s_wave[NT / 64];
     __shared__ u64 s_b[4];  // ticket, bracket lo, bracket hi, -
     __shared__ u64 s_ex[2];
-    __shared__ u64 s_smp[NS];  // ancestor keys at NS evenly spaced bracket positions
+    __shared__ u64 s_smp[HAVE_A ? 1 : NS];  // ancestor keys at NS evenly spaced bracket positions
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const u64 n = HAVE_A ? g.c2[1] : g.c2[3];
     while (true) {

@@ -1316,13 +1316,22 @@ __global__ __launch_bounds__(64) void k_place3(const u32* __restrict__ stage_con
 //      LDS, its row from LDS): the three OIDs and the ancestor's / the path's name offsets;
 //   5. the ancestor's filename (HBM window) against the path's name (LDS).
 // Results are k_join3's (same staging, same k_place3).
+// Where the time goes (C4, 50M rows, r5 timing probes KD_J3B_STOP / KD_J3B_PROBE_NONAMES, 2.67 ms
+// in all): split records + the DMA batch 0.97 ms (~6.5 TB/s of staged bytes), + merge path and
+// matched pairs 0.53 ms (0.2 of it the filename compare), + the differing paths 1.2 ms.  SQ counters
+// put VALU at ~60 % of each SIMD's cycles with 4 waves per SIMD (LDS 35 KB and ~105 VGPRs per
+// 256-thread block both allow 4), so cutting round trips alone does not pay: staging the ancestor's
+// name offsets so its filename loads with the OIDs (one round trip less) measured 2.67 -> 2.70 ms,
+// a resident grid prefetching the next tile's split records 2.83 -> 3.21, and the split form (join
+// stages candidates, k_resolve3 resolves) 2.12 + 1.83 ms.  What paid: waves holding no differing
+// path skip the resolve (most: ~30 per tile), a 32-bit ancestor search, and a cheaper compare.
 #ifndef KD_J3B_IPT
 #define KD_J3B_IPT 2  // 512-item tiles: C4's ~36-B names of a tile (+ halo) fit 22.5 KB of LDS
 #endif
 constexpr int J3B_IPT = KD_J3B_IPT;
 constexpr int J3B_TILE = C2_NT * J3B_IPT;
 #ifndef KD_J3B_ACAP
-#define KD_J3B_ACAP (J3B_TILE + 128)  // ancestor keys staged (a tile's range is ~half its items)
+#define KD_J3B_ACAP (J3B_TILE / 2 + 128)  // ancestor keys staged (a tile's range is ~half its items)
 #endif
 constexpr int J3B_ACAP = KD_J3B_ACAP;
 #ifndef KD_J3B_NAME_CH
@@ -1332,6 +1341,16 @@ constexpr int J3B_ACAP = KD_J3B_ACAP;
 #define KD_J3B_HALO 16
 #endif
 constexpr u64 J3B_HALO = KD_J3B_HALO;
+#ifndef KD_J3B_PERSIST
+#define KD_J3B_PERSIST 0  // 1: a resident grid walking the tiles, the next split records prefetched (slower)
+#endif
+constexpr bool J3B_PERSIST = KD_J3B_PERSIST;
+#ifndef KD_J3B_STOP
+#define KD_J3B_STOP 0
+#endif
+#ifndef KD_J3B_PROBE_NONAMES
+#define KD_J3B_PROBE_NONAMES 0
+#endif
 
 // apart[t] and (nsplit) the name-arena offsets around split t: ours rows i_t -/+ halo, theirs rows
 // j_t - halo and j_t + 1 + halo (clamped), j_t = min(t * tile, nO + nT) - i_t
@@ -1394,8 +1413,10 @@ __device__ __forceinline__ bool glb_lds_name_eq(const u8* __restrict__ na, u64 a
     return true;
 }
 
-template <int NT, int IPT, bool HASH, bool PERM>
-__global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
+// SPLIT: the differing paths are staged as candidates (a, o, t) with the ancestor entry found in LDS
+// (no OID or filename load in the tile) and k_resolve3<HAVE_A> applies the rule over the placed list
+template <int NT, int IPT, bool HASH, bool PERM, bool SPLIT = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_join3b(Join3Args g3) {
     const Join2Args& g = g3.j;
     using LD = Join2Lds<NT, IPT>;
     constexpr int TILE = LD::TILE;
@@ -1412,15 +1433,21 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
     __shared__ u32 s_wave[3 * NT / 64];
     typedef const __attribute__((address_space(1))) u32* gp32;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const u64 tile = blockIdx.x;
-    // ---- 1. split records of both tile ends ----
-    const u64 p0 = g.part[tile], p1 = g.part[tile + 1];
-    const u64 a0 = g3.apart[tile], a1 = g3.apart[tile + 1];
+    const u64 ntiles = g.ntiles;
+    u64 tile = blockIdx.x;
+    if (tile >= ntiles) return;  // block-uniform
+    // ---- 1. split records of both tile ends (later tiles': prefetched with the previous tile's DMA) ----
+    u64 p0 = g.part[tile], p1 = g.part[tile + 1];
+    u64 a0 = g3.apart[tile], a1 = g3.apart[tile + 1];
     u64 nmA0 = 0, nmA1 = 0, nmB0 = 0, nmB1 = 0;
     if (HASH) {
         nmA0 = g3.nsplit[4 * tile]; nmB0 = g3.nsplit[4 * tile + 2];
         nmA1 = g3.nsplit[4 * tile + 5]; nmB1 = g3.nsplit[4 * tile + 7];
     }
+    u32 err = 0;
+    for (;;) {  // persistent: tiles blockIdx.x, + gridDim.x, ...
+    const u64 tnext = tile + gridDim.x;
+    const bool more = J3B_PERSIST && tnext < ntiles;  // block-uniform
     const TileGeo q = tile_geo_from(g, tile, TILE, p0, p1);
     bool bad = !q.ok;
     const TileRanges r = tile_ranges(g, q);
@@ -1466,7 +1493,25 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
             qq = dma_range<NT>(rnB, s_nm + rnA.nch, qq);
         }
     }
+    // the next tile's split records, in flight with the batch (the name bounds in their own
+    // registers: this tile's are read until its end)
+    u64 xA0 = 0, xA1 = 0, xB0 = 0, xB1 = 0;
+    if (more) {
+        p0 = g.part[tnext]; p1 = g.part[tnext + 1];
+        a0 = g3.apart[tnext]; a1 = g3.apart[tnext + 1];
+        if (HASH) {
+            xA0 = g3.nsplit[4 * tnext]; xB0 = g3.nsplit[4 * tnext + 2];
+            xA1 = g3.nsplit[4 * tnext + 5]; xB1 = g3.nsplit[4 * tnext + 7];
+        }
+    }
     __syncthreads();  // vmcnt(0) + barrier: everything staged has landed
+#if KD_J3B_STOP == 1  // timing probe only (results invalid): split records + the DMA batch
+    if (tid == 0) { u32* cc = g.tile_cnt + 4 * tile; cc[0] = cc[1] = cc[2] = cc[3] = 0; }
+    if (!more) break;
+    tile = tnext; nmA0 = xA0; nmA1 = xA1; nmB0 = xB0; nmB1 = xB1;
+    __syncthreads();
+    continue;
+#endif
     const u64* sA = (const u64*)((const u8*)s_ch + r.ka.skew) + q.has_lbA;
     const u64* sB = (const u64*)((const u8*)(s_ch + r.c1) + r.kb.skew) + q.has_lbB;
     const u64* sK = (const u64*)((const u8*)s_k + rk.skew) + has_lbK;
@@ -1515,7 +1560,11 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
             if (PERM && (ra[k] < rA0 || ra[k] >= rA1 || rb[k] < rB0 || rb[k] >= rB1))
                 ne |= !names_eq(g.nameA, g.nameOffA, ra[k], g.nameB, g.nameOffB, rb[k]);
             else
+#if KD_J3B_PROBE_NONAMES  // timing probe only (results invalid): the LDS name compare skipped
+                ne |= la != lb || (baseA + oa0[k] == 7u && baseB + ob0[k] == 5u);
+#else
                 ne |= la != lb || !lds_eq_bytes(baseA + (oa0[k] - (u32)nmA0), baseB + (ob0[k] - (u32)nmB0), la);
+#endif
         }
     } else if (HASH) {
         u32 act = 0;
@@ -1523,7 +1572,15 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
         for (int k = 0; k < IPT; k++) act |= (u32)((rec[k] >> 25) == R_MATCH) << k;
         ne |= names_ne_batch<IPT, 8>(g.nameA, g.nameOffA, ra, g.nameB, g.nameOffB, rb, act) != 0;
     }
-    if (bad) atomicOr(g.err, 1u);
+    if (bad) err |= 1u;
+#if KD_J3B_STOP == 2  // timing probe only (results invalid): + the merge path and the matched pairs
+    if (ne) err |= 2u;
+    __syncthreads();
+    if (tid == 0) { u32* cc = g.tile_cnt + 4 * tile; cc[0] = cc[1] = cc[2] = cc[3] = 0; }
+    if (!more) break;
+    tile = tnext; nmA0 = xA0; nmA1 = xA1; nmB0 = xB0; nmB1 = xB1;
+    continue;
+#endif
     // ---- the paths where ours and theirs differ, compacted in path order ----
     u32 dif = 0, clean = 0;
 #pragma unroll
@@ -1561,22 +1618,31 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
     for (u32 c0 = 0; c0 < ndif; c0 += NT) {  // block-uniform
         const u32 x = c0 + tid;
         const bool act = x < ndif;
+        u32 ik = KD_NONE, io = KD_NONE, itt = KD_NONE;
+        bool md = false, cf = false;
+        // the join is VALU-bound (r5 SQ counters): waves holding no differing path (most of them —
+        // C4 has ~30 per 512-item tile) skip straight to the scan
+        if (c0 + 64u * (u32)wid < ndif) {  // wave-uniform
         const u32 r0 = act ? s_drec[x] : 0u;
         const u32 kind = r0 >> 25, ia = r0 & 0xFFF, jb = (r0 >> 12) & 0xFFF;
         const u64 key = kind == R_INS ? sB[jb] : sA[ia];
-        u64 lo = 0, hi = act ? nk : 0;
+        const u32 nk32 = (u32)nk;
+        u32 lo = 0, hi = act ? nk32 : 0;
         for (int it = 0; it < rounds; it++) {
-            const u64 m = (lo + hi) >> 1;
-            const u64 mi = m < nk ? m : (nk ? nk - 1 : 0);
+            const u32 m = (lo + hi) >> 1;
+            const u32 mi = m < nk32 ? m : (nk32 ? nk32 - 1 : 0);
             const u64 v = lk ? sK[mi] : g3.K[k0 + mi];
             const bool on = lo < hi, lt = v < key;
             lo = on && lt ? m + 1 : lo;
             hi = on && !lt ? m : hi;
         }
-        const bool found = act && lo < nk && (lk ? sK[lo] : g3.K[k0 + lo]) == key;
-        const u32 ik = found ? (u32)(k0 + lo) : KD_NONE;
-        const u32 io = act && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
-        const u32 itt = act && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
+        const bool found = act && lo < nk32 && (lk ? sK[lo] : g3.K[k0 + lo]) == key;
+        ik = found ? (u32)(k0 + lo) : KD_NONE;
+        io = act && kind != R_INS ? (u32)(q.i0 + ia) : KD_NONE;
+        itt = act && kind != R_DEL ? (u32)(q.j0 + jb) : KD_NONE;
+        if constexpr (SPLIT) {
+            cf = act;  // a candidate, resolved by k_resolve3
+        } else {
         // ---- 4. rows (LDS), then the three OIDs and the name offsets ----
         u32 rk3 = ik, ro = io, rt = itt;
         if (PERM) {
@@ -1604,7 +1670,7 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
             dko |= xk ^ po[w];
             dkt |= xk ^ pt[w];
         }
-        // ---- 5. the ancestor's name (HBM) against the path's (LDS, else HBM) ----
+        // ---- 5. the ancestor's name against the path's (LDS, else HBM) ----
         if (HASH && chk) {
             const u32 len = (u32)(kn1 - kn0);
             if (len != (u32)(sn1 - sn0)) {
@@ -1623,9 +1689,11 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
         const bool pa = ik != KD_NONE, pO = io != KD_NONE, pT = itt != KD_NONE;
         const bool a_eq_o = pa == pO && (!pa || dko == 0);
         const bool a_eq_t = pa == pT && (!pa || dkt == 0);
-        const bool md = act && a_eq_o;
-        const bool cf = act && !a_eq_o && !a_eq_t;
+        md = act && a_eq_o;
+        cf = act && !a_eq_o && !a_eq_t;
         clean += (act && !a_eq_o && a_eq_t && pO) || (md && pT);
+        }  // (!SPLIT)
+        }  // (a wave with differing paths)
         u32 tot;
         const u32 off = block_excl_scan<NT>((u32)cf | (u32)md << 16, s_wave, &tot);
         if (cf) {
@@ -1636,8 +1704,8 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
         tc += tot & 0xFFFF;
         tm += tot >> 16;
     }
-    if (ne) atomicOr(g.err, 2u);
-    const u32 tcl = block_sum<NT>(clean, s_wave);
+    if (ne) err |= 2u;
+    const u32 tcl = block_sum<NT>(clean, s_wave);  // (its barriers: every LDS read of this tile is done)
     if (tid == 0) {
         u32* cc = g.tile_cnt + 4 * tile;
         cc[0] = tcl; cc[1] = tm; cc[2] = 0; cc[3] = tc;
@@ -1645,6 +1713,11 @@ __global__ __launch_bounds__(NT) void k_join3b(Join3Args g3) {
         atomicAdd((unsigned long long*)gs, (unsigned long long)(tc | (u64)tm << 32));
         atomicAdd((unsigned long long*)gs + 1, (unsigned long long)tcl);
     }
+    if (!more) break;
+    tile = tnext;
+    nmA0 = xA0; nmA1 = xA1; nmB0 = xB0; nmB1 = xB1;
+    }
+    if (err) atomicOr(g.err, err);
 }
 
 // the three-way merge through k_join3 (sides device-resident; ord* non-null: late materialisation)
@@ -1657,7 +1730,7 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     // 4.02 vs 3.78 ms from walk order, 2.37 vs 2.16 presorted — the default resolves in the join)
     const bool split = ctx->opt.merge3_split == 1;
     const bool j3_ol = ctx->opt.j3_ol == 1;  // (sorted-form sides' OIDs staged with the keys)
-    const bool v2 = ctx->opt.j3_v != 0 && !split && !(j3_ol && !perm);  // k_join3b
+    const bool v2 = ctx->opt.j3_v != 0 && !(j3_ol && !perm);  // k_join3b
     const int TILE = v2 ? J3B_TILE : J3_TILE;
     if (hash) KD_CHECK((nK == 0 || (K.name && K.name_off)) && (nO == 0 || (O.name && O.name_off)) &&
                        (nT == 0 || (T.name && T.name_off)), "merge3: KD_KEY_HASH needs filenames");
@@ -1722,16 +1795,25 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
         if ((rc = ensure(ctx, "c3.cand3", (total + 1) * 12, &cand3))) return rc;
         if ((rc = ensure(ctx, "c3.c2j", 64, &c2))) return rc;
     }
+    auto j3b_grid = [&](const void* kern) {
+        if (!J3B_PERSIST) return (unsigned)ntiles;
+        return (unsigned)std::max<u64>(1, std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)occupancy(ctx, kern, C2_NT, 0)));
+    };
     rc = launch(ctx, "k_join3", [&] {
 #define KD_J3(H, PM, S) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, H, PM, S>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
-        if (split) {
+        if (v2) {
+#define KD_J3B(H, PM, S) hipLaunchKernelGGL((k_join3b<C2_NT, J3B_IPT, H, PM, S>), dim3(j3b_grid((const void*)k_join3b<C2_NT, J3B_IPT, H, PM, S>)), dim3(C2_NT), 0, ctx->stream, a)
+            if (split) {
+                if (hash) { if (perm) KD_J3B(true, true, true); else KD_J3B(true, false, true); }
+                else { if (perm) KD_J3B(false, true, true); else KD_J3B(false, false, true); }
+            } else {
+                if (hash) { if (perm) KD_J3B(true, true, false); else KD_J3B(true, false, false); }
+                else { if (perm) KD_J3B(false, true, false); else KD_J3B(false, false, false); }
+            }
+#undef KD_J3B
+        } else if (split) {
             if (hash) { if (perm) KD_J3(true, true, true); else KD_J3(true, false, true); }
             else { if (perm) KD_J3(false, true, true); else KD_J3(false, false, true); }
-        } else if (v2) {
-#define KD_J3B(H, PM) hipLaunchKernelGGL((k_join3b<C2_NT, J3B_IPT, H, PM>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
-            if (hash) { if (perm) KD_J3B(true, true); else KD_J3B(true, false); }
-            else { if (perm) KD_J3B(false, true); else KD_J3B(false, false); }
-#undef KD_J3B
         } else if (j3_ol && !perm) {
             if (hash) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, true, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a);
             else hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, false, false, false, true>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a);

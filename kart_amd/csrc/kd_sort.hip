@@ -638,83 +638,112 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
     __shared__ u16 s_st[SEG_E];  // start of the entry's run (LDS index)
     __shared__ u16 s_en[SEG_E];  // end (exclusive; SEG_E fits 16 bits)
     __shared__ u32 s_w[SEG_NT / 64];
-    const int tid = threadIdx.x;
-    const u64 t0 = (u64)blockIdx.x * SEG_T;
-    const i64 g0 = (i64)t0 - SEG_H;  // global index of s_k[0]
-    const int vlo = g0 < 0 ? (int)(-g0) : 0;                                   // valid LDS entries: [vlo, vhi)
-    const int vhi = (int)min<i64>((i64)SEG_E, (i64)n - g0);
-    for (int x = tid; x < SEG_E; x += SEG_NT) s_k[x] = (x >= vlo && x < vhi) ? key[g0 + x] : 0;
-    __syncthreads();
-    // run heads: an entry whose top bits differ from its predecessor's (or the first valid entry);
-    // invalid entries are runs of their own.  Starts: the last head at or before the entry (a max-scan
-    // of head index + 1, 0 = none yet); ends: the first head after it (a min-scan from the right)
-    auto is_head = [&](int x) {
-        return !(x >= vlo && x < vhi) || x == vlo || (s_k[x] >> shift) != (s_k[x - 1] >> shift);
-    };
-    const int x0 = tid * SEG_EPT;
-    u32 st_loc[SEG_EPT], en_loc[SEG_EPT];
-    u32 runp1 = 0;
-    bool bad1 = false;
-#pragma unroll
-    for (int j = 0; j < SEG_EPT; j++) {
-        const int x = x0 + j;
-        const bool head = is_head(x);
-        if (head) runp1 = (u32)x + 1;
-        st_loc[j] = runp1;
-        // descending top bits: checked at the heads of the tile's own range (each boundary once)
-        if (head && x > vlo && x < vhi && x >= SEG_H && x < SEG_H + SEG_T)
-            bad1 |= (s_k[x] >> shift) < (s_k[x - 1] >> shift);
-    }
-    u32 nxt = SEG_E;
-#pragma unroll
-    for (int j = SEG_EPT - 1; j >= 0; j--) {
-        en_loc[j] = nxt;
-        if (is_head(x0 + j)) nxt = (u32)(x0 + j);
-    }
     __shared__ u32 s_inc[SEG_NT];
-    const u32 fwd = seg_block_scan<true>(runp1, s_w, false);
-    s_inc[tid] = fwd;
-    __syncthreads();
-    const u32 before = tid ? s_inc[tid - 1] : 0u;  // the last head before this thread's chunk (+1)
-    __syncthreads();
-    const u32 bwd = seg_block_scan<false>(nxt, s_w, true);
-    s_inc[tid] = bwd;
-    __syncthreads();
-    const u32 after = tid + 1 < SEG_NT ? s_inc[tid + 1] : (u32)SEG_E;  // the first head after the chunk
+    const int tid = threadIdx.x;
+    const u64 ntiles = (n + SEG_T - 1) / SEG_T;
+    // Persistent grid: tile t + gridDim.x's keys are loaded into registers (all SEG_EPT loads in
+    // flight together, clamped rows masked when staged) while tile t is ranked and written.  (A
+    // guarded load-then-store staging loop compiled to one HBM round trip per entry a thread stages.)
+    auto geo = [&](u64 t, i64& g0, int& vlo, int& vhi) {
+        g0 = (i64)(t * SEG_T) - SEG_H;  // global index of s_k[0]
+        vlo = g0 < 0 ? (int)(-g0) : 0;  // valid LDS entries: [vlo, vhi)
+        vhi = (int)min<i64>((i64)SEG_E, (i64)n - g0);
+    };
+    u64 v[SEG_EPT];
+    auto fetch = [&](u64 t) {
+        i64 g0;
+        int vlo, vhi;
+        geo(t, g0, vlo, vhi);
 #pragma unroll
-    for (int j = 0; j < SEG_EPT; j++) {
-        s_st[x0 + j] = (u16)((st_loc[j] ? st_loc[j] : before) - 1);
-        s_en[x0 + j] = (u16)(en_loc[j] != (u32)SEG_E ? en_loc[j] : after);
-    }
-    __syncthreads();
-    // ranks of the tile's own entries
-    u32 bad = bad1 ? 1u : 0u;
+        for (int j = 0; j < SEG_EPT; j++) {
+            const int x = tid + j * SEG_NT;
+            v[j] = key[g0 + (x < vlo ? vlo : (x >= vhi ? vhi - 1 : x))];
+        }
+    };
+    u64 tile = blockIdx.x;
+    if (tile < ntiles) fetch(tile);
+    u32 bad = 0;
+    for (; tile < ntiles; tile += gridDim.x) {  // block-uniform
+        i64 g0;
+        int vlo, vhi;
+        geo(tile, g0, vlo, vhi);
+#pragma unroll
+        for (int j = 0; j < SEG_EPT; j++) {
+            const int x = tid + j * SEG_NT;
+            s_k[x] = (x >= vlo && x < vhi) ? v[j] : 0;
+        }
+        __syncthreads();
+        if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
+        // run heads: an entry whose top bits differ from its predecessor's (or the first valid entry);
+        // invalid entries are runs of their own.  Starts: the last head at or before the entry (a
+        // max-scan of head index + 1, 0 = none yet); ends: the first head after it (a min-scan from
+        // the right)
+        auto is_head = [&](int x) {
+            return !(x >= vlo && x < vhi) || x == vlo || (s_k[x] >> shift) != (s_k[x - 1] >> shift);
+        };
+        const int x0 = tid * SEG_EPT;
+        u32 st_loc[SEG_EPT], en_loc[SEG_EPT];
+        u32 runp1 = 0;
+#pragma unroll
+        for (int j = 0; j < SEG_EPT; j++) {
+            const int x = x0 + j;
+            const bool head = is_head(x);
+            if (head) runp1 = (u32)x + 1;
+            st_loc[j] = runp1;
+            // descending top bits: checked at the heads of the tile's own range (each boundary once)
+            if (head && x > vlo && x < vhi && x >= SEG_H && x < SEG_H + SEG_T && (s_k[x] >> shift) < (s_k[x - 1] >> shift))
+                bad |= 1u;
+        }
+        u32 nxt = SEG_E;
+#pragma unroll
+        for (int j = SEG_EPT - 1; j >= 0; j--) {
+            en_loc[j] = nxt;
+            if (is_head(x0 + j)) nxt = (u32)(x0 + j);
+        }
+        const u32 fwd = seg_block_scan<true>(runp1, s_w, false);
+        s_inc[tid] = fwd;
+        __syncthreads();
+        const u32 before = tid ? s_inc[tid - 1] : 0u;  // the last head before this thread's chunk (+1)
+        __syncthreads();
+        const u32 bwd = seg_block_scan<false>(nxt, s_w, true);
+        s_inc[tid] = bwd;
+        __syncthreads();
+        const u32 after = tid + 1 < SEG_NT ? s_inc[tid + 1] : (u32)SEG_E;  // the first head after the chunk
+#pragma unroll
+        for (int j = 0; j < SEG_EPT; j++) {
+            s_st[x0 + j] = (u16)((st_loc[j] ? st_loc[j] : before) - 1);
+            s_en[x0 + j] = (u16)(en_loc[j] != (u32)SEG_E ? en_loc[j] : after);
+        }
+        __syncthreads();
+        // ranks of the tile's own entries
 #pragma unroll 2
-    for (int j = 0; j < SEG_IPT; j++) {
-        const int x = SEG_H + j * SEG_NT + tid;  // consecutive lanes: consecutive entries
-        if (x >= vhi) break;
-        const u64 k = s_k[x];
-        const u32 s0 = s_st[x], e0 = s_en[x];
-        if ((s0 == 0 && g0 > 0) || (e0 == (u32)SEG_E && g0 + SEG_E < (i64)n) || e0 - s0 > (u32)RS_SEG_MAX) {
-            bad |= 4u;  // a run longer than RS_SEG_MAX (or reaching past the halo)
-            continue;
+        for (int j = 0; j < SEG_IPT; j++) {
+            const int x = SEG_H + j * SEG_NT + tid;  // consecutive lanes: consecutive entries
+            if (x >= vhi) break;
+            const u64 k = s_k[x];
+            const u32 s0 = s_st[x], e0 = s_en[x];
+            if ((s0 == 0 && g0 > 0) || (e0 == (u32)SEG_E && g0 + SEG_E < (i64)n) || e0 - s0 > (u32)RS_SEG_MAX) {
+                bad |= 4u;  // a run longer than RS_SEG_MAX (or reaching past the halo)
+                continue;
+            }
+            u32 rank = 0, dup = 0;
+            u32 y = s0;
+            for (; y + 4 <= e0; y += 4) {
+                const u64 a = s_k[y], b = s_k[y + 1], c = s_k[y + 2], d = s_k[y + 3];
+                rank += (a < k) + (b < k) + (c < k) + (d < k);
+                dup += (a == k) + (b == k) + (c == k) + (d == k);
+            }
+            for (; y < e0; y++) {
+                const u64 a = s_k[y];
+                rank += a < k;
+                dup += a == k;
+            }
+            bad |= dup > 1 ? 1u : 0u;
+            const u64 dst = (u64)(g0 + (i64)s0) + rank;
+            kout[dst] = k;
+            order[dst] = (u32)(g0 + x);
         }
-        u32 rank = 0, dup = 0;
-        u32 y = s0;
-        for (; y + 4 <= e0; y += 4) {
-            const u64 a = s_k[y], b = s_k[y + 1], c = s_k[y + 2], d = s_k[y + 3];
-            rank += (a < k) + (b < k) + (c < k) + (d < k);
-            dup += (a == k) + (b == k) + (c == k) + (d == k);
-        }
-        for (; y < e0; y++) {
-            const u64 a = s_k[y];
-            rank += a < k;
-            dup += a == k;
-        }
-        bad |= dup > 1 ? 1u : 0u;
-        const u64 dst = (u64)(g0 + (i64)s0) + rank;
-        kout[dst] = k;
-        order[dst] = (u32)(g0 + x);
+        __syncthreads();  // s_k / s_st / s_en are restaged for the next tile
     }
     if (__ballot(bad != 0) && bad) atomicOr(err, bad);
 }
@@ -1009,13 +1038,17 @@ extern "C" int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uin
     if (n == 0) return KD_OK;
     const u64 ntiles = (n + SEG_T - 1) / SEG_T;
     const bool small = max_seg > 0 && max_seg <= SEG_HS;
+    // one workgroup per tile (the kernel also walks tiles grid-stride with the next tile's keys
+    // prefetched, but a resident grid of occupancy x CUs measured slower: 0.272 vs 0.250 ms per 50M
+    // C4 side, r5e)
+    const unsigned grid = (unsigned)ntiles;
     return launch(ctx, "k_seg_sort", [&] {
         if (small)
-            hipLaunchKernelGGL(k_seg_sort<SEG_HS>, dim3((unsigned)ntiles), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
-                               64 - seg_bits, d_key_out, d_order, d_err);
+            hipLaunchKernelGGL(k_seg_sort<SEG_HS>, dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n, 64 - seg_bits,
+                               d_key_out, d_order, d_err);
         else
-            hipLaunchKernelGGL(k_seg_sort<RS_SEG_MAX>, dim3((unsigned)ntiles), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
-                               64 - seg_bits, d_key_out, d_order, d_err);
+            hipLaunchKernelGGL(k_seg_sort<RS_SEG_MAX>, dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n, 64 - seg_bits,
+                               d_key_out, d_order, d_err);
     });
 }
 
