@@ -627,6 +627,9 @@ __device__ __forceinline__ DenseLd dense_load_pp(const GfHeadArgs& g, u64 c, u64
 #ifndef KD_GFD_TR
 #define KD_GFD_TR false  // k_gf_dense: heads loaded as lane-contiguous runs, transposed through LDS
 #endif
+#ifndef KD_GFD_ZW
+#define KD_GFD_ZW 0
+#endif
 #ifndef KD_GFD_WAVES
 #define KD_GFD_WAVES 4  // k_gf_dense<1, false>: waves per SIMD the register budget is cut for
 #endif
@@ -682,8 +685,15 @@ __global__ __launch_bounds__(GF_NT) __attribute__((amdgpu_waves_per_eu(PF == 1 &
         const uint2 pr = A.pr;
         bool keep = false, deferred = false;
         u8 ok = 0;
+#if KD_GFD_ZW  // the wave's slice zeroed as dwords (64 nb bytes = 16 nb dwords), not nb bytes per lane
+        if (a.enc) {
+            for (int k = lane; k < 16 * nb; k += 64) ((u32*)wenc)[k] = 0;
+            __builtin_amdgcn_wave_barrier();
+        }
+#else
         if (a.enc)
             for (int k = 0; k < nb; k++) wenc[lane * nb + k] = 0;
+#endif
         if (d < n) {
             GHit h;
 #ifdef KD_GF_PROBE_NODECODE  // profiling variant: the loads and stores alone
