@@ -216,8 +216,16 @@ def timed(H, eng, step, steps):
     return H.max(time.perf_counter() - t0)
 
 
-ROCPROF_STATS = {"c3": "profiles/r04/c3_kernel_stats.csv", "c3v": "profiles/r04/c3v_kernel_stats.csv", "c4": "profiles/r04/c4_kernel_stats.csv",
-                 "c5": "profiles/r04/c5_kernel_stats.csv"}
+PROFILE_ROUNDS = ("r05", "r04")  # committed profiles, newest first
+
+
+def rocprof_stats_path(workload):
+    """the newest committed `rocprofv3 --kernel-trace --stats` summary of the workload"""
+    for d in PROFILE_ROUNDS:
+        path = os.path.join(ROOT, "profiles", d, f"{workload}_kernel_stats.csv")
+        if os.path.exists(path):
+            return path
+    return None
 
 
 # the HIP-event name a role is timed under -> the kernel symbols rocprof lists for it
@@ -227,8 +235,10 @@ KERNEL_SYMBOLS = {"k_gf_heads": ("k_gf_dense", "k_gf_heads")}
 
 def rocprof_avg_ms(workload, kernel):
     """the kernel's average duration in the committed `rocprofv3 --kernel-trace --stats` summary of
-    this workload (profiles/r04), or None"""
-    path = os.path.join(ROOT, ROCPROF_STATS.get(workload, "-"))
+    this workload (the newest of PROFILE_ROUNDS), or None"""
+    path = rocprof_stats_path(workload)
+    if path is None:
+        return None
     names = KERNEL_SYMBOLS.get(kernel, (kernel,))
     try:
         import csv
@@ -977,7 +987,7 @@ def run_c5env(args, H):
     # algorithmic bytes per k_envelopes launch: offsets (8 B) + GPKG header (8 B) + stored envelope
     # (32 B, polygons) or point WKB (21 B) read; match + enc_ok flags (2 B) + encoded envelope written
     alg = n * (8 + 8 + 2 + nb) + npt * 21 + (n - npt) * 32
-    roof = roofline(kern, "k_envelopes", alg, args.traffic_json, n)
+    roof = roofline(kern, "k_envelopes", alg, args.traffic_json, n, "c5env")
     heads_path = None
     if not args.no_heads_path:
         heads_path = c5env_heads_path(args, H, eng, data, off, d_data, d_off, n, bits, nb, enc, ok)
@@ -1129,7 +1139,7 @@ def run_c6(args, H):
     total = sum(H.allgather(n))
     kern = kernel_times(eng, ("k_hex", "k_wkb_start"))
     # algorithmic bytes per k_hex launch: the geometry arena read once, two hex chars written per byte
-    roof = roofline(kern, "k_hex", 3 * nbytes, args.traffic_json, n)
+    roof = roofline(kern, "k_hex", 3 * nbytes, args.traffic_json, n, "c6")
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
         m = min(n, 200_000)
