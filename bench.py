@@ -230,7 +230,8 @@ def rocprof_stats_path(workload):
 
 # the HIP-event name a role is timed under -> the kernel symbols rocprof lists for it
 # (kd_geom_filter_deltas times k_gf_dense, the dense-heads form, under "k_gf_heads")
-KERNEL_SYMBOLS = {"k_gf_heads": ("k_gf_dense", "k_gf_heads")}
+# (kd_merge3_device times k_join3b, the one-batch join, under "k_join3")
+KERNEL_SYMBOLS = {"k_gf_heads": ("k_gf_dense", "k_gf_heads"), "k_join3": ("k_join3b", "k_join3")}
 
 
 def rocprof_avg_ms(workload, kernel):
