@@ -1259,19 +1259,43 @@ def run_c4(args, H):
     eng.sync()
     eng.prof_enable(False)
     parts = kernel_times(eng, C4_KERNELS)
-    # classify3 in one pass (k_join3): dominant kernel k_join3, algorithmic bytes per
-    # launch: every ours/theirs key + OID once (28 B), every ours/theirs filename once (hash keys are
-    # verified against the names), every ancestor key once (8 B), and per differing path the staged
-    # candidate (a, o, t) (12 B); with the OIDs in walk order, one 4-B order entry per matched pair.  (KD_MERGE3_JOIN=0: the two-step path, k_join2 + k_resolve3, k_join2 dominant.)
-    (kO, oO, _), (kT, oT, _) = srt[1], srt[2]
+    # classify3 in one pass (k_join3b): dominant kernel k_join3, algorithmic bytes per
+    # launch — what the join must read with the sides in walk order (late materialisation):
+    #   per ours / theirs entry: key 8 + OID 20 + walk row 4 B, and its filename;
+    #   per matched pair: both name offsets (8 B each: a hash key is verified against the names);
+    #   every ancestor key (8 B);
+    #   per differing path with an ancestor entry: its walk row, OID, name offset and filename, and
+    #   the path's own name offset when it is one-sided;
+    #   per differing path the staged result (12 B).
+    # (Round 4's formula — 28 B per ours / theirs entry + names + 8 B per ancestor key + 12 B per
+    # differing path + 4 B per matched pair — left out the walk rows, the name offsets and the
+    # ancestor's reads; it is reported beside, `algorithmic_bytes_r4_formula`.)
+    (kA, _, ordA), (kO, oO, _), (kT, oT, _) = srt[0], srt[1], srt[2]
     _, io, it = np.intersect1d(kO, kT, assume_unique=True, return_indices=True)
-    n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero((oO[io] != oT[it]).any(axis=1)))
+    chg = (oO[io] != oT[it]).any(axis=1)
+    n_cand = int(O_.n + T.n - 2 * io.size + np.count_nonzero(chg))
+    one_o = np.ones(O_.n, bool)
+    one_o[io] = False
+    one_t = np.ones(T.n, bool)
+    one_t[it] = False
+    one_keys = np.concatenate([kO[one_o], kT[one_t]])
+    dif_keys = np.concatenate([one_keys, kO[io][chg]])
+    pa = np.searchsorted(kA, dif_keys)
+    has_a = (pa < kA.size) & (kA[np.minimum(pa, kA.size - 1)] == dif_keys)
+    rows = ordA[pa[has_a]]
+    anc_name = int((A.name_off[rows + 1] - A.name_off[rows]).sum())
+    n_anc = int(np.count_nonzero(has_a))
+    n_one_anc = int(np.count_nonzero(has_a[:one_keys.size]))
+    alg_r4 = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * A.n + 12 * n_cand + 4 * io.size
     j3 = "k_join3" in kern
-    if j3:  # (split form: the join stages a 12-B candidate per differing path, k_resolve3 reads its OIDs)
-        alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * A.n + 12 * n_cand + 4 * io.size
-    else:
+    if j3:
+        alg = (32 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 16 * io.size + 8 * A.n
+               + 32 * n_anc + anc_name + 8 * n_one_anc + 12 * n_cand)
+    else:  # (KD_MERGE3_JOIN=0: the two-step path, k_join2 + k_resolve3, k_join2 dominant)
         alg = 28 * (O_.n + T.n) + int(O_.name.size + T.name.size) + 8 * n_cand + 8 * io.size
     roof = roofline(kern, "k_join3" if j3 else "k_join2", alg, args.traffic_json, n, "c4" if H.world == 1 else None)
+    if roof and j3:
+        roof["algorithmic_bytes_r4_formula"] = int(alg_r4)
     seg_alg = 20 * nall  # per entry: the key read, key + 4-B order written (neighbours hit the cache)
     seg = {"what": "kd_sort_segmented_into x3: each bucket's entries (git filename order) ordered by key",
            "ms_per_step_events": round(parts["k_seg_sort"][0] * parts["k_seg_sort"][1] / 3, 4) if "k_seg_sort" in parts else None,
