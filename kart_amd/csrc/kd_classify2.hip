@@ -1326,19 +1326,26 @@ __global__ __launch_bounds__(64) void k_place3(const u32* __restrict__ stage_con
 // stages candidates, k_resolve3 resolves) 2.12 + 1.83 ms.  What paid: waves holding no differing
 // path skip the resolve (most: ~30 per tile), a 32-bit ancestor search, and a cheaper compare.
 #ifndef KD_J3B_IPT
-#define KD_J3B_IPT 2  // 512-item tiles: C4's ~36-B names of a tile (+ halo) fit 22.5 KB of LDS
+#define KD_J3B_IPT 2
 #endif
 constexpr int J3B_IPT = KD_J3B_IPT;
-constexpr int J3B_TILE = C2_NT * J3B_IPT;
+// 192 threads x 2 items: 384-item tiles whose LDS (26.4 KB: C4's ~36-B names of a tile + halo in
+// 16 KB) lets 6 blocks share a CU — 2.34 vs 2.56 ms for 256 x 2 (4 blocks per CU) on C4 (r5o;
+// 128 x 4 / 192 x 3 / 128 x 3: 2.87 / 2.57 / 2.81; 192 x 2 with a 16-row halo, 27.2 KB, 5 blocks: 2.61)
+#ifndef KD_J3B_NT
+#define KD_J3B_NT 192
+#endif
+constexpr int J3B_NT = KD_J3B_NT;
+constexpr int J3B_TILE = J3B_NT * J3B_IPT;
 #ifndef KD_J3B_ACAP
 #define KD_J3B_ACAP (J3B_TILE / 2 + 128)  // ancestor keys staged (a tile's range is ~half its items)
 #endif
 constexpr int J3B_ACAP = KD_J3B_ACAP;
 #ifndef KD_J3B_NAME_CH
-#define KD_J3B_NAME_CH 1408
+#define KD_J3B_NAME_CH (J3B_TILE == 384 ? 1000 : J3B_TILE * 11 / 4)  // 16 KB at 384 items (6 blocks per CU)
 #endif
 #ifndef KD_J3B_HALO
-#define KD_J3B_HALO 16
+#define KD_J3B_HALO 8  // (a 16-row halo measured the same at 512-item tiles; C4's leaf trees hold ~3)
 #endif
 constexpr u64 J3B_HALO = KD_J3B_HALO;
 #ifndef KD_J3B_PERSIST
@@ -1527,6 +1534,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     } else {
         for (u64 x = k0 + tid; x < k1; x += NT) bad |= x > 0 && g3.K[x - 1] >= g3.K[x];
     }
+#if KD_J3B_STOP == 3  // timing probe only (results invalid): + the merge-path walk and order checks
+    if (bad) err |= 1u;
+    if ((rec[0] ^ rec[IPT - 1]) == 0x7FFFFFFFu) err |= 8u;
+    __syncthreads();
+    if (tid == 0) { u32* cc = g.tile_cnt + 4 * tile; cc[0] = cc[1] = cc[2] = cc[3] = 0; }
+    if (!more) break;
+    tile = tnext; nmA0 = xA0; nmA1 = xA1; nmB0 = xB0; nmB1 = xB1;
+    continue;
+#endif
     // ---- 3. matched pairs: rows from LDS, then OIDs and name offsets ----
     u32 ra[IPT], rb[IPT];
 #pragma unroll
@@ -1610,7 +1626,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if ((dif >> k) & 1) s_drec[od++] = rec[k];
     __syncthreads();  // (s_wave reused below)
     const u64 nk = k1e - k0;
-    const int rounds = nk ? 64 - __clzll((long long)nk) : 0;  // wave-uniform
+    // 4-ary lower bound: ceil(log4(nk + 1)) rounds of three independent LDS reads (wave-uniform)
+    // (a round leaves at most max(q - 1, w - 3q) of w, q = ceil(w / 4): 5 rounds for 384 keys)
+    int rounds = 0;
+    for (u64 w = nk; w > 0; rounds++) {
+        const u64 q = (w + 3) / 4;
+        const u64 r = w > 3 * q ? w - 3 * q : 0;
+        w = q - 1 > r ? q - 1 : r;
+    }
     u32 tc = 0, tm = 0;
     u32* sc = g3.stage_conf + tile * (u64)C2_STAGE * 3;
     uint2* sm = g3.stage_md + tile * (u64)C2_STAGE;
@@ -1627,14 +1650,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const u32 kind = r0 >> 25, ia = r0 & 0xFFF, jb = (r0 >> 12) & 0xFFF;
         const u64 key = kind == R_INS ? sB[jb] : sA[ia];
         const u32 nk32 = (u32)nk;
+        // invariant: every index < lo holds a smaller key, every index >= hi a key >= key
         u32 lo = 0, hi = act ? nk32 : 0;
+        const u32 last = nk32 ? nk32 - 1 : 0;
         for (int it = 0; it < rounds; it++) {
-            const u32 m = (lo + hi) >> 1;
-            const u32 mi = m < nk32 ? m : (nk32 ? nk32 - 1 : 0);
-            const u64 v = lk ? sK[mi] : g3.K[k0 + mi];
-            const bool on = lo < hi, lt = v < key;
-            lo = on && lt ? m + 1 : lo;
-            hi = on && !lt ? m : hi;
+            const u32 st = (hi - lo + 3) >> 2;
+            const u32 p1 = lo + st - 1, p2 = p1 + st, p3 = p2 + st;
+            const u32 q1 = p1 < last ? p1 : last, q2 = p2 < last ? p2 : last, q3 = p3 < last ? p3 : last;
+            const u64 v1 = lk ? sK[q1] : g3.K[k0 + q1], v2 = lk ? sK[q2] : g3.K[k0 + q2], v3 = lk ? sK[q3] : g3.K[k0 + q3];
+            const bool on = lo < hi;
+            const bool l1 = on && p1 < hi && v1 < key, l2 = on && p2 < hi && v2 < key, l3 = on && p3 < hi && v3 < key;
+            const u32 nlo = l3 ? p3 + 1 : l2 ? p2 + 1 : l1 ? p1 + 1 : lo;
+            const u32 nhi = !on ? hi : !l1 ? (p1 < hi ? p1 : hi) : !l2 ? (p2 < hi ? p2 : hi) : !l3 ? (p3 < hi ? p3 : hi) : hi;
+            lo = nlo;
+            hi = nhi;
         }
         const bool found = act && lo < nk32 && (lk ? sK[lo] : g3.K[k0 + lo]) == key;
         ik = found ? (u32)(k0 + lo) : KD_NONE;
@@ -1694,18 +1723,39 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         clean += (act && !a_eq_o && a_eq_t && pO) || (md && pT);
         }  // (!SPLIT)
         }  // (a wave with differing paths)
-        u32 tot;
-        const u32 off = block_excl_scan<NT>((u32)cf | (u32)md << 16, s_wave, &tot);
+        // path-order places of the conflicts and merge deltas: ballots within the wave, the waves'
+        // counts through LDS (one barrier pair; a shuffle scan chains six LDS-latency steps)
+        const u64 bc = __ballot(cf), bm = __ballot(md);
+        if (lane == 0) { s_wave[wid] = (u32)__popcll(bc); s_wave[NT / 64 + wid] = (u32)__popcll(bm); }
+        __syncthreads();
+        u32 pc = 0, pm = 0, nc = 0, nm = 0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; w++) {
+            const u32 xc = s_wave[w], xm = s_wave[NT / 64 + w];
+            if (w < wid) { pc += xc; pm += xm; }
+            nc += xc;
+            nm += xm;
+        }
+        __syncthreads();  // (s_wave reused)
         if (cf) {
-            u32* o = sc + 3 * (tc + (off & 0xFFFF));
+            u32* o = sc + 3 * (tc + pc + __builtin_amdgcn_mbcnt_hi((u32)(bc >> 32), __builtin_amdgcn_mbcnt_lo((u32)bc, 0)));
             o[0] = ik; o[1] = io; o[2] = itt;
         }
-        if (md) sm[tm + (off >> 16)] = make_uint2(io, itt);
-        tc += tot & 0xFFFF;
-        tm += tot >> 16;
+        if (md) sm[tm + pm + __builtin_amdgcn_mbcnt_hi((u32)(bm >> 32), __builtin_amdgcn_mbcnt_lo((u32)bm, 0))] = make_uint2(io, itt);
+        tc += nc;
+        tm += nm;
     }
     if (ne) err |= 2u;
-    const u32 tcl = block_sum<NT>(clean, s_wave);  // (its barriers: every LDS read of this tile is done)
+    // the tile's clean count: per wave by bit-sliced ballots (clean <= IPT + 2 < 8), summed by thread 0
+    {
+        const u32 wcl = (u32)__popcll(__ballot(clean & 1)) + 2u * (u32)__popcll(__ballot((clean >> 1) & 1)) +
+                        4u * (u32)__popcll(__ballot((clean >> 2) & 1));
+        if (lane == 0) s_wave[2 * (NT / 64) + wid] = wcl;
+    }
+    __syncthreads();  // (also: every LDS read of this tile is done before the next tile's DMA)
+    u32 tcl = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) tcl += s_wave[2 * (NT / 64) + w];
     if (tid == 0) {
         u32* cc = g.tile_cnt + 4 * tile;
         cc[0] = tcl; cc[1] = tm; cc[2] = 0; cc[3] = tc;
@@ -1797,12 +1847,12 @@ int merge3_join_device(kd_ctx* ctx, const kd_side& K, const kd_side& O, const kd
     }
     auto j3b_grid = [&](const void* kern) {
         if (!J3B_PERSIST) return (unsigned)ntiles;
-        return (unsigned)std::max<u64>(1, std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)occupancy(ctx, kern, C2_NT, 0)));
+        return (unsigned)std::max<u64>(1, std::min<u64>(ntiles, (u64)ctx->n_cu * (u64)occupancy(ctx, kern, J3B_NT, 0)));
     };
     rc = launch(ctx, "k_join3", [&] {
 #define KD_J3(H, PM, S) hipLaunchKernelGGL((k_join3<C2_NT, J3_IPT, H, PM, S>), dim3((unsigned)ntiles), dim3(C2_NT), 0, ctx->stream, a)
         if (v2) {
-#define KD_J3B(H, PM, S) hipLaunchKernelGGL((k_join3b<C2_NT, J3B_IPT, H, PM, S>), dim3(j3b_grid((const void*)k_join3b<C2_NT, J3B_IPT, H, PM, S>)), dim3(C2_NT), 0, ctx->stream, a)
+#define KD_J3B(H, PM, S) hipLaunchKernelGGL((k_join3b<J3B_NT, J3B_IPT, H, PM, S>), dim3(j3b_grid((const void*)k_join3b<J3B_NT, J3B_IPT, H, PM, S>)), dim3(J3B_NT), 0, ctx->stream, a)
             if (split) {
                 if (hash) { if (perm) KD_J3B(true, true, true); else KD_J3B(true, false, true); }
                 else { if (perm) KD_J3B(false, true, true); else KD_J3B(false, false, true); }
