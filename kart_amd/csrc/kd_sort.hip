@@ -604,7 +604,10 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pk
 constexpr int RS_SEG_MAX = 512;
 // halo SEG_H: RS_SEG_MAX, or 128 when the caller knows every run is at most that long (C4's ~3-entry
 // leaf trees: 0.34 vs 0.46 ms per 50M side; C3's ~64-entry ones likewise)
-constexpr int SEG_NT = 256, SEG_IPT = 8, SEG_T = SEG_NT * SEG_IPT, SEG_HS = 128;
+#ifndef KD_SEG_IPT
+#define KD_SEG_IPT 8
+#endif
+constexpr int SEG_NT = 256, SEG_IPT = KD_SEG_IPT, SEG_T = SEG_NT * SEG_IPT, SEG_HS = 128;
 
 // block-wide inclusive scan (op = max or min) of one u32 per thread, in thread order
 template <bool MAX>
