@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--c3-layer", action="store_true",
                     help="c5: the C3 polygon layer instead of SURVEY's C5 mix (points, straddles, wide, EMPTY, edge)")
     ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
+    ap.add_argument("--update-arenas", action="store_true",
+                    help="c2/c3: field-diff from update-order arenas (the drop-in's form, no pairs) instead of the "
+                         "per-entry arenas through the join's pairs")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/r04/traffic_<wl>.json, else profiles/traffic_<wl>.json)")
     ap.add_argument("--no-heads-path", action="store_true", help="c5env: skip the indexer's heads-path timing")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
@@ -332,6 +335,12 @@ def run_diff(args, H, polygons):
         pipe.step()
     eng.sync()
     counts, delta, upd, masks, status = pipe.results()
+    if args.update_arenas:  # the drop-in's arena form: update-order blobs, no pairs (same bytes)
+        pipe.use_update_arenas(upd)
+        pipe.step()
+        eng.sync()
+        counts, delta, upd2, masks, status = pipe.results()
+        assert np.array_equal(upd2, upd)
     plan = (L.n_insert, L.n_update, L.n_delete)
     if not args.no_check:
         assert (counts["inserts"], counts["updates"], counts["deletes"]) == plan, (counts, plan)

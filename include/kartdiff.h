@@ -149,6 +149,7 @@ int kd_set_stream(kd_ctx* ctx, void* hip_stream);
  *   j2_oidlds_min  [KD_J2_OIDLDS_MIN]  k_join2 stages OIDs in LDS from this many entries (2^26)
  *   j2r            [KD_J2R]            1: the persistent register-prefetched int-key join
  *   fd_stream      [KD_FD_STREAM]      -1 auto, 0 windowed, 1 streamed field diff (contiguous arenas)
+ *   fd_walk        [KD_FD_WALK]        -1 / 0 off, 1 the walked field diff (A/B)
  *   pkm_max_blocks [KD_PKM_MAX_BLOCKS] largest pk range (64-pk blocks) kd_delta_pk_order places by bitmap
  *   trace_host     [KD_TRACE_HOST]     1: stream-synced wall-clock marks of host phases to stderr */
 int kd_set_option(kd_ctx* ctx, const char* name, int64_t value);

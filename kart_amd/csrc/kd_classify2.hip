@@ -583,9 +583,11 @@ __global__ __launch_bounds__(NT) void k_join2(Join2Args g) {
 #pragma unroll
         for (int k = 0; k < IPT; k++) {
             const bool m = (rec[k] >> 25) == R_MATCH;
-            const u64 i = m ? ra[k] : rA0, j = m ? rb[k] : rB0;
-            oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
-            ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
+            // unmatched items load nothing (a placeholder row could be the side's end: off[n + 1]
+            // lies past the caller's n + 1 offsets)
+            const u64 i = m ? ra[k] : 0, j = m ? rb[k] : 0;
+            oa0[k] = m ? offA[2 * i] : 0u; oa1[k] = m ? offA[2 * i + 2] : 0u;
+            ob0[k] = m ? offB[2 * j] : 0u; ob1[k] = m ? offB[2 * j + 2] : 0u;
         }
     }
     if (LOIDS) {  // matched pairs' OIDs from LDS (both tile ranges landed with the keys)
@@ -1119,9 +1121,11 @@ __global__ __launch_bounds__(NT) void k_join3(Join3Args g3) {
 #pragma unroll
         for (int k = 0; k < IPT; k++) {
             const bool m = (rec[k] >> 25) == R_MATCH;
-            const u64 i = m ? ra[k] : rA0, j = m ? rb[k] : rB0;
-            oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
-            ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
+            // unmatched items load nothing (a placeholder row could be the side's end: off[n + 1]
+            // lies past the caller's n + 1 offsets)
+            const u64 i = m ? ra[k] : 0, j = m ? rb[k] : 0;
+            oa0[k] = m ? offA[2 * i] : 0u; oa1[k] = m ? offA[2 * i + 2] : 0u;
+            ob0[k] = m ? offB[2 * j] : 0u; ob1[k] = m ? offB[2 * j + 2] : 0u;
         }
     }
     if (LOIDS) {  // matched pairs' OIDs from LDS (both tile ranges landed with the keys)
@@ -1559,9 +1563,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
         for (int k = 0; k < IPT; k++) {
             const bool m = (rec[k] >> 25) == R_MATCH;
-            const u64 i = m ? ra[k] : rA0, j = m ? rb[k] : rB0;
-            oa0[k] = offA[2 * i]; oa1[k] = offA[2 * i + 2];
-            ob0[k] = offB[2 * j]; ob1[k] = offB[2 * j + 2];
+            // unmatched items load nothing (a placeholder row could be the side's end: off[n + 1]
+            // lies past the caller's n + 1 offsets)
+            const u64 i = m ? ra[k] : 0, j = m ? rb[k] : 0;
+            oa0[k] = m ? offA[2 * i] : 0u; oa1[k] = m ? offA[2 * i + 2] : 0u;
+            ob0[k] = m ? offB[2 * j] : 0u; ob1[k] = m ? offB[2 * j + 2] : 0u;
         }
     }
     tile_oid_cmp<IPT>(g, rec, ra, rb);
@@ -1746,10 +1752,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         tm += nm;
     }
     if (ne) err |= 2u;
-    // the tile's clean count: per wave by bit-sliced ballots (clean <= IPT + 2 < 8), summed by thread 0
+    // the tile's clean count: per wave by bit-sliced ballots, summed by thread 0.  A thread counts at
+    // most its IPT items plus one per compaction pass (at most ceil(ndif / NT) <= IPT passes), so
+    // clean <= 2 IPT < 16: four slices
+    static_assert(2 * IPT < 16, "k_join3b: the clean count's ballot slices");
     {
         const u32 wcl = (u32)__popcll(__ballot(clean & 1)) + 2u * (u32)__popcll(__ballot((clean >> 1) & 1)) +
-                        4u * (u32)__popcll(__ballot((clean >> 2) & 1));
+                        4u * (u32)__popcll(__ballot((clean >> 2) & 1)) + 8u * (u32)__popcll(__ballot((clean >> 3) & 1));
         if (lane == 0) s_wave[2 * (NT / 64) + wid] = wcl;
     }
     __syncthreads();  // (also: every LDS read of this tile is done before the next tile's DMA)

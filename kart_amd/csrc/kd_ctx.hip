@@ -279,7 +279,7 @@ using namespace kd;
 
 namespace kd {
 int occupancy(kd_ctx* ctx, const void* kernel, int block, size_t lds) {
-    const auto key = std::make_pair(kernel, lds);
+    const auto key = std::make_tuple(kernel, block, lds);
     auto it = ctx->occ.find(key);
     if (it != ctx->occ.end()) return it->second;
     int nb = 0;
@@ -318,6 +318,7 @@ const OptDef OPTS[] = {
     {"j2_oidlds_min", "KD_J2_OIDLDS_MIN", nullptr, nullptr, &kd_opts::j2_oidlds_min},
     {"j2r", "KD_J2R", nullptr, &kd_opts::j2r, nullptr},
     {"fd_stream", "KD_FD_STREAM", nullptr, &kd_opts::fd_stream, nullptr},
+    {"fd_walk", "KD_FD_WALK", nullptr, &kd_opts::fd_walk, nullptr},
     {"pkm_max_blocks", "KD_PKM_MAX_BLOCKS", nullptr, nullptr, &kd_opts::pkm_max_blocks},
     {"trace_host", "KD_TRACE_HOST", nullptr, &kd_opts::trace_host, nullptr},
 };

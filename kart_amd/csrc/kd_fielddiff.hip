@@ -247,25 +247,27 @@ __device__ __forceinline__ int find_legend(TP tab, int n, P hex) {
 constexpr u32 FD_MAXV = 4096;  // oracle limit (status 3 above it)
 constexpr int FD_NT = 64;      // one wave per block
 
+// MR mask words live in registers (constant indices: selects, not a dynamic index, so mk stays in
+// VGPRs); words >= MR are ORed in place
+template <int MR = 4>
 __device__ __forceinline__ void set_bit(u64 mk[4], u64* m, int k) {
     const u64 bit = 1ull << (k & 63);
-    const int w = k >> 6;  // selects, not a dynamic index: mk stays in registers
-    mk[0] |= w == 0 ? bit : 0;
-    mk[1] |= w == 1 ? bit : 0;
-    mk[2] |= w == 2 ? bit : 0;
-    mk[3] |= w == 3 ? bit : 0;
-    if (w >= 4) m[w] |= bit;
+    const int w = k >> 6;
+#pragma unroll
+    for (int i = 0; i < MR; i++) mk[i] |= w == i ? bit : 0;
+    if (w >= MR) m[w] |= bit;
 }
 
-// the update's mask words: the first four from registers (constant indices: mk stays in VGPRs), the
-// rest were ORed in place and are cleared when the update failed
+// the update's mask words: the first MR from registers, the rest were ORed in place and are cleared
+// when the update failed
+template <int MR = 4>
 __device__ __forceinline__ void store_masks(u64* m, int words, const u64 mk[4], u8 st) {
     m[0] = mk[0];
-    if (words > 1) m[1] = mk[1];
-    if (words > 2) m[2] = mk[2];
-    if (words > 3) m[3] = mk[3];
+#pragma unroll
+    for (int i = 1; i < MR; i++)
+        if (words > i) m[i] = mk[i];
     if (st)
-        for (int w = 4; w < words; w++) m[w] = 0;
+        for (int w = MR; w < words; w++) m[w] = 0;
 }
 
 // Value `want` of a blob, walking forward from a cursor (idx, pos); a backward request restarts
@@ -417,6 +419,40 @@ struct WBlob {
     }
 };
 
+// One blob of one lane read straight from global memory (k_fdwalk): no LDS image.  Every read is
+// one 16-B load at a byte address (gfx950 runs in unaligned mode: global_load_dwordx4 takes any
+// address), so a decode window costs one load and no realignment.  GUARD: the blob lies within 16 B
+// of its arena's end (`guard`) — loads then stop at `lim` (aligned dwords below it, realigned), so
+// nothing is read past the caller's allocation; every other blob reads unguarded (up to 15 B past its
+// end, inside the arena; callers bound every decoded byte by the blob length).
+template <bool GUARD>
+struct HBlobT {
+    static constexpr bool lds_only = false;
+    u64 start;
+    u32 len;
+    bool guard;  // GUARD: this blob's loads are bounded by lim (else unguarded)
+    u64 lim;     // end of the arena's valid bytes
+};
+typedef u32x4 __attribute__((aligned(1))) u32x4_b;
+typedef const __attribute__((address_space(1))) u32x4_b* gp128b;
+
+template <bool GUARD>
+__device__ __forceinline__ u32x4 h_ld16(const HBlobT<GUARD>& b, u32 p) {
+    const u64 x = b.start + p;
+    if (!GUARD || !b.guard || x + 16 <= b.lim) return *(gp128b)x;
+    const u64 x4 = x & ~3ull;
+    const u32 s = (u32)(x & 3);
+    u32 w[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = x4 + 4 * i < b.lim ? ((gp32)x4)[i] : 0u;
+    u32x4 r;
+    r.x = __builtin_amdgcn_alignbyte(w[1], w[0], s);
+    r.y = __builtin_amdgcn_alignbyte(w[2], w[1], s);
+    r.z = __builtin_amdgcn_alignbyte(w[3], w[2], s);
+    r.w = __builtin_amdgcn_alignbyte(w[4], w[3], s);
+    return r;
+}
+
 __device__ __forceinline__ u32 lds_u32(u32 addr) { return *(lp32)(size_t)addr; }
 
 // bytes [p, p + 12) of a blob as three little-endian words (bytes past the blob: zero or garbage;
@@ -440,6 +476,22 @@ __device__ __forceinline__ void rd12(const BL& b, u32 p, u32& x0, u32& x1, u32& 
     x0 = __builtin_amdgcn_alignbyte(w1, w0, s);
     x1 = __builtin_amdgcn_alignbyte(w2, w1, s);
     x2 = __builtin_amdgcn_alignbyte(w3, w2, s);
+}
+
+template <bool GUARD>
+__device__ __forceinline__ void rd12(const HBlobT<GUARD>& b, u32 p, u32& x0, u32& x1, u32& x2) {
+    const u32x4 v = h_ld16(b, p);
+    x0 = v.x;
+    x1 = v.y;
+    x2 = v.z;
+}
+
+template <bool GUARD>
+__device__ __forceinline__ void rd_legend(const HBlobT<GUARD>& b, u32 lp, u32 h[10]) {
+    const u32x4 c0 = h_ld16(b, lp), c1 = h_ld16(b, lp + 16), c2 = h_ld16(b, lp + 32);
+    h[0] = c0.x; h[1] = c0.y; h[2] = c0.z; h[3] = c0.w;
+    h[4] = c1.x; h[5] = c1.y; h[6] = c1.z; h[7] = c1.w;
+    h[8] = c2.x; h[9] = c2.y;
 }
 
 // the 40 legend hex bytes at blob position lp as 10 words
@@ -610,6 +662,49 @@ __device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb
     return glb_bytes_eq(xa, xb, n) ? 0u : 1u;
 }
 
+// bytes [p, p + 16) of a and b differ, counting only the first n (n >= 1)
+__device__ __forceinline__ bool chunk_ne(const u32x4& a, const u32x4& b, u32 n) {
+    const u32 m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1;
+    const u32 m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1;
+    const u32 m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1;
+    const u32 m3 = n >= 16 ? ~0u : n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1;
+    return (((a.x ^ b.x) & m0) | ((a.y ^ b.y) & m1) | ((a.z ^ b.z) & m2) | ((a.w ^ b.w) & m3)) != 0;
+}
+
+// k_fdwalk's payload compare: up to FD_LOCAL bytes by this lane (every 16-B load of both ranges issued
+// before the first compare), longer payloads queued for the wave's cooperative compare while the
+// queue has room, else by this lane FD_LOCAL bytes at a time
+constexpr u32 FD_LOCAL = 32;
+template <bool GUARD>
+__device__ __forceinline__ u32 range_eq(const HBlobT<GUARD>& A, u32 pa, const HBlobT<GUARD>& B, u32 pb, u32 n, int key,
+                                        const FdQueue& q) {
+    if (n > FD_LOCAL && q.cap && key < 64) {
+        const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t < q.cap) {
+            q.task[3 * t] = A.start + pa;
+            q.task[3 * t + 1] = B.start + pb;
+            q.task[3 * t + 2] = (u64)n | (u64)threadIdx.x << 32 | (u64)key << 48;
+            return 3;
+        }
+    }
+    for (u32 o = 0; o < n; o += FD_LOCAL) {
+        u32x4 a[FD_LOCAL / 16], b[FD_LOCAL / 16];
+        const u32 r = n - o;
+#pragma unroll
+        for (int k = 0; k < (int)(FD_LOCAL / 16); k++)
+            if (16u * k < r) {
+                a[k] = h_ld16(A, pa + o + 16 * k);
+                b[k] = h_ld16(B, pb + o + 16 * k);
+            }
+        bool ne = false;
+#pragma unroll
+        for (int k = 0; k < (int)(FD_LOCAL / 16); k++)
+            if (16u * k < r) ne |= chunk_ne(a[k], b[k], r - 16 * k);
+        if (ne) return 1u;
+    }
+    return 0u;
+}
+
 // byte payloads of a and b (same class, ext, length >= 1) at blob positions pa / pb:
 // 0 equal, 1 changed, 3 queued
 template <class BL>
@@ -738,7 +833,11 @@ __device__ __forceinline__ bool seek_value_w(const BL& b, u32 first, u32 want, u
 }
 
 // one update from its windows: returns the status; mask bits (k < 256) in mk, the rest straight into m
-template <class BL, class TB>
+template <int MR, class BL, class TB>
+__device__ __forceinline__ u8 diff_body(const BL& A, const BL& B, const TB& tb, u32 cvo, u32 po, u32 cvn, u32 pn,
+                                        int li_o, int li_n, u64 mk[4], u64* m, const FdQueue& q);
+
+template <int MR = 4, class BL, class TB>
 __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb, u64 mk[4], u64* m, const FdQueue& q) {
     u32 cvo, cvn, po, pn, lpo, lpn;
     if (parse_header_w(A, &cvo, &po, &lpo) || parse_header_w(B, &cvn, &pn, &lpn)) return 1;
@@ -747,6 +846,53 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
     const int li_o = find_legend_w(tb.leg_o, tb.n_lo, h);
     rd_legend(B, lpn, h);
     const int li_n = find_legend_w(tb.leg_n, tb.n_ln, h);
+    return diff_body<MR>(A, B, tb, cvo, po, cvn, pn, li_o, li_n, mk, m, q);
+}
+
+// k_fdwalk's header read: bytes [0, 48) of the blob in three loads issued together — 0x92, the
+// canonical str8 legend header d9 28 (what msgpack writes for a 40-char str), the 40 legend bytes
+// and the array header — -> 0 ok, 1 malformed (as parse_header_w), -1 another legend header form
+// (the caller takes parse_header_w + rd_legend)
+template <bool GUARD>
+__device__ __forceinline__ int head_h(const HBlobT<GUARD>& b, u32* nvals, u32* off, u32 h[10]) {
+    if (b.len < 44) return 1;
+    const u32x4 c0 = h_ld16(b, 0), c1 = h_ld16(b, 16), c2 = h_ld16(b, 32);
+    const u32 d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+    if ((d[0] & 0xff) != 0x92) return 1;
+    if ((d[0] & 0xffffff) != 0x28d992) return -1;
+#pragma unroll
+    for (int i = 0; i < 10; i++) h[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], 3);  // bytes 3..42
+    const u32 t = d[10] >> 24;  // byte 43: the array header
+    const u32 b44 = d[11] & 0xff, b45 = (d[11] >> 8) & 0xff, b46 = (d[11] >> 16) & 0xff, b47 = d[11] >> 24;
+    if (t >= 0x90 && t <= 0x9f) { *nvals = t & 15; *off = 44; return 0; }
+    if (t == 0xdc) { if (46 > b.len) return 1; *nvals = b44 << 8 | b45; *off = 46; return 0; }
+    if (t == 0xdd) { if (48 > b.len) return 1; *nvals = b44 << 24 | b45 << 16 | b46 << 8 | b47; *off = 48; return 0; }
+    return 1;
+}
+
+template <int MR, bool GUARD, class TB>
+__device__ __forceinline__ u8 diff_one_h(const HBlobT<GUARD>& A, const HBlobT<GUARD>& B, const TB& tb, u64 mk[4], u64* m,
+                                         const FdQueue& q) {
+    u32 cvo = 0, cvn = 0, po = 0, pn = 0, lp, ha[10], hb[10];
+    const int ra = head_h(A, &cvo, &po, ha), rb = head_h(B, &cvn, &pn, hb);
+    if (ra == 1 || rb == 1) return 1;
+    // a non-canonical legend header (str16 / str32): the general header parse
+    if (ra < 0) {
+        if (parse_header_w(A, &cvo, &po, &lp)) return 1;
+        rd_legend(A, lp, ha);
+    }
+    if (rb < 0) {
+        if (parse_header_w(B, &cvn, &pn, &lp)) return 1;
+        rd_legend(B, lp, hb);
+    }
+    const int li_o = find_legend_w(tb.leg_o, tb.n_lo, ha);
+    const int li_n = find_legend_w(tb.leg_n, tb.n_ln, hb);
+    return diff_body<MR>(A, B, tb, cvo, po, cvn, pn, li_o, li_n, mk, m, q);
+}
+
+template <int MR, class BL, class TB>
+__device__ __forceinline__ u8 diff_body(const BL& A, const BL& B, const TB& tb, u32 cvo, u32 po, u32 cvn, u32 pn,
+                                        int li_o, int li_n, u64 mk[4], u64* m, const FdQueue& q) {
     if (li_o < 0 || li_n < 0) return 2;
     if (cvo > FD_MAXV || cvn > FD_MAXV) return 3;
     const bool al = tb.aligned[li_o * tb.n_ln + li_n];
@@ -770,7 +916,7 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
                     r = scalar_eq(a, b);
                     if (r == 2) r = payload_eq(a, A, pa, b, B, pb, k, q);
                 }
-                if (r == 1) set_bit(mk, m, k);
+                if (r == 1) set_bit<MR>(mk, m, k);
             }
             pa += fa.used;
             pb += fb.used;
@@ -812,7 +958,7 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
             r = scalar_eq(a, b);
             if (r == 2) r = payload_eq(a, A, ipo, b, B, ipn, k, q);
         }
-        if (r == 1) set_bit(mk, m, k);
+        if (r == 1) set_bit<MR>(mk, m, k);
     }
     return 0;
 }
@@ -887,6 +1033,76 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
     }
 #pragma unroll
     for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
+}
+
+// bytes [p, p + n) (n < 16) as a 16-B value, zero past n: the aligned dwords holding them, realigned
+// (no byte outside the range's dwords is read)
+__device__ __forceinline__ u32x4 ld_short(u64 p, u32 n) {
+    const u64 p4 = p & ~3ull, e = p + n;
+    const u32 s = (u32)(p & 3);
+    u32 w[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = p4 + 4 * i < e ? ((gp32)p4)[i] : 0u;
+    u32x4 r;
+    r.x = __builtin_amdgcn_alignbyte(w[1], w[0], s);
+    r.y = __builtin_amdgcn_alignbyte(w[2], w[1], s);
+    r.z = __builtin_amdgcn_alignbyte(w[3], w[2], s);
+    r.w = __builtin_amdgcn_alignbyte(w[4], w[3], s);
+    const u32 m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1;
+    const u32 m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1;
+    const u32 m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1;
+    const u32 m3 = n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1;
+    r.x &= m0; r.y &= m1; r.z &= m2; r.w &= m3;
+    return r;
+}
+
+// Cooperative compare of M queued payloads by one G-lane group with byte-addressed 16-B loads (gfx950
+// runs in unaligned mode): lane j of step s compares chunk c = G s + j of both payloads at the same
+// payload offset min(16 c, n - 16) — the last chunk overlaps the one before it instead of running
+// past the payload, so every byte read lies inside both payloads and nothing is masked or
+// realigned.  Payloads under 16 B compare masked (ld_short).  d[m] = "payload m differs", on every
+// lane of the group; an absent payload has n = 0.
+template <int M, int G, int S>
+__device__ __forceinline__ void coop_differs_u(const u64 (&a)[M], const u64 (&b)[M], const u32 (&n)[M], bool (&d)[M]) {
+    const u32 j = threadIdx.x & (G - 1), grp = (threadIdx.x & 63) / G;
+    u32 nmax = 0;
+    bool diff[M];
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+        nmax = n[m] > nmax ? n[m] : nmax;
+        diff[m] = false;
+    }
+    for (u32 c0 = 0; 16 * c0 < nmax; c0 += G * S) {
+        u32x4 A[M][S], B[M][S];
+#pragma unroll
+        for (int m = 0; m < M; m++)
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                const u32 c = c0 + G * s + j;
+                const bool act = 16 * c < n[m];
+                const u32 off = n[m] >= 16 ? min(16 * c, n[m] - 16) : 0;
+                const u32x4 z = {0, 0, 0, 0};
+                A[m][s] = act ? (n[m] >= 16 ? *(gp128b)(a[m] + off) : ld_short(a[m], n[m])) : z;
+                B[m][s] = act ? (n[m] >= 16 ? *(gp128b)(b[m] + off) : ld_short(b[m], n[m])) : z;
+            }
+#pragma unroll
+        for (int m = 0; m < M; m++)
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                const u32x4 x = A[m][s] ^ B[m][s];
+                diff[m] |= (x.x | x.y | x.z | x.w) != 0;
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
+}
+#ifndef KD_FD_COOPU
+#define KD_FD_COOPU 1  // the queued payloads by byte-addressed loads (0: aligned chunks + funnel shifts)
+#endif
+template <int M, int G, int S>
+__device__ __forceinline__ void coop_cmp(const u64 (&a)[M], const u64 (&b)[M], const u32 (&n)[M], bool (&d)[M]) {
+    if (KD_FD_COOPU) coop_differs_u<M, G, S>(a, b, n, d);
+    else coop_differs<M, G, S>(a, b, n, d);
 }
 
 constexpr u32 FD_TAB_LDS_MAX = 16384;
@@ -1099,7 +1315,7 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
                 tn[m] = (u32)tx[m];
             }
             bool d[M];
-            coop_differs<M, G, TS>(ta, tbb, tn, d);
+            coop_cmp<M, G, TS>(ta, tbb, tn, d);
 #pragma unroll
             for (int m = 0; m < M; m++)
                 if (d[m] && (lane & (G - 1)) == 0) {
@@ -1307,6 +1523,148 @@ __global__ __launch_bounds__(FD_NT) void k_fielddiff_s(const u8* __restrict__ od
     }
 }
 
+// ================================================================================================
+// walked variant (k_fdwalk, the default for larger features): no LDS images and no staging.  One
+// wave per workgroup, 64 updates per round, one lane per update; each lane walks its two blobs value
+// by value straight from global memory (HBlobT: one 16-B load per decode window, the header, legend
+// and array header in one batch of three), compares scalars and payloads up to FD_LOCAL bytes in
+// registers, and queues longer payloads (geometries of equal length) for the wave's cooperative
+// compare.  A value the comparison does not need is never read: the middle of a geometry whose
+// length changed costs no bytes.  With no LDS image the kernel keeps few registers and many waves
+// per SIMD in flight, and the latency of the walk's dependent loads (mostly L2 hits after the
+// blob's first line) hides behind the other waves.
+// ================================================================================================
+#ifndef KD_FDW_SHAPE
+#define KD_FDW_SHAPE 1, 16, 2  // cooperative compare: payloads per 16-lane group per pass, lanes per payload, steps
+#endif
+#ifndef KD_FDW_CAP
+#define KD_FDW_CAP 32  // resident workgroups per CU at most
+#endif
+template <int TM, int TG, int TS>
+#ifndef KD_FDW_WPE
+#define KD_FDW_WPE 4  // waves per SIMD the register budget is sized for
+#endif
+__global__ __launch_bounds__(FD_NT) __attribute__((amdgpu_waves_per_eu(KD_FDW_WPE))) void k_fdwalk(const u8* __restrict__ od, const u64* __restrict__ ooff,
+                                                  const u8* __restrict__ nd, const u64* __restrict__ noff,
+                                                  const uint2* __restrict__ pairs, u64 n_upd_host,
+                                                  const u64* __restrict__ n_upd_dev, u64 n_ent_o, u64 n_ent_n,
+                                                  FdTab tg, FdTabOff to, const u8* __restrict__ tab_base,
+                                                  u64* __restrict__ masks, u8* __restrict__ status) {
+    constexpr u32 TCAP = FD_NT;  // queued payload compares per round (then a lane compares alone)
+    __shared__ u64 s_task[3 * TCAP];
+    __shared__ u64 s_res[FD_NT];  // mask bits (keys < 64) found by the cooperative compares
+    __shared__ u32 s_ntask;
+    extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
+    const int lane = threadIdx.x;
+    const bool spec = n_upd_dev && n_upd_host;
+    const u64 n_upd = n_upd_dev ? *n_upd_dev : n_upd_host;
+    const u64 lim = spec ? n_upd_host : n_upd;
+    const u64 end = min(lim, n_upd);
+    const u64 step = (u64)gridDim.x * FD_NT;
+    u64 u0 = (u64)blockIdx.x * FD_NT;
+    if (u0 >= end) return;  // wave-uniform
+    // the arenas' ends: no load crosses them
+    const u64 olim = (u64)od + ooff[n_ent_o], nlim = (u64)nd + noff[n_ent_n];
+    auto load_pair = [&](u64 uu) {
+        uint2 p = make_uint2((u32)uu, (u32)uu);
+        if (pairs && uu < end) p = pairs[uu];
+        return p;
+    };
+    auto load_off = [&](uint2 p, bool a, u64& os_, u64& ns_, u32& on_, u32& nn_) {
+        os_ = ns_ = 0;
+        on_ = nn_ = 0;
+        if (a) {
+            os_ = ooff[p.x];
+            ns_ = noff[p.y];
+            on_ = (u32)(ooff[p.x + 1] - os_);
+            nn_ = (u32)(noff[p.y + 1] - ns_);
+        }
+    };
+    u64 u1 = u0 + step;
+    u64 os, ns;
+    u32 on, nn;
+    load_off(load_pair(u0 + lane), u0 + lane < end, os, ns, on, nn);
+    for (u32 i = 16 * lane; i < to.bytes; i += 16 * FD_NT) *(u32x4*)(s_tab + i) = *(gp128)(tab_base + i);
+    mp_tab_to_lds();
+    s_res[lane] = 0;
+    if (lane == 0) s_ntask = 0;
+    FdTabT<3> tb;
+    tb.n_keys = tg.n_keys; tb.words = tg.words; tb.n_lo = tg.n_lo; tb.n_ln = tg.n_ln; tb.maxv = tg.maxv;
+    typedef __attribute__((address_space(3))) u8* l8;
+    const l8 lt = (l8)s_tab;
+    tb.leg_o = (typename ASP<3, u32>::type)(lt + to.leg_o);
+    tb.leg_n = (typename ASP<3, u32>::type)(lt + to.leg_n);
+    tb.map_o = (typename ASP<3, i16>::type)(lt + to.map_o);
+    tb.map_n = (typename ASP<3, i16>::type)(lt + to.map_n);
+    tb.cmp = (typename ASP<3, u64>::type)(lt + to.cmp);
+    tb.aligned = (typename ASP<3, u8>::type)(lt + to.aligned);
+    tb.key_of_val = (typename ASP<3, i16>::type)(lt + to.key_of_val);
+    const FdQueue queue{(lds_u64p)s_task, (lds_u32p)&s_ntask, TCAP};
+    uint2 pr_n = load_pair(u1 + lane);
+    __syncthreads();  // the tables are in LDS
+    for (;;) {
+        const u64 u = u0 + lane;
+        const bool act = u < end;
+        const bool more = u1 < end;  // wave-uniform
+        u64 os_n = 0, ns_n = 0, u2 = end;
+        u32 on_n = 0, nn_n = 0;
+        if (more) {  // the next round's offsets are in flight during this round's walk
+            load_off(pr_n, u1 + lane < end, os_n, ns_n, on_n, nn_n);
+            u2 = u1 + step;
+        }
+        u64 mk[4] = {0, 0, 0, 0};
+        u8 st = 0;
+        u64* m = masks + u * tb.words;
+        if (act) {
+            for (int w = 1; w < tb.words; w++) m[w] = 0;
+            const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
+            // a blob within 16 B of its arena's end: every load bounded by it
+            const HBlobT<true> A{a0, on, a0 + on + 16 > olim, olim}, B{b0, nn, b0 + nn + 16 > nlim, nlim};
+            st = diff_one_h<1>(A, B, tb, mk, m, queue);
+        }
+        __syncthreads();  // the walk is done: the queue is complete
+        if (more) pr_n = load_pair(u2 + lane);
+        // ---- the queued payloads, TG lanes per payload, TM per group per pass ----
+        const u32 nt = min(s_ntask, TCAP);
+        constexpr int M = TM, G = TG, NG = 64 / TG;
+        for (u32 t = (u32)lane / G; t < nt; t += NG * M) {
+            u64 ta[M], tbb[M], tx[M];
+            u32 tn[M];
+#pragma unroll
+            for (int k = 0; k < M; k++) {
+                const u32 tm = t + NG * k;
+                const bool h = tm < nt;
+                ta[k] = h ? s_task[3 * tm] : 0;
+                tbb[k] = h ? s_task[3 * tm + 1] : 0;
+                tx[k] = h ? s_task[3 * tm + 2] : 0;
+                tn[k] = (u32)tx[k];
+            }
+            bool d[M];
+            coop_cmp<M, G, TS>(ta, tbb, tn, d);
+#pragma unroll
+            for (int k = 0; k < M; k++)
+                if (d[k] && (lane & (G - 1)) == 0) {
+                    const u32 ow = (u32)(tx[k] >> 32) & 0xFFFF, key = (u32)(tx[k] >> 48);
+                    atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
+                }
+        }
+        __syncthreads();  // the compares are in s_res
+        if (act) {
+            mk[0] |= s_res[lane];
+            if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
+            store_masks<1>(m, tb.words, mk, st);
+            status[u] = st;
+        }
+        s_res[lane] = 0;
+        if (lane == 0) s_ntask = 0;
+        if (!more) break;
+        __builtin_amdgcn_wave_barrier();
+        u0 = u1;
+        u1 = u2;
+        os = os_n; ns = ns_n; on = on_n; nn = nn_n;
+    }
+}
+
 // Fallback for tables too large for LDS: one lane per update, blobs parsed straight from global
 // memory.
 __global__ __launch_bounds__(FD_NT) void k_fielddiff_g(const u8* __restrict__ od, const u64* __restrict__ ooff,
@@ -1454,9 +1812,13 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     // 0 / 1 forces it off / on
     const int stream_env = ctx->opt.fd_stream;
     const bool stream = lds_tab && d_pu == nullptr && (stream_env >= 0 ? stream_env > 0 : !small && KD_FD_STREAM_DEFAULT);
+    // the walked kernel (no LDS images; slower: DESIGN §3.2): the fd_walk option 1 forces it
+    const int walk_env = ctx->opt.fd_walk;
+    const bool walk = lds_tab && !stream && walk_env > 0;
     // The kernel loops over rounds (grid stride), so its grid is the resident set (occupancy
     // calculator for this launch's LDS), capped at the measured optimum.
-    const void* kern = stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SPF>
+    const void* kern = walk ? (const void*)k_fdwalk<KD_FDW_SHAPE>
+                       : stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SPF>
                        : !lds_tab ? (const void*)k_fielddiff_g
                        : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
     int per_cu = 0;
@@ -1465,8 +1827,8 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
 #ifndef KD_FD_CAP
 #define KD_FD_CAP 12  // C2 points: 10 / 12 blocks per CU = 36.8 / 35.1 us (C3 is LDS-bound at 8)
 #endif
-    per_cu = std::max(1, std::min(per_cu, stream ? 16 : KD_FD_CAP));
-    const u64 upr = stream ? (u64)fd_stream_t<KD_FD_SSHAPE>() : !lds_tab ? FD_NT : small ? fd_upr<KD_FD_SHAPE_S>(nullptr) : fd_upr<KD_FD_SHAPE_L>(nullptr);
+    per_cu = std::max(1, std::min(per_cu, walk ? KD_FDW_CAP : stream ? 16 : KD_FD_CAP));
+    const u64 upr = walk ? (u64)FD_NT : stream ? (u64)fd_stream_t<KD_FD_SSHAPE>() : !lds_tab ? FD_NT : small ? fd_upr<KD_FD_SHAPE_S>(nullptr) : fd_upr<KD_FD_SHAPE_L>(nullptr);
     unsigned blocks = (unsigned)std::min<u64>((work + upr - 1) / upr, (u64)ctx->n_cu * (u64)per_cu);
     if (blocks == 0) blocks = 1;
     rc = launch(ctx, "k_fielddiff", [&] {
@@ -1475,7 +1837,11 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
                                tb, to, (const u8*)dt, d_masks, d_status);
         };
-        if (stream)
+        if (walk)
+            hipLaunchKernelGGL((k_fdwalk<KD_FDW_SHAPE>), dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
+                               (const u64*)d_ooff, (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd,
+                               (u64)ob->n, (u64)nb->n, tb, to, (const u8*)dt, d_masks, d_status);
+        else if (stream)
             hipLaunchKernelGGL((k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SPF>), dim3(blocks), dim3(FD_NT), o_end, ctx->stream, (const u8*)d_od,
                                (const u64*)d_ooff, (const u8*)d_nd, (const u64*)d_noff, n_upd, d_n_upd, tb, to,
                                (const u8*)dt, d_masks, d_status);

@@ -8,6 +8,7 @@
 #include <utility>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "kartdiff.h"
@@ -72,6 +73,7 @@ struct kd_opts {
     uint64_t j2_oidlds_min = 1ull << 26;  // KD_J2_OIDLDS_MIN: k_join2 stages OIDs in LDS from this many entries
     int j2r = 0;                     // KD_J2R: 1 = the persistent register-prefetched k_join2r
     int fd_stream = -1;              // KD_FD_STREAM: -1 auto, 0 windowed k_fielddiff, 1 streamed k_fielddiff_s
+    int fd_walk = -1;                // KD_FD_WALK: -1 / 0 off, 1 the walked k_fdwalk (A/B)
     uint64_t pkm_max_blocks = 1ull << 26;  // KD_PKM_MAX_BLOCKS: largest pk range (64-pk blocks) of the bitmap pk order
     int trace_host = 0;              // KD_TRACE_HOST: 1 = stream-synced wall-clock marks to stderr
 };
@@ -105,8 +107,8 @@ struct kd_ctx {
     int h_counts_ranks = 0;
     uint64_t gather_send_cap = 0;  // records the last _begin's d_delta holds (base.n + target.n + 1)
     int occ_resolve3 = 0;  // resident k_resolve3 workgroups per CU
-    // resident workgroups per CU by (kernel, dynamic LDS): asked once per context (kd::occupancy)
-    std::map<std::pair<const void*, size_t>, int> occ;
+    // resident workgroups per CU by (kernel, block size, dynamic LDS): asked once per context (kd::occupancy)
+    std::map<std::tuple<const void*, int, size_t>, int> occ;
     uint32_t rs_epoch = 0;  // kd_sort: epoch of the last pass's look-back words (kd_sort.hip)
     // small workspaces come from one slab (one hipMalloc instead of one per slot on a process's
     // first calls); grown slots take a fresh piece, the slab is freed with the context

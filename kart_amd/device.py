@@ -226,6 +226,8 @@ class DiffPipeline:
                 self.seg_err.zero()
         self.OB = DevBlobs(engine, *base_blobs)
         self.NB = DevBlobs(engine, *target_blobs)
+        self.OB_off_host, self.NB_off_host = base_blobs[1], target_blobs[1]
+        self._ob_u = None  # use_update_arenas: update-order arenas (no pairs)
         self.maps = maps
         cap = base.n + target.n + 1
         self.cap = cap
@@ -267,6 +269,32 @@ class DiffPipeline:
             self.all_delta = DevBuf(engine, 8 * self.all_cap)
         engine.reserve(max(base.n, target.n))
         engine.sync()
+
+    def use_update_arenas(self, upd):
+        """field-diff from update-order arenas (the drop-in's form: the blob reader writes update i's
+        blobs at arena index i) instead of the per-entry arenas through the join's pairs.  The
+        per-entry arenas here hold the updated entries' blobs only, back to back in key (= update)
+        order, so the update-order arenas are the same bytes with one offset per update: only those
+        offsets are uploaded.  ``upd`` = the join's update list [m, 2] (the same every step)."""
+        ob, nb = self.OB, self.NB
+        oo_h = self.OB_off_host[np.asarray(upd[:, 0], np.int64)]
+        no_h = self.NB_off_host[np.asarray(upd[:, 1], np.int64)]
+        m = int(upd.shape[0])
+        oo = np.empty(m + 1, np.uint64)
+        no = np.empty(m + 1, np.uint64)
+        oo[:m], no[:m] = oo_h, no_h
+        oo[m] = self.OB_off_host[int(upd[-1, 0]) + 1] if m else 0
+        no[m] = self.NB_off_host[int(upd[-1, 1]) + 1] if m else 0
+        # the arenas must be contiguous in update order (each update's blob right after the last)
+        ob_len = self.OB_off_host[np.asarray(upd[:, 0], np.int64) + 1] - oo_h
+        nb_len = self.NB_off_host[np.asarray(upd[:, 1], np.int64) + 1] - no_h
+        if not (np.array_equal(oo[1:], oo[:-1] + np.append(ob_len, 0)[:m]) and
+                np.array_equal(no[1:], no[:-1] + np.append(nb_len, 0)[:m])):
+            raise ValueError("the per-entry arenas are not contiguous in update order")
+        self.u_off = (DevBuf.from_numpy(self.eng, oo), DevBuf.from_numpy(self.eng, no))
+        self._ob_u, self._nb_u = ob.kd_blobs(), nb.kd_blobs()
+        self._ob_u.n, self._nb_u.n = m, m
+        self._ob_u.off, self._nb_u.off = self.u_off[0].ptr, self.u_off[1].ptr
 
     def reserve_gather(self, max_deltas_per_rank):
         """size the gathered-record buffer for at most this many deltas on any rank"""
@@ -329,9 +357,16 @@ class DiffPipeline:
             N.check(L.kd_diff2_gather_begin(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.gather[0],
                                             self.gather[1], self.flags, self.delta.ptr, self.upd.ptr, self.counts.ptr,
                                             self.counts.ptr + 32, self.all_counts.ptr), "kd_diff2_gather_begin")
-        N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.ptr, self.cap_upd,
+        if self._ob_u is not None:  # update-order arenas: update i's blobs at index i, no pairs
+            N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob_u), ctypes.byref(self._nb_u), None, self.cap_upd,
+                                   ctypes.cast(self.counts.ptr + 8, N.c_u64p), N.KD_MEM_DEVICE,
+                                   ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE),
+                    "kd_fielddiff")
+        else:
+            N.check(L.kd_fielddiff(ctx, ctypes.byref(self._ob), ctypes.byref(self._nb), self.upd.ptr, self.cap_upd,
                                ctypes.cast(self.counts.ptr + 8, N.c_u64p), N.KD_MEM_DEVICE,
-                               ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE), "kd_fielddiff")
+                                   ctypes.byref(self._km), self.masks.ptr, self.status.ptr, N.KD_MEM_DEVICE),
+                    "kd_fielddiff")
         if keys:
             lo, hi = self.pk_range
             N.check(L.kd_delta_pk_order(ctx, ctypes.byref(self._sa), ctypes.byref(self._sb), self.delta.ptr,

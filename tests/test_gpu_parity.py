@@ -27,6 +27,34 @@ def _g_classify(engine):
     return f
 
 
+@pytest.mark.parametrize("kern", ["win", "walk"])
+@pytest.mark.parametrize("name", DIFF_FIXTURES)
+def test_gpu_fielddiff_kernels_golden(engine, request, name, kern):
+    """every golden diff case (schema changes, legend changes, the reference's own repositories)
+    through the windowed and the walked field-diff kernels, whatever size picks by default"""
+    _fd_kernel(engine, request, kern)
+    fx = load(name)
+    for case in fx.cases("diff2"):
+        check_diff_case(fx, case, _g_classify(engine), engine.fielddiff)
+
+
+@pytest.mark.parametrize("kern", ["win", "walk"])
+@pytest.mark.parametrize("layer", ["points", "polygons", "polygons_same"])
+def test_gpu_fielddiff_kernels_pairs(engine, request, layer, kern):
+    """pair-indexed arenas (every entry's blob, the bench's sparse form) through both kernels"""
+    from kart_amd import synth
+    from kart_amd.schema import FieldMaps
+
+    _fd_kernel(engine, request, kern)
+    L = (synth.points_layer(300_000, seed=21) if layer == "points" else
+         synth.polygons_layer(600_000, seed=22, same_len=0.6 if layer == "polygons_same" else 0.0))
+    maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    r = engine.diff2(L.base, L.target)
+    gm, gs = engine.fielddiff(*L.base_blobs, *L.target_blobs, r.upd, maps)
+    om, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, r.upd, maps)
+    assert np.array_equal(gm, om) and np.array_equal(gs, ost)
+
+
 @pytest.mark.parametrize("name", DIFF_FIXTURES)
 def test_gpu_diff2_golden(engine, name):
     fx = load(name)
@@ -707,18 +735,34 @@ def _grow_geometry(blob, extra, rng):
                          default=lambda g: msgpack.ExtType(ord("G"), bytes(g)))
 
 
-@pytest.mark.parametrize("stream", ["0", "1"])
+# kd_fielddiff's kernels by option: (fd_stream, fd_walk)
+FD_KERNELS = {"win": (0, 0), "stream": (1, 0), "walk": (0, 1)}
+
+
+def _fd_kernel(engine, request, kern):
+    stream, walk = FD_KERNELS[kern]
+    engine.set_option("fd_stream", stream)
+    engine.set_option("fd_walk", walk)
+
+    def restore():
+        engine.set_option("fd_stream", -1)
+        engine.set_option("fd_walk", -1)
+
+    request.addfinalizer(restore)
+
+
+@pytest.mark.parametrize("kern", ["win", "stream", "walk"])
 @pytest.mark.parametrize("case", ["c3", "c3v", "huge", "ragged", "points", "one"])
-def test_gpu_fielddiff_contiguous_vs_oracle(engine, request, stream, case):
-    """kd_fielddiff on update arenas laid back to back (no pairs: the drop-in's and the bench's form),
-    through the streamed kernel (fd_stream option 1: whole tile spans into LDS) and the windowed one:
-    C3 / C3v polygons, a tile whose span overflows the LDS buffer (blobs of 20-60 KB, read from
-    global memory past it), update counts that end inside a tile, point features"""
+def test_gpu_fielddiff_contiguous_vs_oracle(engine, request, kern, case):
+    """kd_fielddiff on update arenas laid back to back (no pairs: the drop-in's form), through the
+    streamed kernel (whole tile spans into LDS), the windowed one and the walked one (k_fdwalk, every
+    read straight from HBM): C3 / C3v polygons, a tile whose span overflows the LDS buffer (blobs of
+    20-60 KB: the walk queues their payloads), update counts that end inside a tile, point features.
+    The last blob of every arena ends at the arena's end: the walk's guarded loads"""
     from kart_amd import synth
     from kart_amd.schema import FieldMaps
 
-    engine.set_option("fd_stream", int(stream))
-    request.addfinalizer(lambda: engine.set_option("fd_stream", -1))
+    _fd_kernel(engine, request, kern)
     rng = np.random.default_rng(7)
     if case == "points":
         L = synth.points_layer(300_000, seed=3)
