@@ -51,6 +51,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 REFERENCE_CPU_PATH = {"value": 0.54, "unit": "M feature-pairs/s", "cores": 1, "kind": "reference",
                       "sample": "BASELINE.md: reference kart diff hot path (Python + git diff-tree), synthetic 1M "
                                 "points, 1 % U/I/D, build container (the reference cannot run on the GPU box)"}
+# the same reference path measured on C3's own edit mix (8 % updates, 1 % deletes, 1 % inserts of a 3M
+# polygon layer): profiles/r05/ref_path_3m.json (scripts/ref_path_bench.py, build container, 1 core)
+REFERENCE_CPU_PATH_C3 = {"value": 0.097, "unit": "M feature-pairs/s", "cores": 1, "kind": "reference",
+                         "mix": "C3's mix: 8 % updates / 1 % deletes / 1 % inserts, 3M-polygon layer",
+                         "file": "profiles/r05/ref_path_3m.json",
+                         "sample": "the reference's Dataset3.diff + get_feature of both sides of every update + the "
+                                   "Python == field compare, 1 thread; libgit2's tree diff by git diff-tree (C)",
+                         "differently_mixed": dict(REFERENCE_CPU_PATH, mix="BASELINE.md's points layer at 1 / 1 / 1 % edits")}
 
 
 def parse():
@@ -89,9 +97,9 @@ def parse():
     ap.add_argument("--c3-layer", action="store_true",
                     help="c5: the C3 polygon layer instead of SURVEY's C5 mix (points, straddles, wide, EMPTY, edge)")
     ap.add_argument("--no-arena-timing", action="store_true", help="c5: skip timing the arena path beside the heads")
-    ap.add_argument("--update-arenas", action="store_true",
-                    help="c2/c3: field-diff from update-order arenas (the drop-in's form, no pairs) instead of the "
-                         "per-entry arenas through the join's pairs")
+    ap.add_argument("--pair-arenas", action="store_true",
+                    help="c2/c3: field-diff from the per-entry arenas through the join's update pairs instead of "
+                         "update-order arenas (the drop-in's form: the blob reader writes update i's blobs at index i)")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/r04/traffic_<wl>.json, else profiles/traffic_<wl>.json)")
     ap.add_argument("--no-heads-path", action="store_true", help="c5env: skip the indexer's heads-path timing")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
@@ -335,7 +343,7 @@ def run_diff(args, H, polygons):
         pipe.step()
     eng.sync()
     counts, delta, upd, masks, status = pipe.results()
-    if args.update_arenas:  # the drop-in's arena form: update-order blobs, no pairs (same bytes)
+    if not args.pair_arenas:  # the drop-in's arena form: update-order blobs, no pairs (same bytes)
         pipe.use_update_arenas(upd)
         pipe.step()
         eng.sync()
@@ -426,6 +434,9 @@ def run_diff(args, H, polygons):
                    "delta_order": "tile-grouped (same delta set)" if args.unordered else
                    ("walk (= key) order, then pk order (kd_delta_pk_order)" if pk_sort else "walk (= key) order"),
                    "side_order": "git tree (walk) order as listed, no side sort",
+                   "blob_arenas": ("per-entry arenas read through the join's update pairs" if args.pair_arenas else
+                                   "update-order arenas (the drop-in's form: update i's blobs at index i; the field "
+                                   "diff reads the join's device update count)"),
                    "parallelism": f"bucket-range shards x{world}" + (", RCCL all-gather of counts + delta records"
                                                                       if split else "")},
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
@@ -653,7 +664,7 @@ def cpu_baseline_diff(L, maps, seconds, tag):
                       f"fielddiff on {cores} threads over {parts} bucket-range shards",
             "one_thread": {"value": round(p1 * reps1 / dt1 / 1e6, 3), "unit": "M feature-pairs/s", "cores": 1,
                            "sample": f"one shard ({p1} pairs, 1/{parts} of the layer) x {reps1} reps in {dt1:.1f}s"},
-            "reference_path": REFERENCE_CPU_PATH}
+            "reference_path": REFERENCE_CPU_PATH_C3 if tag == "C3" else REFERENCE_CPU_PATH}
 
 
 def cpu_sharded(work, parts, seconds):

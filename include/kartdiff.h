@@ -472,6 +472,11 @@ int kd_int_keys_to_pks(const uint64_t* keys, uint64_t n, int64_t* pks);
 #define KD_ENOTFOUND (-4) /* object not in the odb (missing, or promised by a partial clone) */
 typedef struct kd_odb kd_odb;
 int kd_odb_open(const char* gitdir, kd_odb** out);
+/* Options of an object store (A/B switches; kd_odb_open seeds each from the environment variable in
+ * brackets).  Unknown names: KD_EINVAL.
+ *   zlib           [KD_ODB_ZLIB]       1: inflate with zlib even when libdeflate.so.0 is present */
+int kd_odb_set_option(kd_odb* odb, const char* name, int64_t value);
+int kd_odb_get_option(kd_odb* odb, const char* name, int64_t* value);
 int kd_odb_close(kd_odb* odb);
 /* One object (*type 1 commit, 2 tree, 3 blob, 4 tag); *data malloc'd (kd_free). */
 int kd_odb_read(kd_odb* odb, const uint8_t oid[20], int* type, uint8_t** data, uint64_t* len);

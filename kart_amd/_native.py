@@ -296,6 +296,8 @@ SIGNATURES = {
     "kd_int_keys_to_pks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "kd_odb_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     "kd_odb_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "kd_odb_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),
+    "kd_odb_get_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "kd_odb_read": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_u8p), c_u64p],

@@ -457,9 +457,23 @@ __device__ __forceinline__ u32 lds_u32(u32 addr) { return *(lp32)(size_t)addr; }
 
 // bytes [p, p + 12) of a blob as three little-endian words (bytes past the blob: zero or garbage;
 // callers bound every access by the blob length)
+#ifndef KD_FD_LDSU
+#define KD_FD_LDSU 0  // 1: LDS windows read by byte-addressed ds_read_b128 (measured ~2 % slower than aligned dwords + v_alignbyte)
+#endif
+typedef const __attribute__((address_space(3))) u32x4_b* lp128b;
+__device__ __forceinline__ u32x4 lds_u128(u32 addr) { return *(lp128b)(size_t)addr; }
+
 template <class BL>
 __device__ __forceinline__ void rd12(const BL& b, u32 p, u32& x0, u32& x1, u32& x2) {
     const u32 x = p + b.s0, x4 = x & ~3u, s = x & 3;
+    if (KD_FD_LDSU) {  // one 16-B read at the byte address (the 4 bytes past the 12 are not used)
+        const u32 o = b.win(x, 12);
+        if (BL::lds_only || o != ~0u) {
+            const u32x4 v = lds_u128(b.img + o);
+            x0 = v.x; x1 = v.y; x2 = v.z;
+            return;
+        }
+    }
     u32 w0, w1, w2, w3;
     const u32 o = b.win(x4, 16);
     if (BL::lds_only || o != ~0u) {
@@ -498,6 +512,16 @@ __device__ __forceinline__ void rd_legend(const HBlobT<GUARD>& b, u32 lp, u32 h[
 template <class BL>
 __device__ __forceinline__ void rd_legend(const BL& b, u32 lp, u32 h[10]) {
     const u32 x = lp + b.s0, x4 = x & ~3u, s = x & 3;
+    if (KD_FD_LDSU) {
+        const u32 o = b.win(x, 40);
+        if (BL::lds_only || o != ~0u) {
+            const u32x4 c0 = lds_u128(b.img + o), c1 = lds_u128(b.img + o + 16), c2 = lds_u128(b.img + o + 32);
+            h[0] = c0.x; h[1] = c0.y; h[2] = c0.z; h[3] = c0.w;
+            h[4] = c1.x; h[5] = c1.y; h[6] = c1.z; h[7] = c1.w;
+            h[8] = c2.x; h[9] = c2.y;
+            return;
+        }
+    }
     u32 w[11];
     const u32 o = b.win(x4, 44);
     if (BL::lds_only || o != ~0u) {
@@ -600,6 +624,22 @@ __device__ bool lds_bytes_eq(u32 a, u32 b, u32 n) {
     return diff == 0;
 }
 
+// LDS byte compare by byte-addressed 16-B reads (the reads may run up to 15 bytes past either range,
+// inside the block's LDS, or return 0 past its end; bytes past n are masked)
+__device__ bool lds_bytes_eq_u(u32 a, u32 b, u32 n) {
+    u32 diff = 0;
+    for (u32 o = 0; o < n && diff == 0; o += 16) {
+        const u32x4 x = lds_u128(a + o) ^ lds_u128(b + o);
+        const u32 r = n - o;
+        const u32 m0 = r >= 4 ? ~0u : (1u << (8 * r)) - 1;
+        const u32 m1 = r >= 8 ? ~0u : r <= 4 ? 0u : (1u << (8 * (r - 4))) - 1;
+        const u32 m2 = r >= 12 ? ~0u : r <= 8 ? 0u : (1u << (8 * (r - 8))) - 1;
+        const u32 m3 = r >= 16 ? ~0u : r <= 12 ? 0u : (1u << (8 * (r - 12))) - 1;
+        diff = (x.x & m0) | (x.y & m1) | (x.z & m2) | (x.w & m3);
+    }
+    return diff == 0;
+}
+
 // global byte compare by one lane (queue overflow, keys >= 256): aligned dword loads, realigned;
 // a dword is loaded only when it holds a byte of its range
 __device__ bool glb_bytes_eq(u64 a, u64 b, u32 n) {
@@ -629,14 +669,29 @@ __device__ bool glb_bytes_eq(u64 a, u64 b, u32 n) {
 #define KD_FD_PROBE_NOLDSCMP 0  // timing probe only (results invalid): in-LDS payload compares skipped
 #endif
 
+#ifndef KD_FD_HEADF
+#define KD_FD_HEADF 1  // windowed kernel: the fast header read (head_fast) before the general parse
+#endif
+
 // Per-round queue of payloads compared cooperatively after the parse (in LDS).
 typedef __attribute__((address_space(3))) u64* lds_u64p;
 typedef __attribute__((address_space(3))) u32* lds_u32p;
 struct FdQueue {
-    lds_u64p task;  // [3 * cap] (old address, new address, len | lane << 32 | key << 48)
+    lds_u64p task;  // [2 * cap]: (old address | lane << 48 | key << 54, new address | len << 48)
     lds_u32p count;
     u32 cap;
 };
+
+// queue the compare of n bytes at a against n bytes at b (16 B per task: device addresses below 2^48,
+// payloads of 16 B to 64 KiB, keys < 64); false when it does not fit (the caller compares alone)
+__device__ __forceinline__ bool task_put(const FdQueue& q, u64 a, u64 b, u32 n, int key) {
+    if (!q.cap || key >= 64 || n < 16 || n >= 65536 || ((a | b) >> 48)) return false;
+    const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (t >= q.cap) return false;
+    q.task[2 * t] = a | (u64)(threadIdx.x & 63) << 48 | (u64)key << 54;
+    q.task[2 * t + 1] = b | (u64)n << 48;
+    return true;
+}
 
 // bytes [pa, pa + n) of blob A against [pb, pb + n) of blob B: 0 equal, 1 changed, 3 queued for
 // the cooperative compare (from the LDS windows when both ranges lie in one, else queued while the
@@ -644,21 +699,21 @@ struct FdQueue {
 template <class BL>
 __device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb, u32 n, int key, const FdQueue& q) {
     const u32 ya = pa + A.s0, yb = pb + B.s0;  // offsets from the head bases
-    const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
-    if (BL::lds_only || (oa != ~0u && ob != ~0u)) {
-        if (KD_FD_PROBE_NOLDSCMP) return 0u;
-        return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
-    }
-    const u64 xa = A.start + pa, xb = B.start + pb;
-    if (q.cap && key < 64) {
-        const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (t < q.cap) {
-            q.task[3 * t] = xa;
-            q.task[3 * t + 1] = xb;
-            q.task[3 * t + 2] = (u64)n | (u64)threadIdx.x << 32 | (u64)key << 48;
-            return 3;
+    if (KD_FD_LDSU) {
+        const u32 oa = A.win(ya, n), ob = B.win(yb, n);
+        if (BL::lds_only || (oa != ~0u && ob != ~0u)) {
+            if (KD_FD_PROBE_NOLDSCMP) return 0u;
+            return lds_bytes_eq_u(A.img + oa, B.img + ob, n) ? 0u : 1u;
+        }
+    } else {
+        const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
+        if (BL::lds_only || (oa != ~0u && ob != ~0u)) {
+            if (KD_FD_PROBE_NOLDSCMP) return 0u;
+            return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
         }
     }
+    const u64 xa = A.start + pa, xb = B.start + pb;
+    if (task_put(q, xa, xb, n, key)) return 3;
     return glb_bytes_eq(xa, xb, n) ? 0u : 1u;
 }
 
@@ -678,15 +733,7 @@ constexpr u32 FD_LOCAL = 32;
 template <bool GUARD>
 __device__ __forceinline__ u32 range_eq(const HBlobT<GUARD>& A, u32 pa, const HBlobT<GUARD>& B, u32 pb, u32 n, int key,
                                         const FdQueue& q) {
-    if (n > FD_LOCAL && q.cap && key < 64) {
-        const u32 t = __hip_atomic_fetch_add(q.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (t < q.cap) {
-            q.task[3 * t] = A.start + pa;
-            q.task[3 * t + 1] = B.start + pb;
-            q.task[3 * t + 2] = (u64)n | (u64)threadIdx.x << 32 | (u64)key << 48;
-            return 3;
-        }
-    }
+    if (n > FD_LOCAL && task_put(q, A.start + pa, B.start + pb, n, key)) return 3;
     for (u32 o = 0; o < n; o += FD_LOCAL) {
         u32x4 a[FD_LOCAL / 16], b[FD_LOCAL / 16];
         const u32 r = n - o;
@@ -849,15 +896,12 @@ __device__ __forceinline__ u8 diff_one_w(const BL& A, const BL& B, const TB& tb,
     return diff_body<MR>(A, B, tb, cvo, po, cvn, pn, li_o, li_n, mk, m, q);
 }
 
-// k_fdwalk's header read: bytes [0, 48) of the blob in three loads issued together — 0x92, the
-// canonical str8 legend header d9 28 (what msgpack writes for a 40-char str), the 40 legend bytes
-// and the array header — -> 0 ok, 1 malformed (as parse_header_w), -1 another legend header form
-// (the caller takes parse_header_w + rd_legend)
-template <bool GUARD>
-__device__ __forceinline__ int head_h(const HBlobT<GUARD>& b, u32* nvals, u32* off, u32 h[10]) {
-    if (b.len < 44) return 1;
-    const u32x4 c0 = h_ld16(b, 0), c1 = h_ld16(b, 16), c2 = h_ld16(b, 32);
-    const u32 d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+// The fast header read: bytes [0, 48) of the blob in one batch — 0x92, the canonical str8 legend
+// header d9 28 (what msgpack writes for a 40-char str), the 40 legend bytes and the array header —
+// -> 0 ok, 1 malformed (as parse_header_w), -1 another legend header form (the caller takes
+// parse_header_w + rd_legend)
+// the header checks of head_fast on bytes [0, 48) of a blob as 12 words
+__device__ __forceinline__ int head_words(const u32 d[12], u32 len, u32* nvals, u32* off, u32 h[10]) {
     if ((d[0] & 0xff) != 0x92) return 1;
     if ((d[0] & 0xffffff) != 0x28d992) return -1;
 #pragma unroll
@@ -865,16 +909,39 @@ __device__ __forceinline__ int head_h(const HBlobT<GUARD>& b, u32* nvals, u32* o
     const u32 t = d[10] >> 24;  // byte 43: the array header
     const u32 b44 = d[11] & 0xff, b45 = (d[11] >> 8) & 0xff, b46 = (d[11] >> 16) & 0xff, b47 = d[11] >> 24;
     if (t >= 0x90 && t <= 0x9f) { *nvals = t & 15; *off = 44; return 0; }
-    if (t == 0xdc) { if (46 > b.len) return 1; *nvals = b44 << 8 | b45; *off = 46; return 0; }
-    if (t == 0xdd) { if (48 > b.len) return 1; *nvals = b44 << 24 | b45 << 16 | b46 << 8 | b47; *off = 48; return 0; }
+    if (t == 0xdc) { if (46 > len) return 1; *nvals = b44 << 8 | b45; *off = 46; return 0; }
+    if (t == 0xdd) { if (48 > len) return 1; *nvals = b44 << 24 | b45 << 16 | b46 << 8 | b47; *off = 48; return 0; }
     return 1;
 }
 
-template <int MR, bool GUARD, class TB>
-__device__ __forceinline__ u8 diff_one_h(const HBlobT<GUARD>& A, const HBlobT<GUARD>& B, const TB& tb, u64 mk[4], u64* m,
-                                         const FdQueue& q) {
+// the same from a windowed blob's head window (it holds bytes [0, 48) whenever it spans 64 B: the
+// blob starts at most 15 B into it): 13 aligned LDS words, realigned once
+template <int NH, int NTL>
+__device__ __forceinline__ int head_fast(const WBlob<NH, NTL>& b, u32* nvals, u32* off, u32 h[10]) {
+    static_assert(16 * NH >= 64, "head window");
+    if (b.len < 44) return 1;
+    const u32 s = b.s0 & 3, q = b.img + (b.s0 & ~3u);
+    u32 w[13], d[12];
+#pragma unroll
+    for (int i = 0; i < 13; i++) w[i] = lds_u32(q + 4 * i);
+#pragma unroll
+    for (int i = 0; i < 12; i++) d[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], s);
+    return head_words(d, b.len, nvals, off, h);
+}
+
+template <bool GUARD>
+__device__ __forceinline__ int head_fast(const HBlobT<GUARD>& b, u32* nvals, u32* off, u32 h[10]) {
+    if (b.len < 44) return 1;
+    const u32x4 c0 = h_ld16(b, 0), c1 = h_ld16(b, 16), c2 = h_ld16(b, 32);
+    const u32 d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+    return head_words(d, b.len, nvals, off, h);
+}
+
+// one update with the fast header read (head_fast), else as diff_one_w
+template <int MR, class BL, class TB>
+__device__ __forceinline__ u8 diff_one_f(const BL& A, const BL& B, const TB& tb, u64 mk[4], u64* m, const FdQueue& q) {
     u32 cvo = 0, cvn = 0, po = 0, pn = 0, lp, ha[10], hb[10];
-    const int ra = head_h(A, &cvo, &po, ha), rb = head_h(B, &cvn, &pn, hb);
+    const int ra = head_fast(A, &cvo, &po, ha), rb = head_fast(B, &cvn, &pn, hb);
     if (ra == 1 || rb == 1) return 1;
     // a non-canonical legend header (str16 / str32): the general header parse
     if (ra < 0) {
@@ -1035,42 +1102,21 @@ __device__ __forceinline__ void coop_differs(const u64 (&a)[M], const u64 (&b)[M
     for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
 }
 
-// bytes [p, p + n) (n < 16) as a 16-B value, zero past n: the aligned dwords holding them, realigned
-// (no byte outside the range's dwords is read)
-__device__ __forceinline__ u32x4 ld_short(u64 p, u32 n) {
-    const u64 p4 = p & ~3ull, e = p + n;
-    const u32 s = (u32)(p & 3);
-    u32 w[5];
-#pragma unroll
-    for (int i = 0; i < 5; i++) w[i] = p4 + 4 * i < e ? ((gp32)p4)[i] : 0u;
-    u32x4 r;
-    r.x = __builtin_amdgcn_alignbyte(w[1], w[0], s);
-    r.y = __builtin_amdgcn_alignbyte(w[2], w[1], s);
-    r.z = __builtin_amdgcn_alignbyte(w[3], w[2], s);
-    r.w = __builtin_amdgcn_alignbyte(w[4], w[3], s);
-    const u32 m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1;
-    const u32 m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1;
-    const u32 m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1;
-    const u32 m3 = n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1;
-    r.x &= m0; r.y &= m1; r.z &= m2; r.w &= m3;
-    return r;
-}
-
 // Cooperative compare of M queued payloads by one G-lane group with byte-addressed 16-B loads (gfx950
 // runs in unaligned mode): lane j of step s compares chunk c = G s + j of both payloads at the same
 // payload offset min(16 c, n - 16) — the last chunk overlaps the one before it instead of running
 // past the payload, so every byte read lies inside both payloads and nothing is masked or
-// realigned.  Payloads under 16 B compare masked (ld_short).  d[m] = "payload m differs", on every
-// lane of the group; an absent payload has n = 0.
+// realigned.  Queued payloads are at least 16 B long (task_put); d[m] = "payload m differs", on
+// every lane of the group; an absent payload has n = 0.
 template <int M, int G, int S>
 __device__ __forceinline__ void coop_differs_u(const u64 (&a)[M], const u64 (&b)[M], const u32 (&n)[M], bool (&d)[M]) {
     const u32 j = threadIdx.x & (G - 1), grp = (threadIdx.x & 63) / G;
     u32 nmax = 0;
-    bool diff[M];
+    u32 diff[M];
 #pragma unroll
     for (int m = 0; m < M; m++) {
         nmax = n[m] > nmax ? n[m] : nmax;
-        diff[m] = false;
+        diff[m] = 0;
     }
     for (u32 c0 = 0; 16 * c0 < nmax; c0 += G * S) {
         u32x4 A[M][S], B[M][S];
@@ -1078,23 +1124,22 @@ __device__ __forceinline__ void coop_differs_u(const u64 (&a)[M], const u64 (&b)
         for (int m = 0; m < M; m++)
 #pragma unroll
             for (int s = 0; s < S; s++) {
-                const u32 c = c0 + G * s + j;
-                const bool act = 16 * c < n[m];
-                const u32 off = n[m] >= 16 ? min(16 * c, n[m] - 16) : 0;
+                const u32 o = 16 * (c0 + G * s + j);
+                const u32 off = min(o, n[m] - 16);
                 const u32x4 z = {0, 0, 0, 0};
-                A[m][s] = act ? (n[m] >= 16 ? *(gp128b)(a[m] + off) : ld_short(a[m], n[m])) : z;
-                B[m][s] = act ? (n[m] >= 16 ? *(gp128b)(b[m] + off) : ld_short(b[m], n[m])) : z;
+                A[m][s] = o < n[m] ? *(gp128b)(a[m] + off) : z;
+                B[m][s] = o < n[m] ? *(gp128b)(b[m] + off) : z;
             }
 #pragma unroll
         for (int m = 0; m < M; m++)
 #pragma unroll
             for (int s = 0; s < S; s++) {
                 const u32x4 x = A[m][s] ^ B[m][s];
-                diff[m] |= (x.x | x.y | x.z | x.w) != 0;
+                diff[m] |= x.x | x.y | x.z | x.w;
             }
     }
 #pragma unroll
-    for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m]) >> (G * grp)) & ((1ull << G) - 1)) != 0;
+    for (int m = 0; m < M; m++) d[m] = ((__ballot(diff[m] != 0) >> (G * grp)) & ((1ull << G) - 1)) != 0;
 }
 #ifndef KD_FD_COOPU
 #define KD_FD_COOPU 1  // the queued payloads by byte-addressed loads (0: aligned chunks + funnel shifts)
@@ -1114,13 +1159,13 @@ constexpr u32 FD_TAB_LDS_MAX = 16384;
 #ifndef KD_FD_TGS_L
 #define KD_FD_TGS_L 16, 2  // lanes per payload, 16-B steps per lane per pass
 #endif
-#define KD_FD_SHAPE_L 60, 5, 4, KD_FD_TM_L, KD_FD_TGS_L  // C3: 44 / 48 (9 blocks) / 52 / 56 / 60 updates per round = 1.691 / 1.753 / 1.705 / 1.659 / 1.633 ms
+#define KD_FD_SHAPE_L 64, 5, 4, KD_FD_TM_L, KD_FD_TGS_L  // C3 (update-order arenas, round 6): 56 / 60 / 64 updates per round = 1.371 / 1.337 / 1.299 ms
 #endif
 #ifndef KD_FD_SHAPE_S
 #define KD_FD_SHAPE_S 32, 8, 3, 1, 16, 2  // C2 (10M points): tail 2 / 3 chunks = 40.5 / 37.4 us
 #endif
 template <int UPR, int NH, int NTL, int TM, int TG, int TS>
-constexpr int fd_upr(const void*) { return UPR; }
+constexpr int fd_upr(const void*) { return UPR; }  // (the shape macros' first entry)
 #ifndef KD_FD_SSHAPE
 #define KD_FD_SSHAPE 32, 16384  // streamed kernel: updates per tile, LDS bytes per side
 #endif
@@ -1140,7 +1185,7 @@ typedef const __attribute__((address_space(1))) void* fd_glb_vp;
 #else
 #define KD_FD_ATTR
 #endif
-template <int UPR, int NH, int NTL, int TM, int TG, int TS>
+template <int UPR, int NH, int NTL, int TM, int TG, int TS, int MR>
 __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __restrict__ od, const u64* __restrict__ ooff,
                                                      const u8* __restrict__ nd, const u64* __restrict__ noff,
                                                      const uint2* __restrict__ pairs, u64 n_upd_host,
@@ -1153,7 +1198,7 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
     constexpr u32 TCAP = UPR;          // queued payload compares per round (then a lane compares alone)
     static_assert(NTL >= 1, "window shape");
     __shared__ u32x4 s_img[NCH];
-    __shared__ u64 s_task[3 * TCAP];
+    __shared__ u64 s_task[2 * TCAP];
     __shared__ u64 s_res[UPR];         // mask bits (keys < 64) found by the cooperative compares
     __shared__ u32 s_ntask;
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
@@ -1226,15 +1271,29 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
     // the one straddling the two halves stages one side only, so it shuffles two descriptor words,
     // not four (the fully unrolled stage keeps every shuffle result live until its one wait).
     constexpr u32 HALF = (u32)UPR * NC;
+    // per staging instruction k, this lane's round-invariant part: the owner lane whose descriptors it
+    // reads (src), the window chunk (head chunk i, or tail chunk j counted back from the blob's last)
+    // and whether that owner is real — packed src | off << 8 | head << 12 | real << 13
+    u32 spk[NCH / 64];
+#pragma unroll
+    for (int k = 0; k < NCH / 64; k++) {
+        const u32 c = 64 * k + (lane & 63);
+        const bool sb = c >= HALF;
+        const u32 cs = sb ? c - HALF : c;
+        const u32 ow = cs / NC, i = cs - ow * NC;
+        const bool real = ow < (u32)UPR;
+        const bool head = i < (u32)NH;
+        const u32 off = head ? i : (u32)(NTL - 1) - (i - NH);
+        spk[k] = (real ? ow : 0u) | off << 8 | (u32)head << 12 | (u32)real << 13;
+    }
     auto stage = [&]() {
 #pragma unroll
         for (int k = 0; k < NCH / 64; k++) {
             const u32 c = 64 * k + (lane & 63);
             const bool sb = c >= HALF;
-            const u32 cs = sb ? c - HALF : c;
-            const u32 ow = cs / NC, i = cs - ow * NC;
-            const bool real = ow < (u32)UPR;
-            const int src = real ? (int)ow : 0;
+            const int src = (int)(spk[k] & 63);
+            const u32 off = (spk[k] >> 8) & 15;
+            const bool head = (spk[k] >> 12) & 1, real = (spk[k] >> 13) & 1;
             u32 h, l;  // chunk indices
             if (64u * k + 63 < HALF) { h = __shfl(dha, src); l = __shfl(dla, src); }
             else if (64u * k >= HALF) { h = __shfl(dhb, src); l = __shfl(dlb, src); }
@@ -1243,8 +1302,10 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
                 h = sb ? hb_ : ha;
                 l = sb ? lb : la;
             }
-            const u32 ci = i < (u32)NH ? h + i : l - (NTL - 1) + (i - NH);
-            const bool valid = real && (int)(ci - h) >= 0 && (int)(l - ci) >= 0 && l >= h;
+            // head chunk h + off, or tail chunk l - off; it exists when the blob spans that many chunks
+            // (no chunk at all: l < h)
+            const u32 ci = head ? h + off : l - off;
+            const bool valid = real && (int)(l - h) >= (int)off;
             const u64 addr = (sb ? nbase : obase) + 16ull * ci;
             // chunks holding no blob byte are not loaded (their LDS bytes are never decoded: every
             // read is bounded by the blob length)
@@ -1273,7 +1334,7 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
         u8 st = 0;
         u64* m = masks + u * tb.words;
         if (act) {
-            for (int w = 4; w < tb.words; w++) m[w] = 0;
+            for (int w = MR; w < tb.words; w++) m[w] = 0;
             const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
             BL A, B;
             A.start = a0; A.len = on; A.s0 = (u32)(a0 & 15);
@@ -1285,7 +1346,7 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
 #if KD_FD_PROBE_NOPARSE  // timing probe only (results invalid): no parse, no queued payloads
             (void)queue;
 #else
-            st = diff_one_w(A, B, tb, mk, m, queue);
+            st = KD_FD_HEADF ? diff_one_f<MR>(A, B, tb, mk, m, queue) : diff_one_w<MR>(A, B, tb, mk, m, queue);
 #endif
         }
         __syncthreads();  // parse done: the image is free, the queue complete
@@ -1309,17 +1370,18 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
             for (int m = 0; m < M; m++) {
                 const u32 tm = t + NG * m;
                 const bool h = tm < nt;
-                ta[m] = h ? s_task[3 * tm] : 0;
-                tbb[m] = h ? s_task[3 * tm + 1] : 0;
-                tx[m] = h ? s_task[3 * tm + 2] : 0;
-                tn[m] = (u32)tx[m];
+                const u64 w0 = h ? s_task[2 * tm] : 0, w1 = h ? s_task[2 * tm + 1] : 0;
+                ta[m] = w0 & 0xFFFFFFFFFFFFull;
+                tbb[m] = w1 & 0xFFFFFFFFFFFFull;
+                tx[m] = w0 >> 48;  // lane | key << 6
+                tn[m] = (u32)(w1 >> 48);
             }
             bool d[M];
             coop_cmp<M, G, TS>(ta, tbb, tn, d);
 #pragma unroll
             for (int m = 0; m < M; m++)
                 if (d[m] && (lane & (G - 1)) == 0) {
-                    const u32 ow = (u32)(tx[m] >> 32) & 0xFFFF, key = (u32)(tx[m] >> 48);
+                    const u32 ow = (u32)tx[m] & 63, key = (u32)(tx[m] >> 6) & 63;
                     atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
                 }
         }
@@ -1327,7 +1389,7 @@ __global__ __launch_bounds__(FD_NT) KD_FD_ATTR void k_fielddiff(const u8* __rest
         if (act) {
             mk[0] |= s_res[lane];
             if (st) { mk[0] = mk[1] = mk[2] = mk[3] = 0; }
-            store_masks(m, tb.words, mk, st);
+            store_masks<MR>(m, tb.words, mk, st);
             status[u] = st;
         }
         if (owner) s_res[lane] = 0;
@@ -1551,7 +1613,7 @@ __global__ __launch_bounds__(FD_NT) __attribute__((amdgpu_waves_per_eu(KD_FDW_WP
                                                   FdTab tg, FdTabOff to, const u8* __restrict__ tab_base,
                                                   u64* __restrict__ masks, u8* __restrict__ status) {
     constexpr u32 TCAP = FD_NT;  // queued payload compares per round (then a lane compares alone)
-    __shared__ u64 s_task[3 * TCAP];
+    __shared__ u64 s_task[2 * TCAP];
     __shared__ u64 s_res[FD_NT];  // mask bits (keys < 64) found by the cooperative compares
     __shared__ u32 s_ntask;
     extern __shared__ __attribute__((aligned(16))) u8 s_tab[];
@@ -1620,7 +1682,7 @@ __global__ __launch_bounds__(FD_NT) __attribute__((amdgpu_waves_per_eu(KD_FDW_WP
             const u64 a0 = (u64)od + os, b0 = (u64)nd + ns;
             // a blob within 16 B of its arena's end: every load bounded by it
             const HBlobT<true> A{a0, on, a0 + on + 16 > olim, olim}, B{b0, nn, b0 + nn + 16 > nlim, nlim};
-            st = diff_one_h<1>(A, B, tb, mk, m, queue);
+            st = diff_one_f<1>(A, B, tb, mk, m, queue);
         }
         __syncthreads();  // the walk is done: the queue is complete
         if (more) pr_n = load_pair(u2 + lane);
@@ -1634,17 +1696,18 @@ __global__ __launch_bounds__(FD_NT) __attribute__((amdgpu_waves_per_eu(KD_FDW_WP
             for (int k = 0; k < M; k++) {
                 const u32 tm = t + NG * k;
                 const bool h = tm < nt;
-                ta[k] = h ? s_task[3 * tm] : 0;
-                tbb[k] = h ? s_task[3 * tm + 1] : 0;
-                tx[k] = h ? s_task[3 * tm + 2] : 0;
-                tn[k] = (u32)tx[k];
+                const u64 w0 = h ? s_task[2 * tm] : 0, w1 = h ? s_task[2 * tm + 1] : 0;
+                ta[k] = w0 & 0xFFFFFFFFFFFFull;
+                tbb[k] = w1 & 0xFFFFFFFFFFFFull;
+                tx[k] = w0 >> 48;  // lane | key << 6
+                tn[k] = (u32)(w1 >> 48);
             }
             bool d[M];
             coop_cmp<M, G, TS>(ta, tbb, tn, d);
 #pragma unroll
             for (int k = 0; k < M; k++)
                 if (d[k] && (lane & (G - 1)) == 0) {
-                    const u32 ow = (u32)(tx[k] >> 32) & 0xFFFF, key = (u32)(tx[k] >> 48);
+                    const u32 ow = (u32)tx[k] & 63, key = (u32)(tx[k] >> 6) & 63;
                     atomicOr((unsigned long long*)&s_res[ow], 1ull << key);
                 }
         }
@@ -1820,7 +1883,8 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
     const void* kern = walk ? (const void*)k_fdwalk<KD_FDW_SHAPE>
                        : stream ? (const void*)k_fielddiff_s<KD_FD_SSHAPE, KD_FD_SPF>
                        : !lds_tab ? (const void*)k_fielddiff_g
-                       : small ? (const void*)k_fielddiff<KD_FD_SHAPE_S> : (const void*)k_fielddiff<KD_FD_SHAPE_L>;
+                       : small ? (W == 1 ? (const void*)k_fielddiff<KD_FD_SHAPE_S, 1> : (const void*)k_fielddiff<KD_FD_SHAPE_S, 4>)
+                       : (W == 1 ? (const void*)k_fielddiff<KD_FD_SHAPE_L, 1> : (const void*)k_fielddiff<KD_FD_SHAPE_L, 4>);
     int per_cu = 0;
     KD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FD_NT, lds_tab ? o_end : 0));
     // (the calculator can count one block per CU more than becomes resident: DESIGN.md §3.2)
@@ -1849,8 +1913,9 @@ extern "C" int kd_fielddiff(kd_ctx* ctx, const kd_blobs* ob, const kd_blobs* nb,
             hipLaunchKernelGGL(k_fielddiff_g, dim3(blocks), dim3(FD_NT), 0, ctx->stream, (const u8*)d_od, (const u64*)d_ooff,
                                (const u8*)d_nd, (const u64*)d_noff, (const uint2*)d_pu, n_upd, d_n_upd, tb, d_masks,
                                d_status);
-        else if (small) args(k_fielddiff<KD_FD_SHAPE_S>);
-        else args(k_fielddiff<KD_FD_SHAPE_L>);
+        // (mask words kept in registers: one for up to 64 union keys, else four)
+        else if (small) W == 1 ? args(k_fielddiff<KD_FD_SHAPE_S, 1>) : args(k_fielddiff<KD_FD_SHAPE_S, 4>);
+        else W == 1 ? args(k_fielddiff<KD_FD_SHAPE_L, 1>) : args(k_fielddiff<KD_FD_SHAPE_L, 4>);
     });
     if (rc) return rc;
     if (out_mem == KD_MEM_HOST) {

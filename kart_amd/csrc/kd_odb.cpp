@@ -144,6 +144,8 @@ struct kd_odb {
     // more than reading a small object (ctypes drops the GIL, so calls may be concurrent)
     std::mutex pool_mu;
     std::vector<Reader*> pool;
+    // options (kd_odb_set_option; kd_odb_open seeds them from the environment)
+    int zlib_only = 0;  // "zlib" [KD_ODB_ZLIB]: 1 = inflate with zlib even when libdeflate is present (A/B)
 };
 
 namespace {
@@ -245,7 +247,6 @@ struct Deflate {
     free_fn release = nullptr;
     zlib_ex_fn zlib_ex = nullptr;
     Deflate() {
-        if (getenv("KD_ODB_ZLIB")) return;  // A/B switch: zlib only
         void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
         alloc = (alloc_fn)dlsym(h, "libdeflate_alloc_decompressor");
@@ -279,7 +280,7 @@ struct Reader {
     explicit Reader(const kd_odb* d) : db(d), cache(CACHE_SLOTS) {
         memset(&z, 0, sizeof z);
         zok = inflateInit(&z) == Z_OK;
-        if (deflate_lib().ok()) dec = deflate_lib().alloc();
+        if (!d->zlib_only && deflate_lib().ok()) dec = deflate_lib().alloc();
     }
     ~Reader() {
         if (zok) inflateEnd(&z);
@@ -809,8 +810,26 @@ extern "C" int kd_odb_open(const char* gitdir, kd_odb** out) {
         return KD_EINVAL;
     }
     kd_odb* db = new kd_odb();
+    if (const char* v = std::getenv("KD_ODB_ZLIB")) db->zlib_only = (int)strtol(v, nullptr, 10) != 0;
     add_objdir(db, dir + "/objects", 0);
     *out = db;
+    return KD_OK;
+}
+
+extern "C" int kd_odb_set_option(kd_odb* odb, const char* name, int64_t value) {
+    if (!odb || !name) { kd::set_error("kd_odb_set_option: NULL"); return KD_EINVAL; }
+    if (strcmp(name, "zlib") != 0) { kd::set_error("kd_odb_set_option: unknown option '%s'", name); return KD_EINVAL; }
+    std::lock_guard<std::mutex> lk(odb->pool_mu);
+    odb->zlib_only = value != 0;
+    for (Reader* r : odb->pool) delete r;  // pooled readers were built for the old setting
+    odb->pool.clear();
+    return KD_OK;
+}
+
+extern "C" int kd_odb_get_option(kd_odb* odb, const char* name, int64_t* value) {
+    if (!odb || !name || !value) { kd::set_error("kd_odb_get_option: NULL"); return KD_EINVAL; }
+    if (strcmp(name, "zlib") != 0) { kd::set_error("kd_odb_get_option: unknown option '%s'", name); return KD_EINVAL; }
+    *value = odb->zlib_only;
     return KD_OK;
 }
 

@@ -632,12 +632,18 @@ __device__ __forceinline__ u32 seg_block_scan(u32 v, u32* s_w, bool reverse) {
     return x;
 }
 
-template <int SEG_H>
+// BM (runs of up to 64 keys that differ only in their low 6 bits — an int-PK leaf tree of one 2^30
+// wrap, C3's fallback): each run's keys set their bit in a 64-bit map (at slot head / 2: heads of
+// runs of two or more entries are at least two apart), and an entry's rank is the popcount of the
+// bits below its own — O(1) per entry instead of a scan of its run.  A run whose map does not hold
+// one bit per entry (a key differing above bit 5, or a duplicate) is scanned as before.
+template <int SEG_H, bool BM>
 __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key, u64 n, int shift, u64* __restrict__ kout,
                                                      u32* __restrict__ order, u32* __restrict__ err) {
     constexpr int SEG_E = SEG_T + 2 * SEG_H, SEG_EPT = SEG_E / SEG_NT;  // staged entries, per thread (contiguous)
     static_assert(SEG_E % SEG_NT == 0 && SEG_E < 65536, "segmented-sort tile shape");
     __shared__ u64 s_k[SEG_E];
+    __shared__ u64 s_bm[BM ? SEG_E / 2 : 1];
     __shared__ u16 s_st[SEG_E];  // start of the entry's run (LDS index)
     __shared__ u16 s_en[SEG_E];  // end (exclusive; SEG_E fits 16 bits)
     __shared__ u32 s_w[SEG_NT / 64];
@@ -718,6 +724,25 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
             s_en[x0 + j] = (u16)(en_loc[j] != (u32)SEG_E ? en_loc[j] : after);
         }
         __syncthreads();
+        if (BM) {  // the runs' bit maps: cleared by the heads, then every entry of the run sets its bit
+#pragma unroll
+            for (int j = 0; j < SEG_EPT; j++) {
+                const int x = x0 + j;
+                const u32 s0 = s_st[x], len = s_en[x] - s0;
+                if (x >= vlo && x < vhi && (u32)x == s0 && len >= 2 && len <= 64) s_bm[x >> 1] = 0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < SEG_EPT; j++) {
+                const int x = x0 + j;
+                const u32 s0 = s_st[x], len = s_en[x] - s0;
+                if (x >= vlo && x < vhi && len >= 2 && len <= 64) {
+                    const u64 k = s_k[x], hk = s_k[s0];
+                    if (((k ^ hk) >> 6) == 0) atomicOr((unsigned long long*)&s_bm[s0 >> 1], 1ull << (k & 63));
+                }
+            }
+            __syncthreads();
+        }
         // ranks of the tile's own entries
 #pragma unroll 2
         for (int j = 0; j < SEG_IPT; j++) {
@@ -728,6 +753,15 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
             if ((s0 == 0 && g0 > 0) || (e0 == (u32)SEG_E && g0 + SEG_E < (i64)n) || e0 - s0 > (u32)RS_SEG_MAX) {
                 bad |= 4u;  // a run longer than RS_SEG_MAX (or reaching past the halo)
                 continue;
+            }
+            if (BM && e0 - s0 >= 2 && e0 - s0 <= 64) {
+                const u64 bm = s_bm[s0 >> 1];
+                if ((u32)__popcll(bm) == e0 - s0) {  // one bit per entry: distinct keys, ranked by the map
+                    const u64 dst = (u64)(g0 + (i64)s0) + (u32)__popcll(bm & ((1ull << (k & 63)) - 1));
+                    kout[dst] = k;
+                    order[dst] = (u32)(g0 + x);
+                    continue;
+                }
             }
             u32 rank = 0, dup = 0;
             u32 y = s0;
@@ -1041,17 +1075,23 @@ extern "C" int kd_sort_segmented_into(kd_ctx* ctx, const uint64_t* d_key_in, uin
     if (n == 0) return KD_OK;
     const u64 ntiles = (n + SEG_T - 1) / SEG_T;
     const bool small = max_seg > 0 && max_seg <= SEG_HS;
+    // the bit-map ranks for leaf trees of more than 16 entries (int-PK leaf trees hold up to 64; a
+    // hash-PK bucket's few entries differ above bit 5 and are scanned)
+    const bool bm = small && max_seg > 16;
     // one workgroup per tile (the kernel also walks tiles grid-stride with the next tile's keys
     // prefetched, but a resident grid of occupancy x CUs measured slower: 0.272 vs 0.250 ms per 50M
     // C4 side, r5e)
     const unsigned grid = (unsigned)ntiles;
     return launch(ctx, "k_seg_sort", [&] {
-        if (small)
-            hipLaunchKernelGGL(k_seg_sort<SEG_HS>, dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n, 64 - seg_bits,
-                               d_key_out, d_order, d_err);
+        if (small && bm)
+            hipLaunchKernelGGL((k_seg_sort<SEG_HS, true>), dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
+                               64 - seg_bits, d_key_out, d_order, d_err);
+        else if (small)
+            hipLaunchKernelGGL((k_seg_sort<SEG_HS, false>), dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
+                               64 - seg_bits, d_key_out, d_order, d_err);
         else
-            hipLaunchKernelGGL(k_seg_sort<RS_SEG_MAX>, dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n, 64 - seg_bits,
-                               d_key_out, d_order, d_err);
+            hipLaunchKernelGGL((k_seg_sort<RS_SEG_MAX, false>), dim3(grid), dim3(SEG_NT), 0, ctx->stream, d_key_in, n,
+                               64 - seg_bits, d_key_out, d_order, d_err);
     });
 }
 

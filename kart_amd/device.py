@@ -227,6 +227,7 @@ class DiffPipeline:
         self.OB = DevBlobs(engine, *base_blobs)
         self.NB = DevBlobs(engine, *target_blobs)
         self.OB_off_host, self.NB_off_host = base_blobs[1], target_blobs[1]
+        self.OB_data_host, self.NB_data_host = base_blobs[0], target_blobs[0]
         self._ob_u = None  # use_update_arenas: update-order arenas (no pairs)
         self.maps = maps
         cap = base.n + target.n + 1
@@ -272,29 +273,34 @@ class DiffPipeline:
 
     def use_update_arenas(self, upd):
         """field-diff from update-order arenas (the drop-in's form: the blob reader writes update i's
-        blobs at arena index i) instead of the per-entry arenas through the join's pairs.  The
-        per-entry arenas here hold the updated entries' blobs only, back to back in key (= update)
-        order, so the update-order arenas are the same bytes with one offset per update: only those
-        offsets are uploaded.  ``upd`` = the join's update list [m, 2] (the same every step)."""
-        ob, nb = self.OB, self.NB
-        oo_h = self.OB_off_host[np.asarray(upd[:, 0], np.int64)]
-        no_h = self.NB_off_host[np.asarray(upd[:, 1], np.int64)]
+        blobs at arena index i) instead of the per-entry arenas through the join's pairs.  When the
+        per-entry arenas hold the updated entries' blobs only, back to back in key (= update) order
+        (the synthetic C3 layers), the update-order arenas are the same bytes with one offset per
+        update and only those offsets are uploaded; otherwise the updates' blobs are gathered on the
+        host into new arenas.  ``upd`` = the join's update list [m, 2] (the same every step)."""
         m = int(upd.shape[0])
-        oo = np.empty(m + 1, np.uint64)
-        no = np.empty(m + 1, np.uint64)
-        oo[:m], no[:m] = oo_h, no_h
-        oo[m] = self.OB_off_host[int(upd[-1, 0]) + 1] if m else 0
-        no[m] = self.NB_off_host[int(upd[-1, 1]) + 1] if m else 0
-        # the arenas must be contiguous in update order (each update's blob right after the last)
-        ob_len = self.OB_off_host[np.asarray(upd[:, 0], np.int64) + 1] - oo_h
-        nb_len = self.NB_off_host[np.asarray(upd[:, 1], np.int64) + 1] - no_h
-        if not (np.array_equal(oo[1:], oo[:-1] + np.append(ob_len, 0)[:m]) and
-                np.array_equal(no[1:], no[:-1] + np.append(nb_len, 0)[:m])):
-            raise ValueError("the per-entry arenas are not contiguous in update order")
-        self.u_off = (DevBuf.from_numpy(self.eng, oo), DevBuf.from_numpy(self.eng, no))
-        self._ob_u, self._nb_u = ob.kd_blobs(), nb.kd_blobs()
-        self._ob_u.n, self._nb_u.n = m, m
-        self._ob_u.off, self._nb_u.off = self.u_off[0].ptr, self.u_off[1].ptr
+        self._u_arenas = []
+        blobs = []
+        for side, off_h, dev in ((0, self.OB_off_host, self.OB), (1, self.NB_off_host, self.NB)):
+            idx = np.asarray(upd[:, side], np.int64)
+            start = off_h[idx]
+            lens = off_h[idx + 1] - start
+            off = np.zeros(m + 1, np.uint64)
+            np.cumsum(lens, out=off[1:])
+            if m == 0 or np.array_equal(start, start[0] + off[:-1]):  # contiguous: same bytes, new offsets
+                u = DevBuf.from_numpy(self.eng, off + (np.uint64(start[0]) if m else np.uint64(0)))
+                self._u_arenas.append(u)
+                b = dev.kd_blobs()
+                b.n, b.off = m, u.ptr
+            else:  # gather the updates' blobs into an update-order arena
+                data = (self.OB_data_host, self.NB_data_host)[side]
+                pos = np.repeat(start.astype(np.int64) - off[:-1].astype(np.int64), lens.astype(np.int64)) + \
+                    np.arange(int(off[-1]), dtype=np.int64)
+                arena = DevBlobs(self.eng, np.ascontiguousarray(data[pos]), off)
+                self._u_arenas.append(arena)
+                b = arena.kd_blobs()
+            blobs.append(b)
+        self._ob_u, self._nb_u = blobs
 
     def reserve_gather(self, max_deltas_per_rank):
         """size the gathered-record buffer for at most this many deltas on any rank"""

@@ -86,8 +86,22 @@ class ObjectDB:
         self._h = None
         self._lock = threading.RLock()
         self._sig = None
+        self._opts = {}
         self.n_opens = 0
         self.reopen()
+
+    def set_option(self, name, value):
+        """an option of the object store (kd_odb_set_option: ``zlib`` 1 inflates with zlib even when
+        libdeflate is present); kept across reopens"""
+        with self._lock:
+            N.check(self.L.kd_odb_set_option(self._h, name.encode(), int(value)), "kd_odb_set_option")
+            self._opts[name] = int(value)
+
+    def get_option(self, name):
+        with self._lock:
+            v = ctypes.c_int64()
+            N.check(self.L.kd_odb_get_option(self._h, name.encode(), ctypes.byref(v)), "kd_odb_get_option")
+            return int(v.value)
 
     def _alternate_dirs(self):
         """objects directories named by objects/info/alternates (recursively, as git follows them)"""
@@ -133,6 +147,8 @@ class ObjectDB:
             self._h = h
             self._sig = sig
             self.n_opens += 1
+            for name, value in self._opts.items():
+                N.check(self.L.kd_odb_set_option(h, name.encode(), value), "kd_odb_set_option")
 
     def refresh(self):
         """reopen if packs or alternates changed since the last open; True when it reopened"""

@@ -334,6 +334,33 @@ def test_gpu_device_pipeline_vs_oracle(engine, n, layer, ordered, walk):
         check_pk_order(pipe, L.base.key, L.target.key, delta, upd)
 
 
+@pytest.mark.parametrize("n,layer", [(1000, "points"), (300_000, "points"), (2_000_000, "polygons"),
+                                     (2_000_000, "polygons_same"), (100_000_000, "polygons")])
+def test_gpu_device_pipeline_update_arenas(engine, n, layer):
+    """the pipeline bench.py times by default: the field diff from update-order arenas (the drop-in's
+    form, no pairs) after the join — the polygon layers' blobs already lie in update order (only
+    per-update offsets are uploaded), the points layer's are gathered"""
+    from kart_amd import synth
+    from kart_amd.device import DiffPipeline
+    from kart_amd.schema import FieldMaps
+
+    L = (synth.points_layer(n, seed=13) if layer == "points" else
+         synth.polygons_layer(n, seed=14, same_len=0.6 if layer == "polygons_same" else 0.0))
+    maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    pipe = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps)
+    pipe.step()
+    engine.sync()
+    _, _, upd, _, _ = pipe.results()
+    pipe.use_update_arenas(upd)
+    for _ in range(2):
+        pipe.step()
+    engine.sync()
+    counts, delta, upd2, masks, status = pipe.results()
+    assert np.array_equal(upd2, upd)
+    om, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
+    assert np.array_equal(masks, om) and np.array_equal(status, ost)
+
+
 def check_pk_order(pipe, kA, kB, delta, upd):
     """kd_delta_pk_order's outputs: the pks of the delta (and update) records ascending, and the
     record index of each — a stable argsort of the records' pks (DeltaDiff.sorted_items order)"""

@@ -180,6 +180,16 @@ def test_deep_delta_chains_and_batch_reads(tmp_path):
     out = subprocess.run([sys.executable, "-c", prog], env=dict(os.environ, KD_ODB_ZLIB="1"), capture_output=True,
                          check=True, text=True).stdout.split()
     assert out == [hashlib.sha256(data.tobytes() + off.tobytes()).hexdigest(), "0"]
+    # the same switch as an option of the open store (kd_odb_set_option), kept across a reopen
+    assert db.get_option("zlib") == 0
+    db.set_option("zlib", 1)
+    db.reopen()
+    assert db.get_option("zlib") == 1
+    d3, o3, s3 = db.read_batch(lv.oids)
+    assert not s3.any() and d3.tobytes() == data.tobytes() and np.array_equal(o3, off)
+    db.set_option("zlib", 0)
+    with pytest.raises(Exception):
+        db.set_option("no_such_option", 1)
 
 
 def test_loose_objects_missing_and_corrupt(tmp_path, repo):
