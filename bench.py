@@ -227,7 +227,7 @@ def timed(H, eng, step, steps):
     return H.max(time.perf_counter() - t0)
 
 
-PROFILE_ROUNDS = ("r05", "r04")  # committed profiles, newest first
+PROFILE_ROUNDS = ("r06", "r05", "r04")  # committed profiles, newest first
 
 
 def rocprof_stats_path(workload):
@@ -835,14 +835,15 @@ def run_c5(args, H):
             gather = {"what": "k_gh_gather: the deltas' 48-B heads copied into delta order (one per present side)",
                       "avg_launch_ms": round(gms, 5), "algorithmic_bytes_per_launch": galg,
                       "frac": round(galg / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    else:
-        # per k_gf_match launch: the delta pairs (8 B); per present side its offsets (16 B) and the
-        # blob head up to the end of the GPKG envelope (<= 96 B); codes + index envelope written
-        head = 0
-        for col, off in ((delta[:, 0], ob_off), (delta[:, 1], nb_off)):
-            prs = col[col != 0xFFFFFFFF].astype(np.int64)
-            head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
-        alg = 8 * nd + head + nd * (2 + bits // 2 + 1)
+    # per k_gf_match launch (the arena path): the delta pairs (8 B); per present side its offsets (16 B)
+    # and the blob head up to the end of the GPKG envelope (<= 96 B); codes + index envelope written
+    head = 0
+    for col, off in ((delta[:, 0], ob_off), (delta[:, 1], nb_off)):
+        prs = col[col != 0xFFFFFFFF].astype(np.int64)
+        head += int(np.minimum(off[prs + 1] - off[prs], 96).sum()) + 16 * prs.size
+    alg_arena = 8 * nd + head + nd * (2 + bits // 2 + 1)
+    if not heads:
+        alg = alg_arena
     roof = roofline(kern, kname, alg, args.traffic_json, n, "c5" if heads and H.world == 1 else None)
     arena_path = None
     if heads and not args.no_arena_timing:  # the same step through kd_geom_filter (blob arenas, msgpack walk)
@@ -855,9 +856,25 @@ def run_c5(args, H):
         el_a = timed(H, eng, pa.step, args.steps)
         eng.prof_enable(False)
         ka = kernel_times(eng, ("k_gf_match",))
+        eng.prof_reset()
+        eng.prof_select(None)
+        eng.prof_enable(True)
+        for _ in range(3):
+            pa.step()
+        eng.sync()
+        eng.prof_enable(False)
+        pa_parts = kernel_times(eng, ("k_partition2", "k_join2", "k_gscan2", "k_place2", "k_gf_match", "k_gf_scan",
+                                      "k_gf_place"))
+        # the arena path's own roofline: k_gf_match's algorithmic bytes over its HIP-event time, and the
+        # measured HBM bytes of its rocprofv3 PMC passes (profiles/<round>/traffic_c5arena.json)
+        ta = args.traffic_json.replace("traffic_c5.json", "traffic_c5arena.json") if args.traffic_json else ""
         arena_path = {"value": round(total_pairs * args.steps / el_a / 1e6, 2),
                       "ms_per_step": round(el_a / args.steps * 1e3, 4),
-                      "kernels_avg_ms": {k: round(v[1], 5) for k, v in ka.items()}}
+                      "kernels_avg_ms": {k: round(v[1], 5) for k, v in ka.items()},
+                      "step_kernels_avg_ms": {k: round(v[1], 5) for k, v in pa_parts.items()},
+                      "largest_step_kernel": max(pa_parts, key=lambda k: pa_parts[k][1]) if pa_parts else None,
+                      "roofline": roofline(ka, "k_gf_match", alg_arena, ta if os.path.exists(ta) else "", n,
+                                           "c5" if H.world == 1 else None)}
         del pa
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
@@ -887,12 +904,17 @@ def run_c5(args, H):
         "kernels_avg_ms": {k: round(v[1], 5) for k, v in kern.items()},
         "step_kernels_avg_ms": {k: round(v[1], 5) for k, v in parts.items()},
         "roofline": roof, "cpu_baseline": cpu, "heads_gather": gather,
+        "largest_step_kernel": max(parts, key=lambda k: parts[k][1]) if parts else None,
     }
     if heads:
         blobs = int(np.count_nonzero(np.diff(L.base_blobs[1])) + np.count_nonzero(np.diff(L.target_blobs[1])))
         out["host"] = {"geom_heads_s": round(pipe.heads_s, 4), "blobs": blobs,
                        "geom_heads_M_blobs_per_s": round(blobs / pipe.heads_s / 1e6, 2),
                        "delta_heads_s": round(pipe.delta_heads_s, 4) if pipe.delta_heads_s is not None else None,
+                       # one diff's device step plus its host layout of the heads in delta order (the
+                       # headline's step excludes that layout: ADVICE r5)
+                       "step_plus_delta_heads_ms": (round(elapsed / args.steps * 1e3 + pipe.delta_heads_s * 1e3, 2)
+                                                    if pipe.delta_heads_s is not None else None),
                        "note": "kd_geom_heads: the blob reader's host pass (msgpack walk of every materialised blob, "
                                f"{host_cores()} threads) that leaves 48 B per blob for the GPU; delta_heads_s: those "
                                "heads laid out in delta order (the reader reads the deltas' blobs after "

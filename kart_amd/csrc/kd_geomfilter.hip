@@ -216,8 +216,11 @@ __device__ __forceinline__ int geom_code(const GfArgs& a, GHit& h, u8 hflags) {
 // decode side s's blob `bi` for one lane
 // (o, len): the blob's arena offset and length, loaded by the caller for both sides up front (the
 // second side's offset loads are not serialised behind the first side's decode)
+// LDSW: the blob's first 112 bytes come from its LDS image (k_gf_match's staged heads: 7 chunks
+// from the blob's 16-B-aligned start at LDS byte address img) instead of 7 global loads
+template <bool LDSW>
 __device__ __forceinline__ void decode_side(const GfArgs& a, int s, u32 bi, u64 o, u64 len, u64 arena_end,
-                                            const u32* s_leg, const i16* s_gidx, GHit& h) {
+                                            const u32* s_leg, const i16* s_gidx, GHit& h, u32 img = 0) {
     typedef const __attribute__((address_space(1))) u32x4* gx4;
     h.r = -1;
     h.pc = -1;
@@ -233,10 +236,17 @@ __device__ __forceinline__ void decode_side(const GfArgs& a, int s, u32 bi, u64 
     const u64 a0 = (u64)b, a4 = a0 & ~(u64)3;
     if (len >= 52 && a4 + 112 <= arena_end) {
         u32 w[28];
-        sfor<0, 7>([&](auto k) {
-            const u32x4 v = *(gx4)(a4 + 16 * k);
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-        });
+        if (LDSW) {  // words from a4 in the image (from a16 = a4 & ~15; the words past its 112 bytes
+                     // are not among the bytes the fast path uses: those end at blob byte 95)
+            typedef const __attribute__((address_space(3))) u32* l32;
+            const u32 q = img + (u32)(a4 & 15);
+            sfor<0, 28>([&](auto k) { w[k] = *(l32)(size_t)(q + 4 * k); });
+        } else {
+            sfor<0, 7>([&](auto k) {
+                const u32x4 v = *(gx4)(a4 + 16 * k);
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            });
+        }
         const u32 sh = (u32)(a0 - a4);
         u32 rr[27];
         sfor<0, 27>([&](auto j) { rr[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh); });
@@ -310,7 +320,19 @@ __device__ __forceinline__ void decode_side(const GfArgs& a, int s, u32 bi, u64 
     h.code = geom_code(a, h, hflags);
 }
 
+// STAGE: each round's blob heads are staged in LDS by LDS-DMA, one side at a time — chunk c of a
+// wave's instruction k goes to owner lane c / 7, head chunk c % 7 — so a wave-instruction reads the
+// heads of ~9 blobs, 7 consecutive chunks each, instead of one 16-B piece of 64 different blobs
+// (per-lane scattered loads run at about half the request rate, scripts/probe/scatter_probe.hip)
+#ifndef KD_GF_STAGE
+#define KD_GF_STAGE 1
+#endif
+constexpr int GF_HCH = 7;  // head chunks per blob (112 B from the 16-B-aligned start: blob bytes >= 97)
+template <bool STAGE>
 __global__ __launch_bounds__(GF_NT) void k_gf_match(GfArgs a) {
+    typedef __attribute__((address_space(3))) void* lvp;
+    typedef const __attribute__((address_space(1))) void* gvp;
+    __shared__ u32x4 s_img[STAGE ? GF_NT * GF_HCH : 1];
     __shared__ u32 s_leg[2][GF_MAXLEG * 10];
     __shared__ i16 s_gidx[2][GF_MAXLEG];
     __shared__ u8 s_enc[GF_NT * 16];
@@ -340,15 +362,59 @@ __global__ __launch_bounds__(GF_NT) void k_gf_match(GfArgs a) {
         u8 ok = 0;
         if (a.enc)
             for (int k = 0; k < nb; k++) s_enc[tid * nb + k] = 0;
-        if (d < n) {
+        if (STAGE) {
+            // both sides' heads through LDS, one side at a time (block-uniform: every lane stages
+            // and waits, valid delta or not)
+            u32 po = KD_NONE, pn = KD_NONE;
+            u64 oo = 0, oe = 0, no = 0, ne = 0;
+            if (d < n) {
+                po = a.pairs[2 * d];
+                pn = a.pairs[2 * d + 1];
+                if ((u64)po < a.nblob[0]) { oo = a.off[0][po]; oe = a.off[0][po + 1]; }
+                if ((u64)pn < a.nblob[1]) { no = a.off[1][pn]; ne = a.off[1][pn + 1]; }
+            }
+            const int lane = tid & 63, wv = tid >> 6;
+            const u32 wimg = (u32)(size_t)(const __attribute__((address_space(3))) u32x4*)s_img + 16u * (u32)(wv * 64 * GF_HCH);
+            int code[2];
+            GHit h;
+#pragma unroll
+            for (int sd = 0; sd < 2; sd++) {
+                const u32 bi = sd ? pn : po;
+                const u64 o = sd ? no : oo, len = sd ? ne - no : oe - oo, aend = sd ? end1 : end0;
+                const u64 a0 = (u64)a.data[sd] + o, a16 = a0 & ~(u64)15;
+                // chunks of this lane's head that lie below the arena's end (a present, long-enough blob)
+                const bool stage = d < n && bi != KD_NONE && (u64)bi < a.nblob[sd] && len >= 52;
+                const u32 nch = stage ? (u32)min<u64>((aend - a16 + 15) >> 4, (u64)GF_HCH) : 0u;
+#pragma unroll
+                for (int k = 0; k < GF_HCH; k++) {
+                    const int c = 64 * k + lane, ow = c / GF_HCH, ci = c - ow * GF_HCH;
+                    const u64 src = __shfl(a16, ow);
+                    const u32 cn = __shfl(nch, ow);
+                    if ((u32)ci < cn)
+                        __builtin_amdgcn_global_load_lds((gvp)(src + 16ull * ci), (lvp)(s_img + wv * 64 * GF_HCH + 64 * k), 16, 0, 0);
+                }
+                __syncthreads();  // vmcnt(0) + barrier: the heads have landed
+                if (d < n)
+                    decode_side<true>(a, sd, bi, o, len, aend, s_leg[sd], s_gidx[sd], h, wimg + 16u * (u32)(GF_HCH * lane));
+                code[sd] = h.code;
+                __syncthreads();  // the image is free for the other side
+            }
+            if (d < n) {
+                const int co = code[0], cn = code[1];
+                keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
+                *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
+                if (a.enc && cn != GF_NONE && cn != GF_FALLBACK && h.r >= 0)
+                    ok = index_env(h.r, h.pc, h.e, h.e, h.empty, a.bits, vmax, [&](int k, u8 v) { s_enc[tid * nb + k] = v; });
+            }
+        } else if (d < n) {
             const u32 po = a.pairs[2 * d], pn = a.pairs[2 * d + 1];
             const bool vo = (u64)po < a.nblob[0], vn = (u64)pn < a.nblob[1];
             const u64 oo = vo ? a.off[0][po] : 0, oe = vo ? a.off[0][po + 1] : 0;
             const u64 no = vn ? a.off[1][pn] : 0, ne = vn ? a.off[1][pn + 1] : 0;
             GHit h;
-            decode_side(a, 0, po, oo, oe - oo, end0, s_leg[0], s_gidx[0], h);
+            decode_side<false>(a, 0, po, oo, oe - oo, end0, s_leg[0], s_gidx[0], h);
             const int co = h.code;
-            decode_side(a, 1, pn, no, ne - no, end1, s_leg[1], s_gidx[1], h);
+            decode_side<false>(a, 1, pn, no, ne - no, end1, s_leg[1], s_gidx[1], h);
             const int cn = h.code;
             keep = (co >= 1 && co <= 3) || (cn >= 1 && cn <= 3);
             *(u16*)(a.match + 2 * d) = (u16)(co | cn << 8);
@@ -946,7 +1012,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
                                })))
                 return rc;
         } else if ((rc = launch(ctx, "k_gf_match", [&] {
-                        hipLaunchKernelGGL(k_gf_match, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a);
+                        hipLaunchKernelGGL(k_gf_match<KD_GF_STAGE != 0>, dim3((unsigned)tiles), dim3(GF_NT), 0, ctx->stream, a);
                     })))
             return rc;
         if ((rc = launch(ctx, "k_gf_scan", [&] {

@@ -231,3 +231,57 @@ def test_gpu_diff2_ex_delta_keys_only(engine, flags):
                     L.target.key[np.minimum(r[:, 1], L.target.n - 1)])
     assert np.array_equal(k, want)
     assert set(map(tuple, ru.tolist())) <= set(map(tuple, r.tolist()))
+
+
+# the A/B switches of kartdiff.h's option table that change which join kernel runs:
+# every one bit-exact with the oracle on the C4 layer (sorted and walk-order forms) and, for the
+# two-way join's OID staging, on the C3 polygon layer
+OPTION_SETS = {
+    "split": {"merge3_split": 1, "j3_v": 1},   # k_join3b<SPLIT=true> stages candidates, k_resolve3 applies the rule
+    "join3_v0": {"j3_v": 0},                    # round 4's k_join3
+    "join3_v0_ol": {"j3_v": 0, "j3_ol": 1},     # k_join3 with ours'/theirs' OIDs in LDS
+    "two_step": {"merge3_join": 0},             # classify2 + k_resolve3
+    "oidlds": {"j2_oidlds_min": 0},             # k_join2 stages OIDs in LDS at every size
+}
+OPTION_DEFAULTS = {"merge3_split": 0, "j3_v": 1, "j3_ol": 0, "merge3_join": 1, "j2_oidlds_min": 1 << 26}
+
+
+@pytest.mark.parametrize("opts", sorted(OPTION_SETS))
+def test_gpu_option_paths_vs_oracle(engine, request, opts):
+    from kart_amd import synth
+    from kart_amd.device import DiffPipeline, MergePipeline
+    from kart_amd.schema import FieldMaps
+
+    for k, v in OPTION_SETS[opts].items():
+        engine.set_option(k, v)
+    request.addfinalizer(lambda: [engine.set_option(k, OPTION_DEFAULTS[k]) for k in OPTION_SETS[opts]])
+    key = lambda rows: sorted(map(tuple, np.asarray(rows).tolist()))
+    # three-way: the sorted form, then the walk-order form (per-bucket sorts, OIDs / names through the orders)
+    M = synth.table3_layers(300_000, seed=31)
+    oc, om, ocl = O.classify3(M.ancestor.key, M.ancestor.oid, M.ours.key, M.ours.oid, M.theirs.key, M.theirs.oid)
+    pipe = MergePipeline(engine, M.ancestor, M.ours, M.theirs)
+    pipe.step()
+    engine.sync()
+    n_clean, conf, md = pipe.results()
+    assert key(conf) == key(oc) and key(md) == key(om) and n_clean == ocl
+    W = synth.table3_layers(300_000, seed=32, walk=True)
+    wp = MergePipeline(engine, W.ancestor, W.ours, W.theirs, segmented=True)
+    wp.step()
+    engine.sync()
+    n_clean, conf, md = wp.results()
+    srt = []
+    for S, order in zip((W.ancestor, W.ours, W.theirs), wp.orders()):
+        srt.append((S.key[order], S.oid[order]))
+    oc, om, ocl = O.classify3(*srt[0], *srt[1], *srt[2])
+    assert key(conf) == key(oc) and key(md) == key(om) and n_clean == ocl
+    # two-way on the polygon layer
+    L = synth.polygons_layer(1_000_000, seed=33)
+    maps = FieldMaps(L.schema, L.legends, L.schema, L.legends)
+    dp = DiffPipeline(engine, L.base, L.target, L.base_blobs, L.target_blobs, maps)
+    dp.step()
+    engine.sync()
+    counts, delta, upd, masks, status = dp.results()
+    od, _ = O.classify2(L.base.key, L.base.oid, L.target.key, L.target.oid)
+    assert np.array_equal(delta, od)
+    om2, ost = O.fielddiff(*L.base_blobs, *L.target_blobs, upd, maps)
+    assert np.array_equal(masks, om2) and np.array_equal(status, ost)
