@@ -290,14 +290,30 @@ def _pks(version, sorted_idx):
 class UpdateBatch:
     """The update deltas one diff_feature run yielded, with both sides' leaf indices (original
     order): what field_diff needs to read the blobs straight into one arena per side, without
-    walking the DeltaDiff or touching a blob object"""
+    walking the DeltaDiff or touching a blob object.  ``prefetch``: a future of those two arenas,
+    read while the deltas were being built (or None)"""
 
-    __slots__ = ("old_v", "new_v", "old_leaf", "new_leaf", "deltas", "keys", "n_total")
+    __slots__ = ("old_v", "new_v", "old_leaf", "new_leaf", "deltas", "keys", "n_total", "prefetch")
 
     def __init__(self):
         self.old_v = self.new_v = None
         self.old_leaf = self.new_leaf = None
         self.deltas, self.keys, self.n_total = [], [], -1
+        self.prefetch = None
+
+
+# diffs with at least this many updates read the updates' blobs while their deltas are built
+PREFETCH_MIN_UPDATES = 10_000
+_PREFETCH_POOL = None
+
+
+def _prefetch_pool():
+    global _PREFETCH_POOL
+    if _PREFETCH_POOL is None:
+        import concurrent.futures
+
+        _PREFETCH_POOL = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="kd-prefetch")
+    return _PREFETCH_POOL
 
 
 def diff_feature(engine, base, target, feature_filter=None, reverse=False, updates=None, _collect=None):
@@ -331,9 +347,15 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
     new_leaf = np.full(n, -1, np.int64)
     old_leaf[ia] = A.order[a_idx[ia]]
     new_leaf[ib] = B.order[b_idx[ib]]
+    match_all = feature_filter is None or getattr(feature_filter, "match_all", False)
+    if updates is not None and match_all and old_v is not None and new_v is not None:
+        # the updates' blobs are read on a worker thread (native, GIL released) while the deltas
+        # are built here: field_diff then takes the arenas from updates.prefetch
+        both = np.nonzero(has_a & has_b)[0]
+        if both.size >= PREFETCH_MIN_UPDATES:
+            updates.prefetch = _prefetch_pool().submit(_arena_pair, old_v, new_v, old_leaf[both], new_leaf[both])
     old_pks, new_pks = _pk_column(old_v, a_idx, ia, n), _pk_column(new_v, b_idx, ib, n)
     t = _lap("pks", t)
-    match_all = feature_filter is None or getattr(feature_filter, "match_all", False)
     # this module's own Delta / KeyValue: built field by field (the constructor's argument
     # normalisation is most of a delta's host cost); Kart's classes through their constructor
     own = S.Delta is _deltas.Delta
@@ -534,7 +556,11 @@ def field_diff(engine, feature_diff, old_version, new_version, stats=None):
             ups = batch.deltas
             if not ups:
                 return 0
-            (od, oo), (nd, no) = _arena_pair(old_version, new_version, batch.old_leaf, batch.new_leaf)
+            if batch.prefetch is not None:  # read while the deltas were built (diff_feature)
+                fut, batch.prefetch = batch.prefetch, None
+                (od, oo), (nd, no) = fut.result()
+            else:
+                (od, oo), (nd, no) = _arena_pair(old_version, new_version, batch.old_leaf, batch.new_leaf)
         else:
             ups = [d for d in feature_diff.values() if d.type == "update"]
             if not ups:

@@ -280,6 +280,37 @@ def test_field_diff_batch_path(eng):
     assert {k: (d.old_value, d.new_value) for k, d in fd2.items()} == {k: v for k, v in vals.items() if k != gone}
 
 
+def test_field_diff_prefetched_arenas(eng, monkeypatch):
+    """diffs over PREFETCH_MIN_UPDATES updates read the updates' blobs on a worker thread while the
+    deltas are built: field_diff takes those arenas (no second read) and attaches the same fields"""
+    fx = load("repo_points")
+    want = D.dataset_diff(eng, version(fx, "head1"), version(fx, "head"))["feature"]
+    assert D.field_diff(eng, want, want._kd_updates.old_v, want._kd_updates.new_v) == 5
+    monkeypatch.setattr(D, "PREFETCH_MIN_UPDATES", 1)
+    old, new = version(fx, "head1"), version(fx, "head")
+    fd = D.dataset_diff(eng, old, new)["feature"]
+    assert fd._kd_updates.prefetch is not None
+    fd._kd_updates.prefetch.result()  # the read is done: field_diff must not read again
+    reads = {"n": 0}
+    for v in (old, new):
+        rb, rbs = v.read_blob, v._read_blobs
+
+        def counted(i, _rb=rb):
+            reads["n"] += 1
+            return _rb(i)
+
+        v.read_blob = counted
+        if rbs is not None:
+            def counted_batch(idx, _rbs=rbs):
+                reads["n"] += 1
+                return _rbs(idx)
+
+            v._read_blobs = counted_batch
+    assert D.field_diff(eng, fd, old, new) == 5
+    assert reads["n"] == 0 and fd._kd_updates.prefetch is None
+    assert {k: d.changed_fields for k, d in fd.items()} == {k: d.changed_fields for k, d in want.items()}
+
+
 def test_changed_names_rows_matches_per_row():
     """the batch decode (one np.unique over the rows' words) equals changed_names row by row, for
     one- and multi-word masks, with a fresh list per row"""
