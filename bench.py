@@ -874,7 +874,7 @@ def run_c5(args, H):
                       "step_kernels_avg_ms": {k: round(v[1], 5) for k, v in pa_parts.items()},
                       "largest_step_kernel": max(pa_parts, key=lambda k: pa_parts[k][1]) if pa_parts else None,
                       "roofline": roofline(ka, "k_gf_match", alg_arena, ta if os.path.exists(ta) else "", n,
-                                           "c5" if H.world == 1 else None)}
+                                           "c5arena" if H.world == 1 else None)}
         del pa
     cpu = None
     if H.rank == 0 and H.world == 1 and not args.no_cpu_baseline:
