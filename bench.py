@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--pair-arenas", action="store_true",
                     help="c2/c3: field-diff from the per-entry arenas through the join's update pairs instead of "
                          "update-order arenas (the drop-in's form: the blob reader writes update i's blobs at index i)")
-    ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (profiles/r04/traffic_<wl>.json, else profiles/traffic_<wl>.json)")
+    ap.add_argument("--traffic-json", default=None, help="measured HBM bytes per launch (the newest profiles/<round>/traffic_<wl>.json)")
     ap.add_argument("--no-heads-path", action="store_true", help="c5env: skip the indexer's heads-path timing")
     ap.add_argument("--no-check", action="store_true", help="profiling variants only: skip the correctness check")
     ap.add_argument("--no-events", action="store_true", help="no per-kernel HIP events in the timed region")
@@ -112,7 +112,7 @@ def parse():
         a.n = {"c2": 10_000_000, "c3": 100_000_000, "c3v": 100_000_000, "c4": 50_000_000, "c5": 100_000_000, "c5env": 20_000_000,
                "c6": 20_000_000}[a.workload]
     if a.traffic_json is None:
-        for d in ("r05", "r04", ""):  # the newest PMC passes of the workload
+        for d in PROFILE_ROUNDS + ("",):  # the newest PMC passes of the workload
             a.traffic_json = os.path.join(ROOT, "profiles", d, f"traffic_{a.workload}.json")
             if os.path.exists(a.traffic_json):
                 break

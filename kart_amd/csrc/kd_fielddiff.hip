@@ -717,6 +717,59 @@ __device__ __forceinline__ u32 range_eq(const BL& A, u32 pa, const BL& B, u32 pb
     return glb_bytes_eq(xa, xb, n) ? 0u : 1u;
 }
 
+#ifndef KD_FD_SPLIT
+// windowed kernel, 1: a long payload's window parts compared from LDS, only its middle queued (C3v
+// 1.49 -> 1.40 ms, but C3 1.30 -> 1.34: its attribute edits compare unchanged geometries either
+// way); 2: the prefix only; 0 (default): the whole payload queued
+#define KD_FD_SPLIT 0
+#endif
+// The windowed kernel's payload compare: the parts of the two ranges that lie in both blobs' head
+// windows (a prefix) and in both tail windows (a suffix) compare from LDS first — a difference there
+// settles the value without any HBM read (a moved vertex changes the GPKG envelope, in the head) —
+// and only the middle, which no window holds, is queued for the cooperative compare.  The window
+// lines are not fetched a second time after the L2 has turned over (round 5's 1.41x traffic).
+template <int NH, int NTL>
+__device__ __forceinline__ u32 range_eq(const WBlob<NH, NTL>& A, u32 pa, const WBlob<NH, NTL>& B, u32 pb, u32 n, int key,
+                                        const FdQueue& q) {
+    const u32 ya = pa + A.s0, yb = pb + B.s0;  // offsets from the head bases
+    {
+        const u32 oa = A.win(ya & ~3u, n + 8), ob = B.win(yb & ~3u, n + 8);
+        if (oa != ~0u && ob != ~0u) {
+            if (KD_FD_PROBE_NOLDSCMP) return 0u;
+            return lds_bytes_eq(A.img + oa + (ya & 3), B.img + ob + (yb & 3), n) ? 0u : 1u;
+        }
+    }
+    u32 pre = 0, suf = n;
+    if (KD_FD_SPLIT) {
+        // prefix: the aligned LDS compare of m bytes at y reads head bytes up to (y & ~3) + m + 8
+        const int hp = min(16 * NH - 8 - (int)ya, 16 * NH - 8 - (int)yb);
+        pre = hp > 0 ? min((u32)hp, n) : 0u;
+        // suffix: from the first offset whose aligned start lies in both tail windows (reads past a
+        // tail window's end are past its blob's last byte)
+        const int ts = max(A.t0 + 3 - (int)ya, B.t0 + 3 - (int)yb);
+        suf = KD_FD_SPLIT == 2 ? n : ts <= (int)pre ? pre : ts >= (int)n ? n : (u32)ts;  // 2: the prefix only
+        if (pre >= 16 || suf + 16 <= n) {
+            bool ne = false;
+            if (pre) ne = !lds_bytes_eq(A.img + (ya & ~3u) + (ya & 3), B.img + (yb & ~3u) + (yb & 3), pre);
+            if (!ne && suf < n) {
+                const u32 za = ya + suf, zb = yb + suf;
+                // (the whole suffix's extent: a head window holds it only if it ends inside)
+                const u32 oa = A.win(za & ~3u, n - suf + 8), ob = B.win(zb & ~3u, n - suf + 8);
+                ne = !lds_bytes_eq(A.img + oa + (za & 3), B.img + ob + (zb & 3), n - suf);
+            }
+            if (ne) return 1u;
+        } else {
+            pre = 0;  // too little in the windows to be worth it: the whole range below
+            suf = n;
+        }
+    }
+    const u32 m = suf - pre;
+    if (m == 0) return 0u;
+    const u64 xa = A.start + pa + pre, xb = B.start + pb + pre;
+    if (task_put(q, xa, xb, m, key)) return 3;
+    return glb_bytes_eq(xa, xb, m) ? 0u : 1u;
+}
+
 // bytes [p, p + 16) of a and b differ, counting only the first n (n >= 1)
 __device__ __forceinline__ bool chunk_ne(const u32x4& a, const u32x4& b, u32 n) {
     const u32 m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1;
