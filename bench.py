@@ -401,8 +401,9 @@ def run_diff(args, H, polygons):
     }
     dom = max((k for k in kern if k in alg), key=lambda k: kern[k][1]) if kern else None
     # (the committed traffic files are 1-GPU profiles of the whole layer: not a shard's bytes)
-    roof = roofline(kern, dom, alg.get(dom, 0), args.traffic_json, n if world == 1 else -1,
-                    args.workload if world == 1 else None) if dom else None
+    # (the committed traffic and rocprof files profile the default update-order arenas)
+    roof = roofline(kern, dom, alg.get(dom, 0), "" if args.pair_arenas else args.traffic_json, n if world == 1 else -1,
+                    args.workload if world == 1 and not args.pair_arenas else None) if dom else None
     cpu = host = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_diff(L, maps, args.cpu_seconds, "C3" if polygons else "C2")
