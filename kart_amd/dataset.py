@@ -316,6 +316,49 @@ def _prefetch_pool():
     return _PREFETCH_POOL
 
 
+class _Prefetch:
+    """the update blobs of both sides being read by one native batched read on a worker thread; the
+    caller does not return before the worker is inside that (GIL-free) call, so the delta
+    construction that follows — one long C call holding the GIL — cannot starve it"""
+
+    def __init__(self, old_v, new_v, oi, ni):
+        import threading
+
+        self.old_v, self.new_v, self.oi, self.ni = old_v, new_v, oi, ni
+        src = old_v._read_blobs.source
+        oids = np.concatenate([old_v.oids[oi], new_v.oids[ni]])
+        started = threading.Event()
+
+        def work():
+            started.set()  # the read below releases the GIL within microseconds
+            return src.read_blobs(oids)
+
+        self.fut = _prefetch_pool().submit(work)
+        started.wait()
+
+    def result(self):
+        """the two update-order arenas, as _arena_pair returns them"""
+        data, off, status = self.fut.result()
+        oi, ni = self.oi, self.ni
+        if status.any():  # the per-side reads raise the reference's KeyError for the first missing blob
+            return self.old_v.blob_arena_leaves(oi), self.new_v.blob_arena_leaves(ni)
+        k = oi.size
+        cut = int(off[k])
+        arenas = ((data[:cut], off[:k + 1]), (data[cut:], off[k:] - off[k]))
+        self.old_v._remember_arena(oi, *arenas[0])
+        self.new_v._remember_arena(ni, *arenas[1])
+        return arenas
+
+
+def _start_prefetch(old_v, new_v, old_leaf, new_leaf):
+    """a _Prefetch of the updates' blobs when both versions read from one repository (else None:
+    the per-side reads happen in field_diff)"""
+    src = getattr(old_v._read_blobs, "source", None)
+    if src is None or src is not getattr(new_v._read_blobs, "source", None):
+        return None
+    return _Prefetch(old_v, new_v, np.asarray(old_leaf, np.int64), np.asarray(new_leaf, np.int64))
+
+
 def diff_feature(engine, base, target, feature_filter=None, reverse=False, updates=None, _collect=None):
     """Generator of Delta with lazy values (RichBaseDataset.diff_feature semantics).
 
@@ -353,7 +396,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
         # are built here: field_diff then takes the arenas from updates.prefetch
         both = np.nonzero(has_a & has_b)[0]
         if both.size >= PREFETCH_MIN_UPDATES:
-            updates.prefetch = _prefetch_pool().submit(_arena_pair, old_v, new_v, old_leaf[both], new_leaf[both])
+            updates.prefetch = _start_prefetch(old_v, new_v, old_leaf[both], new_leaf[both])
     old_pks, new_pks = _pk_column(old_v, a_idx, ia, n), _pk_column(new_v, b_idx, ib, n)
     t = _lap("pks", t)
     # this module's own Delta / KeyValue: built field by field (the constructor's argument

@@ -281,33 +281,52 @@ def test_field_diff_batch_path(eng):
 
 
 def test_field_diff_prefetched_arenas(eng, monkeypatch):
-    """diffs over PREFETCH_MIN_UPDATES updates read the updates' blobs on a worker thread while the
-    deltas are built: field_diff takes those arenas (no second read) and attaches the same fields"""
+    """diffs over PREFETCH_MIN_UPDATES updates of two versions read from one repository start the
+    updates' batched blob read on a worker thread before the deltas are built: field_diff takes
+    those arenas (no second read) and attaches the same fields"""
+    from kart_amd import packing
+
     fx = load("repo_points")
     want = D.dataset_diff(eng, version(fx, "head1"), version(fx, "head"))["feature"]
     assert D.field_diff(eng, want, want._kd_updates.old_v, want._kd_updates.new_v) == 5
     monkeypatch.setattr(D, "PREFETCH_MIN_UPDATES", 1)
     old, new = version(fx, "head1"), version(fx, "head")
+    reads = {"batch": 0, "one": 0}
+
+    class Source:  # one repository's batched reader (what gitsource's read_blobs.source is)
+        def __init__(self, versions):
+            self.where = {}
+            for v in versions:
+                for i in range(v.n):
+                    self.where[v.oids[i].tobytes()] = (v, i)
+
+        def read_blobs(self, oids):
+            reads["batch"] += 1
+            bs = [bytes(v.read_blob(i)) for v, i in (self.where[o.tobytes()] for o in np.asarray(oids))]
+            data, off = packing._arena(bs)
+            return data, off, np.zeros(len(bs), np.uint8)
+
+    src = Source([old, new])
+    for v in (old, new):
+        def rbs(idx, _v=v):
+            return src.read_blobs(_v.oids[np.asarray(idx, np.int64)])
+
+        rbs.source = src
+        v._read_blobs = rbs
     fd = D.dataset_diff(eng, old, new)["feature"]
     assert fd._kd_updates.prefetch is not None
-    fd._kd_updates.prefetch.result()  # the read is done: field_diff must not read again
-    reads = {"n": 0}
+    fd._kd_updates.prefetch.fut.result()  # the read is done: field_diff must not read again
+    assert reads["batch"] == 1
     for v in (old, new):
-        rb, rbs = v.read_blob, v._read_blobs
+        rb = v.read_blob
 
         def counted(i, _rb=rb):
-            reads["n"] += 1
+            reads["one"] += 1
             return _rb(i)
 
         v.read_blob = counted
-        if rbs is not None:
-            def counted_batch(idx, _rbs=rbs):
-                reads["n"] += 1
-                return _rbs(idx)
-
-            v._read_blobs = counted_batch
     assert D.field_diff(eng, fd, old, new) == 5
-    assert reads["n"] == 0 and fd._kd_updates.prefetch is None
+    assert reads == {"batch": 1, "one": 0} and fd._kd_updates.prefetch is None
     assert {k: d.changed_fields for k, d in fd.items()} == {k: d.changed_fields for k, d in want.items()}
 
 
