@@ -387,7 +387,9 @@ struct Reader {
             rc = inflate_exact(pk.pack.p + data, pk.pack.n - data, out.data(), sz);
             if (rc) return rc;
             btype = t;
-            if (!chain.empty()) remember(&pk, cur, t, out);
+            // a chain's base, and every whole tree: a compare walk reads the old side's tree just
+            // before the new side's, which git stores as a delta against it
+            if (!chain.empty() || t == OBJ_TREE) remember(&pk, cur, t, out);
             break;
         }
         for (size_t j = chain.size(); j-- > 0;) {
@@ -481,17 +483,30 @@ struct Reader {
         return result;
     }
 
-    // the pack holding oid (the one that held the previous object first: a batch's objects tend
-    // to share packs, and every miss is a binary search of another index), or -1
-    size_t last_pack = 0;
+    // the pack holding oid, or -1.  The packs that held the last few objects are searched first,
+    // most recent first: a batch's objects tend to share packs, a compare walk alternates between
+    // its roots' packs (one per side and subtree in a repository written by parallel imports), and
+    // every miss is a binary search of another index
+    static constexpr int MRU = 4;
+    size_t mru[MRU] = {~size_t(0), ~size_t(0), ~size_t(0), ~size_t(0)};
     long locate(const u8* oid, u64* off) {
         const size_t np = db->packs.size();
-        for (size_t k = 0; k < np; k++) {
-            const size_t p = k == 0 ? (last_pack < np ? last_pack : 0) : (k <= last_pack ? k - 1 : k);
+        for (int j = 0; j < MRU; j++) {
+            const size_t p = mru[j];
+            if (p >= np) break;
             if (db->packs[p]->find(oid, off)) {
-                last_pack = p;
+                for (int q = j; q > 0; q--) mru[q] = mru[q - 1];
+                mru[0] = p;
                 return (long)p;
             }
+        }
+        for (size_t p = 0; p < np; p++) {
+            bool tried = false;
+            for (int j = 0; j < MRU; j++) tried |= mru[j] == p;
+            if (tried || !db->packs[p]->find(oid, off)) continue;
+            for (int q = MRU - 1; q > 0; q--) mru[q] = mru[q - 1];
+            mru[0] = p;
+            return (long)p;
         }
         return -1;
     }

@@ -9,7 +9,10 @@
  *   240-300) for a whole delta list at once: per delta the lazy blob of each present side, the
  *   promise partial(get_feature_from_blob, blob) (kart/base_dataset.py:506-507: no blob is read and
  *   get_feature is not called here), the two KeyValue halves and the Delta
- *   (kart/diff_structs.py:12-40,47-80), built in C with the slots filled directly. */
+ *   (kart/diff_structs.py:12-40,47-80), built in C with the slots filled directly.
+ *
+ * attach_fields(...) — the changed_fields of a field diff's updates from kd_fielddiff's mask rows:
+ *   one decode per distinct mask, a fresh list per update. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <structmember.h>
@@ -417,9 +420,124 @@ fail:
     return ret;
 }
 
+/* attach_fields(deltas, masks, status, words, names_of, delta_type) — the changed_fields of every
+ * update of a field diff (kart_amd/dataset.py field_diff): delta i gets a fresh list of the names
+ * mask row i (words uint64 per row) stands for, or None where status[i] (uint8) is not 0.  The rows'
+ * distinct masks (a layer's updates share a handful) are found with an open-addressing table over
+ * the mask words and decoded once each by names_of(i) -> list (i: the first row holding that mask).
+ * Deltas of exactly delta_type get the changed_fields slot written directly; any other object goes
+ * through setattr.  Returns the number of distinct masks. */
+typedef struct {
+    Py_ssize_t row;  /* first row of this mask; -1: empty */
+    PyObject* names;
+} MaskEntry;
+
+static unsigned long long mask_hash(const unsigned long long* w, Py_ssize_t words) {
+    unsigned long long h = 0x9E3779B97F4A7C15ull;
+    for (Py_ssize_t k = 0; k < words; k++) {
+        h ^= w[k];
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    return h;
+}
+
+static PyObject* attach_fields(PyObject* self, PyObject* args) {
+    PyObject *dl, *om, *os_, *names_of, *dt;
+    Py_ssize_t words;
+    if (!PyArg_ParseTuple(args, "OOOnOO", &dl, &om, &os_, &words, &names_of, &dt)) return NULL;
+    if (!PyList_Check(dl) || words < 1) {
+        PyErr_SetString(PyExc_TypeError, "attach_fields: deltas must be a list and words >= 1");
+        return NULL;
+    }
+    Py_buffer mb = {0}, sb = {0};
+    MaskEntry* tab = NULL;
+    size_t cap = 0, used = 0;
+    PyObject *attr = NULL, *ret = NULL;
+    if (PyObject_GetBuffer(om, &mb, PyBUF_C_CONTIGUOUS) < 0) return NULL;
+    if (PyObject_GetBuffer(os_, &sb, PyBUF_C_CONTIGUOUS) < 0) goto done;
+    const Py_ssize_t n = PyList_GET_SIZE(dl);
+    if (mb.itemsize != 8 || sb.itemsize != 1 || mb.len < (Py_ssize_t)(8 * words) * n || sb.len < n) {
+        PyErr_SetString(PyExc_ValueError, "attach_fields: masks must be uint64 and status uint8, one row per delta");
+        goto done;
+    }
+    const unsigned long long* m = (const unsigned long long*)mb.buf;
+    const unsigned char* st = (const unsigned char*)sb.buf;
+    Py_ssize_t d_cf = -1;
+    if (PyType_Check(dt)) {
+        d_cf = slot_offset(dt, "changed_fields");
+        if (d_cf < 0) PyErr_Clear();  /* no such slot: setattr for every delta */
+    }
+    attr = PyUnicode_InternFromString("changed_fields");
+    cap = 64;
+    tab = (MaskEntry*)PyMem_Malloc(cap * sizeof(MaskEntry));
+    if (!attr || !tab) { if (!PyErr_Occurred()) PyErr_NoMemory(); goto done; }
+    for (size_t k = 0; k < cap; k++) tab[k].row = -1, tab[k].names = NULL;
+    for (Py_ssize_t i = 0; i < n; i++) {
+        PyObject* v;
+        if (st[i]) {
+            v = Py_None;
+            Py_INCREF(v);
+        } else {
+            const unsigned long long* w = m + i * words;
+            size_t h = (size_t)mask_hash(w, words) & (cap - 1);
+            while (tab[h].row >= 0 && memcmp(m + tab[h].row * words, w, 8 * (size_t)words)) h = (h + 1) & (cap - 1);
+            if (tab[h].row < 0) {
+                PyObject* nm = PyObject_CallFunction(names_of, "n", i);
+                if (!nm) goto done;
+                if (!PyList_Check(nm)) {
+                    Py_DECREF(nm);
+                    PyErr_SetString(PyExc_TypeError, "attach_fields: names_of must return a list");
+                    goto done;
+                }
+                tab[h].row = i;
+                tab[h].names = nm;
+                if (2 * ++used > cap) {  /* grow: rehash every entry into twice the table */
+                    const size_t nc = 2 * cap;
+                    MaskEntry* nt = (MaskEntry*)PyMem_Malloc(nc * sizeof(MaskEntry));
+                    if (!nt) { PyErr_NoMemory(); goto done; }
+                    for (size_t k = 0; k < nc; k++) nt[k].row = -1, nt[k].names = NULL;
+                    for (size_t k = 0; k < cap; k++) {
+                        if (tab[k].row < 0) continue;
+                        size_t g = (size_t)mask_hash(m + tab[k].row * words, words) & (nc - 1);
+                        while (nt[g].row >= 0) g = (g + 1) & (nc - 1);
+                        nt[g] = tab[k];
+                    }
+                    PyMem_Free(tab);
+                    tab = nt;
+                    cap = nc;
+                    h = (size_t)mask_hash(w, words) & (cap - 1);
+                    while (tab[h].row != i) h = (h + 1) & (cap - 1);
+                }
+            }
+            PyObject* src = tab[h].names;
+            v = PyList_GetSlice(src, 0, PyList_GET_SIZE(src));
+            if (!v) goto done;
+        }
+        PyObject* d = PyList_GET_ITEM(dl, i);
+        if (d_cf >= 0 && Py_TYPE(d) == (PyTypeObject*)dt) {
+            set_slot(d, d_cf, v);
+        } else {
+            const int e = PyObject_SetAttr(d, attr, v);
+            Py_DECREF(v);
+            if (e < 0) goto done;
+        }
+    }
+    ret = PyLong_FromSize_t(used);
+done:
+    if (tab)
+        for (size_t k = 0; k < cap; k++) Py_XDECREF(tab[k].names);
+    PyMem_Free(tab);
+    Py_XDECREF(attr);
+    if (mb.obj) PyBuffer_Release(&mb);
+    if (sb.obj) PyBuffer_Release(&sb);
+    return ret;
+}
+
 static PyMethodDef methods[] = {
     {"ascii_slices", ascii_slices, METH_VARARGS, "str per [lo, hi) range of an ASCII buffer"},
     {"build_deltas", build_deltas, METH_VARARGS, "Delta objects with lazy promises for a whole delta list"},
+    {"attach_fields", attach_fields, METH_VARARGS, "changed_fields of every update from its mask row"},
     {NULL, NULL, 0, NULL},
 };
 

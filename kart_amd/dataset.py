@@ -614,9 +614,16 @@ def field_diff(engine, feature_diff, old_version, new_version, stats=None):
         maps = FieldMaps(old_version.schema, old_version.legends, new_version.schema, new_version.legends)
         masks, status = engine.fielddiff(od, oo, nd, no, None, maps)
         t2 = time.perf_counter()
-        names = maps.changed_names_rows(masks[:len(ups)])
-        for d, nm, s in zip(ups, names, status.tolist()):
-            d.changed_fields = nm if s == 0 else None
+        masks = masks[:len(ups)]
+        if _pystr is not None and isinstance(ups, list):
+            # kart_amd/csrc/kd_pystr.c attach_fields: each distinct mask decoded once, a fresh
+            # list per update written into Delta's slot
+            _pystr.attach_fields(ups, masks, status, maps.words,
+                                 lambda i: list(maps.changed_names(masks[i])), _deltas.Delta)
+        else:
+            names = maps.changed_names_rows(masks)
+            for d, nm, s in zip(ups, names, status.tolist()):
+                d.changed_fields = nm if s == 0 else None
         if stats is not None:
             stats.update(read_s=t1 - t0, kernel_s=t2 - t1, attach_s=time.perf_counter() - t2)
         return len(ups)

@@ -350,6 +350,46 @@ def test_changed_names_rows_matches_per_row():
     assert fm.changed_names_rows(np.zeros((0, fm.words), np.uint64)) == []
 
 
+def test_attach_fields_matches_per_row():
+    """the native attach (kd_pystr.c attach_fields) gives every update changed_names of its row as
+    a fresh list, None where the status is not 0, for Delta slots and for plain objects (setattr),
+    one- and multi-word masks, and more distinct masks than its first table holds (growth)"""
+    from kart_amd import _kd_pystr as P
+    from kart_amd.deltas import Delta
+    from kart_amd.schema import FieldMaps
+
+    class Plain:
+        pass
+
+    rng = np.random.default_rng(5)
+    for n_keys, n_distinct in ((5, 7), (64, 300), (130, 40)):
+        fm = object.__new__(FieldMaps)
+        fm.keys = [f"k{i}" for i in range(n_keys)]
+        fm.n_keys, fm.words = n_keys, max(1, (n_keys + 63) // 64)
+        distinct = rng.integers(0, 2**63, (n_distinct, fm.words), dtype=np.uint64)
+        if n_keys % 64:
+            distinct[:, -1] &= np.uint64((1 << (n_keys % 64)) - 1)
+        masks = np.ascontiguousarray(distinct[rng.integers(0, n_distinct, 2000)])
+        status = (rng.random(2000) < 0.1).astype(np.uint8)
+        objs = [Delta.__new__(Delta) if i % 3 else Plain() for i in range(2000)]
+        calls = []
+
+        def names_of(i):
+            calls.append(i)
+            return list(fm.changed_names(masks[i]))
+
+        used = P.attach_fields(objs, masks, status, fm.words, names_of, Delta)
+        assert used == len(calls) == len({masks[i].tobytes() for i in range(2000) if not status[i]})
+        for o, m, s in zip(objs, masks, status):
+            assert o.changed_fields == (None if s else fm.changed_names(m))
+        lists = [o.changed_fields for o in objs if o.changed_fields is not None]
+        assert len({id(x) for x in lists}) == len(lists)
+    with pytest.raises(ValueError):
+        P.attach_fields([Plain()], masks[:1], np.zeros(1, np.int32), fm.words, names_of, Delta)
+    with pytest.raises(ValueError):
+        P.attach_fields([Plain(), Plain()], masks[:1], np.zeros(2, np.uint8), fm.words, names_of, Delta)
+
+
 def test_field_diff_one_read_for_both_sides(tmp_path, eng):
     """versions of one git repository: field_diff reads both sides' update blobs in ONE batched
     read, split into two arenas over the same buffer; the changed fields are those whose values
