@@ -253,7 +253,8 @@ static PyTypeObject PromiseType = {
  * halves are (pk, promise) tuples passed to delta_type(old, new).  blob_type is kart_amd.dataset's
  * LazyBlob (slots _src, _i, _data).
  * Returns (keys, deltas, upd_rows, upd_deltas, upd_keys): the key of each delta (old pk, else new pk)
- * and the delta, and the updates' row numbers, deltas and keys.  out (optional dict): each delta is
+ * and the delta, and the updates' row numbers (bytes: native int64, no int object per row), deltas
+ * and keys.  out (optional dict): each delta is
  * also stored there at its key (a DeltaDiff's dict filled in place). */
 static PyObject* build_deltas(PyObject* self, PyObject* args) {
     PyObject *dt, *kvt, *bt, *pt, *og, *ng, *os_, *ns, *ol_o, *nl_o, *op_o, *np_o, *out = Py_None;
@@ -268,6 +269,8 @@ static PyObject* build_deltas(PyObject* self, PyObject* args) {
     PyObject* const out_dict = out != Py_None ? out : NULL;
     Py_buffer ol = {0}, nl = {0}, opb = {0}, npb = {0};
     PyObject *keys = NULL, *dl = NULL, *urows = NULL, *udl = NULL, *ukeys = NULL, *ret = NULL;
+    long long* ur = NULL;  /* the updates' rows */
+    Py_ssize_t nur = 0;
     PyObject *t_ins = NULL, *t_upd = NULL, *t_del = NULL;
     PartialMaker pm[2];
     memset(pm, 0, sizeof(pm));
@@ -307,8 +310,9 @@ static PyObject* build_deltas(PyObject* self, PyObject* args) {
     zero = PyLong_FromLong(0);
     if (!t_ins || !t_upd || !t_del || !zero) goto fail;
     keys = PyList_New(n); dl = PyList_New(n);
-    urows = PyList_New(0); udl = PyList_New(0); ukeys = PyList_New(0);
-    if (!keys || !dl || !urows || !udl || !ukeys) goto fail;
+    udl = PyList_New(0); ukeys = PyList_New(0);
+    ur = (long long*)PyMem_Malloc(sizeof(long long) * (size_t)(n ? n : 1));
+    if (!keys || !dl || !udl || !ukeys || !ur) { if (!PyErr_Occurred()) PyErr_NoMemory(); goto fail; }
     PyTypeObject* BT = (PyTypeObject*)bt;
     PyTypeObject* KT = (PyTypeObject*)kvt;
     PyTypeObject* DT = (PyTypeObject*)dt;
@@ -399,17 +403,20 @@ static PyObject* build_deltas(PyObject* self, PyObject* args) {
         Py_INCREF(d);
         PyList_SET_ITEM(dl, i, d);
         if (pkv[0] && pkv[1]) {
-            PyObject* r = PyLong_FromSsize_t(i);
-            int e = !r || PyList_Append(urows, r) < 0 || PyList_Append(udl, d) < 0 || PyList_Append(ukeys, pkv[0]) < 0;
-            Py_XDECREF(r);
-            if (e) { Py_DECREF(d); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]); goto fail; }
+            ur[nur++] = i;
+            if (PyList_Append(udl, d) < 0 || PyList_Append(ukeys, pkv[0]) < 0) {
+                Py_DECREF(d); Py_XDECREF(pkv[0]); Py_XDECREF(pkv[1]);
+                goto fail;
+            }
         }
         Py_DECREF(d);
         Py_XDECREF(pkv[0]);
         Py_XDECREF(pkv[1]);
     }
-    ret = PyTuple_Pack(5, keys, dl, urows, udl, ukeys);
+    urows = PyBytes_FromStringAndSize((const char*)ur, (Py_ssize_t)(sizeof(long long) * (size_t)nur));
+    if (urows) ret = PyTuple_Pack(5, keys, dl, urows, udl, ukeys);
 fail:
+    PyMem_Free(ur);
     Py_XDECREF(keys); Py_XDECREF(dl); Py_XDECREF(urows); Py_XDECREF(udl); Py_XDECREF(ukeys);
     Py_XDECREF(t_ins); Py_XDECREF(t_upd); Py_XDECREF(t_del); Py_XDECREF(zero);
     Py_XDECREF(pm[0].kw); Py_XDECREF(pm[1].kw);

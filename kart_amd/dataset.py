@@ -452,7 +452,7 @@ def diff_feature(engine, base, target, feature_filter=None, reverse=False, updat
             else:
                 store(opk if ob is not None else npk, delta)
     if updates is not None:
-        rows = np.asarray(upd_rows, np.int64)
+        rows = np.frombuffer(upd_rows, np.int64) if isinstance(upd_rows, bytes) else np.asarray(upd_rows, np.int64)
         updates.old_v, updates.new_v = old_v, new_v
         updates.old_leaf = old_leaf[rows]
         updates.new_leaf = new_leaf[rows]

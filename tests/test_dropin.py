@@ -518,7 +518,8 @@ def test_native_delta_builder_kart_structs_path(monkeypatch):
     r = P.build_deltas(KD, DL.KeyValue, D.LazyBlob, functools.partial, ov.get_feature_from_blob,
                        nv.get_feature_from_blob, ov, nv, ol, nl, ["a", None, "c"], [None, "b", "c"], False)
     keys, deltas, rows, upd, ukeys = r
-    assert keys == ["a", "b", "c"] and rows == [2] and ukeys == ["c"] and upd == [deltas[2]]
+    assert keys == ["a", "b", "c"] and np.frombuffer(rows, np.int64).tolist() == [2]
+    assert ukeys == ["c"] and upd == [deltas[2]]
     assert calls[0][1] is None and calls[1][0] is None
     assert [c[0][0] if c[0] else None for c in calls] == ["a", None, "c"]
     assert [c[1][1]() if c[1] else None for c in calls] == [None, 4, 6]
