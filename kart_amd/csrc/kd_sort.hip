@@ -732,15 +732,26 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
                 if (x >= vlo && x < vhi && (u32)x == s0 && len >= 2 && len <= 64) s_bm[x >> 1] = 0;
             }
             __syncthreads();
+            // a thread's entries are contiguous, so its bits are OR'd per run in a register and each
+            // (thread, run) pair does one LDS atomic: ~1.3 per thread instead of one per entry, the
+            // ~7 threads of a 64-entry run contending instead of its 64 entries
+            u64 acc = 0;
+            u32 cur = 0;
 #pragma unroll
             for (int j = 0; j < SEG_EPT; j++) {
                 const int x = x0 + j;
                 const u32 s0 = s_st[x], len = s_en[x] - s0;
+                if (s0 != cur) {
+                    if (acc) atomicOr((unsigned long long*)&s_bm[cur >> 1], acc);
+                    acc = 0;
+                    cur = s0;
+                }
                 if (x >= vlo && x < vhi && len >= 2 && len <= 64) {
                     const u64 k = s_k[x], hk = s_k[s0];
-                    if (((k ^ hk) >> 6) == 0) atomicOr((unsigned long long*)&s_bm[s0 >> 1], 1ull << (k & 63));
+                    if (((k ^ hk) >> 6) == 0) acc |= 1ull << (k & 63);
                 }
             }
+            if (acc) atomicOr((unsigned long long*)&s_bm[cur >> 1], acc);
             __syncthreads();
         }
         // ranks of the tile's own entries
