@@ -658,15 +658,20 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
         vlo = g0 < 0 ? (int)(-g0) : 0;  // valid LDS entries: [vlo, vhi)
         vhi = (int)min<i64>((i64)SEG_E, (i64)n - g0);
     };
+    // Addresses are a uniform tile base (SGPRs) + a 32-bit byte offset per lane (LDS-index-sized), so
+    // no lane does 64-bit address arithmetic: the kernel is VALU-bound (r5 counters on C4: ~1,200
+    // VALU instructions per wave and tile, ~5 waves per SIMD each ~18 % VALU-active)
     u64 v[SEG_EPT];
     auto fetch = [&](u64 t) {
         i64 g0;
         int vlo, vhi;
         geo(t, g0, vlo, vhi);
+        const char* kt = (const char*)(key + g0);  // (tile 0: below key; every lane's index is >= vlo)
 #pragma unroll
         for (int j = 0; j < SEG_EPT; j++) {
             const int x = tid + j * SEG_NT;
-            v[j] = key[g0 + (x < vlo ? vlo : (x >= vhi ? vhi - 1 : x))];
+            const u32 xc = (u32)(x < vlo ? vlo : (x >= vhi ? vhi - 1 : x));
+            v[j] = *(const u64*)(kt + 8u * xc);
         }
     };
     u64 tile = blockIdx.x;
@@ -687,27 +692,36 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
         // invalid entries are runs of their own.  Starts: the last head at or before the entry (a
         // max-scan of head index + 1, 0 = none yet); ends: the first head after it (a min-scan from
         // the right)
-        auto is_head = [&](int x) {
-            return !(x >= vlo && x < vhi) || x == vlo || (s_k[x] >> shift) != (s_k[x - 1] >> shift);
-        };
+        // (the thread's SEG_EPT contiguous keys and its predecessor's read once; heads kept as bits)
+        static_assert(SEG_EPT <= 32, "head bits");
         const int x0 = tid * SEG_EPT;
+        u64 kk[SEG_EPT + 1];
+        kk[0] = x0 > 0 ? s_k[x0 - 1] : 0;
+#pragma unroll
+        for (int j = 0; j < SEG_EPT; j++) kk[j + 1] = s_k[x0 + j];
+        u32 hm = 0;
+#pragma unroll
+        for (int j = 0; j < SEG_EPT; j++) {
+            const int x = x0 + j;
+            const bool valid = x >= vlo && x < vhi;
+            const bool head = !valid || x == vlo || ((kk[j + 1] ^ kk[j]) >> shift) != 0;
+            hm |= head ? 1u << j : 0u;
+            // descending top bits: checked at the heads of the tile's own range (each boundary once)
+            if (head && valid && x > vlo && x >= SEG_H && x < SEG_H + SEG_T && (kk[j + 1] >> shift) < (kk[j] >> shift))
+                bad |= 1u;
+        }
         u32 st_loc[SEG_EPT], en_loc[SEG_EPT];
         u32 runp1 = 0;
 #pragma unroll
         for (int j = 0; j < SEG_EPT; j++) {
-            const int x = x0 + j;
-            const bool head = is_head(x);
-            if (head) runp1 = (u32)x + 1;
+            if ((hm >> j) & 1u) runp1 = (u32)(x0 + j) + 1;
             st_loc[j] = runp1;
-            // descending top bits: checked at the heads of the tile's own range (each boundary once)
-            if (head && x > vlo && x < vhi && x >= SEG_H && x < SEG_H + SEG_T && (s_k[x] >> shift) < (s_k[x - 1] >> shift))
-                bad |= 1u;
         }
         u32 nxt = SEG_E;
 #pragma unroll
         for (int j = SEG_EPT - 1; j >= 0; j--) {
             en_loc[j] = nxt;
-            if (is_head(x0 + j)) nxt = (u32)(x0 + j);
+            if ((hm >> j) & 1u) nxt = (u32)(x0 + j);
         }
         const u32 fwd = seg_block_scan<true>(runp1, s_w, false);
         s_inc[tid] = fwd;
@@ -754,23 +768,27 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
             if (acc) atomicOr((unsigned long long*)&s_bm[cur >> 1], acc);
             __syncthreads();
         }
-        // ranks of the tile's own entries
+        // ranks of the tile's own entries; an entry's place = tile base + its LDS-index destination
+        char* const ko = (char*)(kout + g0);
+        char* const oo = (char*)(order + g0);
+        const u32 og = (u32)g0;  // (mod 2^32: g0 + x of a real entry is in [0, n))
+        const bool lo_open = g0 > 0, hi_open = g0 + SEG_E < (i64)n;  // block-uniform
 #pragma unroll 2
         for (int j = 0; j < SEG_IPT; j++) {
             const int x = SEG_H + j * SEG_NT + tid;  // consecutive lanes: consecutive entries
             if (x >= vhi) break;
             const u64 k = s_k[x];
             const u32 s0 = s_st[x], e0 = s_en[x];
-            if ((s0 == 0 && g0 > 0) || (e0 == (u32)SEG_E && g0 + SEG_E < (i64)n) || e0 - s0 > (u32)RS_SEG_MAX) {
+            if ((s0 == 0 && lo_open) || (e0 == (u32)SEG_E && hi_open) || e0 - s0 > (u32)RS_SEG_MAX) {
                 bad |= 4u;  // a run longer than RS_SEG_MAX (or reaching past the halo)
                 continue;
             }
             if (BM && e0 - s0 >= 2 && e0 - s0 <= 64) {
                 const u64 bm = s_bm[s0 >> 1];
                 if ((u32)__popcll(bm) == e0 - s0) {  // one bit per entry: distinct keys, ranked by the map
-                    const u64 dst = (u64)(g0 + (i64)s0) + (u32)__popcll(bm & ((1ull << (k & 63)) - 1));
-                    kout[dst] = k;
-                    order[dst] = (u32)(g0 + x);
+                    const u32 dl = s0 + (u32)__popcll(bm & ((1ull << (k & 63)) - 1));
+                    *(u64*)(ko + 8u * dl) = k;
+                    *(u32*)(oo + 4u * dl) = og + (u32)x;
                     continue;
                 }
             }
@@ -787,9 +805,9 @@ __global__ __launch_bounds__(SEG_NT) void k_seg_sort(const u64* __restrict__ key
                 dup += a == k;
             }
             bad |= dup > 1 ? 1u : 0u;
-            const u64 dst = (u64)(g0 + (i64)s0) + rank;
-            kout[dst] = k;
-            order[dst] = (u32)(g0 + x);
+            const u32 dl = s0 + rank;
+            *(u64*)(ko + 8u * dl) = k;
+            *(u32*)(oo + 4u * dl) = og + (u32)x;
         }
         __syncthreads();  // s_k / s_st / s_en are restaged for the next tile
     }
