@@ -459,7 +459,7 @@ SORT_KERNELS = ("k_rs_bits", "k_sort_hist", "k_sort_scan", "k_sort_pass", "k_gat
 C4_KERNELS = ("k_seg_sort", "k_sorted3", "k_partition2", "k_apart3", "k_join2", "k_join3", "k_gscan2", "k_place2",
               "k_place3", "k_resolve3")
 STEP_KERNELS = ("k_partition2", "k_join2", "k_gscan2", "k_place2", "k_fielddiff", "k_dpk_keys", "k_sort_scan",
-                "k_sort_pass", "k_pkm_mark", "k_pkm_scan", "k_pkm_place")
+                "k_sort_pass", "k_pkm_mark", "k_pkm_scan", "k_pkm_cscan", "k_pkm_place")
 PKM_MAX_BLOCKS = 1 << 26  # kd_delta_pk_order's bitmap path: pk ranges of at most this many 64-pk blocks
 RS_RB = 9  # digit bits per radix pass (kd_sort.hip RS_RB): passes = ceil(varying bits / 9)
 
@@ -491,7 +491,7 @@ def pk_sort_summary(pipe, parts, counts):
     nb = (hi >> 6) - (lo >> 6) + 1
     recs = counts["deltas"] + counts["updates"]
     if nb <= PKM_MAX_BLOCKS:
-        kk = ("k_pkm_mark", "k_pkm_scan", "k_pkm_place")
+        kk = ("k_pkm_mark", "k_pkm_scan", "k_pkm_cscan", "k_pkm_place")
         alg = 28 * recs + 2 * 24 * nb
         how = {"path": "bitmap", "blocks": nb}
     else:

@@ -465,8 +465,8 @@ __global__ __launch_bounds__(RS_HIST_NT) void k_dpk_keys(const uint2* __restrict
 //   k_pkm_mark   pk of each record (saved), its bit OR-ed into its block's mask: records of one
 //                leaf tree are adjacent in walk order, so a wave first ORs runs of equal blocks
 //                together (segmented shuffle reduction) and only each run's head lane does the atomic
-//   k_pkm_scan   per chunk of PKM_CH masks: the popcounts' exclusive prefix (u32) + the chunk total;
-//                the last workgroup to finish scans the chunk totals (one pass, no extra launch)
+//   k_pkm_scan   per chunk of PKM_CH masks: the popcounts' exclusive prefix (u32) + the chunk total
+//   k_pkm_cscan  one block: exclusive prefix of the chunk totals
 //   k_pkm_place  record -> its rank: chunk prefix + in-chunk prefix + popcount(mask below its bit)
 #ifndef KD_PKM_IPT
 #define KD_PKM_IPT 16  // masks per scan thread (r4pk, C3: 2 / 4 / 8 / 16 -> scan 0.111 / 0.074 / 0.052 / 0.038 ms)
@@ -512,66 +512,77 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ r
     }
 }
 
+// (masks and local prefixes moved 16 B per access; each thread's PKM_IPT masks are one 128-B line)
+static_assert(PKM_IPT % 4 == 0, "k_pkm_scan: 16-B loads and stores");
 __global__ __launch_bounds__(PKM_NT) void k_pkm_scan(const u64* __restrict__ masks, u64 nb, u32* __restrict__ local,
-                                                     u32* __restrict__ chunk_tot, u32* __restrict__ done_ctr,
-                                                     u32* __restrict__ chunk_pre) {
+                                                     u32* __restrict__ chunk_tot) {
     __shared__ u32 s_wave[PKM_NT / 64];
-    __shared__ u32 s_last;
     const int tid = threadIdx.x;
     const u64 c0 = (u64)blockIdx.x * PKM_CH + (u64)tid * PKM_IPT;
     u32 cnt[PKM_IPT], sum = 0;
+    if (c0 + PKM_IPT <= nb) {
+        const u32x4* m4 = (const u32x4*)(masks + c0);
 #pragma unroll
-    for (int j = 0; j < PKM_IPT; j++) {
-        cnt[j] = c0 + j < nb ? (u32)__popcll(masks[c0 + j]) : 0u;
-        sum += cnt[j];
+        for (int j = 0; j < PKM_IPT / 2; j++) {
+            const u32x4 v = m4[j];
+            cnt[2 * j] = (u32)__popc(v.x) + (u32)__popc(v.y);
+            cnt[2 * j + 1] = (u32)__popc(v.z) + (u32)__popc(v.w);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < PKM_IPT; j++) cnt[j] = c0 + j < nb ? (u32)__popcll(masks[c0 + j]) : 0u;
     }
+#pragma unroll
+    for (int j = 0; j < PKM_IPT; j++) sum += cnt[j];
     u32 tot;
     u32 ex = block_scan_u32<PKM_NT>(sum, s_wave, &tot);
+    if (c0 + PKM_IPT <= nb) {
+        u32x4* l4 = (u32x4*)(local + c0);
 #pragma unroll
-    for (int j = 0; j < PKM_IPT; j++) {
-        if (c0 + j < nb) local[c0 + j] = ex;
-        ex += cnt[j];
-    }
-    if (tid == 0) {
-        chunk_tot[blockIdx.x] = tot;
-        __threadfence();
-        s_last = atomicAdd(done_ctr, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // the last workgroup: exclusive scan of every chunk's total.  Up to 8 per thread: each thread a
-    // contiguous run, all its loads issued together (one L2 round trip instead of one per 256
-    // totals: the serial tail was most of this kernel, r4pk)
-    __threadfence();
-    const u32 nch = gridDim.x;
-    if (nch <= 8 * PKM_NT) {
-        const u32 per = (nch + PKM_NT - 1) / PKM_NT, k0 = tid * per;
-        u32 v[8], sum = 0;
+        for (int j = 0; j < PKM_IPT / 4; j++) {
+            u32x4 o;
+            o.x = ex; ex += cnt[4 * j];
+            o.y = ex; ex += cnt[4 * j + 1];
+            o.z = ex; ex += cnt[4 * j + 2];
+            o.w = ex; ex += cnt[4 * j + 3];
+            l4[j] = o;
+        }
+    } else {
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            v[j] = (u32)j < per && k0 + j < nch ? __hip_atomic_load(chunk_tot + k0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        for (int j = 0; j < PKM_IPT; j++) {
+            if (c0 + j < nb) local[c0 + j] = ex;
+            ex += cnt[j];
+        }
+    }
+    if (tid == 0) chunk_tot[blockIdx.x] = tot;
+}
+
+// one block: exclusive scan of the chunk totals (a kernel of its own: the launch boundary orders it
+// after every chunk's total, where a last-block-done hand-off cost each block an agent-scope fence —
+// an L2 write-back — and made the scan 37 us at C3's 415 chunks)
+constexpr int PKC_PT = 8;
+__global__ __launch_bounds__(1024) void k_pkm_cscan(const u32* __restrict__ chunk_tot, u32 nch, u32* __restrict__ chunk_pre) {
+    __shared__ u32 s_wave[1024 / 64];
+    const int tid = threadIdx.x;
+    u32 carry = 0;
+    for (u32 base = 0; base < nch; base += 1024 * PKC_PT) {  // (one pass up to 8192 chunks = 2^31 blocks)
+        const u32 k0 = base + (u32)tid * PKC_PT;
+        u32 v[PKC_PT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < PKC_PT; j++) {
+            v[j] = k0 + j < nch ? chunk_tot[k0 + j] : 0u;
             sum += v[j];
         }
         u32 t2;
-        u32 e = block_scan_u32<PKM_NT>(sum, s_wave, &t2);
+        u32 e = block_scan_u32<1024>(sum, s_wave, &t2);
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if ((u32)j < per && k0 + j < nch) chunk_pre[k0 + j] = e;
+        for (int j = 0; j < PKC_PT; j++) {
+            if (k0 + j < nch) chunk_pre[k0 + j] = carry + e;
             e += v[j];
         }
-        if (tid == 0) *done_ctr = 0;
-        return;
-    }
-    u32 carry = 0;
-    for (u32 k0 = 0; k0 < nch; k0 += PKM_NT) {
-        const u32 k = k0 + tid;
-        const u32 v = k < nch ? __hip_atomic_load(chunk_tot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-        u32 t2;
-        const u32 e = block_scan_u32<PKM_NT>(v, s_wave, &t2);
-        if (k < nch) chunk_pre[k] = carry + e;
         carry += t2;
+        __syncthreads();
     }
-    if (tid == 0) *done_ctr = 0;  // ready for the next call
 }
 
 __global__ __launch_bounds__(PKM_NT) void k_pkm_place(const i64* __restrict__ pks, const u64* __restrict__ rkey, u64 ncap,
@@ -1144,15 +1155,12 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
     const u64 nb = (u64)hi_block - (u64)lo_block + 1;
     const u64 pkm_max = ctx->opt.pkm_max_blocks;  // (tests force the radix path with 0)
     if (nb <= pkm_max && nb / PKM_CH < 0xFFFFFFFFull) {
-        void *masks, *local, *ctot, *cpre, *ctr, *tpk;
+        void *masks, *local, *ctot, *cpre, *tpk;
         const u64 nch = (nb + PKM_CH - 1) / PKM_CH;
         if ((rc = ensure(ctx, "pkm.masks", nb * 8, &masks))) return rc;
         if ((rc = ensure(ctx, "pkm.local", nb * 4, &local))) return rc;
         if ((rc = ensure(ctx, "pkm.ctot", nch * 4, &ctot))) return rc;
         if ((rc = ensure(ctx, "pkm.cpre", nch * 4, &cpre))) return rc;
-        const bool fresh = ctx->bufs["pkm.ctr"].p == nullptr;
-        if ((rc = ensure(ctx, "pkm.ctr", 16, &ctr))) return rc;
-        if (fresh) KD_HIP(hipMemsetAsync(ctr, 0, 16, ctx->stream));
         if ((rc = ensure(ctx, "pkm.pk", cap * 8, &tpk))) return rc;
         KD_HIP(hipMemsetAsync(masks, 0, nb * 8, ctx->stream));
         const unsigned g1 = (unsigned)std::max<u64>(1, std::min<u64>((cap + PKM_NT - 1) / PKM_NT, (u64)ctx->n_cu * 8));
@@ -1163,7 +1171,11 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
         if (rc) return rc;
         rc = launch(ctx, "k_pkm_scan", [&] {
             hipLaunchKernelGGL(k_pkm_scan, dim3((unsigned)nch), dim3(PKM_NT), 0, ctx->stream, (const u64*)masks, nb,
-                               (u32*)local, (u32*)ctot, (u32*)ctr, (u32*)cpre);
+                               (u32*)local, (u32*)ctot);
+        });
+        if (rc) return rc;
+        rc = launch(ctx, "k_pkm_cscan", [&] {
+            hipLaunchKernelGGL(k_pkm_cscan, dim3(1), dim3(1024), 0, ctx->stream, (const u32*)ctot, (u32)nch, (u32*)cpre);
         });
         if (rc) return rc;
         return launch(ctx, "k_pkm_place", [&] {
