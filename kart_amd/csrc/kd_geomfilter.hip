@@ -845,15 +845,33 @@ __global__ __launch_bounds__(256) void k_gf_fb(GfArgs a, GfHeadArgs g) {
     }
 }
 
-// one block: exclusive scan of the tile counts in place, the total to *n_keep
+// one block: exclusive scan of the tile counts in place, the total to *n_keep.  GF_SPT counts per
+// thread, contiguous, loaded together (16-B loads where whole): one pass up to 8,192 tiles = 33.5M
+// deltas, instead of 1,024-tile chunks each behind the previous chunk's barrier
+constexpr int GF_SPT = 8;
 __global__ __launch_bounds__(1024) void k_gf_scan(u32* __restrict__ cnt, u32 ntiles, u64* __restrict__ n_keep) {
     __shared__ u32 s_w[16];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     u32 carry = 0;
-    for (u32 base = 0; base < ntiles; base += 1024) {
-        const u32 i = base + tid;
-        const u32 x = i < ntiles ? cnt[i] : 0;
-        u32 s = x;
+    for (u32 base = 0; base < ntiles; base += 1024 * GF_SPT) {  // (block-uniform)
+        const u32 i0 = base + (u32)tid * GF_SPT;
+        const bool whole = i0 + GF_SPT <= ntiles;
+        u32 x[GF_SPT];
+        if (whole) {
+            const u32x4* c4 = (const u32x4*)(cnt + i0);
+#pragma unroll
+            for (int j = 0; j < GF_SPT / 4; j++) {
+                const u32x4 v = c4[j];
+                x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < GF_SPT; j++) x[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
+        }
+        u32 t = 0;
+#pragma unroll
+        for (int j = 0; j < GF_SPT; j++) t += x[j];
+        u32 s = t;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const u32 y = __shfl_up(s, o, 64);
@@ -867,7 +885,25 @@ __global__ __launch_bounds__(1024) void k_gf_scan(u32* __restrict__ cnt, u32 nti
             if (w < wid) wp += s_w[w];
             all += s_w[w];
         }
-        if (i < ntiles) cnt[i] = carry + wp + s - x;
+        u32 e = carry + wp + s - t;
+        if (whole) {
+            u32x4* c4 = (u32x4*)(cnt + i0);
+#pragma unroll
+            for (int j = 0; j < GF_SPT / 4; j++) {
+                u32x4 o;
+                o.x = e; e += x[4 * j];
+                o.y = e; e += x[4 * j + 1];
+                o.z = e; e += x[4 * j + 2];
+                o.w = e; e += x[4 * j + 3];
+                c4[j] = o;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < GF_SPT; j++) {
+                if (i0 + j < ntiles) cnt[i0 + j] = e;
+                e += x[j];
+            }
+        }
         carry += all;
         __syncthreads();
     }
