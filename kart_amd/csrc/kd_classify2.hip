@@ -883,6 +883,10 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
     // 10 % edits): one memory round trip for most tiles instead of two
     const uint2 v0 = sdp[tid];
     const uint2 w0 = out_upd ? sup[tid] : make_uint2(0, 0);
+    // (and the first 64 record keys of each list, when asked for: no second round trip for them)
+    const u64* skd = out_dkey ? stage_dkey + t * (u64)tile_items : nullptr;
+    const u64* sku = out_dkey && out_upd && out_ukey ? stage_ukey + t * (u64)tile_items : nullptr;
+    const u64 kd0 = skd ? skd[tid] : 0, ku0 = sku ? sku[tid] : 0;
     u64 pd = 0, pu = 0;
     if (tid < (int)(t - t_lo)) {
         const uint4 c = *(const uint4*)(tile_cnt + 4 * (t_lo + tid));
@@ -922,12 +926,13 @@ __global__ __launch_bounds__(NT) void k_place2(const uint2* __restrict__ stage_d
             if (r < own.y) out_upd[pu + r] = v[j];
         }
     }
-    if (out_dkey) {  // the records' keys, when the caller asked for them
-        const u64* skd = stage_dkey + t * (u64)tile_items;
-        const u64* sku = stage_ukey + t * (u64)tile_items;
-        for (u32 r = tid; r < own.x; r += NT) out_dkey[pd + r] = skd[r];
-        if (out_upd && out_ukey)
-            for (u32 r = tid; r < own.y; r += NT) out_ukey[pu + r] = sku[r];
+    if (skd) {  // the records' keys, when the caller asked for them
+        if ((u32)tid < own.x) out_dkey[pd + tid] = kd0;
+        for (u32 r = tid + NT; r < own.x; r += NT) out_dkey[pd + r] = skd[r];
+    }
+    if (sku) {
+        if ((u32)tid < own.y) out_ukey[pu + tid] = ku0;
+        for (u32 r = tid + NT; r < own.y; r += NT) out_ukey[pu + r] = sku[r];
     }
 }
 
