@@ -110,6 +110,11 @@ struct kd_ctx {
     // resident workgroups per CU by (kernel, block size, dynamic LDS): asked once per context (kd::occupancy)
     std::map<std::tuple<const void*, int, size_t>, int> occ;
     uint32_t rs_epoch = 0;  // kd_sort: epoch of the last pass's look-back words (kd_sort.hip)
+    // kd_delta_pk_order's two mask buffers: a call marks one and its scan zeroes the other for the
+    // next call; zeroed = (buffer address, blocks known zero) — a reallocated buffer is zeroed again
+    int pkm_cur = 0;
+    void* pkm_zero_ptr[2] = {nullptr, nullptr};
+    uint64_t pkm_zero_nb[2] = {0, 0};
     // small workspaces come from one slab (one hipMalloc instead of one per slot on a process's
     // first calls); grown slots take a fresh piece, the slab is freed with the context
     char* slab = nullptr;

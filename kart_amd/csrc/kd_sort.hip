@@ -514,8 +514,9 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_mark(const uint2* __restrict__ r
 
 // (masks and local prefixes moved 16 B per access; each thread's PKM_IPT masks are one 128-B line)
 static_assert(PKM_IPT % 4 == 0, "k_pkm_scan: 16-B loads and stores");
+// (zero: the other mask buffer, cleared here for the next call — no fill launch per call)
 __global__ __launch_bounds__(PKM_NT) void k_pkm_scan(const u64* __restrict__ masks, u64 nb, u32* __restrict__ local,
-                                                     u32* __restrict__ chunk_tot) {
+                                                     u32* __restrict__ chunk_tot, u64* __restrict__ zero) {
     __shared__ u32 s_wave[PKM_NT / 64];
     const int tid = threadIdx.x;
     const u64 c0 = (u64)blockIdx.x * PKM_CH + (u64)tid * PKM_IPT;
@@ -528,9 +529,15 @@ __global__ __launch_bounds__(PKM_NT) void k_pkm_scan(const u64* __restrict__ mas
             cnt[2 * j] = (u32)__popc(v.x) + (u32)__popc(v.y);
             cnt[2 * j + 1] = (u32)__popc(v.z) + (u32)__popc(v.w);
         }
+        u32x4* z4 = (u32x4*)(zero + c0);
+#pragma unroll
+        for (int j = 0; j < PKM_IPT / 2; j++) z4[j] = u32x4{0u, 0u, 0u, 0u};
     } else {
 #pragma unroll
-        for (int j = 0; j < PKM_IPT; j++) cnt[j] = c0 + j < nb ? (u32)__popcll(masks[c0 + j]) : 0u;
+        for (int j = 0; j < PKM_IPT; j++) {
+            cnt[j] = c0 + j < nb ? (u32)__popcll(masks[c0 + j]) : 0u;
+            if (c0 + j < nb) zero[c0 + j] = 0;
+        }
     }
 #pragma unroll
     for (int j = 0; j < PKM_IPT; j++) sum += cnt[j];
@@ -1155,14 +1162,24 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
     const u64 nb = (u64)hi_block - (u64)lo_block + 1;
     const u64 pkm_max = ctx->opt.pkm_max_blocks;  // (tests force the radix path with 0)
     if (nb <= pkm_max && nb / PKM_CH < 0xFFFFFFFFull) {
-        void *masks, *local, *ctot, *cpre, *tpk;
+        void *mbuf[2], *local, *ctot, *cpre, *tpk;
         const u64 nch = (nb + PKM_CH - 1) / PKM_CH;
-        if ((rc = ensure(ctx, "pkm.masks", nb * 8, &masks))) return rc;
+        if ((rc = ensure(ctx, "pkm.masks0", nb * 8, &mbuf[0]))) return rc;
+        if ((rc = ensure(ctx, "pkm.masks1", nb * 8, &mbuf[1]))) return rc;
+        const int cur = ctx->pkm_cur & 1;
+        void* const masks = mbuf[cur];
+        void* const other = mbuf[cur ^ 1];
         if ((rc = ensure(ctx, "pkm.local", nb * 4, &local))) return rc;
         if ((rc = ensure(ctx, "pkm.ctot", nch * 4, &ctot))) return rc;
         if ((rc = ensure(ctx, "pkm.cpre", nch * 4, &cpre))) return rc;
         if ((rc = ensure(ctx, "pkm.pk", cap * 8, &tpk))) return rc;
-        KD_HIP(hipMemsetAsync(masks, 0, nb * 8, ctx->stream));
+        // this call's masks must be zero for [0, nb): cleared by the previous call's scan, else here
+        ctx->pkm_zero_nb[cur ^ 1] = 0;  // (until this call's scan has cleared it)
+        if (ctx->pkm_zero_ptr[cur] != masks || ctx->pkm_zero_nb[cur] < nb) {
+            ctx->pkm_zero_nb[cur] = 0;
+            KD_HIP(hipMemsetAsync(masks, 0, nb * 8, ctx->stream));
+        }
+        ctx->pkm_zero_nb[cur] = 0;  // marked below
         const unsigned g1 = (unsigned)std::max<u64>(1, std::min<u64>((cap + PKM_NT - 1) / PKM_NT, (u64)ctx->n_cu * 8));
         rc = launch(ctx, "k_pkm_mark", [&] {
             hipLaunchKernelGGL(k_pkm_mark, dim3(g1), dim3(PKM_NT), 0, ctx->stream, (const uint2*)d_delta, cap, d_n, kA,
@@ -1171,9 +1188,12 @@ extern "C" int kd_delta_pk_order(kd_ctx* ctx, const kd_side* base, const kd_side
         if (rc) return rc;
         rc = launch(ctx, "k_pkm_scan", [&] {
             hipLaunchKernelGGL(k_pkm_scan, dim3((unsigned)nch), dim3(PKM_NT), 0, ctx->stream, (const u64*)masks, nb,
-                               (u32*)local, (u32*)ctot);
+                               (u32*)local, (u32*)ctot, (u64*)other);
         });
         if (rc) return rc;
+        ctx->pkm_zero_ptr[cur ^ 1] = other;  // zero for [0, nb) once the scan has run (stream order)
+        ctx->pkm_zero_nb[cur ^ 1] = nb;
+        ctx->pkm_cur = cur ^ 1;
         rc = launch(ctx, "k_pkm_cscan", [&] {
             hipLaunchKernelGGL(k_pkm_cscan, dim3(1), dim3(1024), 0, ctx->stream, (const u32*)ctot, (u32)nch, (u32*)cpre);
         });
