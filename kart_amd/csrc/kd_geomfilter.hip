@@ -1004,7 +1004,10 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
     a.enc = enc ? de : nullptr;
     a.enc_ok = enc ? dok : nullptr;
     a.tile_cnt = (u32*)t_cnt;
-    KD_HIP(hipMemsetAsync(t_nk, 0, 8, ctx->stream));
+    // the kept count goes straight to the caller's device word (no copy after the scan); the scan
+    // writes it whenever there are tiles, so only an empty call sets it here
+    u64* const nk_dst = out_mem == KD_MEM_DEVICE ? n_keep : (u64*)t_nk;
+    if (!tiles) KD_HIP(hipMemsetAsync(nk_dst, 0, 8, ctx->stream));
     GfHeadArgs gh{};
     if (g) {
         gh = *g;
@@ -1052,7 +1055,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
                     })))
             return rc;
         if ((rc = launch(ctx, "k_gf_scan", [&] {
-                 hipLaunchKernelGGL(k_gf_scan, dim3(1), dim3(1024), 0, ctx->stream, (u32*)t_cnt, (u32)tiles, (u64*)t_nk);
+                 hipLaunchKernelGGL(k_gf_scan, dim3(1), dim3(1024), 0, ctx->stream, (u32*)t_cnt, (u32)tiles, nk_dst);
              })))
             return rc;
         if ((rc = launch(ctx, "k_gf_place", [&] {
@@ -1061,10 +1064,7 @@ static int gf_run(kd_ctx* ctx, GfArgs& a, const GfHeadArgs* g, const uint32_t* p
              })))
             return rc;
     }
-    if (out_mem == KD_MEM_DEVICE) {
-        KD_HIP(hipMemcpyAsync(n_keep, t_nk, 8, hipMemcpyDeviceToDevice, ctx->stream));
-        return KD_OK;
-    }
+    if (out_mem == KD_MEM_DEVICE) return KD_OK;
     u64 nk = 0;
     KD_HIP(hipMemcpyAsync(&nk, t_nk, 8, hipMemcpyDeviceToHost, ctx->stream));
     KD_HIP(hipStreamSynchronize(ctx->stream));
