@@ -219,6 +219,17 @@ constexpr u32 RS_EPOCHS = 1u << 22;
 #define KD_RS_LBW 4
 #endif
 constexpr int RS_LBW = KD_RS_LBW;  // look-back words per round trip
+#ifndef KD_RS_SWZ
+#define KD_RS_SWZ 1
+#endif
+// k_sort_pass's per-(digit, wave) u16 counters: [wave][digit] (KD_RS_SWZ) puts a wave's digits in
+// consecutive halfwords, so lanes of different digits spread over all 64 banks (two digits per
+// dword); [digit][wave] with 8 waves gave digit d the bank (4d + wave / 2) mod 64: 16 banks for a
+// wave's 64 lanes, and the block scan's reads of 8 consecutive counters per thread 4-way conflicts
+template <int NW>
+__device__ __forceinline__ u32 rs_ci(u32 d, u32 w) {
+    return KD_RS_SWZ ? w * (u32)RS_RD + d : d * (u32)NW + w;
+}
 __device__ __forceinline__ void rs_store(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ u64 rs_load(const u64* p) {
     return __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -237,7 +248,7 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
     constexpr int NW = NT / 64, TILE = NT * IPT, CPT = RS_RD * NW / NT;
     static_assert(NT >= RS_RD && (RS_RD * NW) % NT == 0, "tile shape");
     static_assert(TILE <= 65535, "s_cnt holds tile-local starts in 16 bits");
-    __shared__ u16 s_cnt[RS_RD * NW];  // [digit][wave]: item counts, then (after the scan) starts (<= TILE)
+    __shared__ u16 s_cnt[RS_RD * NW];  // (digit, wave) at rs_ci: item counts, then (after the scan) starts (<= TILE)
     __shared__ u32 s_hist[RS_RD];      // the tile's digit counts (early: published before the ranking)
     __shared__ CK s_key[TILE];
     __shared__ u32 s_val[TILE];
@@ -288,7 +299,7 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
         const u32 d = (u32)(c[i] >> shift) & dmask;
         const u64 m = digit_peers(d, ok);
         const u32 below = lanes_below(m);
-        u16* ctr = &s_cnt[d * NW + wv];
+        u16* ctr = &s_cnt[rs_ci<NW>(d, wv)];
         const u32 pre = *ctr;  // read by every lane of the group before its lowest lane moves it
         __builtin_amdgcn_wave_barrier();
         if (ok && below == 0) *ctr = (u16)(pre + (u32)__popcll(m));
@@ -300,7 +311,8 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
         u32 x[CPT], s = 0;
 #pragma unroll
         for (int j = 0; j < CPT; j++) {
-            x[j] = s_cnt[tid * CPT + j];
+            const u32 L = (u32)(tid * CPT + j);  // (digit, wave) in digit-major scan order
+            x[j] = s_cnt[rs_ci<NW>(L / NW, L % NW)];
             s += x[j];
         }
         u32 inc = s;
@@ -317,18 +329,19 @@ __global__ __launch_bounds__(NT) void k_sort_pass(const void* __restrict__ kin, 
             if (w < wv) ex += s_wsum[w];
 #pragma unroll
         for (int j = 0; j < CPT; j++) {
-            s_cnt[tid * CPT + j] = (u16)ex;
+            const u32 L = (u32)(tid * CPT + j);
+            s_cnt[rs_ci<NW>(L / NW, L % NW)] = (u16)ex;
             ex += x[j];
         }
     }
     __syncthreads();
     // ---- d. reorder in LDS, look back ----
-    const u32 dstart = tid < RS_RD ? (u32)s_cnt[tid * NW] : 0;
+    const u32 dstart = tid < RS_RD ? (u32)s_cnt[rs_ci<NW>(tid, 0)] : 0;
 #pragma unroll
     for (int i = 0; i < IPT; i++) {
         if (wbase + (u64)i * 64 < n) {
             const u32 d = (u32)(c[i] >> shift) & dmask;
-            const u32 p = s_cnt[d * NW + wv] + rk[i];
+            const u32 p = s_cnt[rs_ci<NW>(d, wv)] + rk[i];
             s_key[p] = c[i];
             s_val[p] = v[i];
         }
