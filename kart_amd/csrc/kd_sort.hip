@@ -139,13 +139,21 @@ __global__ __launch_bounds__(256) void k_rs_bits(const u64* __restrict__ key, u6
 }
 
 // ---- all passes' digit histograms in one read of the keys ----
+// s_h holds digit d of a pass at d + d / 16 (KD_RS_HPAD): a thread counts 16 consecutive keys, so in
+// walk order lane l adds digit ~16 l + j at step j, and unpadded lanes l, l + 4, l + 8, ... met in one
+// bank (16-way); with the pad lane l lands in bank (17 l + j) mod 64
+#ifndef KD_RS_HPAD
+#define KD_RS_HPAD 1
+#endif
+constexpr int RS_HSTRIDE = KD_RS_HPAD ? RS_RD + RS_RD / 16 : RS_RD;
+__device__ __forceinline__ u32 rs_hi(u32 d) { return KD_RS_HPAD ? d + (d >> 4) : d; }
 template <typename CK>
 __global__ __launch_bounds__(RS_HIST_NT) void k_sort_hist(const u64* __restrict__ key, u64 ncap, const u64* __restrict__ dn,
                                                            int npass, int width, SortPlan plan, u32* __restrict__ hist) {
-    __shared__ u32 s_h[8 * RS_RD];
+    __shared__ u32 s_h[8 * RS_HSTRIDE];
     const int tid = threadIdx.x;
     const u64 n = dn ? min(*dn, ncap) : ncap;
-    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT) s_h[i] = 0;
+    for (int i = tid; i < npass * RS_HSTRIDE; i += RS_HIST_NT) s_h[i] = 0;
     __syncthreads();
     const u32 dmask = (1u << width) - 1;
     const bool al16 = ((uintptr_t)key & 15) == 0;
@@ -174,19 +182,21 @@ __global__ __launch_bounds__(RS_HIST_NT) void k_sort_hist(const u64* __restrict_
                 if (j < cnt) {
                     const u32 d = (u32)(c[j] >> sh) & dmask;
                     if (d != cur) {
-                        atomicAdd(&s_h[p * RS_RD + cur], run);
+                        atomicAdd(&s_h[p * RS_HSTRIDE + rs_hi(cur)], run);
                         cur = d;
                         run = 0;
                     }
                     run++;
                 }
             }
-            if (run) atomicAdd(&s_h[p * RS_RD + cur], run);
+            if (run) atomicAdd(&s_h[p * RS_HSTRIDE + rs_hi(cur)], run);
         }
     }
     __syncthreads();
-    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT)
-        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+    for (int i = tid; i < npass * RS_RD; i += RS_HIST_NT) {
+        const u32 x = s_h[(i / RS_RD) * RS_HSTRIDE + rs_hi(i % RS_RD)];
+        if (x) atomicAdd(&hist[i], x);
+    }
 }
 
 // one block: hist[p][d] -> exclusive scan over d (each digit's first output position in pass p)
